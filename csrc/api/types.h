@@ -1,0 +1,245 @@
+// Typed, read-mostly views of the Kubernetes objects the scheduler consumes.
+//
+// Parsed once from the store's JSON documents (store/store.h). Field coverage
+// follows what the reference's plugins read from core/v1 Pod/Node
+// (vendor/k8s.io/api/core/v1/types.go), scheduling.sigs.k8s.io/v1alpha1
+// PodGroup/ElasticQuota (apis/scheduling/v1alpha1/types.go:30-193),
+// topology.node.k8s.io/v1alpha1 NodeResourceTopology, policy/v1 PDB and
+// scheduling/v1 PriorityClass.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "api/resource.h"
+#include "common/json.h"
+
+namespace xsched {
+
+// ---- well-known keys (Appendix A of SURVEY.md) ----
+inline constexpr const char* kPodGroupLabel = "pod-group.scheduling.sigs.k8s.io";
+inline constexpr const char* kDefaultSchedulerName = "default-scheduler";
+
+// Timestamps are microseconds since the Unix epoch; 0 = unset.
+using MicroTime = int64_t;
+MicroTime parse_rfc3339(const std::string& s);
+std::string format_rfc3339(MicroTime t);
+MicroTime wall_now_us();
+
+using StrMap = std::vector<std::pair<std::string, std::string>>;  // small, ordered
+const std::string* strmap_get(const StrMap& m, std::string_view k);
+StrMap strmap_from_json(const Json& j);
+
+struct ObjectMeta {
+  std::string ns, name, uid;
+  int64_t resource_version = 0;
+  StrMap labels, annotations;
+  MicroTime creation = 0;
+  MicroTime deletion = 0;  // deletionTimestamp
+  std::string key() const { return ns.empty() ? name : ns + "/" + name; }
+  static ObjectMeta from_json(const Json& obj);
+  const std::string* label(std::string_view k) const { return strmap_get(labels, k); }
+  const std::string* annotation(std::string_view k) const { return strmap_get(annotations, k); }
+};
+
+// ---- selectors ----
+enum class SelOp : uint8_t { In, NotIn, Exists, DoesNotExist, Gt, Lt };
+struct SelectorRequirement {
+  std::string key;
+  SelOp op = SelOp::In;
+  std::vector<std::string> values;
+};
+bool match_requirement(const SelectorRequirement& r, const StrMap& labels);
+
+struct LabelSelector {  // metav1.LabelSelector
+  bool present = false;  // nil selector matches nothing (PDB), empty matches all
+  StrMap match_labels;
+  std::vector<SelectorRequirement> exprs;
+  bool matches(const StrMap& labels) const;
+  static LabelSelector from_json(const Json* j);
+};
+
+struct NodeSelectorTerm {
+  std::vector<SelectorRequirement> match_expressions;  // against node labels
+  std::vector<SelectorRequirement> match_fields;       // metadata.name only
+};
+struct PreferredSchedulingTerm {
+  int32_t weight = 0;
+  NodeSelectorTerm pref;
+};
+
+struct Toleration {
+  std::string key, op = "Equal", value, effect;
+  int64_t toleration_seconds = -1;
+  bool tolerates(const struct Taint& t) const;
+};
+struct Taint {
+  std::string key, value, effect;  // NoSchedule, PreferNoSchedule, NoExecute
+};
+
+struct ContainerPort {
+  int32_t host_port = 0;
+  std::string protocol = "TCP", host_ip = "0.0.0.0";
+};
+
+struct Container {
+  std::string name;
+  Res requests, limits;
+  std::vector<ContainerPort> ports;
+};
+
+enum class QoS : uint8_t { BestEffort = 0, Burstable = 1, Guaranteed = 2 };
+
+struct PodAffinityTerm {
+  LabelSelector selector;
+  std::vector<std::string> namespaces;
+  std::string topology_key;
+};
+struct WeightedPodAffinityTerm {
+  int32_t weight = 0;
+  PodAffinityTerm term;
+};
+
+// GPU placement of a pod on an MI355X node, decoded from the FlexGPU
+// annotations (plugins/flexgpu.cc documents the format).
+struct GpuAssignment {
+  enum class Kind : uint8_t { None, WholeGpu, Partition, Memory };
+  Kind kind = Kind::None;
+  std::vector<int> gpus;                           // physical GPU indexes
+  std::vector<std::pair<int, int>> partitions;     // (gpu, partition) pairs
+  int64_t memory = 0;                              // memory slice units
+  bool valid() const { return kind != Kind::None; }
+};
+
+struct Pod {
+  ObjectMeta meta;
+  std::string scheduler_name = kDefaultSchedulerName;
+  std::string node_name, nominated_node_name, priority_class_name, phase = "Pending";
+  std::string preemption_policy = "PreemptLowerPriority";
+  int32_t priority = 0;
+  std::vector<Container> containers, init_containers;
+  Res overhead;
+  StrMap node_selector;
+  std::vector<NodeSelectorTerm> required_node_terms;  // OR of terms
+  bool has_required_node_affinity = false;
+  std::vector<PreferredSchedulingTerm> preferred_node_terms;
+  std::vector<Toleration> tolerations;
+  std::vector<PodAffinityTerm> pod_affinity_required, pod_anti_affinity_required;
+  std::vector<WeightedPodAffinityTerm> pod_affinity_preferred, pod_anti_affinity_preferred;
+  MicroTime start_time = 0;
+
+  // ---- derived at parse time ----
+  Res request;          // computePodResourceRequest: max(sum(containers), each init) + overhead
+  Res nonzero_request;  // cpu/memory with scheduler defaults for zero requests
+  Res limit_sum;        // Σ container limits (FlexGPU accounting uses limits)
+  QoS qos = QoS::BestEffort;
+  std::string pod_group;  // value of kPodGroupLabel ("" if none)
+  std::vector<ContainerPort> host_ports;
+  GpuAssignment gpu;      // decoded from annotations (mutable via cache only)
+
+  const std::string& ns() const { return meta.ns; }
+  const std::string& name() const { return meta.name; }
+  const std::string& uid() const { return meta.uid; }
+  std::string key() const { return meta.ns + "/" + meta.name; }
+  bool terminating() const { return meta.deletion != 0; }
+  std::string pg_full_name() const { return pod_group.empty() ? std::string() : meta.ns + "/" + pod_group; }
+
+  static std::shared_ptr<Pod> from_json(const Json& obj);
+  void recompute_gpu_assignment();
+};
+using PodPtr = std::shared_ptr<Pod>;
+
+struct Node {
+  ObjectMeta meta;
+  Res allocatable, capacity;
+  bool unschedulable = false;
+  std::vector<Taint> taints;
+  // MI355X GPU topology as published by the node agent (see flexgpu.cc).
+  int gpu_count = 0;
+  std::vector<int> gpu_partitions;  // partitions per physical GPU (1 = SPX .. 8 = CPX)
+  std::vector<int> gpu_numa;        // NUMA node per GPU (-1 unknown)
+  int64_t gpu_memory_per_gpu = 0;   // memory slice units per physical GPU
+  const std::string& name() const { return meta.name; }
+  static std::shared_ptr<Node> from_json(const Json& obj);
+};
+using NodePtr = std::shared_ptr<Node>;
+
+struct PodGroup {
+  ObjectMeta meta;
+  int32_t min_member = 0;
+  bool has_min_resources = false;
+  Res min_resources;
+  int32_t schedule_timeout_seconds = -1;  // -1 = unset
+  std::string phase, occupied_by;
+  int32_t scheduled = 0, running = 0, succeeded = 0, failed = 0;
+  MicroTime schedule_start_time = 0;
+  static std::shared_ptr<PodGroup> from_json(const Json& obj);
+};
+using PodGroupPtr = std::shared_ptr<PodGroup>;
+
+struct ElasticQuota {
+  ObjectMeta meta;
+  Res min, max, used;
+  bool has_min = false, has_max = false;
+  static std::shared_ptr<ElasticQuota> from_json(const Json& obj);
+};
+using ElasticQuotaPtr = std::shared_ptr<ElasticQuota>;
+
+struct NRTResourceInfo {
+  std::string name;
+  int64_t capacity = 0, allocatable = 0, available = 0;  // in scheduler units
+  int res = -1;
+};
+struct NRTZone {
+  std::string name, type;
+  int numa_id = -1;  // parsed from "node-<id>"
+  std::vector<NRTResourceInfo> resources;
+  std::vector<std::pair<std::string, int64_t>> costs;
+};
+struct NodeResourceTopology {
+  ObjectMeta meta;
+  std::vector<std::string> topology_policies;
+  std::vector<NRTZone> zones;
+  static std::shared_ptr<NodeResourceTopology> from_json(const Json& obj);
+};
+using NRTPtr = std::shared_ptr<NodeResourceTopology>;
+
+struct PodDisruptionBudget {
+  ObjectMeta meta;
+  LabelSelector selector;
+  int32_t disruptions_allowed = 0;
+  StrMap disrupted_pods;  // status.disruptedPods: pod name -> time
+  static std::shared_ptr<PodDisruptionBudget> from_json(const Json& obj);
+};
+using PDBPtr = std::shared_ptr<PodDisruptionBudget>;
+
+struct PriorityClass {
+  ObjectMeta meta;
+  int32_t value = 0;
+  bool global_default = false;
+  std::string preemption_policy;
+  static std::shared_ptr<PriorityClass> from_json(const Json& obj);
+};
+using PriorityClassPtr = std::shared_ptr<PriorityClass>;
+
+// Global GPU naming used by pod/node parsing (configured by FlexGPU args).
+struct GpuNames {
+  std::string gpu = "amd.com/gpu";
+  std::string memory = "amd.com/gpu-memory";
+  std::string xcd = "amd.com/gpu-xcd";
+  std::string index_annotation = "amd.com/gpu-index";
+  std::string partition_annotation = "amd.com/gpu-partitions";
+  std::string partition_label = "amd.com/gpu.compute-partition";     // spx|dpx|qpx|cpx
+  std::string topology_annotation = "amd.com/gpu-topology";          // JSON, per-GPU detail
+  int gpu_id() const;
+  int memory_id() const;
+  int xcd_id() const;
+};
+GpuNames& gpu_names();
+int partitions_for_mode(const std::string& mode);  // spx=1 dpx=2 qpx=4 cpx=8 (0 unknown)
+
+}  // namespace xsched

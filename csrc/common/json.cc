@@ -1,0 +1,422 @@
+#include "common/json.h"
+
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+namespace xsched {
+
+namespace {
+const std::string kEmptyString;
+const Json::Array kEmptyArray;
+const Json::Object kEmptyObject;
+
+class Parser {
+ public:
+  explicit Parser(std::string_view s) : p_(s.data()), end_(s.data() + s.size()) {}
+
+  Json parse_document() {
+    ws();
+    Json v = value(0);
+    ws();
+    if (p_ != end_) fail("trailing characters");
+    return v;
+  }
+
+ private:
+  const char* p_;
+  const char* end_;
+
+  [[noreturn]] void fail(const char* what) {
+    throw JsonError(std::string("json parse error: ") + what);
+  }
+  void ws() {
+    while (p_ < end_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+  }
+  bool lit(const char* l, size_t n) {
+    if (static_cast<size_t>(end_ - p_) >= n && std::memcmp(p_, l, n) == 0) {
+      p_ += n;
+      return true;
+    }
+    return false;
+  }
+
+  Json value(int depth) {
+    if (depth > 256) fail("nesting too deep");
+    if (p_ >= end_) fail("unexpected end");
+    switch (*p_) {
+      case '{': return object(depth);
+      case '[': return array(depth);
+      case '"': return Json(string());
+      case 't': if (lit("true", 4)) return Json(true); fail("bad literal");
+      case 'f': if (lit("false", 5)) return Json(false); fail("bad literal");
+      case 'n': if (lit("null", 4)) return Json(); fail("bad literal");
+      default: return number();
+    }
+  }
+
+  Json object(int depth) {
+    ++p_;
+    Json o = Json::object();
+    auto& m = o.members_mut();
+    ws();
+    if (p_ < end_ && *p_ == '}') { ++p_; return o; }
+    for (;;) {
+      ws();
+      if (p_ >= end_ || *p_ != '"') fail("expected key");
+      std::string k = string();
+      ws();
+      if (p_ >= end_ || *p_ != ':') fail("expected ':'");
+      ++p_;
+      ws();
+      Json v = value(depth + 1);
+      // Duplicate keys: last one wins (encoding/json semantics).
+      bool replaced = false;
+      for (auto& kv : m) {
+        if (kv.first == k) { kv.second = std::move(v); replaced = true; break; }
+      }
+      if (!replaced) m.emplace_back(std::move(k), std::move(v));
+      ws();
+      if (p_ < end_ && *p_ == ',') { ++p_; continue; }
+      if (p_ < end_ && *p_ == '}') { ++p_; return o; }
+      fail("expected ',' or '}'");
+    }
+  }
+
+  Json array(int depth) {
+    ++p_;
+    Json a = Json::array();
+    auto& items = a.items_mut();
+    ws();
+    if (p_ < end_ && *p_ == ']') { ++p_; return a; }
+    for (;;) {
+      ws();
+      items.push_back(value(depth + 1));
+      ws();
+      if (p_ < end_ && *p_ == ',') { ++p_; continue; }
+      if (p_ < end_ && *p_ == ']') { ++p_; return a; }
+      fail("expected ',' or ']'");
+    }
+  }
+
+  static void put_utf8(std::string& out, uint32_t cp) {
+    if (cp < 0x80) {
+      out.push_back(static_cast<char>(cp));
+    } else if (cp < 0x800) {
+      out.push_back(static_cast<char>(0xC0 | (cp >> 6)));
+      out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+      out.push_back(static_cast<char>(0xE0 | (cp >> 12)));
+      out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+      out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    } else {
+      out.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+      out.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+      out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+      out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    }
+  }
+
+  uint32_t hex4() {
+    if (end_ - p_ < 4) fail("bad \\u escape");
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) {
+      char c = *p_++;
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= c - '0';
+      else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+      else fail("bad hex digit");
+    }
+    return v;
+  }
+
+  std::string string() {
+    ++p_;  // opening quote
+    std::string out;
+    const char* run = p_;
+    while (p_ < end_) {
+      char c = *p_;
+      if (c == '"') {
+        out.append(run, p_);
+        ++p_;
+        return out;
+      }
+      if (c == '\\') {
+        out.append(run, p_);
+        ++p_;
+        if (p_ >= end_) fail("bad escape");
+        char e = *p_++;
+        switch (e) {
+          case '"': out.push_back('"'); break;
+          case '\\': out.push_back('\\'); break;
+          case '/': out.push_back('/'); break;
+          case 'b': out.push_back('\b'); break;
+          case 'f': out.push_back('\f'); break;
+          case 'n': out.push_back('\n'); break;
+          case 'r': out.push_back('\r'); break;
+          case 't': out.push_back('\t'); break;
+          case 'u': {
+            uint32_t cp = hex4();
+            if (cp >= 0xD800 && cp <= 0xDBFF && end_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
+              p_ += 2;
+              uint32_t lo = hex4();
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            }
+            put_utf8(out, cp);
+            break;
+          }
+          default: fail("bad escape");
+        }
+        run = p_;
+        continue;
+      }
+      ++p_;
+    }
+    fail("unterminated string");
+  }
+
+  Json number() {
+    const char* start = p_;
+    bool is_float = false;
+    if (p_ < end_ && (*p_ == '-' || *p_ == '+')) ++p_;
+    while (p_ < end_) {
+      char c = *p_;
+      if (c >= '0' && c <= '9') { ++p_; continue; }
+      if (c == '.' || c == 'e' || c == 'E' || c == '-' || c == '+') { is_float = true; ++p_; continue; }
+      break;
+    }
+    if (p_ == start) fail("unexpected character");
+    std::string tok(start, p_);
+    if (!is_float) {
+      errno = 0;
+      char* e = nullptr;
+      long long v = std::strtoll(tok.c_str(), &e, 10);
+      if (errno == 0 && e && *e == '\0') return Json(static_cast<int64_t>(v));
+    }
+    char* e = nullptr;
+    double d = std::strtod(tok.c_str(), &e);
+    if (!e || *e != '\0') fail("bad number");
+    return Json(d);
+  }
+};
+
+void dump_string(std::string& out, const std::string& s) {
+  out.push_back('"');
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\n': out += "\\n"; break;
+      case '\r': out += "\\r"; break;
+      case '\t': out += "\\t"; break;
+      case '\b': out += "\\b"; break;
+      case '\f': out += "\\f"; break;
+      default:
+        if (c < 0x20) {
+          char buf[8];
+          std::snprintf(buf, sizeof buf, "\\u%04x", c);
+          out += buf;
+        } else {
+          out.push_back(static_cast<char>(c));
+        }
+    }
+  }
+  out.push_back('"');
+}
+}  // namespace
+
+const std::string& Json::as_string() const { return t_ == Type::String ? s_ : kEmptyString; }
+const Json::Array& Json::items() const { return t_ == Type::Array ? a_ : kEmptyArray; }
+Json::Array& Json::items_mut() {
+  if (t_ != Type::Array) { *this = array(); }
+  return a_;
+}
+const Json::Object& Json::members() const { return t_ == Type::Object ? o_ : kEmptyObject; }
+Json::Object& Json::members_mut() {
+  if (t_ != Type::Object) { *this = object(); }
+  return o_;
+}
+
+const Json* Json::get(std::string_view key) const {
+  if (t_ != Type::Object) return nullptr;
+  for (const auto& kv : o_)
+    if (kv.first == key) return &kv.second;
+  return nullptr;
+}
+
+Json* Json::get_mut(std::string_view key) {
+  if (t_ != Type::Object) return nullptr;
+  for (auto& kv : o_)
+    if (kv.first == key) return &kv.second;
+  return nullptr;
+}
+
+const Json* Json::path(std::initializer_list<std::string_view> keys) const {
+  const Json* cur = this;
+  for (auto k : keys) {
+    cur = cur->get(k);
+    if (!cur) return nullptr;
+  }
+  return cur;
+}
+
+const Json& Json::operator[](std::string_view key) const {
+  const Json* v = get(key);
+  return v ? *v : json_null();
+}
+
+Json& Json::set(std::string_view key, Json v) {
+  auto& m = members_mut();
+  for (auto& kv : m) {
+    if (kv.first == key) {
+      kv.second = std::move(v);
+      return kv.second;
+    }
+  }
+  m.emplace_back(std::string(key), std::move(v));
+  return m.back().second;
+}
+
+Json& Json::at_or_create(std::string_view key) {
+  auto& m = members_mut();
+  for (auto& kv : m)
+    if (kv.first == key) {
+      if (!kv.second.is_object()) kv.second = object();
+      return kv.second;
+    }
+  m.emplace_back(std::string(key), object());
+  return m.back().second;
+}
+
+bool Json::erase(std::string_view key) {
+  if (t_ != Type::Object) return false;
+  for (auto it = o_.begin(); it != o_.end(); ++it) {
+    if (it->first == key) {
+      o_.erase(it);
+      return true;
+    }
+  }
+  return false;
+}
+
+void Json::push_back(Json v) { items_mut().push_back(std::move(v)); }
+
+bool Json::operator==(const Json& o) const {
+  if (is_number() && o.is_number()) {
+    if (t_ == Type::Int && o.t_ == Type::Int) return i_ == o.i_;
+    return as_double() == o.as_double();
+  }
+  if (t_ != o.t_) return false;
+  switch (t_) {
+    case Type::Null: return true;
+    case Type::Bool: return i_ == o.i_;
+    case Type::String: return s_ == o.s_;
+    case Type::Array: return a_ == o.a_;
+    case Type::Object: {
+      if (o_.size() != o.o_.size()) return false;
+      for (const auto& kv : o_) {
+        const Json* other = o.get(kv.first);
+        if (!other || !(*other == kv.second)) return false;
+      }
+      return true;
+    }
+    default: return false;
+  }
+}
+
+void Json::dump_to(std::string& out) const {
+  switch (t_) {
+    case Type::Null: out += "null"; break;
+    case Type::Bool: out += i_ ? "true" : "false"; break;
+    case Type::Int: out += std::to_string(i_); break;
+    case Type::Double: {
+      if (!std::isfinite(d_)) { out += "null"; break; }
+      char buf[32];
+      std::snprintf(buf, sizeof buf, "%.17g", d_);
+      out += buf;
+      break;
+    }
+    case Type::String: dump_string(out, s_); break;
+    case Type::Array: {
+      out.push_back('[');
+      bool first = true;
+      for (const auto& v : a_) {
+        if (!first) out.push_back(',');
+        first = false;
+        v.dump_to(out);
+      }
+      out.push_back(']');
+      break;
+    }
+    case Type::Object: {
+      out.push_back('{');
+      bool first = true;
+      for (const auto& kv : o_) {
+        if (!first) out.push_back(',');
+        first = false;
+        dump_string(out, kv.first);
+        out.push_back(':');
+        kv.second.dump_to(out);
+      }
+      out.push_back('}');
+      break;
+    }
+  }
+}
+
+std::string Json::dump() const {
+  std::string out;
+  out.reserve(256);
+  dump_to(out);
+  return out;
+}
+
+Json Json::parse(std::string_view text) { return Parser(text).parse_document(); }
+
+void Json::merge_patch(const Json& patch) {
+  if (!patch.is_object()) {
+    *this = patch;
+    return;
+  }
+  if (!is_object()) *this = object();
+  for (const auto& kv : patch.o_) {
+    if (kv.second.is_null()) {
+      erase(kv.first);
+    } else if (kv.second.is_object()) {
+      Json* cur = get_mut(kv.first);
+      if (cur && cur->is_object()) {
+        cur->merge_patch(kv.second);
+      } else {
+        Json fresh = object();
+        fresh.merge_patch(kv.second);
+        set(kv.first, std::move(fresh));
+      }
+    } else {
+      set(kv.first, kv.second);
+    }
+  }
+}
+
+Json Json::diff_merge_patch(const Json& from, const Json& to) {
+  if (!from.is_object() || !to.is_object()) return to;
+  Json patch = object();
+  for (const auto& kv : from.o_) {
+    if (!to.get(kv.first)) patch.set(kv.first, Json());
+  }
+  for (const auto& kv : to.o_) {
+    const Json* old = from.get(kv.first);
+    if (!old) {
+      patch.set(kv.first, kv.second);
+    } else if (!(*old == kv.second)) {
+      if (old->is_object() && kv.second.is_object())
+        patch.set(kv.first, diff_merge_patch(*old, kv.second));
+      else
+        patch.set(kv.first, kv.second);
+    }
+  }
+  return patch;
+}
+
+}  // namespace xsched

@@ -1,0 +1,123 @@
+// Minimal JSON DOM used as the wire/storage format of the object store.
+//
+// Kubernetes objects are JSON documents; the reference reaches them through
+// client-go's typed structs (vendor/k8s.io/api/core/v1/types.go). We keep the
+// document form in the store (so unknown fields, merge patches and the REST
+// adapter round-trip losslessly) and parse typed views (api/types.h) out of it
+// only where the scheduler needs them.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <utility>
+#include <vector>
+
+namespace xsched {
+
+class Json;
+using JsonPtr = std::shared_ptr<const Json>;
+
+class JsonError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+class Json {
+ public:
+  enum class Type : uint8_t { Null, Bool, Int, Double, String, Array, Object };
+  using Array = std::vector<Json>;
+  using Member = std::pair<std::string, Json>;
+  using Object = std::vector<Member>;  // insertion ordered; objects are small
+
+  Json() = default;
+  Json(std::nullptr_t) {}
+  Json(bool b) : t_(Type::Bool), i_(b) {}
+  Json(int v) : t_(Type::Int), i_(v) {}
+  Json(int64_t v) : t_(Type::Int), i_(v) {}
+  Json(uint64_t v) : t_(Type::Int), i_(static_cast<int64_t>(v)) {}
+  Json(double v) : t_(Type::Double), d_(v) {}
+  Json(const char* s) : t_(Type::String), s_(s) {}
+  Json(std::string s) : t_(Type::String), s_(std::move(s)) {}
+  Json(std::string_view s) : t_(Type::String), s_(s) {}
+
+  static Json array() { Json j; j.t_ = Type::Array; return j; }
+  static Json object() { Json j; j.t_ = Type::Object; return j; }
+
+  Type type() const { return t_; }
+  bool is_null() const { return t_ == Type::Null; }
+  bool is_bool() const { return t_ == Type::Bool; }
+  bool is_int() const { return t_ == Type::Int; }
+  bool is_number() const { return t_ == Type::Int || t_ == Type::Double; }
+  bool is_string() const { return t_ == Type::String; }
+  bool is_array() const { return t_ == Type::Array; }
+  bool is_object() const { return t_ == Type::Object; }
+
+  bool as_bool(bool dflt = false) const { return t_ == Type::Bool ? i_ != 0 : dflt; }
+  int64_t as_int(int64_t dflt = 0) const {
+    if (t_ == Type::Int) return i_;
+    if (t_ == Type::Double) return static_cast<int64_t>(d_);
+    return dflt;
+  }
+  double as_double(double dflt = 0.0) const {
+    if (t_ == Type::Double) return d_;
+    if (t_ == Type::Int) return static_cast<double>(i_);
+    return dflt;
+  }
+  const std::string& as_string() const;  // "" for non-strings
+  std::string str_or(std::string_view dflt) const {
+    return t_ == Type::String ? s_ : std::string(dflt);
+  }
+
+  const Array& items() const;  // empty for non-arrays
+  Array& items_mut();
+  const Object& members() const;  // empty for non-objects
+  Object& members_mut();
+
+  size_t size() const {
+    return t_ == Type::Array ? a_.size() : t_ == Type::Object ? o_.size() : 0;
+  }
+
+  // Object access. get() returns nullptr when missing / not an object.
+  const Json* get(std::string_view key) const;
+  Json* get_mut(std::string_view key);
+  // Path lookup: get_path({"metadata","name"}).
+  const Json* path(std::initializer_list<std::string_view> keys) const;
+  const Json& operator[](std::string_view key) const;  // null sentinel when missing
+  Json& set(std::string_view key, Json v);  // insert or replace
+  Json& at_or_create(std::string_view key);  // creates an empty object if missing
+  bool erase(std::string_view key);
+  void push_back(Json v);
+
+  bool operator==(const Json& o) const;
+  bool operator!=(const Json& o) const { return !(*this == o); }
+
+  std::string dump() const;
+  void dump_to(std::string& out) const;
+  static Json parse(std::string_view text);
+
+  // RFC 7386 JSON merge patch (the "application/merge-patch+json" patch type
+  // used by the reference's util.CreateMergePatch callers).
+  void merge_patch(const Json& patch);
+  // Produce a merge patch that turns `from` into `to`.
+  static Json diff_merge_patch(const Json& from, const Json& to);
+
+ private:
+  Type t_ = Type::Null;
+  union {
+    int64_t i_ = 0;
+    double d_;
+  };
+  std::string s_;
+  Array a_;
+  Object o_;
+};
+
+inline const Json& json_null() {
+  static const Json n;
+  return n;
+}
+
+}  // namespace xsched

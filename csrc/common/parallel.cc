@@ -1,0 +1,84 @@
+#include "common/parallel.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace xsched {
+
+Parallelizer::Parallelizer(int workers, int inline_below) : workers_(std::max(1, workers)), inline_below_(inline_below) {
+  for (int i = 0; i < workers_ - 1; ++i) threads_.emplace_back([this] { worker_loop(); });
+}
+
+Parallelizer::~Parallelizer() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void Parallelizer::run_job(Job& job) {
+  for (;;) {
+    if (job.stop && job.stop->load(std::memory_order_relaxed)) return;
+    int start = job.next.fetch_add(job.chunk, std::memory_order_relaxed);
+    if (start >= job.n) return;
+    int end = std::min(job.n, start + job.chunk);
+    for (int i = start; i < end; ++i) {
+      if (job.stop && job.stop->load(std::memory_order_relaxed)) return;
+      (*job.fn)(i);
+    }
+  }
+}
+
+void Parallelizer::worker_loop() {
+  uint64_t seen = 0;
+  for (;;) {
+    Job* job = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || (job_ != nullptr && job_gen_ != seen); });
+      if (stop_) return;
+      seen = job_gen_;
+      job = job_;
+      job->active.fetch_add(1);
+    }
+    run_job(*job);
+    if (job->active.fetch_sub(1) == 1) {
+      std::lock_guard<std::mutex> g(mu_);
+      done_cv_.notify_all();
+    }
+  }
+}
+
+void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop) {
+  if (n <= 0) return;
+  if (n < inline_below_ || threads_.empty()) {
+    for (int i = 0; i < n; ++i) {
+      if (stop && stop->load(std::memory_order_relaxed)) return;
+      fn(i);
+    }
+    return;
+  }
+  std::lock_guard<std::mutex> call(call_mu_);
+  Job job;
+  job.fn = &fn;
+  job.stop = stop;
+  job.n = n;
+  // chunkSizeFor: sqrt(n) capped so every worker gets work.
+  job.chunk = std::max(1, std::min(static_cast<int>(std::sqrt(static_cast<double>(n))), n / workers_ + 1));
+  job.active.store(1);  // the caller
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    job_ = &job;
+    ++job_gen_;
+  }
+  cv_.notify_all();
+  run_job(job);
+  std::unique_lock<std::mutex> lk(mu_);
+  job_ = nullptr;  // no new worker can join after this point
+  job.active.fetch_sub(1);
+  done_cv_.wait(lk, [&] { return job.active.load() == 0; });
+}
+
+}  // namespace xsched

@@ -1,0 +1,56 @@
+// Fork-join parallelizer for node-parallel Filter/Score/preemption dry runs.
+//
+// Equivalent role to the reference's framework/parallelize.Parallelizer
+// (vendor/.../framework/parallelize/parallelism.go:27, 16 workers,
+// workqueue.ParallelizeUntil with chunking). Workers are persistent; the
+// calling thread participates; work is claimed in chunks from an atomic
+// cursor so small node counts stay on the caller (no wakeups at all below
+// `inline_below` items).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace xsched {
+
+class Parallelizer {
+ public:
+  explicit Parallelizer(int workers = 16, int inline_below = 64);
+  ~Parallelizer();
+  Parallelizer(const Parallelizer&) = delete;
+  Parallelizer& operator=(const Parallelizer&) = delete;
+
+  // Runs fn(i) for i in [0, n). `stop` (optional) is polled between items to
+  // allow early exit (e.g. enough feasible nodes found).
+  void until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop = nullptr);
+  int workers() const { return workers_; }
+
+ private:
+  struct Job {
+    const std::function<void(int)>* fn = nullptr;
+    const std::atomic<bool>* stop = nullptr;
+    int n = 0;
+    int chunk = 1;
+    std::atomic<int> next{0};
+    std::atomic<int> active{0};
+  };
+  void worker_loop();
+  void run_job(Job& job);
+
+  int workers_;
+  int inline_below_;
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  Job* job_ = nullptr;
+  uint64_t job_gen_ = 0;
+  bool stop_ = false;
+  std::mutex call_mu_;  // one job at a time
+};
+
+}  // namespace xsched

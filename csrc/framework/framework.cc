@@ -1,0 +1,433 @@
+#include "framework/framework.h"
+
+#include <algorithm>
+#include <atomic>
+#include <stdexcept>
+
+#include "scheduler/metrics.h"
+#include "scheduler/queue.h"
+
+namespace xsched {
+
+namespace {
+const std::pair<const char*, uint32_t> kPointNames[] = {
+    {"queueSort", kQueueSort}, {"preFilter", kPreFilter}, {"filter", kFilter},   {"postFilter", kPostFilter},
+    {"preScore", kPreScore},   {"score", kScore},         {"reserve", kReserve}, {"permit", kPermit},
+    {"preBind", kPreBind},     {"bind", kBind},           {"postBind", kPostBind},
+};
+}  // namespace
+
+const char* ext_point_name(uint32_t p) {
+  for (const auto& kv : kPointNames)
+    if (kv.second == p) return kv.first;
+  return "unknown";
+}
+
+uint32_t ext_point_from_name(const std::string& n) {
+  for (const auto& kv : kPointNames)
+    if (n == kv.first) return kv.second;
+  return 0;
+}
+
+// ------------------------------------------------------------ Registry ----
+Registry& Registry::global() {
+  static Registry* r = new Registry();
+  return *r;
+}
+
+void Registry::add(const std::string& name, PluginFactory f) { factories_[name] = std::move(f); }
+
+PluginPtr Registry::make(const std::string& name, const Json& args, Handle& h) const {
+  auto it = factories_.find(name);
+  if (it == factories_.end()) throw std::runtime_error("plugin \"" + name + "\" does not exist");
+  return it->second(args, h);
+}
+
+std::vector<std::string> Registry::names() const {
+  std::vector<std::string> out;
+  for (const auto& kv : factories_) out.push_back(kv.first);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+void default_normalize_score(int64_t max_priority, bool reverse, std::vector<NodeScore>& scores) {
+  int64_t max_count = 0;
+  for (const auto& s : scores) max_count = std::max(max_count, s.score);
+  if (max_count == 0) {
+    if (reverse)
+      for (auto& s : scores) s.score = max_priority;
+    return;
+  }
+  for (auto& s : scores) {
+    int64_t sc = max_priority * s.score / max_count;
+    if (reverse) sc = max_priority - sc;
+    s.score = sc;
+  }
+}
+
+// ------------------------------------------------------- ProfileConfig ----
+ProfileConfig ProfileConfig::from_json(const Json& j) {
+  ProfileConfig c;
+  c.scheduler_name = j["schedulerName"].str_or(kDefaultSchedulerName);
+  for (const auto& kv : j["plugins"].members()) {
+    uint32_t pt = ext_point_from_name(kv.first);
+    if (!pt) throw std::runtime_error("unknown extension point " + kv.first);
+    auto& vec = c.enabled[pt];
+    for (const auto& e : kv.second.items()) {
+      std::string name = e.is_string() ? e.as_string() : e["name"].as_string();
+      vec.push_back(name);
+      if (pt == kScore) c.score_weights[name] = e.is_object() ? std::max<int64_t>(1, e["weight"].as_int(1)) : 1;
+    }
+  }
+  for (const auto& kv : j["pluginConfig"].members()) c.plugin_args[kv.first] = kv.second;
+  c.percentage_of_nodes_to_score = static_cast<int>(j["percentageOfNodesToScore"].as_int(0));
+  c.run_all_filters = j["runAllFilters"].as_bool(false);
+  return c;
+}
+
+// ----------------------------------------------------------- Framework ----
+Framework::Framework(const ProfileConfig& cfg, Handle handle) : cfg_(cfg), handle_(handle) {
+  handle_.framework = this;
+  auto& reg = Registry::global();
+  for (const auto& [pt, names] : cfg_.enabled) {
+    for (const auto& name : names) {
+      PluginPtr p;
+      auto it = by_name_.find(name);
+      if (it != by_name_.end()) {
+        p = it->second;
+      } else {
+        auto ait = cfg_.plugin_args.find(name);
+        p = reg.make(name, ait == cfg_.plugin_args.end() ? Json::object() : ait->second, handle_);
+        by_name_[name] = p;
+        all_.push_back(p);
+      }
+      if (!(p->points() & pt))
+        throw std::runtime_error("plugin \"" + name + "\" does not extend " + ext_point_name(pt) + " plugin");
+      auto& chain = chain_[pt];
+      if (std::find(chain.begin(), chain.end(), p) != chain.end())
+        throw std::runtime_error("plugin \"" + name + "\" already registered as \"" + ext_point_name(pt) + "\"");
+      chain.push_back(p);
+      if (pt == kScore) scorers_.emplace_back(p, cfg_.score_weights.count(name) ? cfg_.score_weights[name] : 1);
+    }
+  }
+  auto qs = chain_.find(kQueueSort);
+  if (qs == chain_.end() || qs->second.size() != 1)
+    throw std::runtime_error("one queue sort plugin required for profile " + cfg_.scheduler_name);
+  queue_sort_ = qs->second.front();
+  auto bd = chain_.find(kBind);
+  if (bd == chain_.end() || bd->second.empty())
+    throw std::runtime_error("at least one bind plugin is needed for profile " + cfg_.scheduler_name);
+}
+
+Framework::~Framework() = default;
+
+PluginPtr Framework::plugin(const std::string& name) const {
+  auto it = by_name_.find(name);
+  return it == by_name_.end() ? nullptr : it->second;
+}
+
+bool Framework::has(uint32_t point) const {
+  auto it = chain_.find(point);
+  return it != chain_.end() && !it->second.empty();
+}
+
+bool Framework::less(const QueuedPodInfo& a, const QueuedPodInfo& b) const { return queue_sort_->less(a, b); }
+
+void Framework::record(const char* point, const Status& st, int64_t start_us, CycleState& s) {
+  if (!s.record_metrics || !handle_.metrics) return;
+  double d = static_cast<double>(handle_.clock->now_us() - start_us) / 1e6;
+  handle_.metrics
+      ->histogram("scheduler_framework_extension_point_duration_seconds",
+                  std::string("extension_point=\"") + point + "\",profile=\"" + cfg_.scheduler_name + "\",status=\"" +
+                      code_name(st.code()) + "\"")
+      .observe(d);
+}
+
+Status Framework::run_pre_filter(CycleState& s, const Pod& p) {
+  int64_t t0 = s.record_metrics ? handle_.clock->now_us() : 0;
+  auto it = chain_.find(kPreFilter);
+  if (it != chain_.end()) {
+    for (const auto& pl : it->second) {
+      Status st = pl->pre_filter(s, p);
+      if (!st.is_success()) {
+        st.with_plugin(pl->name());
+        if (st.code() == Code::Error) {
+          Status e(Code::Error, "running PreFilter plugin \"" + pl->name() + "\": " + st.message());
+          e.with_plugin(pl->name());
+          record("PreFilter", e, t0, s);
+          return e;
+        }
+        record("PreFilter", st, t0, s);
+        return st;
+      }
+    }
+  }
+  record("PreFilter", Status(), t0, s);
+  return {};
+}
+
+Status Framework::run_pre_filter_add_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_add,
+                                         const NodeInfo& ni) {
+  auto it = chain_.find(kPreFilter);
+  if (it == chain_.end()) return {};
+  for (const auto& pl : it->second) {
+    if (!pl->has_pre_filter_extensions()) continue;
+    Status st = pl->add_pod(s, to_schedule, to_add, ni);
+    if (!st.is_success()) return Status(Code::Error, "running AddPod on PreFilter plugin " + pl->name() + ": " + st.message());
+  }
+  return {};
+}
+
+Status Framework::run_pre_filter_remove_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_remove,
+                                            const NodeInfo& ni) {
+  auto it = chain_.find(kPreFilter);
+  if (it == chain_.end()) return {};
+  for (const auto& pl : it->second) {
+    if (!pl->has_pre_filter_extensions()) continue;
+    Status st = pl->remove_pod(s, to_schedule, to_remove, ni);
+    if (!st.is_success())
+      return Status(Code::Error, "running RemovePod on PreFilter plugin " + pl->name() + ": " + st.message());
+  }
+  return {};
+}
+
+Status Framework::run_filter(CycleState& s, const Pod& p, const NodeInfo& ni) {
+  auto it = chain_.find(kFilter);
+  if (it == chain_.end()) return {};
+  Status merged;
+  bool failed = false;
+  for (const auto& pl : it->second) {
+    Status st = pl->filter(s, p, ni);
+    if (st.is_success()) continue;
+    if (!st.is_unschedulable()) {
+      Status e(Code::Error, "running \"" + pl->name() + "\" filter plugin: " + st.message());
+      e.with_plugin(pl->name());
+      return e;
+    }
+    st.with_plugin(pl->name());
+    if (!cfg_.run_all_filters) return st;
+    if (!failed) {
+      merged = st;
+      failed = true;
+    }
+  }
+  return failed ? merged : Status();
+}
+
+Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, const NodeInfo& ni) {
+  Status st;
+  bool pods_added = false;
+  for (int i = 0; i < 2; ++i) {
+    CycleState* state_to_use = &s;
+    const NodeInfo* ni_to_use = &ni;
+    std::shared_ptr<CycleState> state_out;
+    std::shared_ptr<NodeInfo> ni_out;
+    if (i == 0) {
+      std::vector<PodPtr> nominated;
+      if (handle_.nominator && ni.node) nominated = handle_.nominator->nominated_pods_for_node(ni.name());
+      for (const auto& np : nominated) {
+        if (np->priority < p.priority || np->uid() == p.uid()) continue;
+        if (!ni_out) {
+          ni_out = ni.clone();
+          state_out = s.clone();
+        }
+        ni_out->add_pod(np);
+        Status ast = run_pre_filter_add_pod(*state_out, p, np, *ni_out);
+        if (!ast.is_success()) return ast;
+        pods_added = true;
+      }
+      if (pods_added) {
+        state_to_use = state_out.get();
+        ni_to_use = ni_out.get();
+      }
+    } else if (!pods_added || !st.is_success()) {
+      break;
+    }
+    st = run_filter(*state_to_use, p, *ni_to_use);
+    if (!st.is_success() && !st.is_unschedulable()) return st;
+  }
+  return st;
+}
+
+std::pair<PostFilterResult, Status> Framework::run_post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m) {
+  int64_t t0 = s.record_metrics ? handle_.clock->now_us() : 0;
+  auto it = chain_.find(kPostFilter);
+  Status last(Code::Unschedulable);
+  if (it != chain_.end()) {
+    for (const auto& pl : it->second) {
+      auto [res, st] = pl->post_filter(s, p, m);
+      if (st.is_success()) {
+        record("PostFilter", st, t0, s);
+        return {res, st};
+      }
+      if (!st.is_unschedulable()) {
+        record("PostFilter", st, t0, s);
+        return {PostFilterResult{}, Status(Code::Error, st.message()).with_plugin(pl->name())};
+      }
+      last = st;
+      last.with_plugin(pl->name());
+    }
+  }
+  record("PostFilter", last, t0, s);
+  return {PostFilterResult{}, last};
+}
+
+Status Framework::run_pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) {
+  auto it = chain_.find(kPreScore);
+  if (it == chain_.end()) return {};
+  for (const auto& pl : it->second) {
+    Status st = pl->pre_score(s, p, nodes);
+    if (!st.is_success()) return Status(Code::Error, "running PreScore plugin " + pl->name() + ": " + st.message());
+  }
+  return {};
+}
+
+Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes,
+                            std::vector<NodeScore>& total) {
+  int64_t t0 = s.record_metrics ? handle_.clock->now_us() : 0;
+  size_t n = nodes.size();
+  total.assign(n, NodeScore{});
+  for (size_t i = 0; i < n; ++i) total[i].name = nodes[i]->name();
+  if (scorers_.empty()) return {};
+  std::vector<std::vector<NodeScore>> per(scorers_.size(), std::vector<NodeScore>(n));
+  std::atomic<bool> failed{false};
+  std::string err;
+  std::mutex err_mu;
+  // Node-parallel scoring: one task per node runs every score plugin.
+  handle_.parallelizer->until(static_cast<int>(n), [&](int i) {
+    for (size_t k = 0; k < scorers_.size(); ++k) {
+      auto [sc, st] = scorers_[k].first->score(s, p, *nodes[i]);
+      if (!st.is_success()) {
+        std::lock_guard<std::mutex> g(err_mu);
+        err = "running Score plugin " + scorers_[k].first->name() + ": " + st.message();
+        failed.store(true);
+        return;
+      }
+      per[k][i] = NodeScore{total[i].name, sc};
+    }
+  }, &failed);
+  if (failed.load()) return Status(Code::Error, err);
+  for (size_t k = 0; k < scorers_.size(); ++k) {
+    auto& pl = scorers_[k].first;
+    if (pl->has_normalize_score()) {
+      Status st = pl->normalize_score(s, p, per[k]);
+      if (!st.is_success()) return Status(Code::Error, "running Normalize on Score plugin " + pl->name() + ": " + st.message());
+    }
+    int64_t w = scorers_[k].second;
+    for (size_t i = 0; i < n; ++i) {
+      int64_t sc = per[k][i].score;
+      if (sc > kMaxNodeScore || sc < kMinNodeScore)
+        return Status(Code::Error, "plugin \"" + pl->name() + "\" returns an invalid score " + std::to_string(sc) +
+                                       ", it should in the range of [0, 100] after normalizing");
+      total[i].score += sc * w;
+    }
+  }
+  record("Score", Status(), t0, s);
+  return {};
+}
+
+Status Framework::run_reserve(CycleState& s, const PodPtr& p, const std::string& node) {
+  auto it = chain_.find(kReserve);
+  if (it == chain_.end()) return {};
+  for (const auto& pl : it->second) {
+    Status st = pl->reserve(s, p, node);
+    if (!st.is_success()) {
+      Status e(Code::Error, "running Reserve plugin \"" + pl->name() + "\": " + st.message());
+      if (st.is_unschedulable()) e = Status(st.code(), st.message());
+      e.with_plugin(pl->name());
+      return e;
+    }
+  }
+  return {};
+}
+
+void Framework::run_unreserve(CycleState& s, const PodPtr& p, const std::string& node) {
+  auto it = chain_.find(kReserve);
+  if (it == chain_.end()) return;
+  for (auto rit = it->second.rbegin(); rit != it->second.rend(); ++rit) (*rit)->unreserve(s, p, node);
+}
+
+Status Framework::run_permit(CycleState& s, const PodPtr& p, const std::string& node,
+                             std::function<void(const Status&)> on_done) {
+  auto it = chain_.find(kPermit);
+  if (it == chain_.end()) return {};
+  std::map<std::string, int64_t> timeouts;
+  for (const auto& pl : it->second) {
+    auto [st, timeout] = pl->permit(s, p, node);
+    if (st.is_success()) continue;
+    if (st.is_unschedulable()) {
+      st.with_plugin(pl->name());
+      return st;
+    }
+    if (st.is_wait()) {
+      timeouts[pl->name()] = std::min(std::max<int64_t>(timeout, 0), kMaxPermitTimeoutUs);
+      continue;
+    }
+    return Status(Code::Error, "running Permit plugin " + pl->name() + ": " + st.message()).with_plugin(pl->name());
+  }
+  if (timeouts.empty()) return {};
+  handle_.waiting_pods->add(p, node, timeouts, std::move(on_done));
+  return Status(Code::Wait, "one or more plugins asked to wait and no plugin rejected pod " + p->name());
+}
+
+Status Framework::run_pre_bind(CycleState& s, const PodPtr& p, const std::string& node) {
+  auto it = chain_.find(kPreBind);
+  if (it == chain_.end()) return {};
+  for (const auto& pl : it->second) {
+    Status st = pl->pre_bind(s, p, node);
+    if (!st.is_success()) return Status(Code::Error, "running PreBind plugin " + pl->name() + ": " + st.message());
+  }
+  return {};
+}
+
+Status Framework::run_bind(CycleState& s, const PodPtr& p, const std::string& node) {
+  auto it = chain_.find(kBind);
+  if (it == chain_.end()) return Status(Code::Skip);
+  for (const auto& pl : it->second) {
+    Status st = pl->bind(s, p, node);
+    if (st.is_skip()) continue;
+    if (!st.is_success()) return Status(Code::Error, "plugin \"" + pl->name() + "\" failed to bind pod: " + st.message());
+    return st;
+  }
+  return Status(Code::Skip);
+}
+
+void Framework::run_post_bind(CycleState& s, const PodPtr& p, const std::string& node) {
+  auto it = chain_.find(kPostBind);
+  if (it == chain_.end()) return;
+  for (const auto& pl : it->second) pl->post_bind(s, p, node);
+}
+
+std::vector<ClusterEvent> Framework::events_for(const std::string& plugin) const {
+  auto it = by_name_.find(plugin);
+  if (it == by_name_.end()) return {};
+  return it->second->events_to_register();
+}
+
+std::vector<std::string> Framework::watched_kinds() const {
+  std::vector<std::string> out;
+  for (const auto& p : all_)
+    for (const auto& k : p->watched_kinds())
+      if (std::find(out.begin(), out.end(), k) == out.end()) out.push_back(k);
+  return out;
+}
+
+void Framework::dispatch_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) {
+  for (const auto& p : all_) {
+    for (const auto& k : p->watched_kinds())
+      if (k == kind) {
+        p->on_object_event(kind, type, obj, old);
+        break;
+      }
+  }
+}
+
+void Framework::start() {
+  for (const auto& p : all_) p->start();
+}
+
+void Framework::stop() {
+  for (const auto& p : all_) p->stop();
+}
+
+}  // namespace xsched

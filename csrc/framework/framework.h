@@ -1,0 +1,81 @@
+// Per-profile framework runtime: runs the enabled plugins of each extension
+// point in configured order.
+//
+// Reference: vendor/k8s.io/kubernetes/pkg/scheduler/framework/runtime/
+// framework.go (RunPreFilterPlugins, RunFilterPluginsWithNominatedPods,
+// RunScorePlugins with weights + NormalizeScore, Reserve/Unreserve (reverse),
+// Permit with the 15-minute cap :46, PreBind/Bind/PostBind).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "framework/plugin.h"
+#include "framework/waiting_pods.h"
+
+namespace xsched {
+
+struct ProfileConfig {
+  std::string scheduler_name = kDefaultSchedulerName;
+  std::map<uint32_t, std::vector<std::string>> enabled;  // ext point -> plugin names (ordered)
+  std::map<std::string, int64_t> score_weights;
+  std::map<std::string, Json> plugin_args;
+  int percentage_of_nodes_to_score = 0;
+  bool run_all_filters = false;
+  static ProfileConfig from_json(const Json& j);
+};
+
+class Framework {
+ public:
+  Framework(const ProfileConfig& cfg, Handle handle);
+  ~Framework();
+
+  const std::string& profile_name() const { return cfg_.scheduler_name; }
+  const ProfileConfig& config() const { return cfg_; }
+  Handle& handle() { return handle_; }
+  PluginPtr plugin(const std::string& name) const;
+  const std::vector<PluginPtr>& all_plugins() const { return all_; }
+  bool has(uint32_t point) const;
+
+  bool less(const QueuedPodInfo& a, const QueuedPodInfo& b) const;
+
+  Status run_pre_filter(CycleState& s, const Pod& p);
+  Status run_pre_filter_add_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_add, const NodeInfo& ni);
+  Status run_pre_filter_remove_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_remove, const NodeInfo& ni);
+  Status run_filter(CycleState& s, const Pod& p, const NodeInfo& ni);
+  Status run_filter_with_nominated_pods(CycleState& s, const Pod& p, const NodeInfo& ni);
+  std::pair<PostFilterResult, Status> run_post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m);
+  Status run_pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes);
+  // Weighted sum of all score plugins per node (same order as `nodes`).
+  Status run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes, std::vector<NodeScore>& total);
+  Status run_reserve(CycleState& s, const PodPtr& p, const std::string& node);
+  void run_unreserve(CycleState& s, const PodPtr& p, const std::string& node);
+  // Returns Success, an unschedulable/error status, or Wait (then `on_done`
+  // fires exactly once when the pod is allowed/rejected/timed out).
+  Status run_permit(CycleState& s, const PodPtr& p, const std::string& node, std::function<void(const Status&)> on_done);
+  Status run_pre_bind(CycleState& s, const PodPtr& p, const std::string& node);
+  Status run_bind(CycleState& s, const PodPtr& p, const std::string& node);
+  void run_post_bind(CycleState& s, const PodPtr& p, const std::string& node);
+
+  std::vector<ClusterEvent> events_for(const std::string& plugin) const;
+  std::vector<std::string> watched_kinds() const;
+  void dispatch_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old);
+  void start();
+  void stop();
+
+  static constexpr int64_t kMaxPermitTimeoutUs = 15LL * 60 * 1000000;  // framework.go:46
+
+ private:
+  void record(const char* point, const Status& st, int64_t start_us, CycleState& s);
+  ProfileConfig cfg_;
+  Handle handle_;
+  std::vector<PluginPtr> all_;
+  std::map<std::string, PluginPtr> by_name_;
+  std::map<uint32_t, std::vector<PluginPtr>> chain_;
+  std::vector<std::pair<PluginPtr, int64_t>> scorers_;
+  PluginPtr queue_sort_;
+};
+
+}  // namespace xsched

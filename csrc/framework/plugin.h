@@ -1,0 +1,153 @@
+// Plugin API: one base class with a default (no-op) method per extension
+// point plus a bitmask declaring which points the plugin extends.
+//
+// Maps 1:1 to the reference's framework interfaces (vendor/k8s.io/kubernetes/
+// pkg/scheduler/framework/interface.go): QueueSort, PreFilter(+Extensions),
+// Filter, PostFilter, PreScore, Score(+NormalizeScore), Reserve/Unreserve,
+// Permit, PreBind, Bind, PostBind and EnqueueExtensions. Score receives the
+// NodeInfo directly instead of a node name + snapshot lookup.
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "common/clock.h"
+#include "common/json.h"
+#include "common/parallel.h"
+#include "framework/types.h"
+
+namespace xsched {
+
+class Framework;
+class SchedulerCache;
+class Informers;
+class WaitingPods;
+class Nominator;
+class Metrics;
+
+enum ExtPoint : uint32_t {
+  kQueueSort = 1u << 0,
+  kPreFilter = 1u << 1,
+  kFilter = 1u << 2,
+  kPostFilter = 1u << 3,
+  kPreScore = 1u << 4,
+  kScore = 1u << 5,
+  kReserve = 1u << 6,
+  kPermit = 1u << 7,
+  kPreBind = 1u << 8,
+  kBind = 1u << 9,
+  kPostBind = 1u << 10,
+};
+const char* ext_point_name(uint32_t p);
+uint32_t ext_point_from_name(const std::string& n);  // "filter" -> kFilter (0 if unknown)
+
+// Writes that plugins/scheduler issue against the API server.
+class ApiClient {
+ public:
+  virtual ~ApiClient() = default;
+  virtual void bind(const Pod& pod, const std::string& node, const Json& annotations) = 0;
+  virtual void delete_pod(const Pod& pod) = 0;
+  virtual void patch(const std::string& kind, const std::string& ns, const std::string& name, const Json& patch) = 0;
+  virtual void record_event(const std::string& kind, const std::string& ns, const std::string& name,
+                            const std::string& type, const std::string& reason, const std::string& msg) {}
+};
+
+// Everything a plugin can reach (framework.Handle).
+struct Handle {
+  Framework* framework = nullptr;
+  SchedulerCache* cache = nullptr;
+  Informers* informers = nullptr;
+  ApiClient* client = nullptr;
+  WaitingPods* waiting_pods = nullptr;
+  Parallelizer* parallelizer = nullptr;
+  Nominator* nominator = nullptr;
+  std::shared_ptr<Clock> clock;
+  TimerService* timers = nullptr;
+  Metrics* metrics = nullptr;
+  const Snapshot* snapshot = nullptr;  // the scheduling cycle's snapshot
+};
+
+class Plugin {
+ public:
+  explicit Plugin(std::string name, uint32_t points) : name_(std::move(name)), points_(points) {}
+  virtual ~Plugin() = default;
+  const std::string& name() const { return name_; }
+  uint32_t points() const { return points_; }
+
+  // QueueSort
+  virtual bool less(const QueuedPodInfo& a, const QueuedPodInfo& b) const { return false; }
+  // PreFilter (+ extensions used by preemption dry-runs)
+  virtual Status pre_filter(CycleState& s, const Pod& p) { return {}; }
+  virtual bool has_pre_filter_extensions() const { return false; }
+  virtual Status add_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_add, const NodeInfo& ni) {
+    return {};
+  }
+  virtual Status remove_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_remove, const NodeInfo& ni) {
+    return {};
+  }
+  // Filter
+  virtual Status filter(CycleState& s, const Pod& p, const NodeInfo& ni) { return {}; }
+  // PostFilter
+  virtual std::pair<PostFilterResult, Status> post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m) {
+    return {PostFilterResult{}, Status(Code::Unschedulable)};
+  }
+  // PreScore / Score
+  virtual Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) { return {}; }
+  virtual std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) { return {0, {}}; }
+  virtual bool has_normalize_score() const { return false; }
+  virtual Status normalize_score(CycleState& s, const Pod& p, std::vector<NodeScore>& scores) { return {}; }
+  // Reserve
+  virtual Status reserve(CycleState& s, const PodPtr& p, const std::string& node) { return {}; }
+  virtual void unreserve(CycleState& s, const PodPtr& p, const std::string& node) {}
+  // Permit: (status, timeout_us) — Wait requests a timeout.
+  virtual std::pair<Status, int64_t> permit(CycleState& s, const PodPtr& p, const std::string& node) {
+    return {Status(), 0};
+  }
+  // Binding cycle
+  virtual Status pre_bind(CycleState& s, const PodPtr& p, const std::string& node) { return {}; }
+  virtual Status bind(CycleState& s, const PodPtr& p, const std::string& node) { return Status(Code::Skip); }
+  virtual void post_bind(CycleState& s, const PodPtr& p, const std::string& node) {}
+  // EnqueueExtensions
+  virtual std::vector<ClusterEvent> events_to_register() const { return {}; }
+  // Informer hooks (plugins that maintain their own state from watch events,
+  // e.g. CapacityScheduling's ElasticQuota infos, Trimaran's pod-assign cache).
+  virtual void on_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) {}
+  virtual std::vector<std::string> watched_kinds() const { return {}; }
+  // Periodic work registered at start (metrics refresh, cache cleanup).
+  virtual void start() {}
+  virtual void stop() {}
+
+ protected:
+  std::string name_;
+  uint32_t points_;
+};
+using PluginPtr = std::shared_ptr<Plugin>;
+
+using PluginFactory = std::function<PluginPtr(const Json& args, Handle& handle)>;
+
+class Registry {
+ public:
+  static Registry& global();
+  void add(const std::string& name, PluginFactory f);
+  bool has(const std::string& name) const { return factories_.count(name) > 0; }
+  PluginPtr make(const std::string& name, const Json& args, Handle& h) const;
+  std::vector<std::string> names() const;
+
+ private:
+  std::unordered_map<std::string, PluginFactory> factories_;
+};
+
+// Static registration helper: XSCHED_REGISTER_PLUGIN(Name, factory).
+struct PluginRegistrar {
+  PluginRegistrar(const std::string& name, PluginFactory f) { Registry::global().add(name, std::move(f)); }
+};
+void register_builtin_plugins();  // force-link all plugin translation units
+
+// DefaultNormalizeScore (vendor/.../plugins/helper/normalize_score.go:26-54).
+void default_normalize_score(int64_t max_priority, bool reverse, std::vector<NodeScore>& scores);
+
+}  // namespace xsched

@@ -1,0 +1,205 @@
+// Core framework value types: Status, CycleState, NodeInfo (+ the MI355X GPU
+// ledger), Snapshot, QueuedPodInfo, ClusterEvent.
+//
+// Behavioural reference: vendor/k8s.io/kubernetes/pkg/scheduler/framework/
+// {interface.go (Status codes), cycle_state.go, types.go (NodeInfo,
+// QueuedPodInfo, ClusterEvent)} as used by the reference's plugins.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "api/types.h"
+
+namespace xsched {
+
+// ------------------------------------------------------------- Status ----
+enum class Code : uint8_t { Success = 0, Error, Unschedulable, UnschedulableAndUnresolvable, Wait, Skip };
+const char* code_name(Code c);
+
+class Status {
+ public:
+  Status() = default;
+  explicit Status(Code c) : code_(c) {}
+  Status(Code c, std::string reason) : code_(c) { reasons_.push_back(std::move(reason)); }
+  Status(Code c, std::vector<std::string> reasons) : code_(c), reasons_(std::move(reasons)) {}
+  static Status ok() { return Status(); }
+  static Status error(std::string r) { return Status(Code::Error, std::move(r)); }
+  static Status unschedulable(std::string r) { return Status(Code::Unschedulable, std::move(r)); }
+  static Status unresolvable(std::string r) { return Status(Code::UnschedulableAndUnresolvable, std::move(r)); }
+
+  Code code() const { return code_; }
+  bool is_success() const { return code_ == Code::Success; }
+  bool is_wait() const { return code_ == Code::Wait; }
+  bool is_skip() const { return code_ == Code::Skip; }
+  bool is_unschedulable() const {
+    return code_ == Code::Unschedulable || code_ == Code::UnschedulableAndUnresolvable;
+  }
+  const std::vector<std::string>& reasons() const { return reasons_; }
+  std::string message() const;
+  const std::string& failed_plugin() const { return plugin_; }
+  Status& with_plugin(std::string p) {
+    plugin_ = std::move(p);
+    return *this;
+  }
+
+ private:
+  Code code_ = Code::Success;
+  std::vector<std::string> reasons_;
+  std::string plugin_;
+};
+
+// --------------------------------------------------------- CycleState ----
+class StateData {
+ public:
+  virtual ~StateData() = default;
+  virtual std::shared_ptr<StateData> clone() const = 0;
+};
+
+// Pods the current cycle wants moved to activeQ (framework.PodsToActivate).
+struct PodsToActivate : StateData {
+  std::mutex mu;
+  std::map<std::string, PodPtr> pods;  // "ns/name" -> pod
+  std::shared_ptr<StateData> clone() const override { return nullptr; }  // shared, never cloned
+};
+inline constexpr const char* kPodsToActivateKey = "kubernetes.io/pods-to-activate";
+
+class CycleState {
+ public:
+  std::shared_ptr<StateData> read(const std::string& key) const;
+  template <typename T>
+  T* read_as(const std::string& key) const {
+    return dynamic_cast<T*>(read(key).get());
+  }
+  void write(const std::string& key, std::shared_ptr<StateData> v);
+  void erase(const std::string& key);
+  std::shared_ptr<CycleState> clone() const;
+  bool record_metrics = false;
+  bool skip_filter_plugins_mark = false;
+
+ private:
+  mutable std::mutex mu_;
+  std::vector<std::pair<std::string, std::shared_ptr<StateData>>> kv_;
+};
+using CycleStatePtr = std::shared_ptr<CycleState>;
+
+// ----------------------------------------------------------- GpuLedger ----
+// Per-node accounting of MI355X GPUs. A node has `gpu_count` physical GPUs;
+// GPU g is split into parts[g] compute partitions (SPX=1, DPX=2, QPX=4,
+// CPX=8; each partition owns 8/parts XCDs and mem_per_gpu/parts memory
+// units). The ledger is updated incrementally as pods enter/leave the node,
+// replacing the reference's per-call O(pods) rebuild (gpu_node.go:30-120).
+struct GpuLedger {
+  struct Slot {
+    int exclusive = 0;     // whole-GPU or partition owners (expected 0/1)
+    int64_t used_mem = 0;  // Σ memory-slice pods on this partition
+    int mem_pods = 0;
+  };
+  int gpu_count = 0;
+  int64_t mem_per_gpu = 0;
+  std::vector<int> parts, offset;  // offset[g] = first slot of GPU g
+  std::vector<int> monopoly;       // whole-GPU owners per GPU
+  std::vector<int> numa;
+  std::vector<Slot> slots;
+
+  void init(const Node& n);
+  void apply(const GpuAssignment& a, int sign);
+  int64_t part_mem(int g) const { return parts[g] > 0 ? mem_per_gpu / parts[g] : 0; }
+  int xcds_per_part(int g) const { return parts[g] > 0 ? 8 / parts[g] : 0; }
+  bool gpu_untouched(int g) const;      // no owner and no memory use on any partition
+  bool slot_free(int g, int p) const;   // exclusive-free and no memory use
+  int free_gpus() const;                // GPUScore (gpu_node.go:179-187)
+  int64_t free_memory() const;          // MemScore (gpu_node.go:189-199)
+  int free_xcds() const;
+};
+
+// ------------------------------------------------------------ NodeInfo ----
+struct NodeInfo {
+  NodePtr node;
+  std::vector<PodPtr> pods;
+  std::vector<PodPtr> pods_with_affinity;
+  std::vector<PodPtr> pods_with_required_anti_affinity;
+  std::set<std::tuple<std::string, std::string, int32_t>> used_ports;  // (ip, proto, port)
+  Res requested, nonzero_requested, allocatable;
+  GpuLedger gpu;
+  int64_t generation = 0;
+  std::unordered_map<std::string, int> pg_count;  // "ns/pg" -> pods on this node
+
+  const std::string& name() const;
+  void set_node(const NodePtr& n);
+  void add_pod(const PodPtr& p);
+  bool remove_pod(const std::string& uid);
+  int num_pods() const { return static_cast<int>(pods.size()); }
+  std::shared_ptr<NodeInfo> clone() const { return std::make_shared<NodeInfo>(*this); }
+  const PodPtr* find_pod(const std::string& uid) const;
+};
+using NodeInfoPtr = std::shared_ptr<NodeInfo>;
+
+// ------------------------------------------------------------ Snapshot ----
+struct Snapshot {
+  std::vector<NodeInfoPtr> nodes;  // in cache order
+  std::unordered_map<std::string, NodeInfoPtr> by_name;
+  std::unordered_map<std::string, size_t> index;  // name -> position in `nodes`
+  std::vector<NodeInfoPtr> have_pods_with_affinity;
+  std::vector<NodeInfoPtr> have_pods_with_required_anti_affinity;
+  int64_t generation = 0;
+  NodeInfoPtr get(const std::string& name) const {
+    auto it = by_name.find(name);
+    return it == by_name.end() ? nullptr : it->second;
+  }
+};
+
+// -------------------------------------------------------- QueuedPodInfo ----
+struct QueuedPodInfo {
+  PodPtr pod;
+  int64_t timestamp_us = 0;          // last time added to a queue (monotonic)
+  int64_t initial_attempt_us = 0;    // first time added (monotonic)
+  MicroTime initial_attempt_wall = 0;
+  int attempts = 0;
+  std::set<std::string> unschedulable_plugins;
+  int64_t enqueue_seq = 0;
+};
+using QueuedPodInfoPtr = std::shared_ptr<QueuedPodInfo>;
+
+// -------------------------------------------------------- ClusterEvent ----
+enum ActionType : uint32_t {
+  kAdd = 1, kDelete = 2, kUpdateNodeAllocatable = 4, kUpdateNodeLabel = 8, kUpdateNodeTaint = 16,
+  kUpdateNodeCondition = 32, kUpdate = 4 | 8 | 16 | 32, kAll = 63
+};
+struct ClusterEvent {
+  std::string resource;  // "Pod", "Node", "PodGroup", "ElasticQuota", "*" ...
+  uint32_t action = kAll;
+  std::string label;
+  bool is_wildcard() const { return resource == "*" && action == kAll; }
+  bool matches(const ClusterEvent& other) const {
+    return is_wildcard() || (resource == other.resource && (action & other.action) != 0);
+  }
+};
+
+struct NodeScore {
+  std::string name;
+  int64_t score = 0;
+};
+inline constexpr int64_t kMaxNodeScore = 100;
+inline constexpr int64_t kMinNodeScore = 0;
+
+using NodeStatusMap = std::unordered_map<std::string, Status>;
+
+struct Victims {
+  std::vector<PodPtr> pods;
+  int64_t num_pdb_violations = 0;
+};
+
+struct PostFilterResult {
+  std::string nominated_node_name;
+};
+
+}  // namespace xsched

@@ -1,0 +1,266 @@
+// Coscheduling: PodGroup gang admission.
+//
+// Reference: pkg/coscheduling/coscheduling.go:42-252 and
+// pkg/coscheduling/core/core.go:56-382.
+// Semantics kept: QueueSort by priority, PodGroup creation time, ns/name;
+// PreFilter denies recently-denied groups (TTL cache), groups with fewer
+// labelled pods than minMember and groups whose MinResources do not fit the
+// cluster; Permit waits until assigned+1 >= minMember and then Allows every
+// waiting sibling; Wait activates siblings; PostFilter/Unreserve reject the
+// whole group and deny it for deniedPGExpirationTimeSeconds; PostBind
+// patches the PodGroup status when its phase flips.
+//
+// Differences by design: assigned counts come from the cache's per-group
+// counter (O(1)) instead of a scan of every pod on every node; the TTL maps
+// are swept by the shared timer service.
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+
+#include "framework/plugin.h"
+#include "framework/waiting_pods.h"
+#include "scheduler/cache.h"
+#include "scheduler/informers.h"
+
+namespace xsched {
+namespace {
+
+class TTLSet {
+ public:
+  explicit TTLSet(std::shared_ptr<Clock> c) : clock_(std::move(c)) {}
+  void add(const std::string& k, int64_t ttl_us) {
+    std::lock_guard<std::mutex> g(mu_);
+    m_[k] = clock_->now_us() + ttl_us;
+  }
+  bool has(const std::string& k) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = m_.find(k);
+    if (it == m_.end()) return false;
+    if (clock_->now_us() >= it->second) {
+      m_.erase(it);
+      return false;
+    }
+    return true;
+  }
+  void erase(const std::string& k) {
+    std::lock_guard<std::mutex> g(mu_);
+    m_.erase(k);
+  }
+  void sweep() {
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t now = clock_->now_us();
+    for (auto it = m_.begin(); it != m_.end();) it = now >= it->second ? m_.erase(it) : std::next(it);
+  }
+
+ private:
+  std::shared_ptr<Clock> clock_;
+  std::mutex mu_;
+  std::unordered_map<std::string, int64_t> m_;
+};
+
+class Coscheduling : public Plugin {
+ public:
+  Coscheduling(const Json& args, Handle& h)
+      : Plugin("Coscheduling", kQueueSort | kPreFilter | kPostFilter | kReserve | kPermit | kPostBind),
+        h_(h),
+        denied_(h.clock),
+        permitted_(h.clock) {
+    permit_wait_us_ = args["permitWaitingTimeSeconds"].as_int(60) * 1000000;
+    denied_ttl_us_ = args["deniedPGExpirationTimeSeconds"].as_int(20) * 1000000;
+  }
+
+  void start() override {
+    sweep_id_ = h_.timers->every(3'000'000, [this] {
+      denied_.sweep();
+      permitted_.sweep();
+    });
+  }
+  void stop() override {
+    if (sweep_id_) h_.timers->cancel(sweep_id_);
+  }
+
+  // ---- QueueSort ----
+  MicroTime creation(const QueuedPodInfo& q) const {
+    if (!q.pod->pod_group.empty())
+      if (auto pg = h_.informers->pod_group(q.pod->ns(), q.pod->pod_group)) return pg->meta.creation;
+    return q.initial_attempt_wall;
+  }
+  bool less(const QueuedPodInfo& a, const QueuedPodInfo& b) const override {
+    if (a.pod->priority != b.pod->priority) return a.pod->priority > b.pod->priority;
+    MicroTime ta = creation(a), tb = creation(b);
+    if (ta == tb) return a.pod->key() < b.pod->key();
+    return ta < tb;
+  }
+
+  // ---- PreFilter (core.go:149-196) ----
+  Status pre_filter(CycleState&, const Pod& p) override {
+    if (p.pod_group.empty()) return {};
+    auto pg = h_.informers->pod_group(p.ns(), p.pod_group);
+    if (!pg) return {};
+    std::string full = p.pg_full_name();
+    if (denied_.has(full))
+      return Status::unresolvable("pod with pgName: " + full + " last failed in " +
+                                  std::to_string(denied_ttl_us_ / 1000000) + "s, deny");
+    size_t n = h_.informers->count_pods_in_group(p.ns(), p.pod_group);
+    if (static_cast<int64_t>(n) < pg->min_member)
+      return Status::unresolvable("pre-filter pod " + p.name() + " cannot find enough sibling pods, current pods number: " +
+                                  std::to_string(n) + ", minMember of group: " + std::to_string(pg->min_member));
+    if (!pg->has_min_resources) return {};
+    if (permitted_.has(full)) return {};
+    Res need = pg->min_resources;
+    need.set(kPods, pg->min_member);
+    if (!check_cluster_resource(need, full)) {
+      denied_.add(full, denied_ttl_us_);
+      return Status::unresolvable("resource gap for PodGroup " + full);
+    }
+    permitted_.add(full, wait_time(*pg));
+    return {};
+  }
+
+  // CheckClusterResource (core.go:322-382): greedily subtract each node's
+  // free resources (with this group's own pods counted as free).
+  bool check_cluster_resource(Res need, const std::string& full) const {
+    if (!h_.snapshot) return false;
+    for (const auto& ni : h_.snapshot->nodes) {
+      if (!ni->node) continue;
+      Res left;
+      Res requested = ni->requested;
+      int64_t pods = ni->num_pods();
+      for (const auto& q : ni->pods)
+        if (q->pg_full_name() == full) {
+          requested -= q->request;
+          --pods;
+        }
+      left.set(kPods, ni->allocatable.get(kPods) - pods);
+      for (uint64_t m = ni->allocatable.mask; m; m &= m - 1) {
+        int i = __builtin_ctzll(m);
+        if (i == kPods) continue;
+        left.set(i, ni->allocatable.get(i) - requested.get(i));
+      }
+      bool all_done = true;
+      for (uint64_t m = need.mask; m; m &= m - 1) {
+        int i = __builtin_ctzll(m);
+        if (need.v[i] <= 0) continue;
+        need.v[i] -= left.get(i);
+        if (need.v[i] > 0) all_done = false;
+      }
+      if (all_done) return true;
+    }
+    for (uint64_t m = need.mask; m; m &= m - 1)
+      if (need.v[__builtin_ctzll(m)] > 0) return false;
+    return true;
+  }
+
+  int64_t wait_time(const PodGroup& pg) const {
+    if (pg.schedule_timeout_seconds >= 0) return static_cast<int64_t>(pg.schedule_timeout_seconds) * 1000000;
+    if (permit_wait_us_ > 0) return permit_wait_us_;
+    return 60'000'000;  // util.DefaultWaitTime
+  }
+
+  // ---- PostFilter (coscheduling.go:140-176) ----
+  std::pair<PostFilterResult, Status> post_filter(CycleState&, const Pod& p, const NodeStatusMap&) override {
+    auto pg = p.pod_group.empty() ? nullptr : h_.informers->pod_group(p.ns(), p.pod_group);
+    if (!pg) return {PostFilterResult{}, Status::unschedulable("can not find pod group")};
+    std::string full = p.pg_full_name();
+    int assigned = h_.cache->assigned_in_group(full);
+    if (assigned >= pg->min_member) return {PostFilterResult{}, Status(Code::Unschedulable)};
+    float gap = static_cast<float>(pg->min_member - assigned) / static_cast<float>(std::max(1, pg->min_member));
+    if (gap <= 0.1f) return {PostFilterResult{}, Status(Code::Unschedulable)};
+    reject_group(p.ns(), p.pod_group, "optimistic rejection in PostFilter");
+    denied_.add(full, denied_ttl_us_);
+    permitted_.erase(full);
+    return {PostFilterResult{},
+            Status::unschedulable("PodGroup " + full + " gets rejected due to Pod " + p.name() +
+                                  " is unschedulable even after PostFilter")};
+  }
+
+  void reject_group(const std::string& ns, const std::string& pg, const std::string& msg) {
+    h_.waiting_pods->iterate([&](const WaitingPodPtr& wp) {
+      const Pod& wpod = *wp->pod();
+      if (wpod.ns() == ns && wpod.pod_group == pg) wp->reject(name(), msg);
+    });
+  }
+
+  // ---- Permit (coscheduling.go:184-216, core.go:199-216) ----
+  std::pair<Status, int64_t> permit(CycleState& s, const PodPtr& p, const std::string&) override {
+    if (p->pod_group.empty()) return {Status(), 0};
+    auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
+    if (!pg) return {Status::unschedulable("PodGroup not found"), 0};
+    std::string full = p->pg_full_name();
+    // The cache already holds this (assumed) pod, so `assigned` includes it:
+    // equivalent to the reference's snapshot count + 1.
+    int assigned = h_.cache->assigned_in_group(full);
+    if (assigned < pg->min_member) {
+      activate_siblings(*p, s);
+      return {Status(Code::Wait), wait_time(*pg)};
+    }
+    h_.waiting_pods->iterate([&](const WaitingPodPtr& wp) {
+      if (wp->pod()->pg_full_name() == full) wp->allow(name());
+    });
+    return {Status(), 0};
+  }
+
+  void activate_siblings(const Pod& p, CycleState& s) {
+    auto* pta = s.read_as<PodsToActivate>(kPodsToActivateKey);
+    if (!pta) return;
+    auto pods = h_.informers->pods_in_group(p.ns(), p.pod_group);
+    std::lock_guard<std::mutex> g(pta->mu);
+    for (const auto& q : pods)
+      if (q->uid() != p.uid()) pta->pods[q->key()] = q;
+  }
+
+  // ---- Reserve / Unreserve (coscheduling.go:219-237) ----
+  Status reserve(CycleState&, const PodPtr&, const std::string&) override { return {}; }
+  void unreserve(CycleState&, const PodPtr& p, const std::string&) override {
+    if (p->pod_group.empty()) return;
+    auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
+    if (!pg) return;
+    reject_group(p->ns(), p->pod_group, "rejection in Unreserve");
+    denied_.add(p->pg_full_name(), denied_ttl_us_);
+    permitted_.erase(p->pg_full_name());
+  }
+
+  // ---- PostBind (core.go:220-252) ----
+  void post_bind(CycleState&, const PodPtr& p, const std::string&) override {
+    if (p->pod_group.empty()) return;
+    auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
+    if (!pg) return;
+    int32_t scheduled = pg->scheduled + 1;
+    std::string phase;
+    Json status = Json::object();
+    if (scheduled >= pg->min_member) {
+      phase = "Scheduled";
+    } else {
+      phase = "Scheduling";
+      if (pg->schedule_start_time == 0) status.set("scheduleStartTime", Json(format_rfc3339(wall_now_us())));
+    }
+    if (phase == pg->phase) return;  // the reference PATCHes only on phase change
+    status.set("phase", Json(phase));
+    status.set("scheduled", Json(static_cast<int64_t>(scheduled)));
+    Json patch = Json::object();
+    patch.set("status", std::move(status));
+    try {
+      h_.client->patch("podgroups", pg->meta.ns, pg->meta.name, patch);
+    } catch (const std::exception&) {
+    }
+  }
+
+  std::vector<ClusterEvent> events_to_register() const override {
+    return {{"Pod", kAdd, ""}, {"PodGroup", kAdd | kUpdate, ""}};
+  }
+
+ private:
+  Handle& h_;
+  TTLSet denied_, permitted_;
+  int64_t permit_wait_us_ = 60'000'000;
+  int64_t denied_ttl_us_ = 20'000'000;
+  uint64_t sweep_id_ = 0;
+};
+
+PluginRegistrar reg("Coscheduling", [](const Json& a, Handle& h) { return std::make_shared<Coscheduling>(a, h); });
+
+}  // namespace
+
+void link_coscheduling_plugin() {}
+
+}  // namespace xsched

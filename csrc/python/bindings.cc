@@ -1,0 +1,440 @@
+// pybind11 bindings: the native core as the `_xsched` extension module.
+//
+// The Python control plane (flex_gpu_scheduler_amd/) drives the C++ store and
+// scheduler through this module; hot paths (scheduling cycle, binding, watch
+// fan-out) never enter Python. Bulk entry points take JSON text so a
+// benchmark wave of thousands of pods crosses the boundary once.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "api/types.h"
+#include "common/json.h"
+#include "common/quantity.h"
+#include "scheduler/scheduler.h"
+#include "store/store.h"
+
+namespace py = pybind11;
+using namespace xsched;
+
+namespace {
+
+Json from_py(py::handle h) {
+  if (h.is_none()) return Json();
+  if (py::isinstance<py::bool_>(h)) return Json(h.cast<bool>());
+  if (py::isinstance<py::int_>(h)) return Json(h.cast<int64_t>());
+  if (py::isinstance<py::float_>(h)) return Json(h.cast<double>());
+  if (py::isinstance<py::str>(h)) return Json(h.cast<std::string>());
+  if (py::isinstance<py::dict>(h)) {
+    Json o = Json::object();
+    auto& m = o.members_mut();
+    for (auto kv : h.cast<py::dict>()) m.emplace_back(py::str(kv.first).cast<std::string>(), from_py(kv.second));
+    return o;
+  }
+  if (py::isinstance<py::list>(h) || py::isinstance<py::tuple>(h)) {
+    Json a = Json::array();
+    for (auto v : h) a.push_back(from_py(v));
+    return a;
+  }
+  throw py::type_error("cannot convert object to JSON");
+}
+
+py::object to_py(const Json& j) {
+  switch (j.type()) {
+    case Json::Type::Null: return py::none();
+    case Json::Type::Bool: return py::bool_(j.as_bool());
+    case Json::Type::Int: return py::int_(j.as_int());
+    case Json::Type::Double: return py::float_(j.as_double());
+    case Json::Type::String: return py::str(j.as_string());
+    case Json::Type::Array: {
+      py::list l(j.size());
+      size_t i = 0;
+      for (const auto& v : j.items()) l[i++] = to_py(v);
+      return std::move(l);
+    }
+    case Json::Type::Object: {
+      py::dict d;
+      for (const auto& kv : j.members()) d[py::str(kv.first)] = to_py(kv.second);
+      return std::move(d);
+    }
+  }
+  return py::none();
+}
+
+py::object ptr_to_py(const JsonPtr& p) { return p ? to_py(*p) : py::none(); }
+
+Json json_arg(py::handle h) {
+  if (py::isinstance<py::str>(h)) return Json::parse(h.cast<std::string>());
+  return from_py(h);
+}
+
+// ApiClient implemented in Python (remote kube-apiserver / HTTP store).
+class PyApiClient : public ApiClient {
+ public:
+  void bind(const Pod& pod, const std::string& node, const Json& annotations) override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(this, "bind");
+    if (!f) throw std::runtime_error("PyApiClient.bind not implemented");
+    f(pod.ns(), pod.name(), pod.uid(), node, to_py(annotations));
+  }
+  void delete_pod(const Pod& pod) override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(this, "delete_pod");
+    if (!f) throw std::runtime_error("PyApiClient.delete_pod not implemented");
+    f(pod.ns(), pod.name(), pod.uid());
+  }
+  void patch(const std::string& kind, const std::string& ns, const std::string& name, const Json& patch) override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(this, "patch");
+    if (!f) throw std::runtime_error("PyApiClient.patch not implemented");
+    f(kind, ns, name, to_py(patch));
+  }
+  void record_event(const std::string& kind, const std::string& ns, const std::string& name, const std::string& type,
+                    const std::string& reason, const std::string& msg) override {
+    py::gil_scoped_acquire g;
+    py::function f = py::get_override(this, "record_event");
+    if (f) f(kind, ns, name, type, reason, msg);
+  }
+};
+
+py::dict pod_summary(const Json& obj) {
+  auto p = Pod::from_json(obj);
+  py::dict d;
+  d["key"] = p->key();
+  d["request"] = to_py(p->request.to_json());
+  d["nonzero_request"] = to_py(p->nonzero_request.to_json());
+  d["limits"] = to_py(p->limit_sum.to_json());
+  const char* q[] = {"BestEffort", "Burstable", "Guaranteed"};
+  d["qos"] = q[static_cast<int>(p->qos)];
+  d["pod_group"] = p->pod_group;
+  d["priority"] = p->priority;
+  d["gpus"] = p->gpu.gpus;
+  py::list parts;
+  for (auto [g, pp] : p->gpu.partitions) parts.append(py::make_tuple(g, pp));
+  d["partitions"] = parts;
+  return d;
+}
+
+py::dict node_info_dict(const NodeInfo& ni) {
+  py::dict d;
+  d["name"] = ni.name();
+  d["pods"] = ni.num_pods();
+  d["requested"] = to_py(ni.requested.to_json());
+  d["allocatable"] = to_py(ni.allocatable.to_json());
+  py::dict g;
+  g["gpu_count"] = ni.gpu.gpu_count;
+  g["mem_per_gpu"] = ni.gpu.mem_per_gpu;
+  g["partitions"] = ni.gpu.parts;
+  g["monopoly"] = ni.gpu.monopoly;
+  py::list slots;
+  for (int gi = 0; gi < ni.gpu.gpu_count; ++gi) {
+    py::list ps;
+    for (int s = ni.gpu.offset[gi]; s < ni.gpu.offset[gi + 1]; ++s) {
+      const auto& sl = ni.gpu.slots[s];
+      ps.append(py::make_tuple(sl.exclusive, sl.used_mem, sl.mem_pods));
+    }
+    slots.append(ps);
+  }
+  g["slots"] = slots;
+  g["free_gpus"] = ni.gpu.free_gpus();
+  g["free_xcds"] = ni.gpu.free_xcds();
+  g["free_memory"] = ni.gpu.free_memory();
+  d["gpu"] = g;
+  return d;
+}
+
+void release_scheduler(Scheduler* s) {
+  if (PyGILState_Check()) {
+    py::gil_scoped_release r;
+    delete s;
+  } else {
+    delete s;
+  }
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_xsched, m) {
+  m.doc() = "MI355X-native scheduler core (C++): object store, scheduling framework, plugins";
+
+  py::register_exception<JsonError>(m, "JsonError");
+  static py::exception<StoreError> store_exc(m, "StoreError");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const StoreError& e) {
+      py::object exc = py::handle(store_exc.ptr())(py::str(e.what()));
+      exc.attr("code") = e.code();
+      exc.attr("reason") = e.reason();
+      PyErr_SetObject(store_exc.ptr(), exc.ptr());
+    }
+  });
+
+  // ---- quantities / parsing helpers ----
+  m.def("parse_quantity", [](const std::string& s) {
+    Quantity q = Quantity::parse(s);
+    return py::make_tuple(q.milli_value(), q.value(), q.str());
+  });
+  m.def("canonical_quantity", [](const std::string& s) { return Quantity::parse(s).str(); });
+  m.def("pod_summary", [](py::handle obj) { return pod_summary(json_arg(obj)); });
+  m.def("plugin_names", [] {
+    register_builtin_plugins();
+    return Registry::global().names();
+  });
+  m.def("json_roundtrip", [](const std::string& s) { return Json::parse(s).dump(); });
+  m.def("merge_patch", [](py::handle a, py::handle b) {
+    Json x = json_arg(a);
+    x.merge_patch(json_arg(b));
+    return to_py(x);
+  });
+  m.def("rfc3339", [](int64_t us) { return format_rfc3339(us); });
+  m.def("parse_rfc3339", [](const std::string& s) { return parse_rfc3339(s); });
+  m.def("set_gpu_names", [](py::dict d) {
+    GpuNames& g = gpu_names();
+    if (d.contains("gpu")) g.gpu = d["gpu"].cast<std::string>();
+    if (d.contains("memory")) g.memory = d["memory"].cast<std::string>();
+    if (d.contains("xcd")) g.xcd = d["xcd"].cast<std::string>();
+    if (d.contains("index_annotation")) g.index_annotation = d["index_annotation"].cast<std::string>();
+    if (d.contains("partition_annotation")) g.partition_annotation = d["partition_annotation"].cast<std::string>();
+  });
+
+  // ---- clock ----
+  py::class_<FakeClock, std::shared_ptr<FakeClock>>(m, "FakeClock")
+      .def(py::init<int64_t>(), py::arg("start_us") = 1'000'000'000)
+      .def("now_us", &FakeClock::now_us)
+      .def("advance", [](FakeClock& c, double seconds) { c.advance_us(static_cast<int64_t>(seconds * 1e6)); });
+
+  // ---- store ----
+  py::class_<Watcher, std::shared_ptr<Watcher>>(m, "Watcher")
+      .def(
+          "next",
+          [](Watcher& w, int timeout_ms, size_t max) {
+            std::vector<WatchEvent> evs;
+            {
+              py::gil_scoped_release r;
+              evs = w.next(timeout_ms, max);
+            }
+            py::list out;
+            for (const auto& e : evs)
+              out.append(py::make_tuple(event_type_name(e.type), e.kind, ptr_to_py(e.obj), e.rv));
+            return out;
+          },
+          py::arg("timeout_ms") = 0, py::arg("max") = 4096)
+      .def(
+          "next_json",
+          [](Watcher& w, int timeout_ms, size_t max) {
+            std::vector<WatchEvent> evs;
+            {
+              py::gil_scoped_release r;
+              evs = w.next(timeout_ms, max);
+            }
+            py::list out;
+            for (const auto& e : evs)
+              out.append(py::make_tuple(event_type_name(e.type), e.kind, e.obj ? e.obj->dump() : std::string("null"), e.rv));
+            return out;
+          },
+          py::arg("timeout_ms") = 0, py::arg("max") = 4096)
+      .def("stop", &Watcher::stop)
+      .def("pending", &Watcher::pending)
+      .def_property_readonly("stopped", &Watcher::stopped);
+
+  py::class_<ObjectStore, std::shared_ptr<ObjectStore>>(m, "Store")
+      .def(py::init<>())
+      .def("create", [](ObjectStore& s, const std::string& kind, py::handle obj) { return ptr_to_py(s.create(kind, json_arg(obj))); })
+      .def("create_many",
+           [](ObjectStore& s, const std::string& kind, py::handle objs) {
+             Json arr = json_arg(objs);
+             std::vector<Json> v(arr.items().begin(), arr.items().end());
+             size_t n;
+             {
+               py::gil_scoped_release r;
+               n = s.create_many(kind, std::move(v)).size();
+             }
+             return n;
+           })
+      .def("get",
+           [](ObjectStore& s, const std::string& kind, const std::string& ns, const std::string& name) {
+             return ptr_to_py(s.get(kind, ns, name));
+           })
+      .def("get_json",
+           [](ObjectStore& s, const std::string& kind, const std::string& ns, const std::string& name) -> py::object {
+             auto p = s.get(kind, ns, name);
+             if (!p) return py::none();
+             return py::str(p->dump());
+           })
+      .def(
+          "list",
+          [](ObjectStore& s, const std::string& kind, const std::string& ns) {
+            int64_t rv = 0;
+            auto items = s.list(kind, ns, &rv);
+            py::list out;
+            for (const auto& p : items) out.append(to_py(*p));
+            return py::make_tuple(out, rv);
+          },
+          py::arg("kind"), py::arg("ns") = "")
+      .def(
+          "list_json",
+          [](ObjectStore& s, const std::string& kind, const std::string& ns) {
+            int64_t rv = 0;
+            auto items = s.list(kind, ns, &rv);
+            std::string out = "[";
+            for (size_t i = 0; i < items.size(); ++i) {
+              if (i) out += ",";
+              items[i]->dump_to(out);
+            }
+            out += "]";
+            return py::make_tuple(out, rv);
+          },
+          py::arg("kind"), py::arg("ns") = "")
+      .def(
+          "update",
+          [](ObjectStore& s, const std::string& kind, py::handle obj, bool check_rv) {
+            return ptr_to_py(s.update(kind, json_arg(obj), check_rv));
+          },
+          py::arg("kind"), py::arg("obj"), py::arg("check_rv") = true)
+      .def("patch",
+           [](ObjectStore& s, const std::string& kind, const std::string& ns, const std::string& name, py::handle p) {
+             return ptr_to_py(s.patch(kind, ns, name, json_arg(p)));
+           })
+      .def(
+          "delete",
+          [](ObjectStore& s, const std::string& kind, const std::string& ns, const std::string& name, int64_t grace,
+             const std::string& uid) { return ptr_to_py(s.remove(kind, ns, name, grace, uid)); },
+          py::arg("kind"), py::arg("ns"), py::arg("name"), py::arg("grace_seconds") = 0, py::arg("uid") = "")
+      .def("delete_all", &ObjectStore::delete_all, py::arg("kind"), py::arg("ns") = "",
+           py::call_guard<py::gil_scoped_release>())
+      .def(
+          "bind",
+          [](ObjectStore& s, const std::string& ns, const std::string& name, const std::string& uid,
+             const std::string& node, py::handle ann) { return ptr_to_py(s.bind(ns, name, uid, node, json_arg(ann))); },
+          py::arg("ns"), py::arg("name"), py::arg("uid"), py::arg("node"), py::arg("annotations") = py::dict())
+      .def(
+          "watch",
+          [](ObjectStore& s, std::vector<std::string> kinds, const std::string& ns, int64_t since) {
+            return s.watch(std::set<std::string>(kinds.begin(), kinds.end()), ns, since);
+          },
+          py::arg("kinds") = std::vector<std::string>{}, py::arg("ns") = "", py::arg("since_rv") = 0)
+      .def("unwatch", &ObjectStore::unwatch)
+      .def_property_readonly("resource_version", &ObjectStore::resource_version)
+      .def("count", &ObjectStore::count)
+      .def(
+          "add_fault",
+          [](ObjectStore& s, const std::string& verb, const std::string& kind, double fail_prob, int delay_us,
+             int remaining) { s.add_fault(FaultRule{verb, kind, fail_prob, delay_us, remaining}); },
+          py::arg("verb"), py::arg("kind"), py::arg("fail_prob") = 0.0, py::arg("delay_us") = 0,
+          py::arg("remaining") = -1)
+      .def("clear_faults", &ObjectStore::clear_faults);
+
+  // ---- API client trampoline ----
+  py::class_<ApiClient, PyApiClient, std::shared_ptr<ApiClient>>(m, "ApiClient").def(py::init<>());
+
+  // ---- scheduler ----
+  py::class_<Scheduler, std::shared_ptr<Scheduler>>(m, "Scheduler")
+      .def(py::init([](std::shared_ptr<ObjectStore> store, py::handle config, std::shared_ptr<FakeClock> clock,
+                       std::shared_ptr<ApiClient> client) {
+             Json cfg = json_arg(config);
+             std::shared_ptr<Clock> c = clock;
+             Scheduler* s;
+             {
+               py::gil_scoped_release r;
+               s = new Scheduler(store, cfg, c, client);
+             }
+             return std::shared_ptr<Scheduler>(s, release_scheduler);
+           }),
+           py::arg("store"), py::arg("config"), py::arg("clock") = nullptr, py::arg("client") = nullptr)
+      .def("start", &Scheduler::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Scheduler::stop, py::call_guard<py::gil_scoped_release>())
+      .def("sync_informers", &Scheduler::sync_informers, py::arg("timeout_ms") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("schedule_one", &Scheduler::schedule_one, py::arg("timeout_ms") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("wait_idle", &Scheduler::wait_idle, py::arg("timeout_ms") = 10000, py::call_guard<py::gil_scoped_release>())
+      .def("stats",
+           [](Scheduler& s) {
+             auto st = s.stats();
+             py::dict d;
+             d["attempts"] = st.attempts;
+             d["scheduled"] = st.scheduled;
+             d["unschedulable"] = st.unschedulable;
+             d["errors"] = st.errors;
+             d["bound"] = st.bound;
+             d["bind_failures"] = st.bind_failures;
+             d["preemption_attempts"] = st.preemption_attempts;
+             d["inflight_bindings"] = s.inflight_bindings();
+             return d;
+           })
+      .def(
+          "gang_records",
+          [](Scheduler& s, bool clear) {
+            py::list out;
+            for (const auto& r : s.gang_records(clear)) {
+              py::dict d;
+              d["pod_group"] = r.pg;
+              d["size"] = r.size;
+              d["first_enqueue_us"] = r.first_enqueue_us;
+              d["admit_us"] = r.admit_us;
+              d["bound_us"] = r.bound_us;
+              out.append(d);
+            }
+            return out;
+          },
+          py::arg("clear") = false)
+      .def("queue_counts",
+           [](Scheduler& s) {
+             auto c = s.queue().counts();
+             py::dict d;
+             d["active"] = c.active;
+             d["backoff"] = c.backoff;
+             d["unschedulable"] = c.unschedulable;
+             return d;
+           })
+      .def("flush_backoff", [](Scheduler& s) { s.queue().flush_backoff_completed(); })
+      .def("flush_unschedulable", [](Scheduler& s) { s.queue().flush_unschedulable_leftover(); })
+      .def("move_all", [](Scheduler& s) { s.queue().move_all_to_active_or_backoff(ClusterEvent{"*", kAll, ""}); })
+      .def("poke_timers", &Scheduler::sync_informers, py::arg("timeout_ms") = 0)
+      .def("run_timers", [](Scheduler& s) {
+        py::gil_scoped_release r;
+        s.timers().poke_and_drain();
+      })
+      .def("node_info",
+           [](Scheduler& s, const std::string& name) -> py::object {
+             auto ni = s.cache().node_info_copy(name);
+             if (!ni) return py::none();
+             return node_info_dict(*ni);
+           })
+      .def("node_names", [](Scheduler& s) { return s.cache().node_names(); })
+      .def("cache_counts",
+           [](Scheduler& s) {
+             py::dict d;
+             d["nodes"] = s.cache().node_count();
+             d["pods"] = s.cache().pod_count();
+             d["assumed"] = s.cache().assumed_count();
+             return d;
+           })
+      .def("assigned_in_group", [](Scheduler& s, const std::string& pg) { return s.cache().assigned_in_group(pg); })
+      .def("waiting_pods",
+           [](Scheduler& s) {
+             py::list out;
+             for (const auto& fw : s.frameworks())
+               fw->handle().waiting_pods->iterate([&](const WaitingPodPtr& wp) {
+                 out.append(py::make_tuple(wp->pod()->key(), wp->node(), wp->pending_plugins()));
+               });
+             return out;
+           })
+      .def("metrics_text", [](Scheduler& s) { return s.metrics().expose(); })
+      .def("set_trace", [](Scheduler& s, bool on) { s.tracer().enable(on); })
+      .def("trace_json", [](Scheduler& s) { return s.tracer().chrome_json(); })
+      .def("clear_trace", [](Scheduler& s) { s.tracer().clear(); })
+      .def("profiles", [](Scheduler& s) {
+        py::list out;
+        for (const auto& fw : s.frameworks()) {
+          py::dict d;
+          d["schedulerName"] = fw->profile_name();
+          py::dict pts;
+          for (const auto& [pt, names] : fw->config().enabled) pts[ext_point_name(pt)] = names;
+          d["plugins"] = pts;
+          out.append(d);
+        }
+        return out;
+      });
+}

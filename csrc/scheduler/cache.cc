@@ -1,0 +1,279 @@
+#include "scheduler/cache.h"
+
+#include <algorithm>
+
+namespace xsched {
+
+SchedulerCache::SchedulerCache(std::shared_ptr<Clock> clock, int64_t assumed_ttl_us)
+    : clock_(std::move(clock)), ttl_us_(assumed_ttl_us) {}
+
+NodeInfoPtr& SchedulerCache::info_for(const std::string& node) {
+  auto& ni = nodes_[node];
+  if (!ni) ni = std::make_shared<NodeInfo>();
+  return ni;
+}
+
+void SchedulerCache::mark_dirty(const std::string& node) {
+  dirty_.insert(node);
+  auto it = nodes_.find(node);
+  if (it != nodes_.end()) it->second->generation = ++generation_;
+}
+
+void SchedulerCache::group_delta(const Pod& p, int d) {
+  if (p.pod_group.empty()) return;
+  std::string k = p.pg_full_name();
+  int& c = group_assigned_[k];
+  c += d;
+  if (c <= 0) group_assigned_.erase(k);
+}
+
+void SchedulerCache::add_node(const NodePtr& n) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto& ni = info_for(n->name());
+  bool was_ghost = ni->node == nullptr;
+  ni->set_node(n);
+  if (was_ghost) {
+    order_.push_back(n->name());
+    structure_changed_ = true;
+  }
+  mark_dirty(n->name());
+}
+
+void SchedulerCache::update_node(const NodePtr& n) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto& ni = info_for(n->name());
+  bool was_ghost = ni->node == nullptr;
+  ni->set_node(n);
+  if (was_ghost) {
+    order_.push_back(n->name());
+    structure_changed_ = true;
+  }
+  mark_dirty(n->name());
+}
+
+void SchedulerCache::remove_node(const std::string& name) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = nodes_.find(name);
+  if (it == nodes_.end()) return;
+  order_.erase(std::remove(order_.begin(), order_.end(), name), order_.end());
+  structure_changed_ = true;
+  if (it->second->pods.empty()) {
+    nodes_.erase(it);
+  } else {
+    it->second->node = nullptr;  // ghost until its pods are deleted
+  }
+  dirty_.insert(name);
+}
+
+void SchedulerCache::add_pod_locked(const PodPtr& p) {
+  auto& ni = info_for(p->node_name);
+  ni->add_pod(p);
+  group_delta(*p, +1);
+  mark_dirty(p->node_name);
+}
+
+void SchedulerCache::remove_pod_locked(const Pod& p) {
+  auto it = nodes_.find(p.node_name);
+  if (it == nodes_.end()) return;
+  if (it->second->remove_pod(p.uid())) group_delta(p, -1);
+  mark_dirty(p.node_name);
+  if (it->second->node == nullptr && it->second->pods.empty()) nodes_.erase(it);
+}
+
+Status SchedulerCache::assume_pod(const PodPtr& p) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (pod_states_.count(p->uid())) return Status::error("pod " + p->key() + " is in the cache, so can't be assumed");
+  add_pod_locked(p);
+  pod_states_[p->uid()] = PodState{p, 0, false};
+  assumed_.insert(p->uid());
+  return {};
+}
+
+void SchedulerCache::finish_binding(const Pod& p) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pod_states_.find(p.uid());
+  if (it == pod_states_.end() || !assumed_.count(p.uid())) return;
+  it->second.binding_finished = true;
+  it->second.deadline_us = clock_->now_us() + ttl_us_;
+}
+
+void SchedulerCache::forget_pod(const Pod& p) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pod_states_.find(p.uid());
+  if (it == pod_states_.end()) return;
+  if (!assumed_.count(p.uid())) return;  // only assumed pods can be forgotten
+  PodPtr cur = it->second.pod;
+  remove_pod_locked(*cur);
+  assumed_.erase(p.uid());
+  pod_states_.erase(it);
+}
+
+void SchedulerCache::add_pod(const PodPtr& p) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pod_states_.find(p->uid());
+  if (it != pod_states_.end()) {
+    if (assumed_.count(p->uid())) {
+      // Confirmation of an assumed pod: replace with the informer's object
+      // (it carries the bound annotations) on the node it was bound to.
+      remove_pod_locked(*it->second.pod);
+      add_pod_locked(p);
+      assumed_.erase(p->uid());
+      it->second = PodState{p, 0, false};
+    } else {
+      remove_pod_locked(*it->second.pod);
+      add_pod_locked(p);
+      it->second.pod = p;
+    }
+    return;
+  }
+  add_pod_locked(p);
+  pod_states_[p->uid()] = PodState{p, 0, false};
+}
+
+void SchedulerCache::update_pod(const PodPtr& old_pod, const PodPtr& new_pod) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pod_states_.find(new_pod->uid());
+  if (it == pod_states_.end()) {
+    add_pod_locked(new_pod);
+    pod_states_[new_pod->uid()] = PodState{new_pod, 0, false};
+    return;
+  }
+  if (assumed_.count(new_pod->uid())) {
+    // An update for an assumed pod means it got bound: confirm it.
+    remove_pod_locked(*it->second.pod);
+    add_pod_locked(new_pod);
+    assumed_.erase(new_pod->uid());
+    it->second = PodState{new_pod, 0, false};
+    return;
+  }
+  remove_pod_locked(*it->second.pod);
+  add_pod_locked(new_pod);
+  it->second.pod = new_pod;
+}
+
+void SchedulerCache::remove_pod(const Pod& p) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pod_states_.find(p.uid());
+  if (it == pod_states_.end()) return;
+  remove_pod_locked(*it->second.pod);
+  assumed_.erase(p.uid());
+  pod_states_.erase(it);
+}
+
+bool SchedulerCache::is_assumed(const std::string& uid) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return assumed_.count(uid) > 0;
+}
+
+PodPtr SchedulerCache::get_pod(const std::string& uid) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pod_states_.find(uid);
+  return it == pod_states_.end() ? nullptr : it->second.pod;
+}
+
+PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<void(Pod&)>& fn) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pod_states_.find(uid);
+  if (it == pod_states_.end()) return nullptr;
+  auto fresh = std::make_shared<Pod>(*it->second.pod);
+  fn(*fresh);
+  fresh->recompute_gpu_assignment();
+  remove_pod_locked(*it->second.pod);
+  add_pod_locked(fresh);
+  it->second.pod = fresh;
+  return fresh;
+}
+
+void SchedulerCache::update_snapshot(Snapshot& s) {
+  std::lock_guard<std::mutex> g(mu_);
+  bool affinity_dirty = false;
+  if (structure_changed_) {
+    s.nodes.clear();
+    s.by_name.clear();
+    s.index.clear();
+    s.nodes.reserve(order_.size());
+    for (const auto& name : order_) {
+      auto it = nodes_.find(name);
+      if (it == nodes_.end() || !it->second->node) continue;
+      NodeInfoPtr cl = it->second->clone();
+      s.index[name] = s.nodes.size();
+      s.nodes.push_back(cl);
+      s.by_name[name] = cl;
+    }
+    structure_changed_ = false;
+    affinity_dirty = true;
+  } else {
+    for (const auto& name : dirty_) {
+      auto it = nodes_.find(name);
+      if (it == nodes_.end() || !it->second->node) continue;
+      auto sit = s.by_name.find(name);
+      if (sit == s.by_name.end()) continue;
+      NodeInfoPtr cl = it->second->clone();
+      if (!sit->second->pods_with_affinity.empty() || !cl->pods_with_affinity.empty()) affinity_dirty = true;
+      s.nodes[s.index[name]] = cl;
+      sit->second = cl;
+    }
+  }
+  dirty_.clear();
+  if (affinity_dirty) {
+    s.have_pods_with_affinity.clear();
+    s.have_pods_with_required_anti_affinity.clear();
+    for (const auto& ni : s.nodes) {
+      if (!ni->pods_with_affinity.empty()) s.have_pods_with_affinity.push_back(ni);
+      if (!ni->pods_with_required_anti_affinity.empty()) s.have_pods_with_required_anti_affinity.push_back(ni);
+    }
+  }
+  s.generation = generation_;
+}
+
+void SchedulerCache::cleanup_expired_assumed_pods() {
+  std::lock_guard<std::mutex> g(mu_);
+  int64_t now = clock_->now_us();
+  std::vector<std::string> expired;
+  for (const auto& uid : assumed_) {
+    auto it = pod_states_.find(uid);
+    if (it == pod_states_.end()) continue;
+    if (it->second.binding_finished && it->second.deadline_us > 0 && now > it->second.deadline_us)
+      expired.push_back(uid);
+  }
+  for (const auto& uid : expired) {
+    auto it = pod_states_.find(uid);
+    remove_pod_locked(*it->second.pod);
+    assumed_.erase(uid);
+    pod_states_.erase(it);
+  }
+}
+
+int SchedulerCache::assigned_in_group(const std::string& pg_full_name) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = group_assigned_.find(pg_full_name);
+  return it == group_assigned_.end() ? 0 : it->second;
+}
+
+size_t SchedulerCache::node_count() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return order_.size();
+}
+
+size_t SchedulerCache::pod_count() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return pod_states_.size();
+}
+
+size_t SchedulerCache::assumed_count() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return assumed_.size();
+}
+
+NodeInfoPtr SchedulerCache::node_info_copy(const std::string& name) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = nodes_.find(name);
+  return it == nodes_.end() ? nullptr : it->second->clone();
+}
+
+std::vector<std::string> SchedulerCache::node_names() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return order_;
+}
+
+}  // namespace xsched

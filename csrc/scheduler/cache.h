@@ -1,0 +1,86 @@
+// Scheduler cache: NodeInfos with assumed pods, incremental snapshots.
+//
+// Reference: vendor/k8s.io/kubernetes/pkg/scheduler/internal/cache/cache.go
+// (AssumePod :350, FinishBinding, ForgetPod, AddPod confirming an assumed pod,
+// UpdateSnapshot with generation tracking) and the 15-minute assumed-pod TTL
+// (vendor/.../scheduler.go:62).
+//
+// Differences by design:
+//  * dirty-node tracking instead of a generation-ordered linked list: a
+//    snapshot refresh clones exactly the NodeInfos touched since the last one;
+//  * per-PodGroup assigned counters (O(1) instead of Coscheduling's
+//    O(nodes x pods) CalculateAssignedPods scan, core.go:301-318);
+//  * assumed-pod updates (FlexGPU's GPU index) are copy-on-write so Filter
+//    workers reading an older snapshot never race with Reserve/Unreserve.
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "common/clock.h"
+#include "framework/types.h"
+
+namespace xsched {
+
+class SchedulerCache {
+ public:
+  SchedulerCache(std::shared_ptr<Clock> clock, int64_t assumed_ttl_us);
+
+  void add_node(const NodePtr& n);
+  void update_node(const NodePtr& n);
+  void remove_node(const std::string& name);
+
+  void add_pod(const PodPtr& p);  // assigned pod observed by the informer
+  void update_pod(const PodPtr& old_pod, const PodPtr& new_pod);
+  void remove_pod(const Pod& p);
+
+  Status assume_pod(const PodPtr& p);  // p->node_name must be set
+  void finish_binding(const Pod& p);
+  void forget_pod(const Pod& p);
+  bool is_assumed(const std::string& uid) const;
+  PodPtr get_pod(const std::string& uid) const;
+  // Copy-on-write mutation of a cached (assumed or bound) pod; re-accounts
+  // the pod on its node. Returns the new object (nullptr if not cached).
+  PodPtr mutate_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
+
+  void update_snapshot(Snapshot& s);
+  void cleanup_expired_assumed_pods();
+
+  int assigned_in_group(const std::string& pg_full_name) const;
+  size_t node_count() const;
+  size_t pod_count() const;
+  size_t assumed_count() const;
+  NodeInfoPtr node_info_copy(const std::string& name) const;
+  std::vector<std::string> node_names() const;
+
+ private:
+  struct PodState {
+    PodPtr pod;
+    int64_t deadline_us = 0;
+    bool binding_finished = false;
+  };
+  NodeInfoPtr& info_for(const std::string& node);  // creates a ghost entry
+  void add_pod_locked(const PodPtr& p);
+  void remove_pod_locked(const Pod& p);
+  void mark_dirty(const std::string& node);
+  void group_delta(const Pod& p, int d);
+
+  std::shared_ptr<Clock> clock_;
+  int64_t ttl_us_;
+  mutable std::mutex mu_;
+  std::unordered_map<std::string, NodeInfoPtr> nodes_;
+  std::vector<std::string> order_;  // node names with a Node object, insertion order
+  std::unordered_map<std::string, PodState> pod_states_;
+  std::unordered_set<std::string> assumed_;
+  std::unordered_map<std::string, int> group_assigned_;
+  std::unordered_set<std::string> dirty_;
+  bool structure_changed_ = true;
+  int64_t generation_ = 0;
+};
+
+}  // namespace xsched

@@ -1,0 +1,64 @@
+// Typed informer caches (listers) fed from the store's watch stream.
+//
+// Replaces the reference's generated listers/informers (pkg/generated/
+// listers/scheduling/v1alpha1/*.go, client-go core listers) with one typed,
+// RW-locked cache per kind plus the secondary indexes the plugins query on
+// their hot paths: pods by (namespace, PodGroup label) — Coscheduling's
+// PreFilter/ActivateSiblings list (pkg/coscheduling/core/core.go:111-167) —
+// and ElasticQuotas by namespace (pkg/capacityscheduling/capacity_scheduling.go:703-708).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <shared_mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "api/types.h"
+
+namespace xsched {
+
+class Informers {
+ public:
+  // ---- mutation (informer thread) ----
+  void upsert_pod(const PodPtr& p);
+  void delete_pod(const Pod& p);
+  void upsert_pod_group(const PodGroupPtr& pg);
+  void delete_pod_group(const std::string& key);
+  void upsert_elastic_quota(const ElasticQuotaPtr& eq);
+  void delete_elastic_quota(const std::string& key);
+  void upsert_nrt(const NRTPtr& n);
+  void delete_nrt(const std::string& name);
+  void upsert_pdb(const PDBPtr& p);
+  void delete_pdb(const std::string& key);
+  void upsert_priority_class(const PriorityClassPtr& pc);
+  void delete_priority_class(const std::string& name);
+
+  // ---- listers ----
+  PodPtr pod(const std::string& ns, const std::string& name) const;
+  std::vector<PodPtr> pods_in_group(const std::string& ns, const std::string& pg) const;
+  size_t count_pods_in_group(const std::string& ns, const std::string& pg) const;
+  std::vector<PodPtr> all_pods() const;
+  PodGroupPtr pod_group(const std::string& ns, const std::string& name) const;
+  std::vector<PodGroupPtr> pod_groups() const;
+  ElasticQuotaPtr elastic_quota_for_namespace(const std::string& ns) const;
+  std::vector<ElasticQuotaPtr> elastic_quotas() const;
+  NRTPtr nrt(const std::string& node) const;
+  std::vector<PDBPtr> pdbs() const;
+  PriorityClassPtr priority_class(const std::string& name) const;
+  size_t pod_count() const;
+
+ private:
+  mutable std::shared_mutex mu_;
+  std::unordered_map<std::string, PodPtr> pods_;  // ns/name
+  std::unordered_map<std::string, std::unordered_set<std::string>> pods_by_group_;  // ns/pg -> {ns/name}
+  std::unordered_map<std::string, PodGroupPtr> pgs_;
+  std::map<std::string, ElasticQuotaPtr> eqs_;  // ordered: "first listed wins"
+  std::unordered_map<std::string, NRTPtr> nrts_;
+  std::unordered_map<std::string, PDBPtr> pdbs_;
+  std::unordered_map<std::string, PriorityClassPtr> pcs_;
+};
+
+}  // namespace xsched

@@ -1,0 +1,125 @@
+// Scheduling queue: activeQ (heap ordered by the profile's QueueSort),
+// podBackoffQ (heap by backoff expiry), unschedulableQ, and the nominator.
+//
+// Reference: vendor/k8s.io/kubernetes/pkg/scheduler/internal/queue/
+// scheduling_queue.go (backoff 1s..10s and 60s unschedulable flush,
+// :53-66; moveRequestCycle; Activate; MoveAllToActiveOrBackoffQueue with the
+// clusterEventMap filter from plugins' EventsToRegister).
+#pragma once
+
+#include <condition_variable>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common/clock.h"
+#include "framework/types.h"
+
+namespace xsched {
+
+// Binary heap keyed by pod uid with O(log n) update/delete.
+class PodHeap {
+ public:
+  using Less = std::function<bool(const QueuedPodInfo&, const QueuedPodInfo&)>;
+  explicit PodHeap(Less less) : less_(std::move(less)) {}
+  void set_less(Less l) { less_ = std::move(l); }
+  void push(const QueuedPodInfoPtr& p);  // add or update
+  QueuedPodInfoPtr pop();
+  const QueuedPodInfoPtr& top() const { return v_.front(); }
+  QueuedPodInfoPtr get(const std::string& uid) const;
+  bool erase(const std::string& uid);
+  bool contains(const std::string& uid) const { return pos_.count(uid) > 0; }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  std::vector<QueuedPodInfoPtr> items() const { return v_; }
+
+ private:
+  void up(size_t i);
+  void down(size_t i);
+  void swap_at(size_t a, size_t b);
+  Less less_;
+  std::vector<QueuedPodInfoPtr> v_;
+  std::unordered_map<std::string, size_t> pos_;
+};
+
+// Pods nominated onto nodes by preemption (PodNominator).
+class Nominator {
+ public:
+  void add(const PodPtr& p, const std::string& node);  // node "" = use p->nominated_node_name
+  void remove(const Pod& p);
+  void update(const PodPtr& old_p, const PodPtr& new_p);
+  std::vector<PodPtr> nominated_pods_for_node(const std::string& node) const;
+  std::string nominated_node(const std::string& uid) const;
+  size_t size() const;
+
+ private:
+  mutable std::mutex mu_;
+  std::unordered_map<std::string, std::vector<PodPtr>> by_node_;
+  std::unordered_map<std::string, std::string> node_of_;
+};
+
+struct QueueOptions {
+  int64_t initial_backoff_us = 1'000'000;
+  int64_t max_backoff_us = 10'000'000;
+  int64_t unschedulable_timeout_us = 60'000'000;
+};
+
+class SchedulingQueue {
+ public:
+  SchedulingQueue(PodHeap::Less less, std::shared_ptr<Clock> clock, QueueOptions opts, Nominator* nominator);
+
+  // clusterEventMap: event -> plugin names interested in it.
+  void set_cluster_event_map(std::vector<std::pair<ClusterEvent, std::set<std::string>>> m);
+
+  void add(const PodPtr& p);
+  void activate(const std::map<std::string, PodPtr>& pods);
+  // Returns false if the pod is already queued (active/backoff).
+  bool add_unschedulable_if_not_present(const QueuedPodInfoPtr& p, int64_t pod_scheduling_cycle);
+  int64_t scheduling_cycle() const;
+  // Blocks until a pod is available or the queue is closed (nullptr).
+  QueuedPodInfoPtr pop(int timeout_ms = -1);
+  void update(const PodPtr& old_p, const PodPtr& new_p);
+  void remove(const Pod& p);
+  void assigned_pod_added(const Pod& p);
+  void assigned_pod_updated(const Pod& p);
+  void move_all_to_active_or_backoff(const ClusterEvent& ev);
+  void flush_backoff_completed();
+  void flush_unschedulable_leftover();
+  void close();
+
+  struct Counts {
+    size_t active = 0, backoff = 0, unschedulable = 0;
+  };
+  Counts counts() const;
+  std::vector<QueuedPodInfoPtr> pending_pods() const;
+  bool has_pod(const std::string& uid) const;
+
+ private:
+  QueuedPodInfoPtr new_info(const PodPtr& p) const;
+  bool backing_off(const QueuedPodInfo& p) const;
+  int64_t backoff_expiry(const QueuedPodInfo& p) const;
+  bool matches_event(const QueuedPodInfo& p, const ClusterEvent& ev) const;
+  void move_locked(const std::vector<QueuedPodInfoPtr>& pods, const ClusterEvent& ev);
+  static bool affinity_term_matches(const Pod& waiting, const Pod& assigned);
+
+  std::shared_ptr<Clock> clock_;
+  QueueOptions opts_;
+  Nominator* nominator_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  PodHeap active_;
+  PodHeap backoff_;
+  std::unordered_map<std::string, QueuedPodInfoPtr> unschedulable_;
+  std::vector<std::pair<ClusterEvent, std::set<std::string>>> event_map_;
+  int64_t scheduling_cycle_ = 0;
+  int64_t move_request_cycle_ = -1;
+  int64_t seq_ = 0;
+  bool closed_ = false;
+};
+
+}  // namespace xsched

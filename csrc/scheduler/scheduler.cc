@@ -1,0 +1,850 @@
+#include "scheduler/scheduler.h"
+
+#include <algorithm>
+#include <chrono>
+#include <map>
+#include <stdexcept>
+
+namespace xsched {
+
+// ----------------------------------------------------------- StoreClient ----
+void StoreClient::bind(const Pod& pod, const std::string& node, const Json& annotations) {
+  store_->bind(pod.ns(), pod.name(), pod.uid(), node, annotations);
+}
+
+void StoreClient::delete_pod(const Pod& pod) { store_->remove("pods", pod.ns(), pod.name(), 0, pod.uid()); }
+
+void StoreClient::patch(const std::string& kind, const std::string& ns, const std::string& name, const Json& patch) {
+  store_->patch(kind, ns, name, patch);
+}
+
+void StoreClient::record_event(const std::string& kind, const std::string& ns, const std::string& name,
+                               const std::string& type, const std::string& reason, const std::string& msg) {
+  if (!events_enabled) return;
+  Json ev = Json::object();
+  Json md = Json::object();
+  md.set("generateName", Json(name + "."));
+  md.set("namespace", Json(ns.empty() ? "default" : ns));
+  ev.set("metadata", std::move(md));
+  Json ref = Json::object();
+  ref.set("kind", Json(kind));
+  ref.set("namespace", Json(ns));
+  ref.set("name", Json(name));
+  ev.set("involvedObject", std::move(ref));
+  ev.set("type", Json(type));
+  ev.set("reason", Json(reason));
+  ev.set("message", Json(msg));
+  ev.set("reportingController", Json("xsched"));
+  try {
+    store_->create("events", std::move(ev));
+  } catch (const StoreError&) {
+  }
+}
+
+// -------------------------------------------------------------- Executor ----
+Executor::Executor(int threads) {
+  for (int i = 0; i < std::max(1, threads); ++i) {
+    threads_.emplace_back([this] {
+      for (;;) {
+        std::function<void()> fn;
+        {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+          if (q_.empty()) return;  // stop_ and drained
+          fn = std::move(q_.front());
+          q_.pop_front();
+          busy_.fetch_add(1);
+        }
+        fn();
+        busy_.fetch_sub(1);
+      }
+    });
+  }
+}
+
+Executor::~Executor() { stop(); }
+
+void Executor::submit(std::function<void()> fn) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(fn));
+  }
+  cv_.notify_one();
+}
+
+void Executor::stop() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stop_) return;
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+size_t Executor::pending() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return q_.size() + static_cast<size_t>(busy_.load());
+}
+
+// ------------------------------------------------------- SchedulerOptions ----
+SchedulerOptions SchedulerOptions::from_json(const Json& j) {
+  SchedulerOptions o;
+  o.parallelism = static_cast<int>(j["parallelism"].as_int(o.parallelism));
+  o.bind_workers = static_cast<int>(j["bindWorkers"].as_int(o.bind_workers));
+  o.percentage_of_nodes_to_score = static_cast<int>(j["percentageOfNodesToScore"].as_int(0));
+  if (j["podInitialBackoffSeconds"].is_number())
+    o.pod_initial_backoff_us = static_cast<int64_t>(j["podInitialBackoffSeconds"].as_double() * 1e6);
+  if (j["podMaxBackoffSeconds"].is_number())
+    o.pod_max_backoff_us = static_cast<int64_t>(j["podMaxBackoffSeconds"].as_double() * 1e6);
+  if (j["assumedPodTTLSeconds"].is_number())
+    o.assumed_pod_ttl_us = static_cast<int64_t>(j["assumedPodTTLSeconds"].as_double() * 1e6);
+  o.metrics_sample_rate = j["metricsSampleRate"].as_double(o.metrics_sample_rate);
+  o.status_updates = j["statusUpdates"].as_bool(o.status_updates);
+  o.trace = j["trace"].as_bool(false);
+  o.seed = static_cast<uint64_t>(j["seed"].as_int(0));
+  return o;
+}
+
+// ------------------------------------------------------------- Scheduler ----
+namespace {
+const std::vector<std::string> kBaseKinds = {"pods", "nodes", "podgroups", "elasticquotas", "noderesourcetopologies",
+                                             "poddisruptionbudgets", "priorityclasses"};
+std::string resource_for_kind(const std::string& kind) {
+  if (kind == "pods") return "Pod";
+  if (kind == "nodes") return "Node";
+  if (kind == "podgroups") return "PodGroup";
+  if (kind == "elasticquotas") return "ElasticQuota";
+  if (kind == "noderesourcetopologies") return "NodeResourceTopology";
+  if (kind == "poddisruptionbudgets") return "PodDisruptionBudget";
+  if (kind == "priorityclasses") return "PriorityClass";
+  return kind;
+}
+uint32_t action_for(EventType t) {
+  switch (t) {
+    case EventType::Added: return kAdd;
+    case EventType::Deleted: return kDelete;
+    default: return kUpdate;
+  }
+}
+}  // namespace
+
+Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std::shared_ptr<Clock> clock,
+                     std::shared_ptr<ApiClient> client)
+    : store_(std::move(store)), clock_(clock ? std::move(clock) : std::make_shared<RealClock>()) {
+  register_builtin_plugins();
+  opts_ = SchedulerOptions::from_json(config["options"]);
+  rng_.seed(opts_.seed ? opts_.seed : static_cast<uint64_t>(clock_->now_us()));
+  tracer_.enable(opts_.trace);
+  timers_ = std::make_unique<TimerService>(clock_);
+  parallelizer_ = std::make_unique<Parallelizer>(opts_.parallelism);
+  metrics_ = std::make_unique<Metrics>();
+  cache_ = std::make_unique<SchedulerCache>(clock_, opts_.assumed_pod_ttl_us);
+  informers_ = std::make_unique<Informers>();
+  nominator_ = std::make_unique<Nominator>();
+  client_ = client ? std::move(client) : std::make_shared<StoreClient>(store_);
+
+  const auto& profiles = config["profiles"].items();
+  if (profiles.empty()) throw std::runtime_error("scheduler config has no profiles");
+  for (const auto& pj : profiles) {
+    ProfileConfig pc = ProfileConfig::from_json(pj);
+    if (pc.percentage_of_nodes_to_score == 0) pc.percentage_of_nodes_to_score = opts_.percentage_of_nodes_to_score;
+    if (by_name_.count(pc.scheduler_name)) throw std::runtime_error("duplicate profile " + pc.scheduler_name);
+    waiting_.push_back(std::make_unique<WaitingPods>(timers_.get()));
+    Handle h;
+    h.cache = cache_.get();
+    h.informers = informers_.get();
+    h.client = client_.get();
+    h.waiting_pods = waiting_.back().get();
+    h.parallelizer = parallelizer_.get();
+    h.nominator = nominator_.get();
+    h.clock = clock_;
+    h.timers = timers_.get();
+    h.metrics = metrics_.get();
+    h.snapshot = &snapshot_;
+    frameworks_.push_back(std::make_unique<Framework>(pc, h));
+    by_name_[pc.scheduler_name] = frameworks_.back().get();
+  }
+  // All profiles must share the queue sort (k8s validation); use the first.
+  Framework* first = frameworks_.front().get();
+  QueueOptions qo;
+  qo.initial_backoff_us = opts_.pod_initial_backoff_us;
+  qo.max_backoff_us = opts_.pod_max_backoff_us;
+  queue_ = std::make_unique<SchedulingQueue>(
+      [first](const QueuedPodInfo& a, const QueuedPodInfo& b) { return first->less(a, b); }, clock_, qo,
+      nominator_.get());
+  std::vector<std::pair<ClusterEvent, std::set<std::string>>> emap;
+  for (const auto& fw : frameworks_) {
+    for (const auto& pl : fw->all_plugins()) {
+      for (const auto& ev : pl->events_to_register()) {
+        bool merged = false;
+        for (auto& [e, names] : emap)
+          if (e.resource == ev.resource && e.action == ev.action) {
+            names.insert(pl->name());
+            merged = true;
+          }
+        if (!merged) emap.push_back({ev, {pl->name()}});
+      }
+    }
+    for (const auto& k : fw->watched_kinds())
+      if (std::find(plugin_kinds_.begin(), plugin_kinds_.end(), k) == plugin_kinds_.end()) plugin_kinds_.push_back(k);
+  }
+  queue_->set_cluster_event_map(std::move(emap));
+  binder_ = std::make_unique<Executor>(opts_.bind_workers);
+
+  std::set<std::string> kinds(kBaseKinds.begin(), kBaseKinds.end());
+  for (const auto& k : plugin_kinds_) kinds.insert(k);
+  // Initial LIST (as informers do) then WATCH from that version.
+  int64_t rv = 0;
+  std::vector<WatchEvent> initial;
+  for (const auto& k : kinds) {
+    for (const auto& obj : store_->list(k, "", &rv)) initial.push_back(WatchEvent{EventType::Added, k, obj, nullptr, 0});
+  }
+  // Nodes before pods so assigned pods land on real NodeInfos.
+  std::stable_sort(initial.begin(), initial.end(), [](const WatchEvent& a, const WatchEvent& b) {
+    auto rank = [](const std::string& k) { return k == "nodes" ? 0 : k == "pods" ? 2 : 1; };
+    return rank(a.kind) < rank(b.kind);
+  });
+  watcher_ = store_->watch(kinds, "", 0);
+  // Events committed between list() and watch() would be lost: re-list is
+  // avoided by watching from the listed version when history allows.
+  store_->unwatch(watcher_);
+  watcher_ = store_->watch(kinds, "", rv);
+  for (const auto& ev : initial) handle_event(ev);
+}
+
+Scheduler::~Scheduler() { stop(); }
+
+void Scheduler::start() {
+  if (running_.exchange(true)) return;
+  for (auto& fw : frameworks_) fw->start();
+  timer_ids_.push_back(timers_->every(1'000'000, [this] { queue_->flush_backoff_completed(); }));
+  timer_ids_.push_back(timers_->every(30'000'000, [this] { queue_->flush_unschedulable_leftover(); }));
+  timer_ids_.push_back(timers_->every(1'000'000, [this] { cache_->cleanup_expired_assumed_pods(); }));
+  timer_ids_.push_back(timers_->every(1'000'000, [this] {
+    auto c = queue_->counts();
+    metrics_->set_gauge("scheduler_pending_pods", "queue=\"active\"", static_cast<double>(c.active));
+    metrics_->set_gauge("scheduler_pending_pods", "queue=\"backoff\"", static_cast<double>(c.backoff));
+    metrics_->set_gauge("scheduler_pending_pods", "queue=\"unschedulable\"", static_cast<double>(c.unschedulable));
+  }));
+  informer_thread_ = std::thread([this] { informer_loop(); });
+  sched_thread_ = std::thread([this] { scheduling_loop(); });
+}
+
+void Scheduler::stop() {
+  bool was_running = running_.exchange(false);
+  if (watcher_) {
+    store_->unwatch(watcher_);
+  }
+  queue_->close();
+  if (informer_thread_.joinable()) informer_thread_.join();
+  if (sched_thread_.joinable()) sched_thread_.join();
+  for (uint64_t id : timer_ids_) timers_->cancel(id);
+  timer_ids_.clear();
+  for (auto& w : waiting_) w->reject_all("scheduler stopped");
+  if (binder_) binder_->stop();
+  if (was_running)
+    for (auto& fw : frameworks_) fw->stop();
+  timers_->stop();
+}
+
+Framework* Scheduler::framework_for(const std::string& scheduler_name) {
+  auto it = by_name_.find(scheduler_name);
+  return it == by_name_.end() ? nullptr : it->second;
+}
+
+bool Scheduler::responsible_for(const Pod& p) const { return by_name_.count(p.scheduler_name) > 0; }
+
+Scheduler::Stats Scheduler::stats() const {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  return stats_;
+}
+
+std::vector<GangRecord> Scheduler::gang_records(bool clear) {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  std::vector<GangRecord> out = gang_done_;
+  if (clear) gang_done_.clear();
+  return out;
+}
+
+// ------------------------------------------------------------- informers ----
+void Scheduler::informer_loop() {
+  while (running_.load()) {
+    auto evs = watcher_->next(50, 8192);
+    if (evs.empty()) continue;
+    // Pass 1: listers first, so a PreFilter racing this batch sees every
+    // sibling of a PodGroup created together (Coscheduling counts them).
+    for (const auto& ev : evs) {
+      if (ev.kind != "pods") continue;
+      if (ev.type == EventType::Deleted) continue;
+      informers_->upsert_pod(Pod::from_json(*ev.obj));
+    }
+    for (const auto& ev : evs) handle_event(ev);
+  }
+}
+
+size_t Scheduler::sync_informers(int timeout_ms) {
+  size_t n = 0;
+  for (;;) {
+    auto evs = watcher_->next(n == 0 ? timeout_ms : 0, 8192);
+    if (evs.empty()) break;
+    for (const auto& ev : evs) handle_event(ev);
+    n += evs.size();
+  }
+  return n;
+}
+
+void Scheduler::handle_event(const WatchEvent& ev) {
+  try {
+    if (ev.kind == "pods") {
+      handle_pod_event(ev);
+    } else if (ev.kind == "nodes") {
+      handle_node_event(ev);
+    } else {
+      const Json& o = *ev.obj;
+      bool del = ev.type == EventType::Deleted;
+      if (ev.kind == "podgroups") {
+        auto pg = PodGroup::from_json(o);
+        if (del) informers_->delete_pod_group(pg->meta.key()); else informers_->upsert_pod_group(pg);
+      } else if (ev.kind == "elasticquotas") {
+        auto eq = ElasticQuota::from_json(o);
+        if (del) informers_->delete_elastic_quota(eq->meta.key()); else informers_->upsert_elastic_quota(eq);
+      } else if (ev.kind == "noderesourcetopologies") {
+        auto n = NodeResourceTopology::from_json(o);
+        if (del) informers_->delete_nrt(n->meta.name); else informers_->upsert_nrt(n);
+      } else if (ev.kind == "poddisruptionbudgets") {
+        auto p = PodDisruptionBudget::from_json(o);
+        if (del) informers_->delete_pdb(p->meta.key()); else informers_->upsert_pdb(p);
+      } else if (ev.kind == "priorityclasses") {
+        auto pc = PriorityClass::from_json(o);
+        if (del) informers_->delete_priority_class(pc->meta.name); else informers_->upsert_priority_class(pc);
+      }
+      for (auto& fw : frameworks_) fw->dispatch_object_event(ev.kind, static_cast<int>(ev.type), ev.obj, ev.old);
+      queue_->move_all_to_active_or_backoff(ClusterEvent{resource_for_kind(ev.kind), action_for(ev.type), ""});
+    }
+  } catch (const std::exception& e) {
+    // A malformed object must not kill the informer thread.
+    metrics_->inc("xsched_informer_errors_total", "kind=\"" + ev.kind + "\"");
+  }
+}
+
+void Scheduler::handle_pod_event(const WatchEvent& ev) {
+  for (auto& fw : frameworks_) fw->dispatch_object_event("pods", static_cast<int>(ev.type), ev.obj, ev.old);
+  if (ev.type == EventType::Deleted) {
+    auto p = Pod::from_json(*ev.obj);
+    PodPtr known = informers_->pod(p->ns(), p->name());
+    informers_->delete_pod(*p);
+    if (!p->node_name.empty()) {
+      cache_->remove_pod(*p);
+      queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+    } else {
+      queue_->remove(*p);
+      for (auto& w : waiting_)
+        if (auto wp = w->get(p->uid())) wp->reject("", "pod " + p->key() + " was deleted");
+      // An assumed-but-unbound pod may still sit in the cache.
+      if (cache_->is_assumed(p->uid())) {
+        if (auto cached = cache_->get_pod(p->uid())) {
+          cache_->forget_pod(*cached);
+          queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+        }
+      }
+    }
+    return;
+  }
+  auto np = Pod::from_json(*ev.obj);
+  PodPtr old = informers_->pod(np->ns(), np->name());
+  if (old && old->uid() != np->uid()) old = nullptr;  // recreated with same name
+  informers_->upsert_pod(np);
+  bool assigned = !np->node_name.empty();
+  if (ev.type == EventType::Added || !old) {
+    if (assigned) {
+      cache_->add_pod(np);
+      queue_->assigned_pod_added(*np);
+    } else if (responsible_for(*np) && !np->terminating()) {
+      queue_->add(np);
+      note_gang_enqueue(*np, clock_->now_us());
+    }
+    return;
+  }
+  bool was_assigned = !old->node_name.empty();
+  if (was_assigned && assigned) {
+    cache_->update_pod(old, np);
+    queue_->assigned_pod_updated(*np);
+  } else if (!was_assigned && assigned) {
+    queue_->remove(*old);
+    cache_->add_pod(np);
+    queue_->assigned_pod_added(*np);
+  } else if (!assigned && responsible_for(*np)) {
+    if (np->terminating()) {
+      queue_->remove(*np);
+    } else if (!cache_->is_assumed(np->uid())) {
+      queue_->update(old, np);
+    }
+  }
+}
+
+void Scheduler::handle_node_event(const WatchEvent& ev) {
+  if (ev.type == EventType::Deleted) {
+    auto n = Node::from_json(*ev.obj);
+    cache_->remove_node(n->name());
+    return;
+  }
+  auto n = Node::from_json(*ev.obj);
+  if (ev.type == EventType::Added || !ev.old) {
+    cache_->add_node(n);
+    queue_->move_all_to_active_or_backoff(ClusterEvent{"Node", kAdd, "NodeAdd"});
+    return;
+  }
+  auto o = Node::from_json(*ev.old);
+  cache_->update_node(n);
+  uint32_t action = 0;
+  if (!(o->allocatable == n->allocatable)) action |= kUpdateNodeAllocatable;
+  if (o->meta.labels != n->meta.labels) action |= kUpdateNodeLabel;
+  if (o->taints.size() != n->taints.size() || o->unschedulable != n->unschedulable) action |= kUpdateNodeTaint;
+  else
+    for (size_t i = 0; i < o->taints.size(); ++i)
+      if (o->taints[i].key != n->taints[i].key || o->taints[i].value != n->taints[i].value ||
+          o->taints[i].effect != n->taints[i].effect)
+        action |= kUpdateNodeTaint;
+  if (o->meta.annotations != n->meta.annotations) action |= kUpdateNodeLabel;  // GPU topology annotation
+  if (action) queue_->move_all_to_active_or_backoff(ClusterEvent{"Node", action, "NodeUpdate"});
+}
+
+// -------------------------------------------------------- gang tracking ----
+void Scheduler::note_gang_enqueue(const Pod& p, int64_t t) {
+  if (p.pod_group.empty()) return;
+  std::lock_guard<std::mutex> g(stats_mu_);
+  auto& r = gangs_[p.pg_full_name()];
+  if (r.pg.empty()) {
+    r.pg = p.pg_full_name();
+    r.first_enqueue_us = t;
+  }
+}
+
+void Scheduler::note_gang_event(const Pod& p, bool bound) {
+  if (p.pod_group.empty()) return;
+  auto pg = informers_->pod_group(p.ns(), p.pod_group);
+  if (!pg) return;
+  int need = std::max(1, pg->min_member);
+  std::lock_guard<std::mutex> g(stats_mu_);
+  auto it = gangs_.find(p.pg_full_name());
+  if (it == gangs_.end()) return;
+  GangRecord& r = it->second;
+  r.size = need;
+  int64_t now = clock_->now_us();
+  if (!bound) {
+    if (r.admit_us == 0) r.admit_us = now;
+    return;
+  }
+  if (++r.bound < need) return;
+  r.bound_us = now;
+  if (r.admit_us == 0) r.admit_us = now;
+  metrics_->histogram("xsched_gang_admit_seconds", "size=\"" + std::to_string(need) + "\"")
+      .observe(static_cast<double>(r.bound_us - r.first_enqueue_us) / 1e6);
+  gang_done_.push_back(r);
+  gangs_.erase(it);
+}
+
+// -------------------------------------------------------- scheduling ----
+void Scheduler::scheduling_loop() {
+  while (running_.load()) {
+    auto qpi = queue_->pop(100);
+    if (!qpi) continue;
+    std::lock_guard<std::mutex> g(sched_mu_);
+    in_cycle_.fetch_add(1);
+    schedule_cycle(qpi);
+    in_cycle_.fetch_sub(1);
+  }
+}
+
+bool Scheduler::schedule_one(int timeout_ms) {
+  auto qpi = queue_->pop(timeout_ms);
+  if (!qpi) return false;
+  std::lock_guard<std::mutex> g(sched_mu_);
+  in_cycle_.fetch_add(1);
+  schedule_cycle(qpi);
+  in_cycle_.fetch_sub(1);
+  return true;
+}
+
+bool Scheduler::wait_idle(int timeout_ms) {
+  int64_t deadline = clock_->now_us() + static_cast<int64_t>(timeout_ms) * 1000;
+  RealClock rc;
+  int64_t real_deadline = rc.now_us() + static_cast<int64_t>(timeout_ms) * 1000;
+  for (;;) {
+    auto c = queue_->counts();
+    size_t waiting = 0;
+    for (auto& w : waiting_) waiting += w->size();
+    if (c.active == 0 && c.backoff == 0 && waiting == 0 && inflight_.load() == 0 && in_cycle_.load() == 0 &&
+        watcher_->pending() == 0)
+      return true;
+    if (rc.now_us() > real_deadline && clock_->now_us() > deadline) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+int Scheduler::num_feasible_nodes_to_find(Framework& fw, int n) const {
+  constexpr int kMinFeasible = 100;       // generic_scheduler.go:47
+  constexpr int kMinPercentage = 5;
+  int pct = fw.config().percentage_of_nodes_to_score;
+  if (n < kMinFeasible || pct >= 100) return n;
+  int adaptive = pct;
+  if (adaptive <= 0) {
+    adaptive = 50 - n / 125;
+    if (adaptive < kMinPercentage) adaptive = kMinPercentage;
+  }
+  int num = n * adaptive / 100;
+  if (num < kMinFeasible) return kMinFeasible;
+  return num;
+}
+
+Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d,
+                                      std::vector<NodeInfoPtr>& feasible) {
+  Status st = fw.run_pre_filter(s, p);
+  const auto& all = snapshot_.nodes;
+  if (!st.is_success()) {
+    if (!st.is_unschedulable()) return st;
+    for (const auto& ni : all) d.node_to_status[ni->name()] = st;
+    d.unschedulable_plugins.insert(st.failed_plugin());
+    return Status(Code::Unschedulable, st.message()).with_plugin(st.failed_plugin());
+  }
+  // Prefer the nominated node (PreferNominatedNode, beta in 1.23).
+  if (!p.nominated_node_name.empty()) {
+    if (auto ni = snapshot_.get(p.nominated_node_name)) {
+      Status nst = fw.run_filter_with_nominated_pods(s, p, *ni);
+      if (nst.is_success()) {
+        feasible.push_back(ni);
+        return {};
+      }
+      if (!nst.is_unschedulable()) return nst;
+    }
+  }
+  int n = static_cast<int>(all.size());
+  if (n == 0) return Status(Code::Unschedulable, "no nodes available to schedule pods");
+  int to_find = num_feasible_nodes_to_find(fw, n);
+  if (!fw.has(kFilter)) {
+    for (int i = 0; i < std::min(n, to_find); ++i) feasible.push_back(all[(next_start_node_ + i) % n]);
+    next_start_node_ = (next_start_node_ + static_cast<int>(feasible.size())) % n;
+    return {};
+  }
+  std::vector<NodeInfoPtr> found(to_find);
+  std::atomic<int> count{0};
+  std::atomic<int> processed{0};
+  std::atomic<bool> stop{false};
+  std::mutex mu;
+  Status first_err;
+  bool has_err = false;
+  int start = next_start_node_;
+  parallelizer_->until(n, [&](int i) {
+    const NodeInfoPtr& ni = all[(start + i) % n];
+    Status fst = fw.run_filter_with_nominated_pods(s, p, *ni);
+    processed.fetch_add(1, std::memory_order_relaxed);
+    if (fst.is_success()) {
+      int len = count.fetch_add(1) + 1;
+      if (len > to_find) {
+        stop.store(true);
+        count.fetch_sub(1);
+      } else {
+        found[len - 1] = ni;
+        if (len == to_find) stop.store(true);
+      }
+      return;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    if (fst.is_unschedulable()) {
+      d.node_to_status[ni->name()] = fst;
+      d.unschedulable_plugins.insert(fst.failed_plugin());
+    } else if (!has_err) {
+      first_err = fst;
+      has_err = true;
+      stop.store(true);
+    }
+  }, &stop);
+  if (has_err) return first_err;
+  int c = std::min(count.load(), to_find);
+  next_start_node_ = (start + processed.load()) % n;
+  feasible.assign(found.begin(), found.begin() + c);
+  if (feasible.empty()) {
+    // FitError message: "0/N nodes are available: k reason, ..."
+    std::map<std::string, int> reasons;
+    for (const auto& kv : d.node_to_status)
+      for (const auto& r : kv.second.reasons()) ++reasons[r];
+    std::string msg = "0/" + std::to_string(n) + " nodes are available:";
+    bool first = true;
+    for (const auto& kv : reasons) {
+      msg += (first ? " " : ", ") + std::to_string(kv.second) + " " + kv.first;
+      first = false;
+    }
+    msg += ".";
+    return Status(Code::Unschedulable, msg);
+  }
+  return {};
+}
+
+std::string Scheduler::select_host(const std::vector<NodeScore>& scores) {
+  if (scores.empty()) return {};
+  int64_t best = scores[0].score;
+  size_t sel = 0;
+  int cnt = 1;
+  for (size_t i = 1; i < scores.size(); ++i) {
+    if (scores[i].score > best) {
+      best = scores[i].score;
+      sel = i;
+      cnt = 1;
+    } else if (scores[i].score == best) {
+      ++cnt;
+      if (rng_() % static_cast<uint64_t>(cnt) == 0) sel = i;  // reservoir sampling
+    }
+  }
+  return scores[sel].name;
+}
+
+void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
+  PodPtr pod = qpi->pod;
+  Framework* fw = framework_for(pod->scheduler_name);
+  if (!fw) return;
+  // skipPodSchedule: deleted or already assumed.
+  PodPtr latest = informers_->pod(pod->ns(), pod->name());
+  if (!latest || latest->uid() != pod->uid() || latest->terminating() || !latest->node_name.empty()) return;
+  if (cache_->is_assumed(pod->uid())) return;
+
+  int64_t cycle_start = clock_->now_us();
+  auto state = std::make_shared<CycleState>();
+  state->record_metrics = std::uniform_real_distribution<double>(0, 1)(rng_) < opts_.metrics_sample_rate;
+  auto to_activate = std::make_shared<PodsToActivate>();
+  state->write(kPodsToActivateKey, to_activate);
+  int64_t cycle = queue_->scheduling_cycle();
+  if (tracer_.enabled())
+    tracer_.record(TraceEvent{"queue_wait", pod->key(), "", qpi->timestamp_us, cycle_start - qpi->timestamp_us, 0});
+
+  cache_->update_snapshot(snapshot_);
+  const std::string& profile = fw->profile_name();
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    ++stats_.attempts;
+  }
+
+  Diagnosis diag;
+  std::vector<NodeInfoPtr> feasible;
+  Status st = find_nodes_that_fit(*fw, *state, *pod, diag, feasible);
+  std::string host;
+  if (st.is_success()) {
+    if (feasible.size() == 1) {
+      host = feasible[0]->name();
+    } else {
+      std::vector<NodeScore> scores;
+      if (!fw->has(kScore)) {
+        scores.reserve(feasible.size());
+        for (const auto& ni : feasible) scores.push_back(NodeScore{ni->name(), 1});
+        st = Status();
+      } else {
+        st = fw->run_pre_score(*state, *pod, feasible);
+        if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores);
+      }
+      if (st.is_success()) host = select_host(scores);
+    }
+  }
+  int64_t algo_end = clock_->now_us();
+  metrics_->histogram("scheduler_scheduling_algorithm_duration_seconds", "")
+      .observe(static_cast<double>(algo_end - cycle_start) / 1e6);
+  if (tracer_.enabled())
+    tracer_.record(TraceEvent{"schedule", pod->key(), st.is_success() ? host : st.message(), cycle_start,
+                              algo_end - cycle_start, 0});
+
+  if (!st.is_success()) {
+    std::string nominated;
+    bool fit_error = st.is_unschedulable();
+    if (fit_error && fw->has(kPostFilter)) {
+      auto [res, pst] = fw->run_post_filter(*state, *pod, diag.node_to_status);
+      if (pst.is_success()) nominated = res.nominated_node_name;
+      {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        ++stats_.preemption_attempts;
+      }
+    }
+    std::string result = fit_error ? "unschedulable" : "error";
+    metrics_->inc("scheduler_schedule_attempts_total", "profile=\"" + profile + "\",result=\"" + result + "\"");
+    metrics_->histogram("scheduler_scheduling_attempt_duration_seconds", "profile=\"" + profile + "\",result=\"" + result + "\"")
+        .observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
+    {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      if (fit_error) ++stats_.unschedulable; else ++stats_.errors;
+    }
+    handle_failure(*fw, qpi, st, fit_error ? "Unschedulable" : "SchedulerError", nominated, cycle,
+                   diag.unschedulable_plugins);
+    return;
+  }
+
+  // Assume.
+  auto assumed = std::make_shared<Pod>(*pod);
+  assumed->node_name = host;
+  Status ast = cache_->assume_pod(assumed);
+  if (!ast.is_success()) {
+    handle_failure(*fw, qpi, ast, "SchedulerError", "", cycle, {});
+    return;
+  }
+  // Reserve.
+  Status rst = fw->run_reserve(*state, assumed, host);
+  if (!rst.is_success()) {
+    fw->run_unreserve(*state, assumed, host);
+    cache_->forget_pod(*assumed);
+    std::lock_guard<std::mutex> g(stats_mu_);
+    ++stats_.errors;
+    handle_failure(*fw, qpi, rst, rst.is_unschedulable() ? "Unschedulable" : "SchedulerError", "", cycle,
+                   rst.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{rst.failed_plugin()});
+    return;
+  }
+  // Permit.
+  int64_t permit_start = clock_->now_us();
+  inflight_.fetch_add(1);
+  auto self = this;
+  Status pst = fw->run_permit(*state, assumed, host,
+                              [self, fw, state, qpi, assumed, host, cycle, permit_start, to_activate](const Status& wst) {
+                                self->binder_->submit([=] {
+                                  self->binding_cycle(fw, state, qpi, assumed, host, cycle, wst, permit_start, to_activate);
+                                });
+                              });
+  if (!pst.is_success() && !pst.is_wait()) {
+    inflight_.fetch_sub(1);
+    fw->run_unreserve(*state, assumed, host);
+    cache_->forget_pod(*assumed);
+    {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      ++stats_.unschedulable;
+    }
+    handle_failure(*fw, qpi, pst, pst.is_unschedulable() ? "Unschedulable" : "SchedulerError", "", cycle,
+                   pst.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{pst.failed_plugin()});
+    return;
+  }
+  if (pst.is_success()) note_gang_event(*assumed, false);
+  // Activate siblings stashed by plugins (scheduler.go:543-548).
+  {
+    std::map<std::string, PodPtr> act;
+    {
+      std::lock_guard<std::mutex> g(to_activate->mu);
+      act.swap(to_activate->pods);
+    }
+    if (!act.empty()) queue_->activate(act);
+  }
+  metrics_->inc("scheduler_schedule_attempts_total", "profile=\"" + profile + "\",result=\"scheduled\"");
+  metrics_->histogram("scheduler_scheduling_attempt_duration_seconds", "profile=\"" + profile + "\",result=\"scheduled\"")
+      .observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    ++stats_.scheduled;
+  }
+  if (pst.is_success()) {
+    binder_->submit([=] { binding_cycle(fw, state, qpi, assumed, host, cycle, Status(), permit_start, to_activate); });
+  }
+}
+
+void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
+                              int64_t cycle, Status permit_status, int64_t wait_start_us,
+                              std::shared_ptr<PodsToActivate> to_activate) {
+  int64_t t0 = clock_->now_us();
+  auto fail = [&](const Status& st, const std::string& reason) {
+    fw->run_unreserve(*s, assumed, host);
+    cache_->forget_pod(*assumed);
+    // A forgotten pod frees resources: let waiting pods retry (AssignedPodDelete).
+    queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+    {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      ++stats_.bind_failures;
+    }
+    handle_failure(*fw, qpi, st, reason, "", cycle,
+                   st.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{st.failed_plugin()});
+    inflight_.fetch_sub(1);
+  };
+  if (wait_start_us > 0 && t0 - wait_start_us > 0) {
+    metrics_->histogram("scheduler_permit_wait_duration_seconds",
+                        std::string("result=\"") + (permit_status.is_success() ? "Success" : "Unschedulable") + "\"")
+        .observe(static_cast<double>(t0 - wait_start_us) / 1e6);
+    if (tracer_.enabled())
+      tracer_.record(TraceEvent{"permit_wait", assumed->key(), code_name(permit_status.code()), wait_start_us,
+                                t0 - wait_start_us, 1});
+  }
+  if (!permit_status.is_success()) {
+    fail(permit_status, permit_status.is_unschedulable() ? "Unschedulable" : "SchedulerError");
+    return;
+  }
+  Status st = fw->run_pre_bind(*s, assumed, host);
+  if (!st.is_success()) {
+    fail(st, "SchedulerError");
+    return;
+  }
+  st = fw->run_bind(*s, assumed, host);
+  if (st.is_skip()) st = Status(Code::Error, "no bind plugin bound the pod");
+  if (!st.is_success()) {
+    fail(st, "SchedulerError");
+    return;
+  }
+  cache_->finish_binding(*assumed);
+  int64_t t1 = clock_->now_us();
+  metrics_->histogram("xsched_binding_duration_seconds", "").observe(static_cast<double>(t1 - t0) / 1e6);
+  metrics_->histogram("scheduler_e2e_scheduling_duration_seconds", "profile=\"" + fw->profile_name() + "\"")
+      .observe(static_cast<double>(t1 - qpi->timestamp_us) / 1e6);
+  metrics_->histogram("scheduler_pod_scheduling_duration_seconds", "attempts=\"" + std::to_string(qpi->attempts) + "\"")
+      .observe(static_cast<double>(t1 - qpi->initial_attempt_us) / 1e6);
+  metrics_->histogram("scheduler_pod_scheduling_attempts", "").observe(qpi->attempts);
+  if (tracer_.enabled()) tracer_.record(TraceEvent{"bind", assumed->key(), host, t0, t1 - t0, 1});
+  fw->run_post_bind(*s, assumed, host);
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    ++stats_.bound;
+  }
+  note_gang_event(*assumed, true);
+  {
+    std::map<std::string, PodPtr> act;
+    {
+      std::lock_guard<std::mutex> g(to_activate->mu);
+      act.swap(to_activate->pods);
+    }
+    if (!act.empty()) queue_->activate(act);
+  }
+  inflight_.fetch_sub(1);
+}
+
+void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const Status& st, const std::string& reason,
+                               const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins) {
+  PodPtr pod = qpi->pod;
+  if (!nominated.empty()) {
+    nominator_->add(pod, nominated);
+  }
+  // Requeue the latest version unless it was deleted or got assigned.
+  PodPtr latest = informers_->pod(pod->ns(), pod->name());
+  if (latest && latest->uid() == pod->uid() && latest->node_name.empty() && !latest->terminating()) {
+    auto nq = std::make_shared<QueuedPodInfo>(*qpi);
+    nq->pod = latest;
+    nq->unschedulable_plugins = plugins;
+    queue_->add_unschedulable_if_not_present(nq, cycle);
+  }
+  fw.handle().client->record_event("Pod", pod->ns(), pod->name(), "Warning", "FailedScheduling", st.message());
+  if (!opts_.status_updates) return;
+  // updatePod: PodScheduled=False condition + nominatedNodeName, only when changed.
+  std::string msg = st.message();
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    auto& last = last_condition_[pod->uid()];
+    if (last == msg + "|" + nominated && nominated == pod->nominated_node_name) return;
+    last = msg + "|" + nominated;
+    if (last_condition_.size() > 200000) last_condition_.clear();
+  }
+  Json patch = Json::object();
+  Json status = Json::object();
+  Json cond = Json::object();
+  cond.set("type", Json("PodScheduled"));
+  cond.set("status", Json("False"));
+  cond.set("reason", Json(reason));
+  cond.set("message", Json(msg));
+  Json conds = Json::array();
+  conds.push_back(std::move(cond));
+  status.set("conditions", std::move(conds));
+  if (!nominated.empty()) status.set("nominatedNodeName", Json(nominated));
+  patch.set("status", std::move(status));
+  try {
+    fw.handle().client->patch("pods", pod->ns(), pod->name(), patch);
+  } catch (const std::exception&) {
+  }
+}
+
+}  // namespace xsched

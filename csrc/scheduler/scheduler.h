@@ -1,0 +1,196 @@
+// The scheduler: informer ingestion, the serialized scheduling cycle and the
+// asynchronous binding cycle.
+//
+// Reference call stacks: SURVEY.md §3.1-3.3, i.e. vendor/k8s.io/kubernetes/
+// pkg/scheduler/scheduler.go:425-638 (scheduleOne), generic_scheduler.go:93-426
+// (findNodesThatFitPod / prioritizeNodes / selectHost, numFeasibleNodesToFind
+// with the 100-node minimum :47), eventhandlers.go (informer → cache/queue).
+//
+// Threads: one informer thread (store watch → informers/cache/queue), one
+// scheduling thread, a binding executor pool (Permit waits are continuations,
+// not blocked threads), the timer service, and the Filter/Score parallelizer.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "common/clock.h"
+#include "common/parallel.h"
+#include "framework/framework.h"
+#include "scheduler/cache.h"
+#include "scheduler/informers.h"
+#include "scheduler/metrics.h"
+#include "scheduler/queue.h"
+#include "scheduler/trace.h"
+#include "store/store.h"
+
+namespace xsched {
+
+// ApiClient backed by the in-process ObjectStore.
+class StoreClient : public ApiClient {
+ public:
+  explicit StoreClient(std::shared_ptr<ObjectStore> s) : store_(std::move(s)) {}
+  void bind(const Pod& pod, const std::string& node, const Json& annotations) override;
+  void delete_pod(const Pod& pod) override;
+  void patch(const std::string& kind, const std::string& ns, const std::string& name, const Json& patch) override;
+  void record_event(const std::string& kind, const std::string& ns, const std::string& name, const std::string& type,
+                    const std::string& reason, const std::string& msg) override;
+  bool events_enabled = false;
+
+ private:
+  std::shared_ptr<ObjectStore> store_;
+};
+
+// Bounded worker pool for binding cycles.
+class Executor {
+ public:
+  explicit Executor(int threads);
+  ~Executor();
+  void submit(std::function<void()> fn);
+  void stop();
+  size_t pending() const;
+
+ private:
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> threads_;
+  bool stop_ = false;
+  std::atomic<int> busy_{0};
+};
+
+struct SchedulerOptions {
+  int parallelism = 16;
+  int bind_workers = 16;
+  int percentage_of_nodes_to_score = 0;
+  int64_t pod_initial_backoff_us = 1'000'000;
+  int64_t pod_max_backoff_us = 10'000'000;
+  int64_t assumed_pod_ttl_us = 15LL * 60 * 1'000'000;
+  double metrics_sample_rate = 0.1;  // fraction of cycles with per-extension-point metrics
+  bool status_updates = true;        // PodScheduled=False condition patches on failure
+  bool trace = false;
+  uint64_t seed = 0;
+  static SchedulerOptions from_json(const Json& j);
+};
+
+struct GangRecord {
+  std::string pg;  // ns/name
+  int size = 0;
+  int bound = 0;
+  int64_t first_enqueue_us = 0;
+  int64_t admit_us = 0;   // last member allowed at Permit
+  int64_t bound_us = 0;   // last member bound
+};
+
+class Scheduler {
+ public:
+  // config JSON: {"profiles":[...ProfileConfig...], "options":{...}}
+  Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std::shared_ptr<Clock> clock = nullptr,
+            std::shared_ptr<ApiClient> client = nullptr);
+  ~Scheduler();
+
+  void start();  // informer + scheduling threads
+  void stop();
+  // Synchronously drain pending watch events (tests / deterministic drivers).
+  size_t sync_informers(int timeout_ms = 0);
+  // Run exactly one scheduling cycle on the calling thread (tests). Returns
+  // false when the queue was empty within timeout.
+  bool schedule_one(int timeout_ms = 0);
+  // Wait until no pod is in activeQ/backoff, no binding is in flight and no
+  // pod waits at Permit, or timeout. Returns true when idle.
+  bool wait_idle(int timeout_ms);
+
+  SchedulingQueue& queue() { return *queue_; }
+  SchedulerCache& cache() { return *cache_; }
+  Informers& informers() { return *informers_; }
+  Metrics& metrics() { return *metrics_; }
+  Tracer& tracer() { return tracer_; }
+  TimerService& timers() { return *timers_; }
+  Framework* framework_for(const std::string& scheduler_name);
+  const std::vector<std::unique_ptr<Framework>>& frameworks() const { return frameworks_; }
+  std::shared_ptr<Clock> clock() const { return clock_; }
+  std::shared_ptr<ObjectStore> store() const { return store_; }
+
+  struct Stats {
+    uint64_t attempts = 0, scheduled = 0, unschedulable = 0, errors = 0, bound = 0, bind_failures = 0;
+    uint64_t preemption_attempts = 0;
+  };
+  Stats stats() const;
+  std::vector<GangRecord> gang_records(bool clear = false);
+  size_t inflight_bindings() const { return inflight_.load(); }
+
+ private:
+  struct ScheduleResult {
+    std::string host;
+    int evaluated = 0, feasible = 0;
+  };
+  struct Diagnosis {
+    NodeStatusMap node_to_status;
+    std::set<std::string> unschedulable_plugins;
+  };
+
+  void informer_loop();
+  void handle_event(const WatchEvent& ev);
+  void handle_pod_event(const WatchEvent& ev);
+  void handle_node_event(const WatchEvent& ev);
+  void scheduling_loop();
+  void schedule_cycle(const QueuedPodInfoPtr& qpi);
+  Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, std::vector<NodeInfoPtr>& feasible);
+  int num_feasible_nodes_to_find(Framework& fw, int n) const;
+  std::string select_host(const std::vector<NodeScore>& scores);
+  void binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
+                     int64_t cycle, Status permit_status, int64_t wait_start_us,
+                     std::shared_ptr<PodsToActivate> to_activate);
+  void handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const Status& st, const std::string& reason,
+                      const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins);
+  void note_gang_enqueue(const Pod& p, int64_t t);
+  void note_gang_event(const Pod& p, bool bound);
+  bool responsible_for(const Pod& p) const;
+
+  std::shared_ptr<ObjectStore> store_;
+  std::shared_ptr<Clock> clock_;
+  SchedulerOptions opts_;
+  std::unique_ptr<TimerService> timers_;
+  std::unique_ptr<Parallelizer> parallelizer_;
+  std::unique_ptr<Metrics> metrics_;
+  std::unique_ptr<SchedulerCache> cache_;
+  std::unique_ptr<Informers> informers_;
+  std::unique_ptr<Nominator> nominator_;
+  std::unique_ptr<SchedulingQueue> queue_;
+  std::shared_ptr<ApiClient> client_;
+  std::vector<std::unique_ptr<WaitingPods>> waiting_;
+  std::vector<std::unique_ptr<Framework>> frameworks_;
+  std::unordered_map<std::string, Framework*> by_name_;
+  std::unique_ptr<Executor> binder_;
+  Snapshot snapshot_;
+  Tracer tracer_;
+  WatcherPtr watcher_;
+  std::vector<std::string> plugin_kinds_;
+
+  std::thread informer_thread_, sched_thread_;
+  std::atomic<bool> running_{false};
+  std::mutex sched_mu_;  // serializes scheduling cycles (loop vs schedule_one)
+  std::atomic<int> inflight_{0};
+  std::atomic<int> in_cycle_{0};
+  int next_start_node_ = 0;
+  std::mt19937_64 rng_;
+  std::vector<uint64_t> timer_ids_;
+
+  mutable std::mutex stats_mu_;
+  Stats stats_;
+  std::unordered_map<std::string, GangRecord> gangs_;  // open groups
+  std::vector<GangRecord> gang_done_;
+  std::unordered_map<std::string, std::string> last_condition_;  // uid -> last failure message
+};
+
+}  // namespace xsched

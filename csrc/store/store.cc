@@ -1,0 +1,366 @@
+#include "store/store.h"
+
+#include <chrono>
+#include <cstdio>
+#include <thread>
+
+#include "api/types.h"
+
+namespace xsched {
+
+const char* event_type_name(EventType t) {
+  switch (t) {
+    case EventType::Added: return "ADDED";
+    case EventType::Modified: return "MODIFIED";
+    case EventType::Deleted: return "DELETED";
+    case EventType::Bookmark: return "BOOKMARK";
+  }
+  return "UNKNOWN";
+}
+
+// -------------------------------------------------------------- Watcher ----
+void Watcher::push(const WatchEvent& ev) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(ev);
+  }
+  cv_.notify_one();
+}
+
+std::vector<WatchEvent> Watcher::next(int timeout_ms, size_t max) {
+  std::vector<WatchEvent> out;
+  std::unique_lock<std::mutex> lk(mu_);
+  if (q_.empty() && !stopped_.load()) {
+    if (timeout_ms < 0)
+      cv_.wait(lk, [&] { return !q_.empty() || stopped_.load(); });
+    else
+      cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || stopped_.load(); });
+  }
+  size_t n = std::min(max, q_.size());
+  out.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    out.push_back(std::move(q_.front()));
+    q_.pop_front();
+  }
+  return out;
+}
+
+void Watcher::stop() {
+  stopped_.store(true);
+  cv_.notify_all();
+}
+
+size_t Watcher::pending() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return q_.size();
+}
+
+// ---------------------------------------------------------- ObjectStore ----
+ObjectStore::ObjectStore() {
+  uid_salt_ = static_cast<uint64_t>(std::chrono::steady_clock::now().time_since_epoch().count());
+}
+
+bool ObjectStore::namespaced(const std::string& kind) {
+  return !(kind == "nodes" || kind == "priorityclasses" || kind == "noderesourcetopologies" || kind == "namespaces");
+}
+
+void ObjectStore::stamp(Json& obj, int64_t rv) {
+  obj.at_or_create("metadata").set("resourceVersion", Json(std::to_string(rv)));
+}
+
+void ObjectStore::check_faults(const std::string& verb, const std::string& kind) {
+  if (!has_faults_.load(std::memory_order_relaxed)) return;
+  int delay = 0;
+  bool fail = false;
+  {
+    std::lock_guard<std::mutex> g(fault_mu_);
+    for (auto& r : faults_) {
+      if (r.remaining == 0) continue;
+      if ((r.verb == "*" || r.verb == verb) && (r.kind == "*" || r.kind == kind)) {
+        if (r.remaining > 0) --r.remaining;
+        delay += r.delay_us;
+        if (r.fail_prob > 0.0 && std::uniform_real_distribution<double>(0, 1)(fault_rng_) < r.fail_prob) fail = true;
+      }
+    }
+  }
+  if (delay > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay));
+  if (fail) throw StoreError(500, "InternalError", "injected fault: " + verb + " " + kind);
+}
+
+void ObjectStore::add_fault(const FaultRule& r) {
+  std::lock_guard<std::mutex> g(fault_mu_);
+  faults_.push_back(r);
+  has_faults_.store(true);
+}
+
+void ObjectStore::clear_faults() {
+  std::lock_guard<std::mutex> g(fault_mu_);
+  faults_.clear();
+  has_faults_.store(false);
+}
+
+void ObjectStore::emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv) {
+  WatchEvent ev{t, kind, obj, old, rv};
+  const Json& md = (*obj)["metadata"];
+  const std::string& ns = md["namespace"].as_string();
+  for (auto& w : watchers_)
+    if (!w->stopped() && w->wants(kind, ns)) w->push(ev);
+  history_.push_back(std::move(ev));
+  if (history_.size() > history_cap_) {
+    compacted_rv_ = history_.front().rv;
+    history_.pop_front();
+  }
+}
+
+JsonPtr ObjectStore::create_locked(const std::string& kind, Json obj) {
+  Json& md = obj.at_or_create("metadata");
+  std::string name = md["name"].as_string();
+  if (name.empty()) {
+    std::string gen = md["generateName"].as_string();
+    if (gen.empty()) throw StoreError(422, "Invalid", "metadata.name: Required value");
+    char buf[16];
+    std::snprintf(buf, sizeof buf, "%05llx", static_cast<unsigned long long>((uid_counter_ * 2654435761u) & 0xfffff));
+    name = gen + buf;
+    md.set("name", Json(name));
+  }
+  std::string ns = md["namespace"].as_string();
+  if (namespaced(kind) && ns.empty()) {
+    ns = "default";
+    md.set("namespace", Json(ns));
+  }
+  auto& km = kinds_[kind];
+  std::string key = key_of(namespaced(kind) ? ns : "", name);
+  if (km.count(key)) throw StoreError(409, "AlreadyExists", kind + " \"" + name + "\" already exists");
+  ++uid_counter_;
+  char uid[48];
+  uint64_t a = uid_counter_ ^ uid_salt_;
+  std::snprintf(uid, sizeof uid, "%08llx-%04llx-4%03llx-8%03llx-%012llx",
+                static_cast<unsigned long long>(a & 0xffffffff), static_cast<unsigned long long>((a >> 32) & 0xffff),
+                static_cast<unsigned long long>((a >> 48) & 0xfff), static_cast<unsigned long long>(uid_counter_ & 0xfff),
+                static_cast<unsigned long long>(uid_counter_));
+  if (md["uid"].as_string().empty()) md.set("uid", Json(std::string(uid)));
+  if (!md["creationTimestamp"].is_string()) md.set("creationTimestamp", Json(format_rfc3339(wall_now_us())));
+  if (kind == "pods") {
+    Json& st = obj.at_or_create("status");
+    if (!st["phase"].is_string()) st.set("phase", Json("Pending"));
+  }
+  int64_t rv = rv_.fetch_add(1) + 1;
+  stamp(obj, rv);
+  auto ptr = std::make_shared<const Json>(std::move(obj));
+  km[key] = Entry{ptr};
+  emit_locked(EventType::Added, kind, ptr, nullptr, rv);
+  return ptr;
+}
+
+JsonPtr ObjectStore::create(const std::string& kind, Json obj) {
+  check_faults("create", kind);
+  std::lock_guard<std::mutex> g(mu_);
+  return create_locked(kind, std::move(obj));
+}
+
+std::vector<JsonPtr> ObjectStore::create_many(const std::string& kind, std::vector<Json> objs) {
+  check_faults("create", kind);
+  std::vector<JsonPtr> out;
+  out.reserve(objs.size());
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& o : objs) out.push_back(create_locked(kind, std::move(o)));
+  return out;
+}
+
+JsonPtr ObjectStore::get(const std::string& kind, const std::string& ns, const std::string& name) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto kit = kinds_.find(kind);
+  if (kit == kinds_.end()) return nullptr;
+  auto it = kit->second.find(key_of(namespaced(kind) ? ns : "", name));
+  return it == kit->second.end() ? nullptr : it->second.obj;
+}
+
+std::vector<JsonPtr> ObjectStore::list(const std::string& kind, const std::string& ns, int64_t* rv_out) const {
+  std::vector<JsonPtr> out;
+  std::lock_guard<std::mutex> g(mu_);
+  if (rv_out) *rv_out = rv_.load();
+  auto kit = kinds_.find(kind);
+  if (kit == kinds_.end()) return out;
+  out.reserve(kit->second.size());
+  for (const auto& kv : kit->second) {
+    if (!ns.empty() && (*kv.second.obj)["metadata"]["namespace"].as_string() != ns) continue;
+    out.push_back(kv.second.obj);
+  }
+  return out;
+}
+
+size_t ObjectStore::count(const std::string& kind) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto kit = kinds_.find(kind);
+  return kit == kinds_.end() ? 0 : kit->second.size();
+}
+
+JsonPtr ObjectStore::update(const std::string& kind, Json obj, bool check_rv) {
+  check_faults("update", kind);
+  std::lock_guard<std::mutex> g(mu_);
+  const Json& md = obj["metadata"];
+  std::string ns = namespaced(kind) ? md["namespace"].str_or("default") : "";
+  std::string name = md["name"].as_string();
+  auto& km = kinds_[kind];
+  auto it = km.find(key_of(ns, name));
+  if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
+  const Json& cur_md = (*it->second.obj)["metadata"];
+  if (check_rv && md["resourceVersion"].is_string() &&
+      md["resourceVersion"].as_string() != cur_md["resourceVersion"].as_string())
+    throw StoreError(409, "Conflict",
+                     "Operation cannot be fulfilled on " + kind + " \"" + name +
+                         "\": the object has been modified; please apply your changes to the latest version and try again");
+  // Immutable metadata carried over.
+  Json& nmd = obj.at_or_create("metadata");
+  nmd.set("uid", cur_md["uid"]);
+  nmd.set("creationTimestamp", cur_md["creationTimestamp"]);
+  if (ns.size()) nmd.set("namespace", Json(ns));
+  int64_t rv = rv_.fetch_add(1) + 1;
+  stamp(obj, rv);
+  auto ptr = std::make_shared<const Json>(std::move(obj));
+  JsonPtr old = it->second.obj;
+  it->second.obj = ptr;
+  emit_locked(EventType::Modified, kind, ptr, old, rv);
+  return ptr;
+}
+
+JsonPtr ObjectStore::patch(const std::string& kind, const std::string& ns, const std::string& name,
+                           const Json& merge_patch) {
+  check_faults("patch", kind);
+  std::lock_guard<std::mutex> g(mu_);
+  auto& km = kinds_[kind];
+  auto it = km.find(key_of(namespaced(kind) ? ns : "", name));
+  if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
+  Json obj = *it->second.obj;
+  Json saved_md = obj["metadata"];
+  obj.merge_patch(merge_patch);
+  Json& md = obj.at_or_create("metadata");
+  for (const char* k : {"uid", "creationTimestamp", "name", "namespace"})
+    if (const Json* v = saved_md.get(k)) md.set(k, *v);
+  if (obj == *it->second.obj) return it->second.obj;  // no-op patch: no new version
+  int64_t rv = rv_.fetch_add(1) + 1;
+  stamp(obj, rv);
+  auto ptr = std::make_shared<const Json>(std::move(obj));
+  JsonPtr old = it->second.obj;
+  it->second.obj = ptr;
+  emit_locked(EventType::Modified, kind, ptr, old, rv);
+  return ptr;
+}
+
+JsonPtr ObjectStore::remove(const std::string& kind, const std::string& ns, const std::string& name,
+                            int64_t grace_seconds, const std::string& uid_precondition) {
+  check_faults("delete", kind);
+  std::lock_guard<std::mutex> g(mu_);
+  auto& km = kinds_[kind];
+  auto it = km.find(key_of(namespaced(kind) ? ns : "", name));
+  if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
+  if (!uid_precondition.empty() && (*it->second.obj)["metadata"]["uid"].as_string() != uid_precondition)
+    throw StoreError(409, "Conflict", "Precondition failed: UID in precondition does not match");
+  if (kind == "pods" && grace_seconds > 0) {
+    Json obj = *it->second.obj;
+    Json& md = obj.at_or_create("metadata");
+    if (md["deletionTimestamp"].is_string()) return it->second.obj;  // already terminating
+    md.set("deletionTimestamp", Json(format_rfc3339(wall_now_us() + grace_seconds * 1000000)));
+    md.set("deletionGracePeriodSeconds", Json(grace_seconds));
+    int64_t rv = rv_.fetch_add(1) + 1;
+    stamp(obj, rv);
+    auto ptr = std::make_shared<const Json>(std::move(obj));
+    JsonPtr old = it->second.obj;
+    it->second.obj = ptr;
+    emit_locked(EventType::Modified, kind, ptr, old, rv);
+    return ptr;
+  }
+  JsonPtr old = it->second.obj;
+  km.erase(it);
+  int64_t rv = rv_.fetch_add(1) + 1;
+  emit_locked(EventType::Deleted, kind, old, old, rv);
+  return old;
+}
+
+size_t ObjectStore::delete_all(const std::string& kind, const std::string& ns) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto kit = kinds_.find(kind);
+  if (kit == kinds_.end()) return 0;
+  size_t n = 0;
+  for (auto it = kit->second.begin(); it != kit->second.end();) {
+    if (!ns.empty() && (*it->second.obj)["metadata"]["namespace"].as_string() != ns) {
+      ++it;
+      continue;
+    }
+    JsonPtr old = it->second.obj;
+    it = kit->second.erase(it);
+    int64_t rv = rv_.fetch_add(1) + 1;
+    emit_locked(EventType::Deleted, kind, old, old, rv);
+    ++n;
+  }
+  return n;
+}
+
+JsonPtr ObjectStore::bind(const std::string& ns, const std::string& name, const std::string& uid,
+                          const std::string& node, const Json& annotations) {
+  check_faults("bind", "pods");
+  std::lock_guard<std::mutex> g(mu_);
+  auto& km = kinds_["pods"];
+  auto it = km.find(key_of(ns, name));
+  if (it == km.end()) throw StoreError(404, "NotFound", "pods \"" + name + "\" not found");
+  const Json& cur = *it->second.obj;
+  if (!uid.empty() && cur["metadata"]["uid"].as_string() != uid)
+    throw StoreError(409, "Conflict", "Precondition failed: UID in precondition does not match");
+  if (!cur["spec"]["nodeName"].as_string().empty())
+    throw StoreError(409, "Conflict",
+                     "pod " + name + " is already assigned to node \"" + cur["spec"]["nodeName"].as_string() + "\"");
+  if (cur["metadata"]["deletionTimestamp"].is_string())
+    throw StoreError(409, "Conflict", "pod " + name + " is being deleted, cannot be assigned to a host");
+  Json obj = cur;
+  obj.at_or_create("spec").set("nodeName", Json(node));
+  if (annotations.is_object() && annotations.size()) {
+    Json& ann = obj.at_or_create("metadata").at_or_create("annotations");
+    for (const auto& kv : annotations.members()) ann.set(kv.first, kv.second);
+  }
+  Json& st = obj.at_or_create("status");
+  Json cond = Json::object();
+  cond.set("type", Json("PodScheduled"));
+  cond.set("status", Json("True"));
+  cond.set("lastTransitionTime", Json(format_rfc3339(wall_now_us())));
+  Json conds = Json::array();
+  for (const auto& c : st["conditions"].items())
+    if (c["type"].as_string() != "PodScheduled") conds.push_back(c);
+  conds.push_back(std::move(cond));
+  st.set("conditions", std::move(conds));
+  int64_t rv = rv_.fetch_add(1) + 1;
+  stamp(obj, rv);
+  auto ptr = std::make_shared<const Json>(std::move(obj));
+  JsonPtr old = it->second.obj;
+  it->second.obj = ptr;
+  emit_locked(EventType::Modified, "pods", ptr, old, rv);
+  return ptr;
+}
+
+WatcherPtr ObjectStore::watch(const std::set<std::string>& kinds, const std::string& ns, int64_t since_rv) {
+  auto w = std::make_shared<Watcher>(kinds, ns);
+  std::lock_guard<std::mutex> g(mu_);
+  if (since_rv > 0) {
+    if (since_rv < compacted_rv_)
+      throw StoreError(410, "Expired", "too old resource version: " + std::to_string(since_rv));
+    for (const auto& ev : history_) {
+      if (ev.rv <= since_rv) continue;
+      const std::string& ens = (*ev.obj)["metadata"]["namespace"].as_string();
+      if (w->wants(ev.kind, ens)) w->push(ev);
+    }
+  }
+  watchers_.push_back(w);
+  return w;
+}
+
+void ObjectStore::unwatch(const WatcherPtr& w) {
+  w->stop();
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto it = watchers_.begin(); it != watchers_.end(); ++it) {
+    if (*it == w) {
+      watchers_.erase(it);
+      break;
+    }
+  }
+}
+
+}  // namespace xsched

@@ -1,0 +1,152 @@
+// In-process API object store with LIST/WATCH semantics.
+//
+// Plays the role the reference delegates to kube-apiserver + etcd (the
+// integration tests boot a real one through envtest, test/integration/
+// main_test.go:31-49). Objects are JSON documents keyed by kind and
+// namespace/name; every write bumps a global resourceVersion and fans a watch
+// event out to subscribers in commit order. Semantics kept from the apiserver:
+//  * create assigns uid / resourceVersion / creationTimestamp, 409 on exists;
+//  * update with a stale resourceVersion is a 409 Conflict;
+//  * merge-patch (RFC 7386) for PodGroup / ElasticQuota status PATCHes;
+//  * pods/binding copies Binding annotations onto the Pod (the behaviour
+//    FlexGPU.Bind relies on, pkg/flexgpu/flex_gpu.go:230-242) and 409s when
+//    the pod is already bound;
+//  * graceful pod deletion sets deletionTimestamp (terminating) first.
+// A fault-injection hook (drop/delay/fail per verb+kind) backs the failure
+// tests that the reference never had.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <random>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common/json.h"
+
+namespace xsched {
+
+class StoreError : public std::runtime_error {
+ public:
+  StoreError(int code, const std::string& reason, const std::string& msg)
+      : std::runtime_error(msg), code_(code), reason_(reason) {}
+  int code() const { return code_; }
+  const std::string& reason() const { return reason_; }
+
+ private:
+  int code_;
+  std::string reason_;
+};
+
+enum class EventType : uint8_t { Added, Modified, Deleted, Bookmark };
+const char* event_type_name(EventType t);
+
+struct WatchEvent {
+  EventType type;
+  std::string kind;
+  JsonPtr obj;     // new object (or last state for Deleted)
+  JsonPtr old;     // previous object for Modified/Deleted (nullptr for Added)
+  int64_t rv = 0;
+};
+
+class Watcher {
+ public:
+  explicit Watcher(std::set<std::string> kinds, std::string ns) : kinds_(std::move(kinds)), ns_(std::move(ns)) {}
+  // Blocks up to timeout_ms for at least one event; returns up to max events.
+  std::vector<WatchEvent> next(int timeout_ms, size_t max = 4096);
+  void stop();
+  bool stopped() const { return stopped_.load(); }
+  size_t pending() const;
+  bool wants(const std::string& kind, const std::string& ns) const {
+    return (kinds_.empty() || kinds_.count(kind)) && (ns_.empty() || ns.empty() || ns == ns_);
+  }
+  void push(const WatchEvent& ev);
+
+ private:
+  std::set<std::string> kinds_;
+  std::string ns_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<WatchEvent> q_;
+  std::atomic<bool> stopped_{false};
+};
+using WatcherPtr = std::shared_ptr<Watcher>;
+
+struct FaultRule {
+  std::string verb;   // create|update|patch|delete|bind|* ...
+  std::string kind;   // pods|nodes|...|*
+  double fail_prob = 0.0;  // raise 500
+  int delay_us = 0;        // sleep before executing
+  int remaining = -1;      // -1 = unlimited
+};
+
+class ObjectStore {
+ public:
+  ObjectStore();
+
+  JsonPtr create(const std::string& kind, Json obj);
+  JsonPtr get(const std::string& kind, const std::string& ns, const std::string& name) const;  // nullptr if absent
+  std::vector<JsonPtr> list(const std::string& kind, const std::string& ns, int64_t* rv_out = nullptr) const;
+  JsonPtr update(const std::string& kind, Json obj, bool check_rv = true);
+  JsonPtr patch(const std::string& kind, const std::string& ns, const std::string& name, const Json& merge_patch);
+  // Deletes the object; for pods with grace_seconds > 0 sets deletionTimestamp instead.
+  JsonPtr remove(const std::string& kind, const std::string& ns, const std::string& name, int64_t grace_seconds = 0,
+                 const std::string& uid_precondition = "");
+  JsonPtr bind(const std::string& ns, const std::string& name, const std::string& uid, const std::string& node,
+               const Json& annotations);
+
+  // Watch. since_rv > 0 replays retained history after that version (410 Gone
+  // if it has been compacted away).
+  WatcherPtr watch(const std::set<std::string>& kinds, const std::string& ns = "", int64_t since_rv = 0);
+  void unwatch(const WatcherPtr& w);
+
+  int64_t resource_version() const { return rv_.load(); }
+  size_t count(const std::string& kind) const;
+
+  void add_fault(const FaultRule& r);
+  void clear_faults();
+
+  // Bulk helpers for benchmarks (one lock hold, one event per object).
+  std::vector<JsonPtr> create_many(const std::string& kind, std::vector<Json> objs);
+  size_t delete_all(const std::string& kind, const std::string& ns = "");
+
+  static std::string key_of(const std::string& ns, const std::string& name) { return ns.empty() ? name : ns + "/" + name; }
+  static bool namespaced(const std::string& kind);
+
+ private:
+  struct Entry {
+    JsonPtr obj;
+  };
+  using KindMap = std::unordered_map<std::string, Entry>;
+
+  void check_faults(const std::string& verb, const std::string& kind);
+  void emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv);
+  JsonPtr create_locked(const std::string& kind, Json obj);
+  static void stamp(Json& obj, int64_t rv);
+
+  mutable std::mutex mu_;
+  std::unordered_map<std::string, KindMap> kinds_;
+  std::atomic<int64_t> rv_{0};
+  std::vector<WatcherPtr> watchers_;
+  std::deque<WatchEvent> history_;
+  size_t history_cap_ = 50000;
+  int64_t compacted_rv_ = 0;
+  uint64_t uid_counter_ = 0;
+  uint64_t uid_salt_;
+
+  std::mutex fault_mu_;
+  std::vector<FaultRule> faults_;
+  std::atomic<bool> has_faults_{false};
+  std::mt19937_64 fault_rng_{12345};
+};
+
+}  // namespace xsched

@@ -1,0 +1,394 @@
+"""KubeSchedulerConfiguration loading, plugin-set resolution and plugin-args
+defaulting.
+
+Accepts the same YAML the reference ships (``kubescheduler.config.k8s.io``
+v1beta2 and v1beta3, e.g. manifests/flexgpu/templates/configmap.yaml and
+manifests/*/scheduler-config.yaml) and resolves it into the flat per-profile
+plugin lists the native framework consumes.
+
+Semantics reproduced:
+  * per-extension-point ``enabled`` appended to the defaults, ``disabled``
+    removing defaults (``"*"`` removes all) — kube-scheduler's mergePlugins;
+  * v1beta3 ``multiPoint`` expansion (a plugin enabled at every point it
+    implements, weights carried to score);
+  * plugin args defaults of apis/config/v1beta2/defaults.go:28-157
+    (identical in v1beta3) and upstream DefaultPreemptionArgs;
+  * strict decoding: unknown args fields are errors (scheme.go:35 uses the
+    strict codec).
+"""
+from __future__ import annotations
+
+import copy
+import json
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any
+
+import yaml
+
+API_VERSIONS = ("kubescheduler.config.k8s.io/v1beta2", "kubescheduler.config.k8s.io/v1beta3")
+EXT_POINTS = ("queueSort", "preFilter", "filter", "postFilter", "preScore", "score", "reserve", "permit",
+              "preBind", "bind", "postBind")
+
+# Extension points each native plugin implements (csrc/plugins/*.cc).
+PLUGIN_POINTS: dict[str, tuple[str, ...]] = {
+    # in-tree defaults
+    "PrioritySort": ("queueSort",),
+    "NodeUnschedulable": ("filter",),
+    "NodeName": ("filter",),
+    "NodePorts": ("preFilter", "filter"),
+    "NodeResourcesFit": ("preFilter", "filter", "score"),
+    "NodeResourcesBalancedAllocation": ("score",),
+    "TaintToleration": ("filter", "preScore", "score"),
+    "NodeAffinity": ("preFilter", "filter", "preScore", "score"),
+    "PodTopologySpread": ("preFilter", "filter", "preScore", "score"),
+    "InterPodAffinity": ("preFilter", "filter", "preScore", "score"),
+    "ImageLocality": ("score",),
+    "DefaultPreemption": ("postFilter",),
+    "DefaultBinder": ("bind",),
+    # out-of-tree (the reference's pkg/*)
+    "FlexGPU": ("filter", "score", "reserve", "bind"),
+    "Coscheduling": ("queueSort", "preFilter", "postFilter", "reserve", "permit", "postBind"),
+    "CapacityScheduling": ("preFilter", "postFilter", "reserve"),
+    "NodeResourcesAllocatable": ("score",),
+    "NodeResourceTopologyMatch": ("filter", "score"),
+    "TargetLoadPacking": ("score",),
+    "LoadVariationRiskBalancing": ("score",),
+    "PreemptionToleration": ("postFilter",),
+    "PodState": ("score",),
+    "QOSSort": ("queueSort",),
+}
+
+# Volume plugins are part of upstream's default set but have no meaning for a
+# store without PersistentVolumes; accepted in configs and ignored.
+NOT_APPLICABLE = {"VolumeRestrictions", "EBSLimits", "GCEPDLimits", "NodeVolumeLimits", "AzureDiskLimits",
+                  "VolumeBinding", "VolumeZone", "CinderLimits", "SelectorSpread"}
+
+# kube-scheduler 1.23 v1beta2 default plugin set (default_plugins.go:34-106),
+# minus NOT_APPLICABLE.
+DEFAULT_PLUGINS: dict[str, list[tuple[str, int]]] = {
+    "queueSort": [("PrioritySort", 0)],
+    "preFilter": [("NodeResourcesFit", 0), ("NodePorts", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0),
+                  ("NodeAffinity", 0)],
+    "filter": [("NodeUnschedulable", 0), ("NodeName", 0), ("TaintToleration", 0), ("NodeAffinity", 0),
+               ("NodePorts", 0), ("NodeResourcesFit", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
+    "postFilter": [("DefaultPreemption", 0)],
+    "preScore": [("InterPodAffinity", 0), ("PodTopologySpread", 0), ("TaintToleration", 0), ("NodeAffinity", 0)],
+    "score": [("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1), ("InterPodAffinity", 1),
+              ("NodeResourcesFit", 1), ("NodeAffinity", 1), ("PodTopologySpread", 2), ("TaintToleration", 1)],
+    "reserve": [],
+    "permit": [],
+    "preBind": [],
+    "bind": [("DefaultBinder", 0)],
+    "postBind": [],
+}
+
+
+class ConfigError(ValueError):
+    pass
+
+
+# ----------------------------------------------------------------- args ----
+def _strict(name: str, args: dict, allowed: set[str]) -> None:
+    extra = set(args) - allowed - {"apiVersion", "kind"}
+    if extra:
+        raise ConfigError(f'strict decoding error: unknown field(s) {sorted(extra)} in {name}Args')
+
+
+def _resource_specs(v: Any, where: str) -> list[dict]:
+    if v is None:
+        return []
+    if not isinstance(v, list):
+        raise ConfigError(f"{where}: resources must be a list")
+    out = []
+    for r in v:
+        if not isinstance(r, dict) or "name" not in r:
+            raise ConfigError(f"{where}: resource spec needs a name")
+        out.append({"name": str(r["name"]), "weight": int(r.get("weight", 0))})
+    return out
+
+
+def _metric_provider(args: dict, where: str) -> dict:
+    mp = dict(args.get("metricProvider") or {})
+    _strict(where + ".metricProvider", mp, {"type", "address", "token", "insecureSkipVerify"})
+    return mp
+
+
+def default_plugin_args(name: str, args: dict | None) -> dict:
+    """Apply SetDefaults_<Name>Args (apis/config/v1beta2/defaults.go)."""
+    a = copy.deepcopy(args or {})
+    if name == "Coscheduling":
+        _strict(name, a, {"permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds", "kubeConfigPath", "kubeMaster"})
+        a.setdefault("permitWaitingTimeSeconds", 60)
+        a.setdefault("deniedPGExpirationTimeSeconds", 20)
+        for k in ("permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds"):
+            if int(a[k]) < 0:
+                raise ConfigError(f"{name}Args.{k} must be >= 0")
+    elif name == "NodeResourcesAllocatable":
+        _strict(name, a, {"resources", "mode"})
+        res = _resource_specs(a.get("resources"), name)
+        a["resources"] = res or [{"name": "cpu", "weight": 1 << 20}, {"name": "memory", "weight": 1}]
+        a["mode"] = a.get("mode") or "Least"
+        if a["mode"] not in ("Least", "Most"):
+            raise ConfigError(f"{name}Args.mode must be Least or Most, got {a['mode']!r}")
+    elif name == "TargetLoadPacking":
+        _strict(name, a, {"defaultRequests", "defaultRequestsMultiplier", "targetUtilization", "metricProvider",
+                          "watcherAddress"})
+        a.setdefault("defaultRequests", {"cpu": "1000m"})
+        if a.get("defaultRequestsMultiplier") is None:
+            a["defaultRequestsMultiplier"] = "1.5"
+        if a.get("targetUtilization") is None or int(a["targetUtilization"]) <= 0:
+            a["targetUtilization"] = 40
+        mp = _metric_provider(a, name)
+        if a.get("watcherAddress") is None and not mp.get("type"):
+            mp["type"] = "KubernetesMetricsServer"
+        if mp.get("type") == "Prometheus" and mp.get("insecureSkipVerify") is None:
+            mp["insecureSkipVerify"] = True
+        a["metricProvider"] = mp
+    elif name == "LoadVariationRiskBalancing":
+        _strict(name, a, {"metricProvider", "watcherAddress", "safeVarianceMargin", "safeVarianceSensitivity"})
+        mp = _metric_provider(a, name)
+        if a.get("watcherAddress") is None and not mp.get("type"):
+            mp["type"] = "KubernetesMetricsServer"
+        if mp.get("type") == "Prometheus" and mp.get("insecureSkipVerify") is None:
+            mp["insecureSkipVerify"] = True
+        a["metricProvider"] = mp
+        if a.get("safeVarianceMargin") is None or float(a["safeVarianceMargin"]) < 0:
+            a["safeVarianceMargin"] = 1.0
+        if a.get("safeVarianceSensitivity") is None or float(a["safeVarianceSensitivity"]) < 0:
+            a["safeVarianceSensitivity"] = 1.0
+    elif name == "NodeResourceTopologyMatch":
+        _strict(name, a, {"scoringStrategy"})
+        ss = dict(a.get("scoringStrategy") or {})
+        _strict(name + ".scoringStrategy", ss, {"type", "resources"})
+        ss.setdefault("type", "LeastAllocated")
+        if ss["type"] not in ("LeastAllocated", "MostAllocated", "BalancedAllocation", "XGMIGangAffinity"):
+            raise ConfigError(f"{name}Args.scoringStrategy.type {ss['type']!r} is not supported")
+        res = _resource_specs(ss.get("resources"), name) or [{"name": "cpu", "weight": 1}, {"name": "memory", "weight": 1}]
+        for r in res:
+            if r["weight"] == 0:
+                r["weight"] = 1
+        ss["resources"] = res
+        a["scoringStrategy"] = ss
+    elif name in ("PreemptionToleration", "DefaultPreemption"):
+        _strict(name, a, {"minCandidateNodesPercentage", "minCandidateNodesAbsolute"})
+        a.setdefault("minCandidateNodesPercentage", 10)
+        a.setdefault("minCandidateNodesAbsolute", 100)
+        p, n = int(a["minCandidateNodesPercentage"]), int(a["minCandidateNodesAbsolute"])
+        if not 0 <= p <= 100:
+            raise ConfigError(f"{name}Args.minCandidateNodesPercentage must be in [0, 100]")
+        if n < 0 or (p == 0 and n == 0):
+            raise ConfigError(f"{name}Args: both minCandidateNodes values cannot be zero")
+    elif name == "FlexGPU":
+        _strict(name, a, {"gpuResourceName", "memoryResourceName", "xcdResourceName", "indexAnnotationKey",
+                          "partitionAnnotationKey"})
+        a.setdefault("gpuResourceName", "amd.com/gpu")
+        a.setdefault("memoryResourceName", "amd.com/gpu-memory")
+        a.setdefault("xcdResourceName", "amd.com/gpu-xcd")
+        a.setdefault("indexAnnotationKey", "amd.com/gpu-index")
+        a.setdefault("partitionAnnotationKey", "amd.com/gpu-partitions")
+    elif name == "NodeResourcesFit":
+        _strict(name, a, {"ignoredResources", "ignoredResourceGroups", "scoringStrategy"})
+        ss = dict(a.get("scoringStrategy") or {})
+        ss.setdefault("type", "LeastAllocated")
+        ss["resources"] = _resource_specs(ss.get("resources"), name) or [
+            {"name": "cpu", "weight": 1}, {"name": "memory", "weight": 1}]
+        a["scoringStrategy"] = ss
+    elif name == "NodeResourcesBalancedAllocation":
+        _strict(name, a, {"resources"})
+        a["resources"] = _resource_specs(a.get("resources"), name) or [
+            {"name": "cpu", "weight": 1}, {"name": "memory", "weight": 1}]
+    elif name == "PodTopologySpread":
+        _strict(name, a, {"defaultConstraints", "defaultingType"})
+        a.setdefault("defaultingType", "System")
+    elif name == "InterPodAffinity":
+        _strict(name, a, {"hardPodAffinityWeight"})
+        a.setdefault("hardPodAffinityWeight", 1)
+    elif name == "NodeAffinity":
+        _strict(name, a, {"addedAffinity"})
+    return a
+
+
+# -------------------------------------------------------------- profiles ----
+@dataclass
+class Profile:
+    scheduler_name: str = "default-scheduler"
+    plugins: dict[str, list[str]] = field(default_factory=dict)
+    score_weights: dict[str, int] = field(default_factory=dict)
+    plugin_config: dict[str, dict] = field(default_factory=dict)
+    percentage_of_nodes_to_score: int = 0
+
+    def to_native(self) -> dict:
+        plugins = {}
+        for pt in EXT_POINTS:
+            names = self.plugins.get(pt, [])
+            if not names:
+                continue
+            if pt == "score":
+                plugins[pt] = [{"name": n, "weight": self.score_weights.get(n, 1)} for n in names]
+            else:
+                plugins[pt] = list(names)
+        used = {n for names in self.plugins.values() for n in names}
+        return {
+            "schedulerName": self.scheduler_name,
+            "plugins": plugins,
+            "pluginConfig": {n: a for n, a in self.plugin_config.items() if n in used},
+            "percentageOfNodesToScore": self.percentage_of_nodes_to_score,
+        }
+
+
+@dataclass
+class SchedulerConfiguration:
+    profiles: list[Profile]
+    parallelism: int = 16
+    percentage_of_nodes_to_score: int = 0
+    pod_initial_backoff_seconds: float = 1.0
+    pod_max_backoff_seconds: float = 10.0
+    leader_elect: bool = False
+    bind_workers: int = 16
+    status_updates: bool = True
+    trace: bool = False
+    api_version: str = API_VERSIONS[0]
+    raw: dict = field(default_factory=dict)
+
+    def to_native(self, **overrides) -> dict:
+        opts = {
+            "parallelism": self.parallelism,
+            "percentageOfNodesToScore": self.percentage_of_nodes_to_score,
+            "podInitialBackoffSeconds": self.pod_initial_backoff_seconds,
+            "podMaxBackoffSeconds": self.pod_max_backoff_seconds,
+            "bindWorkers": self.bind_workers,
+            "statusUpdates": self.status_updates,
+            "trace": self.trace,
+        }
+        opts.update(overrides)
+        return {"profiles": [p.to_native() for p in self.profiles], "options": opts}
+
+    def profile(self, name: str) -> Profile:
+        for p in self.profiles:
+            if p.scheduler_name == name:
+                return p
+        raise KeyError(name)
+
+
+def _names(entries: Any) -> list[tuple[str, int]]:
+    out = []
+    for e in entries or []:
+        if isinstance(e, str):
+            out.append((e, 0))
+        elif isinstance(e, dict) and "name" in e:
+            out.append((str(e["name"]), int(e.get("weight", 0) or 0)))
+        else:
+            raise ConfigError(f"invalid plugin entry {e!r}")
+    return out
+
+
+def _resolve_profile(p: dict, api_version: str, available: set[str] | None) -> Profile:
+    prof = Profile(scheduler_name=p.get("schedulerName") or "default-scheduler")
+    if "percentageOfNodesToScore" in p and p["percentageOfNodesToScore"] is not None:
+        prof.percentage_of_nodes_to_score = int(p["percentageOfNodesToScore"])
+    spec = p.get("plugins") or {}
+    unknown = set(spec) - set(EXT_POINTS) - {"multiPoint"}
+    if unknown:
+        raise ConfigError(f"unknown extension point(s) {sorted(unknown)}")
+    if "multiPoint" in spec and not api_version.endswith("v1beta3"):
+        raise ConfigError("multiPoint requires kubescheduler.config.k8s.io/v1beta3")
+    weights: dict[str, int] = {}
+    resolved: dict[str, list[str]] = {}
+    mp = spec.get("multiPoint") or {}
+    mp_enabled = _names(mp.get("enabled"))
+    mp_disabled = {n for n, _ in _names(mp.get("disabled"))}
+    for pt in EXT_POINTS:
+        defaults = [] if "*" in mp_disabled else [(n, w) for n, w in DEFAULT_PLUGINS[pt] if n not in mp_disabled]
+        pts = spec.get(pt) or {}
+        disabled = {n for n, _ in _names(pts.get("disabled"))}
+        enabled = _names(pts.get("enabled"))
+        cur: list[tuple[str, int]] = []
+        if "*" not in disabled:
+            cur = [(n, w) for n, w in defaults if n not in disabled]
+        for n, w in mp_enabled:
+            if pt in PLUGIN_POINTS.get(n, ()) and n not in {x for x, _ in cur}:
+                cur.append((n, w))
+        for n, w in enabled:
+            cur = [(x, y) for x, y in cur if x != n]  # explicit enable re-positions/overrides weight
+            cur.append((n, w))
+        names = []
+        for n, w in cur:
+            if n in NOT_APPLICABLE:
+                continue
+            if n not in PLUGIN_POINTS:
+                raise ConfigError(f'plugin "{n}" does not exist')
+            if pt not in PLUGIN_POINTS[n]:
+                raise ConfigError(f'plugin "{n}" does not extend {pt} plugin')
+            if available is not None and n not in available:
+                continue  # registered in config tables but not compiled into this build
+            names.append(n)
+            if pt == "score":
+                weights[n] = w if w > 0 else weights.get(n, 1)
+        if pt == "queueSort" and len(names) > 1:
+            raise ConfigError(f"profile {prof.scheduler_name}: only one queueSort plugin may be enabled, got {names}")
+        resolved[pt] = names
+    prof.plugins = resolved
+    prof.score_weights = weights
+    for pc in p.get("pluginConfig") or []:
+        name = pc.get("name")
+        if not name:
+            raise ConfigError("pluginConfig entry without name")
+        prof.plugin_config[name] = default_plugin_args(name, pc.get("args"))
+    used = {n for names in resolved.values() for n in names}
+    for n in used:
+        if n not in prof.plugin_config:
+            prof.plugin_config[n] = default_plugin_args(n, None)
+    return prof
+
+
+def _available_plugins() -> set[str] | None:
+    try:
+        from ._native import native
+
+        return set(native().plugin_names())
+    except Exception:  # pragma: no cover - config parsing works without the core
+        return None
+
+
+def load_config(src: str | Path | dict | None = None, *, restrict_to_native: bool = True) -> SchedulerConfiguration:
+    """Load a KubeSchedulerConfiguration from a YAML path/string or a dict."""
+    if src is None:
+        doc: dict = {"apiVersion": API_VERSIONS[0], "kind": "KubeSchedulerConfiguration"}
+    elif isinstance(src, dict):
+        doc = copy.deepcopy(src)
+    else:
+        text = Path(src).read_text() if (isinstance(src, Path) or (isinstance(src, str) and "\n" not in src
+                                                                   and Path(src).exists())) else str(src)
+        doc = yaml.safe_load(text) or {}
+    api = doc.get("apiVersion", API_VERSIONS[0])
+    if api not in API_VERSIONS:
+        raise ConfigError(f"unsupported apiVersion {api!r}")
+    if doc.get("kind", "KubeSchedulerConfiguration") != "KubeSchedulerConfiguration":
+        raise ConfigError(f"unsupported kind {doc.get('kind')!r}")
+    available = _available_plugins() if restrict_to_native else None
+    profiles_raw = doc.get("profiles") or [{"schedulerName": "default-scheduler"}]
+    profiles = [_resolve_profile(p, api, available) for p in profiles_raw]
+    names = [p.scheduler_name for p in profiles]
+    if len(set(names)) != len(names):
+        raise ConfigError(f"duplicate profile schedulerName in {names}")
+    qs = {tuple(p.plugins.get("queueSort", [])) for p in profiles}
+    if len(qs) > 1:
+        raise ConfigError("all profiles must use the same queueSort plugin")
+    cfg = SchedulerConfiguration(profiles=profiles, api_version=api, raw=doc)
+    if doc.get("parallelism") is not None:
+        cfg.parallelism = int(doc["parallelism"])
+        if cfg.parallelism <= 0:
+            raise ConfigError("parallelism must be > 0")
+    if doc.get("percentageOfNodesToScore") is not None:
+        cfg.percentage_of_nodes_to_score = int(doc["percentageOfNodesToScore"])
+    if doc.get("podInitialBackoffSeconds") is not None:
+        cfg.pod_initial_backoff_seconds = float(doc["podInitialBackoffSeconds"])
+    if doc.get("podMaxBackoffSeconds") is not None:
+        cfg.pod_max_backoff_seconds = float(doc["podMaxBackoffSeconds"])
+    cfg.leader_elect = bool((doc.get("leaderElection") or {}).get("leaderElect", False))
+    return cfg
+
+
+def native_config_json(cfg: SchedulerConfiguration, **overrides) -> str:
+    return json.dumps(cfg.to_native(**overrides))
