@@ -1,0 +1,137 @@
+#!/usr/bin/env python
+"""Headline benchmark: scheduling throughput (pods/s) and p99 PodGroup
+gang-admit latency for 1/2/4/8-GPU groups on synthetic 8x MI355X nodes.
+
+Metric and config come from BASELINE.json (the reference publishes no
+numbers, so vs_baseline is null). One process per GPU; each rank runs one
+scheduler shard (its own store + scheduler over `--nodes` 8x MI355X nodes),
+so per-GPU work is fixed as N grows (weak scaling) and `value` is the sum of
+pods/s over ranks divided by the slowest rank's time.
+
+GPU use: each rank discovers its MI355X with the HIP probe (device props +
+checksum health test, untimed) and sizes the synthetic nodes' HBM from it;
+after the timed steps, N>1 runs an RCCL all-reduce sweep over the ranks to
+report xGMI bus bandwidth for the placement (untimed).
+
+    python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "pods/sec sched throughput + p99 PodGroup gang-admit latency, 1/2/4/8-GPU groups"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nodes", type=int, default=64, help="8x MI355X nodes per scheduler shard")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-gpu-probe", action="store_true")
+    ap.add_argument("--trace", default="", help="write a Chrome trace of rank 0's timed steps")
+    args = ap.parse_args()
+
+    from flex_gpu_scheduler_amd.parallel.dist import init_distributed
+    from flex_gpu_scheduler_amd.utils.benchrun import Shard, gang_latency_summary
+    from flex_gpu_scheduler_amd.utils.workload import ClusterSpec
+
+    ctx = init_distributed(want_cuda=True)
+    extras: dict = {}
+    hbm_gib = 288
+    if ctx.cuda and not args.no_gpu_probe:
+        from flex_gpu_scheduler_amd.ops.hip_probe import probe
+
+        pr = probe()
+        props = pr.props(ctx.local_rank)
+        health = pr.health(ctx.local_rank)
+        if not health["healthy"]:
+            raise SystemExit(f"GPU {ctx.local_rank} failed the checksum health test: {health}")
+        hbm_gib = max(1, int(props["totalGlobalMem"]) // (1 << 30))
+        extras["gpu"] = {"name": props.get("gcnArchName"), "computeUnits": props.get("computeUnits"),
+                         "hbm_gib": hbm_gib}
+
+    spec = ClusterSpec(nodes=args.nodes, hbm_gib=hbm_gib)
+    shard = Shard(spec, namespace=f"bench-r{ctx.rank}", seed=args.seed + 7919 * ctx.rank)
+    # Pre-render every wave's JSON (data preparation, outside the timed region).
+    waves = [shard.wave(i) for i in range(args.warmup + args.steps)]
+    prepared = [(w.groups_json(), w.pods_json()) for w in waves]
+
+    for i in range(args.warmup):
+        shard.run(waves[i], prepared=prepared[i])
+
+    if args.trace and ctx.rank == 0:
+        shard.sched.set_trace(True)
+    ctx.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    pods = 0
+    gangs: list[dict] = []
+    for i in range(args.warmup, args.warmup + args.steps):
+        r = shard.run(waves[i], prepared=prepared[i])
+        pods += r.pods
+        gangs.extend(r.gangs)
+    ctx.sync()
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    if args.trace and ctx.rank == 0:
+        with open(args.trace, "w") as f:
+            f.write(shard.sched.trace_json())
+
+    t_max = ctx.all_max(elapsed)
+    pods_total = ctx.all_sum(float(pods))
+    all_gangs = [g for part in ctx.gather(gangs) for g in part]
+    stats = shard.sched.stats()
+    shard.close()
+
+    if ctx.distributed and ctx.cuda:
+        from flex_gpu_scheduler_amd.parallel.rccl_probe import allreduce_sweep
+
+        res = allreduce_sweep()
+        extras["rccl_allreduce"] = [{"MiB": r.bytes >> 20, "busbw_GBps": round(r.busbw_gbps, 1)} for r in res]
+
+    value = pods_total / t_max if t_max > 0 else 0.0
+    if ctx.rank == 0:
+        lat = gang_latency_summary(all_gangs)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "pods/s",
+            "n_gpus": args.gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max * 1000.0 / max(1, args.steps), 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic pod specs / random resource requests (BASELINE.json configs)",
+            "config": {
+                "model": "FlexGPU(MI355X SPX/CPX/HBM) + Coscheduling + NRT xGMI gang placement",
+                "global_batch": int(round(pods_total / max(1, args.steps))),
+                "seq_len": None,
+                "parallelism": f"{ctx.world_size} scheduler shard(s), one per GPU",
+                "nodes_per_shard": args.nodes,
+                "gpus_per_shard": args.nodes * 8,
+                "p99_gang_admit_ms": {k: v["p99_ms"] for k, v in lat.items()},
+                "gang_admit": lat,
+                "attempts": stats["attempts"],
+                "unschedulable_attempts": stats["unschedulable"],
+                **extras,
+            },
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -9,8 +9,17 @@ ResourceRegistry& ResourceRegistry::get() {
   return *r;
 }
 
+uint8_t ResourceRegistry::flags_for(std::string_view n) {
+  uint8_t f = 0;
+  // v1helper.IsNativeResource: no domain prefix or the kubernetes.io/ domain.
+  if (n.find('/') == std::string_view::npos || n.rfind("kubernetes.io/", 0) == 0) f |= kNative;
+  if (n.rfind("hugepages-", 0) == 0) f |= kHuge;
+  return f;
+}
+
 ResourceRegistry::ResourceRegistry() {
   for (const char* n : {"cpu", "memory", "ephemeral-storage", "pods"}) {
+    flags_[names_.size()] = flags_for(n);
     ids_.emplace(n, static_cast<int>(names_.size()));
     names_.emplace_back(n);
   }
@@ -23,6 +32,7 @@ int ResourceRegistry::id(std::string_view name) {
   if (static_cast<int>(names_.size()) >= kMaxRes)
     throw std::runtime_error("too many distinct resource names (max " + std::to_string(kMaxRes) + ")");
   int id = static_cast<int>(names_.size());
+  flags_[id] = flags_for(name);
   names_.emplace_back(name);
   ids_.emplace(std::string(name), id);
   return id;
@@ -42,19 +52,6 @@ std::string ResourceRegistry::name(int id) const {
 int ResourceRegistry::size() const {
   std::lock_guard<std::mutex> g(mu_);
   return static_cast<int>(names_.size());
-}
-
-bool ResourceRegistry::is_hugepages(int id) const {
-  std::string n = name(id);
-  return n.rfind("hugepages-", 0) == 0;
-}
-
-bool ResourceRegistry::is_native(int id) const {
-  if (id <= kPods) return true;
-  std::string n = name(id);
-  // v1helper.IsNativeResource: no domain prefix or kubernetes.io/ domain.
-  if (n.find('/') == std::string::npos) return true;
-  return n.rfind("kubernetes.io/", 0) == 0;
 }
 
 int64_t quantity_to_res_units(int id, const Quantity& q) {

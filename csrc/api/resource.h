@@ -34,11 +34,15 @@ class ResourceRegistry {
   std::string name(int id) const;
   int size() const;
   // Native resources per k8s (cpu, memory, ephemeral-storage, pods, hugepages-*).
-  bool is_native(int id) const;
-  bool is_hugepages(int id) const;
+  // Flags are fixed at interning time, so these are lock-free.
+  bool is_native(int id) const { return id >= 0 && id < kMaxRes && (flags_[id] & kNative); }
+  bool is_hugepages(int id) const { return id >= 0 && id < kMaxRes && (flags_[id] & kHuge); }
 
  private:
+  enum : uint8_t { kNative = 1, kHuge = 2 };
+  static uint8_t flags_for(std::string_view name);
   ResourceRegistry();
+  std::array<uint8_t, kMaxRes> flags_{};
   mutable std::mutex mu_;
   std::vector<std::string> names_;
   std::unordered_map<std::string, int> ids_;

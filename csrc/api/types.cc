@@ -386,6 +386,7 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
   p->request = sum;
   p->qos = compute_qos(*p);
   if (const std::string* pg = p->meta.label(kPodGroupLabel)) p->pod_group = *pg;
+  p->gpu_demand = compute_gpu_demand(*p);
   p->recompute_gpu_assignment();
   return p;
 }
@@ -512,8 +513,15 @@ std::shared_ptr<NodeResourceTopology> NodeResourceTopology::from_json(const Json
       zone.resources.push_back(ri);
     }
     for (const auto& c : z["costs"].items()) zone.costs.emplace_back(c["name"].as_string(), c["value"].as_int());
+    if (zone.type == "Node" && zone.numa_id >= 0 && zone.numa_id <= 63) {
+      NumaZone nz;
+      nz.id = zone.numa_id;
+      for (const auto& r : zone.resources) nz.res.emplace_back(r.res, r.available);
+      nrt->numa.push_back(std::move(nz));
+    }
     nrt->zones.push_back(std::move(zone));
   }
+  std::sort(nrt->numa.begin(), nrt->numa.end(), [](const NumaZone& a, const NumaZone& b) { return a.id < b.id; });
   return nrt;
 }
 
@@ -540,8 +548,40 @@ GpuNames& gpu_names() {
   static GpuNames* g = new GpuNames();
   return *g;
 }
-int GpuNames::gpu_id() const { return res_id(gpu); }
-int GpuNames::memory_id() const { return res_id(memory); }
-int GpuNames::xcd_id() const { return res_id(xcd); }
+void GpuNames::refresh() const {
+  gpu_rid_ = res_id(gpu);
+  mem_rid_ = res_id(memory);
+  xcd_rid_ = res_id(xcd);
+  ids_ready_ = true;
+}
+
+GpuDemand compute_gpu_demand(const Pod& p) {
+  const GpuNames& gn = gpu_names();
+  int gid = gn.gpu_id(), mid = gn.memory_id(), xid = gn.xcd_id();
+  bool has_g = false, has_m = false, has_x = false;
+  for (const auto& c : p.containers) {  // presence per container limit (podResourceLimit)
+    has_g |= c.limits.has(gid);
+    has_m |= c.limits.has(mid);
+    has_x |= c.limits.has(xid);
+  }
+  GpuDemand d;
+  int kinds = int(has_g) + int(has_m) + int(has_x);
+  if (kinds == 0) return d;
+  if (kinds > 1) {
+    d.kind = GpuDemand::Conflict;
+    return d;
+  }
+  if (has_g) {
+    d.kind = GpuDemand::Gpu;
+    d.amount = p.limit_sum.get(gid);
+  } else if (has_x) {
+    d.kind = GpuDemand::Xcd;
+    d.amount = p.limit_sum.get(xid);
+  } else {
+    d.kind = GpuDemand::Memory;
+    d.amount = p.limit_sum.get(mid);
+  }
+  return d;
+}
 
 }  // namespace xsched

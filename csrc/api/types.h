@@ -115,6 +115,13 @@ struct GpuAssignment {
   bool valid() const { return kind != Kind::None; }
 };
 
+// What a pod asks of the FlexGPU plugin (decoded once at parse time).
+struct GpuDemand {
+  enum Kind : uint8_t { None, Gpu, Xcd, Memory, Conflict };
+  Kind kind = None;
+  int64_t amount = 0;
+};
+
 struct Pod {
   ObjectMeta meta;
   std::string scheduler_name = kDefaultSchedulerName;
@@ -140,6 +147,7 @@ struct Pod {
   std::string pod_group;  // value of kPodGroupLabel ("" if none)
   std::vector<ContainerPort> host_ports;
   GpuAssignment gpu;      // decoded from annotations (mutable via cache only)
+  GpuDemand gpu_demand;   // FlexGPU demand from container limits
 
   const std::string& ns() const { return meta.ns; }
   const std::string& name() const { return meta.name; }
@@ -200,10 +208,21 @@ struct NRTZone {
   std::vector<NRTResourceInfo> resources;
   std::vector<std::pair<std::string, int64_t>> costs;
 };
+struct NumaZone {  // zone of type "Node" named node-<0..63>, available per resource
+  int id = 0;
+  std::vector<std::pair<int, int64_t>> res;  // (resource id, available)
+  int64_t* find(int rid) {
+    for (auto& kv : res)
+      if (kv.first == rid) return &kv.second;
+    return nullptr;
+  }
+  const int64_t* find(int rid) const { return const_cast<NumaZone*>(this)->find(rid); }
+};
 struct NodeResourceTopology {
   ObjectMeta meta;
   std::vector<std::string> topology_policies;
   std::vector<NRTZone> zones;
+  std::vector<NumaZone> numa;  // precomputed createNUMANodeList, sorted by id
   static std::shared_ptr<NodeResourceTopology> from_json(const Json& obj);
 };
 using NRTPtr = std::shared_ptr<NodeResourceTopology>;
@@ -235,11 +254,29 @@ struct GpuNames {
   std::string partition_annotation = "amd.com/gpu-partitions";
   std::string partition_label = "amd.com/gpu.compute-partition";     // spx|dpx|qpx|cpx
   std::string topology_annotation = "amd.com/gpu-topology";          // JSON, per-GPU detail
-  int gpu_id() const;
-  int memory_id() const;
-  int xcd_id() const;
+  // Resource ids are interned once per name change (hot paths call these
+  // per node per pod).
+  int gpu_id() const {
+    if (!ids_ready_) refresh();
+    return gpu_rid_;
+  }
+  int memory_id() const {
+    if (!ids_ready_) refresh();
+    return mem_rid_;
+  }
+  int xcd_id() const {
+    if (!ids_ready_) refresh();
+    return xcd_rid_;
+  }
+  void invalidate() { ids_ready_ = false; }
+
+ private:
+  void refresh() const;
+  mutable int gpu_rid_ = -1, mem_rid_ = -1, xcd_rid_ = -1;
+  mutable bool ids_ready_ = false;
 };
 GpuNames& gpu_names();
+GpuDemand compute_gpu_demand(const Pod& p);
 int partitions_for_mode(const std::string& mode);  // spx=1 dpx=2 qpx=4 cpx=8 (0 unknown)
 
 }  // namespace xsched

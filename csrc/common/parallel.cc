@@ -37,10 +37,11 @@ void Parallelizer::worker_loop() {
     Job* job = nullptr;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || (job_ != nullptr && job_gen_ != seen); });
+      cv_.wait(lk, [&] { return stop_ || (job_ != nullptr && job_gen_ != seen && job_->seats > 0); });
       if (stop_) return;
       seen = job_gen_;
       job = job_;
+      --job->seats;
       job->active.fetch_add(1);
     }
     run_job(*job);
@@ -53,7 +54,11 @@ void Parallelizer::worker_loop() {
 
 void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop) {
   if (n <= 0) return;
-  if (n < inline_below_ || threads_.empty()) {
+  // Helpers only pay off when each gets >= inline_below_/2 items: a fork/join
+  // round costs a few microseconds of wake-ups, more than filtering dozens of
+  // nodes with the allocation-free plugins.
+  int helpers = std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1);
+  if (n < inline_below_ || helpers <= 0) {
     for (int i = 0; i < n; ++i) {
       if (stop && stop->load(std::memory_order_relaxed)) return;
       fn(i);
@@ -65,15 +70,19 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
   job.fn = &fn;
   job.stop = stop;
   job.n = n;
-  // chunkSizeFor: sqrt(n) capped so every worker gets work.
-  job.chunk = std::max(1, std::min(static_cast<int>(std::sqrt(static_cast<double>(n))), n / workers_ + 1));
+  job.seats = helpers;
+  // chunkSizeFor: sqrt(n), capped so every participant gets work.
+  job.chunk = std::max(1, std::min(static_cast<int>(std::sqrt(static_cast<double>(n))), n / (helpers + 1)));
   job.active.store(1);  // the caller
   {
     std::lock_guard<std::mutex> g(mu_);
     job_ = &job;
     ++job_gen_;
   }
-  cv_.notify_all();
+  if (helpers >= static_cast<int>(threads_.size()))
+    cv_.notify_all();
+  else
+    for (int i = 0; i < helpers; ++i) cv_.notify_one();
   run_job(job);
   std::unique_lock<std::mutex> lk(mu_);
   job_ = nullptr;  // no new worker can join after this point

@@ -20,7 +20,7 @@ namespace xsched {
 
 class Parallelizer {
  public:
-  explicit Parallelizer(int workers = 16, int inline_below = 64);
+  explicit Parallelizer(int workers = 16, int inline_below = 128);
   ~Parallelizer();
   Parallelizer(const Parallelizer&) = delete;
   Parallelizer& operator=(const Parallelizer&) = delete;
@@ -36,6 +36,7 @@ class Parallelizer {
     const std::atomic<bool>* stop = nullptr;
     int n = 0;
     int chunk = 1;
+    int seats = 0;  // helpers allowed to join (guarded by mu_)
     std::atomic<int> next{0};
     std::atomic<int> active{0};
   };

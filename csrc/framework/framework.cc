@@ -224,7 +224,8 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
     std::shared_ptr<NodeInfo> ni_out;
     if (i == 0) {
       std::vector<PodPtr> nominated;
-      if (handle_.nominator && ni.node) nominated = handle_.nominator->nominated_pods_for_node(ni.name());
+      if (handle_.nominator && ni.node && !handle_.nominator->empty())
+        nominated = handle_.nominator->nominated_pods_for_node(ni.name());
       for (const auto& np : nominated) {
         if (np->priority < p.priority || np->uid() == p.uid()) continue;
         if (!ni_out) {
@@ -303,7 +304,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
         failed.store(true);
         return;
       }
-      per[k][i] = NodeScore{total[i].name, sc};
+      per[k][i].score = sc;  // names live in `total` only (normalizers use scores)
     }
   }, &failed);
   if (failed.load()) return Status(Code::Error, err);

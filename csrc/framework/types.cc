@@ -115,7 +115,7 @@ bool GpuLedger::slot_free(int g, int p) const {
 
 int GpuLedger::free_gpus() const {
   int n = 0;
-  for (int g = 0; g < gpu_count; ++g) n += gpu_untouched(g) ? 1 : 0;
+  for (int g = 0; g < gpu_count; ++g) n += whole_gpu_free(g) ? 1 : 0;
   return n;
 }
 

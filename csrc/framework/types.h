@@ -115,8 +115,11 @@ struct GpuLedger {
   int64_t part_mem(int g) const { return parts[g] > 0 ? mem_per_gpu / parts[g] : 0; }
   int xcds_per_part(int g) const { return parts[g] > 0 ? 8 / parts[g] : 0; }
   bool gpu_untouched(int g) const;      // no owner and no memory use on any partition
+  // A whole-GPU claim needs an untouched GPU in SPX mode: on a partitioned
+  // GPU the container would see 2/4/8 separate devices, not one MI355X.
+  bool whole_gpu_free(int g) const { return parts[g] == 1 && gpu_untouched(g); }
   bool slot_free(int g, int p) const;   // exclusive-free and no memory use
-  int free_gpus() const;                // GPUScore (gpu_node.go:179-187)
+  int free_gpus() const;                // GPUScore (gpu_node.go:179-187): free whole (SPX) GPUs
   int64_t free_memory() const;          // MemScore (gpu_node.go:189-199)
   int free_xcds() const;
 };
@@ -130,6 +133,7 @@ struct NodeInfo {
   std::set<std::tuple<std::string, std::string, int32_t>> used_ports;  // (ip, proto, port)
   Res requested, nonzero_requested, allocatable;
   GpuLedger gpu;
+  NRTPtr nrt;  // this node's NodeResourceTopology (set by the cache from the informer)
   int64_t generation = 0;
   std::unordered_map<std::string, int> pg_count;  // "ns/pg" -> pods on this node
 
@@ -166,6 +170,9 @@ struct QueuedPodInfo {
   int attempts = 0;
   std::set<std::string> unschedulable_plugins;
   int64_t enqueue_seq = 0;
+  // QueueSort plugins may memoize an immutable sort key here (e.g.
+  // Coscheduling's PodGroup creation time); INT64_MIN = not cached.
+  mutable int64_t sort_key_cache = INT64_MIN;
 };
 using QueuedPodInfoPtr = std::shared_ptr<QueuedPodInfo>;
 

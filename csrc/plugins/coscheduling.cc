@@ -80,9 +80,16 @@ class Coscheduling : public Plugin {
   }
 
   // ---- QueueSort ----
+  // GetCreationTimestamp (core.go:255-265). A PodGroup's creationTimestamp
+  // never changes, so once found it is memoized on the queued pod (Less runs
+  // O(log n) times per heap operation, under the queue lock).
   MicroTime creation(const QueuedPodInfo& q) const {
+    if (q.sort_key_cache != INT64_MIN) return q.sort_key_cache;
     if (!q.pod->pod_group.empty())
-      if (auto pg = h_.informers->pod_group(q.pod->ns(), q.pod->pod_group)) return pg->meta.creation;
+      if (auto pg = h_.informers->pod_group(q.pod->ns(), q.pod->pod_group)) {
+        q.sort_key_cache = pg->meta.creation;
+        return q.sort_key_cache;
+      }
     return q.initial_attempt_wall;
   }
   bool less(const QueuedPodInfo& a, const QueuedPodInfo& b) const override {
@@ -158,9 +165,15 @@ class Coscheduling : public Plugin {
   }
 
   // ---- PostFilter (coscheduling.go:140-176) ----
-  std::pair<PostFilterResult, Status> post_filter(CycleState&, const Pod& p, const NodeStatusMap&) override {
+  std::pair<PostFilterResult, Status> post_filter(CycleState&, const Pod& p, const NodeStatusMap& m) override {
     auto pg = p.pod_group.empty() ? nullptr : h_.informers->pod_group(p.ns(), p.pod_group);
     if (!pg) return {PostFilterResult{}, Status::unschedulable("can not find pod group")};
+    // Deliberate deviation: when the cycle failed on this plugin's own
+    // PreFilter (siblings not created yet, or group already denied) there is
+    // no placement evidence, so the group is not (re-)denied — the reference
+    // would deny it and, for the "denied" case, keep refreshing the TTL.
+    if (!m.empty() && m.begin()->second.failed_plugin() == name())
+      return {PostFilterResult{}, Status(Code::Unschedulable)};
     std::string full = p.pg_full_name();
     int assigned = h_.cache->assigned_in_group(full);
     if (assigned >= pg->min_member) return {PostFilterResult{}, Status(Code::Unschedulable)};

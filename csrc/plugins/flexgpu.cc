@@ -36,41 +36,7 @@ namespace {
 
 constexpr const char* kFlexGPUStateKey = "FlexGPU/assignment";
 
-struct Demand {
-  enum Kind { None, Gpu, Xcd, Memory, Conflict } kind = None;
-  int64_t amount = 0;
-};
-
-Demand pod_demand(const Pod& p) {
-  const GpuNames& gn = gpu_names();
-  int gid = gn.gpu_id(), mid = gn.memory_id(), xid = gn.xcd_id();
-  int kinds = 0;
-  Demand d;
-  // Presence is per container limit (podResourceLimit sums limits).
-  bool has_g = false, has_m = false, has_x = false;
-  for (const auto& c : p.containers) {
-    has_g |= c.limits.has(gid);
-    has_m |= c.limits.has(mid);
-    has_x |= c.limits.has(xid);
-  }
-  kinds = int(has_g) + int(has_m) + int(has_x);
-  if (kinds == 0) return d;
-  if (kinds > 1) {
-    d.kind = Demand::Conflict;
-    return d;
-  }
-  if (has_g) {
-    d.kind = Demand::Gpu;
-    d.amount = p.limit_sum.get(gid);
-  } else if (has_x) {
-    d.kind = Demand::Xcd;
-    d.amount = p.limit_sum.get(xid);
-  } else {
-    d.kind = Demand::Memory;
-    d.amount = p.limit_sum.get(mid);
-  }
-  return d;
-}
+using Demand = GpuDemand;
 
 struct Placement {
   std::vector<int> gpus;
@@ -85,7 +51,7 @@ Placement place_whole(const GpuLedger& L, int64_t k) {
   if (k <= 0) k = 1;
   std::vector<int> free;
   for (int g = 0; g < L.gpu_count; ++g)
-    if (L.gpu_untouched(g)) free.push_back(g);
+    if (L.whole_gpu_free(g)) free.push_back(g);
   if (static_cast<int64_t>(free.size()) < k) return pl;
   std::map<int, std::vector<int>> by_numa;
   for (int g : free) by_numa[L.numa[g]].push_back(g);
@@ -104,12 +70,20 @@ Placement place_whole(const GpuLedger& L, int64_t k) {
   return pl;
 }
 
-// x XCDs from exclusive partitions of one GPU, best-fit GPU (fewest free
-// XCDs that still fits), lowest free partition indexes inside it.
-Placement place_xcd(const GpuLedger& L, int64_t x) {
+// x XCDs from exclusive partitions of one GPU. The GPU is chosen by
+// (wasted XCDs, free XCDs): a 2-XCD request on a CPX GPU wastes nothing, on
+// an SPX GPU it strands 6 XCDs, so partitioned GPUs win whenever they fit;
+// among equals the fullest GPU (best fit). Lowest free partitions inside it.
+int xcd_waste(const GpuLedger& L, int g, int64_t x) {
+  int xpp = L.xcds_per_part(g);
+  int need = static_cast<int>((x + xpp - 1) / xpp);
+  return static_cast<int>(need * xpp - x);
+}
+
+Placement place_xcd(const GpuLedger& L, int64_t x, int* waste_out = nullptr) {
   Placement pl;
   if (x <= 0) return pl;
-  int best_g = -1, best_free = 1 << 30;
+  int best_g = -1, best_free = 1 << 30, best_waste = 1 << 30;
   for (int g = 0; g < L.gpu_count; ++g) {
     if (L.monopoly[g] > 0) continue;
     int xpp = L.xcds_per_part(g);
@@ -119,11 +93,14 @@ Placement place_xcd(const GpuLedger& L, int64_t x) {
     for (int p = 0; p < L.parts[g]; ++p) free += L.slot_free(g, p) ? 1 : 0;
     if (free < need) continue;
     int free_x = free * xpp;
-    if (free_x < best_free) {
+    int waste = xcd_waste(L, g, x);
+    if (waste < best_waste || (waste == best_waste && free_x < best_free)) {
+      best_waste = waste;
       best_free = free_x;
       best_g = g;
     }
   }
+  if (waste_out) *waste_out = best_g < 0 ? 0 : best_waste;
   if (best_g < 0) return pl;
   int xpp = L.xcds_per_part(best_g);
   int need = static_cast<int>((x + xpp - 1) / xpp);
@@ -134,26 +111,32 @@ Placement place_xcd(const GpuLedger& L, int64_t x) {
 }
 
 // Memory slice on the partition with the least remaining memory after
-// placement (best fit, value semantics — fixes Appendix C1).
-Placement place_memory(const GpuLedger& L, int64_t m) {
+// placement (best fit, value semantics — fixes Appendix C1). A slice never
+// breaks an untouched SPX GPU while any other partition can take it: that GPU
+// is the only kind a whole-GPU (training-rank) pod can use.
+Placement place_memory(const GpuLedger& L, int64_t m, bool* breaks_whole = nullptr) {
   Placement pl;
   int bg = -1, bp = -1;
   int64_t best_remain = 0;
+  bool best_breaks = true;
   for (int g = 0; g < L.gpu_count; ++g) {
     if (L.monopoly[g] > 0) continue;
     int64_t cap = L.part_mem(g);
+    bool breaks = L.whole_gpu_free(g);
     for (int p = 0; p < L.parts[g]; ++p) {
       const auto& s = L.slots[L.offset[g] + p];
       if (s.exclusive > 0) continue;
       int64_t remain = cap - s.used_mem - m;
       if (remain < 0) continue;
-      if (bg < 0 || remain < best_remain) {
+      if (bg < 0 || (!breaks && best_breaks) || (breaks == best_breaks && remain < best_remain)) {
         bg = g;
         bp = p;
         best_remain = remain;
+        best_breaks = breaks;
       }
     }
   }
+  if (breaks_whole) *breaks_whole = bg >= 0 && best_breaks;
   if (bg < 0) return pl;
   pl.gpus.push_back(bg);
   pl.parts.emplace_back(bg, bp);
@@ -195,10 +178,11 @@ class FlexGPU : public Plugin {
     if (args["xcdResourceName"].is_string()) gn.xcd = args["xcdResourceName"].as_string();
     if (args["indexAnnotationKey"].is_string()) gn.index_annotation = args["indexAnnotationKey"].as_string();
     if (args["partitionAnnotationKey"].is_string()) gn.partition_annotation = args["partitionAnnotationKey"].as_string();
+    gn.invalidate();
   }
 
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
-    Demand d = pod_demand(p);
+    const Demand& d = p.gpu_demand;
     if (d.kind == Demand::None) return {};
     if (d.kind == Demand::Conflict) return Status::unresolvable("pod conflict resources");
     const GpuNames& gn = gpu_names();
@@ -208,17 +192,63 @@ class FlexGPU : public Plugin {
     // Node-level sum check (flex_gpu.go:82-98).
     if (ni.requested.get(kid) + d.amount > ni.allocatable.get(kid))
       return Status::unschedulable("insufficient resource " + ResourceRegistry::get().name(kid));
-    if (!place(ni.gpu, d).ok())
-      return Status::unschedulable("no fit indexes resource " + ResourceRegistry::get().name(kid));
+    if (!fits(ni.gpu, d)) return Status::unschedulable("no fit indexes resource " + ResourceRegistry::get().name(kid));
     return {};
   }
 
+  // Allocation-free feasibility check (Filter runs per node per pod; the
+  // concrete placement is only materialized in Reserve).
+  static bool fits(const GpuLedger& L, const Demand& d) {
+    switch (d.kind) {
+      case Demand::Gpu: {
+        int64_t need = d.amount > 0 ? d.amount : 1, free = 0;
+        for (int g = 0; g < L.gpu_count && free < need; ++g) free += L.whole_gpu_free(g) ? 1 : 0;
+        return free >= need;
+      }
+      case Demand::Xcd: {
+        if (d.amount <= 0) return false;
+        for (int g = 0; g < L.gpu_count; ++g) {
+          if (L.monopoly[g] > 0) continue;
+          int xpp = L.xcds_per_part(g);
+          if (xpp <= 0) continue;
+          int need = static_cast<int>((d.amount + xpp - 1) / xpp), free = 0;
+          for (int p = 0; p < L.parts[g] && free < need; ++p) free += L.slot_free(g, p) ? 1 : 0;
+          if (free >= need) return true;
+        }
+        return false;
+      }
+      case Demand::Memory: {
+        for (int g = 0; g < L.gpu_count; ++g) {
+          if (L.monopoly[g] > 0) continue;
+          int64_t cap = L.part_mem(g);
+          for (int p = 0; p < L.parts[g]; ++p) {
+            const auto& s = L.slots[L.offset[g] + p];
+            if (s.exclusive == 0 && cap - s.used_mem >= d.amount) return true;
+          }
+        }
+        return false;
+      }
+      default: return false;
+    }
+  }
+
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
-    Demand d = pod_demand(p);
+    const Demand& d = p.gpu_demand;
     switch (d.kind) {
       case Demand::Gpu: return {ni.gpu.free_gpus(), {}};
-      case Demand::Xcd: return {ni.gpu.free_xcds(), {}};
-      case Demand::Memory: return {ni.gpu.free_memory(), {}};
+      case Demand::Xcd: {
+        // Stranded XCDs dominate: a node that can host the slice without
+        // waste always outranks one that would burn a whole SPX GPU on it.
+        int waste = 0;
+        place_xcd(ni.gpu, d.amount, &waste);
+        return {ni.gpu.free_xcds() + 64 * waste, {}};
+      }
+      case Demand::Memory: {
+        // Breaking a whole SPX GPU for a slice costs more than any packing gain.
+        bool breaks = false;
+        place_memory(ni.gpu, d.amount, &breaks);
+        return {ni.gpu.free_memory() + (breaks ? 8 * ni.gpu.mem_per_gpu : 0), {}};
+      }
       default: return {0, {}};
     }
   }
@@ -229,7 +259,7 @@ class FlexGPU : public Plugin {
   }
 
   Status reserve(CycleState& s, const PodPtr& p, const std::string& node) override {
-    Demand d = pod_demand(*p);
+    const Demand& d = p->gpu_demand;
     if (d.kind == Demand::None) return {};
     if (d.kind == Demand::Conflict) return Status::unresolvable("pod conflict resources");
     NodeInfoPtr ni = h_.snapshot ? h_.snapshot->get(node) : nullptr;

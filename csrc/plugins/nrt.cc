@@ -1,0 +1,380 @@
+// NodeResourceTopologyMatch with MI355X xGMI-aware gang placement.
+//
+// Reference: pkg/noderesourcetopology/{plugin.go,filter.go,score.go,
+// least_allocated.go,most_allocated.go,balanced_allocation.go,
+// pluginhelpers.go}:
+//  * zones of type "Node" named node-<id> (0..63) form the NUMA list;
+//  * Filter skips BestEffort pods and nodes without an NRT, and runs the
+//    SingleNUMANode{Container,Pod}Level handlers: per resource a bitmask of
+//    NUMA nodes that fit, AND-ed; non-Guaranteed pods always fit cpu/memory/
+//    hugepages; non-native resources without NUMA affinity pass; container
+//    scope subtracts the chosen (lowest) NUMA before the next container;
+//  * Score: non-Guaranteed pods get 100; otherwise the minimum non-zero
+//    per-NUMA strategy score (Least/Most/Balanced), mean over containers in
+//    container scope.
+//
+// MI355X additions:
+//  * GPU resources of a zone (amd.com/gpu, -xcd, -memory) are capped by the
+//    scheduler's own GPU ledger for that socket, so zone availability is live
+//    between exporter refreshes (the reference trusts the CR only);
+//  * scoringStrategy XGMIGangAffinity: for a pod of a PodGroup, prefer the
+//    node where the remaining ranks of the gang fit together (all RCCL hops on
+//    the 7-link-per-GPU xGMI mesh of one 8x MI355X node), tightest fit first,
+//    nodes already hosting siblings highest. Inside a node the xGMI mesh is
+//    uniform, so there is no hop distance to optimise — only co-location.
+//  * The sparse-NUMA-id index panic (Appendix C7) cannot happen: no array is
+//    indexed by NUMA id.
+#include <algorithm>
+#include <cmath>
+#include <map>
+
+#include "framework/plugin.h"
+#include "scheduler/cache.h"
+#include "scheduler/informers.h"
+
+namespace xsched {
+namespace {
+
+using NumaNode = NumaZone;
+
+// Per-cycle gang facts for XGMIGangAffinity, computed once in PreScore.
+struct GangCtx : StateData {
+  bool gang = false;
+  std::string full;         // ns/pg
+  int64_t remaining = 0;    // members still to place (>= 1)
+  enum { kWhole, kXcd } kind = kWhole;
+  int64_t amount = 0;       // per member: GPUs or XCDs
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<GangCtx>(*this); }
+};
+constexpr const char* kGangKey = "NodeResourceTopologyMatch/gang";
+
+enum class Strategy { Least, Most, Balanced, XGMI };
+
+int64_t value_units(int id, int64_t v) {  // Quantity.Value() semantics (cpu rounds up to cores)
+  if (id == kCPU) return v >= 0 ? (v + 999) / 1000 : v / 1000;
+  return v;
+}
+
+class TopologyMatch : public Plugin {
+ public:
+  TopologyMatch(const Json& args, Handle& h) : Plugin("NodeResourceTopologyMatch", kFilter | kPreScore | kScore), h_(h) {
+    const Json& ss = args["scoringStrategy"];
+    std::string t = ss["type"].str_or("LeastAllocated");
+    if (t == "MostAllocated") strategy_ = Strategy::Most;
+    else if (t == "BalancedAllocation") strategy_ = Strategy::Balanced;
+    else if (t == "XGMIGangAffinity") strategy_ = Strategy::XGMI;
+    else if (t == "LeastAllocated") strategy_ = Strategy::Least;
+    else throw std::runtime_error("illegal scoring strategy found");
+    for (const auto& r : ss["resources"].items()) weights_[res_id(r["name"].as_string())] = r["weight"].as_int(1);
+  }
+
+  int64_t weight(int id) const {
+    auto it = weights_.find(id);
+    return it == weights_.end() || it->second < 1 ? 1 : it->second;
+  }
+
+  std::vector<NumaNode> numa_list(const NodeResourceTopology& nrt, const NodeInfo& ni) const {
+    std::vector<NumaNode> out = nrt.numa;  // precomputed at parse time
+    const GpuNames& gn = gpu_names();
+    int gid = gn.gpu_id(), xid = gn.xcd_id(), mid = gn.memory_id();
+    const GpuLedger& L = ni.gpu;
+    for (auto& n : out) {
+      // Live GPU availability from the ledger for GPUs on this socket.
+      bool any_numa = false;
+      int free_g = 0, free_x = 0;
+      int64_t free_m = 0;
+      for (int g = 0; g < L.gpu_count; ++g) {
+        if (L.numa[g] != n.id) continue;
+        any_numa = true;
+        if (L.whole_gpu_free(g)) ++free_g;
+        if (L.monopoly[g] > 0) continue;
+        for (int p = 0; p < L.parts[g]; ++p) {
+          if (L.slot_free(g, p)) free_x += L.xcds_per_part(g);
+          const auto& s = L.slots[L.offset[g] + p];
+          if (s.exclusive == 0) free_m += L.part_mem(g) - s.used_mem;
+        }
+      }
+      if (!any_numa) continue;
+      if (int64_t* v = n.find(gid)) *v = std::min<int64_t>(*v, free_g);
+      if (int64_t* v = n.find(xid)) *v = std::min<int64_t>(*v, free_x);
+      if (int64_t* v = n.find(mid)) *v = std::min<int64_t>(*v, free_m);
+    }
+    return out;
+  }
+
+  static bool numa_suitable(QoS qos, int id, int64_t want, int64_t have) {
+    if (qos != QoS::Guaranteed) {
+      if (id == kCPU || id == kMemory || ResourceRegistry::get().is_hugepages(id)) return true;
+    }
+    return have >= want;
+  }
+
+  // Returns the lowest fitting NUMA id or -1.
+  static int any_numa_fits(const std::vector<NumaNode>& nodes, const Res& req, QoS qos, const NodeInfo& ni) {
+    uint64_t mask = ~uint64_t{0};
+    for (uint64_t m = req.mask; m; m &= m - 1) {
+      int id = __builtin_ctzll(m);
+      int64_t want = req.v[id];
+      if (want == 0) continue;
+      if (!ni.allocatable.has(id)) return -1;
+      bool affinity = false;
+      uint64_t rmask = 0;
+      for (const auto& n : nodes) {
+        const int64_t* have = n.find(id);
+        if (!have) continue;
+        affinity = true;
+        if (numa_suitable(qos, id, want, *have)) rmask |= uint64_t{1} << n.id;
+      }
+      if (!affinity && !ResourceRegistry::get().is_native(id)) continue;
+      mask &= rmask;
+      if (!mask) return -1;
+    }
+    // A mask with no NUMA constraint at all still has to name a zone.
+    for (const auto& n : nodes)
+      if (mask & (uint64_t{1} << n.id)) return n.id;
+    return nodes.empty() ? -1 : -1;
+  }
+
+  // Live per-zone GPU availability, computed without allocation.
+  struct LiveGpu {
+    int64_t g[64], x[64], m[64];
+    bool any[64];
+  };
+  static void live_gpu(const NodeInfo& ni, const NodeResourceTopology& nrt, LiveGpu& out) {
+    const GpuLedger& L = ni.gpu;
+    for (size_t z = 0; z < nrt.numa.size(); ++z) {
+      int id = nrt.numa[z].id;
+      out.g[z] = out.x[z] = out.m[z] = 0;
+      out.any[z] = false;
+      for (int g = 0; g < L.gpu_count; ++g) {
+        if (L.numa[g] != id) continue;
+        out.any[z] = true;
+        if (L.whole_gpu_free(g)) ++out.g[z];
+        if (L.monopoly[g] > 0) continue;
+        for (int p = 0; p < L.parts[g]; ++p) {
+          if (L.slot_free(g, p)) out.x[z] += L.xcds_per_part(g);
+          const auto& s = L.slots[L.offset[g] + p];
+          if (s.exclusive == 0) out.m[z] += L.part_mem(g) - s.used_mem;
+        }
+      }
+    }
+  }
+
+  // Allocation-free resourcesAvailableInAnyNUMANodes for one request vector.
+  static bool fits_fast(const NodeResourceTopology& nrt, const NodeInfo& ni, const Res& req, QoS qos) {
+    if (nrt.numa.size() > 64) return true;
+    const GpuNames& gn = gpu_names();
+    int gid = gn.gpu_id(), xid = gn.xcd_id(), mid = gn.memory_id();
+    LiveGpu live;
+    bool live_ready = false;
+    uint64_t mask = ~uint64_t{0};
+    for (uint64_t m = req.mask; m; m &= m - 1) {
+      int id = __builtin_ctzll(m);
+      int64_t want = req.v[id];
+      if (want == 0) continue;
+      if (!ni.allocatable.has(id)) return false;
+      bool affinity = false;
+      uint64_t rmask = 0;
+      for (size_t z = 0; z < nrt.numa.size(); ++z) {
+        const int64_t* have = nrt.numa[z].find(id);
+        if (!have) continue;
+        affinity = true;
+        int64_t h = *have;
+        if (id == gid || id == xid || id == mid) {
+          if (!live_ready) {
+            live_gpu(ni, nrt, live);
+            live_ready = true;
+          }
+          if (live.any[z]) h = std::min(h, id == gid ? live.g[z] : id == xid ? live.x[z] : live.m[z]);
+        }
+        if (numa_suitable(qos, id, want, h)) rmask |= uint64_t{1} << nrt.numa[z].id;
+      }
+      if (!affinity && !ResourceRegistry::get().is_native(id)) continue;
+      mask &= rmask;
+      if (!mask) return false;
+    }
+    for (const auto& z : nrt.numa)
+      if (mask & (uint64_t{1} << z.id)) return true;
+    return false;
+  }
+
+  Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
+    if (!ni.node) return Status::error("node not found");
+    if (p.qos == QoS::BestEffort) return {};
+    const NodeResourceTopology* nrt = ni.nrt.get();
+    if (!nrt) return {};
+    for (const auto& pol : nrt->topology_policies) {
+      bool container_scope = pol == "SingleNUMANodeContainerLevel";
+      if (container_scope && p.init_containers.empty() && p.containers.size() == 1) {
+        // One container: container scope == pod scope, no subtraction needed.
+        if (!fits_fast(*nrt, ni, p.containers[0].requests, p.qos))
+          return Status::unschedulable("cannot align container: " + p.containers[0].name);
+        continue;
+      }
+      if (pol == "SingleNUMANodePodLevel") {
+        if (!fits_fast(*nrt, ni, p.request, p.qos)) return Status::unschedulable("cannot align pod: " + p.name());
+        continue;
+      }
+      if (container_scope) {
+        auto nodes = numa_list(*nrt, ni);
+        for (const auto& c : p.init_containers)
+          if (any_numa_fits(nodes, c.requests, p.qos, ni) < 0)
+            return Status::unschedulable("cannot align init container: " + c.name);
+        for (const auto& c : p.containers) {
+          int id = any_numa_fits(nodes, c.requests, p.qos, ni);
+          if (id < 0) return Status::unschedulable("cannot align container: " + c.name);
+          for (auto& n : nodes)
+            if (n.id == id)
+              for (uint64_t m = c.requests.mask; m; m &= m - 1) {
+                int r = __builtin_ctzll(m);
+                if (int64_t* v = n.find(r)) *v -= c.requests.v[r];
+              }
+        }
+      }
+    }
+    return {};
+  }
+
+  int64_t strategy_score(const Res& req, const NumaNode& n) const {
+    if (strategy_ == Strategy::Balanced) {
+      double fr[kMaxRes];
+      int k = 0;
+      for (uint64_t m = req.mask; m; m &= m - 1) {
+        int id = __builtin_ctzll(m);
+        const int64_t* have = n.find(id);
+        int64_t cap = have ? value_units(id, *have) : 0;
+        double f = cap == 0 ? 1.0 : static_cast<double>(value_units(id, req.v[id])) / static_cast<double>(cap);
+        if (f > 1) return 0;
+        fr[k++] = f;
+      }
+      if (k < 2) return kMaxNodeScore;  // gonum Variance of <2 samples is 0
+      double mean = 0;
+      for (int i = 0; i < k; ++i) mean += fr[i];
+      mean /= k;
+      double var = 0;
+      for (int i = 0; i < k; ++i) var += (fr[i] - mean) * (fr[i] - mean);
+      var /= (k - 1);  // stat.Variance is the unbiased estimator
+      return static_cast<int64_t>((1 - var) * kMaxNodeScore);
+    }
+    int64_t num = 0, wsum = 0;
+    for (uint64_t m = req.mask; m; m &= m - 1) {
+      int id = __builtin_ctzll(m);
+      const int64_t* have = n.find(id);
+      int64_t cap = have ? value_units(id, *have) : 0;
+      int64_t want = value_units(id, req.v[id]);
+      int64_t s = 0;
+      if (cap != 0 && want <= cap) s = strategy_ == Strategy::Most ? want * kMaxNodeScore / cap : (cap - want) * kMaxNodeScore / cap;
+      num += s * weight(id);
+      wsum += weight(id);
+    }
+    return wsum ? num / wsum : 0;
+  }
+
+  int64_t min_numa_score(const Res& req, const std::vector<NumaNode>& nodes) const {
+    int64_t mn = 0;
+    for (const auto& n : nodes) {
+      int64_t s = strategy_score(req, n);
+      if (mn == 0 || (s != 0 && s < mn)) mn = s;
+    }
+    return mn;
+  }
+
+  // PreScore: gang facts shared by every node's Score (one PodGroup lookup
+  // and one assigned-count read per cycle instead of per node).
+  Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>&) override {
+    if (strategy_ != Strategy::XGMI) return {};
+    auto ctx = std::make_shared<GangCtx>();
+    if (!p.pod_group.empty()) {
+      auto pg = h_.informers->pod_group(p.ns(), p.pod_group);
+      const GpuDemand& d = p.gpu_demand;
+      if (pg && pg->min_member > 1 && d.amount > 0 && (d.kind == GpuDemand::Gpu || d.kind == GpuDemand::Xcd)) {
+        ctx->gang = true;
+        ctx->full = p.pg_full_name();
+        ctx->remaining = std::max<int64_t>(1, pg->min_member - h_.cache->assigned_in_group(ctx->full));
+        ctx->kind = d.kind == GpuDemand::Gpu ? GangCtx::kWhole : GangCtx::kXcd;
+        ctx->amount = d.amount;
+      }
+    }
+    s.write(kGangKey, ctx);
+    return {};
+  }
+
+  // Gang co-location score in [0, 100] (XGMIGangAffinity).
+  static int64_t gang_score(const GangCtx& c, const NodeInfo& ni) {
+    if (!c.gang) return 50;
+    const GpuLedger& L = ni.gpu;
+    int64_t per = 0, free = 0;
+    if (c.kind == GangCtx::kWhole) {
+      per = c.amount;
+      free = L.free_gpus();
+    } else {
+      // A member consumes whole partitions: on SPX GPUs a 2-XCD rank burns 8.
+      for (int g = 0; g < L.gpu_count; ++g) {
+        if (L.monopoly[g] > 0 || L.xcds_per_part(g) <= 0) continue;
+        int64_t xpp = L.xcds_per_part(g);
+        int64_t use = (c.amount + xpp - 1) / xpp * xpp;
+        if (per == 0 || use < per) per = use;
+      }
+      if (per == 0) return 0;
+      free = L.free_xcds();
+    }
+    if (free <= 0) return 0;
+    int64_t remaining = c.remaining * per;
+    auto it = ni.pg_count.find(c.full);
+    bool co_located = it != ni.pg_count.end() && it->second > 0;
+    bool fits_all = remaining <= free;
+    if (fits_all && co_located) return 100;
+    if (fits_all) return 60 + 30 * remaining / free;  // tightest whole-gang fit first
+    if (co_located) return 50;
+    return 40 * std::min(free, remaining) / remaining;  // most of the gang on one node
+  }
+
+  std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) override {
+    if (strategy_ == Strategy::XGMI) {
+      if (auto* c = s.read_as<GangCtx>(kGangKey)) return {gang_score(*c, ni), {}};
+      // PreScore not enabled for this profile: derive the context per node.
+      CycleState local;
+      std::vector<NodeInfoPtr> none;
+      pre_score(local, p, none);
+      return {gang_score(*local.read_as<GangCtx>(kGangKey), ni), {}};
+    }
+    if (p.qos != QoS::Guaranteed) return {kMaxNodeScore, {}};
+    NRTPtr nrt = ni.nrt;
+    if (!nrt) return {0, {}};
+    for (const auto& pol : nrt->topology_policies) {
+      if (pol != "SingleNUMANodePodLevel" && pol != "SingleNUMANodeContainerLevel") continue;
+      auto nodes = numa_list(*nrt, ni);
+      if (pol == "SingleNUMANodePodLevel") return {min_numa_score(p.request, nodes), {}};
+      double sum = 0;
+      size_t n = 0;
+      for (const auto& c : p.init_containers) {
+        sum += static_cast<double>(min_numa_score(c.requests, nodes));
+        ++n;
+      }
+      for (const auto& c : p.containers) {
+        sum += static_cast<double>(min_numa_score(c.requests, nodes));
+        ++n;
+      }
+      return {n ? static_cast<int64_t>(sum / static_cast<double>(n)) : 0, {}};
+    }
+    return {0, {}};
+  }
+
+  std::vector<ClusterEvent> events_to_register() const override {
+    return {{"Pod", kDelete, ""}, {"Node", kAdd | kUpdateNodeAllocatable, ""}, {"NodeResourceTopology", kAdd | kUpdate, ""}};
+  }
+
+ private:
+  Handle& h_;
+  Strategy strategy_ = Strategy::Least;
+  std::map<int, int64_t> weights_;
+};
+
+PluginRegistrar reg("NodeResourceTopologyMatch",
+                    [](const Json& a, Handle& h) { return std::make_shared<TopologyMatch>(a, h); });
+
+}  // namespace
+
+void link_nrt_plugin() {}
+
+}  // namespace xsched

@@ -3,7 +3,6 @@ namespace xsched {
 void link_preemption_plugins() {}
 void link_capacity_plugin() {}
 void link_noderesources_plugin() {}
-void link_nrt_plugin() {}
 void link_trimaran_plugins() {}
 void link_sample_plugins() {}
 }  // namespace xsched

@@ -196,6 +196,7 @@ PYBIND11_MODULE(_xsched, m) {
     if (d.contains("xcd")) g.xcd = d["xcd"].cast<std::string>();
     if (d.contains("index_annotation")) g.index_annotation = d["index_annotation"].cast<std::string>();
     if (d.contains("partition_annotation")) g.partition_annotation = d["partition_annotation"].cast<std::string>();
+    g.invalidate();
   });
 
   // ---- clock ----

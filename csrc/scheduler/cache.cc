@@ -65,6 +65,18 @@ void SchedulerCache::remove_node(const std::string& name) {
   dirty_.insert(name);
 }
 
+void SchedulerCache::set_nrt(const std::string& node, const NRTPtr& nrt) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = nodes_.find(node);
+  if (it == nodes_.end()) {
+    if (!nrt) return;
+    info_for(node);  // ghost until the Node arrives; keeps the NRT
+    it = nodes_.find(node);
+  }
+  it->second->nrt = nrt;
+  mark_dirty(node);
+}
+
 void SchedulerCache::add_pod_locked(const PodPtr& p) {
   auto& ni = info_for(p->node_name);
   ni->add_pod(p);

@@ -34,6 +34,7 @@ class SchedulerCache {
   void add_node(const NodePtr& n);
   void update_node(const NodePtr& n);
   void remove_node(const std::string& name);
+  void set_nrt(const std::string& node, const NRTPtr& nrt);  // nullptr clears
 
   void add_pod(const PodPtr& p);  // assigned pod observed by the informer
   void update_pod(const PodPtr& old_pod, const PodPtr& new_pod);

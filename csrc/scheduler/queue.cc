@@ -89,9 +89,11 @@ void Nominator::add(const PodPtr& p, const std::string& node) {
     if (vec.empty()) by_node_.erase(it->second);
     node_of_.erase(it);
   }
-  if (n.empty()) return;
-  node_of_[p->uid()] = n;
-  by_node_[n].push_back(p);
+  if (!n.empty()) {
+    node_of_[p->uid()] = n;
+    by_node_[n].push_back(p);
+  }
+  count_.store(node_of_.size(), std::memory_order_relaxed);
 }
 
 void Nominator::remove(const Pod& p) {
@@ -102,6 +104,7 @@ void Nominator::remove(const Pod& p) {
   vec.erase(std::remove_if(vec.begin(), vec.end(), [&](const PodPtr& x) { return x->uid() == p.uid(); }), vec.end());
   if (vec.empty()) by_node_.erase(it->second);
   node_of_.erase(it);
+  count_.store(node_of_.size(), std::memory_order_relaxed);
 }
 
 void Nominator::update(const PodPtr& old_p, const PodPtr& new_p) {

@@ -7,6 +7,7 @@
 // clusterEventMap filter from plugins' EventsToRegister).
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -56,8 +57,10 @@ class Nominator {
   std::vector<PodPtr> nominated_pods_for_node(const std::string& node) const;
   std::string nominated_node(const std::string& uid) const;
   size_t size() const;
+  bool empty() const { return count_.load(std::memory_order_relaxed) == 0; }  // lock-free fast path
 
  private:
+  std::atomic<size_t> count_{0};
   mutable std::mutex mu_;
   std::unordered_map<std::string, std::vector<PodPtr>> by_node_;
   std::unordered_map<std::string, std::string> node_of_;

@@ -272,14 +272,28 @@ void Scheduler::informer_loop() {
   while (running_.load()) {
     auto evs = watcher_->next(50, 8192);
     if (evs.empty()) continue;
-    // Pass 1: listers first, so a PreFilter racing this batch sees every
-    // sibling of a PodGroup created together (Coscheduling counts them).
-    for (const auto& ev : evs) {
-      if (ev.kind != "pods") continue;
-      if (ev.type == EventType::Deleted) continue;
-      informers_->upsert_pod(Pod::from_json(*ev.obj));
+    // Pass 1: parse every pod once and publish it to the listers first, so a
+    // PreFilter racing this batch sees every sibling of a PodGroup created
+    // together (Coscheduling counts them). Pass 2 drives cache and queue.
+    std::vector<PodPtr> parsed(evs.size());
+    std::vector<PodPtr> prev(evs.size());
+    for (size_t i = 0; i < evs.size(); ++i) {
+      const auto& ev = evs[i];
+      if (ev.kind != "pods" || ev.type == EventType::Deleted) continue;
+      try {
+        parsed[i] = Pod::from_json(*ev.obj);
+      } catch (const std::exception&) {
+        continue;
+      }
+      prev[i] = informers_->pod(parsed[i]->ns(), parsed[i]->name());
+      informers_->upsert_pod(parsed[i]);
     }
-    for (const auto& ev : evs) handle_event(ev);
+    for (size_t i = 0; i < evs.size(); ++i) {
+      if (parsed[i])
+        handle_parsed_pod_event(evs[i], parsed[i], prev[i]);
+      else
+        handle_event(evs[i]);
+    }
   }
 }
 
@@ -312,6 +326,7 @@ void Scheduler::handle_event(const WatchEvent& ev) {
       } else if (ev.kind == "noderesourcetopologies") {
         auto n = NodeResourceTopology::from_json(o);
         if (del) informers_->delete_nrt(n->meta.name); else informers_->upsert_nrt(n);
+        cache_->set_nrt(n->meta.name, del ? nullptr : n);
       } else if (ev.kind == "poddisruptionbudgets") {
         auto p = PodDisruptionBudget::from_json(o);
         if (del) informers_->delete_pdb(p->meta.key()); else informers_->upsert_pdb(p);
@@ -353,8 +368,21 @@ void Scheduler::handle_pod_event(const WatchEvent& ev) {
   }
   auto np = Pod::from_json(*ev.obj);
   PodPtr old = informers_->pod(np->ns(), np->name());
-  if (old && old->uid() != np->uid()) old = nullptr;  // recreated with same name
   informers_->upsert_pod(np);
+  apply_pod_update(ev, np, old);
+}
+
+void Scheduler::handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, PodPtr old) {
+  try {
+    for (auto& fw : frameworks_) fw->dispatch_object_event("pods", static_cast<int>(ev.type), ev.obj, ev.old);
+    apply_pod_update(ev, np, std::move(old));
+  } catch (const std::exception&) {
+    metrics_->inc("xsched_informer_errors_total", "kind=\"pods\"");
+  }
+}
+
+void Scheduler::apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr old) {
+  if (old && old->uid() != np->uid()) old = nullptr;  // recreated with same name
   bool assigned = !np->node_name.empty();
   if (ev.type == EventType::Added || !old) {
     if (assigned) {
@@ -363,6 +391,15 @@ void Scheduler::handle_pod_event(const WatchEvent& ev) {
     } else if (responsible_for(*np) && !np->terminating()) {
       queue_->add(np);
       note_gang_enqueue(*np, clock_->now_us());
+      // A new member may complete its PodGroup: re-activate siblings parked
+      // in unschedulableQ/backoffQ (targeted form of the Pod/Add cluster
+      // event Coscheduling registers; O(group size), not O(queue)).
+      if (!np->pod_group.empty()) {
+        std::map<std::string, PodPtr> sib;
+        for (const auto& q : informers_->pods_in_group(np->ns(), np->pod_group))
+          if (q->uid() != np->uid() && q->node_name.empty()) sib[q->key()] = q;
+        if (!sib.empty()) queue_->activate(sib);
+      }
     }
     return;
   }
@@ -623,10 +660,15 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     std::lock_guard<std::mutex> g(stats_mu_);
     ++stats_.attempts;
   }
+  int64_t snap_end = clock_->now_us();
+  if (tracer_.enabled()) tracer_.record(TraceEvent{"snapshot", pod->key(), "", cycle_start, snap_end - cycle_start, 0});
 
   Diagnosis diag;
   std::vector<NodeInfoPtr> feasible;
   Status st = find_nodes_that_fit(*fw, *state, *pod, diag, feasible);
+  if (tracer_.enabled())
+    tracer_.record(TraceEvent{"filter", pod->key(), std::to_string(feasible.size()), snap_end,
+                              clock_->now_us() - snap_end, 0});
   std::string host;
   if (st.is_success()) {
     if (feasible.size() == 1) {

@@ -142,6 +142,8 @@ class Scheduler {
   void informer_loop();
   void handle_event(const WatchEvent& ev);
   void handle_pod_event(const WatchEvent& ev);
+  void handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, PodPtr old);
+  void apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr old);
   void handle_node_event(const WatchEvent& ev);
   void scheduling_loop();
   void schedule_cycle(const QueuedPodInfoPtr& qpi);

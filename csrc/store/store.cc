@@ -27,6 +27,14 @@ void Watcher::push(const WatchEvent& ev) {
   cv_.notify_one();
 }
 
+void Watcher::push_batch(std::vector<WatchEvent> evs) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& e : evs) q_.push_back(std::move(e));
+  }
+  cv_.notify_one();
+}
+
 std::vector<WatchEvent> Watcher::next(int timeout_ms, size_t max) {
   std::vector<WatchEvent> out;
   std::unique_lock<std::mutex> lk(mu_);
@@ -101,10 +109,14 @@ void ObjectStore::clear_faults() {
 
 void ObjectStore::emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv) {
   WatchEvent ev{t, kind, obj, old, rv};
-  const Json& md = (*obj)["metadata"];
-  const std::string& ns = md["namespace"].as_string();
-  for (auto& w : watchers_)
-    if (!w->stopped() && w->wants(kind, ns)) w->push(ev);
+  if (batch_) {
+    batch_->push_back(ev);
+  } else {
+    const Json& md = (*obj)["metadata"];
+    const std::string& ns = md["namespace"].as_string();
+    for (auto& w : watchers_)
+      if (!w->stopped() && w->wants(kind, ns)) w->push(ev);
+  }
   history_.push_back(std::move(ev));
   if (history_.size() > history_cap_) {
     compacted_rv_ = history_.front().rv;
@@ -163,8 +175,33 @@ std::vector<JsonPtr> ObjectStore::create_many(const std::string& kind, std::vect
   std::vector<JsonPtr> out;
   out.reserve(objs.size());
   std::lock_guard<std::mutex> g(mu_);
-  for (auto& o : objs) out.push_back(create_locked(kind, std::move(o)));
+  std::vector<WatchEvent> batch;
+  batch_ = &batch;
+  try {
+    for (auto& o : objs) out.push_back(create_locked(kind, std::move(o)));
+  } catch (...) {
+    batch_ = nullptr;
+    flush_batch_locked(batch);
+    throw;
+  }
+  batch_ = nullptr;
+  flush_batch_locked(batch);
   return out;
+}
+
+void ObjectStore::flush_batch_locked(std::vector<WatchEvent>& batch) {
+  // One hand-off (one lock + one wake-up) per watcher for the whole batch, so
+  // an informer sees a bulk create atomically (all PodGroup siblings at once).
+  for (auto& w : watchers_) {
+    if (w->stopped()) continue;
+    std::vector<WatchEvent> mine;
+    mine.reserve(batch.size());
+    for (const auto& ev : batch) {
+      const std::string& ns = (*ev.obj)["metadata"]["namespace"].as_string();
+      if (w->wants(ev.kind, ns)) mine.push_back(ev);
+    }
+    if (!mine.empty()) w->push_batch(std::move(mine));
+  }
 }
 
 JsonPtr ObjectStore::get(const std::string& kind, const std::string& ns, const std::string& name) const {
@@ -282,6 +319,16 @@ size_t ObjectStore::delete_all(const std::string& kind, const std::string& ns) {
   auto kit = kinds_.find(kind);
   if (kit == kinds_.end()) return 0;
   size_t n = 0;
+  std::vector<WatchEvent> batch;
+  batch_ = &batch;
+  struct Flush {
+    ObjectStore* s;
+    std::vector<WatchEvent>* b;
+    ~Flush() {
+      s->batch_ = nullptr;
+      s->flush_batch_locked(*b);
+    }
+  } flush{this, &batch};
   for (auto it = kit->second.begin(); it != kit->second.end();) {
     if (!ns.empty() && (*it->second.obj)["metadata"]["namespace"].as_string() != ns) {
       ++it;

@@ -70,6 +70,7 @@ class Watcher {
     return (kinds_.empty() || kinds_.count(kind)) && (ns_.empty() || ns.empty() || ns == ns_);
   }
   void push(const WatchEvent& ev);
+  void push_batch(std::vector<WatchEvent> evs);
 
  private:
   std::set<std::string> kinds_;
@@ -131,7 +132,9 @@ class ObjectStore {
   void check_faults(const std::string& verb, const std::string& kind);
   void emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv);
   JsonPtr create_locked(const std::string& kind, Json obj);
+  void flush_batch_locked(std::vector<WatchEvent>& batch);
   static void stamp(Json& obj, int64_t rv);
+  std::vector<WatchEvent>* batch_ = nullptr;  // bulk ops collect events here (under mu_)
 
   mutable std::mutex mu_;
   std::unordered_map<std::string, KindMap> kinds_;

@@ -1,0 +1,83 @@
+// Native driver: replays benchmark waves against the C++ store + scheduler
+// without Python. Used for (a) ThreadSanitizer runs of the concurrent core
+// (build_ext --tsan) and (b) profiling the scheduling cycle.
+//
+//   xsched_stress <dir> [waves]
+// <dir> holds nodes.json, nrts.json, config.json (native profile config) and
+// wave_<i>.json files {"podgroups":[...],"pods":[...]} written by
+// flex_gpu_scheduler_amd/tools/stress.py.
+#include <chrono>
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+
+#include "scheduler/scheduler.h"
+
+using namespace xsched;
+
+static std::string slurp(const std::string& p) {
+  std::ifstream f(p);
+  if (!f) {
+    std::fprintf(stderr, "cannot read %s\n", p.c_str());
+    std::exit(2);
+  }
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s <dir> [waves]\n", argv[0]);
+    return 2;
+  }
+  std::string dir = argv[1];
+  int waves = argc > 2 ? std::atoi(argv[2]) : 4;
+  auto store = std::make_shared<ObjectStore>();
+  auto load_many = [&](const std::string& kind, const std::string& file) {
+    Json arr = Json::parse(slurp(dir + "/" + file));
+    std::vector<Json> v(arr.items().begin(), arr.items().end());
+    store->create_many(kind, std::move(v));
+  };
+  load_many("nodes", "nodes.json");
+  load_many("noderesourcetopologies", "nrts.json");
+  Json cfg = Json::parse(slurp(dir + "/config.json"));
+  Scheduler sched(store, cfg);
+  sched.start();
+  uint64_t bound = 0;
+  double total_s = 0;
+  size_t total_pods = 0;
+  for (int w = 0; w < waves; ++w) {
+    Json wave = Json::parse(slurp(dir + "/wave_" + std::to_string(w % 4) + ".json"));
+    std::vector<Json> pgs(wave["podgroups"].items().begin(), wave["podgroups"].items().end());
+    std::vector<Json> pods(wave["pods"].items().begin(), wave["pods"].items().end());
+    size_t n = pods.size();
+    auto t0 = std::chrono::steady_clock::now();
+    store->create_many("podgroups", std::move(pgs));
+    store->create_many("pods", std::move(pods));
+    auto deadline = t0 + std::chrono::seconds(60);
+    while (sched.stats().bound < bound + n) {
+      if (std::chrono::steady_clock::now() > deadline) {
+        std::fprintf(stderr, "wave %d timed out: bound %llu/%zu\n", w,
+                     static_cast<unsigned long long>(sched.stats().bound - bound), n);
+        sched.stop();
+        return 1;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    bound += n;
+    std::string ns = wave["namespace"].str_or("bench");
+    store->delete_all("pods", ns);
+    store->delete_all("podgroups", ns);
+    while (sched.cache().pod_count() > 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
+    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    total_s += s;
+    total_pods += n;
+    std::printf("wave %d: %zu pods in %.4fs (%.0f pods/s)\n", w, n, s, n / s);
+  }
+  sched.stop();
+  std::printf("total: %zu pods in %.4fs (%.0f pods/s)\n", total_pods, total_s, total_pods / total_s);
+  return 0;
+}

@@ -51,7 +51,7 @@ PLUGIN_POINTS: dict[str, tuple[str, ...]] = {
     "Coscheduling": ("queueSort", "preFilter", "postFilter", "reserve", "permit", "postBind"),
     "CapacityScheduling": ("preFilter", "postFilter", "reserve"),
     "NodeResourcesAllocatable": ("score",),
-    "NodeResourceTopologyMatch": ("filter", "score"),
+    "NodeResourceTopologyMatch": ("filter", "preScore", "score"),
     "TargetLoadPacking": ("score",),
     "LoadVariationRiskBalancing": ("score",),
     "PreemptionToleration": ("postFilter",),

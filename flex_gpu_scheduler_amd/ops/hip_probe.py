@@ -1,0 +1,92 @@
+"""ctypes front-end for the HIP/CDNA4 device probes (csrc/hip/hbm_probe.hip).
+
+The probes are what the node agent runs before advertising an MI355X as
+schedulable: device properties, HBM streaming bandwidth (optionally with a
+partition-sized CU budget), an XCD census that verifies the compute-partition
+mode, and a checksum health test.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+from dataclasses import dataclass
+from pathlib import Path
+
+_LIB = Path(__file__).resolve().parent / "_hipprobe.so"
+MODES = {"read": 0, "write": 1, "copy": 2, "triad": 3}
+
+
+class ProbeError(RuntimeError):
+    pass
+
+
+@dataclass
+class Bandwidth:
+    mode: str
+    bytes: int
+    gbps: float
+    ms_per_iter: float
+    cu_limit: int
+
+
+class HipProbe:
+    def __init__(self, path: str | Path = _LIB):
+        if not Path(path).exists():
+            raise ProbeError(f"{path} not built; run `python -m flex_gpu_scheduler_amd.build_ext --hip`")
+        self.lib = ctypes.CDLL(str(path))
+        L = self.lib
+        L.xs_last_error.restype = ctypes.c_char_p
+        L.xs_device_count.restype = ctypes.c_int
+        L.xs_device_props.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.xs_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.xs_xcd_census.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                    ctypes.POINTER(ctypes.c_int)]
+        L.xs_health_check.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_ulonglong),
+                                      ctypes.POINTER(ctypes.c_ulonglong)]
+
+    def _err(self, rc: int, what: str) -> ProbeError:
+        return ProbeError(f"{what} failed ({rc}): {self.lib.xs_last_error().decode(errors='replace')}")
+
+    def device_count(self) -> int:
+        return int(self.lib.xs_device_count())
+
+    def props(self, dev: int = 0) -> dict:
+        buf = ctypes.create_string_buffer(4096)
+        rc = self.lib.xs_device_props(dev, buf, len(buf))
+        if rc < 0:
+            raise self._err(rc, "device_props")
+        return json.loads(buf.value.decode())
+
+    def hbm_bandwidth(self, dev: int = 0, nbytes: int = 1 << 30, iters: int = 20, cu_limit: int = 0,
+                      mode: str = "copy") -> Bandwidth:
+        g, ms = ctypes.c_double(), ctypes.c_double()
+        rc = self.lib.xs_hbm_bandwidth(dev, nbytes, iters, cu_limit, MODES[mode], ctypes.byref(g), ctypes.byref(ms))
+        if rc != 0:
+            raise self._err(rc, "hbm_bandwidth")
+        return Bandwidth(mode, nbytes, g.value, ms.value, cu_limit)
+
+    def xcd_census(self, dev: int = 0, blocks: int = 4096) -> dict:
+        hist = (ctypes.c_int * 8)()
+        cus = ctypes.c_int()
+        rc = self.lib.xs_xcd_census(dev, blocks, hist, ctypes.byref(cus))
+        if rc < 0:
+            raise self._err(rc, "xcd_census")
+        return {"distinct_xcds": rc, "blocks_per_xcd": list(hist), "distinct_cu_slots": cus.value}
+
+    def health(self, dev: int = 0, nbytes: int = 64 << 20) -> dict:
+        d, h = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        rc = self.lib.xs_health_check(dev, nbytes, ctypes.byref(d), ctypes.byref(h))
+        if rc < 0:
+            raise self._err(rc, "health_check")
+        return {"healthy": rc == 0, "device_sum": d.value, "host_sum": h.value}
+
+
+_probe: HipProbe | None = None
+
+
+def probe() -> HipProbe:
+    global _probe
+    if _probe is None:
+        _probe = HipProbe()
+    return _probe

@@ -1,0 +1,37 @@
+"""Write the inputs of the native stress driver (csrc/tools/stress_main.cc):
+nodes, NRTs, the resolved flagship scheduler config and four waves."""
+from __future__ import annotations
+
+import argparse
+import json
+from pathlib import Path
+
+from ..config import load_config
+from ..utils.workload import ClusterSpec, flagship_config, make_wave
+
+
+def write_inputs(out: str | Path, nodes: int = 64, seed: int = 0, options: dict | None = None) -> Path:
+    d = Path(out)
+    d.mkdir(parents=True, exist_ok=True)
+    spec = ClusterSpec(nodes=nodes)
+    (d / "nodes.json").write_text(json.dumps(spec.node_objects()))
+    (d / "nrts.json").write_text(json.dumps(spec.nrt_objects()))
+    cfg = load_config(flagship_config()).to_native(**(options or {}))
+    (d / "config.json").write_text(json.dumps(cfg))
+    for i in range(4):
+        w = make_wave(spec, i, namespace="bench", seed=seed)
+        (d / f"wave_{i}.json").write_text(json.dumps({"namespace": "bench", "podgroups": w.pod_groups, "pods": w.pods}))
+    return d
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--nodes", type=int, default=64)
+    ap.add_argument("--parallelism", type=int, default=16)
+    a = ap.parse_args()
+    write_inputs(a.out, a.nodes, options={"parallelism": a.parallelism})
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,89 @@
+"""Benchmark runner: one scheduler shard over a synthetic 8x MI355X cluster.
+
+A "step" is one wave (utils/workload.py): create the PodGroups and pods of the
+wave in the store, wait until every pod is bound, then delete the wave and
+wait until the scheduler's cache has dropped it. Everything — API writes,
+informer ingestion, scheduling and binding cycles, PodGroup status PATCHes,
+deletions — happens inside the step.
+"""
+from __future__ import annotations
+
+import json
+import time
+from dataclasses import dataclass, field
+
+from ..config import load_config
+from ..scheduler import Store, new_scheduler
+from .workload import ClusterSpec, Wave, flagship_config, make_wave, percentile
+
+
+class WaveTimeout(RuntimeError):
+    pass
+
+
+@dataclass
+class StepResult:
+    pods: int
+    seconds: float
+    gangs: list[dict] = field(default_factory=list)
+
+
+class Shard:
+    def __init__(self, spec: ClusterSpec, *, namespace: str = "bench", seed: int = 0, config: dict | None = None,
+                 options: dict | None = None):
+        self.spec = spec
+        self.ns = namespace
+        self.seed = seed
+        self.store = Store()
+        self.store.create_many("nodes", json.dumps(spec.node_objects()))
+        self.store.create_many("noderesourcetopologies", json.dumps(spec.nrt_objects()))
+        opts = {"seed": seed + 1, **(options or {})}
+        self.sched = new_scheduler(self.store, load_config(config or flagship_config()), **opts)
+        self.sched.start()
+        self._bound = 0
+
+    def wave(self, step: int) -> Wave:
+        return make_wave(self.spec, step, namespace=self.ns, seed=self.seed)
+
+    def run(self, wave: Wave, timeout_s: float = 120.0, *, prepared: tuple[str, str] | None = None) -> StepResult:
+        groups_js, pods_js = prepared if prepared else (wave.groups_json(), wave.pods_json())
+        n = len(wave.pods)
+        target = self._bound + n
+        t0 = time.perf_counter()
+        self.store.create_many("podgroups", groups_js)
+        self.store.create_many("pods", pods_js)
+        deadline = t0 + timeout_s
+        sched = self.sched
+        while True:
+            b = sched.stats()["bound"]
+            if b >= target:
+                break
+            if time.perf_counter() > deadline:
+                raise WaveTimeout(f"wave not bound after {timeout_s}s: {b - self._bound}/{n} "
+                                  f"queue={sched.queue_counts()} stats={sched.stats()}")
+            time.sleep(0.0002)
+        self._bound = target
+        gangs = sched.gang_records(True)
+        self.store.delete_all("pods", self.ns)
+        self.store.delete_all("podgroups", self.ns)
+        while sched.cache_counts()["pods"] > 0:
+            if time.perf_counter() > deadline:
+                raise WaveTimeout("wave deletion not observed by the scheduler cache")
+            time.sleep(0.0002)
+        return StepResult(n, time.perf_counter() - t0, gangs)
+
+    def close(self) -> None:
+        self.sched.stop()
+
+
+def gang_latency_summary(gangs: list[dict], sizes: dict[str, int] | None = None) -> dict:
+    """p50/p99 first-member-enqueue -> last-member-bound (ms) per group size."""
+    by: dict[int, list[float]] = {}
+    for g in gangs:
+        sz = g["size"]
+        by.setdefault(sz, []).append((g["bound_us"] - g["first_enqueue_us"]) / 1000.0)
+    out = {}
+    for sz in sorted(by):
+        xs = by[sz]
+        out[str(sz)] = {"n": len(xs), "p50_ms": round(percentile(xs, 50), 3), "p99_ms": round(percentile(xs, 99), 3)}
+    return out

@@ -1,0 +1,151 @@
+"""Synthetic MI355X cluster + gang workload generator (the benchmark's data).
+
+BASELINE.json names the metric "pods/sec sched throughput + p99 PodGroup
+gang-admit latency, 1/2/4/8-GPU groups" over synthetic pod specs with random
+resource requests. A wave mixes, per the BASELINE configs:
+  * PodGroups of 1, 2, 4 and 8 ranks, one whole MI355X per rank
+    (distributed-training gangs, Coscheduling + FlexGPU + xGMI placement);
+  * "4 pods x 0.25 amd.com/gpu" CPX fractional gangs (amd.com/gpu-xcd: 2);
+  * shared-HBM slice pods (amd.com/gpu-memory) for inference-style packing;
+with random CPU/memory requests. Waves are sized to a target fraction of
+cluster GPU capacity so every wave is schedulable.
+"""
+from __future__ import annotations
+
+import json
+import random
+from dataclasses import dataclass, field
+
+from ..models.mi355x import GPU, GPU_MEMORY, GPU_XCD, default_gpus, mi355x_node, mi355x_nrt
+from ..models.objects import make_container, make_pod, make_pod_group
+
+GROUP_SIZES = (1, 2, 4, 8)
+
+
+@dataclass
+class ClusterSpec:
+    nodes: int = 64
+    cpx_fraction: float = 0.25  # share of nodes whose GPUs run in CPX mode
+    hbm_gib: int = 288
+    cpu: str = "256"
+    memory: str = "3Ti"
+
+    def node_objects(self, prefix: str = "mi355x") -> list[dict]:
+        out = []
+        n_cpx = int(round(self.nodes * self.cpx_fraction))
+        for i in range(self.nodes):
+            mode = "cpx" if i < n_cpx else "spx"
+            gpus = default_gpus(8, mode)
+            for g in gpus:
+                g.hbm_gib = self.hbm_gib
+            out.append(mi355x_node(f"{prefix}-{i:04d}", gpus=gpus, cpu=self.cpu, memory=self.memory))
+        return out
+
+    def nrt_objects(self, prefix: str = "mi355x") -> list[dict]:
+        return [mi355x_nrt(f"{prefix}-{i:04d}") for i in range(self.nodes)]
+
+    @property
+    def spx_gpus(self) -> int:
+        return (self.nodes - int(round(self.nodes * self.cpx_fraction))) * 8
+
+    @property
+    def cpx_xcds(self) -> int:
+        return int(round(self.nodes * self.cpx_fraction)) * 8 * 8
+
+
+@dataclass
+class Wave:
+    pod_groups: list[dict] = field(default_factory=list)
+    pods: list[dict] = field(default_factory=list)
+    group_sizes: dict[str, int] = field(default_factory=dict)
+
+    def pods_json(self) -> str:
+        return json.dumps(self.pods)
+
+    def groups_json(self) -> str:
+        return json.dumps(self.pod_groups)
+
+
+def _rand_cpu_mem(rng: random.Random) -> dict:
+    return {"cpu": f"{rng.choice([500, 1000, 2000, 4000])}m", "memory": f"{rng.choice([2, 4, 8, 16])}Gi"}
+
+
+def make_wave(spec: ClusterSpec, step: int, *, namespace: str = "bench", fill: float = 0.85, seed: int = 0,
+              scheduler_name: str | None = None) -> Wave:
+    """One wave of gangs filling ~`fill` of the SPX GPUs and CPX XCDs."""
+    rng = random.Random(seed * 1_000_003 + step)
+    w = Wave()
+    gpu_budget = int(spec.spx_gpus * fill)
+    # Whole-GPU gangs: cycle through sizes so each wave has all four.
+    gi = 0
+    while gpu_budget > 0:
+        size = GROUP_SIZES[gi % len(GROUP_SIZES)] if gi < 4 else rng.choice(GROUP_SIZES)
+        gi += 1
+        if size > gpu_budget:
+            size = 1
+        name = f"s{step}-g{gi}-x{size}"
+        w.pod_groups.append(make_pod_group(name, namespace, size))
+        w.group_sizes[f"{namespace}/{name}"] = size
+        req = _rand_cpu_mem(rng)
+        for r in range(size):
+            c = make_container("trainer", requests=req, limits={GPU: "1"})
+            w.pods.append(make_pod(f"{name}-r{r}", namespace, containers=[c], pod_group=name,
+                                   scheduler_name=scheduler_name))
+        gpu_budget -= size
+    # CPX fractional gangs: 4 pods x 0.25 GPU (2 XCDs each) = one CPX GPU.
+    xcd_budget = int(spec.cpx_xcds * fill * 0.75)
+    fi = 0
+    while xcd_budget >= 8:
+        fi += 1
+        name = f"s{step}-q{fi}"
+        w.pod_groups.append(make_pod_group(name, namespace, 4))
+        w.group_sizes[f"{namespace}/{name}"] = 4
+        req = _rand_cpu_mem(rng)
+        for r in range(4):
+            c = make_container("shard", requests=req, limits={GPU_XCD: "2"})
+            w.pods.append(make_pod(f"{name}-r{r}", namespace, containers=[c], pod_group=name,
+                                   scheduler_name=scheduler_name))
+        xcd_budget -= 8
+    # Shared-HBM inference pods packed into the remaining CPX partitions.
+    for m in range(int(spec.cpx_xcds * fill * 0.25 / 2)):
+        c = make_container("infer", requests=_rand_cpu_mem(rng), limits={GPU_MEMORY: str(rng.choice([8, 12, 16]))})
+        w.pods.append(make_pod(f"s{step}-m{m}", namespace, containers=[c], scheduler_name=scheduler_name))
+    return w
+
+
+def flagship_config(permit_wait_s: int = 10, denied_s: int = 3) -> dict:
+    """KubeSchedulerConfiguration of the benchmark: Coscheduling gangs +
+    FlexGPU MI355X packing (FlexGPU binds) + NRT xGMI gang placement."""
+    return {
+        "apiVersion": "kubescheduler.config.k8s.io/v1beta3",
+        "kind": "KubeSchedulerConfiguration",
+        "profiles": [{
+            "schedulerName": "default-scheduler",
+            "plugins": {
+                "queueSort": {"enabled": [{"name": "Coscheduling"}], "disabled": [{"name": "*"}]},
+                "preFilter": {"enabled": [{"name": "Coscheduling"}]},
+                "filter": {"enabled": [{"name": "FlexGPU"}, {"name": "NodeResourceTopologyMatch"}]},
+                "postFilter": {"enabled": [{"name": "Coscheduling"}]},
+                "preScore": {"enabled": [{"name": "NodeResourceTopologyMatch"}]},
+                "score": {"enabled": [{"name": "FlexGPU", "weight": 1},
+                                      {"name": "NodeResourceTopologyMatch", "weight": 2}]},
+                "reserve": {"enabled": [{"name": "Coscheduling"}, {"name": "FlexGPU"}]},
+                "permit": {"enabled": [{"name": "Coscheduling"}]},
+                "bind": {"enabled": [{"name": "FlexGPU"}], "disabled": [{"name": "DefaultBinder"}]},
+                "postBind": {"enabled": [{"name": "Coscheduling"}]},
+            },
+            "pluginConfig": [
+                {"name": "Coscheduling",
+                 "args": {"permitWaitingTimeSeconds": permit_wait_s, "deniedPGExpirationTimeSeconds": denied_s}},
+                {"name": "NodeResourceTopologyMatch", "args": {"scoringStrategy": {"type": "XGMIGangAffinity"}}},
+            ],
+        }],
+    }
+
+
+def percentile(xs: list[float], q: float) -> float:
+    if not xs:
+        return float("nan")
+    s = sorted(xs)
+    k = max(0, min(len(s) - 1, int(round(q / 100.0 * (len(s) - 1)))))
+    return s[k]

@@ -1,0 +1,167 @@
+"""FlexGPU on MI355X nodes: whole-GPU, CPX partition and HBM-slice packing.
+
+The reference FlexGPU has no tests at all; these pin the
+behaviour of pkg/flexgpu/{flex_gpu,gpu_node}.go plus the MI355X partition
+model and the deliberate Appendix C fixes."""
+import time
+
+import pytest
+
+from flex_gpu_scheduler_amd.models import (GPU, GPU_MEMORY, GPU_XCD, GpuInfo, make_pod, make_pod_group,
+                                           mi355x_node)
+from helpers import FLEXGPU_PLUGINS, annotations, coscheduling_config, create_all, placements, start, wait_bound
+
+
+def cfg():
+    return coscheduling_config(FLEXGPU_PLUGINS)
+
+
+def test_whole_gpu_indexes_are_distinct(store):
+    store.create("nodes", mi355x_node("n0"))
+    s = start(store, cfg())
+    try:
+        create_all(store, "pods", [make_pod(f"p{i}", limits={GPU: "1"}) for i in range(8)])
+        wait_bound(s, 8)
+        idx = sorted(int(annotations(store, f"p{i}")["amd.com/gpu-index"]) for i in range(8))
+        assert idx == list(range(8))
+        store.create("pods", make_pod("p8", limits={GPU: "1"}))
+        time.sleep(0.3)
+        assert placements(store)["p8"] == ""  # 9th whole GPU does not exist
+    finally:
+        s.stop()
+
+
+def test_multi_gpu_pod_prefers_one_socket(store):
+    store.create("nodes", mi355x_node("n0"))
+    s = start(store, cfg())
+    try:
+        store.create("pods", make_pod("one", limits={GPU: "1"}))
+        wait_bound(s, 1)
+        store.create("pods", make_pod("four", limits={GPU: "4"}))
+        wait_bound(s, 2)
+        gpus = [int(x) for x in annotations(store, "four")["amd.com/gpu-index"].split(",")]
+        assert len(gpus) == 4 and len({g // 4 for g in gpus}) == 1  # all on one NUMA socket
+    finally:
+        s.stop()
+
+
+def test_cpx_quarter_gpu_slices(store):
+    # BASELINE config: 4 pods x 0.25 amd.com/gpu on one MI355X (CPX partition)
+    store.create("nodes", mi355x_node("cpx", n_gpus=1, mode="cpx"))
+    s = start(store, cfg())
+    try:
+        create_all(store, "pods", [make_pod(f"q{i}", limits={GPU_XCD: "2"}) for i in range(4)])
+        wait_bound(s, 4)
+        parts = set()
+        for i in range(4):
+            a = annotations(store, f"q{i}")
+            assert a["amd.com/gpu-index"] == "0"
+            ps = a["amd.com/gpu-partitions"].split(",")
+            assert len(ps) == 2
+            parts.update(ps)
+        assert len(parts) == 8  # the 8 CPX partitions are split disjointly
+        store.create("pods", make_pod("q4", limits={GPU_XCD: "1"}))
+        time.sleep(0.3)
+        assert placements(store)["q4"] == ""
+    finally:
+        s.stop()
+
+
+def test_xcd_slice_avoids_stranding_spx_gpu(store):
+    store.create("nodes", mi355x_node("spx", n_gpus=8, mode="spx"))
+    store.create("nodes", mi355x_node("cpx", n_gpus=1, mode="cpx"))
+    s = start(store, cfg())
+    try:
+        store.create("pods", make_pod("q", limits={GPU_XCD: "2"}))
+        wait_bound(s, 1)
+        assert placements(store)["q"] == "cpx"
+    finally:
+        s.stop()
+
+
+def test_memory_slices_best_fit_and_capacity(store):
+    # Per-GPU memory = allocatable / GPUs (gpu_node.go:51-55); best fit packs
+    # slices onto the fullest GPU (Appendix C1 fixed: value semantics).
+    store.create("nodes", mi355x_node("n", gpus=[GpuInfo(0, hbm_gib=100), GpuInfo(1, hbm_gib=100)]))
+    s = start(store, cfg())
+    try:
+        store.create("pods", make_pod("m0", limits={GPU_MEMORY: "60"}))
+        wait_bound(s, 1)
+        g0 = annotations(store, "m0")["amd.com/gpu-index"]
+        store.create("pods", make_pod("m1", limits={GPU_MEMORY: "30"}))
+        wait_bound(s, 2)
+        assert annotations(store, "m1")["amd.com/gpu-index"] == g0  # fits beside m0 -> same GPU
+        store.create("pods", make_pod("m2", limits={GPU_MEMORY: "50"}))
+        wait_bound(s, 3)
+        assert annotations(store, "m2")["amd.com/gpu-index"] != g0
+        store.create("pods", make_pod("m3", limits={GPU_MEMORY: "60"}))
+        time.sleep(0.3)
+        assert placements(store)["m3"] == ""  # 40 + 50 free, no single GPU has 60
+    finally:
+        s.stop()
+
+
+def test_conflicting_resources_unresolvable(store):
+    store.create("nodes", mi355x_node("n"))
+    s = start(store, cfg())
+    try:
+        store.create("pods", make_pod("bad", limits={GPU: "1", GPU_MEMORY: "10"}))
+        time.sleep(0.3)
+        cond = store.get("pods", "default", "bad")["status"]["conditions"][0]
+        assert "pod conflict resources" in cond["message"]
+    finally:
+        s.stop()
+
+
+def test_node_without_gpu_resources_is_unresolvable(store):
+    from flex_gpu_scheduler_amd.models import make_node
+
+    store.create("nodes", make_node("cpu-only"))
+    s = start(store, cfg())
+    try:
+        store.create("pods", make_pod("g", limits={GPU: "1"}))
+        time.sleep(0.3)
+        assert "unknown resource type" in store.get("pods", "default", "g")["status"]["conditions"][0]["message"] \
+            or "Insufficient" in store.get("pods", "default", "g")["status"]["conditions"][0]["message"]
+    finally:
+        s.stop()
+
+
+def test_gpu_freed_on_delete_is_reused(store):
+    store.create("nodes", mi355x_node("n", n_gpus=1))
+    s = start(store, cfg())
+    try:
+        store.create("pods", make_pod("a", limits={GPU: "1"}))
+        wait_bound(s, 1)
+        store.create("pods", make_pod("b", limits={GPU: "1"}))
+        time.sleep(0.2)
+        assert placements(store)["b"] == ""
+        store.delete("pods", "default", "a")  # AssignedPodDelete re-queues b
+        wait_bound(s, 2)
+        assert placements(store)["b"] == "n"
+    finally:
+        s.stop()
+
+
+def test_gang_ranks_colocate_on_one_node(store):
+    import json
+
+    from flex_gpu_scheduler_amd import load_config, new_scheduler
+    from flex_gpu_scheduler_amd.models import mi355x_nrt
+    from flex_gpu_scheduler_amd.utils.workload import flagship_config
+
+    for i in range(4):
+        store.create("nodes", mi355x_node(f"n{i}"))
+        store.create("noderesourcetopologies", mi355x_nrt(f"n{i}"))
+    s = new_scheduler(store, load_config(flagship_config()), start=True)
+    try:
+        # Partially fill two nodes so a naive bin-packer would split the gang.
+        create_all(store, "pods", [make_pod(f"f{i}", limits={GPU: "1"}) for i in range(6)])
+        wait_bound(s, 6)
+        store.create("podgroups", make_pod_group("ring", "default", 8))
+        create_all(store, "pods", [make_pod(f"r{i}", pod_group="ring", limits={GPU: "1"}) for i in range(8)])
+        wait_bound(s, 14)
+        nodes = {placements(store)[f"r{i}"] for i in range(8)}
+        assert len(nodes) == 1, nodes  # all 8 ranks share one node's xGMI mesh
+    finally:
+        s.stop()

@@ -1,0 +1,83 @@
+"""GPU-side checks on a real MI355X (run by `pytest -m gpu` on the GPU box).
+
+The HIP probe is native code that must load and run (no fallback): device
+properties, XCD census (partition-mode verification), checksum health, and
+HBM streaming bandwidth against the device's ~8 TB/s HBM3E."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def pr():
+    from flex_gpu_scheduler_amd import build_ext
+
+    build_ext.build_hip(verbose=False)
+    from flex_gpu_scheduler_amd.ops.hip_probe import HipProbe
+
+    p = HipProbe()
+    assert p.device_count() >= 1
+    return p
+
+
+def test_device_props_mi355x(pr):
+    props = pr.props(0)
+    assert props["gcnArchName"].startswith("gfx950"), props
+    assert props["warpSize"] == 64
+    assert props["computeUnits"] >= 32  # 256 in SPX, 32 per XCD in CPX
+    assert props["totalGlobalMem"] > (16 << 30)
+
+
+def test_health_checksum(pr):
+    h = pr.health(0, 256 << 20)
+    assert h["healthy"], h
+
+
+def test_xcd_census_matches_partition_mode(pr):
+    c = pr.xcd_census(0, 4096)
+    props = pr.props(0)
+    assert 1 <= c["distinct_xcds"] <= 8
+    # SPX exposes all 8 XCDs (256 CUs) to one device; CPX one XCD (32 CUs).
+    expected = max(1, props["computeUnits"] // 32)
+    assert c["distinct_xcds"] == expected, (c, props["computeUnits"])
+    assert sum(c["blocks_per_xcd"]) == 4096
+
+
+@pytest.mark.parametrize("mode", ["read", "copy", "triad"])
+def test_hbm_bandwidth(pr, mode):
+    bw = pr.hbm_bandwidth(0, 1 << 30, iters=10, mode=mode)
+    # HBM3E: 8 TB/s peak, ~6.3 TB/s measured for a float4 copy; a streaming
+    # kernel that reaches < 3 TB/s on a full device is broken.
+    assert bw.gbps > 3000, bw
+
+
+def test_partition_sized_probe_scales_down(pr):
+    full = pr.hbm_bandwidth(0, 512 << 20, iters=5, mode="copy", cu_limit=0)
+    part = pr.hbm_bandwidth(0, 512 << 20, iters=5, mode="copy", cu_limit=32)
+    assert part.gbps < full.gbps
+
+
+def test_smoke_entry():
+    r = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.smoke()"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["smoke"] == "ok"
+
+
+def test_bench_one_gpu_json_contract():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--nodes", "16"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in line
+    assert line["value"] > 0 and line["config"]["gpu"]["name"].startswith("gfx950")
