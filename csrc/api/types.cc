@@ -357,6 +357,9 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
   if (status["phase"].is_string()) p->phase = status["phase"].as_string();
   p->nominated_node_name = status["nominatedNodeName"].as_string();
   if (status["startTime"].is_string()) p->start_time = parse_rfc3339(status["startTime"].as_string());
+  for (const auto& c : status["conditions"].items())
+    if (c["type"].as_string() == "PodScheduled" && c["status"].as_string() == "True")
+      p->scheduled_at = parse_rfc3339(c["lastTransitionTime"].as_string());
 
   // Derived request/limit vectors.
   Res sum;

@@ -138,6 +138,7 @@ struct Pod {
   std::vector<PodAffinityTerm> pod_affinity_required, pod_anti_affinity_required;
   std::vector<WeightedPodAffinityTerm> pod_affinity_preferred, pod_anti_affinity_preferred;
   MicroTime start_time = 0;
+  MicroTime scheduled_at = 0;  // PodScheduled=True lastTransitionTime (0 = not scheduled)
 
   // ---- derived at parse time ----
   Res request;          // computePodResourceRequest: max(sum(containers), each init) + overhead

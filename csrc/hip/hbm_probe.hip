@@ -4,14 +4,21 @@
 // counts extended resources. An MI355X-native scheduler must validate what it
 // promises, so the node agent runs these probes on the box:
 //
-//  * xs_hbm_bandwidth   streaming read / write / copy / triad over N bytes
-//                       with 16-byte lanes (global_load/store_dwordx4),
-//                       grid = cu_limit x 8 blocks of 256 threads. cu_limit
-//                       emulates a compute partition's CU budget (CPX: 32
-//                       CUs/XCD); the result is HBM GB/s that a slice can
-//                       expect (HBM3E peak 8 TB/s, ~6.3 TB/s achievable).
+//  * xs_hbm_bandwidth   streaming read / write / copy / triad over N bytes with
+//                       16-byte lanes (global_load/store_dwordx4). Variants:
+//                       unroll 1/4/8 (independent 16 B accesses in flight per
+//                       lane), non-temporal vs default cache policy, 4/8/16
+//                       workgroups of 256 threads per CU; probe_bench sweeps
+//                       them and the node agent keeps the fastest. HBM3E peak
+//                       is 8 TB/s; ~6.3 TB/s is the achievable streaming rate.
+//  * xs_hbm_bandwidth_xcd  the same traffic executed only by workgroups that
+//                       land on the XCDs in `xcd_mask` (work handed out by an
+//                       atomic chunk counter, so every launched workgroup
+//                       exits): the HBM bandwidth one CPX partition (one XCD,
+//                       32 CUs) or a QPX/DPX partition can pull, measured on
+//                       an SPX device.
 //  * xs_xcd_census      every workgroup records s_getreg(HW_REG_XCC_ID):
-//                       counts XCDs/CUs visible to this device — verifies the
+//                       counts XCDs visible to this device — verifies the
 //                       compute-partition mode the node advertises (SPX -> 8
 //                       XCDs, CPX -> 1).
 //  * xs_health_check    deterministic integer checksum over a pattern buffer
@@ -25,76 +32,99 @@
 #include <cstdio>
 #include <cstring>
 
-#define XS_CHECK(x)                                  \
-  do {                                               \
-    hipError_t e_ = (x);                             \
-    if (e_ != hipSuccess) {                          \
+#define XS_CHECK(x)                                                            \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
       std::snprintf(g_err, sizeof g_err, "%s: %s", #x, hipGetErrorString(e_)); \
-      return -static_cast<int>(e_) - 1;             \
-    }                                                \
+      return -static_cast<int>(e_) - 1;                                        \
+    }                                                                          \
   } while (0)
 
 namespace {
 
 char g_err[512];
 
-constexpr int kBlock = 256;       // 4 waves of 64 lanes
-constexpr int kBlocksPerCU = 8;   // enough waves in flight to cover HBM latency
-constexpr int kUnroll = 4;        // 4 x 16 B in flight per lane per iteration
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
-typedef uint32_t vec4 __attribute__((ext_vector_type(4)));  // 16 B/lane -> global_load_dwordx4
+typedef uint32_t vec4 __attribute__((ext_vector_type(4)));  // 16 B/lane
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Every kernel walks the buffer in grid-stride "rows" of kUnroll*grid lanes so
-// each wave-instruction touches 1 KiB contiguous (full 128 B lines).
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T v, T* p) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
+// Grid-stride walk in rows of U*grid lanes: one wave-instruction touches
+// 1 KiB contiguous, U independent 16-B accesses per lane in flight.
+template <int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_read(const vec4* __restrict__ src, size_t n, uint32_t* __restrict__ sink) {
   const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
   size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
   uint32_t acc = 0;
-  for (; i + (kUnroll - 1) * stride < n; i += kUnroll * stride) {
-    vec4 v[kUnroll];
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    vec4 v[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) v[u] = __builtin_nontemporal_load(&src[i + u * stride]);
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&src[i + u * stride]);
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
   }
   for (; i < n; i += stride) {
-    vec4 v = __builtin_nontemporal_load(&src[i]);
+    vec4 v = ld<NT>(&src[i]);
     acc ^= v.x ^ v.y ^ v.z ^ v.w;
   }
-  if (acc == 0x9e3779b9u) sink[0] = acc;  // practically never true: defeats DCE without a store per lane
+  if (acc == 0x9e3779b9u) sink[0] = acc;  // defeats DCE without a store per lane
 }
 
+template <int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_write(vec4* __restrict__ dst, size_t n, uint32_t seed) {
   const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
   vec4 v = {seed, seed ^ 0x55555555u, seed + 1, ~seed};
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride)
-    __builtin_nontemporal_store(v, &dst[i]);
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(v, &dst[i + u * stride]);
+  }
+  for (; i < n; i += stride) st<NT>(v, &dst[i]);
 }
 
+template <int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_copy(const vec4* __restrict__ src, vec4* __restrict__ dst, size_t n) {
   const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
   size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  for (; i + (kUnroll - 1) * stride < n; i += kUnroll * stride) {
-    vec4 v[kUnroll];
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    vec4 v[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) v[u] = __builtin_nontemporal_load(&src[i + u * stride]);
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(&src[i + u * stride]);
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) __builtin_nontemporal_store(v[u], &dst[i + u * stride]);
+    for (int u = 0; u < U; ++u) st<NT>(v[u], &dst[i + u * stride]);
   }
-  for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
+  for (; i < n; i += stride) st<NT>(ld<NT>(&src[i]), &dst[i]);
 }
 
 // STREAM triad a = b + s*c on float4 lanes.
+template <int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_triad(f32x4* __restrict__ a, const f32x4* __restrict__ b,
                                                   const f32x4* __restrict__ c, float s, size_t n) {
   const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
-    f32x4 x = __builtin_nontemporal_load(&b[i]);
-    f32x4 y = __builtin_nontemporal_load(&c[i]);
-    __builtin_nontemporal_store(x + s * y, &a[i]);
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    f32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u] = ld<NT>(&b[i + u * stride]);
+      y[u] = ld<NT>(&c[i + u * stride]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(x[u] + s * y[u], &a[i + u * stride]);
   }
+  for (; i < n; i += stride) st<NT>(ld<NT>(&b[i]) + s * ld<NT>(&c[i]), &a[i]);
 }
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -104,10 +134,58 @@ __device__ __forceinline__ uint32_t xcc_id() {
 }
 
 __device__ __forceinline__ uint32_t hw_cu_id() {
-  // HW_ID register: CU_ID in bits [11:8], SE_ID in [14:13] on CDNA.
   uint32_t v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
   return v;
+}
+
+// XCD-pinned streaming: workgroups off the selected XCDs exit at once; the
+// rest pull 64 KiB chunks from an atomic counter until the buffer is done, so
+// the launch always drains. mode 0 read, 1 write, 2 copy.
+__global__ __launch_bounds__(kBlock) void k_pinned(const vec4* __restrict__ src, vec4* __restrict__ dst, size_t n,
+                                                   uint32_t xcd_mask, unsigned* __restrict__ counter, int mode,
+                                                   uint32_t* __restrict__ sink) {
+  if (!((xcd_mask >> xcc_id()) & 1u)) return;
+  constexpr size_t kChunk = 4096;  // vec4s = 64 KiB
+  __shared__ unsigned chunk;
+  uint32_t acc = 0;
+  const vec4 fill = {1u, 2u, 3u, 4u};
+  for (;;) {
+    if (threadIdx.x == 0) chunk = atomicAdd(counter, 1u);
+    __syncthreads();
+    size_t base = static_cast<size_t>(chunk) * kChunk;
+    __syncthreads();
+    if (base >= n) break;
+    size_t end = base + kChunk < n ? base + kChunk : n;
+    size_t i = base + threadIdx.x;
+    for (; i + 3 * kBlock < end; i += 4 * kBlock) {
+      if (mode == 1) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(fill, &dst[i + u * kBlock]);
+      } else {
+        vec4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(&src[i + u * kBlock]);
+        if (mode == 2) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], &dst[i + u * kBlock]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+      }
+    }
+    for (; i < end; i += kBlock) {
+      if (mode == 1) {
+        __builtin_nontemporal_store(fill, &dst[i]);
+      } else {
+        vec4 v = __builtin_nontemporal_load(&src[i]);
+        if (mode == 2) __builtin_nontemporal_store(v, &dst[i]);
+        else acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      }
+    }
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
 __global__ __launch_bounds__(64) void k_census(uint32_t* __restrict__ xcd_of_block, uint32_t* __restrict__ hwid_of_block) {
@@ -143,12 +221,51 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint32_t* __restrict_
   }
 }
 
-int grid_for(int dev, int cu_limit) {
+int cu_count(int dev) {
   hipDeviceProp_t p;
-  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256 * kBlocksPerCU;
-  int cus = p.multiProcessorCount;
-  if (cu_limit > 0 && cu_limit < cus) cus = cu_limit;
-  return cus * kBlocksPerCU;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
+  return p.multiProcessorCount;
+}
+
+// variant = unroll(1|4|8) | (nt ? 0x100 : 0) | (blocks_per_cu << 16); 0 = default.
+struct Variant {
+  int unroll = 4;
+  bool nt = true;
+  int bpc = 8;
+};
+Variant decode(int v) {
+  Variant o;
+  if (v == 0) return o;
+  int u = v & 0xff;
+  o.unroll = (u == 1 || u == 4 || u == 8) ? u : 4;
+  o.nt = (v & 0x100) != 0;
+  int b = (v >> 16) & 0xff;
+  o.bpc = (b == 4 || b == 8 || b == 16) ? b : 8;
+  return o;
+}
+
+template <int U, bool NT>
+void launch_t(int mode, int grid, hipStream_t s, void* a, void* b, void* c, size_t n, uint32_t* sink) {
+  switch (mode) {
+    case 0: k_read<U, NT><<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), n, sink); break;
+    case 1: k_write<U, NT><<<grid, kBlock, 0, s>>>(static_cast<vec4*>(a), n, 7); break;
+    case 2: k_copy<U, NT><<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), static_cast<vec4*>(b), n); break;
+    default:
+      k_triad<U, NT><<<grid, kBlock, 0, s>>>(static_cast<f32x4*>(a), static_cast<const f32x4*>(b),
+                                            static_cast<const f32x4*>(c), 3.0f, n);
+  }
+}
+
+void launch(const Variant& v, int mode, int grid, hipStream_t s, void* a, void* b, void* c, size_t n, uint32_t* sink) {
+  if (v.nt) {
+    if (v.unroll == 1) launch_t<1, true>(mode, grid, s, a, b, c, n, sink);
+    else if (v.unroll == 8) launch_t<8, true>(mode, grid, s, a, b, c, n, sink);
+    else launch_t<4, true>(mode, grid, s, a, b, c, n, sink);
+  } else {
+    if (v.unroll == 1) launch_t<1, false>(mode, grid, s, a, b, c, n, sink);
+    else if (v.unroll == 8) launch_t<8, false>(mode, grid, s, a, b, c, n, sink);
+    else launch_t<4, false>(mode, grid, s, a, b, c, n, sink);
+  }
 }
 
 }  // namespace
@@ -181,46 +298,39 @@ int xs_device_props(int dev, char* out, int len) {
   return n;
 }
 
-// mode: 0 read, 1 write, 2 copy, 3 triad. bytes = working-set per array.
-// Returns 0 and writes GB/s (bytes moved / time) and ms per iteration.
-int xs_hbm_bandwidth(int dev, size_t bytes, int iters, int cu_limit, int mode, double* gbps, double* ms_per_iter) {
+// mode: 0 read, 1 write, 2 copy, 3 triad. bytes = working set per array.
+// cu_limit > 0 caps the grid at cu_limit * blocks_per_cu workgroups.
+int xs_hbm_bandwidth_v(int dev, size_t bytes, int iters, int cu_limit, int mode, int variant, double* gbps,
+                       double* ms_per_iter) {
   XS_CHECK(hipSetDevice(dev));
   if (iters <= 0) iters = 10;
   size_t n = bytes / sizeof(vec4);
-  if (n == 0) return -1000;
+  if (n == 0 || mode < 0 || mode > 3) return -1000;
   bytes = n * sizeof(vec4);
+  Variant v = decode(variant);
   void *a = nullptr, *b = nullptr, *c = nullptr;
   uint32_t* sink = nullptr;
   XS_CHECK(hipMalloc(&a, bytes));
   XS_CHECK(hipMalloc(&b, bytes));
   if (mode == 3) XS_CHECK(hipMalloc(&c, bytes));
   XS_CHECK(hipMalloc(&sink, sizeof(uint32_t)));
-  int grid = grid_for(dev, cu_limit);
+  int cus = cu_count(dev);
+  if (cu_limit > 0 && cu_limit < cus) cus = cu_limit;
+  int grid = cus * v.bpc;
   hipStream_t s;
   XS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  // Touch everything once (page-in) and warm the launch path.
-  k_write<<<grid, kBlock, 0, s>>>(static_cast<vec4*>(a), n, 1);
-  k_write<<<grid, kBlock, 0, s>>>(static_cast<vec4*>(b), n, 2);
-  if (c) k_write<<<grid, kBlock, 0, s>>>(static_cast<vec4*>(c), n, 3);
+  // Page everything in and warm the launch path.
+  launch(Variant{}, 1, grid, s, a, nullptr, nullptr, n, sink);
+  launch(Variant{}, 1, grid, s, b, nullptr, nullptr, n, sink);
+  if (c) launch(Variant{}, 1, grid, s, c, nullptr, nullptr, n, sink);
   XS_CHECK(hipGetLastError());
-  XS_CHECK(hipStreamSynchronize(s));
-  auto launch = [&]() {
-    switch (mode) {
-      case 0: k_read<<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), n, sink); break;
-      case 1: k_write<<<grid, kBlock, 0, s>>>(static_cast<vec4*>(a), n, 7); break;
-      case 2: k_copy<<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), static_cast<vec4*>(b), n); break;
-      default:
-        k_triad<<<grid, kBlock, 0, s>>>(static_cast<f32x4*>(a), static_cast<const f32x4*>(b),
-                                        static_cast<const f32x4*>(c), 3.0f, n);
-    }
-  };
-  launch();
+  launch(v, mode, grid, s, a, b, c, n, sink);
   XS_CHECK(hipStreamSynchronize(s));
   hipEvent_t e0, e1;
   XS_CHECK(hipEventCreate(&e0));
   XS_CHECK(hipEventCreate(&e1));
   XS_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) launch();
+  for (int i = 0; i < iters; ++i) launch(v, mode, grid, s, a, b, c, n, sink);
   XS_CHECK(hipEventRecord(e1, s));
   XS_CHECK(hipEventSynchronize(e1));
   XS_CHECK(hipGetLastError());
@@ -235,7 +345,63 @@ int xs_hbm_bandwidth(int dev, size_t bytes, int iters, int cu_limit, int mode, d
   (void)hipStreamDestroy(s);
   (void)hipFree(a);
   (void)hipFree(b);
-  if (c) hipFree(c);
+  if (c) (void)hipFree(c);
+  (void)hipFree(sink);
+  return 0;
+}
+
+int xs_hbm_bandwidth(int dev, size_t bytes, int iters, int cu_limit, int mode, double* gbps, double* ms_per_iter) {
+  return xs_hbm_bandwidth_v(dev, bytes, iters, cu_limit, mode, 0, gbps, ms_per_iter);
+}
+
+// Bandwidth pulled by the workgroups resident on the XCDs in xcd_mask
+// (mode 0 read, 1 write, 2 copy).
+int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, int mode, double* gbps,
+                         double* ms_per_iter) {
+  XS_CHECK(hipSetDevice(dev));
+  if (iters <= 0) iters = 10;
+  if (mode < 0 || mode > 2 || xcd_mask == 0) return -1000;
+  size_t n = bytes / sizeof(vec4);
+  if (n == 0 || n / 4096 >= 0xffffff00ull) return -1000;
+  bytes = n * sizeof(vec4);
+  void *a = nullptr, *b = nullptr;
+  unsigned* counters = nullptr;
+  uint32_t* sink = nullptr;
+  XS_CHECK(hipMalloc(&a, bytes));
+  XS_CHECK(hipMalloc(&b, bytes));
+  XS_CHECK(hipMalloc(&counters, sizeof(unsigned) * (iters + 1)));
+  XS_CHECK(hipMalloc(&sink, sizeof(uint32_t)));
+  XS_CHECK(hipMemset(counters, 0, sizeof(unsigned) * (iters + 1)));
+  int grid = cu_count(dev) * 8;  // every CU gets 8 workgroups; only masked XCDs work
+  hipStream_t s;
+  XS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  k_write<4, true><<<grid, kBlock, 0, s>>>(static_cast<vec4*>(a), n, 1);
+  k_pinned<<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), static_cast<vec4*>(b), n, xcd_mask, &counters[iters],
+                                   mode, sink);
+  XS_CHECK(hipGetLastError());
+  XS_CHECK(hipStreamSynchronize(s));
+  hipEvent_t e0, e1;
+  XS_CHECK(hipEventCreate(&e0));
+  XS_CHECK(hipEventCreate(&e1));
+  XS_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i)
+    k_pinned<<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), static_cast<vec4*>(b), n, xcd_mask, &counters[i],
+                                     mode, sink);
+  XS_CHECK(hipEventRecord(e1, s));
+  XS_CHECK(hipEventSynchronize(e1));
+  XS_CHECK(hipGetLastError());
+  float ms = 0;
+  XS_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  double per = ms / iters;
+  double moved = static_cast<double>(bytes) * (mode == 2 ? 2.0 : 1.0);
+  if (gbps) *gbps = moved / (per * 1e-3) / 1e9;
+  if (ms_per_iter) *ms_per_iter = per;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  (void)hipFree(counters);
   (void)hipFree(sink);
   return 0;
 }
@@ -262,7 +428,7 @@ int xs_xcd_census(int dev, int blocks, int* xcd_hist8, int* distinct_cus) {
   if (xcd_hist8)
     for (int i = 0; i < 8; ++i) xcd_hist8[i] = hist[i];
   if (distinct_cus) {
-    // Unique (xcd, hw_id & 0xfff) pairs approximate distinct CUs touched.
+    // Unique (xcd, HW_ID CU/SE bits) pairs approximate distinct CUs touched.
     int uniq = 0;
     for (int i = 0; i < blocks; ++i) {
       uint32_t key = ((hx[i] & 0xf) << 16) | (hh[i] & 0xfff0);
@@ -290,7 +456,7 @@ int xs_health_check(int dev, size_t bytes, unsigned long long* device_sum, unsig
   XS_CHECK(hipMalloc(&buf, n * sizeof(uint32_t)));
   XS_CHECK(hipMalloc(&out, sizeof(unsigned long long)));
   XS_CHECK(hipMemset(out, 0, sizeof(unsigned long long)));
-  int grid = grid_for(dev, 0);
+  int grid = cu_count(dev) * 8;
   k_pattern<<<grid, kBlock>>>(buf, n);
   k_checksum<<<grid, kBlock>>>(buf, n, out);
   XS_CHECK(hipGetLastError());

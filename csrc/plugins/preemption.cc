@@ -1,0 +1,117 @@
+// DefaultPreemption and PreemptionToleration (PostFilter plugins on the
+// shared Evaluator, scheduler/preemption.h).
+//
+// PreemptionToleration reference: pkg/preemptiontoleration/
+// preemption_toleration.go:102-315 and preemption_toleration_policy.go:25-82.
+// A victim candidate (lower priority than the preemptor) is exempt iff its
+// PriorityClass parses and: the preemptor's policy is Never, or preemptor
+// priority < minimum-preemptable-priority (default PC.value+1) and
+// (toleration-seconds < 0, or the victim is not scheduled yet, or it was
+// scheduled less than toleration-seconds ago).
+#include <cstdlib>
+#include <random>
+
+#include "framework/plugin.h"
+#include "scheduler/informers.h"
+#include "scheduler/preemption.h"
+
+namespace xsched {
+namespace {
+
+inline constexpr const char* kAnnMinPreemptable = "preemption-toleration.scheduling.sigs.k8s.io/minimum-preemptable-priority";
+inline constexpr const char* kAnnTolerationSeconds = "preemption-toleration.scheduling.sigs.k8s.io/toleration-seconds";
+
+class DefaultPreemption : public Plugin, public PreemptionPolicy {
+ public:
+  DefaultPreemption(const Json& args, Handle& h, std::string name = "DefaultPreemption")
+      : Plugin(std::move(name), kPostFilter), h_(h), ev_(name_, h, this) {
+    pct_ = static_cast<int>(args["minCandidateNodesPercentage"].as_int(10));
+    abs_ = static_cast<int>(args["minCandidateNodesAbsolute"].as_int(100));
+    rng_.seed(static_cast<uint64_t>(wall_now_us()));
+  }
+
+  std::pair<PostFilterResult, Status> post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m) override {
+    return ev_.preempt(s, p, m);
+  }
+
+  std::pair<int, int> offset_and_num_candidates(int n) override {
+    std::lock_guard<std::mutex> g(rng_mu_);
+    int off = n > 0 ? static_cast<int>(rng_() % static_cast<uint64_t>(n)) : 0;
+    return {off, calculate_num_candidates(n, pct_, abs_)};
+  }
+  bool eligible(const Pod& pod, const Status* nom) override { return default_eligible(h_, pod, nom); }
+  Status select_victims_on_node(CycleState& s, const Pod& preemptor, NodeInfo& ni, const std::vector<PDBPtr>& pdbs,
+                                std::vector<PodPtr>& victims, int& num_violating) override {
+    int32_t prio = preemptor.priority;
+    return select_victims_default(h_, s, preemptor, ni, pdbs, [&](const Pod& p) { return p.priority < prio; }, victims,
+                                 num_violating);
+  }
+
+ protected:
+  Handle& h_;
+  Evaluator ev_;
+  int pct_ = 10, abs_ = 100;
+  std::mutex rng_mu_;
+  std::mt19937_64 rng_;
+};
+
+struct TolerationPolicy {
+  int32_t min_preemptable = 0;
+  int64_t toleration_seconds = 0;
+};
+
+bool parse_policy(const PriorityClass& pc, TolerationPolicy* out) {
+  out->min_preemptable = pc.value + 1;
+  out->toleration_seconds = 0;
+  if (const std::string* v = pc.meta.annotation(kAnnMinPreemptable)) {
+    char* e = nullptr;
+    long long x = std::strtoll(v->c_str(), &e, 10);
+    if (v->empty() || *e || x < INT32_MIN || x > INT32_MAX) return false;
+    out->min_preemptable = static_cast<int32_t>(x);
+  }
+  if (const std::string* v = pc.meta.annotation(kAnnTolerationSeconds)) {
+    char* e = nullptr;
+    long long x = std::strtoll(v->c_str(), &e, 10);
+    if (v->empty() || *e) return false;
+    out->toleration_seconds = x;
+  }
+  return true;
+}
+
+class PreemptionToleration : public DefaultPreemption {
+ public:
+  PreemptionToleration(const Json& args, Handle& h) : DefaultPreemption(args, h, "PreemptionToleration") {}
+
+  // ExemptedFromPreemption (preemption_toleration.go:125-175).
+  bool exempted(const Pod& victim, const Pod& preemptor, MicroTime now) const {
+    if (victim.priority_class_name.empty()) return false;
+    auto pc = h_.informers->priority_class(victim.priority_class_name);
+    if (!pc) return false;  // lister miss: no toleration (the reference surfaces the error)
+    if (preemptor.preemption_policy == "Never") return true;
+    TolerationPolicy pol;
+    if (!parse_policy(*pc, &pol)) return false;
+    if (preemptor.priority >= pol.min_preemptable) return false;
+    if (pol.toleration_seconds < 0) return true;
+    if (victim.scheduled_at == 0) return true;
+    return victim.scheduled_at + pol.toleration_seconds * 1000000 > now;
+  }
+
+  Status select_victims_on_node(CycleState& s, const Pod& preemptor, NodeInfo& ni, const std::vector<PDBPtr>& pdbs,
+                                std::vector<PodPtr>& victims, int& num_violating) override {
+    int32_t prio = preemptor.priority;
+    MicroTime now = wall_now_us();
+    return select_victims_default(
+        h_, s, preemptor, ni, pdbs, [&](const Pod& p) { return p.priority < prio && !exempted(p, preemptor, now); },
+        victims, num_violating);
+  }
+};
+
+PluginRegistrar r1("DefaultPreemption", [](const Json& a, Handle& h) { return std::make_shared<DefaultPreemption>(a, h); });
+PluginRegistrar r2("PreemptionToleration",
+                   [](const Json& a, Handle& h) { return std::make_shared<PreemptionToleration>(a, h); });
+
+}  // namespace
+
+void link_preemption_plugins() {}
+
+}  // namespace xsched

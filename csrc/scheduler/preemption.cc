@@ -1,0 +1,253 @@
+#include "scheduler/preemption.h"
+
+#include <algorithm>
+#include <atomic>
+#include <climits>
+#include <map>
+#include <mutex>
+
+#include "framework/framework.h"
+#include "framework/waiting_pods.h"
+#include "scheduler/informers.h"
+#include "scheduler/metrics.h"
+#include "scheduler/queue.h"
+
+namespace xsched {
+
+int64_t pod_start_time(const Pod& p) { return p.start_time ? p.start_time : wall_now_us(); }
+
+bool more_important_pod(const Pod& a, const Pod& b) {
+  if (a.priority != b.priority) return a.priority > b.priority;
+  return pod_start_time(a) < pod_start_time(b);
+}
+
+void filter_pods_with_pdb_violation(const std::vector<PodPtr>& pods, const std::vector<PDBPtr>& pdbs,
+                                    std::vector<PodPtr>& violating, std::vector<PodPtr>& non_violating) {
+  std::vector<int64_t> allowed(pdbs.size());
+  for (size_t i = 0; i < pdbs.size(); ++i) allowed[i] = pdbs[i]->disruptions_allowed;
+  for (const auto& p : pods) {
+    bool violated = false;
+    if (!p->meta.labels.empty()) {
+      for (size_t i = 0; i < pdbs.size(); ++i) {
+        const auto& pdb = *pdbs[i];
+        if (pdb.meta.ns != p->ns()) continue;
+        // A nil or empty selector matches nothing.
+        if (!pdb.selector.present || (pdb.selector.match_labels.empty() && pdb.selector.exprs.empty())) continue;
+        if (!pdb.selector.matches(p->meta.labels)) continue;
+        if (strmap_get(pdb.disrupted_pods, p->name())) continue;  // already processed by the API server
+        if (--allowed[i] < 0) violated = true;
+      }
+    }
+    (violated ? violating : non_violating).push_back(p);
+  }
+}
+
+Status select_victims_default(Handle& h, CycleState& s, const Pod& preemptor, NodeInfo& ni,
+                              const std::vector<PDBPtr>& pdbs, const std::function<bool(const Pod&)>& may_evict,
+                              std::vector<PodPtr>& victims, int& num_violating) {
+  Framework& fw = *h.framework;
+  std::vector<PodPtr> potential;
+  for (const auto& p : std::vector<PodPtr>(ni.pods)) {
+    if (!may_evict(*p)) continue;
+    potential.push_back(p);
+    ni.remove_pod(p->uid());
+    Status st = fw.run_pre_filter_remove_pod(s, preemptor, p, ni);
+    if (!st.is_success()) return st;
+  }
+  if (potential.empty())
+    return Status::unresolvable("No victims found on node " + ni.name() + " for preemptor pod " + preemptor.name());
+  Status st = fw.run_filter_with_nominated_pods(s, preemptor, ni);
+  if (!st.is_success()) return st;
+  std::sort(potential.begin(), potential.end(),
+            [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*a, *b); });
+  std::vector<PodPtr> violating, non_violating;
+  filter_pods_with_pdb_violation(potential, pdbs, violating, non_violating);
+  auto reprieve = [&](const PodPtr& p) -> std::pair<bool, Status> {
+    ni.add_pod(p);
+    Status ast = fw.run_pre_filter_add_pod(s, preemptor, p, ni);
+    if (!ast.is_success()) return {false, ast};
+    bool fits = fw.run_filter_with_nominated_pods(s, preemptor, ni).is_success();
+    if (!fits) {
+      ni.remove_pod(p->uid());
+      Status rst = fw.run_pre_filter_remove_pod(s, preemptor, p, ni);
+      if (!rst.is_success()) return {false, rst};
+      victims.push_back(p);
+    }
+    return {fits, Status()};
+  };
+  for (const auto& p : violating) {
+    auto [fits, err] = reprieve(p);
+    if (!err.is_success()) return err;
+    if (!fits) ++num_violating;
+  }
+  for (const auto& p : non_violating) {
+    auto [fits, err] = reprieve(p);
+    if (!err.is_success()) return err;
+  }
+  return {};
+}
+
+bool default_eligible(Handle& h, const Pod& pod, const Status* nominated_status) {
+  if (pod.preemption_policy == "Never") return false;
+  if (!pod.nominated_node_name.empty()) {
+    if (nominated_status && nominated_status->code() == Code::UnschedulableAndUnresolvable) return true;
+    if (h.snapshot) {
+      if (auto ni = h.snapshot->get(pod.nominated_node_name)) {
+        for (const auto& p : ni->pods)
+          if (p->terminating() && p->priority < pod.priority) return false;  // victims still terminating
+      }
+    }
+  }
+  return true;
+}
+
+int calculate_num_candidates(int num_nodes, int pct, int min_abs) {
+  int n = num_nodes * pct / 100;
+  if (n < min_abs) n = min_abs;
+  if (n > num_nodes) n = num_nodes;
+  return n;
+}
+
+std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
+                                          const std::vector<PDBPtr>& pdbs, int offset, int num_candidates) {
+  std::vector<Candidate> violating, non_violating;
+  std::mutex mu;
+  std::atomic<bool> stop{false};
+  int n = static_cast<int>(potential.size());
+  h_.parallelizer->until(n, [&](int i) {
+    const NodeInfoPtr& src = potential[(offset + i) % n];
+    auto ni = src->clone();
+    auto st = s.clone();
+    Candidate c;
+    c.node = ni->name();
+    Status vs = policy_->select_victims_on_node(*st, pod, *ni, pdbs, c.victims, c.num_pdb_violations);
+    if (!vs.is_success() || c.victims.empty()) return;
+    std::lock_guard<std::mutex> g(mu);
+    if (c.num_pdb_violations == 0)
+      non_violating.push_back(std::move(c));
+    else
+      violating.push_back(std::move(c));
+    int nv = static_cast<int>(non_violating.size());
+    if (nv > 0 && nv + static_cast<int>(violating.size()) >= num_candidates) stop.store(true);
+  }, &stop);
+  std::vector<Candidate> out = std::move(non_violating);
+  for (auto& c : violating) out.push_back(std::move(c));
+  return out;
+}
+
+std::string Evaluator::pick_one_node(const std::vector<Candidate>& cands) {
+  if (cands.empty()) return {};
+  std::vector<const Candidate*> cur;
+  for (const auto& c : cands) {
+    if (c.victims.empty()) return c.node;  // no preemption needed at all
+    cur.push_back(&c);
+  }
+  auto keep_min = [&](auto key) {
+    int64_t best = LLONG_MAX;
+    for (auto* c : cur) best = std::min<int64_t>(best, key(*c));
+    std::vector<const Candidate*> next;
+    for (auto* c : cur)
+      if (key(*c) == best) next.push_back(c);
+    cur.swap(next);
+  };
+  // victims are sorted most-important first, so victims[0] is the highest priority.
+  keep_min([](const Candidate& c) { return static_cast<int64_t>(c.num_pdb_violations); });
+  if (cur.size() > 1) keep_min([](const Candidate& c) { return static_cast<int64_t>(c.victims[0]->priority); });
+  if (cur.size() > 1)
+    keep_min([](const Candidate& c) {
+      int64_t sum = 0;
+      for (const auto& v : c.victims) sum += static_cast<int64_t>(v->priority) + INT32_MAX + 1;
+      return sum;
+    });
+  if (cur.size() > 1) keep_min([](const Candidate& c) { return static_cast<int64_t>(c.victims.size()); });
+  if (cur.size() > 1) {
+    // The node whose earliest-started victim started latest.
+    const Candidate* best = nullptr;
+    int64_t latest = LLONG_MIN;
+    for (auto* c : cur) {
+      int64_t earliest = LLONG_MAX;
+      for (const auto& v : c->victims) earliest = std::min(earliest, pod_start_time(*v));
+      if (earliest > latest) {
+        latest = earliest;
+        best = c;
+      }
+    }
+    return best->node;
+  }
+  return cur.front()->node;
+}
+
+Status Evaluator::prepare_candidate(const Candidate& c, const Pod& pod) {
+  for (const auto& v : c.victims) {
+    if (auto wp = h_.waiting_pods->get(v->uid())) {
+      wp->reject(plugin_, "preempted");
+    } else {
+      try {
+        h_.client->delete_pod(*v);
+      } catch (const std::exception& e) {
+        std::string msg = e.what();
+        if (msg.find("not found") == std::string::npos) return Status::error(msg);
+      }
+    }
+    h_.client->record_event("Pod", v->ns(), v->name(), "Normal", "Preempted",
+                            "Preempted by " + pod.key() + " on node " + c.node);
+  }
+  if (h_.metrics) h_.metrics->histogram("scheduler_preemption_victims", "").observe(static_cast<double>(c.victims.size()));
+  // Lower-priority pods nominated to this node may no longer fit.
+  if (h_.nominator) {
+    for (const auto& np : h_.nominator->nominated_pods_for_node(c.node)) {
+      if (np->priority >= pod.priority || np->uid() == pod.uid()) continue;
+      h_.nominator->remove(*np);
+      Json patch = Json::object();
+      Json st = Json::object();
+      st.set("nominatedNodeName", Json());
+      patch.set("status", std::move(st));
+      try {
+        h_.client->patch("pods", np->ns(), np->name(), patch);
+      } catch (const std::exception&) {
+      }
+    }
+  }
+  return {};
+}
+
+std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod& pod_in, const NodeStatusMap& m) {
+  if (h_.metrics) h_.metrics->inc("scheduler_preemption_attempts_total", "");
+  // 0) latest version of the pod
+  PodPtr latest = h_.informers ? h_.informers->pod(pod_in.ns(), pod_in.name()) : nullptr;
+  const Pod& pod = latest ? *latest : pod_in;
+  // 1) eligibility
+  const Status* nom = nullptr;
+  auto nit = m.find(pod.nominated_node_name);
+  if (nit != m.end()) nom = &nit->second;
+  if (!policy_->eligible(pod, nom))
+    return {PostFilterResult{}, Status::unschedulable("Pod is not eligible for preemption")};
+  // 2) candidates: nodes where preemption might help
+  if (!h_.snapshot || h_.snapshot->nodes.empty()) return {PostFilterResult{}, Status::error("no nodes available")};
+  std::vector<NodeInfoPtr> potential;
+  for (const auto& ni : h_.snapshot->nodes) {
+    auto it = m.find(ni->name());
+    if (it != m.end() && it->second.code() == Code::UnschedulableAndUnresolvable) continue;
+    potential.push_back(ni);
+  }
+  if (potential.empty())
+    return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +
+                                                      " nodes are available: preemption is not helpful for scheduling.")};
+  std::vector<PDBPtr> pdbs = h_.informers ? h_.informers->pdbs() : std::vector<PDBPtr>{};
+  auto [offset, num] = policy_->offset_and_num_candidates(static_cast<int>(potential.size()));
+  auto cands = dry_run(s, pod, potential, pdbs, offset, num);
+  if (cands.empty())
+    return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +
+                                                      " nodes are available: no preemption victims found.")};
+  // 4) best candidate
+  std::string node = pick_one_node(cands);
+  const Candidate* best = nullptr;
+  for (const auto& c : cands)
+    if (c.node == node) best = &c;
+  // 5) prepare
+  Status st = prepare_candidate(*best, pod);
+  if (!st.is_success()) return {PostFilterResult{}, st};
+  return {PostFilterResult{node}, Status()};
+}
+
+}  // namespace xsched

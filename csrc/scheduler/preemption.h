@@ -1,0 +1,75 @@
+// Preemption evaluator shared by DefaultPreemption, CapacityScheduling and
+// PreemptionToleration.
+//
+// Reference: vendor/k8s.io/kubernetes/pkg/scheduler/framework/preemption/
+// preemption.go (Evaluator.Preempt: PodEligibleToPreemptOthers ->
+// findCandidates (nodes where preemption might help, random offset,
+// numCandidates = max(minAbsolute, n*pct/100)) -> DryRunPreemption (parallel
+// SelectVictimsOnNode on cloned NodeInfo + CycleState) -> SelectCandidate
+// (pickOneNodeForPreemption ordering) -> prepareCandidate (reject waiting
+// victims, delete the others, clear lower-priority nominations)), and
+// DefaultPreemption's SelectVictimsOnNode with the PDB-violation reprieve
+// order (util.MoreImportantPod).
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "framework/plugin.h"
+
+namespace xsched {
+
+// The per-plugin policy (preemption.Interface).
+class PreemptionPolicy {
+ public:
+  virtual ~PreemptionPolicy() = default;
+  virtual std::pair<int, int> offset_and_num_candidates(int num_nodes) = 0;
+  virtual bool eligible(const Pod& pod, const Status* nominated_node_status) = 0;
+  // Selects victims on a cloned NodeInfo (mutated), cloned state.
+  virtual Status select_victims_on_node(CycleState& s, const Pod& preemptor, NodeInfo& ni,
+                                        const std::vector<PDBPtr>& pdbs, std::vector<PodPtr>& victims,
+                                        int& num_violating) = 0;
+};
+
+struct Candidate {
+  std::string node;
+  std::vector<PodPtr> victims;
+  int num_pdb_violations = 0;
+};
+
+class Evaluator {
+ public:
+  Evaluator(std::string plugin_name, Handle& h, PreemptionPolicy* policy)
+      : plugin_(std::move(plugin_name)), h_(h), policy_(policy) {}
+  std::pair<PostFilterResult, Status> preempt(CycleState& s, const Pod& pod, const NodeStatusMap& m);
+
+  // Exposed for tests / other plugins.
+  std::vector<Candidate> dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
+                                 const std::vector<PDBPtr>& pdbs, int offset, int num_candidates);
+  static std::string pick_one_node(const std::vector<Candidate>& cands);
+
+ private:
+  Status prepare_candidate(const Candidate& c, const Pod& pod);
+  std::string plugin_;
+  Handle& h_;
+  PreemptionPolicy* policy_;
+};
+
+// ---- helpers shared by policies ----
+int64_t pod_start_time(const Pod& p);  // status.startTime, else "now"
+bool more_important_pod(const Pod& a, const Pod& b);
+void filter_pods_with_pdb_violation(const std::vector<PodPtr>& pods, const std::vector<PDBPtr>& pdbs,
+                                    std::vector<PodPtr>& violating, std::vector<PodPtr>& non_violating);
+// DefaultPreemption.SelectVictimsOnNode with a pluggable "may this pod be a
+// victim" predicate (lower priority for the default; + quota / toleration
+// rules for the other policies).
+Status select_victims_default(Handle& h, CycleState& s, const Pod& preemptor, NodeInfo& ni,
+                              const std::vector<PDBPtr>& pdbs, const std::function<bool(const Pod&)>& may_evict,
+                              std::vector<PodPtr>& victims, int& num_violating);
+bool default_eligible(Handle& h, const Pod& pod, const Status* nominated_status);
+int calculate_num_candidates(int num_nodes, int pct, int min_abs);
+
+}  // namespace xsched

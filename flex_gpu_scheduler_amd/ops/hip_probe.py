@@ -40,6 +40,10 @@ class HipProbe:
         L.xs_device_props.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.xs_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.xs_hbm_bandwidth_v.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.xs_hbm_bandwidth_xcd.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.xs_xcd_census.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                     ctypes.POINTER(ctypes.c_int)]
         L.xs_health_check.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_ulonglong),
@@ -65,6 +69,41 @@ class HipProbe:
         if rc != 0:
             raise self._err(rc, "hbm_bandwidth")
         return Bandwidth(mode, nbytes, g.value, ms.value, cu_limit)
+
+    @staticmethod
+    def variant(unroll: int = 4, nontemporal: bool = True, blocks_per_cu: int = 8) -> int:
+        return unroll | (0x100 if nontemporal else 0) | (blocks_per_cu << 16)
+
+    def hbm_bandwidth_variant(self, dev: int, nbytes: int, iters: int, mode: str, unroll: int, nontemporal: bool,
+                              blocks_per_cu: int, cu_limit: int = 0) -> Bandwidth:
+        g, ms = ctypes.c_double(), ctypes.c_double()
+        v = self.variant(unroll, nontemporal, blocks_per_cu)
+        rc = self.lib.xs_hbm_bandwidth_v(dev, nbytes, iters, cu_limit, MODES[mode], v, ctypes.byref(g), ctypes.byref(ms))
+        if rc != 0:
+            raise self._err(rc, "hbm_bandwidth_v")
+        return Bandwidth(mode, nbytes, g.value, ms.value, cu_limit)
+
+    def tune(self, dev: int = 0, mode: str = "copy", nbytes: int = 1 << 30, iters: int = 10) -> dict:
+        """Sweep unroll x cache policy x workgroups/CU; return the fastest."""
+        results = []
+        for unroll in (1, 4, 8):
+            for nt in (True, False):
+                for bpc in (4, 8, 16):
+                    bw = self.hbm_bandwidth_variant(dev, nbytes, iters, mode, unroll, nt, bpc)
+                    results.append({"unroll": unroll, "nontemporal": nt, "blocks_per_cu": bpc,
+                                    "GBps": round(bw.gbps, 1)})
+        best = max(results, key=lambda r: r["GBps"])
+        return {"mode": mode, "best": best, "all": results}
+
+    def hbm_bandwidth_xcd(self, dev: int = 0, xcd_mask: int = 0x1, nbytes: int = 1 << 30, iters: int = 10,
+                          mode: str = "read") -> Bandwidth:
+        """HBM bandwidth pulled by the workgroups on the XCDs of `xcd_mask`
+        only — what one CPX (1 XCD) / QPX (2) / DPX (4) partition can stream."""
+        g, ms = ctypes.c_double(), ctypes.c_double()
+        rc = self.lib.xs_hbm_bandwidth_xcd(dev, nbytes, iters, xcd_mask, MODES[mode], ctypes.byref(g), ctypes.byref(ms))
+        if rc != 0:
+            raise self._err(rc, "hbm_bandwidth_xcd")
+        return Bandwidth(mode, nbytes, g.value, ms.value, bin(xcd_mask).count("1") * 32)
 
     def xcd_census(self, dev: int = 0, blocks: int = 4096) -> dict:
         hist = (ctypes.c_int * 8)()

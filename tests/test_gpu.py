@@ -58,10 +58,19 @@ def test_hbm_bandwidth(pr, mode):
     assert bw.gbps > 3000, bw
 
 
-def test_partition_sized_probe_scales_down(pr):
-    full = pr.hbm_bandwidth(0, 512 << 20, iters=5, mode="copy", cu_limit=0)
-    part = pr.hbm_bandwidth(0, 512 << 20, iters=5, mode="copy", cu_limit=32)
-    assert part.gbps < full.gbps
+def test_xcd_pinned_probe_partition_bandwidth(pr):
+    # Work executed only by workgroups on XCD 0 (a CPX partition's CUs) pulls
+    # less HBM bandwidth than all 8 XCDs; the kernel drains either way.
+    if pr.xcd_census(0, 2048)["distinct_xcds"] < 8:
+        pytest.skip("device is already partitioned")
+    one = pr.hbm_bandwidth_xcd(0, 0x01, 512 << 20, iters=5, mode="read")
+    all8 = pr.hbm_bandwidth_xcd(0, 0xFF, 512 << 20, iters=5, mode="read")
+    assert 50 < one.gbps < all8.gbps, (one, all8)
+
+
+def test_tuned_variants_run(pr):
+    r = pr.tune(0, "write", 256 << 20, 3)
+    assert len(r["all"]) == 18 and r["best"]["GBps"] > 1000
 
 
 def test_smoke_entry():
