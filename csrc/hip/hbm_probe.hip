@@ -308,6 +308,14 @@ int xs_hbm_bandwidth_v(int dev, size_t bytes, int iters, int cu_limit, int mode,
   if (n == 0 || mode < 0 || mode > 3) return -1000;
   bytes = n * sizeof(vec4);
   Variant v = decode(variant);
+  if (variant == 0) {
+    // Measured optimum per mode on MI355X (profiles/r1b_probe_sweep.json):
+    // one 16-B access per lane per iteration wins; non-temporal loads help,
+    // plain stores beat nt stores for pure writes; 4-8 workgroups per CU.
+    v.unroll = 1;
+    v.nt = mode != 1;
+    v.bpc = mode == 0 ? 8 : 4;
+  }
   void *a = nullptr, *b = nullptr, *c = nullptr;
   uint32_t* sink = nullptr;
   XS_CHECK(hipMalloc(&a, bytes));

@@ -1,0 +1,367 @@
+// CapacityScheduling: ElasticQuota admission (min guaranteed, max cap) and
+// quota-aware preemption.
+//
+// Reference: pkg/capacityscheduling/capacity_scheduling.go:54-907 and
+// elasticquota.go:26-181. Kept semantics:
+//  * one quota per namespace, the first one listed wins;
+//  * PreFilter snapshots every quota into the CycleState, sums nominated pods
+//    (same namespace with priority >= preemptor into both sums, other
+//    namespaces whose quota is not over min into the global sum) and rejects
+//    when used+inEQ > Max or Σused+global > ΣMin;
+//  * cmp2 compares cpu, memory and only the scalar resources present in the
+//    request (a scalar missing from the bound counts as 0);
+//  * AddPod/RemovePod PreFilter extensions update the snapshot during
+//    preemption dry runs; Reserve/Unreserve update the live quota;
+//  * PostFilter preempts on every node (offset 0, all candidates) with the
+//    quota-aware victim rules of SelectVictimsOnNode.
+// Fixed (Appendix C5): the live quota map is only touched under the plugin
+// lock (the reference reads it unlocked in PreFilter / addElasticQuota).
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <set>
+
+#include "framework/framework.h"
+#include "framework/plugin.h"
+#include "scheduler/informers.h"
+#include "scheduler/preemption.h"
+#include "scheduler/queue.h"
+#include "store/store.h"
+
+namespace xsched {
+namespace {
+
+// cmp2(x1, x2, y): x1 + x2 > y on cpu, memory, or any scalar present in x1.
+bool cmp2(const Res& x1, const Res& x2, const Res& y) {
+  if (x1.get(kCPU) + x2.get(kCPU) > y.get(kCPU)) return true;
+  if (x1.get(kMemory) + x2.get(kMemory) > y.get(kMemory)) return true;
+  for (uint64_t m = x1.mask; m; m &= m - 1) {
+    int id = __builtin_ctzll(m);
+    if (id <= kPods) continue;  // ScalarResources only
+    if (x1.v[id] + x2.get(id) > y.get(id)) return true;
+  }
+  return false;
+}
+bool cmp(const Res& x, const Res& y) { return cmp2(x, Res{}, y); }
+
+struct EQInfo {
+  std::string ns;
+  std::set<std::string> pods;
+  Res min, max, used;
+  bool used_over_min_with(const Res& req) const { return cmp2(req, used, min); }
+  bool used_over_max_with(const Res& req) const { return cmp2(req, used, max); }
+  bool used_over_min() const { return cmp(used, min); }
+  void add_pod(const Pod& p) {
+    if (!pods.insert(p.key()).second) return;
+    used += p.request;
+  }
+  void delete_pod(const Pod& p) {
+    if (!pods.erase(p.key())) return;
+    used -= p.request;
+  }
+};
+using EQInfos = std::map<std::string, EQInfo>;
+
+bool aggregated_used_over_min_with(const EQInfos& infos, const Res& req) {
+  Res used, min;
+  for (const auto& [ns, e] : infos) {
+    used += e.used;
+    min += e.min;
+  }
+  used += req;
+  return cmp(used, min);
+}
+
+struct EQSnapshot : StateData {
+  EQInfos infos;
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<EQSnapshot>(*this); }
+};
+struct CSPreFilterState : StateData {
+  Res pod_req, nominated_in_eq_with_req, nominated_with_req;
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<CSPreFilterState>(*this); }
+};
+constexpr const char* kSnapKey = "CapacityScheduling/ElasticQuotaSnapshot";
+constexpr const char* kStateKey = "PreFilterCapacityScheduling";
+
+class CapacityScheduling : public Plugin, public PreemptionPolicy {
+ public:
+  explicit CapacityScheduling(Handle& h)
+      : Plugin("CapacityScheduling", kPreFilter | kPostFilter | kReserve), h_(h), ev_("CapacityScheduling", h, this) {}
+
+  // ---- informer handlers (capacity_scheduling.go:646-751) ----
+  std::vector<std::string> watched_kinds() const override { return {"elasticquotas", "pods"}; }
+
+  void on_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) override {
+    EventType t = static_cast<EventType>(type);
+    if (kind == "elasticquotas") {
+      auto eq = ElasticQuota::from_json(*obj);
+      std::lock_guard<std::mutex> g(mu_);
+      if (t == EventType::Deleted) {
+        infos_.erase(eq->meta.ns);
+        return;
+      }
+      auto it = infos_.find(eq->meta.ns);
+      if (t == EventType::Added && it != infos_.end()) return;  // first listed wins
+      EQInfo info{eq->meta.ns, {}, eq->min, eq->max, {}};
+      if (it != infos_.end()) {
+        info.pods = it->second.pods;
+        info.used = it->second.used;
+      }
+      infos_[eq->meta.ns] = std::move(info);
+      return;
+    }
+    // pods: FilteringResourceEventHandler over assigned pods.
+    auto np = Pod::from_json(*obj);
+    bool now_assigned = !np->node_name.empty();
+    PodPtr op = old ? Pod::from_json(*old) : nullptr;
+    bool was_assigned = op && !op->node_name.empty();
+    std::lock_guard<std::mutex> g(mu_);
+    if (t == EventType::Deleted) {
+      if (now_assigned) delete_pod_locked(*np);
+      return;
+    }
+    if (now_assigned && !was_assigned) {
+      add_pod_locked(*np);
+    } else if (now_assigned && was_assigned) {
+      if (op->phase == "Succeeded" || op->phase == "Failed") return;
+      if (np->phase != "Running" && np->phase != "Pending") {
+        auto it = infos_.find(np->ns());
+        if (it != infos_.end()) it->second.delete_pod(*np);
+      }
+    } else if (!now_assigned && was_assigned) {
+      delete_pod_locked(*op);
+    }
+  }
+
+  void add_pod_locked(const Pod& p) {
+    auto it = infos_.find(p.ns());
+    if (it == infos_.end()) {
+      auto eq = h_.informers->elastic_quota_for_namespace(p.ns());
+      if (!eq) return;
+      it = infos_.emplace(p.ns(), EQInfo{p.ns(), {}, eq->min, eq->max, {}}).first;
+    }
+    it->second.add_pod(p);
+  }
+  void delete_pod_locked(const Pod& p) {
+    auto it = infos_.find(p.ns());
+    if (it != infos_.end()) it->second.delete_pod(p);
+  }
+
+  // ---- PreFilter (capacity_scheduling.go:201-275) ----
+  Status pre_filter(CycleState& s, const Pod& pod) override {
+    auto snap = std::make_shared<EQSnapshot>();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      snap->infos = infos_;
+    }
+    s.write(kSnapKey, snap);
+    auto pfs = std::make_shared<CSPreFilterState>();
+    pfs->pod_req = pod.request;
+    auto eit = snap->infos.find(pod.ns());
+    if (eit == snap->infos.end()) {
+      s.write(kStateKey, pfs);
+      return {};
+    }
+    Res in_eq, global;
+    if (h_.snapshot && h_.nominator && !h_.nominator->empty()) {
+      for (const auto& ni : h_.snapshot->nodes) {
+        for (const auto& np : h_.nominator->nominated_pods_for_node(ni->name())) {
+          if (np->uid() == pod.uid()) continue;
+          auto it = snap->infos.find(np->ns());
+          if (it == snap->infos.end()) continue;
+          if (np->ns() == pod.ns() && np->priority >= pod.priority) {
+            in_eq += np->request;
+            global += np->request;
+          } else if (np->ns() != pod.ns() && !it->second.used_over_min()) {
+            global += np->request;
+          }
+        }
+      }
+    }
+    in_eq += pod.request;
+    global += pod.request;
+    pfs->nominated_in_eq_with_req = in_eq;
+    pfs->nominated_with_req = global;
+    s.write(kStateKey, pfs);
+    if (eit->second.used_over_max_with(in_eq))
+      return Status::unschedulable("Pod " + pod.key() + " is rejected in PreFilter because ElasticQuota " + pod.ns() +
+                                   " is more than Max");
+    if (aggregated_used_over_min_with(snap->infos, global))
+      return Status::unschedulable("Pod " + pod.key() +
+                                   " is rejected in PreFilter because total ElasticQuota used is more than min");
+    return {};
+  }
+
+  bool has_pre_filter_extensions() const override { return true; }
+  Status add_pod(CycleState& s, const Pod&, const PodPtr& to_add, const NodeInfo&) override {
+    if (auto* snap = s.read_as<EQSnapshot>(kSnapKey)) {
+      auto it = snap->infos.find(to_add->ns());
+      if (it != snap->infos.end()) it->second.add_pod(*to_add);
+    }
+    return {};
+  }
+  Status remove_pod(CycleState& s, const Pod&, const PodPtr& to_remove, const NodeInfo&) override {
+    if (auto* snap = s.read_as<EQSnapshot>(kSnapKey)) {
+      auto it = snap->infos.find(to_remove->ns());
+      if (it != snap->infos.end()) it->second.delete_pod(*to_remove);
+    }
+    return {};
+  }
+
+  // ---- PostFilter: quota-aware preemption ----
+  std::pair<PostFilterResult, Status> post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m) override {
+    cur_state_ = &s;
+    auto r = ev_.preempt(s, p, m);
+    cur_state_ = nullptr;
+    return r;
+  }
+  std::pair<int, int> offset_and_num_candidates(int n) override { return {0, n}; }
+
+  bool eligible(const Pod& pod, const Status* nom) override {
+    if (pod.preemption_policy == "Never") return false;
+    CycleState* s = cur_state_;
+    auto* pfs = s ? s->read_as<CSPreFilterState>(kStateKey) : nullptr;
+    if (!pfs) return false;
+    if (pod.nominated_node_name.empty()) return true;
+    if (nom && nom->code() == Code::UnschedulableAndUnresolvable) return true;
+    auto* snap = s->read_as<EQSnapshot>(kSnapKey);
+    if (!snap) return true;
+    auto ni = h_.snapshot ? h_.snapshot->get(pod.nominated_node_name) : nullptr;
+    if (!ni) return true;
+    auto pit = snap->infos.find(pod.ns());
+    if (pit != snap->infos.end()) {
+      bool more_than_min = pit->second.used_over_min_with(pfs->nominated_in_eq_with_req);
+      for (const auto& p : ni->pods) {
+        if (!p->terminating()) continue;
+        auto it = snap->infos.find(p->ns());
+        if (it == snap->infos.end()) continue;
+        if (p->ns() == pod.ns() && p->priority < pod.priority) return false;
+        if (p->ns() != pod.ns() && !more_than_min && it->second.used_over_min()) return false;
+      }
+    } else {
+      for (const auto& p : ni->pods) {
+        if (snap->infos.count(p->ns())) continue;
+        if (p->terminating() && p->priority < pod.priority) return false;
+      }
+    }
+    return true;
+  }
+
+  // SelectVictimsOnNode (capacity_scheduling.go:465-644).
+  Status select_victims_on_node(CycleState& s, const Pod& pod, NodeInfo& ni, const std::vector<PDBPtr>& pdbs,
+                                std::vector<PodPtr>& victims, int& num_violating) override {
+    auto* snap = s.read_as<EQSnapshot>(kSnapKey);
+    auto* pfs = s.read_as<CSPreFilterState>(kStateKey);
+    if (!snap) return Status::unschedulable("Failed to read elasticQuotaSnapshot from cycleState");
+    if (!pfs) return Status::unschedulable("Failed to read preFilterState from cycleState");
+    Framework& fw = *h_.framework;
+    EQInfos& infos = snap->infos;
+    auto pit = infos.find(pod.ns());
+    bool with_eq = pit != infos.end();
+    auto remove = [&](const PodPtr& p) {
+      ni.remove_pod(p->uid());
+      return fw.run_pre_filter_remove_pod(s, pod, p, ni);
+    };
+    auto add = [&](const PodPtr& p) {
+      ni.add_pod(p);
+      return fw.run_pre_filter_add_pod(s, pod, p, ni);
+    };
+    std::vector<PodPtr> pods = ni.pods;
+    std::sort(pods.begin(), pods.end(), [](const PodPtr& a, const PodPtr& b) { return !more_important_pod(*a, *b); });
+    std::vector<PodPtr> potential;
+    if (with_eq) {
+      bool more_than_min = pit->second.used_over_min_with(pfs->nominated_in_eq_with_req);
+      for (const auto& p : pods) {
+        auto it = infos.find(p->ns());
+        if (it == infos.end()) continue;
+        bool victim = more_than_min ? (p->ns() == pod.ns() && p->priority < pod.priority)
+                                    : (p->ns() != pod.ns() && it->second.used_over_min());
+        if (victim) {
+          potential.push_back(p);
+          Status st = remove(p);
+          if (!st.is_success()) return st;
+        }
+      }
+    } else {
+      for (const auto& p : pods) {
+        if (infos.count(p->ns())) continue;
+        if (p->priority < pod.priority) {
+          potential.push_back(p);
+          Status st = remove(p);
+          if (!st.is_success()) return st;
+        }
+      }
+    }
+    if (potential.empty())
+      return Status::unresolvable("No victims found on node " + ni.name() + " for preemptor pod " + pod.name());
+    Status fst = fw.run_filter_with_nominated_pods(s, pod, ni);
+    if (!fst.is_success()) return fst;
+    pit = infos.find(pod.ns());
+    if (with_eq && (pit->second.used_over_max_with(pfs->pod_req) || aggregated_used_over_min_with(infos, pfs->pod_req)))
+      return Status::unschedulable("global quota max exceeded");
+    std::sort(potential.begin(), potential.end(),
+              [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*a, *b); });
+    std::vector<PodPtr> violating, non_violating;
+    filter_pods_with_pdb_violation(potential, pdbs, violating, non_violating);
+    auto reprieve = [&](const PodPtr& p) -> std::pair<bool, Status> {
+      Status ast = add(p);
+      if (!ast.is_success()) return {false, ast};
+      bool fits = fw.run_filter_with_nominated_pods(s, pod, ni).is_success();
+      if (!fits) {
+        Status rst = remove(p);
+        if (!rst.is_success()) return {false, rst};
+        victims.push_back(p);
+      }
+      auto pit2 = infos.find(pod.ns());
+      if (pit2 != infos.end() && (pit2->second.used_over_max_with(pfs->nominated_in_eq_with_req) ||
+                                  aggregated_used_over_min_with(infos, pfs->nominated_with_req))) {
+        Status rst = remove(p);
+        if (!rst.is_success()) return {false, rst};
+        victims.push_back(p);
+      }
+      return {fits, Status()};
+    };
+    for (const auto& p : violating) {
+      auto [fits, err] = reprieve(p);
+      if (!err.is_success()) return err;
+      if (!fits) ++num_violating;
+    }
+    for (const auto& p : non_violating) {
+      auto [fits, err] = reprieve(p);
+      if (!err.is_success()) return err;
+    }
+    return {};
+  }
+
+  // ---- Reserve / Unreserve (capacity_scheduling.go:340-366) ----
+  Status reserve(CycleState&, const PodPtr& p, const std::string&) override {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = infos_.find(p->ns());
+    if (it != infos_.end()) it->second.add_pod(*p);
+    return {};
+  }
+  void unreserve(CycleState&, const PodPtr& p, const std::string&) override {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = infos_.find(p->ns());
+    if (it != infos_.end()) it->second.delete_pod(*p);
+  }
+
+  std::vector<ClusterEvent> events_to_register() const override {
+    return {{"Pod", kDelete, ""}, {"ElasticQuota", kAll, ""}};
+  }
+
+ private:
+  Handle& h_;
+  Evaluator ev_;
+  std::mutex mu_;
+  EQInfos infos_;
+  CycleState* cur_state_ = nullptr;  // PostFilter runs on the scheduling thread only
+};
+
+PluginRegistrar reg("CapacityScheduling", [](const Json&, Handle& h) { return std::make_shared<CapacityScheduling>(h); });
+
+}  // namespace
+
+void link_capacity_plugin() {}
+
+}  // namespace xsched

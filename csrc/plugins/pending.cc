@@ -1,6 +1,5 @@
 // Link anchors for plugin families not yet split into their own files.
 namespace xsched {
-void link_capacity_plugin() {}
 void link_noderesources_plugin() {}
 void link_trimaran_plugins() {}
 void link_sample_plugins() {}
