@@ -267,7 +267,10 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       return fw.run_pre_filter_add_pod(s, pod, p, ni);
     };
     std::vector<PodPtr> pods = ni.pods;
-    std::sort(pods.begin(), pods.end(), [](const PodPtr& a, const PodPtr& b) { return !more_important_pod(*a, *b); });
+    // Least important first (the reference sorts with !MoreImportantPod, which
+    // is not a strict weak order; the reversed comparator is).
+    std::stable_sort(pods.begin(), pods.end(),
+                     [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*b, *a); });
     std::vector<PodPtr> potential;
     if (with_eq) {
       bool more_than_min = pit->second.used_over_min_with(pfs->nominated_in_eq_with_req);
@@ -299,7 +302,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     pit = infos.find(pod.ns());
     if (with_eq && (pit->second.used_over_max_with(pfs->pod_req) || aggregated_used_over_min_with(infos, pfs->pod_req)))
       return Status::unschedulable("global quota max exceeded");
-    std::sort(potential.begin(), potential.end(),
+    std::stable_sort(potential.begin(), potential.end(),
               [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*a, *b); });
     std::vector<PodPtr> violating, non_violating;
     filter_pods_with_pdb_violation(potential, pdbs, violating, non_violating);

@@ -14,7 +14,15 @@
 
 namespace xsched {
 
-int64_t pod_start_time(const Pod& p) { return p.start_time ? p.start_time : wall_now_us(); }
+// GetPodStartTime falls back to "now" for pods without status.startTime; a
+// clock read per comparison would make sort comparators inconsistent, so use
+// the latest timestamp we know instead (scheduled, created), else "latest".
+int64_t pod_start_time(const Pod& p) {
+  if (p.start_time) return p.start_time;
+  if (p.scheduled_at) return p.scheduled_at;
+  if (p.meta.creation) return p.meta.creation;
+  return INT64_MAX;
+}
 
 bool more_important_pod(const Pod& a, const Pod& b) {
   if (a.priority != b.priority) return a.priority > b.priority;
@@ -58,7 +66,7 @@ Status select_victims_default(Handle& h, CycleState& s, const Pod& preemptor, No
     return Status::unresolvable("No victims found on node " + ni.name() + " for preemptor pod " + preemptor.name());
   Status st = fw.run_filter_with_nominated_pods(s, preemptor, ni);
   if (!st.is_success()) return st;
-  std::sort(potential.begin(), potential.end(),
+  std::stable_sort(potential.begin(), potential.end(),
             [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*a, *b); });
   std::vector<PodPtr> violating, non_violating;
   filter_pods_with_pdb_violation(potential, pdbs, violating, non_violating);
