@@ -284,7 +284,7 @@ Status Framework::run_pre_score(CycleState& s, const Pod& p, const std::vector<N
 }
 
 Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes,
-                            std::vector<NodeScore>& total) {
+                            std::vector<NodeScore>& total, ScoreBreakdown* breakdown) {
   int64_t t0 = s.record_metrics ? handle_.clock->now_us() : 0;
   size_t n = nodes.size();
   total.assign(n, NodeScore{});
@@ -315,6 +315,11 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
       if (!st.is_success()) return Status(Code::Error, "running Normalize on Score plugin " + pl->name() + ": " + st.message());
     }
     int64_t w = scorers_[k].second;
+    if (breakdown) {
+      std::vector<int64_t> v(n);
+      for (size_t i = 0; i < n; ++i) v[i] = per[k][i].score;
+      breakdown->emplace_back(pl->name() + "*" + std::to_string(w), std::move(v));
+    }
     for (size_t i = 0; i < n; ++i) {
       int64_t sc = per[k][i].score;
       if (sc > kMaxNodeScore || sc < kMinNodeScore)

@@ -49,7 +49,10 @@ class Framework {
   std::pair<PostFilterResult, Status> run_post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m);
   Status run_pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes);
   // Weighted sum of all score plugins per node (same order as `nodes`).
-  Status run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes, std::vector<NodeScore>& total);
+  // `breakdown` (optional) receives ("Plugin*weight", normalized scores).
+  using ScoreBreakdown = std::vector<std::pair<std::string, std::vector<int64_t>>>;
+  Status run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes, std::vector<NodeScore>& total,
+                   ScoreBreakdown* breakdown = nullptr);
   Status run_reserve(CycleState& s, const PodPtr& p, const std::string& node);
   void run_unreserve(CycleState& s, const PodPtr& p, const std::string& node);
   // Returns Success, an unschedulable/error status, or Wait (then `on_done`

@@ -1,0 +1,324 @@
+// Trimaran load-aware scoring: TargetLoadPacking and
+// LoadVariationRiskBalancing, fed by load-watcher WatcherMetrics.
+//
+// Reference: pkg/trimaran/{handler.go, targetloadpacking/targetloadpacking.go:
+// 181-294, loadvariationriskbalancing/{loadvariationriskbalancing.go:91-130,
+// analysis.go:48-161, collector.go}} and the load-watcher wire types
+// (vendor/github.com/paypal/load-watcher/pkg/watcher/watcher.go:63-101).
+//
+// Metrics transport (MI355X-native): the control plane (Python telemetry
+// provider: rocm-smi / amd-smi / sysfs, or an external load-watcher service)
+// publishes the WatcherMetrics document as a `loadwatchermetrics` object in
+// the API store; the plugins watch that kind, so Score never does I/O and a
+// refresh is one informer event. GPU metric types ("GPU" utilization %,
+// "GPUMemory" %) extend the CPU/Memory set:
+//  * TargetLoadPacking arg `resourceType: GPU` packs on live MI355X busy %
+//    (capacity = amd.com/gpu, a pod's predicted use = its GPU limit);
+//  * LoadVariationRiskBalancing adds a GPU risk dimension when GPU metrics are
+//    present and the pod requests GPUs (score = min over valid dimensions).
+// Fixed: the pod-assign cache drops fully-stale node entries (the reference's
+// cleanupCache keeps them when every entry is stale, handler.go:114-138).
+#include <cmath>
+#include <cstdlib>
+#include <map>
+#include <shared_mutex>
+#include <unordered_map>
+
+#include "framework/plugin.h"
+#include "store/store.h"
+
+namespace xsched {
+namespace {
+
+constexpr int64_t kReportingIntervalS = 60;   // metricsAgentReportingIntervalSeconds
+constexpr int64_t kCacheCleanupUs = 5LL * 60 * 1000000;
+
+struct Metric {
+  std::string type, op;
+  double value = 0;
+};
+struct WatcherMetrics {
+  bool present = false;
+  int64_t window_end = 0;
+  std::unordered_map<std::string, std::vector<Metric>> nodes;
+};
+
+WatcherMetrics parse_metrics(const Json& j) {
+  WatcherMetrics m;
+  const Json* data = j.get("data");
+  if (!data) return m;
+  const Json* nmm = data->get("NodeMetricsMap");
+  if (!nmm) nmm = data->get("nodeMetricsMap");
+  if (!nmm || !nmm->is_object()) return m;
+  m.present = true;
+  m.window_end = j["window"]["end"].as_int(0);
+  for (const auto& [node, nm] : nmm->members()) {
+    auto& vec = m.nodes[node];
+    for (const auto& x : nm["metrics"].items())
+      vec.push_back(Metric{x["type"].as_string(), x["operator"].as_string(), x["value"].as_double()});
+  }
+  return m;
+}
+
+// Shared state of one Trimaran plugin instance: latest metrics + the
+// recently-bound pod cache.
+class TrimaranBase : public Plugin {
+ public:
+  TrimaranBase(std::string name, Handle& h) : Plugin(std::move(name), kScore), h_(h) {}
+
+  std::vector<std::string> watched_kinds() const override { return {"loadwatchermetrics", "pods"}; }
+
+  void on_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) override {
+    EventType t = static_cast<EventType>(type);
+    if (kind == "loadwatchermetrics") {
+      auto m = std::make_shared<WatcherMetrics>(t == EventType::Deleted ? WatcherMetrics{} : parse_metrics(*obj));
+      std::unique_lock<std::shared_mutex> g(mu_);
+      metrics_ = std::move(m);
+      return;
+    }
+    // Pod-assign cache over assigned pods (handler.go:68-101).
+    auto np = Pod::from_json(*obj);
+    std::unique_lock<std::shared_mutex> g(mu_);
+    if (t == EventType::Deleted) {
+      auto it = assigned_.find(np->node_name);
+      if (it == assigned_.end()) return;
+      auto& v = it->second;
+      for (size_t i = 0; i < v.size(); ++i)
+        if (v[i].second->uid() == np->uid()) {
+          v.erase(v.begin() + static_cast<long>(i));
+          break;
+        }
+      return;
+    }
+    std::string old_node;
+    if (old) old_node = (*old)["spec"]["nodeName"].as_string();
+    if (!np->node_name.empty() && np->node_name != old_node)
+      assigned_[np->node_name].emplace_back(wall_now_us() / 1000000, np);
+  }
+
+  void start() override {
+    timer_ = h_.timers->every(kCacheCleanupUs, [this] { cleanup(); });
+  }
+  void stop() override {
+    if (timer_) h_.timers->cancel(timer_);
+  }
+
+  void cleanup() {
+    std::unique_lock<std::shared_mutex> g(mu_);
+    int64_t now = wall_now_us() / 1000000;
+    for (auto it = assigned_.begin(); it != assigned_.end();) {
+      auto& v = it->second;
+      size_t idx = 0;
+      while (idx < v.size() && v[idx].first + kReportingIntervalS <= now) ++idx;
+      v.erase(v.begin(), v.begin() + static_cast<long>(idx));
+      it = v.empty() ? assigned_.erase(it) : std::next(it);
+    }
+  }
+
+ protected:
+  std::shared_ptr<const WatcherMetrics> metrics() const {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    return metrics_;
+  }
+  // Pods bound to `node` after the metrics window (or within one reporting
+  // interval of its end) are not reflected in the metrics yet.
+  template <typename F>
+  void for_missing(const std::string& node, int64_t window_end, F&& f) const {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    auto it = assigned_.find(node);
+    if (it == assigned_.end()) return;
+    for (const auto& [ts, pod] : it->second)
+      if (ts > window_end || (ts <= window_end && window_end - ts < kReportingIntervalS)) f(*pod);
+  }
+
+  Handle& h_;
+  mutable std::shared_mutex mu_;
+  std::shared_ptr<const WatcherMetrics> metrics_ = std::make_shared<WatcherMetrics>();
+  std::unordered_map<std::string, std::vector<std::pair<int64_t, PodPtr>>> assigned_;
+  uint64_t timer_ = 0;
+};
+
+// --------------------------------------------------------- TargetLoadPacking ----
+class TargetLoadPacking : public TrimaranBase {
+ public:
+  TargetLoadPacking(const Json& args, Handle& h) : TrimaranBase("TargetLoadPacking", h) {
+    target_ = static_cast<double>(args["targetUtilization"].as_int(40));
+    if (target_ <= 0) target_ = 40;
+    const Json& mult = args["defaultRequestsMultiplier"];
+    multiplier_ = mult.is_string() ? std::strtod(mult.as_string().c_str(), nullptr) : mult.as_double(1.5);
+    if (multiplier_ <= 0) multiplier_ = 1.5;
+    const Json& dr = args["defaultRequests"]["cpu"];
+    default_milli_ = dr.is_string() ? Quantity::parse(dr.as_string()).milli_value() : 1000;
+    gpu_mode_ = args["resourceType"].str_or("CPU") == "GPU";
+  }
+
+  // PredictUtilisation (targetloadpacking.go:286-294).
+  int64_t predict(const Container& c) const {
+    if (gpu_mode_) {
+      int gid = gpu_names().gpu_id();
+      return c.limits.has(gid) ? c.limits.get(gid) * 1000 : 0;  // milli-GPUs
+    }
+    if (c.limits.has(kCPU)) return c.limits.get(kCPU);
+    if (c.requests.has(kCPU)) return static_cast<int64_t>(std::llround(static_cast<double>(c.requests.get(kCPU)) * multiplier_));
+    return default_milli_;
+  }
+  int64_t pod_usage(const Pod& p) const {
+    int64_t u = 0;
+    for (const auto& c : p.containers) u += predict(c);
+    if (!gpu_mode_) u += p.overhead.get(kCPU);
+    return u;
+  }
+
+  std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
+    auto m = metrics();
+    if (!m->present) return {kMinNodeScore, {}};
+    auto it = m->nodes.find(ni.name());
+    if (it == m->nodes.end()) return {kMinNodeScore, {}};
+    const char* want = gpu_mode_ ? "GPU" : "CPU";
+    double util = 0;
+    bool found = false;
+    for (const auto& x : it->second)
+      if (x.type == want && (x.op == "AVG" || x.op == "Latest")) {
+        util = x.value;
+        found = true;
+      }
+    if (!found) return {kMinNodeScore, {}};
+    double cap = gpu_mode_ ? static_cast<double>(ni.node->capacity.get(gpu_names().gpu_id()) * 1000)
+                           : static_cast<double>(ni.node->capacity.get(kCPU));
+    double used = util / 100.0 * cap;
+    int64_t missing = 0;
+    for_missing(ni.name(), m->window_end, [&](const Pod& q) { missing += pod_usage(q); });
+    double pred = 0;
+    if (cap != 0) pred = 100.0 * (used + static_cast<double>(pod_usage(p)) + static_cast<double>(missing)) / cap;
+    if (pred > target_) {
+      if (pred > 100) return {kMinNodeScore, {}};
+      return {static_cast<int64_t>(std::llround(target_ * (100 - pred) / (100 - target_))), {}};
+    }
+    return {static_cast<int64_t>(std::llround((100 - target_) * pred / target_ + target_)), {}};
+  }
+
+ private:
+  double target_ = 40, multiplier_ = 1.5;
+  int64_t default_milli_ = 1000;
+  bool gpu_mode_ = false;
+};
+
+// ------------------------------------------------ LoadVariationRiskBalancing ----
+struct ResourceStats {
+  double used_avg = 0, used_std = 0, req = 0, capacity = 0;
+  // computeScore (analysis.go:48-78)
+  double score(double margin, double sensitivity) {
+    if (capacity <= 0) return 0;
+    req = std::max(req, 0.0);
+    used_avg = std::max(std::min(used_avg, capacity), 0.0);
+    used_std = std::max(std::min(used_std, capacity), 0.0);
+    double mu = std::max(std::min((used_avg + req) / capacity, 1.0), 0.0);
+    double sigma = std::max(std::min(used_std / capacity, 1.0), 0.0);
+    if (sensitivity >= 0) sigma = std::pow(sigma, 1.0 / sensitivity);
+    sigma = std::max(std::min(sigma * margin, 1.0), 0.0);
+    return (1.0 - (mu + sigma) / 2.0) * kMaxNodeScore;
+  }
+};
+
+bool resource_data(const std::vector<Metric>& ms, const std::string& type, double* avg, double* sd) {
+  bool valid = false, avg_found = false;
+  *avg = *sd = 0;
+  for (const auto& x : ms) {
+    if (x.type != type) continue;
+    if (x.op == "AVG") {
+      *avg = x.value;
+      avg_found = true;
+    } else if (x.op == "STD") {
+      *sd = x.value;
+    } else if ((x.op.empty() || x.op == "Latest") && !avg_found) {
+      *avg = x.value;
+    }
+    valid = true;
+  }
+  return valid;
+}
+
+class LoadVariationRiskBalancing : public TrimaranBase {
+ public:
+  LoadVariationRiskBalancing(const Json& args, Handle& h) : TrimaranBase("LoadVariationRiskBalancing", h) {
+    margin_ = args["safeVarianceMargin"].as_double(1.0);
+    sensitivity_ = args["safeVarianceSensitivity"].as_double(1.0);
+    if (margin_ < 0) margin_ = 1.0;
+    if (sensitivity_ < 0) sensitivity_ = 1.0;
+  }
+
+  std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
+    auto m = metrics();
+    if (!m->present) return {kMinNodeScore, {}};
+    auto it = m->nodes.find(ni.name());
+    if (it == m->nodes.end()) return {kMinNodeScore, {}};
+    // getResourceRequested: Σ containers, max with init containers (cpu/mem), + overhead.
+    int64_t req_cpu = 0, req_mem = 0;
+    for (const auto& c : p.containers) {
+      req_cpu += c.requests.get(kCPU);
+      req_mem += c.requests.get(kMemory);
+    }
+    for (const auto& c : p.init_containers) {
+      req_cpu = std::max(req_cpu, c.requests.get(kCPU));
+      req_mem = std::max(req_mem, c.requests.get(kMemory));
+    }
+    req_cpu += p.overhead.get(kCPU);
+    req_mem += p.overhead.get(kMemory);
+    double scores[3];
+    bool valid[3] = {false, false, false};
+    double avg, sd;
+    if (resource_data(it->second, "CPU", &avg, &sd)) {
+      ResourceStats rs;
+      rs.capacity = static_cast<double>(ni.node->allocatable.get(kCPU));
+      rs.req = static_cast<double>(req_cpu);
+      rs.used_avg = avg * rs.capacity / 100;
+      rs.used_std = sd * rs.capacity / 100;
+      scores[0] = rs.score(margin_, sensitivity_);
+      valid[0] = true;
+    }
+    if (resource_data(it->second, "Memory", &avg, &sd)) {
+      ResourceStats rs;
+      const double mega = 1.0 / 1024.0 / 1024.0;
+      rs.capacity = static_cast<double>(ni.node->allocatable.get(kMemory)) * mega;
+      rs.req = static_cast<double>(req_mem) * mega;
+      rs.used_avg = avg * rs.capacity / 100;
+      rs.used_std = sd * rs.capacity / 100;
+      scores[1] = rs.score(margin_, sensitivity_);
+      valid[1] = true;
+    }
+    int gid = gpu_names().gpu_id();
+    if (p.limit_sum.get(gid) > 0 && resource_data(it->second, "GPU", &avg, &sd)) {
+      ResourceStats rs;
+      rs.capacity = static_cast<double>(ni.node->allocatable.get(gid));
+      rs.req = static_cast<double>(p.limit_sum.get(gid));
+      rs.used_avg = avg * rs.capacity / 100;
+      rs.used_std = sd * rs.capacity / 100;
+      scores[2] = rs.score(margin_, sensitivity_);
+      valid[2] = true;
+    }
+    int n_valid = int(valid[0]) + int(valid[1]) + int(valid[2]);
+    double total = 0;
+    if (n_valid >= 2) {
+      total = 1e300;
+      for (int i = 0; i < 3; ++i)
+        if (valid[i]) total = std::min(total, scores[i]);
+    } else {
+      for (int i = 0; i < 3; ++i)
+        if (valid[i]) total = std::max(total, scores[i]);
+    }
+    return {static_cast<int64_t>(std::llround(total)), {}};
+  }
+
+ private:
+  double margin_ = 1.0, sensitivity_ = 1.0;
+};
+
+PluginRegistrar r1("TargetLoadPacking", [](const Json& a, Handle& h) { return std::make_shared<TargetLoadPacking>(a, h); });
+PluginRegistrar r2("LoadVariationRiskBalancing",
+                   [](const Json& a, Handle& h) { return std::make_shared<LoadVariationRiskBalancing>(a, h); });
+
+}  // namespace
+
+void link_trimaran_plugins() {}
+
+}  // namespace xsched

@@ -422,6 +422,16 @@ PYBIND11_MODULE(_xsched, m) {
                });
              return out;
            })
+      .def("explain",
+           [](Scheduler& s, py::handle pod) {
+             Json j = json_arg(pod);
+             Json out;
+             {
+               py::gil_scoped_release r;
+               out = s.explain(j);
+             }
+             return to_py(out);
+           })
       .def("metrics_text", [](Scheduler& s) { return s.metrics().expose(); })
       .def("set_trace", [](Scheduler& s, bool on) { s.tracer().enable(on); })
       .def("trace_json", [](Scheduler& s) { return s.tracer().chrome_json(); })

@@ -780,6 +780,61 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   }
 }
 
+Json Scheduler::explain(const Json& pod_obj) {
+  std::lock_guard<std::mutex> g(sched_mu_);
+  Json out = Json::object();
+  auto pod = Pod::from_json(pod_obj);
+  Framework* fw = framework_for(pod->scheduler_name);
+  if (!fw) {
+    out.set("error", Json("no profile for schedulerName " + pod->scheduler_name));
+    return out;
+  }
+  if (pod->uid().empty()) pod->meta.uid = "explain-" + pod->key();
+  cache_->update_snapshot(snapshot_);
+  auto state = std::make_shared<CycleState>();
+  state->write(kPodsToActivateKey, std::make_shared<PodsToActivate>());
+  Diagnosis d;
+  std::vector<NodeInfoPtr> feasible;
+  int saved_start = next_start_node_;
+  Status st = find_nodes_that_fit(*fw, *state, *pod, d, feasible);
+  next_start_node_ = saved_start;
+  out.set("code", Json(code_name(st.code())));
+  out.set("message", Json(st.message()));
+  Json filt = Json::object();
+  for (const auto& [node, s] : d.node_to_status) {
+    Json e = Json::object();
+    e.set("plugin", Json(s.failed_plugin()));
+    e.set("reason", Json(s.message()));
+    filt.set(node, std::move(e));
+  }
+  out.set("filtered", std::move(filt));
+  Json feas = Json::array();
+  for (const auto& ni : feasible) feas.push_back(Json(ni->name()));
+  out.set("feasible", std::move(feas));
+  if (st.is_success() && !feasible.empty() && fw->has(kScore)) {
+    std::vector<NodeScore> scores;
+    Framework::ScoreBreakdown bd;
+    Status ps = fw->run_pre_score(*state, *pod, feasible);
+    if (ps.is_success()) ps = fw->run_score(*state, *pod, feasible, scores, &bd);
+    if (ps.is_success()) {
+      Json sc = Json::object();
+      for (size_t i = 0; i < feasible.size(); ++i) {
+        Json node = Json::object();
+        for (const auto& [plugin, vals] : bd) node.set(plugin, Json(vals[i]));
+        node.set("total", Json(scores[i].score));
+        sc.set(feasible[i]->name(), std::move(node));
+      }
+      out.set("scores", std::move(sc));
+      out.set("selected", Json(select_host(scores)));
+    } else {
+      out.set("score_error", Json(ps.message()));
+    }
+  } else if (feasible.size() == 1) {
+    out.set("selected", Json(feasible[0]->name()));
+  }
+  return out;
+}
+
 void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
                               int64_t cycle, Status permit_status, int64_t wait_start_us,
                               std::shared_ptr<PodsToActivate> to_activate) {

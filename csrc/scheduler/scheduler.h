@@ -109,6 +109,9 @@ class Scheduler {
   // Wait until no pod is in activeQ/backoff, no binding is in flight and no
   // pod waits at Permit, or timeout. Returns true when idle.
   bool wait_idle(int timeout_ms);
+  // Dry-run one scheduling cycle for `pod` (no assume/bind): filter verdicts
+  // per node, per-plugin normalized scores and the host that would be chosen.
+  Json explain(const Json& pod);
 
   SchedulingQueue& queue() { return *queue_; }
   SchedulerCache& cache() { return *cache_; }

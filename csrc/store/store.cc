@@ -69,7 +69,8 @@ ObjectStore::ObjectStore() {
 }
 
 bool ObjectStore::namespaced(const std::string& kind) {
-  return !(kind == "nodes" || kind == "priorityclasses" || kind == "noderesourcetopologies" || kind == "namespaces");
+  return !(kind == "nodes" || kind == "priorityclasses" || kind == "noderesourcetopologies" || kind == "namespaces" ||
+           kind == "loadwatchermetrics");
 }
 
 void ObjectStore::stamp(Json& obj, int64_t rv) {

@@ -125,7 +125,7 @@ def build_hip(verbose: bool = True) -> Path | None:
 def build_tsan(verbose: bool = True) -> Path:
     """Native concurrency stress driver built with -fsanitize=thread (host only)."""
     includes = [str(CSRC)]
-    extra = ["-fsanitize=thread", "-g", "-O1"]
+    extra = ["-fsanitize=thread", "-g", "-O1", "-include", str(CSRC / "tools" / "tsan_compat.h")]
     objs = build_objects(core_sources() + [CSRC / "tools" / "stress_main.cc"], BUILD / "tsan", extra, includes)
     out = BUILD / "xsched_stress_tsan"
     cmd = ["g++", "-fsanitize=thread", "-pthread", *[str(o) for o in objs], "-o", str(out)]
