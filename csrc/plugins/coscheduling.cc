@@ -238,7 +238,12 @@ class Coscheduling : public Plugin {
     if (p->pod_group.empty()) return;
     auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
     if (!pg) return;
-    int32_t scheduled = pg->scheduled + 1;
+    // Deliberate fix: the reference increments the lister's status.scheduled,
+    // which is only written back on a phase change (core.go:220-252), so the
+    // count goes stale after the first member (a gang of 4 sticks at
+    // Scheduling/1). We take the larger of that and the group's assigned
+    // (assumed + bound) pods from the cache.
+    int32_t scheduled = std::max<int32_t>(pg->scheduled + 1, h_.cache->assigned_in_group(p->pg_full_name()));
     std::string phase;
     Json status = Json::object();
     if (scheduled >= pg->min_member) {

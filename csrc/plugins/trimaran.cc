@@ -41,6 +41,11 @@ struct WatcherMetrics {
   bool present = false;
   int64_t window_end = 0;
   std::unordered_map<std::string, std::vector<Metric>> nodes;
+  std::unordered_map<std::string, int64_t> node_end;  // per-node window end (merged views)
+  int64_t end_for(const std::string& node) const {
+    auto it = node_end.find(node);
+    return it == node_end.end() ? window_end : it->second;
+  }
 };
 
 WatcherMetrics parse_metrics(const Json& j) {
@@ -71,9 +76,29 @@ class TrimaranBase : public Plugin {
   void on_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) override {
     EventType t = static_cast<EventType>(type);
     if (kind == "loadwatchermetrics") {
-      auto m = std::make_shared<WatcherMetrics>(t == EventType::Deleted ? WatcherMetrics{} : parse_metrics(*obj));
+      // Several documents may coexist: one cluster-wide document (a
+      // load-watcher service) and/or one per node (our node agents publish
+      // their own window). The view is their union; for a node present in
+      // several, the freshest window wins.
+      const std::string& name = (*obj)["metadata"]["name"].as_string();
       std::unique_lock<std::shared_mutex> g(mu_);
-      metrics_ = std::move(m);
+      if (t == EventType::Deleted)
+        sources_.erase(name);
+      else
+        sources_[name] = std::make_shared<const WatcherMetrics>(parse_metrics(*obj));
+      auto merged = std::make_shared<WatcherMetrics>();
+      for (const auto& [src, wm] : sources_) {
+        if (!wm->present) continue;
+        merged->present = true;
+        merged->window_end = std::max(merged->window_end, wm->window_end);
+        for (const auto& [node, vec] : wm->nodes) {
+          auto it = merged->node_end.find(node);
+          if (it != merged->node_end.end() && it->second >= wm->window_end) continue;
+          merged->nodes[node] = vec;
+          merged->node_end[node] = wm->window_end;
+        }
+      }
+      metrics_ = std::move(merged);
       return;
     }
     // Pod-assign cache over assigned pods (handler.go:68-101).
@@ -134,6 +159,7 @@ class TrimaranBase : public Plugin {
   Handle& h_;
   mutable std::shared_mutex mu_;
   std::shared_ptr<const WatcherMetrics> metrics_ = std::make_shared<WatcherMetrics>();
+  std::map<std::string, std::shared_ptr<const WatcherMetrics>> sources_;
   std::unordered_map<std::string, std::vector<std::pair<int64_t, PodPtr>>> assigned_;
   uint64_t timer_ = 0;
 };
@@ -187,7 +213,7 @@ class TargetLoadPacking : public TrimaranBase {
                            : static_cast<double>(ni.node->capacity.get(kCPU));
     double used = util / 100.0 * cap;
     int64_t missing = 0;
-    for_missing(ni.name(), m->window_end, [&](const Pod& q) { missing += pod_usage(q); });
+    for_missing(ni.name(), m->end_for(ni.name()), [&](const Pod& q) { missing += pod_usage(q); });
     double pred = 0;
     if (cap != 0) pred = 100.0 * (used + static_cast<double>(pod_usage(p)) + static_cast<double>(missing)) / cap;
     if (pred > target_) {

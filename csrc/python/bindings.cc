@@ -8,6 +8,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <map>
+#include <set>
+
 #include "api/types.h"
 #include "common/json.h"
 #include "common/quantity.h"
@@ -176,6 +179,39 @@ PYBIND11_MODULE(_xsched, m) {
     return py::make_tuple(q.milli_value(), q.value(), q.str());
   });
   m.def("canonical_quantity", [](const std::string& s) { return Quantity::parse(s).str(); });
+  m.def("quantity_cmp", [](const std::string& a, const std::string& b) {
+    return Quantity::parse(a).cmp(Quantity::parse(b));
+  });
+  // ResourceList arithmetic (k8s.io/apiserver/pkg/quota/v1 Add/Subtract/Max):
+  // exact Quantity math; a sum keeps the format of the first non-zero operand.
+  m.def("resource_list_op", [](const std::map<std::string, std::string>& a,
+                               const std::map<std::string, std::string>& b, const std::string& op) {
+    std::map<std::string, std::string> out;
+    std::set<std::string> keys;
+    for (const auto& kv : a) keys.insert(kv.first);
+    for (const auto& kv : b) keys.insert(kv.first);
+    for (const auto& k : keys) {
+      auto ia = a.find(k), ib = b.find(k);
+      bool ha = ia != a.end(), hb = ib != b.end();
+      Quantity qa = ha ? Quantity::parse(ia->second) : Quantity();
+      Quantity qb = hb ? Quantity::parse(ib->second) : Quantity();
+      if (op == "max") {
+        out[k] = (!ha || (hb && qb.cmp(qa) > 0) ? qb : qa).str();
+        continue;
+      }
+      if (op != "add" && op != "sub") throw std::invalid_argument("op must be add, sub or max");
+      if (qa.is_zero() && !ha) {
+        qa = Quantity::from_int(0, qb.format());
+      }
+      if (op == "add") {
+        qa.add(qb);
+      } else {
+        qa.sub(qb);
+      }
+      out[k] = qa.str();
+    }
+    return out;
+  });
   m.def("pod_summary", [](py::handle obj) { return pod_summary(json_arg(obj)); });
   m.def("plugin_names", [] {
     register_builtin_plugins();
