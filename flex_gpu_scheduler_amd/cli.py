@@ -1,0 +1,373 @@
+"""Command-line entry points (`python -m flex_gpu_scheduler_amd <command>`).
+
+  scheduler    the scheduler service (reference: cmd/scheduler/main.go:30-51 =
+               kube-scheduler + out-of-tree registry; here every plugin of the
+               suite is registered, fixing SURVEY.md Appendix C9)
+  controller   PodGroup + ElasticQuota controllers (cmd/controller, flags of
+               cmd/controller/app/options.go:39-47)
+  apiserver    the HTTP API server over the native store (envtest analog),
+               with JSON checkpoint/restore of all objects
+  node-agent   MI355X discovery -> Node/NRT/telemetry publisher
+  load-watcher GET /watcher over the published WatcherMetrics (:2020)
+  explain      dry-run one pod against the live cluster and print filter
+               verdicts, per-plugin scores and the chosen node
+  apply        create/replace objects from YAML/JSON files (a tiny kubectl)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import signal
+import socket
+import sys
+import threading
+import time
+from pathlib import Path
+
+log = logging.getLogger("xsched")
+
+
+# ------------------------------------------------------------------ helpers
+def _setup_logging(v: int) -> None:
+    level = logging.WARNING if v <= 0 else logging.INFO if v < 5 else logging.DEBUG
+    logging.basicConfig(level=level, format='{"ts":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s",'
+                                            '"msg":"%(message)s"}')
+
+
+def master_from_kubeconfig(path: str) -> tuple[str, str | None]:
+    """(server URL, bearer token) of the current context of a kubeconfig."""
+    import yaml
+
+    with open(path) as f:
+        kc = yaml.safe_load(f) or {}
+    ctx_name = kc.get("current-context")
+    ctxs = {c["name"]: c.get("context") or {} for c in kc.get("contexts") or []}
+    ctx = ctxs.get(ctx_name) or (next(iter(ctxs.values())) if ctxs else {})
+    clusters = {c["name"]: c.get("cluster") or {} for c in kc.get("clusters") or []}
+    users = {u["name"]: u.get("user") or {} for u in kc.get("users") or []}
+    cluster = clusters.get(ctx.get("cluster")) or (next(iter(clusters.values())) if clusters else {})
+    user = users.get(ctx.get("user")) or (next(iter(users.values())) if users else {})
+    return cluster.get("server", "http://127.0.0.1:6443"), user.get("token")
+
+
+def _client(args):
+    from .control.client import RestClient
+
+    master = getattr(args, "master", None) or getattr(args, "masterUrl", None)
+    token = getattr(args, "token", None)
+    kc = getattr(args, "kubeconfig", None) or getattr(args, "kubeConfig", None)
+    if kc and not master:
+        master, kt = master_from_kubeconfig(kc)
+        token = token or kt
+    if getattr(args, "incluster", False) and not master:
+        host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        master = f"https://{host}:{port}"
+        tok = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+        if os.path.exists(tok):
+            token = Path(tok).read_text().strip()
+    return RestClient(master or "http://127.0.0.1:6443", token=token)
+
+
+def _wait_forever(stop: threading.Event) -> None:
+    def handler(*_):
+        stop.set()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            signal.signal(sig, handler)
+        except ValueError:  # not the main thread
+            pass
+    while not stop.is_set():
+        stop.wait(1.0)
+
+
+def _hostport(s: str, default_port: int) -> tuple[str, int]:
+    if ":" not in s:
+        return s or "127.0.0.1", default_port
+    host, _, port = s.rpartition(":")
+    return host or "127.0.0.1", int(port)
+
+
+def load_objects(path: str) -> list[dict]:
+    import yaml
+
+    text = Path(path).read_text() if path != "-" else sys.stdin.read()
+    docs = [d for d in yaml.safe_load_all(text) if d]
+    out = []
+    for d in docs:
+        if d.get("kind", "").endswith("List") and "items" in d:
+            out.extend(d["items"])
+        else:
+            out.append(d)
+    return out
+
+
+# ---------------------------------------------------------------- commands
+def cmd_apiserver(args) -> int:
+    from . import Store
+    from .control.apiserver import ApiServer
+    from .control.snapshot import restore, snapshot_to_file
+
+    store = Store()
+    if args.load and os.path.exists(args.load):
+        n = restore(store, json.loads(Path(args.load).read_text()))
+        log.info("restored %d objects from %s", n, args.load)
+    host, port = _hostport(args.bind_address, args.port)
+    srv = ApiServer(store, host, port, token=args.token).start()
+    print(json.dumps({"apiserver": srv.url}), flush=True)
+    stop = threading.Event()
+    if args.save and args.save_period > 0:
+        def saver():
+            while not stop.wait(args.save_period):
+                snapshot_to_file(store, args.save)
+        threading.Thread(target=saver, daemon=True).start()
+    _wait_forever(stop)
+    if args.save:
+        snapshot_to_file(store, args.save)
+    srv.stop()
+    return 0
+
+
+def _watcher_addresses(cfg) -> set[str]:
+    out = set()
+    for p in cfg.profiles:
+        for name in ("TargetLoadPacking", "LoadVariationRiskBalancing"):
+            addr = (p.plugin_config.get(name) or {}).get("watcherAddress")
+            if addr:
+                out.add(addr)
+    return out
+
+
+def cmd_scheduler(args) -> int:
+    from .config import load_config
+    from .control.client import LocalClient
+    from .control.httpserve import ServiceHTTP
+    from .control.leaderelection import LeaderElector
+    from .control.remote import RemoteScheduler
+    from .gpu.telemetry import WatcherFetcher
+
+    cfg = load_config(args.config)
+    remote = _client(args)
+    options = {}
+    if args.trace:
+        options["trace"] = True
+    rs = RemoteScheduler(remote, cfg, **options)
+    fetchers = [WatcherFetcher(a, LocalClient(rs.store), name=f"load-watcher-{i}")
+                for i, a in enumerate(sorted(_watcher_addresses(cfg)))]
+    host, port = _hostport(args.metrics_bind_address, 10259)
+    http = ServiceHTTP(host, port)
+    http.add_metrics(rs.scheduler.metrics_text)
+    http.add_route("GET", "/debug/trace", lambda q, b: (200, "application/json", rs.scheduler.trace_json()))
+    http.add_route("POST", "/debug/explain", lambda q, b: (200, "application/json", rs.scheduler.explain(b)))
+    http.add_route("GET", "/debug/stats", lambda q, b: (200, "application/json", {
+        "stats": rs.scheduler.stats(), "queue": rs.scheduler.queue_counts(), "mirror_applied": rs.mirror.applied}))
+    http.start()
+    print(json.dumps({"scheduler": [p.scheduler_name for p in cfg.profiles], "metrics": http.url}), flush=True)
+    stop = threading.Event()
+
+    def lead():
+        for f in fetchers:
+            f.start()
+        rs.start()
+
+    if args.leader_elect or cfg.leader_elect:
+        identity = f"{socket.gethostname()}_{os.getpid()}"
+        le = LeaderElector(remote, args.lock_name or cfg.profiles[0].scheduler_name, args.lock_namespace, identity,
+                           on_started_leading=lead, on_stopped_leading=stop.set)
+        threading.Thread(target=le.run, daemon=True).start()
+        _wait_forever(stop)
+        le.stop()
+    else:
+        lead()
+        _wait_forever(stop)
+    for f in fetchers:
+        f.stop()
+    rs.stop()
+    http.stop()
+    return 0
+
+
+def cmd_controller(args) -> int:
+    from .control.controllers import ControllerManager
+    from .control.leaderelection import LeaderElector
+
+    client = _client(args)
+    stop = threading.Event()
+    mgr = ControllerManager(client, workers=args.workers)
+    if args.enableLeaderElection:
+        identity = f"{socket.gethostname()}_{os.getpid()}"
+        le = LeaderElector(client, "sched-plugins-controller", "kube-system", identity,
+                           on_started_leading=mgr.run, on_stopped_leading=stop.set)
+        threading.Thread(target=le.run, daemon=True).start()
+        _wait_forever(stop)
+        le.stop()
+        # The reference exits when the lease is lost (server.go:107-117).
+    else:
+        mgr.run()
+        _wait_forever(stop)
+    mgr.stop()
+    return 0
+
+
+def cmd_node_agent(args) -> int:
+    from .control.node_agent import NodeAgent, hip_health_fn
+    from .gpu.discovery import discover_host, fake_host
+
+    client = _client(args)
+    if args.fake_gpus:
+        host_fn = lambda: fake_host(args.fake_gpus, args.fake_partition)  # noqa: E731
+    else:
+        host_fn = lambda: discover_host(args.sysfs_root)  # noqa: E731
+    agent = NodeAgent(client, args.node_name or socket.gethostname(), host_fn=host_fn, root=args.sysfs_root,
+                      heartbeat=args.heartbeat, telemetry_period=args.telemetry_period,
+                      publish_metrics=not args.no_telemetry, reserved_cpu=args.reserved_cpu,
+                      reserved_memory_gib=args.reserved_memory_gib,
+                      health_fn=hip_health_fn() if args.health_probe else None).start()
+    print(json.dumps({"node": agent.name, "gpus": len(agent.host.gpus)}), flush=True)
+    stop = threading.Event()
+    _wait_forever(stop)
+    agent.stop()
+    return 0
+
+
+def cmd_load_watcher(args) -> int:
+    from .control.httpserve import ServiceHTTP
+    from .gpu.telemetry import LoadWatcherService
+
+    client = _client(args)
+    host, port = _hostport(args.bind_address, args.port)
+    http = ServiceHTTP(host, port)
+    LoadWatcherService(client, http)
+    http.start()
+    print(json.dumps({"load-watcher": http.url + "/watcher"}), flush=True)
+    stop = threading.Event()
+    _wait_forever(stop)
+    http.stop()
+    return 0
+
+
+def cmd_explain(args) -> int:
+    from .config import load_config
+    from .control.remote import RemoteScheduler
+
+    rs = RemoteScheduler(_client(args), load_config(args.config))
+    rs.mirror.start()
+    rs.mirror.wait_for_sync(30)
+    rs.scheduler.sync_informers(2000)
+    pods = load_objects(args.pod)
+    for p in pods:
+        print(json.dumps(rs.scheduler.explain(p), indent=1 if args.pretty else None))
+    rs.mirror.stop()
+    rs.scheduler.stop()
+    return 0
+
+
+def cmd_apply(args) -> int:
+    from .control.client import is_already_exists
+    from .control.resources import resource
+
+    client = _client(args)
+    for path in args.files:
+        for obj in load_objects(path):
+            kind = resource(obj.get("kind", "")).kind_plural
+            md = obj.setdefault("metadata", {})
+            if args.namespace and resource(kind).namespaced:
+                md.setdefault("namespace", args.namespace)
+            try:
+                client.create(kind, obj)
+                print(f"{kind}/{md.get('name')} created")
+            except Exception as e:  # noqa: BLE001
+                if not is_already_exists(e):
+                    raise
+                cur = client.get(kind, md.get("namespace", ""), md["name"])
+                md["resourceVersion"] = cur["metadata"]["resourceVersion"]
+                client.update(kind, obj)
+                print(f"{kind}/{md.get('name')} configured")
+    return 0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="xsched", description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
+    ap.add_argument("-v", "--v", type=int, default=2, dest="verbosity", help="log verbosity (klog-style)")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def conn(p, reference_flags=False):
+        p.add_argument("--master", help="API server URL")
+        p.add_argument("--kubeconfig", help="kubeconfig path (server + token of the current context)")
+        p.add_argument("--token", help="bearer token")
+        p.add_argument("--incluster", action="store_true", help="use the in-cluster service account")
+        if reference_flags:
+            p.add_argument("--masterUrl", help="alias of --master (reference controller flag)")
+            p.add_argument("--kubeConfig", help="alias of --kubeconfig (reference controller flag)")
+            p.add_argument("--qps", type=float, default=5.0, help="accepted for compatibility")
+            p.add_argument("--burst", type=int, default=10, help="accepted for compatibility")
+
+    p = sub.add_parser("apiserver", help="HTTP API server over the native store")
+    p.add_argument("--bind-address", default="127.0.0.1")
+    p.add_argument("--port", type=int, default=6443)
+    p.add_argument("--token")
+    p.add_argument("--load", help="restore objects from a JSON snapshot at start")
+    p.add_argument("--save", help="write a JSON snapshot on exit (and every --save-period s)")
+    p.add_argument("--save-period", type=float, default=0.0)
+    p.set_defaults(fn=cmd_apiserver)
+
+    p = sub.add_parser("scheduler", help="the scheduler service")
+    conn(p)
+    p.add_argument("--config", help="KubeSchedulerConfiguration YAML (v1beta2/v1beta3)")
+    p.add_argument("--metrics-bind-address", default="127.0.0.1:10259")
+    p.add_argument("--leader-elect", action="store_true")
+    p.add_argument("--lock-name")
+    p.add_argument("--lock-namespace", default="kube-system")
+    p.add_argument("--trace", action="store_true", help="record per-cycle phase traces (/debug/trace)")
+    p.set_defaults(fn=cmd_scheduler)
+
+    p = sub.add_parser("controller", help="PodGroup + ElasticQuota controllers")
+    conn(p, reference_flags=True)
+    p.add_argument("--workers", type=int, default=1)
+    p.add_argument("--enableLeaderElection", action="store_true")
+    p.set_defaults(fn=cmd_controller)
+
+    p = sub.add_parser("node-agent", help="MI355X node agent")
+    conn(p)
+    p.add_argument("--node-name")
+    p.add_argument("--sysfs-root", default="/")
+    p.add_argument("--fake-gpus", type=int, default=0, help="advertise a synthetic node with N GPUs")
+    p.add_argument("--fake-partition", default="SPX")
+    p.add_argument("--heartbeat", type=float, default=10.0)
+    p.add_argument("--telemetry-period", type=float, default=60.0)
+    p.add_argument("--no-telemetry", action="store_true")
+    p.add_argument("--health-probe", action="store_true", help="run the HIP health probe on each GPU")
+    p.add_argument("--reserved-cpu", type=int, default=0)
+    p.add_argument("--reserved-memory-gib", type=int, default=0)
+    p.set_defaults(fn=cmd_node_agent)
+
+    p = sub.add_parser("load-watcher", help="serve GET /watcher")
+    conn(p)
+    p.add_argument("--bind-address", default="127.0.0.1")
+    p.add_argument("--port", type=int, default=2020)
+    p.set_defaults(fn=cmd_load_watcher)
+
+    p = sub.add_parser("explain", help="dry-run pods against the cluster")
+    conn(p)
+    p.add_argument("--config")
+    p.add_argument("--pod", required=True, help="pod YAML/JSON file ('-' = stdin)")
+    p.add_argument("--pretty", action="store_true")
+    p.set_defaults(fn=cmd_explain)
+
+    p = sub.add_parser("apply", help="create or replace objects from files")
+    conn(p)
+    p.add_argument("-f", "--filename", dest="files", action="append", required=True)
+    p.add_argument("-n", "--namespace")
+    p.set_defaults(fn=cmd_apply)
+    return ap
+
+
+def main(argv: list[str] | None = None) -> int:
+    args = build_parser().parse_args(argv)
+    _setup_logging(args.verbosity)
+    return int(args.fn(args) or 0)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
