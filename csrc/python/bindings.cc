@@ -8,6 +8,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <map>
 #include <set>
 
@@ -146,6 +147,17 @@ py::dict node_info_dict(const NodeInfo& ni) {
   return d;
 }
 
+// Python threads currently blocked inside a native wait with the GIL
+// released. At interpreter exit the control plane stops every watcher and
+// waits for this to reach zero: a daemon thread that re-acquires the GIL
+// during finalization is terminated by CPython from inside pybind11's
+// (noexcept) gil_scoped_release destructor, which aborts the process.
+std::atomic<int> g_native_waiters{0};
+struct WaiterGuard {
+  WaiterGuard() { g_native_waiters.fetch_add(1); }
+  ~WaiterGuard() { g_native_waiters.fetch_sub(1); }
+};
+
 void release_scheduler(Scheduler* s) {
   if (PyGILState_Check()) {
     py::gil_scoped_release r;
@@ -224,6 +236,7 @@ PYBIND11_MODULE(_xsched, m) {
     return to_py(x);
   });
   m.def("rfc3339", [](int64_t us) { return format_rfc3339(us); });
+  m.def("native_waiters", [] { return g_native_waiters.load(); });
   m.def("parse_rfc3339", [](const std::string& s) { return parse_rfc3339(s); });
   m.def("set_gpu_names", [](py::dict d) {
     GpuNames& g = gpu_names();
@@ -248,6 +261,7 @@ PYBIND11_MODULE(_xsched, m) {
           [](Watcher& w, int timeout_ms, size_t max) {
             std::vector<WatchEvent> evs;
             {
+              WaiterGuard wg;
               py::gil_scoped_release r;
               evs = w.next(timeout_ms, max);
             }
@@ -262,6 +276,7 @@ PYBIND11_MODULE(_xsched, m) {
           [](Watcher& w, int timeout_ms, size_t max) {
             std::vector<WatchEvent> evs;
             {
+              WaiterGuard wg;
               py::gil_scoped_release r;
               evs = w.next(timeout_ms, max);
             }

@@ -725,6 +725,10 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     handle_failure(*fw, qpi, ast, "SchedulerError", "", cycle, {});
     return;
   }
+  // An assumed pod is accounted on its node; drop its nomination so it is not
+  // counted twice by nominated-pod-aware checks (scheduler.go assume():
+  // DeleteNominatedPodIfExists).
+  if (!nominator_->empty()) nominator_->remove(*assumed);
   // Reserve.
   Status rst = fw->run_reserve(*state, assumed, host);
   if (!rst.is_success()) {

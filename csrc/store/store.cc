@@ -54,7 +54,10 @@ std::vector<WatchEvent> Watcher::next(int timeout_ms, size_t max) {
 }
 
 void Watcher::stop() {
-  stopped_.store(true);
+  {
+    std::lock_guard<std::mutex> g(mu_);  // no lost wake-up against next()
+    stopped_.store(true);
+  }
   cv_.notify_all();
 }
 
@@ -269,6 +272,16 @@ JsonPtr ObjectStore::patch(const std::string& kind, const std::string& ns, const
   auto& km = kinds_[kind];
   auto it = km.find(key_of(namespaced(kind) ? ns : "", name));
   if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
+  // A patch carrying metadata.resourceVersion is a precondition (optimistic
+  // concurrency, as kube-apiserver applies it to merge patches).
+  if (const Json* pmd = merge_patch.get("metadata")) {
+    const Json& prv = (*pmd)["resourceVersion"];
+    if (prv.is_string() && !prv.as_string().empty() &&
+        prv.as_string() != (*it->second.obj)["metadata"]["resourceVersion"].as_string())
+      throw StoreError(409, "Conflict",
+                       "Operation cannot be fulfilled on " + kind + " \"" + name +
+                           "\": the object has been modified; please apply your changes to the latest version and try again");
+  }
   Json obj = *it->second.obj;
   Json saved_md = obj["metadata"];
   obj.merge_patch(merge_patch);

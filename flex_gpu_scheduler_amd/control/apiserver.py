@@ -38,6 +38,7 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any
 from urllib.parse import parse_qs, urlsplit
 
+from .. import _lifecycle
 from .._native import native
 from .resources import RESOURCES, Resource, parse_path, with_type_meta
 from .selectors import combine, field_matcher, label_matcher
@@ -130,11 +131,14 @@ class ApiServer:
         self.token = token
         self.bookmark_interval = bookmark_interval
         self._stopping = threading.Event()
+        self._active: set = set()
+        self._active_lock = threading.Lock()
         self.requests = 0
         handler = type("Handler", (_Handler,), {"api": self})
         self.httpd = ThreadingHTTPServer((host, port), handler)
         self.httpd.daemon_threads = True
         self._thread: threading.Thread | None = None
+        _lifecycle.register(self)
 
     @property
     def address(self) -> tuple[str, int]:
@@ -151,12 +155,28 @@ class ApiServer:
         self._thread.start()
         return self
 
-    def stop(self) -> None:
+    def _wake_watches(self) -> None:
         self._stopping.set()
+        with self._active_lock:
+            active = list(self._active)
+        for w in active:
+            self.store.unwatch(w)
+
+    def shutdown_for_exit(self) -> None:
+        self._wake_watches()
+
+    def stop(self) -> None:
+        self._wake_watches()
         self.httpd.shutdown()
         self.httpd.server_close()
         if self._thread:
             self._thread.join(timeout=5)
+        deadline = time.monotonic() + 5
+        while time.monotonic() < deadline:
+            with self._active_lock:
+                if not self._active:
+                    break
+            time.sleep(0.01)
 
     def __enter__(self):
         return self.start()
@@ -352,6 +372,11 @@ class _Handler(BaseHTTPRequestHandler):
             if getattr(e, "code", 0) != 410:
                 raise
             expired, w = e, None
+        if w is not None:
+            with self.api._active_lock:
+                self.api._active.add(w)
+            if self.api._stopping.is_set():
+                store.unwatch(w)
         self.send_response(200)
         self.send_header("Content-Type", "application/json")
         self.send_header("Transfer-Encoding", "chunked")
@@ -402,3 +427,5 @@ class _Handler(BaseHTTPRequestHandler):
         finally:
             if w is not None:
                 store.unwatch(w)
+                with self.api._active_lock:
+                    self.api._active.discard(w)

@@ -17,6 +17,7 @@ import time
 from typing import Any, Iterable
 from urllib.parse import urlencode, urlsplit
 
+from .. import _lifecycle
 from .resources import RESOURCES, resource, with_type_meta
 from .selectors import combine, field_matcher, label_matcher
 
@@ -80,6 +81,7 @@ class Client:
 class _LocalWatch(WatchStream):
     def __init__(self, store, w):
         self._store, self._w = store, w
+        _lifecycle.register(self, _lifecycle.WATCH, "stop")
 
     def next(self, timeout_ms: int = 0, max: int = 4096) -> list[Event]:  # noqa: A002
         return self._w.next(timeout_ms, max)

@@ -218,7 +218,15 @@ class PodGroupController(_Controller):
         old = pg.get("status") or {}
         if status != old:
             try:
-                self.client.patch("podgroups", ns, name, {"status": merge_patch_between(old, status)})
+                # resourceVersion precondition: the scheduler's PostBind also
+                # writes status.phase; a stale cache copy must not overwrite
+                # a newer phase (the reference patches unconditionally,
+                # podgroup.go:275-289). On 409 the key is requeued.
+                rv = (pg.get("metadata") or {}).get("resourceVersion")
+                patch = {"status": merge_patch_between(old, status)}
+                if rv:
+                    patch["metadata"] = {"resourceVersion": rv}
+                self.client.patch("podgroups", ns, name, patch)
             except Exception as e:  # noqa: BLE001
                 if is_not_found(e):
                     return

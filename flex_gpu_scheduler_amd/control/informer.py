@@ -20,6 +20,7 @@ import threading
 import time
 from typing import Callable
 
+from .. import _lifecycle
 from .client import Client
 from .selectors import label_matcher
 
@@ -51,6 +52,10 @@ class Informer:
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
         self.relists = 0
+        _lifecycle.register(self)
+
+    def shutdown_for_exit(self) -> None:
+        self._stop.set()
 
     # -------------------------------------------------------------- handlers
     def add_event_handler(self, on_add: Callable[[dict], None] | None = None,

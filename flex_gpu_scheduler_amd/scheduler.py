@@ -6,6 +6,7 @@ import json
 from pathlib import Path
 from typing import Any
 
+from . import _lifecycle
 from ._native import native
 from .config import SchedulerConfiguration, load_config
 
@@ -28,6 +29,7 @@ def new_scheduler(store, config: SchedulerConfiguration | dict | str | Path | No
     """
     cfg = config if isinstance(config, SchedulerConfiguration) else load_config(config)
     s = native().Scheduler(store, json.dumps(cfg.to_native(**options)), clock, client)
+    _lifecycle.register(s, _lifecycle.LATE, "stop")
     if start:
         s.start()
     return s
