@@ -195,6 +195,7 @@ namespace {
 Container parse_container(const Json& c) {
   Container out;
   out.name = c["name"].as_string();
+  out.image = c["image"].as_string();
   const Json& res = c["resources"];
   out.limits = Res::from_json(res["limits"]);
   out.requests = Res::from_json(res["requests"]);
@@ -224,6 +225,7 @@ PodAffinityTerm parse_pod_affinity_term(const Json& t) {
   PodAffinityTerm out;
   out.selector = LabelSelector::from_json(t.get("labelSelector"));
   for (const auto& n : t["namespaces"].items()) out.namespaces.push_back(n.as_string());
+  out.namespace_selector = LabelSelector::from_json(t.get("namespaceSelector"));
   out.topology_key = t["topologyKey"].as_string();
   return out;
 }
@@ -345,6 +347,14 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
     parse_pod_affinity(*pa, &p->pod_affinity_required, &p->pod_affinity_preferred);
   if (const Json* paa = spec.path({"affinity", "podAntiAffinity"}))
     parse_pod_affinity(*paa, &p->pod_anti_affinity_required, &p->pod_anti_affinity_preferred);
+  for (const auto& c : spec["topologySpreadConstraints"].items()) {
+    TopologySpreadConstraint tc;
+    tc.max_skew = static_cast<int32_t>(c["maxSkew"].as_int(1));
+    tc.topology_key = c["topologyKey"].as_string();
+    tc.hard = c["whenUnsatisfiable"].str_or("DoNotSchedule") != "ScheduleAnyway";
+    tc.selector = LabelSelector::from_json(c.get("labelSelector"));
+    p->spread_constraints.push_back(std::move(tc));
+  }
   for (const auto& t : spec["tolerations"].items()) {
     Toleration tol;
     tol.key = t["key"].as_string();
@@ -405,6 +415,29 @@ int partitions_for_mode(const std::string& mode) {
   return 0;
 }
 
+bool node_selector_term_matches(const NodeSelectorTerm& t, const Node& n) {
+  if (t.match_expressions.empty() && t.match_fields.empty()) return false;
+  for (const auto& r : t.match_expressions)
+    if (!match_requirement(r, n.meta.labels)) return false;
+  for (const auto& r : t.match_fields) {
+    if (r.key != "metadata.name") return false;
+    StrMap f{{"metadata.name", n.name()}};
+    if (!match_requirement(r, f)) return false;
+  }
+  return true;
+}
+
+bool pod_matches_node_selector_and_affinity(const Pod& p, const Node& n) {
+  for (const auto& kv : p.node_selector) {
+    const std::string* v = n.meta.label(kv.first);
+    if (!v || *v != kv.second) return false;
+  }
+  if (!p.has_required_node_affinity) return true;
+  for (const auto& t : p.required_node_terms)
+    if (node_selector_term_matches(t, n)) return true;
+  return false;
+}
+
 std::shared_ptr<Node> Node::from_json(const Json& obj) {
   auto n = std::make_shared<Node>();
   n->meta = ObjectMeta::from_json(obj);
@@ -416,6 +449,12 @@ std::shared_ptr<Node> Node::from_json(const Json& obj) {
   n->unschedulable = spec["unschedulable"].as_bool(false);
   for (const auto& t : spec["taints"].items()) {
     n->taints.push_back(Taint{t["key"].as_string(), t["value"].as_string(), t["effect"].as_string()});
+  }
+  for (const auto& im : status["images"].items()) {
+    ContainerImage ci;
+    for (const auto& nm : im["names"].items()) ci.names.push_back(nm.as_string());
+    ci.size_bytes = im["sizeBytes"].as_int(0);
+    n->images.push_back(std::move(ci));
   }
   const GpuNames& gn = gpu_names();
   int gid = gn.gpu_id();

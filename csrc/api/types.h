@@ -87,7 +87,7 @@ struct ContainerPort {
 };
 
 struct Container {
-  std::string name;
+  std::string name, image;
   Res requests, limits;
   std::vector<ContainerPort> ports;
 };
@@ -97,7 +97,21 @@ enum class QoS : uint8_t { BestEffort = 0, Burstable = 1, Guaranteed = 2 };
 struct PodAffinityTerm {
   LabelSelector selector;
   std::vector<std::string> namespaces;
+  LabelSelector namespace_selector;  // present => also match namespaces by labels
   std::string topology_key;
+};
+
+// v1.TopologySpreadConstraint (k8s 1.23 fields).
+struct TopologySpreadConstraint {
+  int32_t max_skew = 1;
+  std::string topology_key;
+  bool hard = true;  // whenUnsatisfiable: DoNotSchedule (true) / ScheduleAnyway
+  LabelSelector selector;
+};
+
+struct ContainerImage {
+  std::vector<std::string> names;
+  int64_t size_bytes = 0;
 };
 struct WeightedPodAffinityTerm {
   int32_t weight = 0;
@@ -137,6 +151,7 @@ struct Pod {
   std::vector<Toleration> tolerations;
   std::vector<PodAffinityTerm> pod_affinity_required, pod_anti_affinity_required;
   std::vector<WeightedPodAffinityTerm> pod_affinity_preferred, pod_anti_affinity_preferred;
+  std::vector<TopologySpreadConstraint> spread_constraints;
   MicroTime start_time = 0;
   MicroTime scheduled_at = 0;  // PodScheduled=True lastTransitionTime (0 = not scheduled)
 
@@ -167,6 +182,7 @@ struct Node {
   Res allocatable, capacity;
   bool unschedulable = false;
   std::vector<Taint> taints;
+  std::vector<ContainerImage> images;  // status.images (ImageLocality)
   // MI355X GPU topology as published by the node agent (see flexgpu.cc).
   int gpu_count = 0;
   std::vector<int> gpu_partitions;  // partitions per physical GPU (1 = SPX .. 8 = CPX)
@@ -176,6 +192,11 @@ struct Node {
   static std::shared_ptr<Node> from_json(const Json& obj);
 };
 using NodePtr = std::shared_ptr<Node>;
+
+// nodeSelector + required node affinity (nodeaffinity.GetRequiredNodeAffinity
+// (pod).Match(node)); used by NodeAffinity and PodTopologySpread.
+bool node_selector_term_matches(const NodeSelectorTerm& t, const Node& n);
+bool pod_matches_node_selector_and_affinity(const Pod& p, const Node& n);
 
 struct PodGroup {
   ObjectMeta meta;

@@ -117,6 +117,8 @@ Framework::Framework(const ProfileConfig& cfg, Handle handle) : cfg_(cfg), handl
   auto bd = chain_.find(kBind);
   if (bd == chain_.end() || bd->second.empty())
     throw std::runtime_error("at least one bind plugin is needed for profile " + cfg_.scheduler_name);
+  for (const auto& p : all_)
+    for (const auto& k : p->watched_kinds()) kind_watchers_[k].push_back(p);
 }
 
 Framework::~Framework() = default;
@@ -150,10 +152,10 @@ Status Framework::run_pre_filter(CycleState& s, const Pod& p) {
     for (const auto& pl : it->second) {
       Status st = pl->pre_filter(s, p);
       if (!st.is_success()) {
-        st.with_plugin(pl->name());
+        st.with_plugin(pl->name_ptr());
         if (st.code() == Code::Error) {
           Status e(Code::Error, "running PreFilter plugin \"" + pl->name() + "\": " + st.message());
-          e.with_plugin(pl->name());
+          e.with_plugin(pl->name_ptr());
           record("PreFilter", e, t0, s);
           return e;
         }
@@ -201,10 +203,10 @@ Status Framework::run_filter(CycleState& s, const Pod& p, const NodeInfo& ni) {
     if (st.is_success()) continue;
     if (!st.is_unschedulable()) {
       Status e(Code::Error, "running \"" + pl->name() + "\" filter plugin: " + st.message());
-      e.with_plugin(pl->name());
+      e.with_plugin(pl->name_ptr());
       return e;
     }
-    st.with_plugin(pl->name());
+    st.with_plugin(pl->name_ptr());
     if (!cfg_.run_all_filters) return st;
     if (!failed) {
       merged = st;
@@ -263,10 +265,10 @@ std::pair<PostFilterResult, Status> Framework::run_post_filter(CycleState& s, co
       }
       if (!st.is_unschedulable()) {
         record("PostFilter", st, t0, s);
-        return {PostFilterResult{}, Status(Code::Error, st.message()).with_plugin(pl->name())};
+        return {PostFilterResult{}, Status(Code::Error, st.message()).with_plugin(pl->name_ptr())};
       }
       last = st;
-      last.with_plugin(pl->name());
+      last.with_plugin(pl->name_ptr());
     }
   }
   record("PostFilter", last, t0, s);
@@ -340,7 +342,7 @@ Status Framework::run_reserve(CycleState& s, const PodPtr& p, const std::string&
     if (!st.is_success()) {
       Status e(Code::Error, "running Reserve plugin \"" + pl->name() + "\": " + st.message());
       if (st.is_unschedulable()) e = Status(st.code(), st.message());
-      e.with_plugin(pl->name());
+      e.with_plugin(pl->name_ptr());
       return e;
     }
   }
@@ -362,14 +364,14 @@ Status Framework::run_permit(CycleState& s, const PodPtr& p, const std::string& 
     auto [st, timeout] = pl->permit(s, p, node);
     if (st.is_success()) continue;
     if (st.is_unschedulable()) {
-      st.with_plugin(pl->name());
+      st.with_plugin(pl->name_ptr());
       return st;
     }
     if (st.is_wait()) {
       timeouts[pl->name()] = std::min(std::max<int64_t>(timeout, 0), kMaxPermitTimeoutUs);
       continue;
     }
-    return Status(Code::Error, "running Permit plugin " + pl->name() + ": " + st.message()).with_plugin(pl->name());
+    return Status(Code::Error, "running Permit plugin " + pl->name() + ": " + st.message()).with_plugin(pl->name_ptr());
   }
   if (timeouts.empty()) return {};
   handle_.waiting_pods->add(p, node, timeouts, std::move(on_done));
@@ -419,13 +421,9 @@ std::vector<std::string> Framework::watched_kinds() const {
 }
 
 void Framework::dispatch_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) {
-  for (const auto& p : all_) {
-    for (const auto& k : p->watched_kinds())
-      if (k == kind) {
-        p->on_object_event(kind, type, obj, old);
-        break;
-      }
-  }
+  auto it = kind_watchers_.find(kind);
+  if (it == kind_watchers_.end()) return;
+  for (const auto& p : it->second) p->on_object_event(kind, type, obj, old);
 }
 
 void Framework::start() {

@@ -10,6 +10,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "framework/plugin.h"
@@ -78,6 +79,7 @@ class Framework {
   std::map<std::string, PluginPtr> by_name_;
   std::map<uint32_t, std::vector<PluginPtr>> chain_;
   std::vector<std::pair<PluginPtr, int64_t>> scorers_;
+  std::unordered_map<std::string, std::vector<PluginPtr>> kind_watchers_;
   PluginPtr queue_sort_;
 };
 

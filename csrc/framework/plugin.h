@@ -73,9 +73,11 @@ struct Handle {
 
 class Plugin {
  public:
-  explicit Plugin(std::string name, uint32_t points) : name_(std::move(name)), points_(points) {}
+  explicit Plugin(std::string name, uint32_t points)
+      : name_(std::move(name)), name_ptr_(std::make_shared<const std::string>(name_)), points_(points) {}
   virtual ~Plugin() = default;
   const std::string& name() const { return name_; }
+  const std::shared_ptr<const std::string>& name_ptr() const { return name_ptr_; }
   uint32_t points() const { return points_; }
 
   // QueueSort
@@ -123,6 +125,7 @@ class Plugin {
 
  protected:
   std::string name_;
+  std::shared_ptr<const std::string> name_ptr_;
   uint32_t points_;
 };
 using PluginPtr = std::shared_ptr<Plugin>;

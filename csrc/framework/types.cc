@@ -16,35 +16,60 @@ const char* code_name(Code c) {
   return "Unknown";
 }
 
+const std::vector<std::string>& Status::reasons() const {
+  static const std::vector<std::string> kNone;
+  return reasons_ ? *reasons_ : kNone;
+}
+
+const std::string& Status::failed_plugin() const {
+  static const std::string kNone;
+  return plugin_ ? *plugin_ : kNone;
+}
+
 std::string Status::message() const {
   std::string s;
-  for (size_t i = 0; i < reasons_.size(); ++i) {
+  if (!reasons_) return s;
+  for (size_t i = 0; i < reasons_->size(); ++i) {
     if (i) s += ", ";
-    s += reasons_[i];
+    s += (*reasons_)[i];
   }
   return s;
 }
 
 // ----------------------------------------------------------- CycleState ----
-std::shared_ptr<StateData> CycleState::read(const std::string& key) const {
+uint64_t CycleState::next_version() {
+  static std::atomic<uint64_t> counter{1};
+  return counter.fetch_add(1, std::memory_order_relaxed);
+}
+
+std::shared_ptr<StateData> CycleState::read(std::string_view key) const {
   std::lock_guard<std::mutex> g(mu_);
   for (const auto& kv : kv_)
     if (kv.first == key) return kv.second;
   return nullptr;
 }
 
-void CycleState::write(const std::string& key, std::shared_ptr<StateData> v) {
+StateData* CycleState::read_raw(std::string_view key) const {
   std::lock_guard<std::mutex> g(mu_);
+  for (const auto& kv : kv_)
+    if (kv.first == key) return kv.second.get();
+  return nullptr;
+}
+
+void CycleState::write(std::string_view key, std::shared_ptr<StateData> v) {
+  std::lock_guard<std::mutex> g(mu_);
+  version_.store(next_version(), std::memory_order_release);
   for (auto& kv : kv_)
     if (kv.first == key) {
       kv.second = std::move(v);
       return;
     }
-  kv_.emplace_back(key, std::move(v));
+  kv_.emplace_back(std::string(key), std::move(v));
 }
 
-void CycleState::erase(const std::string& key) {
+void CycleState::erase(std::string_view key) {
   std::lock_guard<std::mutex> g(mu_);
+  version_.store(next_version(), std::memory_order_release);
   kv_.erase(std::remove_if(kv_.begin(), kv_.end(), [&](const auto& kv) { return kv.first == key; }), kv_.end());
 }
 
@@ -72,6 +97,54 @@ void GpuLedger::init(const Node& n) {
   for (int g = 0; g < gpu_count; ++g) offset[g + 1] = offset[g] + std::max(1, parts[g]);
   monopoly.assign(gpu_count, 0);
   slots.assign(offset[gpu_count], Slot{});
+  free.assign(gpu_count, GpuFree{});
+  tot_whole = tot_xcds = 0;
+  tot_mem = 0;
+  std::fill(std::begin(zone_gpus), std::end(zone_gpus), 0);
+  std::fill(std::begin(zone_whole), std::end(zone_whole), 0);
+  std::fill(std::begin(zone_xcds), std::end(zone_xcds), 0);
+  std::fill(std::begin(zone_mem), std::end(zone_mem), 0);
+  for (int g = 0; g < gpu_count; ++g) {
+    if (numa[g] >= 0 && numa[g] < kMaxZones) ++zone_gpus[numa[g]];
+    refresh(g);
+  }
+}
+
+GpuLedger::GpuFree GpuLedger::compute(int g) const {
+  GpuFree f;
+  if (monopoly[g] > 0) return f;
+  int xpp = xcds_per_part(g);
+  int64_t pm = part_mem(g);
+  bool untouched = true;
+  for (int s = offset[g]; s < offset[g + 1]; ++s) {
+    const Slot& sl = slots[s];
+    if (sl.exclusive > 0 || sl.used_mem > 0 || sl.mem_pods > 0) untouched = false;
+    if (sl.exclusive == 0 && sl.used_mem == 0 && sl.mem_pods == 0) {
+      ++f.free_slots;
+      f.xcds += xpp;
+    }
+    if (sl.exclusive == 0) {
+      f.mem += pm - sl.used_mem;
+      f.max_slot_mem = std::max(f.max_slot_mem, pm - sl.used_mem);
+    }
+  }
+  f.whole = parts[g] == 1 && untouched ? 1 : 0;
+  return f;
+}
+
+void GpuLedger::refresh(int g) {
+  GpuFree nf = compute(g);
+  GpuFree& of = free[g];
+  tot_whole += nf.whole - of.whole;
+  tot_xcds += nf.xcds - of.xcds;
+  tot_mem += nf.mem - of.mem;
+  int z = numa[g];
+  if (z >= 0 && z < kMaxZones) {
+    zone_whole[z] += nf.whole - of.whole;
+    zone_xcds[z] += nf.xcds - of.xcds;
+    zone_mem[z] += nf.mem - of.mem;
+  }
+  of = nf;
 }
 
 void GpuLedger::apply(const GpuAssignment& a, int sign) {
@@ -79,11 +152,17 @@ void GpuLedger::apply(const GpuAssignment& a, int sign) {
   switch (a.kind) {
     case GpuAssignment::Kind::WholeGpu:
       for (int g : a.gpus)
-        if (g >= 0 && g < gpu_count) monopoly[g] += sign;  // bounds-checked (Appendix C2)
+        if (g >= 0 && g < gpu_count) {  // bounds-checked (Appendix C2)
+          monopoly[g] += sign;
+          refresh(g);
+        }
       break;
     case GpuAssignment::Kind::Partition:
       for (auto [g, p] : a.partitions)
-        if (g >= 0 && g < gpu_count && p >= 0 && p < parts[g]) slots[offset[g] + p].exclusive += sign;
+        if (g >= 0 && g < gpu_count && p >= 0 && p < parts[g]) {
+          slots[offset[g] + p].exclusive += sign;
+          refresh(g);
+        }
       break;
     case GpuAssignment::Kind::Memory: {
       int g = a.gpus.empty() ? -1 : a.gpus[0];
@@ -93,6 +172,7 @@ void GpuLedger::apply(const GpuAssignment& a, int sign) {
         Slot& s = slots[offset[g] + p];
         s.used_mem += sign * a.memory;
         s.mem_pods += sign;
+        refresh(g);
       }
       break;
     }
@@ -111,33 +191,6 @@ bool GpuLedger::slot_free(int g, int p) const {
   if (monopoly[g] > 0) return false;
   const Slot& s = slots[offset[g] + p];
   return s.exclusive == 0 && s.used_mem == 0 && s.mem_pods == 0;
-}
-
-int GpuLedger::free_gpus() const {
-  int n = 0;
-  for (int g = 0; g < gpu_count; ++g) n += whole_gpu_free(g) ? 1 : 0;
-  return n;
-}
-
-int64_t GpuLedger::free_memory() const {
-  int64_t free = 0;
-  for (int g = 0; g < gpu_count; ++g) {
-    if (monopoly[g] > 0) continue;
-    int64_t pm = part_mem(g);
-    for (int s = offset[g]; s < offset[g + 1]; ++s)
-      if (slots[s].exclusive == 0) free += pm - slots[s].used_mem;
-  }
-  return free;
-}
-
-int GpuLedger::free_xcds() const {
-  int n = 0;
-  for (int g = 0; g < gpu_count; ++g) {
-    if (monopoly[g] > 0) continue;
-    for (int p = 0; p < parts[g]; ++p)
-      if (slot_free(g, p)) n += xcds_per_part(g);
-  }
-  return n;
 }
 
 // ------------------------------------------------------------- NodeInfo ----

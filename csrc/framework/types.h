@@ -6,6 +6,7 @@
 // QueuedPodInfo, ClusterEvent)} as used by the reference's plugins.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <map>
@@ -13,6 +14,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -25,12 +27,17 @@ namespace xsched {
 enum class Code : uint8_t { Success = 0, Error, Unschedulable, UnschedulableAndUnresolvable, Wait, Skip };
 const char* code_name(Code c);
 
+// Copies are cheap (two refcounts): Filter returns a Status per node per
+// plugin and the diagnosis keeps one per node, so failure reasons are shared,
+// not re-allocated. Plugins keep their fixed failure statuses prebuilt.
 class Status {
  public:
   Status() = default;
   explicit Status(Code c) : code_(c) {}
-  Status(Code c, std::string reason) : code_(c) { reasons_.push_back(std::move(reason)); }
-  Status(Code c, std::vector<std::string> reasons) : code_(c), reasons_(std::move(reasons)) {}
+  Status(Code c, std::string reason)
+      : code_(c), reasons_(std::make_shared<const std::vector<std::string>>(1, std::move(reason))) {}
+  Status(Code c, std::vector<std::string> reasons)
+      : code_(c), reasons_(std::make_shared<const std::vector<std::string>>(std::move(reasons))) {}
   static Status ok() { return Status(); }
   static Status error(std::string r) { return Status(Code::Error, std::move(r)); }
   static Status unschedulable(std::string r) { return Status(Code::Unschedulable, std::move(r)); }
@@ -43,18 +50,22 @@ class Status {
   bool is_unschedulable() const {
     return code_ == Code::Unschedulable || code_ == Code::UnschedulableAndUnresolvable;
   }
-  const std::vector<std::string>& reasons() const { return reasons_; }
+  const std::vector<std::string>& reasons() const;
   std::string message() const;
-  const std::string& failed_plugin() const { return plugin_; }
+  const std::string& failed_plugin() const;
   Status& with_plugin(std::string p) {
+    plugin_ = std::make_shared<const std::string>(std::move(p));
+    return *this;
+  }
+  Status& with_plugin(std::shared_ptr<const std::string> p) {
     plugin_ = std::move(p);
     return *this;
   }
 
  private:
   Code code_ = Code::Success;
-  std::vector<std::string> reasons_;
-  std::string plugin_;
+  std::shared_ptr<const std::vector<std::string>> reasons_;
+  std::shared_ptr<const std::string> plugin_;
 };
 
 // --------------------------------------------------------- CycleState ----
@@ -74,19 +85,36 @@ inline constexpr const char* kPodsToActivateKey = "kubernetes.io/pods-to-activat
 
 class CycleState {
  public:
-  std::shared_ptr<StateData> read(const std::string& key) const;
+  CycleState() : version_(next_version()) {}
+  std::shared_ptr<StateData> read(std::string_view key) const;
+  StateData* read_raw(std::string_view key) const;
+  // Filter/Score run a plugin once per node on up to 16 threads against the
+  // same CycleState; a per-thread memo (invalidated by any write, since every
+  // write takes a fresh global version) turns the repeated lookup into two
+  // loads instead of a mutex + refcount round-trip per node.
   template <typename T>
-  T* read_as(const std::string& key) const {
-    return dynamic_cast<T*>(read(key).get());
+  T* read_as(std::string_view key) const {
+    thread_local uint64_t memo_version = 0;
+    thread_local std::string memo_key;
+    thread_local T* memo = nullptr;
+    uint64_t v = version_.load(std::memory_order_acquire);
+    if (memo_version == v && memo_key == key) return memo;
+    T* r = dynamic_cast<T*>(read_raw(key));
+    memo_version = v;
+    memo_key.assign(key.data(), key.size());
+    memo = r;
+    return r;
   }
-  void write(const std::string& key, std::shared_ptr<StateData> v);
-  void erase(const std::string& key);
+  void write(std::string_view key, std::shared_ptr<StateData> v);
+  void erase(std::string_view key);
   std::shared_ptr<CycleState> clone() const;
   bool record_metrics = false;
   bool skip_filter_plugins_mark = false;
 
  private:
+  static uint64_t next_version();
   mutable std::mutex mu_;
+  std::atomic<uint64_t> version_;
   std::vector<std::pair<std::string, std::shared_ptr<StateData>>> kv_;
 };
 using CycleStatePtr = std::shared_ptr<CycleState>;
@@ -110,6 +138,22 @@ struct GpuLedger {
   std::vector<int> numa;
   std::vector<Slot> slots;
 
+  // Derived per-GPU availability, kept current by init()/apply() so Filter
+  // and Score read O(#GPUs) or O(1) aggregates instead of walking slots.
+  struct GpuFree {
+    int whole = 0;         // 1 if an untouched SPX GPU
+    int free_slots = 0;    // partitions with no owner and no memory use
+    int xcds = 0;          // XCDs in those partitions
+    int64_t mem = 0;       // free memory over non-exclusive partitions
+    int64_t max_slot_mem = -1;  // largest free memory of one non-exclusive partition (-1: none)
+  };
+  static constexpr int kMaxZones = 64;
+  std::vector<GpuFree> free;
+  int tot_whole = 0, tot_xcds = 0;
+  int64_t tot_mem = 0;
+  int zone_gpus[kMaxZones] = {}, zone_whole[kMaxZones] = {}, zone_xcds[kMaxZones] = {};
+  int64_t zone_mem[kMaxZones] = {};
+
   void init(const Node& n);
   void apply(const GpuAssignment& a, int sign);
   int64_t part_mem(int g) const { return parts[g] > 0 ? mem_per_gpu / parts[g] : 0; }
@@ -117,11 +161,15 @@ struct GpuLedger {
   bool gpu_untouched(int g) const;      // no owner and no memory use on any partition
   // A whole-GPU claim needs an untouched GPU in SPX mode: on a partitioned
   // GPU the container would see 2/4/8 separate devices, not one MI355X.
-  bool whole_gpu_free(int g) const { return parts[g] == 1 && gpu_untouched(g); }
+  bool whole_gpu_free(int g) const { return free[g].whole != 0; }
   bool slot_free(int g, int p) const;   // exclusive-free and no memory use
-  int free_gpus() const;                // GPUScore (gpu_node.go:179-187): free whole (SPX) GPUs
-  int64_t free_memory() const;          // MemScore (gpu_node.go:189-199)
-  int free_xcds() const;
+  int free_gpus() const { return tot_whole; }  // GPUScore (gpu_node.go:179-187): free whole (SPX) GPUs
+  int64_t free_memory() const { return tot_mem; }  // MemScore (gpu_node.go:189-199)
+  int free_xcds() const { return tot_xcds; }
+
+ private:
+  GpuFree compute(int g) const;
+  void refresh(int g);
 };
 
 // ------------------------------------------------------------ NodeInfo ----

@@ -89,8 +89,7 @@ Placement place_xcd(const GpuLedger& L, int64_t x, int* waste_out = nullptr) {
     int xpp = L.xcds_per_part(g);
     if (xpp <= 0) continue;
     int need = static_cast<int>((x + xpp - 1) / xpp);
-    int free = 0;
-    for (int p = 0; p < L.parts[g]; ++p) free += L.slot_free(g, p) ? 1 : 0;
+    int free = L.free[g].free_slots;
     if (free < need) continue;
     int free_x = free * xpp;
     int waste = xcd_waste(L, g, x);
@@ -190,42 +189,42 @@ class FlexGPU : public Plugin {
     int kid = d.kind == Demand::Gpu ? gid : d.kind == Demand::Xcd ? gn.xcd_id() : gn.memory_id();
     if (!ni.allocatable.has(gid) || !ni.allocatable.has(kid)) return Status::unresolvable("unknown resource type");
     // Node-level sum check (flex_gpu.go:82-98).
-    if (ni.requested.get(kid) + d.amount > ni.allocatable.get(kid))
-      return Status::unschedulable("insufficient resource " + ResourceRegistry::get().name(kid));
-    if (!fits(ni.gpu, d)) return Status::unschedulable("no fit indexes resource " + ResourceRegistry::get().name(kid));
+    if (ni.requested.get(kid) + d.amount > ni.allocatable.get(kid)) return failure(kid, false);
+    if (!fits(ni.gpu, d)) return failure(kid, true);
     return {};
+  }
+
+  // Prebuilt per resource id (Filter fails on most nodes of a busy cluster).
+  static Status failure(int kid, bool no_fit) {
+    thread_local std::unordered_map<int, std::pair<Status, Status>> memo;
+    auto it = memo.find(kid);
+    if (it == memo.end()) {
+      const std::string n = ResourceRegistry::get().name(kid);
+      it = memo.emplace(kid, std::make_pair(Status::unschedulable("insufficient resource " + n),
+                                            Status::unschedulable("no fit indexes resource " + n))).first;
+    }
+    return no_fit ? it->second.second : it->second.first;
   }
 
   // Allocation-free feasibility check (Filter runs per node per pod; the
   // concrete placement is only materialized in Reserve).
   static bool fits(const GpuLedger& L, const Demand& d) {
     switch (d.kind) {
-      case Demand::Gpu: {
-        int64_t need = d.amount > 0 ? d.amount : 1, free = 0;
-        for (int g = 0; g < L.gpu_count && free < need; ++g) free += L.whole_gpu_free(g) ? 1 : 0;
-        return free >= need;
-      }
+      case Demand::Gpu:
+        return L.free_gpus() >= (d.amount > 0 ? d.amount : 1);
       case Demand::Xcd: {
-        if (d.amount <= 0) return false;
+        if (d.amount <= 0 || L.free_xcds() < d.amount) return false;
         for (int g = 0; g < L.gpu_count; ++g) {
-          if (L.monopoly[g] > 0) continue;
           int xpp = L.xcds_per_part(g);
           if (xpp <= 0) continue;
-          int need = static_cast<int>((d.amount + xpp - 1) / xpp), free = 0;
-          for (int p = 0; p < L.parts[g] && free < need; ++p) free += L.slot_free(g, p) ? 1 : 0;
-          if (free >= need) return true;
+          if (L.free[g].free_slots >= static_cast<int>((d.amount + xpp - 1) / xpp)) return true;
         }
         return false;
       }
       case Demand::Memory: {
-        for (int g = 0; g < L.gpu_count; ++g) {
-          if (L.monopoly[g] > 0) continue;
-          int64_t cap = L.part_mem(g);
-          for (int p = 0; p < L.parts[g]; ++p) {
-            const auto& s = L.slots[L.offset[g] + p];
-            if (s.exclusive == 0 && cap - s.used_mem >= d.amount) return true;
-          }
-        }
+        if (L.free_memory() < d.amount) return false;
+        for (int g = 0; g < L.gpu_count; ++g)
+          if (L.free[g].max_slot_mem >= d.amount) return true;
         return false;
       }
       default: return false;

@@ -113,8 +113,10 @@ class NodeResourcesFit : public Plugin {
   }
 
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
-    std::vector<std::string> reasons;
-    if (ni.num_pods() + 1 > ni.allocatable.get(kPods) && ni.allocatable.has(kPods)) reasons.push_back("Too many pods");
+    // Failures are encoded as a resource bitmask (bit kPods = "Too many
+    // pods") and their Status is built once per distinct mask per thread.
+    uint64_t fail = 0;
+    if (ni.num_pods() + 1 > ni.allocatable.get(kPods) && ni.allocatable.has(kPods)) fail |= 1ull << kPods;
     const Res& req = p.request;
     for (uint64_t m = req.mask; m; m &= m - 1) {
       int i = __builtin_ctzll(m);
@@ -123,10 +125,17 @@ class NodeResourcesFit : public Plugin {
       if (want == 0) continue;
       if (i > kPods && ignored(i)) continue;
       int64_t free = ni.allocatable.get(i) - ni.requested.get(i);
-      if (want > free) reasons.push_back("Insufficient " + ResourceRegistry::get().name(i));
+      if (want > free) fail |= 1ull << i;
     }
-    if (reasons.empty()) return {};
-    return Status(Code::Unschedulable, std::move(reasons));
+    if (!fail) return {};
+    thread_local std::unordered_map<uint64_t, Status> memo;
+    auto it = memo.find(fail);
+    if (it != memo.end()) return it->second;
+    std::vector<std::string> reasons;
+    if (fail & (1ull << kPods)) reasons.push_back("Too many pods");
+    for (uint64_t m = fail & ~(1ull << kPods); m; m &= m - 1)
+      reasons.push_back("Insufficient " + ResourceRegistry::get().name(__builtin_ctzll(m)));
+    return memo.emplace(fail, Status(Code::Unschedulable, std::move(reasons))).first->second;
   }
 
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
@@ -243,17 +252,7 @@ class TaintToleration : public Plugin {
 };
 
 // ---------------------------------------------------------- NodeAffinity ----
-bool term_matches(const NodeSelectorTerm& t, const Node& n) {
-  if (t.match_expressions.empty() && t.match_fields.empty()) return false;
-  for (const auto& r : t.match_expressions)
-    if (!match_requirement(r, n.meta.labels)) return false;
-  for (const auto& r : t.match_fields) {
-    if (r.key != "metadata.name") return false;
-    StrMap f{{"metadata.name", n.name()}};
-    if (!match_requirement(r, f)) return false;
-  }
-  return true;
-}
+bool term_matches(const NodeSelectorTerm& t, const Node& n) { return node_selector_term_matches(t, n); }
 
 class NodeAffinity : public Plugin {
  public:
@@ -275,16 +274,7 @@ class NodeAffinity : public Plugin {
       }
     }
   }
-  static bool required_matches(const Pod& p, const Node& n) {
-    for (const auto& kv : p.node_selector) {
-      const std::string* v = n.meta.label(kv.first);
-      if (!v || *v != kv.second) return false;
-    }
-    if (!p.has_required_node_affinity) return true;
-    for (const auto& t : p.required_node_terms)
-      if (term_matches(t, n)) return true;
-    return false;
-  }
+  static bool required_matches(const Pod& p, const Node& n) { return pod_matches_node_selector_and_affinity(p, n); }
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     if (!ni.node) return Status::error("node not found");
     if (has_added_) {

@@ -80,21 +80,8 @@ class TopologyMatch : public Plugin {
     const GpuLedger& L = ni.gpu;
     for (auto& n : out) {
       // Live GPU availability from the ledger for GPUs on this socket.
-      bool any_numa = false;
-      int free_g = 0, free_x = 0;
-      int64_t free_m = 0;
-      for (int g = 0; g < L.gpu_count; ++g) {
-        if (L.numa[g] != n.id) continue;
-        any_numa = true;
-        if (L.whole_gpu_free(g)) ++free_g;
-        if (L.monopoly[g] > 0) continue;
-        for (int p = 0; p < L.parts[g]; ++p) {
-          if (L.slot_free(g, p)) free_x += L.xcds_per_part(g);
-          const auto& s = L.slots[L.offset[g] + p];
-          if (s.exclusive == 0) free_m += L.part_mem(g) - s.used_mem;
-        }
-      }
-      if (!any_numa) continue;
+      if (n.id < 0 || n.id >= GpuLedger::kMaxZones || L.zone_gpus[n.id] == 0) continue;
+      int64_t free_g = L.zone_whole[n.id], free_x = L.zone_xcds[n.id], free_m = L.zone_mem[n.id];
       if (int64_t* v = n.find(gid)) *v = std::min<int64_t>(*v, free_g);
       if (int64_t* v = n.find(xid)) *v = std::min<int64_t>(*v, free_x);
       if (int64_t* v = n.find(mid)) *v = std::min<int64_t>(*v, free_m);
@@ -144,19 +131,11 @@ class TopologyMatch : public Plugin {
     const GpuLedger& L = ni.gpu;
     for (size_t z = 0; z < nrt.numa.size(); ++z) {
       int id = nrt.numa[z].id;
-      out.g[z] = out.x[z] = out.m[z] = 0;
-      out.any[z] = false;
-      for (int g = 0; g < L.gpu_count; ++g) {
-        if (L.numa[g] != id) continue;
-        out.any[z] = true;
-        if (L.whole_gpu_free(g)) ++out.g[z];
-        if (L.monopoly[g] > 0) continue;
-        for (int p = 0; p < L.parts[g]; ++p) {
-          if (L.slot_free(g, p)) out.x[z] += L.xcds_per_part(g);
-          const auto& s = L.slots[L.offset[g] + p];
-          if (s.exclusive == 0) out.m[z] += L.part_mem(g) - s.used_mem;
-        }
-      }
+      bool ok = id >= 0 && id < GpuLedger::kMaxZones;
+      out.any[z] = ok && L.zone_gpus[id] > 0;
+      out.g[z] = out.any[z] ? L.zone_whole[id] : 0;
+      out.x[z] = out.any[z] ? L.zone_xcds[id] : 0;
+      out.m[z] = out.any[z] ? L.zone_mem[id] : 0;
     }
   }
 
@@ -212,7 +191,15 @@ class TopologyMatch : public Plugin {
         continue;
       }
       if (pol == "SingleNUMANodePodLevel") {
-        if (!fits_fast(*nrt, ni, p.request, p.qos)) return Status::unschedulable("cannot align pod: " + p.name());
+        if (!fits_fast(*nrt, ni, p.request, p.qos)) {
+          thread_local std::string memo_uid;
+          thread_local Status memo;
+          if (memo_uid != p.uid()) {
+            memo = Status::unschedulable("cannot align pod: " + p.name());
+            memo_uid = p.uid();
+          }
+          return memo;
+        }
         continue;
       }
       if (container_scope) {

@@ -13,6 +13,7 @@ void link_noderesources_plugin();
 void link_nrt_plugin();
 void link_trimaran_plugins();
 void link_sample_plugins();
+void link_topology_plugins();
 
 void register_builtin_plugins() {
   link_intree_plugins();
@@ -24,6 +25,7 @@ void register_builtin_plugins() {
   link_nrt_plugin();
   link_trimaran_plugins();
   link_sample_plugins();
+  link_topology_plugins();
 }
 
 }  // namespace xsched

@@ -1,0 +1,547 @@
+// Upstream default plugins that reason about where *other* pods are:
+// PodTopologySpread, InterPodAffinity and ImageLocality.
+//
+// The reference runs them implicitly in every profile through the vendored
+// kube-scheduler's default plugin set (vendor/k8s.io/kubernetes/pkg/scheduler/
+// apis/config/v1beta2/default_plugins.go:34-106; implementations under
+// vendor/k8s.io/kubernetes/pkg/scheduler/framework/plugins/{podtopologyspread,
+// interpodaffinity,imagelocality}). Semantics follow k8s 1.23:
+//  * PodTopologySpread: hard constraints filter on skew = matching pods in the
+//    node's domain + self - the minimum over eligible domains (critical paths);
+//    soft constraints score cnt*log(#domains+2) + maxSkew-1, normalised so
+//    fewer matching pods is better; system default constraints need a
+//    Service/ReplicaSet selector, which this API has none of, so they never
+//    apply (as upstream for bare pods).
+//  * InterPodAffinity: required (anti-)affinity of the incoming pod and the
+//    required anti-affinity of existing pods, counted per topology pair in
+//    PreFilter and kept current through AddPod/RemovePod for preemption
+//    dry-runs; preferred terms (and existing pods' hard affinity with
+//    hardPodAffinityWeight) score per topology value, min-max normalised.
+//  * ImageLocality: Σ image size × spread over containers, clamped to
+//    [23 MiB, 1000 MiB × containers] and scaled to 0..100.
+// Fast paths: a profile whose pods use none of these features pays one
+// emptiness check per cycle (no per-node work).
+#include <algorithm>
+#include <array>
+#include <climits>
+#include <cmath>
+#include <shared_mutex>
+#include <unordered_map>
+#include <unordered_set>
+
+#include "framework/plugin.h"
+#include "store/store.h"
+
+namespace xsched {
+namespace {
+
+const char* kHostnameLabel = "kubernetes.io/hostname";
+
+inline std::string pair_key(const std::string& k, const std::string& v) {
+  std::string s;
+  s.reserve(k.size() + v.size() + 1);
+  s += k;
+  s += '\n';
+  s += v;
+  return s;
+}
+
+int64_t count_matching(const std::vector<PodPtr>& pods, const LabelSelector& sel, const std::string& ns) {
+  int64_t n = 0;
+  for (const auto& q : pods)
+    if (!q->terminating() && q->ns() == ns && sel.matches(q->meta.labels)) ++n;
+  return n;
+}
+
+// ===================================================== PodTopologySpread ====
+struct CriticalPath {
+  std::string value;
+  int64_t num = INT32_MAX;
+};
+
+struct SpreadFilterState : StateData {
+  std::vector<TopologySpreadConstraint> constraints;
+  std::unordered_map<std::string, int64_t> pair_num;                     // key\nvalue -> matching pods
+  std::unordered_map<std::string, std::array<CriticalPath, 2>> critical;  // topology key -> two smallest
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<SpreadFilterState>(*this); }
+
+  void update_critical(const std::string& key, const std::string& value, int64_t num) {
+    auto& p = critical[key];
+    int i = value == p[0].value ? 0 : value == p[1].value ? 1 : -1;
+    if (i >= 0) {
+      p[i].num = num;
+      if (p[0].num > p[1].num) std::swap(p[0], p[1]);
+    } else if (num < p[0].num) {
+      p[1] = p[0];
+      p[0] = CriticalPath{value, num};
+    } else if (num < p[1].num) {
+      p[1] = CriticalPath{value, num};
+    }
+  }
+};
+
+struct SpreadScoreState : StateData {
+  std::vector<TopologySpreadConstraint> constraints;
+  std::unordered_set<std::string> ignored;
+  std::unordered_map<std::string, int64_t> pair_count;
+  std::vector<double> weight;
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<SpreadScoreState>(*this); }
+};
+
+bool has_all_keys(const Node& n, const std::vector<TopologySpreadConstraint>& cs) {
+  for (const auto& c : cs)
+    if (!n.meta.label(c.topology_key)) return false;
+  return true;
+}
+
+class PodTopologySpread : public Plugin {
+ public:
+  explicit PodTopologySpread(Handle& h)
+      : Plugin("PodTopologySpread", kPreFilter | kFilter | kPreScore | kScore), h_(h) {}
+
+  static constexpr const char* kFilterKey = "PreFilterPodTopologySpread";
+  static constexpr const char* kScoreKey = "PreScorePodTopologySpread";
+
+  Status pre_filter(CycleState& s, const Pod& p) override {
+    auto st = std::make_shared<SpreadFilterState>();
+    for (const auto& c : p.spread_constraints)
+      if (c.hard) st->constraints.push_back(c);
+    if (!st->constraints.empty() && h_.snapshot) {
+      for (const auto& ni : h_.snapshot->nodes) {
+        const Node& n = *ni->node;
+        if (!pod_matches_node_selector_and_affinity(p, n) || !has_all_keys(n, st->constraints)) continue;
+        for (const auto& c : st->constraints)
+          st->pair_num[pair_key(c.topology_key, *n.meta.label(c.topology_key))] +=
+              count_matching(ni->pods, c.selector, p.ns());
+      }
+      for (const auto& c : st->constraints) st->critical[c.topology_key];
+      for (const auto& [pk, num] : st->pair_num) {
+        size_t nl = pk.find('\n');
+        st->update_critical(pk.substr(0, nl), pk.substr(nl + 1), num);
+      }
+    }
+    s.write(kFilterKey, st);
+    return {};
+  }
+  bool has_pre_filter_extensions() const override { return true; }
+
+  void update_with_pod(CycleState& s, const Pod& preemptor, const Pod& q, const NodeInfo& ni, int64_t delta) {
+    auto* st = s.read_as<SpreadFilterState>(kFilterKey);
+    if (!st || st->constraints.empty() || !ni.node) return;
+    const Node& n = *ni.node;
+    if (!pod_matches_node_selector_and_affinity(preemptor, n) || !has_all_keys(n, st->constraints)) return;
+    if (q.ns() != preemptor.ns()) return;
+    for (const auto& c : st->constraints) {
+      if (!c.selector.matches(q.meta.labels)) continue;
+      const std::string& v = *n.meta.label(c.topology_key);
+      int64_t& num = st->pair_num[pair_key(c.topology_key, v)];
+      num += delta;
+      st->update_critical(c.topology_key, v, num);
+    }
+  }
+  Status add_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
+    update_with_pod(s, p, *q, ni, 1);
+    return {};
+  }
+  Status remove_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
+    update_with_pod(s, p, *q, ni, -1);
+    return {};
+  }
+
+  Status filter(CycleState& s, const Pod& p, const NodeInfo& ni) override {
+    auto* st = s.read_as<SpreadFilterState>(kFilterKey);
+    if (!st) return Status::error("PodTopologySpread: no PreFilter state");
+    if (st->constraints.empty()) return {};
+    const Node& n = *ni.node;
+    for (const auto& c : st->constraints) {
+      const std::string* v = n.meta.label(c.topology_key);
+      if (!v) return Status::unresolvable("node(s) didn't match pod topology spread constraints (missing required label)");
+      int64_t self = c.selector.matches(p.meta.labels) ? 1 : 0;
+      auto cit = st->critical.find(c.topology_key);
+      if (cit == st->critical.end()) return Status::error("PodTopologySpread: internal error: no critical paths");
+      int64_t min_num = cit->second[0].num;
+      auto it = st->pair_num.find(pair_key(c.topology_key, *v));
+      int64_t num = it == st->pair_num.end() ? 0 : it->second;
+      if (num + self - min_num > c.max_skew)
+        return Status::unschedulable("node(s) didn't match pod topology spread constraints");
+    }
+    return {};
+  }
+
+  Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) override {
+    auto st = std::make_shared<SpreadScoreState>();
+    for (const auto& c : p.spread_constraints)
+      if (!c.hard) st->constraints.push_back(c);
+    if (st->constraints.empty() || nodes.empty()) {
+      s.write(kScoreKey, st);
+      return {};
+    }
+    std::vector<int64_t> size(st->constraints.size(), 0);
+    for (const auto& ni : nodes) {
+      const Node& n = *ni->node;
+      if (!has_all_keys(n, st->constraints)) {
+        st->ignored.insert(n.name());
+        continue;
+      }
+      for (size_t i = 0; i < st->constraints.size(); ++i) {
+        const auto& c = st->constraints[i];
+        if (c.topology_key == kHostnameLabel) {
+          ++size[i];
+          continue;
+        }
+        auto [it, fresh] = st->pair_count.emplace(pair_key(c.topology_key, *n.meta.label(c.topology_key)), 0);
+        if (fresh) ++size[i];
+      }
+    }
+    for (int64_t sz : size) st->weight.push_back(std::log(static_cast<double>(sz + 2)));
+    if (h_.snapshot) {
+      for (const auto& ni : h_.snapshot->nodes) {
+        const Node& n = *ni->node;
+        if (!pod_matches_node_selector_and_affinity(p, n) || !has_all_keys(n, st->constraints)) continue;
+        for (const auto& c : st->constraints) {
+          if (c.topology_key == kHostnameLabel) continue;
+          auto it = st->pair_count.find(pair_key(c.topology_key, *n.meta.label(c.topology_key)));
+          if (it == st->pair_count.end()) continue;
+          it->second += count_matching(ni->pods, c.selector, p.ns());
+        }
+      }
+    }
+    s.write(kScoreKey, st);
+    return {};
+  }
+
+  std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) override {
+    auto* st = s.read_as<SpreadScoreState>(kScoreKey);
+    if (!st) return {0, Status::error("PodTopologySpread: no PreScore state")};
+    if (st->constraints.empty() || st->ignored.count(ni.name())) return {0, {}};
+    double score = 0;
+    for (size_t i = 0; i < st->constraints.size(); ++i) {
+      const auto& c = st->constraints[i];
+      const std::string* v = ni.node->meta.label(c.topology_key);
+      if (!v) continue;
+      int64_t cnt;
+      if (c.topology_key == kHostnameLabel) {
+        cnt = count_matching(ni.pods, c.selector, p.ns());
+      } else {
+        auto it = st->pair_count.find(pair_key(c.topology_key, *v));
+        cnt = it == st->pair_count.end() ? 0 : it->second;
+      }
+      score += static_cast<double>(cnt) * st->weight[i] + static_cast<double>(c.max_skew - 1);
+    }
+    return {static_cast<int64_t>(score), {}};
+  }
+  bool has_normalize_score() const override { return true; }
+  Status normalize_score(CycleState& s, const Pod&, std::vector<NodeScore>& scores) override {
+    auto* st = s.read_as<SpreadScoreState>(kScoreKey);
+    if (!st) return Status::error("PodTopologySpread: no PreScore state");
+    int64_t lo = INT64_MAX, hi = 0;
+    std::vector<char> invalid(scores.size(), 0);
+    for (size_t i = 0; i < scores.size(); ++i) {
+      if (st->ignored.count(scores[i].name)) {
+        invalid[i] = 1;
+        continue;
+      }
+      lo = std::min(lo, scores[i].score);
+      hi = std::max(hi, scores[i].score);
+    }
+    for (size_t i = 0; i < scores.size(); ++i) {
+      if (invalid[i]) {
+        scores[i].score = 0;
+      } else if (hi == 0) {
+        scores[i].score = kMaxNodeScore;
+      } else {
+        scores[i].score = kMaxNodeScore * (hi + lo - scores[i].score) / hi;
+      }
+    }
+    return {};
+  }
+  std::vector<ClusterEvent> events_to_register() const override {
+    return {{"Pod", kAll, ""}, {"Node", kAdd | kDelete | kUpdateNodeLabel, ""}};
+  }
+
+ private:
+  Handle& h_;
+};
+
+// ====================================================== InterPodAffinity ====
+using PairCounts = std::unordered_map<std::string, int64_t>;
+
+struct AffinityFilterState : StateData {
+  PairCounts existing_anti, affinity, anti;
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<AffinityFilterState>(*this); }
+};
+struct AffinityScoreState : StateData {
+  std::unordered_map<std::string, std::unordered_map<std::string, int64_t>> topo_score;  // key -> value -> score
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<AffinityScoreState>(*this); }
+};
+
+void bump(PairCounts& m, const Node& n, const std::string& key, int64_t v) {
+  const std::string* tv = n.meta.label(key);
+  if (!tv) return;
+  std::string k = pair_key(key, *tv);
+  int64_t& c = m[k];
+  c += v;
+  if (c == 0) m.erase(k);
+}
+
+class InterPodAffinity : public Plugin {
+ public:
+  InterPodAffinity(const Json& args, Handle& h)
+      : Plugin("InterPodAffinity", kPreFilter | kFilter | kPreScore | kScore), h_(h) {
+    hard_weight_ = static_cast<int32_t>(args["hardPodAffinityWeight"].as_int(1));
+  }
+  static constexpr const char* kFilterKey = "PreFilterInterPodAffinity";
+  static constexpr const char* kScoreKey = "PreScoreInterPodAffinity";
+
+  std::vector<std::string> watched_kinds() const override { return {"namespaces"}; }
+  void on_object_event(const std::string&, int type, const JsonPtr& obj, const JsonPtr&) override {
+    auto md = ObjectMeta::from_json(*obj);
+    std::unique_lock<std::shared_mutex> g(ns_mu_);
+    if (static_cast<EventType>(type) == EventType::Deleted)
+      ns_labels_.erase(md.name);
+    else
+      ns_labels_[md.name] = md.labels;
+  }
+  StrMap ns_labels(const std::string& ns) const {
+    std::shared_lock<std::shared_mutex> g(ns_mu_);
+    auto it = ns_labels_.find(ns);
+    return it == ns_labels_.end() ? StrMap{} : it->second;
+  }
+
+  // AffinityTerm.Matches: namespace in the term's set (default: the owner's
+  // namespace) or selected by namespaceSelector, and label selector match.
+  bool term_matches(const PodAffinityTerm& t, const std::string& owner_ns, const Pod& q) const {
+    bool ns_ok = false;
+    if (t.namespaces.empty() && !t.namespace_selector.present) {
+      ns_ok = q.ns() == owner_ns;
+    } else {
+      for (const auto& n : t.namespaces)
+        if (n == q.ns()) {
+          ns_ok = true;
+          break;
+        }
+      if (!ns_ok && t.namespace_selector.present) ns_ok = t.namespace_selector.matches(ns_labels(q.ns()));
+    }
+    return ns_ok && t.selector.matches(q.meta.labels);
+  }
+  bool matches_all(const std::vector<PodAffinityTerm>& ts, const std::string& owner_ns, const Pod& q) const {
+    if (ts.empty()) return false;
+    for (const auto& t : ts)
+      if (!term_matches(t, owner_ns, q)) return false;
+    return true;
+  }
+
+  // updateWithPod: `q` (existing) entering/leaving node `n` for incoming `p`.
+  void update(AffinityFilterState& st, const Pod& p, const Pod& q, const Node& n, int64_t d) const {
+    for (const auto& t : q.pod_anti_affinity_required)
+      if (term_matches(t, q.ns(), p)) bump(st.existing_anti, n, t.topology_key, d);
+    if (matches_all(p.pod_affinity_required, p.ns(), q))
+      for (const auto& t : p.pod_affinity_required) bump(st.affinity, n, t.topology_key, d);
+    for (const auto& t : p.pod_anti_affinity_required)
+      if (term_matches(t, p.ns(), q)) bump(st.anti, n, t.topology_key, d);
+  }
+
+  Status pre_filter(CycleState& s, const Pod& p) override {
+    auto st = std::make_shared<AffinityFilterState>();
+    if (h_.snapshot) {
+      for (const auto& ni : h_.snapshot->have_pods_with_required_anti_affinity)
+        for (const auto& q : ni->pods_with_required_anti_affinity)
+          for (const auto& t : q->pod_anti_affinity_required)
+            if (term_matches(t, q->ns(), p)) bump(st->existing_anti, *ni->node, t.topology_key, 1);
+      if (!p.pod_affinity_required.empty() || !p.pod_anti_affinity_required.empty()) {
+        for (const auto& ni : h_.snapshot->nodes)
+          for (const auto& q : ni->pods) {
+            if (matches_all(p.pod_affinity_required, p.ns(), *q))
+              for (const auto& t : p.pod_affinity_required) bump(st->affinity, *ni->node, t.topology_key, 1);
+            for (const auto& t : p.pod_anti_affinity_required)
+              if (term_matches(t, p.ns(), *q)) bump(st->anti, *ni->node, t.topology_key, 1);
+          }
+      }
+    }
+    s.write(kFilterKey, st);
+    return {};
+  }
+  bool has_pre_filter_extensions() const override { return true; }
+  Status add_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
+    if (auto* st = s.read_as<AffinityFilterState>(kFilterKey)) update(*st, p, *q, *ni.node, 1);
+    return {};
+  }
+  Status remove_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
+    if (auto* st = s.read_as<AffinityFilterState>(kFilterKey)) update(*st, p, *q, *ni.node, -1);
+    return {};
+  }
+
+  Status filter(CycleState& s, const Pod& p, const NodeInfo& ni) override {
+    auto* st = s.read_as<AffinityFilterState>(kFilterKey);
+    if (!st) return Status::error("InterPodAffinity: no PreFilter state");
+    const Node& n = *ni.node;
+    // satisfyPodAffinity
+    if (!p.pod_affinity_required.empty()) {
+      bool exist = true;
+      for (const auto& t : p.pod_affinity_required) {
+        const std::string* v = n.meta.label(t.topology_key);
+        if (!v) return Status::unresolvable("node(s) didn't match pod affinity rules");
+        auto it = st->affinity.find(pair_key(t.topology_key, *v));
+        if (it == st->affinity.end() || it->second <= 0) exist = false;
+      }
+      // The first pod of a self-affine series may go anywhere.
+      if (!exist && !(st->affinity.empty() && matches_all(p.pod_affinity_required, p.ns(), p)))
+        return Status::unresolvable("node(s) didn't match pod affinity rules");
+    }
+    // satisfyPodAntiAffinity
+    if (!st->anti.empty())
+      for (const auto& t : p.pod_anti_affinity_required) {
+        const std::string* v = n.meta.label(t.topology_key);
+        if (!v) continue;
+        auto it = st->anti.find(pair_key(t.topology_key, *v));
+        if (it != st->anti.end() && it->second > 0)
+          return Status::unschedulable("node(s) didn't match pod anti-affinity rules");
+      }
+    // satisfyExistingPodsAntiAffinity
+    if (!st->existing_anti.empty())
+      for (const auto& [k, v] : n.meta.labels) {
+        auto it = st->existing_anti.find(pair_key(k, v));
+        if (it != st->existing_anti.end() && it->second > 0)
+          return Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
+      }
+    return {};
+  }
+
+  void add_term(AffinityScoreState& st, const PodAffinityTerm& t, int64_t w, const std::string& owner_ns,
+                const Pod& q, const Node& n) const {
+    if (w == 0 || !term_matches(t, owner_ns, q)) return;
+    if (const std::string* v = n.meta.label(t.topology_key)) st.topo_score[t.topology_key][*v] += w;
+  }
+
+  Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) override {
+    auto st = std::make_shared<AffinityScoreState>();
+    bool has_pref = !p.pod_affinity_preferred.empty() || !p.pod_anti_affinity_preferred.empty();
+    if (h_.snapshot && !nodes.empty() && (has_pref || !h_.snapshot->have_pods_with_affinity.empty())) {
+      const auto& scan = has_pref ? h_.snapshot->nodes : h_.snapshot->have_pods_with_affinity;
+      for (const auto& ni : scan) {
+        const Node& n = *ni->node;
+        const auto& pods = has_pref ? ni->pods : ni->pods_with_affinity;
+        for (const auto& q : pods) {
+          for (const auto& wt : p.pod_affinity_preferred) add_term(*st, wt.term, wt.weight, p.ns(), *q, n);
+          for (const auto& wt : p.pod_anti_affinity_preferred) add_term(*st, wt.term, -wt.weight, p.ns(), *q, n);
+          if (hard_weight_ > 0)
+            for (const auto& t : q->pod_affinity_required) add_term(*st, t, hard_weight_, q->ns(), p, n);
+          for (const auto& wt : q->pod_affinity_preferred) add_term(*st, wt.term, wt.weight, q->ns(), p, n);
+          for (const auto& wt : q->pod_anti_affinity_preferred) add_term(*st, wt.term, -wt.weight, q->ns(), p, n);
+        }
+      }
+    }
+    s.write(kScoreKey, st);
+    return {};
+  }
+  std::pair<int64_t, Status> score(CycleState& s, const Pod&, const NodeInfo& ni) override {
+    auto* st = s.read_as<AffinityScoreState>(kScoreKey);
+    if (!st) return {0, Status::error("InterPodAffinity: no PreScore state")};
+    int64_t score = 0;
+    for (const auto& [key, vals] : st->topo_score) {
+      const std::string* v = ni.node->meta.label(key);
+      if (!v) continue;
+      auto it = vals.find(*v);
+      if (it != vals.end()) score += it->second;
+    }
+    return {score, {}};
+  }
+  bool has_normalize_score() const override { return true; }
+  Status normalize_score(CycleState& s, const Pod&, std::vector<NodeScore>& scores) override {
+    auto* st = s.read_as<AffinityScoreState>(kScoreKey);
+    if (!st || st->topo_score.empty()) return {};
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (const auto& x : scores) {
+      lo = std::min(lo, x.score);
+      hi = std::max(hi, x.score);
+    }
+    int64_t diff = hi - lo;
+    for (auto& x : scores)
+      x.score = diff > 0 ? static_cast<int64_t>(static_cast<double>(kMaxNodeScore) *
+                                                (static_cast<double>(x.score - lo) / static_cast<double>(diff)))
+                         : 0;
+    return {};
+  }
+  std::vector<ClusterEvent> events_to_register() const override {
+    return {{"Pod", kAll, ""}, {"Node", kAdd | kUpdateNodeLabel, ""}};
+  }
+
+ private:
+  Handle& h_;
+  int32_t hard_weight_ = 1;
+  mutable std::shared_mutex ns_mu_;
+  std::unordered_map<std::string, StrMap> ns_labels_;
+};
+
+// ========================================================= ImageLocality ====
+class ImageLocality : public Plugin {
+ public:
+  explicit ImageLocality(Handle& h) : Plugin("ImageLocality", kScore), h_(h) {}
+  static constexpr int64_t kMB = 1024 * 1024;
+  static constexpr int64_t kMinThreshold = 23 * kMB;
+  static constexpr int64_t kMaxContainerThreshold = 1000 * kMB;
+
+  std::vector<std::string> watched_kinds() const override { return {"nodes"}; }
+  void on_object_event(const std::string&, int type, const JsonPtr& obj, const JsonPtr&) override {
+    auto n = Node::from_json(*obj);
+    std::unique_lock<std::shared_mutex> g(mu_);
+    auto old = node_images_.find(n->name());
+    if (old != node_images_.end()) {
+      for (const auto& [img, _] : old->second) {
+        auto it = image_nodes_.find(img);
+        if (it != image_nodes_.end() && --it->second == 0) image_nodes_.erase(it);
+      }
+      node_images_.erase(old);
+    }
+    if (static_cast<EventType>(type) == EventType::Deleted) return;
+    auto& mine = node_images_[n->name()];
+    for (const auto& im : n->images)
+      for (const auto& name : im.names)
+        if (mine.emplace(name, im.size_bytes).second) ++image_nodes_[name];
+  }
+
+  static std::string normalized(const std::string& image) {
+    size_t colon = image.rfind(':'), slash = image.rfind('/');
+    bool has_tag = colon != std::string::npos && (slash == std::string::npos || colon > slash);
+    return has_tag ? image : image + ":latest";
+  }
+
+  std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
+    int64_t total_nodes = h_.snapshot ? static_cast<int64_t>(h_.snapshot->nodes.size()) : 1;
+    int64_t sum = 0;
+    {
+      std::shared_lock<std::shared_mutex> g(mu_);
+      auto nit = node_images_.find(ni.name());
+      if (nit != node_images_.end() && total_nodes > 0)
+        for (const auto& c : p.containers) {
+          auto it = nit->second.find(normalized(c.image));
+          if (it == nit->second.end()) continue;
+          auto cnt = image_nodes_.find(it->first);
+          int64_t spread = cnt == image_nodes_.end() ? 0 : cnt->second;
+          sum += static_cast<int64_t>(static_cast<double>(it->second) * static_cast<double>(spread) /
+                                      static_cast<double>(total_nodes));
+        }
+    }
+    int64_t max_threshold = kMaxContainerThreshold * static_cast<int64_t>(p.containers.size());
+    if (max_threshold <= kMinThreshold) return {0, {}};
+    sum = std::clamp(sum, kMinThreshold, max_threshold);
+    return {kMaxNodeScore * (sum - kMinThreshold) / (max_threshold - kMinThreshold), {}};
+  }
+
+ private:
+  Handle& h_;
+  mutable std::shared_mutex mu_;
+  std::unordered_map<std::string, std::unordered_map<std::string, int64_t>> node_images_;  // node -> image -> size
+  std::unordered_map<std::string, int64_t> image_nodes_;                                   // image -> #nodes
+};
+
+PluginRegistrar r1("PodTopologySpread", [](const Json&, Handle& h) { return std::make_shared<PodTopologySpread>(h); });
+PluginRegistrar r2("InterPodAffinity",
+                   [](const Json& a, Handle& h) { return std::make_shared<InterPodAffinity>(a, h); });
+PluginRegistrar r3("ImageLocality", [](const Json&, Handle& h) { return std::make_shared<ImageLocality>(h); });
+
+}  // namespace
+
+void link_topology_plugins() {}
+
+}  // namespace xsched

@@ -421,6 +421,7 @@ void Scheduler::apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr 
 }
 
 void Scheduler::handle_node_event(const WatchEvent& ev) {
+  for (auto& fw : frameworks_) fw->dispatch_object_event("nodes", static_cast<int>(ev.type), ev.obj, ev.old);
   if (ev.type == EventType::Deleted) {
     auto n = Node::from_json(*ev.obj);
     cache_->remove_node(n->name());

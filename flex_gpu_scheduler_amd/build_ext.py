@@ -137,12 +137,35 @@ def build_tsan(verbose: bool = True) -> Path:
     return out
 
 
+def build_prof(verbose: bool = True, gprof: bool = True) -> Path:
+    """Native stress driver (no Python in the loop). With `gprof` it is built
+    with -pg for a per-function CPU profile of the scheduling hot path;
+    without, at the core's optimisation level for timing."""
+    includes = [str(CSRC)]
+    extra = ["-pg", "-g", "-O2", "-fno-omit-frame-pointer", "-fno-inline-functions-called-once"] if gprof else []
+    sub = "prof" if gprof else "stress"
+    objs = build_objects(core_sources() + [CSRC / "tools" / "stress_main.cc"], BUILD / sub, extra, includes)
+    out = BUILD / ("xsched_stress_prof" if gprof else "xsched_stress")
+    cmd = ["g++", *(["-pg"] if gprof else []), "-pthread", *[str(o) for o in objs], "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"prof link failed:\n{r.stderr[-8000:]}")
+    if verbose:
+        print(f"[build_ext] built {out.relative_to(ROOT)}")
+    return out
+
+
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--core", action="store_true")
     ap.add_argument("--hip", action="store_true")
     ap.add_argument("--tsan", action="store_true")
+    ap.add_argument("--prof", action="store_true")
+    ap.add_argument("--stress", action="store_true")
     a = ap.parse_args(argv)
+    if a.prof or a.stress:
+        build_prof(gprof=a.prof)
+        return 0
     everything = not (a.core or a.hip or a.tsan)
     if a.core or everything:
         build_core()
