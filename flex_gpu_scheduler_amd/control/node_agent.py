@@ -94,6 +94,9 @@ class NodeAgent:
         node = mi355x_node(self.name, gpus=infos, cpu=str(max(1, host.cpus - self.reserved_cpu)),
                            memory=f"{mem_kib}Ki", pods=max(110, host.cpus), labels=labels,
                            taints=[UNHEALTHY_TAINT] if host.gpus and not healthy else None)
+        if not host.gpus:  # a CPU-only node carries no GPU identity labels
+            for k in ("amd.com/gpu.compute-partition", "amd.com/gpu.product", "amd.com/gpu.family"):
+                node["metadata"]["labels"].pop(k, None)
         topo = json.loads(node["metadata"]["annotations"][TOPOLOGY_ANNOTATION])
         by_index = {g.index: g for g in healthy}
         for i, entry in enumerate(topo["gpus"]):

@@ -19,6 +19,7 @@ step() {  # name timeout cmd...
   esac
 }
 step pytest_gpu 420 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+step agent_check 120 python -m flex_gpu_scheduler_amd.tools.agent_check
 step bench1 240 python bench.py
 step probe_sweep 120 python -m flex_gpu_scheduler_amd.tools.probe_bench
 step rocprof_probe 180 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_probe" -o probe -- python3 -m flex_gpu_scheduler_amd.tools.probe_bench
