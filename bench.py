@@ -38,6 +38,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-gpu-probe", action="store_true")
     ap.add_argument("--trace", default="", help="write a Chrome trace of rank 0's timed steps")
+    ap.add_argument("--no-scenarios", action="store_true",
+                    help="skip the per-BASELINE-config scenarios (untimed, reported under config.scenarios)")
     args = ap.parse_args()
 
     from flex_gpu_scheduler_amd.parallel.dist import init_distributed
@@ -99,6 +101,12 @@ def main() -> int:
         extras["rccl_allreduce"] = [{"MiB": r.bytes >> 20, "busbw_GBps": round(r.busbw_gbps, 1)} for r in res]
 
     value = pods_total / t_max if t_max > 0 else 0.0
+    if ctx.rank == 0 and not args.no_scenarios:
+        # The five BASELINE.json configurations, each with its placement check
+        # (outside the timed region; utils/scenarios.py).
+        from flex_gpu_scheduler_amd.utils.scenarios import run_all
+
+        extras["scenarios"] = run_all()
     if ctx.rank == 0:
         lat = gang_latency_summary(all_gangs)
         line = {

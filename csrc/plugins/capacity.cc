@@ -315,8 +315,10 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
         if (!rst.is_success()) return {false, rst};
         victims.push_back(p);
       }
+      // The reference re-removes (and double-lists) a pod that already
+      // failed the fit check; only a reprieved pod is re-checked here.
       auto pit2 = infos.find(pod.ns());
-      if (pit2 != infos.end() && (pit2->second.used_over_max_with(pfs->nominated_in_eq_with_req) ||
+      if (fits && pit2 != infos.end() && (pit2->second.used_over_max_with(pfs->nominated_in_eq_with_req) ||
                                   aggregated_used_over_min_with(infos, pfs->nominated_with_req))) {
         Status rst = remove(p);
         if (!rst.is_success()) return {false, rst};

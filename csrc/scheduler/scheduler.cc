@@ -218,7 +218,9 @@ Scheduler::~Scheduler() { stop(); }
 void Scheduler::start() {
   if (running_.exchange(true)) return;
   for (auto& fw : frameworks_) fw->start();
-  timer_ids_.push_back(timers_->every(1'000'000, [this] { queue_->flush_backoff_completed(); }));
+  // Backoff expiry is checked every 100 ms (upstream: 1 s), so a retried
+  // pod waits its backoff, not its backoff plus up to a second of tick phase.
+  timer_ids_.push_back(timers_->every(100'000, [this] { queue_->flush_backoff_completed(); }));
   timer_ids_.push_back(timers_->every(30'000'000, [this] { queue_->flush_unschedulable_leftover(); }));
   timer_ids_.push_back(timers_->every(1'000'000, [this] { cache_->cleanup_expired_assumed_pods(); }));
   timer_ids_.push_back(timers_->every(1'000'000, [this] {
@@ -909,9 +911,6 @@ void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr q
 void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const Status& st, const std::string& reason,
                                const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins) {
   PodPtr pod = qpi->pod;
-  if (!nominated.empty()) {
-    nominator_->add(pod, nominated);
-  }
   // Requeue the latest version unless it was deleted or got assigned.
   PodPtr latest = informers_->pod(pod->ns(), pod->name());
   if (latest && latest->uid() == pod->uid() && latest->node_name.empty() && !latest->terminating()) {
@@ -920,6 +919,10 @@ void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const
     nq->unschedulable_plugins = plugins;
     queue_->add_unschedulable_if_not_present(nq, cycle);
   }
+  // After the requeue (which re-registers the pod's *observed* nomination):
+  // the next cycle must already see this one, before the status patch comes
+  // back through the informer (scheduler.go handleSchedulingFailure).
+  if (!nominated.empty()) nominator_->add(latest && latest->uid() == pod->uid() ? latest : pod, nominated);
   fw.handle().client->record_event("Pod", pod->ns(), pod->name(), "Warning", "FailedScheduling", st.message());
   if (!opts_.status_updates) return;
   // updatePod: PodScheduled=False condition + nominatedNodeName, only when changed.

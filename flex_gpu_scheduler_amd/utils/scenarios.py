@@ -1,0 +1,280 @@
+"""The five BASELINE.json configurations as small, checked scenarios.
+
+`bench.py`'s headline number is the mixed gang workload (utils/workload.py).
+This module runs each named configuration on its own store and scheduler
+(untimed by the bench contract; reported under `config.scenarios`), both to
+measure it and to assert the placement property the configuration is about:
+
+  coscheduling_cpu     PodGroups minMember=2 of CPU-only pods (plumbing)
+  flexgpu_cpx_quarter  4 pods x 0.25 GPU (amd.com/gpu-xcd: 2) on one CPX MI355X
+  gang8_xgmi           8-rank gangs on 8x MI355X nodes, NRT XGMIGangAffinity
+  capacity_preemption  2 namespaces contend for 8 MI355X (ElasticQuota + preemption)
+  trimaran_tlp         TargetLoadPacking(GPU) fed by live amdgpu utilisation
+"""
+from __future__ import annotations
+
+import json
+import time
+from typing import Callable
+
+from ..config import load_config
+from ..models.mi355x import GPU, GPU_XCD, INDEX_ANNOTATION, PARTITION_ANNOTATION, mi355x_node, mi355x_nrt
+from ..models.objects import make_elastic_quota, make_node, make_pod, make_pod_group
+from ..scheduler import Store, new_scheduler
+from .workload import flagship_config, percentile
+
+
+def _wait(pred: Callable[[], bool], timeout: float = 30.0, poll: float = 0.0002) -> bool:
+    deadline = time.perf_counter() + timeout
+    while not pred():
+        if time.perf_counter() > deadline:
+            return False
+        time.sleep(poll)
+    return True
+
+
+def _summary(lat_ms: list[float], pods: int, seconds: float) -> dict:
+    return {"pods": pods, "pods_per_s": round(pods / seconds, 1) if seconds > 0 else 0.0,
+            "p50_ms": round(percentile(lat_ms, 50), 3), "p99_ms": round(percentile(lat_ms, 99), 3)}
+
+
+def _bound(store, ns: str) -> list[dict]:
+    return [p for p in store.list("pods", ns)[0] if p["spec"].get("nodeName")]
+
+
+def _cosched_cfg(extra: dict | None = None, args: list | None = None) -> dict:
+    plugins = {"queueSort": {"enabled": [{"name": "Coscheduling"}], "disabled": [{"name": "*"}]},
+               "preFilter": {"enabled": [{"name": "Coscheduling"}]},
+               "postFilter": {"enabled": [{"name": "Coscheduling"}]},
+               "permit": {"enabled": [{"name": "Coscheduling"}]},
+               "reserve": {"enabled": [{"name": "Coscheduling"}]},
+               "postBind": {"enabled": [{"name": "Coscheduling"}]}}
+    for pt, spec in (extra or {}).items():
+        for k, v in spec.items():
+            plugins.setdefault(pt, {}).setdefault(k, []).extend(v)
+    return {"apiVersion": "kubescheduler.config.k8s.io/v1beta3", "kind": "KubeSchedulerConfiguration",
+            "profiles": [{"schedulerName": "default-scheduler", "plugins": plugins, "pluginConfig": [
+                {"name": "Coscheduling", "args": {"permitWaitingTimeSeconds": 10, "deniedPGExpirationTimeSeconds": 3}},
+                *(args or [])]}]}
+
+
+def coscheduling_cpu(waves: int = 4, groups: int = 100, nodes: int = 16) -> dict:
+    store = Store()
+    store.create_many("nodes", json.dumps([make_node(f"kind-{i}", {"cpu": "64", "memory": "256Gi", "pods": "110"})
+                                           for i in range(nodes)]))
+    s = new_scheduler(store, load_config(_cosched_cfg()), start=True)
+    lat: list[float] = []
+    t_total, pods = 0.0, 0
+    try:
+        for w in range(waves + 1):
+            ns = f"cpu-{w}"
+            pgs = [make_pod_group(f"pg{i}", ns, 2) for i in range(groups)]
+            pl = [make_pod(f"pg{i}-{r}", ns, pod_group=f"pg{i}", requests={"cpu": "500m", "memory": "512Mi"})
+                  for i in range(groups) for r in range(2)]
+            t0 = time.perf_counter()
+            store.create_many("podgroups", json.dumps(pgs))
+            store.create_many("pods", json.dumps(pl))
+            ok = _wait(lambda: s.stats()["bound"] >= (w + 1) * len(pl))
+            dt = time.perf_counter() - t0
+            recs = s.gang_records(True)
+            if w > 0:  # first wave is warm-up
+                t_total += dt
+                pods += len(pl)
+                lat += [(g["bound_us"] - g["first_enqueue_us"]) / 1000.0 for g in recs]
+            store.delete_all("pods", ns)
+            store.delete_all("podgroups", ns)
+            _wait(lambda: s.cache_counts()["pods"] == 0)
+            if not ok:
+                return {"error": "wave did not bind"}
+    finally:
+        s.stop()
+    return _summary(lat, pods, t_total) | {"groups_per_wave": groups, "nodes": nodes}
+
+
+def flexgpu_cpx_quarter(iterations: int = 40) -> dict:
+    """4 pods x amd.com/gpu-xcd: 2 on one MI355X in CPX mode: all four share the
+    GPU, each on its own pair of XCD partitions."""
+    store = Store()
+    store.create("nodes", mi355x_node("mi355x-cpx", n_gpus=1, mode="cpx"))
+    cfg = _cosched_cfg({"filter": {"enabled": [{"name": "FlexGPU"}]}, "score": {"enabled": [{"name": "FlexGPU"}]},
+                        "reserve": {"enabled": [{"name": "FlexGPU"}]},
+                        "bind": {"enabled": [{"name": "FlexGPU"}], "disabled": [{"name": "DefaultBinder"}]}})
+    s = new_scheduler(store, load_config(cfg), start=True)
+    lat: list[float] = []
+    t_total, pods, shared_ok = 0.0, 0, 0
+    try:
+        for it in range(iterations + 2):
+            ns = f"cpx-{it}"
+            pl = [make_pod(f"q{i}", ns, limits={GPU_XCD: "2"}, requests={GPU_XCD: "2"}) for i in range(4)]
+            t0 = time.perf_counter()
+            store.create_many("pods", json.dumps(pl))
+            ok = _wait(lambda: len(_bound(store, ns)) == 4)
+            dt = time.perf_counter() - t0
+            if not ok:
+                return {"error": "quarter-GPU pods did not bind"}
+            bound = _bound(store, ns)
+            parts = [p["metadata"]["annotations"].get(PARTITION_ANNOTATION, "") for p in bound]
+            flat = [x for ps in parts for x in ps.split(",") if x]
+            if len(flat) == 8 and len(set(flat)) == 8 and {x.split(":")[0] for x in flat} == {"0"}:
+                shared_ok += 1
+            if it >= 2:
+                t_total += dt
+                pods += 4
+                lat.append(dt * 1000.0)
+            store.delete_all("pods", ns)
+            _wait(lambda: s.cache_counts()["pods"] == 0)
+    finally:
+        s.stop()
+    return _summary(lat, pods, t_total) | {"four_pods_share_one_gpu": f"{shared_ok}/{iterations + 2}",
+                                            "latency": "4-pod batch create -> all bound"}
+
+
+def gang8_xgmi(iterations: int = 30, nodes: int = 4) -> dict:
+    """8-rank gangs with XGMIGangAffinity: every gang must land on one node's
+    xGMI mesh. Background load leaves exactly one node able to host a gang."""
+    store = Store()
+    store.create_many("nodes", json.dumps([mi355x_node(f"mi355x-{i}") for i in range(nodes)]))
+    store.create_many("noderesourcetopologies", json.dumps([mi355x_nrt(f"mi355x-{i}") for i in range(nodes)]))
+    s = new_scheduler(store, load_config(flagship_config()), start=True)
+    lat: list[float] = []
+    t_total, pods, colocated = 0.0, 0, 0
+    try:
+        # Background: node i (i < nodes-1) has 1..7 GPUs busy, so a gang of 8
+        # only fits on the last node; partial-fit scores must not split it.
+        bg = []
+        for i in range(nodes - 1):
+            for k in range(1 + (i * 3) % 7):
+                p = make_pod(f"bg-{i}-{k}", "bg", limits={GPU: "1"}, requests={GPU: "1"})
+                p["spec"]["nodeSelector"] = {"kubernetes.io/hostname": f"mi355x-{i}"}
+                bg.append(p)
+        store.create_many("pods", json.dumps(bg))
+        if not _wait(lambda: len(_bound(store, "bg")) == len(bg)):
+            return {"error": "background pods did not bind"}
+        for it in range(iterations + 2):
+            ns = f"g8-{it}"
+            store.create("podgroups", make_pod_group("ranks", ns, 8))
+            pl = [make_pod(f"rank-{r}", ns, pod_group="ranks", limits={GPU: "1"}, requests={GPU: "1"})
+                  for r in range(8)]
+            t0 = time.perf_counter()
+            store.create_many("pods", json.dumps(pl))
+            ok = _wait(lambda: len(_bound(store, ns)) == 8)
+            dt = time.perf_counter() - t0
+            if not ok:
+                return {"error": "gang did not bind"}
+            bound = _bound(store, ns)
+            if len({p["spec"]["nodeName"] for p in bound}) == 1 and \
+                    len({p["metadata"]["annotations"][INDEX_ANNOTATION] for p in bound}) == 8:
+                colocated += 1
+            recs = s.gang_records(True)
+            if it >= 2:
+                t_total += dt
+                pods += 8
+                lat += [(g["bound_us"] - g["first_enqueue_us"]) / 1000.0 for g in recs] or [dt * 1000.0]
+            store.delete_all("pods", ns)
+            store.delete_all("podgroups", ns)
+            _wait(lambda: s.cache_counts()["pods"] == len(bg))
+    finally:
+        s.stop()
+    return _summary(lat, pods, t_total) | {"gangs_on_one_xgmi_node": f"{colocated}/{iterations + 2}",
+                                            "nodes": nodes}
+
+
+def capacity_preemption(iterations: int = 2) -> dict:
+    """Team A borrows all 8 GPUs; team B then claims its guaranteed 4:
+    exactly team A's borrowed GPUs are preempted."""
+    cfg = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
+           "profiles": [{"schedulerName": "default-scheduler", "plugins": {
+               "preFilter": {"enabled": [{"name": "CapacityScheduling"}]},
+               "postFilter": {"enabled": [{"name": "CapacityScheduling"}], "disabled": [{"name": "*"}]},
+               "reserve": {"enabled": [{"name": "CapacityScheduling"}]}}}]}
+    lat: list[float] = []
+    correct = 0
+    for it in range(iterations):
+        store = Store()
+        store.create("nodes", mi355x_node("mi355x-0"))
+        for team in ("team-a", "team-b"):
+            store.create("elasticquotas", make_elastic_quota(f"q-{team}", team, min={GPU: "4", "cpu": "64"},
+                                                             max={GPU: "8", "cpu": "256"}))
+        s = new_scheduler(store, load_config(cfg), start=True)
+        try:
+            store.create_many("pods", json.dumps([make_pod(f"a{i}", "team-a", requests={"cpu": "1"},
+                                                           limits={GPU: "1"}) for i in range(8)]))
+            if not _wait(lambda: len(_bound(store, "team-a")) == 8):
+                return {"error": "team-a did not bind"}
+            t0 = time.perf_counter()
+            store.create_many("pods", json.dumps([make_pod(f"b{i}", "team-b", requests={"cpu": "1"},
+                                                           limits={GPU: "1"}) for i in range(4)]))
+            ok = _wait(lambda: len(_bound(store, "team-b")) == 4, timeout=60)
+            dt = time.perf_counter() - t0
+            if ok:
+                lat.append(dt * 1000.0)
+                correct += int(len(_bound(store, "team-a")) == 4)
+        finally:
+            s.stop()
+    return {"reclaim_ms": [round(x, 1) for x in lat], "p99_ms": round(percentile(lat, 99), 1) if lat else None,
+            "exactly_borrowed_preempted": f"{correct}/{iterations}",
+            "note": "includes upstream pod backoff (1s initial) between preemption and re-scheduling"}
+
+
+def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None) -> dict:
+    """TargetLoadPacking in GPU mode on 8 MI355X nodes whose WatcherMetrics
+    carry the live busy % of this host's amdgpu devices (one physical GPU's
+    utilisation per simulated node; synthetic values without sysfs)."""
+    from ..gpu.telemetry import HostSampler, NodeTelemetry, Sample, publish
+    from ..control.client import LocalClient
+
+    live = []
+    try:
+        live = [b for b, _ in (sampler or HostSampler()).gpu_samples()]
+    except Exception:  # noqa: BLE001 - no amdgpu sysfs
+        live = []
+    source = "amdgpu sysfs gpu_busy_percent" if any(b is not None for b in live) else "synthetic"
+    busy = [(live[i % len(live)] if live and live[i % len(live)] is not None else (i * 13) % 100)
+            for i in range(nodes)]
+    store = Store()
+    store.create_many("nodes", json.dumps([mi355x_node(f"mi355x-{i}") for i in range(nodes)]))
+    c = LocalClient(store)
+    for i in range(nodes):
+        t = NodeTelemetry(f"mi355x-{i}", source=source)
+        t.add(Sample(time.time(), None, None, float(busy[i]), None))
+        publish(c, t.watcher_metrics())
+    cfg = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
+           "profiles": [{"schedulerName": "default-scheduler", "plugins": {
+               "score": {"enabled": [{"name": "TargetLoadPacking"}], "disabled": [{"name": "*"}]}},
+               "pluginConfig": [{"name": "TargetLoadPacking", "args": {"resourceType": "GPU"}}]}]}
+    s = new_scheduler(store, load_config(cfg), start=True)
+    try:
+        _wait(lambda: s.cache_counts()["nodes"] == nodes)
+        first = s.explain(make_pod("probe", "tlp", limits={GPU: "1"}, requests={GPU: "1"}))
+        t0 = time.perf_counter()
+        store.create_many("pods", json.dumps([make_pod(f"p{i}", "tlp", requests={"cpu": "100m"})
+                                              for i in range(pods)]))
+        ok = _wait(lambda: s.stats()["bound"] >= pods)
+        dt = time.perf_counter() - t0
+    finally:
+        s.stop()
+    return {"pods_per_s": round(pods / dt, 1) if ok else None, "metrics_source": source,
+            "node_gpu_busy_pct": busy, "first_gpu_pod_node": first.get("selected"),
+            "tlp_scores": {n: v["TargetLoadPacking*1"] for n, v in (first.get("scores") or {}).items()}}
+
+
+ALL = {"coscheduling_cpu": coscheduling_cpu, "flexgpu_cpx_quarter": flexgpu_cpx_quarter, "gang8_xgmi": gang8_xgmi,
+       "capacity_preemption": capacity_preemption, "trimaran_tlp": trimaran_tlp}
+
+
+def run_all(names=None) -> dict:
+    out = {}
+    for name, fn in ALL.items():
+        if names and name not in names:
+            continue
+        t0 = time.perf_counter()
+        try:
+            out[name] = fn()
+        except Exception as e:  # noqa: BLE001 - a scenario failure is reported, not fatal
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+        out[name]["wall_s"] = round(time.perf_counter() - t0, 2)
+    return out
+
+
+if __name__ == "__main__":
+    print(json.dumps(run_all(), indent=1))
