@@ -1,0 +1,318 @@
+// Native unit tests for the C++ core (no Python in the loop): Quantity, JSON,
+// the GPU ledger's incremental aggregates (checked against a brute-force
+// recomputation over random assignment sequences), the pod heap and
+// scheduling-queue backoff under a fake clock, the timer service, CycleState
+// memo invalidation and store watch replay/expiry.
+//
+// Built by `python -m flex_gpu_scheduler_amd.build_ext --tests` into
+// build/xsched_native_tests and run by tests/test_native_unit.py.
+#include <cstdio>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "api/types.h"
+#include "common/clock.h"
+#include "common/json.h"
+#include "common/quantity.h"
+#include "framework/types.h"
+#include "scheduler/queue.h"
+#include "store/store.h"
+
+using namespace xsched;
+
+namespace {
+
+int g_failed = 0, g_checks = 0;
+#define CHECK(cond)                                                          \
+  do {                                                                       \
+    ++g_checks;                                                              \
+    if (!(cond)) {                                                           \
+      ++g_failed;                                                            \
+      std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #cond); \
+    }                                                                        \
+  } while (0)
+#define CHECK_EQ(a, b) CHECK((a) == (b))
+
+struct TestCase {
+  const char* name;
+  std::function<void()> fn;
+};
+std::vector<TestCase>& tests() {
+  static std::vector<TestCase> t;
+  return t;
+}
+struct Reg {
+  Reg(const char* n, std::function<void()> f) { tests().push_back({n, std::move(f)}); }
+};
+#define TEST(name)            \
+  void name();                \
+  Reg reg_##name(#name, name); \
+  void name()
+
+// ------------------------------------------------------------------ Quantity
+TEST(quantity_parse_format) {
+  CHECK_EQ(Quantity::parse("1536Mi").str(), "1536Mi");
+  CHECK_EQ(Quantity::parse("2048Mi").str(), "2Gi");
+  CHECK_EQ(Quantity::parse("1.5").str(), "1500m");
+  CHECK_EQ(Quantity::parse("500m").milli_value(), 500);
+  CHECK_EQ(Quantity::parse("500m").value(), 1);  // rounds up
+  CHECK_EQ(Quantity::parse("288Gi").value(), 288LL << 30);
+  Quantity a = Quantity::parse("1"), b = Quantity::parse("250m");
+  a.add(b);
+  CHECK_EQ(a.milli_value(), 1250);
+  a.sub(Quantity::parse("2"));
+  CHECK_EQ(a.sign(), -1);
+  Quantity bad;
+  CHECK(!Quantity::try_parse("1.2.3", &bad));
+}
+
+// ---------------------------------------------------------------------- JSON
+TEST(json_roundtrip_and_merge_patch) {
+  Json j = Json::parse(R"({"a":[1,2,{"b":null}],"c":"x\"y","d":{"e":1.5,"f":true}})");
+  CHECK_EQ(Json::parse(j.dump()).dump(), j.dump());
+  Json p = Json::parse(R"({"c":null,"d":{"e":2,"g":"new"}})");
+  j.merge_patch(p);
+  CHECK(!j.get("c"));
+  CHECK_EQ(j["d"]["e"].as_int(), 2);
+  CHECK_EQ(j["d"]["g"].as_string(), "new");
+  CHECK(j["d"]["f"].as_bool());
+  Json from = Json::parse(R"({"a":1,"b":{"c":2,"d":3}})"), to = Json::parse(R"({"a":1,"b":{"c":5},"e":[1]})");
+  Json diff = Json::diff_merge_patch(from, to);
+  Json applied = from;
+  applied.merge_patch(diff);
+  CHECK_EQ(applied.dump(), to.dump());
+}
+
+// ----------------------------------------------------------------- GpuLedger
+GpuLedger::GpuFree brute(const GpuLedger& L, int g) {
+  GpuLedger::GpuFree f;
+  if (L.monopoly[g] > 0) return f;
+  bool untouched = true;
+  for (int p = 0; p < L.parts[g]; ++p) {
+    const auto& s = L.slots[L.offset[g] + p];
+    if (s.exclusive || s.used_mem || s.mem_pods) untouched = false;
+    if (!s.exclusive && !s.used_mem && !s.mem_pods) {
+      ++f.free_slots;
+      f.xcds += L.xcds_per_part(g);
+    }
+    if (!s.exclusive) {
+      f.mem += L.part_mem(g) - s.used_mem;
+      f.max_slot_mem = std::max(f.max_slot_mem, L.part_mem(g) - s.used_mem);
+    }
+  }
+  f.whole = L.parts[g] == 1 && untouched;
+  return f;
+}
+
+TEST(gpu_ledger_aggregates_match_bruteforce) {
+  std::mt19937 rng(7);
+  for (int trial = 0; trial < 50; ++trial) {
+    Node n;
+    n.gpu_count = 8;
+    n.gpu_memory_per_gpu = 288;
+    const int modes[] = {1, 2, 4, 8};
+    for (int g = 0; g < 8; ++g) {
+      n.gpu_partitions.push_back(modes[rng() % 4]);
+      n.gpu_numa.push_back(g / 4);
+    }
+    GpuLedger L;
+    L.init(n);
+    std::vector<GpuAssignment> live;
+    for (int step = 0; step < 200; ++step) {
+      if (!live.empty() && rng() % 3 == 0) {
+        size_t i = rng() % live.size();
+        L.apply(live[i], -1);
+        live.erase(live.begin() + static_cast<long>(i));
+      } else {
+        GpuAssignment a;
+        int g = static_cast<int>(rng() % 8);
+        switch (rng() % 3) {
+          case 0:
+            a.kind = GpuAssignment::Kind::WholeGpu;
+            a.gpus = {g};
+            break;
+          case 1:
+            a.kind = GpuAssignment::Kind::Partition;
+            a.gpus = {g};
+            a.partitions = {{g, static_cast<int>(rng() % static_cast<unsigned>(n.gpu_partitions[g]))}};
+            break;
+          default:
+            a.kind = GpuAssignment::Kind::Memory;
+            a.gpus = {g};
+            a.partitions = {{g, static_cast<int>(rng() % static_cast<unsigned>(n.gpu_partitions[g]))}};
+            a.memory = 1 + rng() % 20;
+        }
+        L.apply(a, +1);
+        live.push_back(a);
+      }
+      int whole = 0, xcds = 0;
+      int64_t mem = 0;
+      int zw[2] = {0, 0}, zx[2] = {0, 0};
+      for (int g = 0; g < 8; ++g) {
+        auto b = brute(L, g);
+        CHECK_EQ(L.free[g].whole, b.whole);
+        CHECK_EQ(L.free[g].free_slots, b.free_slots);
+        CHECK_EQ(L.free[g].xcds, b.xcds);
+        CHECK_EQ(L.free[g].mem, b.mem);
+        CHECK_EQ(L.free[g].max_slot_mem, b.max_slot_mem);
+        whole += b.whole;
+        xcds += b.xcds;
+        mem += b.mem;
+        zw[g / 4] += b.whole;
+        zx[g / 4] += b.xcds;
+      }
+      CHECK_EQ(L.free_gpus(), whole);
+      CHECK_EQ(L.free_xcds(), xcds);
+      CHECK_EQ(L.free_memory(), mem);
+      CHECK_EQ(L.zone_whole[0], zw[0]);
+      CHECK_EQ(L.zone_xcds[1], zx[1]);
+    }
+  }
+}
+
+// --------------------------------------------------------------- PodHeap/queue
+PodPtr mk_pod(const std::string& name, int prio) {
+  Json j = Json::parse(R"({"metadata":{"namespace":"d","name":")" + name + R"(","uid":")" + name +
+                       R"("},"spec":{"priority":)" + std::to_string(prio) + R"(,"containers":[{"name":"c"}]}})");
+  return Pod::from_json(j);
+}
+
+TEST(pod_heap_orders_and_updates) {
+  PodHeap h([](const QueuedPodInfo& a, const QueuedPodInfo& b) { return a.pod->priority > b.pod->priority; });
+  for (int i = 0; i < 20; ++i) {
+    auto q = std::make_shared<QueuedPodInfo>();
+    q->pod = mk_pod("p" + std::to_string(i), (i * 7) % 11);
+    h.push(q);
+  }
+  auto upd = std::make_shared<QueuedPodInfo>();
+  upd->pod = mk_pod("p3", 100);
+  h.push(upd);  // update in place
+  CHECK_EQ(h.size(), 20u);
+  CHECK_EQ(h.pop()->pod->name(), "p3");
+  int last = 1 << 30;
+  while (!h.empty()) {
+    int p = h.pop()->pod->priority;
+    CHECK(p <= last);
+    last = p;
+  }
+}
+
+TEST(queue_backoff_and_unschedulable_flush) {
+  auto clock = std::make_shared<FakeClock>();
+  Nominator nom;
+  QueueOptions o;
+  SchedulingQueue q([](const QueuedPodInfo& a, const QueuedPodInfo& b) { return a.pod->priority > b.pod->priority; },
+                    clock, o, &nom);
+  q.add(mk_pod("a", 1));
+  auto qa = q.pop(0);
+  CHECK(qa && qa->pod->name() == "a");
+  qa->unschedulable_plugins = {"X"};
+  q.add_unschedulable_if_not_present(qa, q.scheduling_cycle());
+  CHECK_EQ(q.counts().unschedulable, 1u);
+  // An event nobody registered leaves it where it is; a wildcard moves it to backoff.
+  q.move_all_to_active_or_backoff(ClusterEvent{"*", kAll, ""});
+  CHECK_EQ(q.counts().unschedulable + q.counts().backoff + q.counts().active, 1u);
+  q.flush_backoff_completed();
+  clock->advance_us(1'100'000);
+  q.flush_backoff_completed();
+  auto again = q.pop(0);
+  CHECK(again && again->pod->name() == "a");
+  // Leftover flush after 60 s.
+  again->unschedulable_plugins = {"Y"};
+  q.add_unschedulable_if_not_present(again, q.scheduling_cycle());
+  clock->advance_us(61'000'000);
+  q.flush_unschedulable_leftover();
+  q.flush_backoff_completed();
+  CHECK_EQ(q.counts().unschedulable, 0u);
+  q.close();
+}
+
+// -------------------------------------------------------------- TimerService
+TEST(timers_fire_in_deadline_order_with_fake_clock) {
+  auto clock = std::make_shared<FakeClock>();
+  TimerService ts(clock);
+  std::vector<int> fired;
+  std::mutex mu;
+  ts.schedule_after(300, [&] { std::lock_guard<std::mutex> g(mu); fired.push_back(3); });
+  ts.schedule_after(100, [&] { std::lock_guard<std::mutex> g(mu); fired.push_back(1); });
+  uint64_t c = ts.schedule_after(200, [&] { std::lock_guard<std::mutex> g(mu); fired.push_back(2); });
+  CHECK(ts.cancel(c));
+  clock->advance_us(1000);
+  ts.poke_and_drain();
+  std::lock_guard<std::mutex> g(mu);
+  CHECK_EQ(fired.size(), 2u);
+  if (fired.size() == 2) {
+    CHECK_EQ(fired[0], 1);
+    CHECK_EQ(fired[1], 3);
+  }
+  ts.stop();
+}
+
+// ---------------------------------------------------------------- CycleState
+struct IntState : StateData {
+  int v = 0;
+  explicit IntState(int x) : v(x) {}
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<IntState>(v); }
+};
+
+TEST(cycle_state_memo_invalidated_by_writes) {
+  CycleState s;
+  s.write("k", std::make_shared<IntState>(1));
+  CHECK_EQ(s.read_as<IntState>("k")->v, 1);
+  s.write("k", std::make_shared<IntState>(2));
+  CHECK_EQ(s.read_as<IntState>("k")->v, 2);
+  auto c = s.clone();
+  CHECK_EQ(c->read_as<IntState>("k")->v, 2);
+  c->write("k", std::make_shared<IntState>(3));
+  CHECK_EQ(s.read_as<IntState>("k")->v, 2);
+  CHECK_EQ(c->read_as<IntState>("k")->v, 3);
+  s.erase("k");
+  CHECK(s.read_as<IntState>("k") == nullptr);
+  // Different keys, same type: the memo keys on the name too.
+  s.write("a", std::make_shared<IntState>(10));
+  s.write("b", std::make_shared<IntState>(20));
+  CHECK_EQ(s.read_as<IntState>("a")->v, 10);
+  CHECK_EQ(s.read_as<IntState>("b")->v, 20);
+}
+
+// --------------------------------------------------------------------- Store
+TEST(store_watch_replay_and_expiry) {
+  ObjectStore st;
+  st.create("pods", Json::parse(R"({"metadata":{"name":"a","namespace":"d"}})"));
+  int64_t rv = st.resource_version();
+  st.create("pods", Json::parse(R"({"metadata":{"name":"b","namespace":"d"}})"));
+  auto w = st.watch({"pods"}, "d", rv);
+  auto evs = w->next(100, 10);
+  CHECK_EQ(evs.size(), 1u);
+  if (!evs.empty()) CHECK_EQ((*evs[0].obj)["metadata"]["name"].as_string(), "b");
+  st.unwatch(w);
+  Json patch = Json::parse(R"({"metadata":{"resourceVersion":"1"},"spec":{"x":1}})");
+  bool conflict = false;
+  try {
+    st.patch("pods", "d", "b", patch);
+  } catch (const StoreError& e) {
+    conflict = e.code() == 409;
+  }
+  CHECK(conflict);
+  bool dup = false;
+  try {
+    st.create("pods", Json::parse(R"({"metadata":{"name":"a","namespace":"d"}})"));
+  } catch (const StoreError& e) {
+    dup = e.code() == 409;
+  }
+  CHECK(dup);
+}
+
+}  // namespace
+
+int main() {
+  for (const auto& t : tests()) {
+    int before = g_failed;
+    t.fn();
+    std::printf("[%s] %s\n", g_failed == before ? " OK " : "FAIL", t.name);
+  }
+  std::printf("%d checks, %d failed, %zu tests\n", g_checks, g_failed, tests().size());
+  return g_failed == 0 ? 0 : 1;
+}

@@ -155,6 +155,25 @@ def build_prof(verbose: bool = True, gprof: bool = True) -> Path:
     return out
 
 
+def build_tests(verbose: bool = True) -> Path:
+    """Native unit-test binary (csrc/tests/native_tests.cc)."""
+    # Same flags as the extension's objects, so the core objects are shared
+    # with build/core (no second compile of the core).
+    includes = [str(CSRC)]
+    objs = build_objects(core_sources() + [CSRC / "tests" / "native_tests.cc"], BUILD / "core", [], includes)
+    out = BUILD / "xsched_native_tests"
+    newest = max(o.stat().st_mtime for o in objs)
+    if out.exists() and out.stat().st_mtime >= newest:
+        return out
+    cmd = ["g++", "-pthread", *[str(o) for o in objs], "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native tests link failed:\n{r.stderr[-8000:]}")
+    if verbose:
+        print(f"[build_ext] built {out.relative_to(ROOT)}")
+    return out
+
+
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--core", action="store_true")
@@ -162,7 +181,11 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--tsan", action="store_true")
     ap.add_argument("--prof", action="store_true")
     ap.add_argument("--stress", action="store_true")
+    ap.add_argument("--tests", action="store_true")
     a = ap.parse_args(argv)
+    if a.tests:
+        build_tests()
+        return 0
     if a.prof or a.stress:
         build_prof(gprof=a.prof)
         return 0
