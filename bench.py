@@ -57,6 +57,9 @@ def main() -> int:
         health = pr.health(ctx.local_rank)
         if not health["healthy"]:
             raise SystemExit(f"GPU {ctx.local_rank} failed the checksum health test: {health}")
+        mfma = pr.mfma_check(ctx.local_rank)
+        if not mfma["healthy"]:
+            raise SystemExit(f"GPU {ctx.local_rank} failed the MFMA tile check: {mfma}")
         hbm_gib = max(1, int(props["totalGlobalMem"]) // (1 << 30))
         extras["gpu"] = {"name": props.get("gcnArchName"), "computeUnits": props.get("computeUnits"),
                          "hbm_gib": hbm_gib}

@@ -231,11 +231,14 @@ class NodeAgent:
 
 
 def hip_health_fn() -> Callable[[int], bool]:
-    """Health callback backed by the HIP probe (pattern + checksum per GPU)."""
+    """Health callback backed by the HIP probes (HBM pattern + checksum and an
+    MFMA tile check per GPU)."""
     from ..ops.hip_probe import probe
 
     p = probe()
-    return lambda dev: bool(p.health(dev)["healthy"])
+    # HBM pattern/checksum and an exact-integer MFMA tile: a GPU whose matrix
+    # cores mis-compute is withheld even if its memory checks out.
+    return lambda dev: bool(p.health(dev)["healthy"]) and bool(p.mfma_check(dev)["healthy"])
 
 
 def run_forever(agent: NodeAgent) -> None:  # pragma: no cover - CLI

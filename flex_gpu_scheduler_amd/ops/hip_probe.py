@@ -1,9 +1,12 @@
-"""ctypes front-end for the HIP/CDNA4 device probes (csrc/hip/hbm_probe.hip).
+"""ctypes front-end for the HIP/CDNA4 device probes (csrc/hip/hbm_probe.hip,
+csrc/hip/mfma_probe.hip).
 
 The probes are what the node agent runs before advertising an MI355X as
 schedulable: device properties, HBM streaming bandwidth (optionally with a
 partition-sized CU budget), an XCD census that verifies the compute-partition
-mode, and a checksum health test.
+mode, a checksum health test, an exact-integer MFMA tile check of the matrix
+cores and the dense bf16 MFMA throughput of the whole GPU or of one
+partition's XCDs.
 """
 from __future__ import annotations
 
@@ -48,6 +51,11 @@ class HipProbe:
                                     ctypes.POINTER(ctypes.c_int)]
         L.xs_health_check.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_ulonglong),
                                       ctypes.POINTER(ctypes.c_ulonglong)]
+        L.xs_mfma_last_error.restype = ctypes.c_char_p
+        L.xs_mfma_check.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.xs_mfma_peak.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_int)]
 
     def _err(self, rc: int, what: str) -> ProbeError:
         return ProbeError(f"{what} failed ({rc}): {self.lib.xs_last_error().decode(errors='replace')}")
@@ -119,6 +127,22 @@ class HipProbe:
         if rc < 0:
             raise self._err(rc, "health_check")
         return {"healthy": rc == 0, "device_sum": d.value, "host_sum": h.value}
+
+
+    def mfma_check(self, dev: int = 0, k: int = 64) -> dict:
+        """C[32x32] = A·B through v_mfma_f32_32x32x16_bf16 on exact integers."""
+        rc = self.lib.xs_mfma_check(dev, k)
+        if rc < 0:
+            raise ProbeError(f"mfma_check failed: {self.lib.xs_mfma_last_error().decode(errors='replace')}")
+        return {"healthy": rc == 0, "mismatches": int(rc), "k": k}
+
+    def mfma_peak(self, dev: int = 0, xcd_mask: int = 0xFF, iters: int = 4096, blocks: int = 0) -> dict:
+        """Dense bf16 MFMA TFLOP/s on the XCDs of `xcd_mask`."""
+        tf, ms, act = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        rc = self.lib.xs_mfma_peak(dev, iters, xcd_mask, blocks, ctypes.byref(tf), ctypes.byref(ms), ctypes.byref(act))
+        if rc != 0:
+            raise ProbeError(f"mfma_peak failed: {self.lib.xs_mfma_last_error().decode(errors='replace')}")
+        return {"tflops": tf.value, "ms": ms.value, "active_blocks": act.value, "xcd_mask": xcd_mask}
 
 
 _probe: HipProbe | None = None

@@ -23,6 +23,12 @@ def main() -> int:
             bw = pr.hbm_bandwidth_xcd(dev, mask, 2 << 30, 10, mode)
             parts.append({"partition": label, "mode": mode, "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4)})
     out["partitions"] = parts
+    out["mfma_check"] = pr.mfma_check(dev, 256)
+    out["mfma_bf16"] = []
+    for label, mask in (("cpx-1xcd", 0x01), ("qpx-2xcd", 0x03), ("dpx-4xcd", 0x0F), ("spx-8xcd", 0xFF)):
+        r = pr.mfma_peak(dev, mask, iters=8192)
+        out["mfma_bf16"].append({"partition": label, "TFLOPs": round(r["tflops"], 1), "ms": round(r["ms"], 3),
+                                 "active_blocks": r["active_blocks"]})
     print(json.dumps(out))
     return 0
 

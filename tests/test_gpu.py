@@ -90,3 +90,27 @@ def test_bench_one_gpu_json_contract():
               "vs_baseline", "dtype", "data", "config"):
         assert k in line
     assert line["value"] > 0 and line["config"]["gpu"]["name"].startswith("gfx950")
+
+
+@pytest.mark.gpu
+def test_mfma_tile_exact():
+    """v_mfma_f32_32x32x16_bf16 on exact integers matches the integer GEMM
+    bit for bit (A/B fragment and C/D lane maps of gfx950)."""
+    from flex_gpu_scheduler_amd.ops.hip_probe import probe
+    for k in (16, 64, 256):
+        r = probe().mfma_check(0, k)
+        assert r["mismatches"] == 0, r
+
+
+@pytest.mark.gpu
+def test_mfma_peak_scales_with_xcds():
+    from flex_gpu_scheduler_amd.ops.hip_probe import probe
+    p = probe()
+    full = p.mfma_peak(0, 0xFF, iters=8192)
+    one = p.mfma_peak(0, 0x01, iters=8192)
+    assert full["active_blocks"] == 2 * p.props(0)["computeUnits"]
+    # Dense bf16: well above the f32 vector rate, below the 2.5 PF spec peak.
+    assert 300.0 < full["tflops"] < 2600.0, full
+    # One XCD is an eighth of the chip (CPX partition budget).
+    ratio = one["tflops"] / full["tflops"]
+    assert 0.08 < ratio < 0.2, (one, full)
