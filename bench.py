@@ -100,8 +100,11 @@ def main() -> int:
     if ctx.distributed and ctx.cuda:
         from flex_gpu_scheduler_amd.parallel.rccl_probe import allreduce_sweep
 
-        res = allreduce_sweep()
-        extras["rccl_allreduce"] = [{"MiB": r.bytes >> 20, "busbw_GBps": round(r.busbw_gbps, 1)} for r in res]
+        try:
+            res = allreduce_sweep()
+            extras["rccl_allreduce"] = [{"MiB": r.bytes >> 20, "busbw_GBps": round(r.busbw_gbps, 1)} for r in res]
+        except Exception as e:  # noqa: BLE001 - the probe is informational, never fatal
+            extras["rccl_allreduce_error"] = f"{type(e).__name__}: {e}"
 
     value = pods_total / t_max if t_max > 0 else 0.0
     if ctx.rank == 0 and not args.no_scenarios:
