@@ -92,6 +92,7 @@ SchedulerOptions SchedulerOptions::from_json(const Json& j) {
   SchedulerOptions o;
   o.parallelism = static_cast<int>(j["parallelism"].as_int(o.parallelism));
   o.bind_workers = static_cast<int>(j["bindWorkers"].as_int(o.bind_workers));
+  o.parallel_inline_below = static_cast<int>(j["parallelInlineBelow"].as_int(o.parallel_inline_below));
   o.percentage_of_nodes_to_score = static_cast<int>(j["percentageOfNodesToScore"].as_int(0));
   if (j["podInitialBackoffSeconds"].is_number())
     o.pod_initial_backoff_us = static_cast<int64_t>(j["podInitialBackoffSeconds"].as_double() * 1e6);
@@ -137,7 +138,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
   rng_.seed(opts_.seed ? opts_.seed : static_cast<uint64_t>(clock_->now_us()));
   tracer_.enable(opts_.trace);
   timers_ = std::make_unique<TimerService>(clock_);
-  parallelizer_ = std::make_unique<Parallelizer>(opts_.parallelism);
+  parallelizer_ = std::make_unique<Parallelizer>(opts_.parallelism, opts_.parallel_inline_below);
   metrics_ = std::make_unique<Metrics>();
   cache_ = std::make_unique<SchedulerCache>(clock_, opts_.assumed_pod_ttl_us);
   informers_ = std::make_unique<Informers>();

@@ -71,6 +71,7 @@ class Executor {
 
 struct SchedulerOptions {
   int parallelism = 16;
+  int parallel_inline_below = 128;  // node count under which Filter/Score run on the scheduling thread
   int bind_workers = 16;
   int percentage_of_nodes_to_score = 0;
   int64_t pod_initial_backoff_us = 1'000'000;
