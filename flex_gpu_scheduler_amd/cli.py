@@ -223,7 +223,14 @@ def cmd_node_agent(args) -> int:
                       heartbeat=args.heartbeat, telemetry_period=args.telemetry_period,
                       publish_metrics=not args.no_telemetry, reserved_cpu=args.reserved_cpu,
                       reserved_memory_gib=args.reserved_memory_gib,
-                      health_fn=hip_health_fn() if args.health_probe else None).start()
+                      health_fn=hip_health_fn() if args.health_probe else None,
+                      kubelet_managed=args.kubelet_managed).start()
+    if args.device_plugin:
+        from .control.device_plugin import start_plugins
+
+        agent.device_plugins = start_plugins(agent.host, client, agent.name, socket_dir=args.device_plugin_dir)
+        for dp in agent.device_plugins:
+            dp.set_unhealthy(agent.unhealthy)
     print(json.dumps({"node": agent.name, "gpus": len(agent.host.gpus)}), flush=True)
     stop = threading.Event()
     _wait_forever(stop)
@@ -340,6 +347,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--health-probe", action="store_true", help="run the HIP health probe on each GPU")
     p.add_argument("--reserved-cpu", type=int, default=0)
     p.add_argument("--reserved-memory-gib", type=int, default=0)
+    p.add_argument("--device-plugin", action="store_true",
+                   help="serve the kubelet device-plugin API for amd.com/gpu, gpu-xcd and gpu-memory")
+    p.add_argument("--device-plugin-dir", default="/var/lib/kubelet/device-plugins/")
+    p.add_argument("--kubelet-managed", action="store_true",
+                   help="leave amd.com/* capacity to kubelet (device plugins) instead of writing node status")
     p.set_defaults(fn=cmd_node_agent)
 
     p = sub.add_parser("load-watcher", help="serve GET /watcher")

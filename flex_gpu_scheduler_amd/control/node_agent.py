@@ -46,7 +46,7 @@ class NodeAgent:
     def __init__(self, client: Client, node_name: str, *, host_fn: Callable[[], HostInfo] | None = None,
                  root: str = "/", labels: dict | None = None, reserved_cpu: int = 0, reserved_memory_gib: int = 0,
                  heartbeat: float = 10.0, telemetry_period: float = 60.0, publish_metrics: bool = True,
-                 health_fn: Callable[[int], bool] | None = None, sampler=None):
+                 health_fn: Callable[[int], bool] | None = None, sampler=None, kubelet_managed: bool = False):
         self.client, self.name = client, node_name
         self.host_fn = host_fn or (lambda: discover_host(root))
         self.labels = dict(labels or {})
@@ -61,6 +61,10 @@ class NodeAgent:
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self.host: HostInfo | None = None
+        # With a kubelet on the node, the device plugins advertise amd.com/*
+        # capacity; the agent must not write those fields (kubelet owns them).
+        self.kubelet_managed = kubelet_managed
+        self.device_plugins: list = []
 
     # --------------------------------------------------------------- objects
     def check_health(self, host: HostInfo) -> set[int]:
@@ -112,6 +116,10 @@ class NodeAgent:
         cap[GPU_XCD] = str(XCDS_PER_GPU * len(host.gpus))
         cap[GPU_MEMORY] = str(sum(g.hbm_gib for g in host.gpus))
         node["status"]["capacity"] = cap
+        if self.kubelet_managed:
+            for k in (GPU, GPU_XCD, GPU_MEMORY):
+                node["status"]["allocatable"].pop(k, None)
+                node["status"]["capacity"].pop(k, None)
         node["status"]["conditions"] = [self._ready_condition()]
         node["status"]["nodeInfo"] = {"architecture": "amd64", "operatingSystem": "linux",
                                       "kubeletVersion": "v1.23.3-xsched-agent"}
@@ -176,6 +184,9 @@ class NodeAgent:
     def sync(self) -> HostInfo:
         host = self.host_fn()
         self.unhealthy = self.check_health(host)
+        for dp in self.device_plugins:
+            dp.host = host
+            dp.set_unhealthy(self.unhealthy)
         self._upsert("nodes", self.build_node(host, self.unhealthy), keep_spec=True)
         self._upsert("noderesourcetopologies", self.build_nrt(host, self.unhealthy), keep_spec=False)
         self.host = host
