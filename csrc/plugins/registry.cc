@@ -14,6 +14,7 @@ void link_nrt_plugin();
 void link_trimaran_plugins();
 void link_sample_plugins();
 void link_topology_plugins();
+void link_crossnode_plugin();
 
 void register_builtin_plugins() {
   link_intree_plugins();
@@ -26,6 +27,7 @@ void register_builtin_plugins() {
   link_trimaran_plugins();
   link_sample_plugins();
   link_topology_plugins();
+  link_crossnode_plugin();
 }
 
 }  // namespace xsched

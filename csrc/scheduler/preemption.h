@@ -50,9 +50,11 @@ class Evaluator {
   std::vector<Candidate> dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
                                  const std::vector<PDBPtr>& pdbs, int offset, int num_candidates);
   static std::string pick_one_node(const std::vector<Candidate>& cands);
+  // prepareCandidate: reject waiting victims, delete the others, clear
+  // lower-priority nominations on the node (also used by CrossNodePreemption).
+  Status prepare_candidate(const Candidate& c, const Pod& pod);
 
  private:
-  Status prepare_candidate(const Candidate& c, const Pod& pod);
   std::string plugin_;
   Handle& h_;
   PreemptionPolicy* policy_;

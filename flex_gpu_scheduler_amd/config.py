@@ -55,6 +55,7 @@ PLUGIN_POINTS: dict[str, tuple[str, ...]] = {
     "TargetLoadPacking": ("score",),
     "LoadVariationRiskBalancing": ("score",),
     "PreemptionToleration": ("postFilter",),
+    "CrossNodePreemption": ("postFilter",),
     "PodState": ("score",),
     "QOSSort": ("queueSort",),
 }
@@ -182,6 +183,16 @@ def default_plugin_args(name: str, args: dict | None) -> dict:
             raise ConfigError(f"{name}Args.minCandidateNodesPercentage must be in [0, 100]")
         if n < 0 or (p == 0 and n == 0):
             raise ConfigError(f"{name}Args: both minCandidateNodes values cannot be zero")
+    elif name == "CrossNodePreemption":
+        # No Args type upstream (the plugin is commented out); these bound the
+        # minimum-victim subset search (csrc/plugins/crossnode.cc).
+        _strict(name, a, {"maxVictims", "maxPoolPods", "maxCombinations"})
+        a.setdefault("maxVictims", 3)
+        a.setdefault("maxPoolPods", 32)
+        a.setdefault("maxCombinations", 20000)
+        for k in ("maxVictims", "maxPoolPods", "maxCombinations"):
+            if int(a[k]) < 1:
+                raise ConfigError(f"{name}Args.{k} must be >= 1")
     elif name == "FlexGPU":
         _strict(name, a, {"gpuResourceName", "memoryResourceName", "xcdResourceName", "indexAnnotationKey",
                           "partitionAnnotationKey"})
