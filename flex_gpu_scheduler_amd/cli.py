@@ -139,6 +139,37 @@ def _watcher_addresses(cfg) -> set[str]:
     return out
 
 
+def _library_watchers(cfg, remote, store_client) -> list:
+    """load-watcher library mode for Trimaran plugins without `watcherAddress`
+    (targetloadpacking.go:125-138 starts watcher.NewWatcher over the
+    configured metricProvider). Prometheus/SignalFx are started as given;
+    KubernetesMetricsServer only if the cluster serves metrics.k8s.io (an
+    in-process cluster relies on the node agents' own documents instead)."""
+    from .gpu.providers import K8S_CLIENT_NAME, KubernetesMetricsServerProvider, Watcher, new_provider
+
+    seen, out = set(), []
+    for p in cfg.profiles:
+        for name in ("TargetLoadPacking", "LoadVariationRiskBalancing"):
+            a = p.plugin_config.get(name)
+            if a is None or name not in p.plugins.get("score", []) or a.get("watcherAddress"):
+                continue
+            mp = a.get("metricProvider") or {}
+            key = (mp.get("type"), mp.get("address"))
+            if key in seen:
+                continue
+            seen.add(key)
+            if (mp.get("type") or K8S_CLIENT_NAME) == K8S_CLIENT_NAME:
+                if not hasattr(remote, "request") or not KubernetesMetricsServerProvider(remote).health():
+                    continue
+            try:
+                prov = new_provider(mp, remote)
+            except ValueError as e:
+                log.error("%s metricProvider: %s", name, e)
+                continue
+            out.append(Watcher(prov).publish_to(store_client, f"load-watcher-{prov.name.lower()}"))
+    return out
+
+
 def cmd_scheduler(args) -> int:
     from .config import load_config
     from .control.client import LocalClient
@@ -155,6 +186,7 @@ def cmd_scheduler(args) -> int:
     rs = RemoteScheduler(remote, cfg, **options)
     fetchers = [WatcherFetcher(a, LocalClient(rs.store), name=f"load-watcher-{i}")
                 for i, a in enumerate(sorted(_watcher_addresses(cfg)))]
+    fetchers += _library_watchers(cfg, remote, LocalClient(rs.store))
     host, port = _hostport(args.metrics_bind_address, 10259)
     http = ServiceHTTP(host, port)
     http.add_metrics(rs.scheduler.metrics_text)
@@ -242,14 +274,26 @@ def cmd_load_watcher(args) -> int:
     from .control.httpserve import ServiceHTTP
     from .gpu.telemetry import LoadWatcherService
 
-    client = _client(args)
     host, port = _hostport(args.bind_address, args.port)
     http = ServiceHTTP(host, port)
-    LoadWatcherService(client, http)
+    watcher = None
+    if args.provider:
+        # Standalone load-watcher over an external metrics source
+        # (load-watcher's own binary: watcher.NewWatcher(client).StartWatching()).
+        from .gpu.providers import Watcher, new_provider
+
+        mp = {"type": args.provider, "address": args.provider_address, "token": args.provider_token,
+              "insecureSkipVerify": args.insecure_skip_verify}
+        client = _client(args) if args.provider == "KubernetesMetricsServer" else None
+        watcher = Watcher(new_provider(mp, client), period=args.period).serve(http).start()
+    else:
+        LoadWatcherService(_client(args), http)
     http.start()
     print(json.dumps({"load-watcher": http.url + "/watcher"}), flush=True)
     stop = threading.Event()
     _wait_forever(stop)
+    if watcher:
+        watcher.stop()
     http.stop()
     return 0
 
@@ -358,6 +402,12 @@ def build_parser() -> argparse.ArgumentParser:
     conn(p)
     p.add_argument("--bind-address", default="127.0.0.1")
     p.add_argument("--port", type=int, default=2020)
+    p.add_argument("--provider", choices=["KubernetesMetricsServer", "Prometheus", "SignalFx"],
+                   help="library-mode watcher over this metrics source (default: serve the node agents' documents)")
+    p.add_argument("--provider-address", default="")
+    p.add_argument("--provider-token", default="")
+    p.add_argument("--insecure-skip-verify", action="store_true")
+    p.add_argument("--period", type=float, default=60.0, help="fetch period in seconds (load-watcher: 1 minute)")
     p.set_defaults(fn=cmd_load_watcher)
 
     p = sub.add_parser("explain", help="dry-run pods against the cluster")
