@@ -8,7 +8,10 @@
   apiserver    the HTTP API server over the native store (envtest analog),
                with JSON checkpoint/restore of all objects
   node-agent   MI355X discovery -> Node/NRT/telemetry publisher
-  load-watcher GET /watcher over the published WatcherMetrics (:2020)
+  manager      controller-runtime style PodGroup/ElasticQuota reconcilers
+               (the kustomize scaffold's /manager, deploy/config)
+  load-watcher GET /watcher over the published WatcherMetrics (:2020), or a
+               library-mode watcher over metrics-server/Prometheus/SignalFx
   explain      dry-run one pod against the live cluster and print filter
                verdicts, per-plugin scores and the chosen node
   apply        create/replace objects from YAML/JSON files (a tiny kubectl)
@@ -242,6 +245,35 @@ def cmd_controller(args) -> int:
     return 0
 
 
+def cmd_manager(args) -> int:
+    """controller-runtime style manager (the `/manager` binary of the
+    reference's config/manager/manager.yaml): PodGroup + ElasticQuota
+    reconcilers, /healthz and /readyz on --health-probe-bind-address,
+    controller-runtime metrics on --metrics-bind-address."""
+    from .control.httpserve import ServiceHTTP
+    from .control.runtime import ElasticQuotaReconciler, Manager, PodGroupReconciler
+
+    client = _client(args)
+    probe = ServiceHTTP(*_hostport(args.health_probe_bind_address, 8081))
+    metrics = ServiceHTTP(*_hostport(args.metrics_bind_address, 8080))
+    mgr = Manager(client, leader_election=args.leader_elect, leader_election_id=args.leader_election_id,
+                  leader_election_namespace=args.leader_election_namespace,
+                  identity=f"{socket.gethostname()}_{os.getpid()}", probe_http=probe, metrics_http=metrics)
+    mgr.add(PodGroupReconciler(client)).add(ElasticQuotaReconciler(client))
+    probe.start()
+    metrics.start()
+    mgr.start()
+    print(json.dumps({"manager": [c.name for c in mgr.controllers], "probes": probe.url, "metrics": metrics.url}),
+          flush=True)
+    stop = threading.Event()
+    threading.Thread(target=lambda: (mgr.wait_stopped(), stop.set()), daemon=True).start()
+    _wait_forever(stop)
+    mgr.stop()
+    probe.stop()
+    metrics.stop()
+    return 0
+
+
 def cmd_node_agent(args) -> int:
     from .control.node_agent import NodeAgent, hip_health_fn
     from .gpu.discovery import discover_host, fake_host
@@ -397,6 +429,15 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--kubelet-managed", action="store_true",
                    help="leave amd.com/* capacity to kubelet (device plugins) instead of writing node status")
     p.set_defaults(fn=cmd_node_agent)
+
+    p = sub.add_parser("manager", help="controller-runtime style PodGroup/ElasticQuota reconcilers (kustomize deploy)")
+    conn(p)
+    p.add_argument("--leader-elect", action="store_true")
+    p.add_argument("--leader-election-id", default="sched-plugins-manager")
+    p.add_argument("--leader-election-namespace", default="kube-system")
+    p.add_argument("--health-probe-bind-address", default=":8081")
+    p.add_argument("--metrics-bind-address", default="127.0.0.1:8080")
+    p.set_defaults(fn=cmd_manager)
 
     p = sub.add_parser("load-watcher", help="serve GET /watcher")
     conn(p)
