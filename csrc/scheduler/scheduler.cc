@@ -102,6 +102,7 @@ SchedulerOptions SchedulerOptions::from_json(const Json& j) {
     o.assumed_pod_ttl_us = static_cast<int64_t>(j["assumedPodTTLSeconds"].as_double() * 1e6);
   o.metrics_sample_rate = j["metricsSampleRate"].as_double(o.metrics_sample_rate);
   o.status_updates = j["statusUpdates"].as_bool(o.status_updates);
+  o.events = j["events"].as_bool(o.events);
   o.trace = j["trace"].as_bool(false);
   o.seed = static_cast<uint64_t>(j["seed"].as_int(0));
   return o;
@@ -143,7 +144,13 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
   cache_ = std::make_unique<SchedulerCache>(clock_, opts_.assumed_pod_ttl_us);
   informers_ = std::make_unique<Informers>();
   nominator_ = std::make_unique<Nominator>();
-  client_ = client ? std::move(client) : std::make_shared<StoreClient>(store_);
+  if (client) {
+    client_ = std::move(client);
+  } else {
+    auto sc = std::make_shared<StoreClient>(store_);
+    sc->events_enabled = opts_.events;
+    client_ = std::move(sc);
+  }
 
   const auto& profiles = config["profiles"].items();
   if (profiles.empty()) throw std::runtime_error("scheduler config has no profiles");

@@ -79,6 +79,7 @@ struct SchedulerOptions {
   int64_t assumed_pod_ttl_us = 15LL * 60 * 1'000'000;
   double metrics_sample_rate = 0.1;  // fraction of cycles with per-extension-point metrics
   bool status_updates = true;        // PodScheduled=False condition patches on failure
+  bool events = true;                // FailedScheduling / Preempted events (in-process StoreClient)
   bool trace = false;
   uint64_t seed = 0;
   static SchedulerOptions from_json(const Json& j);
