@@ -1,10 +1,11 @@
 """CrossNodePreemption (pkg/crossnodepreemption/cross_node_preemption.go,
 commented out upstream together with test/integration/cross_node_preemption_test.go:19-133).
 
-Parity for the cross-node cases is pinned by these scenarios, since the
-reference has no runnable test: a pod blocked by an anti-affinity peer on a
-node it can never use is admitted by evicting that peer; DefaultPreemption
-cannot do this because it only evicts pods on the node being considered.
+The reference's two (commented-out) integration cases run at the end of this
+file. The other scenarios pin the MI355X-relevant cross-node cases: a pod
+blocked by an anti-affinity peer on a node it can never use is admitted by
+evicting that peer; DefaultPreemption cannot do this because it only evicts
+pods on the node being considered.
 """
 import time
 
@@ -154,3 +155,45 @@ def test_args_defaults_and_validation():
         default_plugin_args("CrossNodePreemption", {"maxVictims": 0})
     with pytest.raises(ConfigError):
         default_plugin_args("CrossNodePreemption", {"bogus": 1})
+
+
+# The reference's (commented-out) integration cases,
+# test/integration/cross_node_preemption_test.go:40-73: a zone1 pair of
+# low-priority "foo" pods must BOTH go for a high-priority pod whose hard
+# spread constraint / required anti-affinity spans the zone; node-x (zone2)
+# holds no pods. DefaultPreemption runs first and cannot help (one victim
+# per node); CrossNodePreemption is appended after it, as upstream.
+FOO_EXISTS = {"matchExpressions": [{"key": "foo", "operator": "Exists"}]}
+
+
+def _reference_cluster(store):
+    for n, zone, pods in (("node-a", "zone1", "10"), ("node-b", "zone1", "10"), ("node-x", "zone2", "0")):
+        store.create("nodes", make_node(n, {"cpu": "8", "memory": "64Gi", "pods": pods}, labels={"zone": zone, "node": n}))
+    for n in ("a", "b"):
+        store.create("pods", make_pod(f"pod-{n}", labels={"foo": ""}, node_name=f"node-{n}", uid=f"pod-{n}"))
+
+
+APPENDED = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
+            "profiles": [{"schedulerName": "default-scheduler",
+                          "plugins": {"postFilter": {"enabled": [{"name": "CrossNodePreemption"}]}}}]}
+
+
+@pytest.mark.parametrize("kind", ["PodTopologySpread", "PodAntiAffinity"])
+def test_reference_cases_preempt_two_pods_in_zone1(store, kind):
+    _reference_cluster(store)
+    if kind == "PodTopologySpread":
+        p = make_pod("p", labels={"foo": ""}, priority=1000, uid="p")
+        p["spec"]["topologySpreadConstraints"] = [{"maxSkew": 1, "topologyKey": "zone",
+                                                   "whenUnsatisfiable": "DoNotSchedule", "labelSelector": FOO_EXISTS}]
+    else:
+        p = make_pod("p", labels={"foo": ""}, priority=1000, uid="p", affinity={"podAntiAffinity": {
+            "requiredDuringSchedulingIgnoredDuringExecution": [{"labelSelector": FOO_EXISTS, "topologyKey": "zone"}]}})
+    s = new_scheduler(store, load_config(APPENDED), start=True)
+    try:
+        s.sync_informers(50)
+        store.create("pods", p)
+        wait_for(lambda: store.get("pods", "default", "pod-a") is None and store.get("pods", "default", "pod-b") is None)
+        wait_for(lambda: bool(store.get("pods", "default", "p")["spec"].get("nodeName")))
+        assert store.get("pods", "default", "p")["spec"]["nodeName"] in ("node-a", "node-b")
+    finally:
+        s.stop()
