@@ -38,6 +38,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-gpu-probe", action="store_true")
     ap.add_argument("--trace", default="", help="write a Chrome trace of rank 0's timed steps")
+    ap.add_argument("--sched-options", default="{}",
+                    help='JSON scheduler options for A/B runs, e.g. \'{"equivalenceCache": false}\'')
     ap.add_argument("--no-scenarios", action="store_true",
                     help="skip the per-BASELINE-config scenarios (untimed, reported under config.scenarios)")
     args = ap.parse_args()
@@ -65,7 +67,8 @@ def main() -> int:
                          "hbm_gib": hbm_gib}
 
     spec = ClusterSpec(nodes=args.nodes, hbm_gib=hbm_gib)
-    shard = Shard(spec, namespace=f"bench-r{ctx.rank}", seed=args.seed + 7919 * ctx.rank)
+    shard = Shard(spec, namespace=f"bench-r{ctx.rank}", seed=args.seed + 7919 * ctx.rank,
+                  options=json.loads(args.sched_options))
     # Pre-render every wave's JSON (data preparation, outside the timed region).
     waves = [shard.wave(i) for i in range(args.warmup + args.steps)]
     prepared = [(w.groups_json(), w.pods_json()) for w in waves]
@@ -139,6 +142,8 @@ def main() -> int:
                 "gang_admit": lat,
                 "attempts": stats["attempts"],
                 "unschedulable_attempts": stats["unschedulable"],
+                "eq_cache_filter_hit_rate": round(stats["eq_filter_hits"] / max(1, stats["eq_filter_hits"] +
+                                                                                 stats["eq_filter_misses"]), 3),
                 **extras,
             },
         }

@@ -164,6 +164,10 @@ struct Pod {
   std::vector<ContainerPort> host_ports;
   GpuAssignment gpu;      // decoded from annotations (mutable via cache only)
   GpuDemand gpu_demand;   // FlexGPU demand from container limits
+  // Equivalence class: hash of namespace, labels, annotations and spec (minus
+  // nodeName). Pods of one PodGroup/Job template share it, so Filter verdicts
+  // and Score values of node-local plugins can be reused across them.
+  uint64_t template_hash = 0;
 
   const std::string& ns() const { return meta.ns; }
   const std::string& name() const { return meta.name; }

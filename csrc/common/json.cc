@@ -419,4 +419,53 @@ Json Json::diff_merge_patch(const Json& from, const Json& to) {
   return patch;
 }
 
+namespace {
+inline uint64_t fnv(uint64_t h, const void* data, size_t n) {
+  const unsigned char* p = static_cast<const unsigned char*>(data);
+  for (size_t i = 0; i < n; ++i) {
+    h ^= p[i];
+    h *= 1099511628211ULL;
+  }
+  return h;
+}
+}  // namespace
+
+uint64_t json_hash(const Json& j, uint64_t h, std::string_view skip_key) {
+  uint8_t tag = static_cast<uint8_t>(j.type());
+  h = fnv(h, &tag, 1);
+  switch (j.type()) {
+    case Json::Type::Null:
+      break;
+    case Json::Type::Bool: {
+      uint8_t b = j.as_bool() ? 1 : 0;
+      h = fnv(h, &b, 1);
+      break;
+    }
+    case Json::Type::Int: {
+      int64_t v = j.as_int();
+      h = fnv(h, &v, sizeof v);
+      break;
+    }
+    case Json::Type::Double: {
+      double v = j.as_double();
+      h = fnv(h, &v, sizeof v);
+      break;
+    }
+    case Json::Type::String:
+      h = fnv(h, j.as_string().data(), j.as_string().size());
+      break;
+    case Json::Type::Array:
+      for (const auto& x : j.items()) h = json_hash(x, h);
+      break;
+    case Json::Type::Object:
+      for (const auto& [k, v] : j.members()) {
+        if (!skip_key.empty() && k == skip_key) continue;
+        h = fnv(h, k.data(), k.size() + 1);  // include the terminator: "ab"+"c" != "a"+"bc"
+        h = json_hash(v, h);
+      }
+      break;
+  }
+  return h;
+}
+
 }  // namespace xsched

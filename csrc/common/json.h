@@ -120,4 +120,9 @@ inline const Json& json_null() {
   return n;
 }
 
+// Structural FNV-1a hash of a JSON value (type tags, keys, scalars; object
+// members in insertion order). Members named `skip_key` at the top level are
+// ignored. Used for the scheduler's pod-template equivalence classes.
+uint64_t json_hash(const Json& j, uint64_t h = 1469598103934665603ULL, std::string_view skip_key = {});
+
 }  // namespace xsched

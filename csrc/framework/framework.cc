@@ -285,8 +285,27 @@ Status Framework::run_pre_score(CycleState& s, const Pod& p, const std::vector<N
   return {};
 }
 
+bool Framework::filters_node_local(const Pod& p, const Snapshot& snap) const {
+  auto it = chain_.find(kFilter);
+  if (it == chain_.end()) return true;
+  for (const auto& pl : it->second)
+    if (!pl->filter_node_local(p, snap)) return false;
+  return true;
+}
+
+std::vector<char> Framework::local_scorers(const Pod& p, const Snapshot& snap) const {
+  std::vector<char> out(scorers_.size(), 0);
+  bool any = false;
+  for (size_t k = 0; k < scorers_.size(); ++k) {
+    out[k] = scorers_[k].first->score_node_local(p, snap) ? 1 : 0;
+    any = any || out[k];
+  }
+  if (!any) out.clear();
+  return out;
+}
+
 Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes,
-                            std::vector<NodeScore>& total, ScoreBreakdown* breakdown) {
+                            std::vector<NodeScore>& total, ScoreBreakdown* breakdown, EqScoreCache* eq) {
   int64_t t0 = s.record_metrics ? handle_.clock->now_us() : 0;
   size_t n = nodes.size();
   total.assign(n, NodeScore{});
@@ -298,7 +317,15 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
   std::mutex err_mu;
   // Node-parallel scoring: one task per node runs every score plugin.
   handle_.parallelizer->until(static_cast<int>(n), [&](int i) {
+    // Equivalence cache: node-local raw scores of this pod template on an
+    // unchanged node are reused; the others are recomputed.
+    EqSlot* slot = eq ? eq->slots[i] : nullptr;
+    const bool hit = slot && slot->score_gen == nodes[i]->generation && slot->raw.size() == scorers_.size();
     for (size_t k = 0; k < scorers_.size(); ++k) {
+      if (hit && eq->local[k]) {
+        per[k][i].score = slot->raw[k];
+        continue;
+      }
       auto [sc, st] = scorers_[k].first->score(s, p, *nodes[i]);
       if (!st.is_success()) {
         std::lock_guard<std::mutex> g(err_mu);
@@ -307,6 +334,11 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
         return;
       }
       per[k][i].score = sc;  // names live in `total` only (normalizers use scores)
+    }
+    if (slot && !hit) {
+      slot->raw.resize(scorers_.size());
+      for (size_t k = 0; k < scorers_.size(); ++k) slot->raw[k] = per[k][i].score;
+      slot->score_gen = nodes[i]->generation;
     }
   }, &failed);
   if (failed.load()) return Status(Code::Error, err);

@@ -28,6 +28,20 @@ struct ProfileConfig {
   static ProfileConfig from_json(const Json& j);
 };
 
+// One (pod template, node) entry of the scheduler's equivalence cache:
+// the Filter verdict and raw (pre-normalization) Score values last computed
+// for that template on that node, valid while the node's generation matches.
+struct EqSlot {
+  int64_t filter_gen = -1;
+  Status filter;
+  int64_t score_gen = -1;
+  std::vector<int64_t> raw;  // per scorer, in Framework scorer order
+};
+struct EqScoreCache {
+  std::vector<char> local;       // per scorer: raw score is node-local for this pod
+  std::vector<EqSlot*> slots;    // per node passed to run_score (nullptr: uncached)
+};
+
 class Framework {
  public:
   Framework(const ProfileConfig& cfg, Handle handle);
@@ -53,7 +67,11 @@ class Framework {
   // `breakdown` (optional) receives ("Plugin*weight", normalized scores).
   using ScoreBreakdown = std::vector<std::pair<std::string, std::vector<int64_t>>>;
   Status run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes, std::vector<NodeScore>& total,
-                   ScoreBreakdown* breakdown = nullptr);
+                   ScoreBreakdown* breakdown = nullptr, EqScoreCache* eq = nullptr);
+  // Equivalence cache: every Filter plugin node-local for `p`?
+  bool filters_node_local(const Pod& p, const Snapshot& s) const;
+  // Per scorer (scorer order): raw Score node-local for `p`? Empty if none is.
+  std::vector<char> local_scorers(const Pod& p, const Snapshot& s) const;
   Status run_reserve(CycleState& s, const PodPtr& p, const std::string& node);
   void run_unreserve(CycleState& s, const PodPtr& p, const std::string& node);
   // Returns Success, an unschedulable/error status, or Wait (then `on_done`

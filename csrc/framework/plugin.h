@@ -113,6 +113,13 @@ class Plugin {
   virtual Status pre_bind(CycleState& s, const PodPtr& p, const std::string& node) { return {}; }
   virtual Status bind(CycleState& s, const PodPtr& p, const std::string& node) { return Status(Code::Skip); }
   virtual void post_bind(CycleState& s, const PodPtr& p, const std::string& node) {}
+  // Equivalence-cache contract (scheduler.cc eq-cache). True when this
+  // plugin's Filter verdict / raw Score for `p` on a node is a function of the
+  // pod's template (Pod::template_hash) and that NodeInfo's content (its
+  // generation) alone, for the snapshot's node epoch. Plugins that read
+  // cluster-wide, time-varying or cross-pod state for this pod return false.
+  virtual bool filter_node_local(const Pod& p, const Snapshot& s) const { return false; }
+  virtual bool score_node_local(const Pod& p, const Snapshot& s) const { return false; }
   // EnqueueExtensions
   virtual std::vector<ClusterEvent> events_to_register() const { return {}; }
   // Informer hooks (plugins that maintain their own state from watch events,

@@ -170,6 +170,9 @@ struct AssignmentState : StateData {
 
 class FlexGPU : public Plugin {
  public:
+  // Filter/Score read only the node's GPU ledger, allocatable and the pod's demand.
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   FlexGPU(const Json& args, Handle& h) : Plugin("FlexGPU", kFilter | kScore | kReserve | kBind), h_(h) {
     GpuNames& gn = gpu_names();
     if (args["gpuResourceName"].is_string()) gn.gpu = args["gpuResourceName"].as_string();

@@ -26,6 +26,8 @@ class PrioritySort : public Plugin {
 // ----------------------------------------------------- NodeUnschedulable ----
 class NodeUnschedulable : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   NodeUnschedulable() : Plugin("NodeUnschedulable", kFilter) {}
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     if (!ni.node) return Status::unresolvable("node not found");
@@ -43,6 +45,8 @@ class NodeUnschedulable : public Plugin {
 // -------------------------------------------------------------- NodeName ----
 class NodeName : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   NodeName() : Plugin("NodeName", kFilter) {}
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     if (p.node_name.empty() || p.node_name == ni.name()) return {};
@@ -54,6 +58,8 @@ class NodeName : public Plugin {
 // ------------------------------------------------------------- NodePorts ----
 class NodePorts : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   NodePorts() : Plugin("NodePorts", kPreFilter | kFilter) {}
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     for (const auto& port : p.host_ports) {
@@ -88,6 +94,8 @@ std::vector<ResourceWeight> parse_weights(const Json& arr, std::vector<ResourceW
 
 class NodeResourcesFit : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   explicit NodeResourcesFit(const Json& args) : Plugin("NodeResourcesFit", kPreFilter | kFilter | kScore) {
     for (const auto& r : args["ignoredResources"].items()) ignored_.push_back(res_id(r.as_string()));
     for (const auto& g : args["ignoredResourceGroups"].items()) ignored_groups_.push_back(g.as_string());
@@ -186,6 +194,8 @@ class NodeResourcesFit : public Plugin {
 // ------------------------------------------ NodeResourcesBalancedAllocation ----
 class BalancedAllocation : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   explicit BalancedAllocation(const Json& args) : Plugin("NodeResourcesBalancedAllocation", kScore) {
     weights_ = parse_weights(args["resources"], {{kCPU, 1}, {kMemory, 1}});
   }
@@ -217,6 +227,8 @@ class BalancedAllocation : public Plugin {
 // ------------------------------------------------------- TaintToleration ----
 class TaintToleration : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   TaintToleration() : Plugin("TaintToleration", kFilter | kPreScore | kScore) {}
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     if (!ni.node) return Status::error("invalid nodeInfo");
@@ -256,6 +268,8 @@ bool term_matches(const NodeSelectorTerm& t, const Node& n) { return node_select
 
 class NodeAffinity : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   explicit NodeAffinity(const Json& args) : Plugin("NodeAffinity", kPreFilter | kFilter | kPreScore | kScore) {
     if (const Json* aa = args.get("addedAffinity")) {
       if (const Json* req = aa->path({"requiredDuringSchedulingIgnoredDuringExecution", "nodeSelectorTerms"})) {

@@ -57,6 +57,13 @@ int64_t value_units(int id, int64_t v) {  // Quantity.Value() semantics (cpu rou
 
 class TopologyMatch : public Plugin {
  public:
+  // Zones come from the node's NRT and GPU ledger. XGMIGangAffinity scores a
+  // gang member against the group's remaining ranks (cluster-wide), so it is
+  // node-local only for pods outside a PodGroup.
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod& p, const Snapshot&) const override {
+    return strategy_ != Strategy::XGMI || p.pod_group.empty();
+  }
   TopologyMatch(const Json& args, Handle& h) : Plugin("NodeResourceTopologyMatch", kFilter | kPreScore | kScore), h_(h) {
     const Json& ss = args["scoringStrategy"];
     std::string t = ss["type"].str_or("LeastAllocated");

@@ -25,6 +25,8 @@ void min_max_normalize(std::vector<NodeScore>& scores) {
 
 class NodeResourcesAllocatable : public Plugin {
  public:
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   explicit NodeResourcesAllocatable(const Json& args) : Plugin("NodeResourcesAllocatable", kScore) {
     most_ = args["mode"].str_or("Least") == "Most";
     for (const auto& r : args["resources"].items()) weights_.emplace_back(res_id(r["name"].as_string()), r["weight"].as_int(1));

@@ -96,6 +96,9 @@ bool has_all_keys(const Node& n, const std::vector<TopologySpreadConstraint>& cs
 
 class PodTopologySpread : public Plugin {
  public:
+  // Without constraints the pod's Filter/Score ignore other pods entirely.
+  bool filter_node_local(const Pod& p, const Snapshot&) const override { return p.spread_constraints.empty(); }
+  bool score_node_local(const Pod& p, const Snapshot&) const override { return p.spread_constraints.empty(); }
   explicit PodTopologySpread(Handle& h)
       : Plugin("PodTopologySpread", kPreFilter | kFilter | kPreScore | kScore), h_(h) {}
 
@@ -286,6 +289,14 @@ void bump(PairCounts& m, const Node& n, const std::string& key, int64_t v) {
 
 class InterPodAffinity : public Plugin {
  public:
+  // Node-local only when neither the pod nor any existing pod carries affinity terms.
+  static bool no_terms(const Pod& p, const Snapshot& s) {
+    return p.pod_affinity_required.empty() && p.pod_anti_affinity_required.empty() &&
+           p.pod_affinity_preferred.empty() && p.pod_anti_affinity_preferred.empty() &&
+           s.have_pods_with_affinity.empty() && s.have_pods_with_required_anti_affinity.empty();
+  }
+  bool filter_node_local(const Pod& p, const Snapshot& s) const override { return no_terms(p, s); }
+  bool score_node_local(const Pod& p, const Snapshot& s) const override { return no_terms(p, s); }
   InterPodAffinity(const Json& args, Handle& h)
       : Plugin("InterPodAffinity", kPreFilter | kFilter | kPreScore | kScore), h_(h) {
     hard_weight_ = static_cast<int32_t>(args["hardPodAffinityWeight"].as_int(1));
@@ -476,6 +487,9 @@ class InterPodAffinity : public Plugin {
 // ========================================================= ImageLocality ====
 class ImageLocality : public Plugin {
  public:
+  // Node images + cluster-wide image spread: both change only with Node objects (node epoch).
+  bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   explicit ImageLocality(Handle& h) : Plugin("ImageLocality", kScore), h_(h) {}
   static constexpr int64_t kMB = 1024 * 1024;
   static constexpr int64_t kMinThreshold = 23 * kMB;

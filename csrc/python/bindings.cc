@@ -412,6 +412,8 @@ PYBIND11_MODULE(_xsched, m) {
              d["bound"] = st.bound;
              d["bind_failures"] = st.bind_failures;
              d["preemption_attempts"] = st.preemption_attempts;
+             d["eq_filter_hits"] = st.eq_filter_hits;
+             d["eq_filter_misses"] = st.eq_filter_misses;
              d["inflight_bindings"] = s.inflight_bindings();
              return d;
            })

@@ -29,6 +29,7 @@ void SchedulerCache::group_delta(const Pod& p, int d) {
 
 void SchedulerCache::add_node(const NodePtr& n) {
   std::lock_guard<std::mutex> g(mu_);
+  ++node_epoch_;
   auto& ni = info_for(n->name());
   bool was_ghost = ni->node == nullptr;
   ni->set_node(n);
@@ -41,6 +42,7 @@ void SchedulerCache::add_node(const NodePtr& n) {
 
 void SchedulerCache::update_node(const NodePtr& n) {
   std::lock_guard<std::mutex> g(mu_);
+  ++node_epoch_;
   auto& ni = info_for(n->name());
   bool was_ghost = ni->node == nullptr;
   ni->set_node(n);
@@ -55,6 +57,7 @@ void SchedulerCache::remove_node(const std::string& name) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = nodes_.find(name);
   if (it == nodes_.end()) return;
+  ++node_epoch_;
   order_.erase(std::remove(order_.begin(), order_.end(), name), order_.end());
   structure_changed_ = true;
   if (it->second->pods.empty()) {
@@ -236,6 +239,7 @@ void SchedulerCache::update_snapshot(Snapshot& s) {
     }
   }
   s.generation = generation_;
+  s.node_epoch = node_epoch_;
 }
 
 void SchedulerCache::cleanup_expired_assumed_pods() {

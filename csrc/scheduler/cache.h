@@ -82,6 +82,7 @@ class SchedulerCache {
   std::unordered_set<std::string> dirty_;
   bool structure_changed_ = true;
   int64_t generation_ = 0;
+  uint64_t node_epoch_ = 1;
 };
 
 }  // namespace xsched

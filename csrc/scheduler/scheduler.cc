@@ -103,6 +103,7 @@ SchedulerOptions SchedulerOptions::from_json(const Json& j) {
   o.metrics_sample_rate = j["metricsSampleRate"].as_double(o.metrics_sample_rate);
   o.status_updates = j["statusUpdates"].as_bool(o.status_updates);
   o.events = j["events"].as_bool(o.events);
+  o.equivalence_cache = j["equivalenceCache"].as_bool(o.equivalence_cache);
   o.trace = j["trace"].as_bool(false);
   o.seed = static_cast<uint64_t>(j["seed"].as_int(0));
   return o;
@@ -546,8 +547,26 @@ int Scheduler::num_feasible_nodes_to_find(Framework& fw, int n) const {
   return num;
 }
 
+Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
+  if (!opts_.equivalence_cache || p.template_hash == 0) return nullptr;
+  auto& per_fw = eq_[&fw];
+  auto& e = per_fw[p.template_hash];
+  if (!e) {
+    if (per_fw.size() > 256) {  // bounded: drop every template (they refill on demand)
+      per_fw.clear();
+      return eq_entry(fw, p);
+    }
+    e = std::make_unique<EqEntry>();
+  }
+  if (e->epoch != snapshot_.node_epoch || e->slots.size() != snapshot_.nodes.size()) {
+    e->epoch = snapshot_.node_epoch;
+    e->slots.assign(snapshot_.nodes.size(), EqSlot{});
+  }
+  return e.get();
+}
+
 Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d,
-                                      std::vector<NodeInfoPtr>& feasible) {
+                                      std::vector<NodeInfoPtr>& feasible, EqEntry* eq) {
   Status st = fw.run_pre_filter(s, p);
   const auto& all = snapshot_.nodes;
   if (!st.is_success()) {
@@ -575,6 +594,9 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     next_start_node_ = (next_start_node_ + static_cast<int>(feasible.size())) % n;
     return {};
   }
+  // Filter verdicts are reused only when every Filter plugin is node-local for
+  // this pod and no nominated pod can change a node's verdict.
+  const bool eq_filter = eq && (!nominator_ || nominator_->empty()) && fw.filters_node_local(p, snapshot_);
   std::vector<NodeInfoPtr> found(to_find);
   std::atomic<int> count{0};
   std::atomic<int> processed{0};
@@ -583,9 +605,24 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   Status first_err;
   bool has_err = false;
   int start = next_start_node_;
+  std::atomic<uint64_t> hits{0};
   parallelizer_->until(n, [&](int i) {
-    const NodeInfoPtr& ni = all[(start + i) % n];
-    Status fst = fw.run_filter_with_nominated_pods(s, p, *ni);
+    const int pos = (start + i) % n;
+    const NodeInfoPtr& ni = all[pos];
+    Status fst;
+    if (eq_filter) {
+      EqSlot& slot = eq->slots[pos];
+      if (slot.filter_gen == ni->generation) {
+        fst = slot.filter;
+        hits.fetch_add(1, std::memory_order_relaxed);
+      } else {
+        fst = fw.run_filter(s, p, *ni);
+        slot.filter = fst;
+        slot.filter_gen = ni->generation;
+      }
+    } else {
+      fst = fw.run_filter_with_nominated_pods(s, p, *ni);
+    }
     processed.fetch_add(1, std::memory_order_relaxed);
     if (fst.is_success()) {
       int len = count.fetch_add(1) + 1;
@@ -608,6 +645,12 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       stop.store(true);
     }
   }, &stop);
+  if (eq_filter) {
+    uint64_t h = hits.load();
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.eq_filter_hits += h;
+    stats_.eq_filter_misses += static_cast<uint64_t>(processed.load()) - h;
+  }
   if (has_err) return first_err;
   int c = std::min(count.load(), to_find);
   next_start_node_ = (start + processed.load()) % n;
@@ -676,7 +719,8 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
 
   Diagnosis diag;
   std::vector<NodeInfoPtr> feasible;
-  Status st = find_nodes_that_fit(*fw, *state, *pod, diag, feasible);
+  EqEntry* eq = eq_entry(*fw, *pod);
+  Status st = find_nodes_that_fit(*fw, *state, *pod, diag, feasible, eq);
   if (tracer_.enabled())
     tracer_.record(TraceEvent{"filter", pod->key(), std::to_string(feasible.size()), snap_end,
                               clock_->now_us() - snap_end, 0});
@@ -692,7 +736,16 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         st = Status();
       } else {
         st = fw->run_pre_score(*state, *pod, feasible);
-        if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores);
+        EqScoreCache esc;
+        if (eq) esc.local = fw->local_scorers(*pod, snapshot_);
+        if (!esc.local.empty()) {
+          esc.slots.resize(feasible.size());
+          for (size_t i = 0; i < feasible.size(); ++i) {
+            auto it = snapshot_.index.find(feasible[i]->name());
+            esc.slots[i] = it != snapshot_.index.end() ? &eq->slots[it->second] : nullptr;
+          }
+        }
+        if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores, nullptr, esc.local.empty() ? nullptr : &esc);
       }
       if (st.is_success()) host = select_host(scores);
     }

@@ -80,6 +80,7 @@ struct SchedulerOptions {
   double metrics_sample_rate = 0.1;  // fraction of cycles with per-extension-point metrics
   bool status_updates = true;        // PodScheduled=False condition patches on failure
   bool events = true;                // FailedScheduling / Preempted events (in-process StoreClient)
+  bool equivalence_cache = true;     // reuse node-local Filter/Score results across a pod template
   bool trace = false;
   uint64_t seed = 0;
   static SchedulerOptions from_json(const Json& j);
@@ -129,6 +130,7 @@ class Scheduler {
   struct Stats {
     uint64_t attempts = 0, scheduled = 0, unschedulable = 0, errors = 0, bound = 0, bind_failures = 0;
     uint64_t preemption_attempts = 0;
+    uint64_t eq_filter_hits = 0, eq_filter_misses = 0;  // equivalence-cache Filter lookups
   };
   Stats stats() const;
   std::vector<GangRecord> gang_records(bool clear = false);
@@ -143,6 +145,13 @@ class Scheduler {
     NodeStatusMap node_to_status;
     std::set<std::string> unschedulable_plugins;
   };
+  // Equivalence cache for one (profile, pod template): a slot per snapshot
+  // node position, valid for one node epoch (node set / Node objects).
+  struct EqEntry {
+    uint64_t epoch = 0;
+    std::vector<EqSlot> slots;
+  };
+  EqEntry* eq_entry(Framework& fw, const Pod& p);
 
   void informer_loop();
   void handle_event(const WatchEvent& ev);
@@ -152,7 +161,8 @@ class Scheduler {
   void handle_node_event(const WatchEvent& ev);
   void scheduling_loop();
   void schedule_cycle(const QueuedPodInfoPtr& qpi);
-  Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, std::vector<NodeInfoPtr>& feasible);
+  Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, std::vector<NodeInfoPtr>& feasible,
+                             EqEntry* eq = nullptr);
   int num_feasible_nodes_to_find(Framework& fw, int n) const;
   std::string select_host(const std::vector<NodeScore>& scores);
   void binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
@@ -192,6 +202,7 @@ class Scheduler {
   int next_start_node_ = 0;
   std::mt19937_64 rng_;
   std::vector<uint64_t> timer_ids_;
+  std::unordered_map<Framework*, std::unordered_map<uint64_t, std::unique_ptr<EqEntry>>> eq_;  // scheduling thread only
 
   mutable std::mutex stats_mu_;
   Stats stats_;
