@@ -322,11 +322,10 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
   p->meta = ObjectMeta::from_json(obj);
   const Json& spec = obj["spec"];
   const Json& status = obj["status"];
-  {
+  if (spec["nodeName"].as_string().empty()) {  // only pending pods are ever scheduled
     const Json& md = obj["metadata"];
     uint64_t h = json_hash(spec, 1469598103934665603ULL, "nodeName");
     h = json_hash(md["namespace"], h);
-    h = json_hash(md["labels"], h);
     p->template_hash = json_hash(md["annotations"], h);
   }
   if (spec["schedulerName"].is_string()) p->scheduler_name = spec["schedulerName"].as_string();

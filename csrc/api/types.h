@@ -164,9 +164,12 @@ struct Pod {
   std::vector<ContainerPort> host_ports;
   GpuAssignment gpu;      // decoded from annotations (mutable via cache only)
   GpuDemand gpu_demand;   // FlexGPU demand from container limits
-  // Equivalence class: hash of namespace, labels, annotations and spec (minus
-  // nodeName). Pods of one PodGroup/Job template share it, so Filter verdicts
-  // and Score values of node-local plugins can be reused across them.
+  // Equivalence class: hash of namespace, annotations and spec (minus
+  // nodeName). Pods with the same resource shape share it across PodGroups,
+  // so Filter verdicts and Score values of node-local plugins can be reused.
+  // Labels are left out on purpose: the only plugins that read a pod's labels
+  // (InterPodAffinity, PodTopologySpread, XGMIGangAffinity via the PodGroup)
+  // declare themselves non-local whenever those labels can matter.
   uint64_t template_hash = 0;
 
   const std::string& ns() const { return meta.ns; }

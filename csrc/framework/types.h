@@ -204,6 +204,9 @@ struct Snapshot {
   std::vector<NodeInfoPtr> have_pods_with_required_anti_affinity;
   int64_t generation = 0;
   uint64_t node_epoch = 0;  // bumped on any Node object / node-set change (not on pod changes)
+  // Versions replaced by the last refreshes. Dropping one can free deleted
+  // pods, so the scheduler releases them off the scheduling thread.
+  std::vector<NodeInfoPtr> retired;
   NodeInfoPtr get(const std::string& name) const {
     auto it = by_name.find(name);
     return it == by_name.end() ? nullptr : it->second;

@@ -13,10 +13,20 @@ NodeInfoPtr& SchedulerCache::info_for(const std::string& node) {
   return ni;
 }
 
+// Copy-on-write: snapshot NodeInfos are the cache's own immutable versions
+// (update_snapshot shares pointers instead of cloning). A version that a
+// snapshot still references is copied before the cache mutates it, so the
+// copy happens on the mutating thread (informer, binder, assume) and never
+// while the scheduling thread refreshes its snapshot.
+NodeInfo& SchedulerCache::writable(NodeInfoPtr& slot) {
+  if (slot.use_count() > 1) slot = slot->clone();
+  return *slot;
+}
+
 void SchedulerCache::mark_dirty(const std::string& node) {
   dirty_.insert(node);
   auto it = nodes_.find(node);
-  if (it != nodes_.end()) it->second->generation = ++generation_;
+  if (it != nodes_.end()) writable(it->second).generation = ++generation_;
 }
 
 void SchedulerCache::group_delta(const Pod& p, int d) {
@@ -32,7 +42,7 @@ void SchedulerCache::add_node(const NodePtr& n) {
   ++node_epoch_;
   auto& ni = info_for(n->name());
   bool was_ghost = ni->node == nullptr;
-  ni->set_node(n);
+  writable(ni).set_node(n);
   if (was_ghost) {
     order_.push_back(n->name());
     structure_changed_ = true;
@@ -45,7 +55,7 @@ void SchedulerCache::update_node(const NodePtr& n) {
   ++node_epoch_;
   auto& ni = info_for(n->name());
   bool was_ghost = ni->node == nullptr;
-  ni->set_node(n);
+  writable(ni).set_node(n);
   if (was_ghost) {
     order_.push_back(n->name());
     structure_changed_ = true;
@@ -63,7 +73,7 @@ void SchedulerCache::remove_node(const std::string& name) {
   if (it->second->pods.empty()) {
     nodes_.erase(it);
   } else {
-    it->second->node = nullptr;  // ghost until its pods are deleted
+    writable(it->second).node = nullptr;  // ghost until its pods are deleted
   }
   dirty_.insert(name);
 }
@@ -76,13 +86,13 @@ void SchedulerCache::set_nrt(const std::string& node, const NRTPtr& nrt) {
     info_for(node);  // ghost until the Node arrives; keeps the NRT
     it = nodes_.find(node);
   }
-  it->second->nrt = nrt;
+  writable(it->second).nrt = nrt;
   mark_dirty(node);
 }
 
 void SchedulerCache::add_pod_locked(const PodPtr& p) {
   auto& ni = info_for(p->node_name);
-  ni->add_pod(p);
+  writable(ni).add_pod(p);
   group_delta(*p, +1);
   mark_dirty(p->node_name);
 }
@@ -90,7 +100,7 @@ void SchedulerCache::add_pod_locked(const PodPtr& p) {
 void SchedulerCache::remove_pod_locked(const Pod& p) {
   auto it = nodes_.find(p.node_name);
   if (it == nodes_.end()) return;
-  if (it->second->remove_pod(p.uid())) group_delta(p, -1);
+  if (writable(it->second).remove_pod(p.uid())) group_delta(p, -1);
   mark_dirty(p.node_name);
   if (it->second->node == nullptr && it->second->pods.empty()) nodes_.erase(it);
 }
@@ -199,10 +209,14 @@ PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<vo
   return fresh;
 }
 
-void SchedulerCache::update_snapshot(Snapshot& s) {
+int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us) {
+  int64_t t0 = lock_wait_us ? clock_->now_us() : 0;
   std::lock_guard<std::mutex> g(mu_);
+  if (lock_wait_us) *lock_wait_us = clock_->now_us() - t0;
+  int clones = 0;
   bool affinity_dirty = false;
   if (structure_changed_) {
+    for (auto& ni : s.nodes) s.retired.push_back(std::move(ni));
     s.nodes.clear();
     s.by_name.clear();
     s.index.clear();
@@ -210,7 +224,8 @@ void SchedulerCache::update_snapshot(Snapshot& s) {
     for (const auto& name : order_) {
       auto it = nodes_.find(name);
       if (it == nodes_.end() || !it->second->node) continue;
-      NodeInfoPtr cl = it->second->clone();
+      const NodeInfoPtr& cl = it->second;
+      ++clones;
       s.index[name] = s.nodes.size();
       s.nodes.push_back(cl);
       s.by_name[name] = cl;
@@ -223,8 +238,11 @@ void SchedulerCache::update_snapshot(Snapshot& s) {
       if (it == nodes_.end() || !it->second->node) continue;
       auto sit = s.by_name.find(name);
       if (sit == s.by_name.end()) continue;
-      NodeInfoPtr cl = it->second->clone();
+      const NodeInfoPtr& cl = it->second;
+      if (sit->second == cl) continue;
+      ++clones;
       if (!sit->second->pods_with_affinity.empty() || !cl->pods_with_affinity.empty()) affinity_dirty = true;
+      s.retired.push_back(s.nodes[s.index[name]]);
       s.nodes[s.index[name]] = cl;
       sit->second = cl;
     }
@@ -240,6 +258,7 @@ void SchedulerCache::update_snapshot(Snapshot& s) {
   }
   s.generation = generation_;
   s.node_epoch = node_epoch_;
+  return clones;
 }
 
 void SchedulerCache::cleanup_expired_assumed_pods() {

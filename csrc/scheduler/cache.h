@@ -49,7 +49,10 @@ class SchedulerCache {
   // the pod on its node. Returns the new object (nullptr if not cached).
   PodPtr mutate_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
 
-  void update_snapshot(Snapshot& s);
+  // Returns the number of NodeInfo versions refreshed (shared, not cloned:
+  // the cache copies on write); replaced versions go to `s.retired`; `lock_wait_us` (optional)
+  // receives the time spent waiting for the cache lock (trace diagnostics).
+  int update_snapshot(Snapshot& s, int64_t* lock_wait_us = nullptr);
   void cleanup_expired_assumed_pods();
 
   int assigned_in_group(const std::string& pg_full_name) const;
@@ -66,6 +69,7 @@ class SchedulerCache {
     bool binding_finished = false;
   };
   NodeInfoPtr& info_for(const std::string& node);  // creates a ghost entry
+  NodeInfo& writable(NodeInfoPtr& slot);            // copy-on-write before mutating
   void add_pod_locked(const PodPtr& p);
   void remove_pod_locked(const Pod& p);
   void mark_dirty(const std::string& node);

@@ -547,6 +547,15 @@ int Scheduler::num_feasible_nodes_to_find(Framework& fw, int n) const {
   return num;
 }
 
+// Replaced snapshot versions may hold the last reference to deleted pods;
+// free them in batches on a binder thread instead of in the scheduling cycle.
+void Scheduler::release_retired() {
+  if (snapshot_.retired.size() < 32) return;
+  auto batch = std::make_shared<std::vector<NodeInfoPtr>>(std::move(snapshot_.retired));
+  snapshot_.retired.clear();
+  binder_->submit([batch] { batch->clear(); });
+}
+
 Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
   if (!opts_.equivalence_cache || p.template_hash == 0) return nullptr;
   auto& per_fw = eq_[&fw];
@@ -566,8 +575,10 @@ Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
 }
 
 Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d,
-                                      std::vector<NodeInfoPtr>& feasible, EqEntry* eq) {
+                                      std::vector<NodeInfoPtr>& feasible, EqEntry* eq, bool full_diagnosis) {
+  int64_t pf0 = tracer_.enabled() ? clock_->now_us() : 0;
   Status st = fw.run_pre_filter(s, p);
+  if (tracer_.enabled()) tracer_.record(TraceEvent{"prefilter", p.key(), "", pf0, clock_->now_us() - pf0, 0});
   const auto& all = snapshot_.nodes;
   if (!st.is_success()) {
     if (!st.is_unschedulable()) return st;
@@ -606,6 +617,11 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   bool has_err = false;
   int start = next_start_node_;
   std::atomic<uint64_t> hits{0};
+  // Per-node failures go to a position-indexed buffer (no lock, no map
+  // insert per node); the NodeToStatusMap is only materialized when the
+  // diagnosis is consumed: no feasible node (PostFilter / FitError) or explain.
+  fail_buf_.assign(n, Status());
+  fail_set_.assign(n, 0);
   parallelizer_->until(n, [&](int i) {
     const int pos = (start + i) % n;
     const NodeInfoPtr& ni = all[pos];
@@ -635,11 +651,13 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       }
       return;
     }
-    std::lock_guard<std::mutex> g(mu);
     if (fst.is_unschedulable()) {
-      d.node_to_status[ni->name()] = fst;
-      d.unschedulable_plugins.insert(fst.failed_plugin());
-    } else if (!has_err) {
+      fail_buf_[pos] = std::move(fst);
+      fail_set_[pos] = 1;
+      return;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    if (!has_err) {
       first_err = fst;
       has_err = true;
       stop.store(true);
@@ -655,6 +673,13 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   int c = std::min(count.load(), to_find);
   next_start_node_ = (start + processed.load()) % n;
   feasible.assign(found.begin(), found.begin() + c);
+  if (feasible.empty() || full_diagnosis) {
+    for (int pos = 0; pos < n; ++pos) {
+      if (!fail_set_[pos]) continue;
+      d.unschedulable_plugins.insert(fail_buf_[pos].failed_plugin());
+      d.node_to_status[all[pos]->name()] = std::move(fail_buf_[pos]);
+    }
+  }
   if (feasible.empty()) {
     // FitError message: "0/N nodes are available: k reason, ..."
     std::map<std::string, int> reasons;
@@ -708,14 +733,23 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   if (tracer_.enabled())
     tracer_.record(TraceEvent{"queue_wait", pod->key(), "", qpi->timestamp_us, cycle_start - qpi->timestamp_us, 0});
 
-  cache_->update_snapshot(snapshot_);
+  int64_t lock_wait = 0;
+  int64_t snap_start = tracer_.enabled() ? clock_->now_us() : 0;
+  int clones = cache_->update_snapshot(snapshot_, tracer_.enabled() ? &lock_wait : nullptr);
+  release_retired();
   const std::string& profile = fw->profile_name();
   {
     std::lock_guard<std::mutex> g(stats_mu_);
     ++stats_.attempts;
   }
   int64_t snap_end = clock_->now_us();
-  if (tracer_.enabled()) tracer_.record(TraceEvent{"snapshot", pod->key(), "", cycle_start, snap_end - cycle_start, 0});
+  if (tracer_.enabled()) {
+    tracer_.record(TraceEvent{"cycle_setup", pod->key(), "", cycle_start, snap_start - cycle_start, 0});
+    tracer_.record(TraceEvent{"snapshot", pod->key(),
+                              "clones=" + std::to_string(clones) + " lock_wait_us=" + std::to_string(lock_wait),
+                              snap_start, snap_end - snap_start, 0});
+    tracer_.record(TraceEvent{"snapshot_lock_wait", pod->key(), "", snap_start, lock_wait, 0});
+  }
 
   Diagnosis diag;
   std::vector<NodeInfoPtr> feasible;
@@ -864,7 +898,7 @@ Json Scheduler::explain(const Json& pod_obj) {
   Diagnosis d;
   std::vector<NodeInfoPtr> feasible;
   int saved_start = next_start_node_;
-  Status st = find_nodes_that_fit(*fw, *state, *pod, d, feasible);
+  Status st = find_nodes_that_fit(*fw, *state, *pod, d, feasible, nullptr, true);
   next_start_node_ = saved_start;
   out.set("code", Json(code_name(st.code())));
   out.set("message", Json(st.message()));

@@ -152,6 +152,9 @@ class Scheduler {
     std::vector<EqSlot> slots;
   };
   EqEntry* eq_entry(Framework& fw, const Pod& p);
+  void release_retired();
+  std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
+  std::vector<char> fail_set_;
 
   void informer_loop();
   void handle_event(const WatchEvent& ev);
@@ -162,7 +165,7 @@ class Scheduler {
   void scheduling_loop();
   void schedule_cycle(const QueuedPodInfoPtr& qpi);
   Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, std::vector<NodeInfoPtr>& feasible,
-                             EqEntry* eq = nullptr);
+                             EqEntry* eq = nullptr, bool full_diagnosis = false);
   int num_feasible_nodes_to_find(Framework& fw, int n) const;
   std::string select_host(const std::vector<NodeScore>& scores);
   void binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
