@@ -317,6 +317,15 @@ void Pod::recompute_gpu_assignment() {
   }
 }
 
+uint64_t pg_key_of(std::string_view full) {
+  uint64_t h = 1469598103934665603ULL;
+  for (unsigned char c : full) {
+    h ^= c;
+    h *= 1099511628211ULL;
+  }
+  return h ? h : 1;
+}
+
 std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
   auto p = std::make_shared<Pod>();
   p->meta = ObjectMeta::from_json(obj);
@@ -404,7 +413,10 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
   p->nonzero_request += p->overhead;
   p->request = sum;
   p->qos = compute_qos(*p);
-  if (const std::string* pg = p->meta.label(kPodGroupLabel)) p->pod_group = *pg;
+  if (const std::string* pg = p->meta.label(kPodGroupLabel)) {
+    p->pod_group = *pg;
+    p->pg_key = pg_key_of(p->pg_full_name());
+  }
   p->gpu_demand = compute_gpu_demand(*p);
   p->recompute_gpu_assignment();
   return p;

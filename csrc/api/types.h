@@ -161,6 +161,7 @@ struct Pod {
   Res limit_sum;        // Σ container limits (FlexGPU accounting uses limits)
   QoS qos = QoS::BestEffort;
   std::string pod_group;  // value of kPodGroupLabel ("" if none)
+  uint64_t pg_key = 0;    // pg_key_of("ns/pod_group"), 0 if no group
   std::vector<ContainerPort> host_ports;
   GpuAssignment gpu;      // decoded from annotations (mutable via cache only)
   GpuDemand gpu_demand;   // FlexGPU demand from container limits
@@ -183,6 +184,9 @@ struct Pod {
   void recompute_gpu_assignment();
 };
 using PodPtr = std::shared_ptr<Pod>;
+
+// 64-bit key of a PodGroup full name "ns/name" (per-node gang counts).
+uint64_t pg_key_of(std::string_view full_name);
 
 struct Node {
   ObjectMeta meta;

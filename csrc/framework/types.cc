@@ -220,7 +220,16 @@ void NodeInfo::add_pod(const PodPtr& p) {
   nonzero_requested += p->nonzero_request;
   for (const auto& port : p->host_ports) used_ports.emplace(port.host_ip, port.protocol, port.host_port);
   gpu.apply(p->gpu, +1);
-  if (!p->pod_group.empty()) ++pg_count[p->pg_full_name()];
+  if (p->pg_key) {
+    bool found = false;
+    for (auto& [k, c] : pg_count)
+      if (k == p->pg_key) {
+        ++c;
+        found = true;
+        break;
+      }
+    if (!found) pg_count.emplace_back(p->pg_key, 1);
+  }
   ++generation;
 }
 
@@ -249,9 +258,15 @@ bool NodeInfo::remove_pod(const std::string& uid) {
   nonzero_requested -= victim->nonzero_request;
   for (const auto& port : victim->host_ports) used_ports.erase({port.host_ip, port.protocol, port.host_port});
   gpu.apply(victim->gpu, -1);
-  if (!victim->pod_group.empty()) {
-    auto it = pg_count.find(victim->pg_full_name());
-    if (it != pg_count.end() && --it->second <= 0) pg_count.erase(it);
+  if (victim->pg_key) {
+    for (size_t i = 0; i < pg_count.size(); ++i)
+      if (pg_count[i].first == victim->pg_key) {
+        if (--pg_count[i].second <= 0) {
+          pg_count[i] = pg_count.back();
+          pg_count.pop_back();
+        }
+        break;
+      }
   }
   ++generation;
   return true;

@@ -183,7 +183,14 @@ struct NodeInfo {
   GpuLedger gpu;
   NRTPtr nrt;  // this node's NodeResourceTopology (set by the cache from the informer)
   int64_t generation = 0;
-  std::unordered_map<std::string, int> pg_count;  // "ns/pg" -> pods on this node
+  // PodGroup key (Pod::pg_key) -> pods of that group on this node. A flat
+  // vector: a node hosts few groups and NodeInfo versions are copied on write.
+  std::vector<std::pair<uint64_t, int>> pg_count;
+  int pg_pods(uint64_t key) const {
+    for (const auto& [k, c] : pg_count)
+      if (k == key) return c;
+    return 0;
+  }
 
   const std::string& name() const;
   void set_node(const NodePtr& n);

@@ -41,6 +41,7 @@ using NumaNode = NumaZone;
 struct GangCtx : StateData {
   bool gang = false;
   std::string full;         // ns/pg
+  uint64_t key = 0;         // pg_key_of(full)
   int64_t remaining = 0;    // members still to place (>= 1)
   enum { kWhole, kXcd } kind = kWhole;
   int64_t amount = 0;       // per member: GPUs or XCDs
@@ -284,6 +285,7 @@ class TopologyMatch : public Plugin {
       if (pg && pg->min_member > 1 && d.amount > 0 && (d.kind == GpuDemand::Gpu || d.kind == GpuDemand::Xcd)) {
         ctx->gang = true;
         ctx->full = p.pg_full_name();
+        ctx->key = p.pg_key;
         ctx->remaining = std::max<int64_t>(1, pg->min_member - h_.cache->assigned_in_group(ctx->full));
         ctx->kind = d.kind == GpuDemand::Gpu ? GangCtx::kWhole : GangCtx::kXcd;
         ctx->amount = d.amount;
@@ -314,8 +316,7 @@ class TopologyMatch : public Plugin {
     }
     if (free <= 0) return 0;
     int64_t remaining = c.remaining * per;
-    auto it = ni.pg_count.find(c.full);
-    bool co_located = it != ni.pg_count.end() && it->second > 0;
+    bool co_located = ni.pg_pods(c.key) > 0;
     bool fits_all = remaining <= free;
     if (fits_all && co_located) return 100;
     if (fits_all) return 60 + 30 * remaining / free;  // tightest whole-gang fit first

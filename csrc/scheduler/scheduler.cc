@@ -283,6 +283,7 @@ void Scheduler::informer_loop() {
   while (running_.load()) {
     auto evs = watcher_->next(50, 8192);
     if (evs.empty()) continue;
+    int64_t batch_start = tracer_.enabled() ? clock_->now_us() : 0;
     // Pass 1: parse every pod once and publish it to the listers first, so a
     // PreFilter racing this batch sees every sibling of a PodGroup created
     // together (Coscheduling counts them). Pass 2 drives cache and queue.
@@ -305,6 +306,9 @@ void Scheduler::informer_loop() {
       else
         handle_event(evs[i]);
     }
+    if (tracer_.enabled() && batch_start)
+      tracer_.record(TraceEvent{"informer_batch", std::to_string(evs.size()) + " events", "", batch_start,
+                                clock_->now_us() - batch_start, 2});
   }
 }
 

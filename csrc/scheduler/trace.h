@@ -21,7 +21,7 @@ struct TraceEvent {
   std::string detail; // node / status
   int64_t start_us = 0;
   int64_t dur_us = 0;
-  int tid = 0;        // 0 = scheduling thread, 1 = binding workers
+  int tid = 0;        // 0 = scheduling thread, 1 = binding workers, 2 = informer
 };
 
 class Tracer {

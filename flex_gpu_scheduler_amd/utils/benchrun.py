@@ -26,6 +26,9 @@ class StepResult:
     pods: int
     seconds: float
     gangs: list[dict] = field(default_factory=list)
+    # wall-clock split of the step (ms): API writes, until every pod is bound,
+    # deletion + cache drain
+    split_ms: dict = field(default_factory=dict)
 
 
 class Shard:
@@ -52,6 +55,7 @@ class Shard:
         t0 = time.perf_counter()
         self.store.create_many("podgroups", groups_js)
         self.store.create_many("pods", pods_js)
+        t_created = time.perf_counter()
         deadline = t0 + timeout_s
         sched = self.sched
         while True:
@@ -63,6 +67,7 @@ class Shard:
                                   f"queue={sched.queue_counts()} stats={sched.stats()}")
             time.sleep(0.0002)
         self._bound = target
+        t_bound = time.perf_counter()
         gangs = sched.gang_records(True)
         self.store.delete_all("pods", self.ns)
         self.store.delete_all("podgroups", self.ns)
@@ -70,7 +75,9 @@ class Shard:
             if time.perf_counter() > deadline:
                 raise WaveTimeout("wave deletion not observed by the scheduler cache")
             time.sleep(0.0002)
-        return StepResult(n, time.perf_counter() - t0, gangs)
+        t_end = time.perf_counter()
+        return StepResult(n, t_end - t0, gangs, {"create": (t_created - t0) * 1e3, "to_bound": (t_bound - t_created) * 1e3,
+                                                 "delete_drain": (t_end - t_bound) * 1e3})
 
     def close(self) -> None:
         self.sched.stop()

@@ -199,6 +199,10 @@ def test_capacity_scheduling_integration(http_cluster, name, exist, add, eqs, ex
         for p in exist:
             client.create("pods", p)
         assert _wait(lambda: all(_bound(client).get(p["metadata"]["name"]) for p in exist), 10)
+        # The existing pods are created already bound; make sure the
+        # scheduler's informers (quota usage, node accounting) have them
+        # before the contenders arrive.
+        assert _wait(lambda: rs.scheduler.cache_counts()["pods"] >= len(exist), 10)
         for p in add:
             client.create("pods", p)
         # Preemption re-schedules after the preemptor's backoff (1 s initial).
