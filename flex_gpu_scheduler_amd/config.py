@@ -7,10 +7,12 @@ manifests/*/scheduler-config.yaml) and resolves it into the flat per-profile
 plugin lists the native framework consumes.
 
 Semantics reproduced:
-  * per-extension-point ``enabled`` appended to the defaults, ``disabled``
-    removing defaults (``"*"`` removes all) — kube-scheduler's mergePlugins;
-  * v1beta3 ``multiPoint`` expansion (a plugin enabled at every point it
-    implements, weights carried to score);
+  * mergePluginSet: a re-enabled default keeps its position and takes the
+    user's weight, other ``enabled`` plugins are appended, ``disabled``
+    removes defaults (``"*"`` removes all);
+  * v1beta3: defaults live in ``multiPoint`` with v1beta3's weights, and each
+    point expands as frameworkImpl.expandMultiPointPlugins does (explicit
+    point plugins first, then the multiPoint plugins implementing it);
   * plugin args defaults of apis/config/v1beta2/defaults.go:28-157
     (identical in v1beta3) and upstream DefaultPreemptionArgs;
   * strict decoding: unknown args fields are errors (scheme.go:35 uses the
@@ -85,6 +87,16 @@ DEFAULT_PLUGINS: dict[str, list[tuple[str, int]]] = {
 }
 
 
+# kube-scheduler 1.23 v1beta3 defaults: every default plugin in multiPoint,
+# with v1beta3's own score weights (v1beta3/default_plugins.go:30-56), minus
+# NOT_APPLICABLE.
+V1BETA3_MULTIPOINT: list[tuple[str, int]] = [
+    ("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0), ("TaintToleration", 3), ("NodeAffinity", 2),
+    ("NodePorts", 0), ("NodeResourcesFit", 1), ("PodTopologySpread", 2), ("InterPodAffinity", 2),
+    ("DefaultPreemption", 0), ("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1), ("DefaultBinder", 0),
+]
+
+
 class ConfigError(ValueError):
     pass
 
@@ -93,7 +105,7 @@ class ConfigError(ValueError):
 def _strict(name: str, args: dict, allowed: set[str]) -> None:
     extra = set(args) - allowed - {"apiVersion", "kind"}
     if extra:
-        raise ConfigError(f'strict decoding error: unknown field(s) {sorted(extra)} in {name}Args')
+        raise ConfigError("strict decoding error: " + ", ".join(f'unknown field "{f}"' for f in sorted(extra)))
 
 
 def _resource_specs(v: Any, where: str) -> list[dict]:
@@ -119,7 +131,7 @@ def default_plugin_args(name: str, args: dict | None) -> dict:
     """Apply SetDefaults_<Name>Args (apis/config/v1beta2/defaults.go)."""
     a = copy.deepcopy(args or {})
     if name == "Coscheduling":
-        _strict(name, a, {"permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds", "kubeConfigPath", "kubeMaster"})
+        _strict(name, a, {"permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds"})
         a.setdefault("permitWaitingTimeSeconds", 60)
         a.setdefault("deniedPGExpirationTimeSeconds", 20)
         for k in ("permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds"):
@@ -297,7 +309,45 @@ def _names(entries: Any) -> list[tuple[str, int]]:
     return out
 
 
-def _resolve_profile(p: dict, api_version: str, available: set[str] | None) -> Profile:
+def _merge_plugin_set(defaults: list[tuple[str, int]], custom: dict) -> tuple[list[tuple[str, int]], set[str]]:
+    """mergePluginSet (v1beta2/v1beta3 default_plugins.go): a default plugin
+    re-enabled by the user is replaced *in place* (order kept, the user's
+    weight wins); disabled defaults are dropped ("*" drops all); the remaining
+    custom plugins are appended in the user's order. Returns (enabled,
+    disabled names)."""
+    disabled = {n for n, _ in _names(custom.get("disabled"))}
+    enabled = _names(custom.get("enabled"))
+    custom_idx = {n: i for i, (n, _) in enumerate(enabled)}
+    out: list[tuple[str, int]] = []
+    replaced: set[int] = set()
+    if "*" not in disabled:
+        for n, w in defaults:
+            if n in disabled:
+                continue
+            if n in custom_idx:
+                i = custom_idx[n]
+                replaced.add(i)
+                out.append(enabled[i])
+            else:
+                out.append((n, w))
+    out += [e for i, e in enumerate(enabled) if i not in replaced]
+    return out, disabled
+
+
+def _resolve_profile(p: dict, api_version: str, available: set[str] | None, index: int = 0) -> Profile:
+    """Resolve one profile the way kube-scheduler 1.23 does.
+
+    v1beta2: per extension point, mergePluginSet(DEFAULT_PLUGINS[pt], user).
+    v1beta3: the defaults live in multiPoint (V1BETA3_MULTIPOINT, with the
+    v1beta3 weights: TaintToleration 3, NodeAffinity / PodTopologySpread /
+    InterPodAffinity 2); multiPoint = mergePluginSet(defaults, user
+    multiPoint) and each point is expanded as in frameworkImpl.
+    expandMultiPointPlugins (framework/runtime/framework.go:420-485): the
+    point's explicit plugins first, then every multiPoint plugin implementing
+    the point that the point neither disables nor configures explicitly; a
+    point with "*" disabled gets no multiPoint plugins. Score weights: an
+    explicit score entry wins, else the multiPoint weight, 0 meaning 1.
+    """
     prof = Profile(scheduler_name=p.get("schedulerName") or "default-scheduler")
     if "percentageOfNodesToScore" in p and p["percentageOfNodesToScore"] is not None:
         prof.percentage_of_nodes_to_score = int(p["percentageOfNodesToScore"])
@@ -305,27 +355,26 @@ def _resolve_profile(p: dict, api_version: str, available: set[str] | None) -> P
     unknown = set(spec) - set(EXT_POINTS) - {"multiPoint"}
     if unknown:
         raise ConfigError(f"unknown extension point(s) {sorted(unknown)}")
-    if "multiPoint" in spec and not api_version.endswith("v1beta3"):
+    v1beta3 = api_version.endswith("v1beta3")
+    if "multiPoint" in spec and not v1beta3:
         raise ConfigError("multiPoint requires kubescheduler.config.k8s.io/v1beta3")
+    mp: list[tuple[str, int]] = []
+    if v1beta3:
+        mp, _ = _merge_plugin_set(V1BETA3_MULTIPOINT, spec.get("multiPoint") or {})
     weights: dict[str, int] = {}
     resolved: dict[str, list[str]] = {}
-    mp = spec.get("multiPoint") or {}
-    mp_enabled = _names(mp.get("enabled"))
-    mp_disabled = {n for n, _ in _names(mp.get("disabled"))}
     for pt in EXT_POINTS:
-        defaults = [] if "*" in mp_disabled else [(n, w) for n, w in DEFAULT_PLUGINS[pt] if n not in mp_disabled]
-        pts = spec.get(pt) or {}
-        disabled = {n for n, _ in _names(pts.get("disabled"))}
-        enabled = _names(pts.get("enabled"))
-        cur: list[tuple[str, int]] = []
-        if "*" not in disabled:
-            cur = [(n, w) for n, w in defaults if n not in disabled]
-        for n, w in mp_enabled:
-            if pt in PLUGIN_POINTS.get(n, ()) and n not in {x for x, _ in cur}:
-                cur.append((n, w))
-        for n, w in enabled:
-            cur = [(x, y) for x, y in cur if x != n]  # explicit enable re-positions/overrides weight
-            cur.append((n, w))
+        if v1beta3:
+            explicit, disabled = _merge_plugin_set([], spec.get(pt) or {})
+            cur = list(explicit)
+            if "*" not in disabled:
+                seen = {n for n, _ in explicit}
+                for n, w in mp:
+                    if pt in PLUGIN_POINTS.get(n, ()) and n not in disabled and n not in seen:
+                        cur.append((n, w))
+                        seen.add(n)
+        else:
+            cur, _ = _merge_plugin_set(DEFAULT_PLUGINS[pt], spec.get(pt) or {})
         names = []
         for n, w in cur:
             if n in NOT_APPLICABLE:
@@ -334,21 +383,28 @@ def _resolve_profile(p: dict, api_version: str, available: set[str] | None) -> P
                 raise ConfigError(f'plugin "{n}" does not exist')
             if pt not in PLUGIN_POINTS[n]:
                 raise ConfigError(f'plugin "{n}" does not extend {pt} plugin')
+            if n in names:
+                raise ConfigError(f'plugin "{n}" already registered as "{pt}"')
             if available is not None and n not in available:
                 continue  # registered in config tables but not compiled into this build
             names.append(n)
             if pt == "score":
-                weights[n] = w if w > 0 else weights.get(n, 1)
+                weights[n] = w if w > 0 else 1
         if pt == "queueSort" and len(names) > 1:
             raise ConfigError(f"profile {prof.scheduler_name}: only one queueSort plugin may be enabled, got {names}")
         resolved[pt] = names
     prof.plugins = resolved
     prof.score_weights = weights
-    for pc in p.get("pluginConfig") or []:
+    for j, pc in enumerate(p.get("pluginConfig") or []):
         name = pc.get("name")
         if not name:
             raise ConfigError("pluginConfig entry without name")
-        prof.plugin_config[name] = default_plugin_args(name, pc.get("args"))
+        try:
+            prof.plugin_config[name] = default_plugin_args(name, pc.get("args"))
+        except ConfigError as e:
+            # the strict codec's error shape (apis/config/scheme/scheme_test.go:313)
+            raise ConfigError(f"decoding .profiles[{index}].pluginConfig[{j}]: decoding args for plugin {name}: {e}") \
+                from None
     used = {n for names in resolved.values() for n in names}
     for n in used:
         if n not in prof.plugin_config:
@@ -382,7 +438,7 @@ def load_config(src: str | Path | dict | None = None, *, restrict_to_native: boo
         raise ConfigError(f"unsupported kind {doc.get('kind')!r}")
     available = _available_plugins() if restrict_to_native else None
     profiles_raw = doc.get("profiles") or [{"schedulerName": "default-scheduler"}]
-    profiles = [_resolve_profile(p, api, available) for p in profiles_raw]
+    profiles = [_resolve_profile(p, api, available, i) for i, p in enumerate(profiles_raw)]
     names = [p.scheduler_name for p in profiles]
     if len(set(names)) != len(names):
         raise ConfigError(f"duplicate profile schedulerName in {names}")
