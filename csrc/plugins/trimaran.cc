@@ -18,6 +18,7 @@
 //    present and the pod requests GPUs (score = min over valid dimensions).
 // Fixed: the pod-assign cache drops fully-stale node entries (the reference's
 // cleanupCache keeps them when every entry is stale, handler.go:114-138).
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <map>
@@ -33,8 +34,27 @@ namespace {
 constexpr int64_t kReportingIntervalS = 60;   // metricsAgentReportingIntervalSeconds
 constexpr int64_t kCacheCleanupUs = 5LL * 60 * 1000000;
 
+// Metric types / operators are interned at parse time so Score compares
+// integers, not strings, per node.
+enum MType : uint8_t { kTCPU, kTMemory, kTGPU, kTGPUMemory, kTOther };
+enum MOp : uint8_t { kOpAVG, kOpSTD, kOpLatest, kOpEmpty, kOpOther };
+MType mtype(const std::string& s) {
+  if (s == "CPU") return kTCPU;
+  if (s == "Memory") return kTMemory;
+  if (s == "GPU") return kTGPU;
+  if (s == "GPUMemory") return kTGPUMemory;
+  return kTOther;
+}
+MOp mop(const std::string& s) {
+  if (s == "AVG") return kOpAVG;
+  if (s == "STD") return kOpSTD;
+  if (s == "Latest") return kOpLatest;
+  if (s.empty()) return kOpEmpty;
+  return kOpOther;
+}
 struct Metric {
-  std::string type, op;
+  MType type = kTOther;
+  MOp op = kOpOther;
   double value = 0;
 };
 struct WatcherMetrics {
@@ -60,7 +80,7 @@ WatcherMetrics parse_metrics(const Json& j) {
   for (const auto& [node, nm] : nmm->members()) {
     auto& vec = m.nodes[node];
     for (const auto& x : nm["metrics"].items())
-      vec.push_back(Metric{x["type"].as_string(), x["operator"].as_string(), x["value"].as_double()});
+      vec.push_back(Metric{mtype(x["type"].as_string()), mop(x["operator"].as_string()), x["value"].as_double()});
   }
   return m;
 }
@@ -103,7 +123,10 @@ class TrimaranBase : public Plugin {
     }
     // Pod-assign cache over assigned pods (handler.go:68-101).
     auto np = Pod::from_json(*obj);
-    std::unique_lock<std::shared_mutex> g(mu_);
+    if (np->node_name.empty()) return;
+    Shard& sh = shard(np->node_name);
+    std::unique_lock<std::shared_mutex> g(sh.mu);
+    auto& assigned_ = sh.assigned;
     if (t == EventType::Deleted) {
       auto it = assigned_.find(np->node_name);
       if (it == assigned_.end()) return;
@@ -129,14 +152,16 @@ class TrimaranBase : public Plugin {
   }
 
   void cleanup() {
-    std::unique_lock<std::shared_mutex> g(mu_);
     int64_t now = wall_now_us() / 1000000;
-    for (auto it = assigned_.begin(); it != assigned_.end();) {
-      auto& v = it->second;
-      size_t idx = 0;
-      while (idx < v.size() && v[idx].first + kReportingIntervalS <= now) ++idx;
-      v.erase(v.begin(), v.begin() + static_cast<long>(idx));
-      it = v.empty() ? assigned_.erase(it) : std::next(it);
+    for (auto& sh : shards_) {
+      std::unique_lock<std::shared_mutex> g(sh.mu);
+      for (auto it = sh.assigned.begin(); it != sh.assigned.end();) {
+        auto& v = it->second;
+        size_t idx = 0;
+        while (idx < v.size() && v[idx].first + kReportingIntervalS <= now) ++idx;
+        v.erase(v.begin(), v.begin() + static_cast<long>(idx));
+        it = v.empty() ? sh.assigned.erase(it) : std::next(it);
+      }
     }
   }
 
@@ -145,22 +170,51 @@ class TrimaranBase : public Plugin {
     std::shared_lock<std::shared_mutex> g(mu_);
     return metrics_;
   }
+  // The metrics document of this scheduling cycle: fetched once per cycle
+  // and kept in CycleState, so the node-parallel Score takes no plugin lock
+  // and no shared_ptr refcount per node.
+  struct MetricsView : StateData {
+    std::shared_ptr<const WatcherMetrics> m;
+    std::shared_ptr<StateData> clone() const override { return std::make_shared<MetricsView>(*this); }
+  };
+  const WatcherMetrics& cycle_metrics(CycleState& s) const {
+    if (auto* v = s.read_as<MetricsView>(view_key_)) return *v->m;
+    std::lock_guard<std::mutex> g(view_mu_);
+    if (auto* v = dynamic_cast<MetricsView*>(s.read_raw(view_key_))) return *v->m;
+    auto v = std::make_shared<MetricsView>();
+    v->m = metrics();
+    const WatcherMetrics* out = v->m.get();
+    s.write(view_key_, std::move(v));
+    return *out;
+  }
   // Pods bound to `node` after the metrics window (or within one reporting
-  // interval of its end) are not reflected in the metrics yet.
+  // interval of its end) are not reflected in the metrics yet. The cache is
+  // sharded by node so parallel Score workers rarely share a lock.
   template <typename F>
   void for_missing(const std::string& node, int64_t window_end, F&& f) const {
-    std::shared_lock<std::shared_mutex> g(mu_);
-    auto it = assigned_.find(node);
-    if (it == assigned_.end()) return;
+    const Shard& sh = shard(node);
+    std::shared_lock<std::shared_mutex> g(sh.mu);
+    auto it = sh.assigned.find(node);
+    if (it == sh.assigned.end()) return;
     for (const auto& [ts, pod] : it->second)
       if (ts > window_end || (ts <= window_end && window_end - ts < kReportingIntervalS)) f(*pod);
   }
 
+  struct Shard {
+    mutable std::shared_mutex mu;
+    std::unordered_map<std::string, std::vector<std::pair<int64_t, PodPtr>>> assigned;
+  };
+  static constexpr size_t kShards = 32;
+  Shard& shard(const std::string& node) { return shards_[std::hash<std::string>{}(node) % kShards]; }
+  const Shard& shard(const std::string& node) const { return shards_[std::hash<std::string>{}(node) % kShards]; }
+
   Handle& h_;
   mutable std::shared_mutex mu_;
+  mutable std::mutex view_mu_;
+  std::string view_key_ = name_ + "/metrics-view";
   std::shared_ptr<const WatcherMetrics> metrics_ = std::make_shared<WatcherMetrics>();
   std::map<std::string, std::shared_ptr<const WatcherMetrics>> sources_;
-  std::unordered_map<std::string, std::vector<std::pair<int64_t, PodPtr>>> assigned_;
+  std::array<Shard, kShards> shards_;
   uint64_t timer_ = 0;
 };
 
@@ -195,16 +249,16 @@ class TargetLoadPacking : public TrimaranBase {
     return u;
   }
 
-  std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
-    auto m = metrics();
+  std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) override {
+    const WatcherMetrics* m = &cycle_metrics(s);
     if (!m->present) return {kMinNodeScore, {}};
     auto it = m->nodes.find(ni.name());
     if (it == m->nodes.end()) return {kMinNodeScore, {}};
-    const char* want = gpu_mode_ ? "GPU" : "CPU";
+    const MType want = gpu_mode_ ? kTGPU : kTCPU;
     double util = 0;
     bool found = false;
     for (const auto& x : it->second)
-      if (x.type == want && (x.op == "AVG" || x.op == "Latest")) {
+      if (x.type == want && (x.op == kOpAVG || x.op == kOpLatest)) {
         util = x.value;
         found = true;
       }
@@ -246,17 +300,17 @@ struct ResourceStats {
   }
 };
 
-bool resource_data(const std::vector<Metric>& ms, const std::string& type, double* avg, double* sd) {
+bool resource_data(const std::vector<Metric>& ms, MType type, double* avg, double* sd) {
   bool valid = false, avg_found = false;
   *avg = *sd = 0;
   for (const auto& x : ms) {
     if (x.type != type) continue;
-    if (x.op == "AVG") {
+    if (x.op == kOpAVG) {
       *avg = x.value;
       avg_found = true;
-    } else if (x.op == "STD") {
+    } else if (x.op == kOpSTD) {
       *sd = x.value;
-    } else if ((x.op.empty() || x.op == "Latest") && !avg_found) {
+    } else if ((x.op == kOpEmpty || x.op == kOpLatest) && !avg_found) {
       *avg = x.value;
     }
     valid = true;
@@ -273,8 +327,8 @@ class LoadVariationRiskBalancing : public TrimaranBase {
     if (sensitivity_ < 0) sensitivity_ = 1.0;
   }
 
-  std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
-    auto m = metrics();
+  std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) override {
+    const WatcherMetrics* m = &cycle_metrics(s);
     if (!m->present) return {kMinNodeScore, {}};
     auto it = m->nodes.find(ni.name());
     if (it == m->nodes.end()) return {kMinNodeScore, {}};
@@ -293,7 +347,7 @@ class LoadVariationRiskBalancing : public TrimaranBase {
     double scores[3];
     bool valid[3] = {false, false, false};
     double avg, sd;
-    if (resource_data(it->second, "CPU", &avg, &sd)) {
+    if (resource_data(it->second, kTCPU, &avg, &sd)) {
       ResourceStats rs;
       rs.capacity = static_cast<double>(ni.node->allocatable.get(kCPU));
       rs.req = static_cast<double>(req_cpu);
@@ -302,7 +356,7 @@ class LoadVariationRiskBalancing : public TrimaranBase {
       scores[0] = rs.score(margin_, sensitivity_);
       valid[0] = true;
     }
-    if (resource_data(it->second, "Memory", &avg, &sd)) {
+    if (resource_data(it->second, kTMemory, &avg, &sd)) {
       ResourceStats rs;
       const double mega = 1.0 / 1024.0 / 1024.0;
       rs.capacity = static_cast<double>(ni.node->allocatable.get(kMemory)) * mega;
@@ -313,7 +367,7 @@ class LoadVariationRiskBalancing : public TrimaranBase {
       valid[1] = true;
     }
     int gid = gpu_names().gpu_id();
-    if (p.limit_sum.get(gid) > 0 && resource_data(it->second, "GPU", &avg, &sd)) {
+    if (p.limit_sum.get(gid) > 0 && resource_data(it->second, kTGPU, &avg, &sd)) {
       ResourceStats rs;
       rs.capacity = static_cast<double>(ni.node->allocatable.get(gid));
       rs.req = static_cast<double>(p.limit_sum.get(gid));

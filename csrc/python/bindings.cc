@@ -485,6 +485,17 @@ PYBIND11_MODULE(_xsched, m) {
              }
              return to_py(out);
            })
+      .def("score_benchmark",
+           [](Scheduler& s, py::handle pod, int iterations) {
+             Json j = json_arg(pod);
+             Json out;
+             {
+               py::gil_scoped_release r;
+               s.score_benchmark(j, iterations, &out);
+             }
+             return to_py(out);
+           },
+           py::arg("pod"), py::arg("iterations") = 100)
       .def("metrics_text", [](Scheduler& s) { return s.metrics().expose(); })
       .def("set_trace", [](Scheduler& s, bool on) { s.tracer().enable(on); })
       .def("trace_json", [](Scheduler& s) { return s.tracer().chrome_json(); })

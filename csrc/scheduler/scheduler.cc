@@ -941,6 +941,33 @@ Json Scheduler::explain(const Json& pod_obj) {
   return out;
 }
 
+double Scheduler::score_benchmark(const Json& pod_obj, int iterations, Json* out) {
+  std::lock_guard<std::mutex> g(sched_mu_);
+  auto pod = Pod::from_json(pod_obj);
+  Framework* fw = framework_for(pod->scheduler_name);
+  if (!fw) throw std::runtime_error("no profile for schedulerName " + pod->scheduler_name);
+  cache_->update_snapshot(snapshot_);
+  const std::vector<NodeInfoPtr>& nodes = snapshot_.nodes;
+  int64_t checksum = 0;
+  int64_t t0 = clock_->now_us();
+  for (int it = 0; it < std::max(1, iterations); ++it) {
+    CycleState st;
+    std::vector<NodeScore> scores;
+    Status s = fw->run_pre_score(st, *pod, nodes);
+    if (s.is_success()) s = fw->run_score(st, *pod, nodes, scores);
+    if (!s.is_success()) throw std::runtime_error(s.message());
+    for (const auto& x : scores) checksum += x.score;
+  }
+  double us = static_cast<double>(clock_->now_us() - t0) / std::max(1, iterations);
+  if (out) {
+    *out = Json::object();
+    out->set("nodes", Json(static_cast<int64_t>(nodes.size())));
+    out->set("us_per_pass", Json(us));
+    out->set("checksum", Json(checksum));
+  }
+  return us;
+}
+
 void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
                               int64_t cycle, Status permit_status, int64_t wait_start_us,
                               std::shared_ptr<PodsToActivate> to_activate) {

@@ -115,6 +115,12 @@ class Scheduler {
   // Dry-run one scheduling cycle for `pod` (no assume/bind): filter verdicts
   // per node, per-plugin normalized scores and the host that would be chosen.
   Json explain(const Json& pod);
+  // Score micro-benchmark (the reference's BenchmarkTargetLoadPackingPlugin,
+  // pkg/trimaran/targetloadpacking/targetloadpacking_test.go:267-360):
+  // PreScore + node-parallel Score + NormalizeScore of `pod` over every node
+  // of the snapshot, `iterations` times. Returns the mean microseconds per
+  // pass (and the node count / a checksum of the totals in `out`).
+  double score_benchmark(const Json& pod, int iterations, Json* out = nullptr);
 
   SchedulingQueue& queue() { return *queue_; }
   SchedulerCache& cache() { return *cache_; }
