@@ -361,8 +361,12 @@ void Scheduler::handle_event(const WatchEvent& ev) {
 void Scheduler::handle_pod_event(const WatchEvent& ev) {
   for (auto& fw : frameworks_) fw->dispatch_object_event("pods", static_cast<int>(ev.type), ev.obj, ev.old);
   if (ev.type == EventType::Deleted) {
-    auto p = Pod::from_json(*ev.obj);
-    PodPtr known = informers_->pod(p->ns(), p->name());
+    // The lister copy stands in for the final state when it is the same pod
+    // on the same node (all deletion needs), saving a parse per delete.
+    const Json& md = (*ev.obj)["metadata"];
+    PodPtr p = informers_->pod(md["namespace"].as_string(), md["name"].as_string());
+    if (!p || p->uid() != md["uid"].as_string() || p->node_name != (*ev.obj)["spec"]["nodeName"].as_string())
+      p = Pod::from_json(*ev.obj);
     informers_->delete_pod(*p);
     if (!p->node_name.empty()) {
       cache_->remove_pod(*p);
@@ -624,25 +628,29 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   // Per-node failures go to a position-indexed buffer (no lock, no map
   // insert per node); the NodeToStatusMap is only materialized when the
   // diagnosis is consumed: no feasible node (PostFilter / FitError) or explain.
-  fail_buf_.assign(n, Status());
-  fail_set_.assign(n, 0);
+  // Equivalence-cache verdicts are referenced in place, not copied: a Status
+  // copy bumps the refcount of a failure status shared by every node, and 16
+  // workers doing that per node serialize on its cache line.
+  if (static_cast<int>(fail_buf_.size()) < n) fail_buf_.resize(n);
+  fail_ptr_.assign(n, nullptr);
   parallelizer_->until(n, [&](int i) {
     const int pos = (start + i) % n;
     const NodeInfoPtr& ni = all[pos];
-    Status fst;
+    Status own;
+    const Status* fp = &own;
     if (eq_filter) {
       EqSlot& slot = eq->slots[pos];
       if (slot.filter_gen == ni->generation) {
-        fst = slot.filter;
         hits.fetch_add(1, std::memory_order_relaxed);
       } else {
-        fst = fw.run_filter(s, p, *ni);
-        slot.filter = fst;
+        slot.filter = fw.run_filter(s, p, *ni);
         slot.filter_gen = ni->generation;
       }
+      fp = &slot.filter;
     } else {
-      fst = fw.run_filter_with_nominated_pods(s, p, *ni);
+      own = fw.run_filter_with_nominated_pods(s, p, *ni);
     }
+    const Status& fst = *fp;
     processed.fetch_add(1, std::memory_order_relaxed);
     if (fst.is_success()) {
       int len = count.fetch_add(1) + 1;
@@ -656,8 +664,11 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       return;
     }
     if (fst.is_unschedulable()) {
-      fail_buf_[pos] = std::move(fst);
-      fail_set_[pos] = 1;
+      if (fp == &own) {
+        fail_buf_[pos] = std::move(own);
+        fp = &fail_buf_[pos];
+      }
+      fail_ptr_[pos] = fp;
       return;
     }
     std::lock_guard<std::mutex> g(mu);
@@ -679,9 +690,9 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   feasible.assign(found.begin(), found.begin() + c);
   if (feasible.empty() || full_diagnosis) {
     for (int pos = 0; pos < n; ++pos) {
-      if (!fail_set_[pos]) continue;
-      d.unschedulable_plugins.insert(fail_buf_[pos].failed_plugin());
-      d.node_to_status[all[pos]->name()] = std::move(fail_buf_[pos]);
+      if (!fail_ptr_[pos]) continue;
+      d.unschedulable_plugins.insert(fail_ptr_[pos]->failed_plugin());
+      d.node_to_status[all[pos]->name()] = *fail_ptr_[pos];
     }
   }
   if (feasible.empty()) {
@@ -884,6 +895,8 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   if (pst.is_success()) {
     binder_->submit([=] { binding_cycle(fw, state, qpi, assumed, host, cycle, Status(), permit_start, to_activate); });
   }
+  if (tracer_.enabled())
+    tracer_.record(TraceEvent{"assume_reserve_permit", assumed->key(), "", algo_end, clock_->now_us() - algo_end, 0});
 }
 
 Json Scheduler::explain(const Json& pod_obj) {

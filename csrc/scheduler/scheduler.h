@@ -160,7 +160,7 @@ class Scheduler {
   EqEntry* eq_entry(Framework& fw, const Pod& p);
   void release_retired();
   std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
-  std::vector<char> fail_set_;
+  std::vector<const Status*> fail_ptr_;
 
   void informer_loop();
   void handle_event(const WatchEvent& ev);
