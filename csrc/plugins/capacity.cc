@@ -106,6 +106,13 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       if (it != infos_.end()) {
         info.pods = it->second.pods;
         info.used = it->second.used;
+      } else {
+        // Pods and quotas arrive on separate watches: assigned pods seen before
+        // their namespace's quota were not counted then, so count them now
+        // (add_pod dedupes by key, so a later pod event cannot double count).
+        for (const auto& p : h_.informers->all_pods())
+          if (p->ns() == eq->meta.ns && !p->node_name.empty() && p->phase != "Succeeded" && p->phase != "Failed")
+            info.add_pod(*p);
       }
       infos_[eq->meta.ns] = std::move(info);
       return;

@@ -465,6 +465,14 @@ PYBIND11_MODULE(_xsched, m) {
              d["assumed"] = s.cache().assumed_count();
              return d;
            })
+      .def("lister_counts",
+           [](Scheduler& s) {
+             py::dict d;
+             d["pods"] = s.informers().pod_count();
+             d["podgroups"] = s.informers().pod_groups().size();
+             d["elasticquotas"] = s.informers().elastic_quotas().size();
+             return d;
+           })
       .def("assigned_in_group", [](Scheduler& s, const std::string& pg) { return s.cache().assigned_in_group(pg); })
       .def("waiting_pods",
            [](Scheduler& s) {

@@ -196,6 +196,9 @@ def test_capacity_scheduling_integration(http_cluster, name, exist, add, eqs, ex
     try:
         for q in eqs:
             client.create("elasticquotas", q)
+        # Quotas and pods come on separate watches; let the quota informer
+        # sync first, as the reference's test waits for its informers.
+        assert _wait(lambda: rs.scheduler.lister_counts()["elasticquotas"] >= len(eqs), 10)
         for p in exist:
             client.create("pods", p)
         assert _wait(lambda: all(_bound(client).get(p["metadata"]["name"]) for p in exist), 10)
