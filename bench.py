@@ -42,6 +42,8 @@ def main() -> int:
                     help='JSON scheduler options for A/B runs, e.g. \'{"equivalenceCache": false}\'')
     ap.add_argument("--no-scenarios", action="store_true",
                     help="skip the per-BASELINE-config scenarios (untimed, reported under config.scenarios)")
+    ap.add_argument("--cpus", default=os.environ.get("XSCHED_CPUS", "l3"),
+                    help="shard CPU placement: none | l3 | l3xK | explicit list (utils/cpuaffinity.py)")
     args = ap.parse_args()
 
     from flex_gpu_scheduler_amd.parallel.dist import init_distributed
@@ -66,6 +68,18 @@ def main() -> int:
         extras["gpu"] = {"name": props.get("gcnArchName"), "computeUnits": props.get("computeUnits"),
                          "hbm_gib": hbm_gib}
 
+    from flex_gpu_scheduler_amd.utils.cpuaffinity import apply as pin_cpus, ranked_domains
+
+    # One L3 domain per shard (8 cores / 16 CPUs on the MI355X hosts): the
+    # shard's threads hand work to each other ~10^5 times/s and floating over
+    # 256 CPUs costs 2x throughput (profiles/r1g_affinity_ab.txt). Rank 0's
+    # idle ranking is shared so the ranks of one node take disjoint domains.
+    order = None
+    if args.cpus.startswith("l3"):
+        order = ctx.gather(ranked_domains())[0] if ctx.distributed else ranked_domains()
+    cpus = pin_cpus(args.cpus, ctx.local_rank, order=order)  # before the shard's threads start
+    if cpus:
+        extras["cpus"] = {"mode": args.cpus, "n": len(cpus), "first": cpus[0]}
     spec = ClusterSpec(nodes=args.nodes, hbm_gib=hbm_gib)
     shard = Shard(spec, namespace=f"bench-r{ctx.rank}", seed=args.seed + 7919 * ctx.rank,
                   options=json.loads(args.sched_options))

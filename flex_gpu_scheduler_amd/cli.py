@@ -181,8 +181,11 @@ def cmd_scheduler(args) -> int:
     from .control.remote import RemoteScheduler
     from .gpu.telemetry import WatcherFetcher
 
+    from .utils.cpuaffinity import apply as pin_cpus
+
     cfg = load_config(args.config)
     remote = _client(args)
+    pin_cpus(getattr(args, "cpu_affinity", "none"))  # before the scheduler's threads start
     options = {}
     if args.trace:
         options["trace"] = True
@@ -403,6 +406,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--lock-name")
     p.add_argument("--lock-namespace", default="kube-system")
     p.add_argument("--trace", action="store_true", help="record per-cycle phase traces (/debug/trace)")
+    p.add_argument("--cpu-affinity", default="none",
+                   help="pin the scheduler's threads: none | l3 | l3xK | CPU list (utils/cpuaffinity.py)")
     p.set_defaults(fn=cmd_scheduler)
 
     p = sub.add_parser("controller", help="PodGroup + ElasticQuota controllers")
