@@ -208,7 +208,8 @@ class Coscheduling : public Plugin {
       return {Status(Code::Wait), wait_time(*pg)};
     }
     h_.waiting_pods->iterate([&](const WaitingPodPtr& wp) {
-      if (wp->pod()->pg_full_name() == full) wp->allow(name());
+      const Pod& q = *wp->pod();  // flat group key first: no string build per waiting pod
+      if (q.pg_key == p->pg_key && q.pod_group == p->pod_group && q.ns() == p->ns()) wp->allow(name());
     });
     return {Status(), 0};
   }

@@ -272,8 +272,8 @@ class FlexGPU : public Plugin {
     auto st = std::make_shared<AssignmentState>();
     st->annotations.set(gn.index_annotation, Json(join_ints(pl.gpus)));
     if (!pl.parts.empty()) st->annotations.set(gn.partition_annotation, Json(join_parts(pl.parts)));
-    Json ann = st->annotations;
-    h_.cache->mutate_pod(p->uid(), [&](Pod& cp) {
+    const Json& ann = st->annotations;
+    h_.cache->mutate_assumed_pod(p->uid(), [&](Pod& cp) {
       for (const auto& kv : ann.members()) {
         bool set = false;
         for (auto& a : cp.meta.annotations)

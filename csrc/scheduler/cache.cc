@@ -209,6 +209,23 @@ PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<vo
   return fresh;
 }
 
+PodPtr SchedulerCache::mutate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = pod_states_.find(uid);
+    if (it == pod_states_.end()) return nullptr;
+    if (assumed_.count(uid) && !it->second.binding_finished) {
+      PodPtr pod = it->second.pod;
+      remove_pod_locked(*pod);
+      fn(*pod);
+      pod->recompute_gpu_assignment();
+      add_pod_locked(pod);
+      return pod;
+    }
+  }
+  return mutate_pod(uid, fn);
+}
+
 int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us) {
   int64_t t0 = lock_wait_us ? clock_->now_us() : 0;
   std::lock_guard<std::mutex> g(mu_);

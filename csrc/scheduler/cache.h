@@ -48,6 +48,10 @@ class SchedulerCache {
   // Copy-on-write mutation of a cached (assumed or bound) pod; re-accounts
   // the pod on its node. Returns the new object (nullptr if not cached).
   PodPtr mutate_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
+  // In-place variant for a pod assumed in the current scheduling cycle
+  // (Reserve): no other thread holds that object yet, so the copy is skipped.
+  // Falls back to mutate_pod for pods that are not assumed.
+  PodPtr mutate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
 
   // Returns the number of NodeInfo versions refreshed (shared, not cloned:
   // the cache copies on write); replaced versions go to `s.retired`; `lock_wait_us` (optional)

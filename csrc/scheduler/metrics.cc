@@ -106,20 +106,28 @@ Histogram& Metrics::histogram(const std::string& name, const std::string& labels
   return *h;
 }
 
-void Metrics::inc(const std::string& name, const std::string& labels, double by) {
-  std::lock_guard<std::mutex> g(mu_);
+Counter& Metrics::cell_locked(const std::string& name, const std::string& labels, const char* type) {
   auto it = fams_.find(name);
   Family& f = it != fams_.end() ? it->second : fams_[name];
-  if (f.type.empty()) f.type = "counter";
-  f.values[labels] += by;
+  if (f.type.empty()) f.type = type;
+  auto& c = f.values[labels];
+  if (!c) c.reset(new Counter());
+  return *c;
+}
+
+Counter& Metrics::counter_ref(const std::string& name, const std::string& labels) {
+  std::lock_guard<std::mutex> g(mu_);
+  return cell_locked(name, labels, "counter");
+}
+
+void Metrics::inc(const std::string& name, const std::string& labels, double by) {
+  std::lock_guard<std::mutex> g(mu_);
+  cell_locked(name, labels, "counter").inc(by);
 }
 
 void Metrics::set_gauge(const std::string& name, const std::string& labels, double v) {
   std::lock_guard<std::mutex> g(mu_);
-  auto it = fams_.find(name);
-  Family& f = it != fams_.end() ? it->second : fams_[name];
-  if (f.type.empty()) f.type = "gauge";
-  f.values[labels] = v;
+  cell_locked(name, labels, "gauge").set(v);
 }
 
 double Metrics::counter(const std::string& name, const std::string& labels) const {
@@ -127,15 +135,18 @@ double Metrics::counter(const std::string& name, const std::string& labels) cons
   auto it = fams_.find(name);
   if (it == fams_.end()) return 0;
   auto vit = it->second.values.find(labels);
-  return vit == it->second.values.end() ? 0 : vit->second;
+  return vit == it->second.values.end() ? 0 : vit->second->value();
 }
 
 void Metrics::reset() {
   std::lock_guard<std::mutex> g(mu_);
   for (auto& kv : fams_) {
+    for (auto& h : kv.second.hists) retired_hists_.push_back(std::move(h.second));
+    for (auto& v : kv.second.values) retired_cells_.push_back(std::move(v.second));
     kv.second.hists.clear();
     kv.second.values.clear();
   }
+  epoch_.fetch_add(1, std::memory_order_release);
 }
 
 std::string Metrics::expose() const {
@@ -146,7 +157,7 @@ std::string Metrics::expose() const {
     if (f.hists.empty() && f.values.empty()) continue;
     out += "# HELP " + name + " " + f.help + "\n# TYPE " + name + " " + f.type + "\n";
     for (const auto& [labels, v] : f.values) {
-      std::snprintf(buf, sizeof buf, "%.17g", v);
+      std::snprintf(buf, sizeof buf, "%.17g", v->value());
       out += name + (labels.empty() ? "" : "{" + labels + "}") + " " + buf + "\n";
     }
     for (const auto& [labels, h] : f.hists) {

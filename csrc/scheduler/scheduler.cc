@@ -730,6 +730,22 @@ std::string Scheduler::select_host(const std::vector<NodeScore>& scores) {
   return scores[sel].name;
 }
 
+Scheduler::CycleMetrics& Scheduler::cycle_metrics(const Framework& fw) {
+  CycleMetrics& m = cycle_metrics_[&fw];
+  uint64_t e = metrics_->epoch();
+  if (m.epoch != e) {
+    static const char* kResults[3] = {"scheduled", "unschedulable", "error"};
+    m.algo = &metrics_->histogram("scheduler_scheduling_algorithm_duration_seconds", "");
+    for (int i = 0; i < 3; ++i) {
+      std::string labels = "profile=\"" + fw.profile_name() + "\",result=\"" + kResults[i] + "\"";
+      m.attempt[i] = &metrics_->histogram("scheduler_scheduling_attempt_duration_seconds", labels);
+      m.attempts[i] = &metrics_->counter_ref("scheduler_schedule_attempts_total", labels);
+    }
+    m.epoch = e;
+  }
+  return m;
+}
+
 void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   PodPtr pod = qpi->pod;
   Framework* fw = framework_for(pod->scheduler_name);
@@ -800,8 +816,8 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     }
   }
   int64_t algo_end = clock_->now_us();
-  metrics_->histogram("scheduler_scheduling_algorithm_duration_seconds", "")
-      .observe(static_cast<double>(algo_end - cycle_start) / 1e6);
+  CycleMetrics& cm = cycle_metrics(*fw);
+  cm.algo->observe(static_cast<double>(algo_end - cycle_start) / 1e6);
   if (tracer_.enabled())
     tracer_.record(TraceEvent{"schedule", pod->key(), st.is_success() ? host : st.message(), cycle_start,
                               algo_end - cycle_start, 0});
@@ -817,10 +833,9 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         ++stats_.preemption_attempts;
       }
     }
-    std::string result = fit_error ? "unschedulable" : "error";
-    metrics_->inc("scheduler_schedule_attempts_total", "profile=\"" + profile + "\",result=\"" + result + "\"");
-    metrics_->histogram("scheduler_scheduling_attempt_duration_seconds", "profile=\"" + profile + "\",result=\"" + result + "\"")
-        .observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
+    const int result = fit_error ? 1 : 2;
+    cm.attempts[result]->inc();
+    cm.attempt[result]->observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
     {
       std::lock_guard<std::mutex> g(stats_mu_);
       if (fit_error) ++stats_.unschedulable; else ++stats_.errors;
@@ -842,8 +857,10 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   // counted twice by nominated-pod-aware checks (scheduler.go assume():
   // DeleteNominatedPodIfExists).
   if (!nominator_->empty()) nominator_->remove(*assumed);
+  int64_t t_assumed = tracer_.enabled() ? clock_->now_us() : 0;
   // Reserve.
   Status rst = fw->run_reserve(*state, assumed, host);
+  int64_t t_reserved = tracer_.enabled() ? clock_->now_us() : 0;
   if (!rst.is_success()) {
     fw->run_unreserve(*state, assumed, host);
     cache_->forget_pod(*assumed);
@@ -875,6 +892,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
                    pst.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{pst.failed_plugin()});
     return;
   }
+  int64_t t_permitted = tracer_.enabled() ? clock_->now_us() : 0;
   if (pst.is_success()) note_gang_event(*assumed, false);
   // Activate siblings stashed by plugins (scheduler.go:543-548).
   {
@@ -885,9 +903,8 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     }
     if (!act.empty()) queue_->activate(act);
   }
-  metrics_->inc("scheduler_schedule_attempts_total", "profile=\"" + profile + "\",result=\"scheduled\"");
-  metrics_->histogram("scheduler_scheduling_attempt_duration_seconds", "profile=\"" + profile + "\",result=\"scheduled\"")
-      .observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
+  cm.attempts[0]->inc();
+  cm.attempt[0]->observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
   {
     std::lock_guard<std::mutex> g(stats_mu_);
     ++stats_.scheduled;
@@ -895,8 +912,14 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   if (pst.is_success()) {
     binder_->submit([=] { binding_cycle(fw, state, qpi, assumed, host, cycle, Status(), permit_start, to_activate); });
   }
-  if (tracer_.enabled())
-    tracer_.record(TraceEvent{"assume_reserve_permit", assumed->key(), "", algo_end, clock_->now_us() - algo_end, 0});
+  if (tracer_.enabled()) {
+    int64_t t_end = clock_->now_us();
+    tracer_.record(TraceEvent{"assume_reserve_permit", assumed->key(), "", algo_end, t_end - algo_end, 0});
+    tracer_.record(TraceEvent{"assume", assumed->key(), "", algo_end, t_assumed - algo_end, 0});
+    tracer_.record(TraceEvent{"reserve", assumed->key(), "", t_assumed, t_reserved - t_assumed, 0});
+    tracer_.record(TraceEvent{"permit", assumed->key(), "", t_reserved, t_permitted - t_reserved, 0});
+    tracer_.record(TraceEvent{"activate_metrics", assumed->key(), "", t_permitted, t_end - t_permitted, 0});
+  }
 }
 
 Json Scheduler::explain(const Json& pod_obj) {

@@ -161,6 +161,16 @@ class Scheduler {
   void release_retired();
   std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
   std::vector<const Status*> fail_ptr_;
+  // Per-profile metric cells of the scheduling cycle, cached per metrics
+  // epoch (scheduling thread / sched_mu_ only).
+  struct CycleMetrics {
+    uint64_t epoch = ~0ULL;
+    Histogram* algo = nullptr;
+    Histogram* attempt[3] = {};  // scheduled, unschedulable, error
+    Counter* attempts[3] = {};
+  };
+  std::unordered_map<const Framework*, CycleMetrics> cycle_metrics_;
+  CycleMetrics& cycle_metrics(const Framework& fw);
 
   void informer_loop();
   void handle_event(const WatchEvent& ev);
