@@ -24,6 +24,29 @@ class Parser {
     return v;
   }
 
+  // Top-level array, one element at a time (bulk creates pipeline parsing
+  // with store inserts and informer hand-off).
+  void parse_array_stream(const std::function<void(Json&&)>& fn) {
+    ws();
+    if (p_ >= end_ || *p_ != '[') fail("expected a JSON array");
+    ++p_;
+    ws();
+    if (p_ < end_ && *p_ == ']') {
+      ++p_;
+    } else {
+      for (;;) {
+        ws();
+        fn(value(1));
+        ws();
+        if (p_ < end_ && *p_ == ',') { ++p_; continue; }
+        if (p_ < end_ && *p_ == ']') { ++p_; break; }
+        fail("expected ',' or ']'");
+      }
+    }
+    ws();
+    if (p_ != end_) fail("trailing characters");
+  }
+
  private:
   const char* p_;
   const char* end_;
@@ -374,6 +397,10 @@ std::string Json::dump() const {
 }
 
 Json Json::parse(std::string_view text) { return Parser(text).parse_document(); }
+
+void Json::parse_array_stream(std::string_view text, const std::function<void(Json&&)>& fn) {
+  Parser(text).parse_array_stream(fn);
+}
 
 void Json::merge_patch(const Json& patch) {
   if (!patch.is_object()) {

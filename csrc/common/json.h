@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -97,6 +98,8 @@ class Json {
   std::string dump() const;
   void dump_to(std::string& out) const;
   static Json parse(std::string_view text);
+  // Calls fn for each element of a top-level JSON array as it is parsed.
+  static void parse_array_stream(std::string_view text, const std::function<void(Json&&)>& fn);
 
   // RFC 7386 JSON merge patch (the "application/merge-patch+json" patch type
   // used by the reference's util.CreateMergePatch callers).

@@ -295,14 +295,21 @@ PYBIND11_MODULE(_xsched, m) {
       .def("create", [](ObjectStore& s, const std::string& kind, py::handle obj) { return ptr_to_py(s.create(kind, json_arg(obj))); })
       .def("create_many",
            [](ObjectStore& s, const std::string& kind, py::handle objs) {
-             Json arr = json_arg(objs);
-             std::vector<Json> v(arr.items().begin(), arr.items().end());
-             size_t n;
-             {
+             // A JSON string is parsed element by element with the GIL
+             // released and committed in PodGroup-aligned chunks, so the
+             // informer and scheduler start on the first gangs while the rest
+             // is still being parsed (see ObjectStore::create_chunked).
+             if (py::isinstance<py::str>(objs)) {
+               std::string text = objs.cast<std::string>();
                py::gil_scoped_release r;
-               n = s.create_many(kind, std::move(v)).size();
+               return s.create_chunked(kind, [&](const std::function<void(Json&&)>& emit) {
+                 Json::parse_array_stream(text, emit);
+               });
              }
-             return n;
+             Json arr = json_arg(objs);
+             std::vector<Json> v = std::move(arr.items_mut());
+             py::gil_scoped_release r;
+             return s.create_many(kind, std::move(v)).size();
            })
       .def("get",
            [](ObjectStore& s, const std::string& kind, const std::string& ns, const std::string& name) {

@@ -284,27 +284,48 @@ void Scheduler::informer_loop() {
     auto evs = watcher_->next(50, 8192);
     if (evs.empty()) continue;
     int64_t batch_start = tracer_.enabled() ? clock_->now_us() : 0;
-    // Pass 1: parse every pod once and publish it to the listers first, so a
-    // PreFilter racing this batch sees every sibling of a PodGroup created
-    // together (Coscheduling counts them). Pass 2 drives cache and queue.
+    // The batch is handled in windows of >= kInformerWindow events that end
+    // on a PodGroup boundary, so the scheduling thread starts on the first
+    // gangs of a bulk create instead of waiting for the whole batch.
+    // Per window, pass 1 parses every pod once and publishes it to the
+    // listers, so a PreFilter racing the window sees every sibling of a
+    // PodGroup created together (Coscheduling counts them); pass 2 then
+    // drives cache and queue.
     std::vector<PodPtr> parsed(evs.size());
     std::vector<PodPtr> prev(evs.size());
-    for (size_t i = 0; i < evs.size(); ++i) {
-      const auto& ev = evs[i];
-      if (ev.kind != "pods" || ev.type == EventType::Deleted) continue;
-      try {
-        parsed[i] = Pod::from_json(*ev.obj);
-      } catch (const std::exception&) {
-        continue;
+    auto group_of = [](const WatchEvent& ev) -> const std::string& {
+      return (*ev.obj)["metadata"]["labels"][kPodGroupLabel].as_string();
+    };
+    size_t lo = 0;
+    while (lo < evs.size()) {
+      size_t hi = lo;
+      while (hi < evs.size()) {
+        const auto& ev = evs[hi];
+        if (hi - lo >= kInformerWindow) {
+          const auto& pe = evs[hi - 1];
+          bool same_group = ev.kind == "pods" && pe.kind == "pods" && ev.type == EventType::Added &&
+                            pe.type == EventType::Added && !group_of(ev).empty() && group_of(ev) == group_of(pe);
+          if (!same_group) break;
+        }
+        ++hi;
+        if (ev.kind != "pods" || ev.type == EventType::Deleted) continue;
+        try {
+          parsed[hi - 1] = Pod::from_json(*ev.obj);
+        } catch (const std::exception&) {
+          continue;
+        }
+        prev[hi - 1] = informers_->pod(parsed[hi - 1]->ns(), parsed[hi - 1]->name());
+        informers_->upsert_pod(parsed[hi - 1]);
       }
-      prev[i] = informers_->pod(parsed[i]->ns(), parsed[i]->name());
-      informers_->upsert_pod(parsed[i]);
-    }
-    for (size_t i = 0; i < evs.size(); ++i) {
-      if (parsed[i])
-        handle_parsed_pod_event(evs[i], parsed[i], prev[i]);
-      else
-        handle_event(evs[i]);
+      for (size_t i = lo; i < hi; ++i) {
+        if (parsed[i])
+          handle_parsed_pod_event(evs[i], parsed[i], prev[i]);
+        else
+          handle_event(evs[i]);
+        parsed[i].reset();
+        prev[i].reset();
+      }
+      lo = hi;
     }
     if (tracer_.enabled() && batch_start)
       tracer_.record(TraceEvent{"informer_batch", std::to_string(evs.size()) + " events", "", batch_start,

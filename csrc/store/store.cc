@@ -193,6 +193,30 @@ std::vector<JsonPtr> ObjectStore::create_many(const std::string& kind, std::vect
   return out;
 }
 
+size_t ObjectStore::create_chunked(const std::string& kind,
+                                  const std::function<void(const std::function<void(Json&&)>&)>& produce) {
+  auto group_of = [](const Json& o) -> const std::string& {
+    return o["metadata"]["labels"]["pod-group.scheduling.sigs.k8s.io"].as_string();
+  };
+  std::vector<Json> chunk;
+  chunk.reserve(2 * kCreateChunk);
+  size_t n = 0;
+  auto flush = [&] {
+    if (chunk.empty()) return;
+    n += create_many(kind, std::move(chunk)).size();
+    chunk.clear();
+  };
+  produce([&](Json&& o) {
+    if (chunk.size() >= kCreateChunk) {
+      const std::string& g = group_of(o);
+      if (g.empty() || g != group_of(chunk.back())) flush();
+    }
+    chunk.push_back(std::move(o));
+  });
+  flush();
+  return n;
+}
+
 void ObjectStore::flush_batch_locked(std::vector<WatchEvent>& batch) {
   // One hand-off (one lock + one wake-up) per watcher for the whole batch, so
   // an informer sees a bulk create atomically (all PodGroup siblings at once).

@@ -118,6 +118,13 @@ class ObjectStore {
 
   // Bulk helpers for benchmarks (one lock hold, one event per object).
   std::vector<JsonPtr> create_many(const std::string& kind, std::vector<Json> objs);
+  // Streaming bulk create: `produce` calls emit(obj) per object. Objects are
+  // committed in chunks of >= kCreateChunk that end on a PodGroup boundary
+  // (pod-group label change), each flushed to watchers as one batch, so a
+  // gang is always seen whole while the next chunk is still being produced.
+  static constexpr size_t kCreateChunk = 64;
+  size_t create_chunked(const std::string& kind,
+                        const std::function<void(const std::function<void(Json&&)>&)>& produce);
   size_t delete_all(const std::string& kind, const std::string& ns = "");
 
   static std::string key_of(const std::string& ns, const std::string& name) { return ns.empty() ? name : ns + "/" + name; }

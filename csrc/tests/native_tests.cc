@@ -305,6 +305,57 @@ TEST(store_watch_replay_and_expiry) {
   CHECK(dup);
 }
 
+TEST(store_create_chunked_keeps_gangs_whole) {
+  // 200 pods in gangs of 3 (plus ungrouped pods every 10th), streamed from
+  // JSON text: watchers see commits of >= kCreateChunk pods, each ending on a
+  // gang boundary, and the first commit before the producer has finished.
+  std::string text = "[";
+  std::vector<std::string> group(200);
+  for (int i = 0; i < 200; ++i) {
+    group[i] = i % 10 == 9 ? "" : "g" + std::to_string(i / 3);
+    std::string labels = group[i].empty() ? "{}" : R"({"pod-group.scheduling.sigs.k8s.io":")" + group[i] + "\"}";
+    text += (i ? "," : "") + std::string(R"({"metadata":{"namespace":"d","name":"p)") + std::to_string(i) +
+            R"(","labels":)" + labels + "}}";
+  }
+  text += "]";
+  ObjectStore st;
+  auto w = st.watch({"pods"}, "d", 0);
+  std::vector<size_t> seen_at_emit;  // visible events when each object was emitted
+  size_t visible = 0, emitted = 0;
+  std::vector<size_t> commits;
+  size_t n = st.create_chunked("pods", [&](const std::function<void(Json&&)>& emit) {
+    Json::parse_array_stream(text, [&](Json&& o) {
+      auto evs = w->next(0, 100000);
+      if (!evs.empty()) {
+        visible += evs.size();
+        commits.push_back(visible);
+      }
+      ++emitted;
+      emit(std::move(o));
+    });
+  });
+  auto rest = w->next(100, 100000);
+  visible += rest.size();
+  CHECK_EQ(n, 200u);
+  CHECK_EQ(visible, 200u);
+  CHECK(!commits.empty());  // pipelined: something was visible mid-stream
+  size_t prev = 0;
+  for (size_t c : commits) {
+    CHECK(c - prev >= ObjectStore::kCreateChunk);
+    CHECK(c < 200);
+    // Commit ends on a gang boundary.
+    CHECK(group[c].empty() || group[c] != group[c - 1]);
+    prev = c;
+  }
+  bool bad_array = false;
+  try {
+    Json::parse_array_stream("{}", [](Json&&) {});
+  } catch (const JsonError&) {
+    bad_array = true;
+  }
+  CHECK(bad_array);
+}
+
 }  // namespace
 
 int main() {

@@ -44,7 +44,7 @@ def _pods(names, pg, phase, owners=None):
     return out
 
 
-def wait_for(fn, timeout=5.0):
+def wait_for(fn, timeout=15.0):  # generous: the suite runs under xdist
     deadline = time.time() + timeout
     while time.time() < deadline:
         v = fn()
@@ -191,8 +191,8 @@ def test_elasticquota_used(store, client, case):
     try:
         for (ns, name), w in want.items():
             assert wait_for(lambda: _eq_norm(_used(store, ns, name)) == _eq_norm(w)), (_used(store, ns, name), w)
-        evs, _ = store.list("events", "")
-        assert any(e["reason"] == "Synced" for e in evs)
+        # The Synced event is recorded after the status patch lands.
+        assert wait_for(lambda: any(e["reason"] == "Synced" for e in store.list("events", "")[0]))
     finally:
         ctrl.stop()
         ctrl.factory.stop()
