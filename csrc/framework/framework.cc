@@ -311,7 +311,12 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
   total.assign(n, NodeScore{});
   for (size_t i = 0; i < n; ++i) total[i].name = nodes[i]->name();
   if (scorers_.empty()) return {};
-  std::vector<std::vector<NodeScore>> per(scorers_.size(), std::vector<NodeScore>(n));
+  // Per-plugin score rows are reused across cycles (no allocation or string
+  // construction per plugin x node in steady state); every cell is written
+  // below before it is read.
+  thread_local std::vector<std::vector<NodeScore>> per;
+  if (per.size() < scorers_.size()) per.resize(scorers_.size());
+  for (size_t k = 0; k < scorers_.size(); ++k) per[k].resize(n);
   std::atomic<bool> failed{false};
   std::string err;
   std::mutex err_mu;
