@@ -232,6 +232,9 @@ struct QueuedPodInfo {
   // QueueSort plugins may memoize an immutable sort key here (e.g.
   // Coscheduling's PodGroup creation time); INT64_MIN = not cached.
   mutable int64_t sort_key_cache = INT64_MIN;
+  // Position in the PodHeap currently holding this entry (a QueuedPodInfo
+  // sits in at most one heap at a time); lets sift-up/down skip uid hashing.
+  size_t heap_index = 0;
 };
 using QueuedPodInfoPtr = std::shared_ptr<QueuedPodInfo>;
 

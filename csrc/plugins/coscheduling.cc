@@ -95,8 +95,23 @@ class Coscheduling : public Plugin {
   bool less(const QueuedPodInfo& a, const QueuedPodInfo& b) const override {
     if (a.pod->priority != b.pod->priority) return a.pod->priority > b.pod->priority;
     MicroTime ta = creation(a), tb = creation(b);
-    if (ta == tb) return a.pod->key() < b.pod->key();
+    if (ta == tb) return key_less(*a.pod, *b.pod);
     return ta < tb;
+  }
+  // "ns/name" < "ns/name" without building the strings (gang members tie on
+  // the group timestamp, so this runs on most heap comparisons).
+  static bool key_less(const Pod& a, const Pod& b) {
+    if (a.ns() == b.ns()) return a.name() < b.name();
+    auto at = [](const Pod& p, size_t i) -> unsigned char {
+      size_t n = p.ns().size();
+      return static_cast<unsigned char>(i < n ? p.ns()[i] : i == n ? '/' : p.name()[i - n - 1]);
+    };
+    size_t la = a.ns().size() + 1 + a.name().size(), lb = b.ns().size() + 1 + b.name().size();
+    for (size_t i = 0, m = std::min(la, lb); i < m; ++i) {
+      unsigned char ca = at(a, i), cb = at(b, i);
+      if (ca != cb) return ca < cb;
+    }
+    return la < lb;
   }
 
   // ---- PreFilter (core.go:149-196) ----

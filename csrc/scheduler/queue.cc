@@ -8,8 +8,8 @@ namespace xsched {
 // ---------------------------------------------------------------- PodHeap ----
 void PodHeap::swap_at(size_t a, size_t b) {
   std::swap(v_[a], v_[b]);
-  pos_[v_[a]->pod->uid()] = a;
-  pos_[v_[b]->pod->uid()] = b;
+  v_[a]->heap_index = a;
+  v_[b]->heap_index = b;
 }
 
 void PodHeap::up(size_t i) {
@@ -36,14 +36,17 @@ void PodHeap::down(size_t i) {
 void PodHeap::push(const QueuedPodInfoPtr& p) {
   auto it = pos_.find(p->pod->uid());
   if (it != pos_.end()) {
-    size_t i = it->second;
+    size_t i = it->second->heap_index;
     v_[i] = p;
+    p->heap_index = i;
+    it->second = p.get();
     up(i);
-    down(pos_[p->pod->uid()]);
+    down(p->heap_index);
     return;
   }
   v_.push_back(p);
-  pos_[p->pod->uid()] = v_.size() - 1;
+  p->heap_index = v_.size() - 1;
+  pos_.emplace(p->pod->uid(), p.get());
   up(v_.size() - 1);
 }
 
@@ -59,17 +62,17 @@ QueuedPodInfoPtr PodHeap::pop() {
 
 QueuedPodInfoPtr PodHeap::get(const std::string& uid) const {
   auto it = pos_.find(uid);
-  return it == pos_.end() ? nullptr : v_[it->second];
+  return it == pos_.end() ? nullptr : v_[it->second->heap_index];
 }
 
 bool PodHeap::erase(const std::string& uid) {
   auto it = pos_.find(uid);
   if (it == pos_.end()) return false;
-  size_t i = it->second;
+  size_t i = it->second->heap_index;
   size_t last = v_.size() - 1;
   if (i != last) swap_at(i, last);
   v_.pop_back();
-  pos_.erase(uid);
+  pos_.erase(it);
   if (i < v_.size()) {
     up(i);
     down(i);

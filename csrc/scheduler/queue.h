@@ -45,7 +45,7 @@ class PodHeap {
   void swap_at(size_t a, size_t b);
   Less less_;
   std::vector<QueuedPodInfoPtr> v_;
-  std::unordered_map<std::string, size_t> pos_;
+  std::unordered_map<std::string, QueuedPodInfo*> pos_;  // uid -> entry (index lives in the entry)
 };
 
 // Pods nominated onto nodes by preemption (PodNominator).
