@@ -56,7 +56,10 @@ int main(int argc, char** argv) {
     size_t n = pods.size();
     auto t0 = std::chrono::steady_clock::now();
     store->create_many("podgroups", std::move(pgs));
-    store->create_many("pods", std::move(pods));
+    // PodGroup-aligned chunks, as the Python bulk-create path commits them.
+    store->create_chunked("pods", [&](const std::function<void(Json&&)>& emit) {
+      for (auto& p : pods) emit(std::move(p));
+    });
     auto deadline = t0 + std::chrono::seconds(60);
     while (sched.stats().bound < bound + n) {
       if (std::chrono::steady_clock::now() > deadline) {
