@@ -1025,6 +1025,23 @@ double Scheduler::score_benchmark(const Json& pod_obj, int iterations, Json* out
   return us;
 }
 
+Scheduler::BindMetrics& Scheduler::bind_metrics() {
+  BindMetrics& m = bind_metrics_;
+  uint64_t e = metrics_->epoch();
+  if (m.epoch.load(std::memory_order_acquire) == e) return m;
+  std::lock_guard<std::mutex> g(bind_metrics_mu_);
+  if (m.epoch.load(std::memory_order_acquire) == e) return m;
+  m.binding.store(&metrics_->histogram("xsched_binding_duration_seconds", ""));
+  m.attempts.store(&metrics_->histogram("scheduler_pod_scheduling_attempts", ""));
+  m.permit_wait[0].store(&metrics_->histogram("scheduler_permit_wait_duration_seconds", "result=\"Success\""));
+  m.permit_wait[1].store(&metrics_->histogram("scheduler_permit_wait_duration_seconds", "result=\"Unschedulable\""));
+  for (int a = 1; a <= 8; ++a)
+    m.pod_duration[a - 1].store(
+        &metrics_->histogram("scheduler_pod_scheduling_duration_seconds", "attempts=\"" + std::to_string(a) + "\""));
+  m.epoch.store(e, std::memory_order_release);
+  return m;
+}
+
 void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
                               int64_t cycle, Status permit_status, int64_t wait_start_us,
                               std::shared_ptr<PodsToActivate> to_activate) {
@@ -1042,10 +1059,10 @@ void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr q
                    st.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{st.failed_plugin()});
     inflight_.fetch_sub(1);
   };
+  BindMetrics& bm = bind_metrics();
   if (wait_start_us > 0 && t0 - wait_start_us > 0) {
-    metrics_->histogram("scheduler_permit_wait_duration_seconds",
-                        std::string("result=\"") + (permit_status.is_success() ? "Success" : "Unschedulable") + "\"")
-        .observe(static_cast<double>(t0 - wait_start_us) / 1e6);
+    bm.permit_wait[permit_status.is_success() ? 0 : 1].load(std::memory_order_relaxed)
+        ->observe(static_cast<double>(t0 - wait_start_us) / 1e6);
     if (tracer_.enabled())
       tracer_.record(TraceEvent{"permit_wait", assumed->key(), code_name(permit_status.code()), wait_start_us,
                                 t0 - wait_start_us, 1});
@@ -1067,12 +1084,15 @@ void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr q
   }
   cache_->finish_binding(*assumed);
   int64_t t1 = clock_->now_us();
-  metrics_->histogram("xsched_binding_duration_seconds", "").observe(static_cast<double>(t1 - t0) / 1e6);
+  bm.binding.load(std::memory_order_relaxed)->observe(static_cast<double>(t1 - t0) / 1e6);
   metrics_->histogram("scheduler_e2e_scheduling_duration_seconds", "profile=\"" + fw->profile_name() + "\"")
       .observe(static_cast<double>(t1 - qpi->timestamp_us) / 1e6);
-  metrics_->histogram("scheduler_pod_scheduling_duration_seconds", "attempts=\"" + std::to_string(qpi->attempts) + "\"")
-      .observe(static_cast<double>(t1 - qpi->initial_attempt_us) / 1e6);
-  metrics_->histogram("scheduler_pod_scheduling_attempts", "").observe(qpi->attempts);
+  Histogram* pd = qpi->attempts >= 1 && qpi->attempts <= 8
+                      ? bm.pod_duration[qpi->attempts - 1].load(std::memory_order_relaxed)
+                      : &metrics_->histogram("scheduler_pod_scheduling_duration_seconds",
+                                             "attempts=\"" + std::to_string(qpi->attempts) + "\"");
+  pd->observe(static_cast<double>(t1 - qpi->initial_attempt_us) / 1e6);
+  bm.attempts.load(std::memory_order_relaxed)->observe(qpi->attempts);
   if (tracer_.enabled()) tracer_.record(TraceEvent{"bind", assumed->key(), host, t0, t1 - t0, 1});
   fw->run_post_bind(*s, assumed, host);
   {

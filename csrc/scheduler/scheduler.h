@@ -172,6 +172,19 @@ class Scheduler {
   };
   std::unordered_map<const Framework*, CycleMetrics> cycle_metrics_;
   CycleMetrics& cycle_metrics(const Framework& fw);
+  // Binding-cycle histograms shared by the binder threads: looked up once
+  // per metrics epoch (under bind_metrics_mu_), then read lock-free. Cells
+  // are never freed (Metrics::reset retires them), so a stale pointer read
+  // across a reset only loses that observation.
+  struct BindMetrics {
+    std::atomic<uint64_t> epoch{~0ULL};
+    std::atomic<Histogram*> binding{nullptr}, attempts{nullptr};
+    std::atomic<Histogram*> permit_wait[2] = {nullptr, nullptr};  // Success, Unschedulable
+    std::atomic<Histogram*> pod_duration[8] = {};                  // attempts=1..8
+  };
+  BindMetrics bind_metrics_;
+  std::mutex bind_metrics_mu_;
+  BindMetrics& bind_metrics();
 
   void informer_loop();
   void handle_event(const WatchEvent& ev);
