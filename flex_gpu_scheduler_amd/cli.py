@@ -41,36 +41,32 @@ def _setup_logging(v: int) -> None:
 
 def master_from_kubeconfig(path: str) -> tuple[str, str | None]:
     """(server URL, bearer token) of the current context of a kubeconfig."""
-    import yaml
+    from .control.client import kubeconfig_connection
 
-    with open(path) as f:
-        kc = yaml.safe_load(f) or {}
-    ctx_name = kc.get("current-context")
-    ctxs = {c["name"]: c.get("context") or {} for c in kc.get("contexts") or []}
-    ctx = ctxs.get(ctx_name) or (next(iter(ctxs.values())) if ctxs else {})
-    clusters = {c["name"]: c.get("cluster") or {} for c in kc.get("clusters") or []}
-    users = {u["name"]: u.get("user") or {} for u in kc.get("users") or []}
-    cluster = clusters.get(ctx.get("cluster")) or (next(iter(clusters.values())) if clusters else {})
-    user = users.get(ctx.get("user")) or (next(iter(users.values())) if users else {})
-    return cluster.get("server", "http://127.0.0.1:6443"), user.get("token")
+    server, token, _ = kubeconfig_connection(path)
+    return server, token
 
 
 def _client(args):
-    from .control.client import RestClient
+    from .control.client import IN_CLUSTER_SA, RestClient, TLSConfig, kubeconfig_connection
 
     master = getattr(args, "master", None) or getattr(args, "masterUrl", None)
     token = getattr(args, "token", None)
+    tls = TLSConfig(insecure=bool(getattr(args, "insecure_skip_tls_verify", False)))
     kc = getattr(args, "kubeconfig", None) or getattr(args, "kubeConfig", None)
     if kc and not master:
-        master, kt = master_from_kubeconfig(kc)
+        master, kt, tls = kubeconfig_connection(kc)
         token = token or kt
     if getattr(args, "incluster", False) and not master:
+        # rest.InClusterConfig: service host/port, the service-account token and CA.
         host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT", "443")
         master = f"https://{host}:{port}"
-        tok = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+        tok, ca = os.path.join(IN_CLUSTER_SA, "token"), os.path.join(IN_CLUSTER_SA, "ca.crt")
         if os.path.exists(tok):
             token = Path(tok).read_text().strip()
-    return RestClient(master or "http://127.0.0.1:6443", token=token)
+        if os.path.exists(ca):
+            tls = TLSConfig(ca_file=ca)
+    return RestClient(master or "http://127.0.0.1:6443", token=token, tls=tls)
 
 
 def _wait_forever(stop: threading.Event) -> None:
@@ -383,6 +379,8 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--kubeconfig", help="kubeconfig path (server + token of the current context)")
         p.add_argument("--token", help="bearer token")
         p.add_argument("--incluster", action="store_true", help="use the in-cluster service account")
+        p.add_argument("--insecure-skip-tls-verify", action="store_true",
+                       help="do not verify the API server certificate (with --master)")
         if reference_flags:
             p.add_argument("--masterUrl", help="alias of --master (reference controller flag)")
             p.add_argument("--kubeConfig", help="alias of --kubeconfig (reference controller flag)")

@@ -9,11 +9,16 @@ separate processes talking to `ApiServer` over HTTP.
 """
 from __future__ import annotations
 
+import base64
 import http.client
 import json
+import os
 import queue
+import ssl
+import tempfile
 import threading
 import time
+from dataclasses import dataclass
 from typing import Any, Iterable
 from urllib.parse import urlencode, urlsplit
 
@@ -231,21 +236,97 @@ class _RestWatch(WatchStream):
             t.join(timeout=2)
 
 
+@dataclass
+class TLSConfig:
+    """TLS settings of a kube-apiserver connection (client-go rest.TLSClientConfig):
+    the cluster CA (file or PEM data), an optional client certificate/key (file
+    or PEM data) and insecure-skip-tls-verify."""
+    ca_file: str | None = None
+    ca_data: bytes | None = None
+    cert_file: str | None = None
+    key_file: str | None = None
+    cert_data: bytes | None = None
+    key_data: bytes | None = None
+    insecure: bool = False
+
+    def context(self) -> ssl.SSLContext:
+        ctx = ssl.create_default_context(cafile=self.ca_file,
+                                         cadata=self.ca_data.decode() if self.ca_data else None)
+        if self.insecure:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        if self.cert_file or self.cert_data:
+            if self.cert_data:
+                # load_cert_chain takes paths only: stage the PEMs in 0600 files.
+                with tempfile.TemporaryDirectory() as d:
+                    cf, kf = os.path.join(d, "tls.crt"), os.path.join(d, "tls.key")
+                    for path, data in ((cf, self.cert_data), (kf, self.key_data or self.cert_data)):
+                        fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o600)
+                        with os.fdopen(fd, "wb") as f:
+                            f.write(data)
+                    ctx.load_cert_chain(cf, kf)
+            else:
+                ctx.load_cert_chain(self.cert_file, self.key_file)
+        return ctx
+
+
+def kubeconfig_connection(path: str) -> tuple[str, str | None, TLSConfig]:
+    """(server URL, bearer token, TLS settings) of the current context of a
+    kubeconfig, following clientcmd: relative file paths resolve against the
+    kubeconfig's directory, `*-data` fields are base64 PEM, `tokenFile` is read."""
+    import yaml
+
+    with open(path) as f:
+        kc = yaml.safe_load(f) or {}
+    base = os.path.dirname(os.path.abspath(path))
+    ctx_name = kc.get("current-context")
+    ctxs = {c["name"]: c.get("context") or {} for c in kc.get("contexts") or []}
+    ctx = ctxs.get(ctx_name) or (next(iter(ctxs.values())) if ctxs else {})
+    clusters = {c["name"]: c.get("cluster") or {} for c in kc.get("clusters") or []}
+    users = {u["name"]: u.get("user") or {} for u in kc.get("users") or []}
+    cluster = clusters.get(ctx.get("cluster")) or (next(iter(clusters.values())) if clusters else {})
+    user = users.get(ctx.get("user")) or (next(iter(users.values())) if users else {})
+
+    def path_of(v):
+        return v if not v or os.path.isabs(v) else os.path.join(base, v)
+
+    def data_of(v):
+        return base64.b64decode(v) if v else None
+
+    tls = TLSConfig(ca_file=path_of(cluster.get("certificate-authority")),
+                    ca_data=data_of(cluster.get("certificate-authority-data")),
+                    cert_file=path_of(user.get("client-certificate")), key_file=path_of(user.get("client-key")),
+                    cert_data=data_of(user.get("client-certificate-data")),
+                    key_data=data_of(user.get("client-key-data")),
+                    insecure=bool(cluster.get("insecure-skip-tls-verify", False)))
+    token = user.get("token")
+    if not token and user.get("tokenFile"):
+        with open(path_of(user["tokenFile"])) as f:
+            token = f.read().strip()
+    return cluster.get("server", "http://127.0.0.1:6443"), token, tls
+
+
+IN_CLUSTER_SA = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
 class RestClient(Client):
     """Kubernetes-REST client over `http.client` (one keep-alive connection
     per thread). Talks to `ApiServer` or any kube-apiserver exposing the same
-    paths (bearer-token auth)."""
+    paths: bearer-token and/or client-certificate auth, TLS verified against
+    the cluster CA (`TLSConfig`)."""
 
-    def __init__(self, base_url: str, token: str | None = None, timeout: float = 30.0):
+    def __init__(self, base_url: str, token: str | None = None, timeout: float = 30.0, tls: TLSConfig | None = None):
         u = urlsplit(base_url)
         self.host, self.port = u.hostname or "127.0.0.1", u.port or (443 if u.scheme == "https" else 80)
         self.https = u.scheme == "https"
         self.token, self.timeout = token, timeout
+        self._ssl = (tls or TLSConfig()).context() if self.https else None
         self._tls = threading.local()
 
     def _new_conn(self) -> http.client.HTTPConnection:
-        cls = http.client.HTTPSConnection if self.https else http.client.HTTPConnection
-        return cls(self.host, self.port, timeout=None)
+        if self.https:
+            return http.client.HTTPSConnection(self.host, self.port, timeout=None, context=self._ssl)
+        return http.client.HTTPConnection(self.host, self.port, timeout=None)
 
     def _headers(self, ctype: str | None = None) -> dict:
         h = {"Accept": "application/json"}
