@@ -12,3 +12,13 @@ def test_tlp_score_pass_runs():
 def test_mi355x_score_pass_runs():
     r = score_bench.run(16, 3, mi355x=True)
     assert r["nodes"] == 16 and r["scorers"].startswith("FlexGPU")
+
+
+def test_timeline_reports_scheduling_thread_busy_span():
+    from flex_gpu_scheduler_amd.tools.timeline import timeline
+
+    t = timeline(nodes=8, warmup=1)
+    assert t["pods"] > 0
+    assert 0 < t["busy_fraction"] <= 1.0
+    assert t["sched_thread_busy_ms"] <= t["sched_thread_span_ms"] + 1e-6
+    assert t["first_cycle_ms"] <= t["last_cycle_end_ms"]
