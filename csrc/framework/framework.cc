@@ -314,7 +314,11 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
   // Per-plugin score rows are reused across cycles (no allocation or string
   // construction per plugin x node in steady state); every cell is written
   // below before it is read.
-  thread_local std::vector<std::vector<NodeScore>> per;
+  // The rows are thread_local to the calling (scheduling) thread; the
+  // node-parallel workers below must reach them through this reference, as
+  // naming a thread_local inside the lambda would resolve to the worker's own.
+  thread_local std::vector<std::vector<NodeScore>> per_rows;
+  std::vector<std::vector<NodeScore>>& per = per_rows;
   if (per.size() < scorers_.size()) per.resize(scorers_.size());
   for (size_t k = 0; k < scorers_.size(); ++k) per[k].resize(n);
   std::atomic<bool> failed{false};

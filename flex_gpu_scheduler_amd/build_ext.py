@@ -137,6 +137,22 @@ def build_tsan(verbose: bool = True) -> Path:
     return out
 
 
+def build_asan(verbose: bool = True) -> Path:
+    """Native stress driver built with -fsanitize=address,undefined (host only)."""
+    includes = [str(CSRC)]
+    flags = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
+    objs = build_objects(core_sources() + [CSRC / "tools" / "stress_main.cc"], BUILD / "asan", [*flags, "-g", "-O1"],
+                         includes)
+    out = BUILD / "xsched_stress_asan"
+    cmd = ["g++", *flags, "-pthread", *[str(o) for o in objs], "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"asan link failed:\n{r.stderr[-8000:]}")
+    if verbose:
+        print(f"[build_ext] built {out.relative_to(ROOT)}")
+    return out
+
+
 def build_prof(verbose: bool = True, gprof: bool = True) -> Path:
     """Native stress driver (no Python in the loop). With `gprof` it is built
     with -pg for a per-function CPU profile of the scheduling hot path;
@@ -179,6 +195,7 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--core", action="store_true")
     ap.add_argument("--hip", action="store_true")
     ap.add_argument("--tsan", action="store_true")
+    ap.add_argument("--asan", action="store_true")
     ap.add_argument("--prof", action="store_true")
     ap.add_argument("--stress", action="store_true")
     ap.add_argument("--tests", action="store_true")
@@ -189,13 +206,15 @@ def main(argv: list[str] | None = None) -> int:
     if a.prof or a.stress:
         build_prof(gprof=a.prof)
         return 0
-    everything = not (a.core or a.hip or a.tsan)
+    everything = not (a.core or a.hip or a.tsan or a.asan)
     if a.core or everything:
         build_core()
     if a.hip or everything:
         build_hip()
     if a.tsan:
         build_tsan()
+    if a.asan:
+        build_asan()
     return 0
 
 

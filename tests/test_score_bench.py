@@ -22,3 +22,18 @@ def test_timeline_reports_scheduling_thread_busy_span():
     assert 0 < t["busy_fraction"] <= 1.0
     assert t["sched_thread_busy_ms"] <= t["sched_thread_span_ms"] + 1e-6
     assert t["first_cycle_ms"] <= t["last_cycle_end_ms"]
+
+
+def test_parallel_filter_and_score_above_inline_threshold():
+    """>= 128 nodes runs Filter/Score on the parallelizer's workers
+    (parallelInlineBelow); a wave must bind completely there too."""
+    from flex_gpu_scheduler_amd.utils.benchrun import Shard
+    from flex_gpu_scheduler_amd.utils.workload import ClusterSpec
+
+    sh = Shard(ClusterSpec(nodes=160), seed=1)
+    try:
+        r = sh.run(sh.wave(0), timeout_s=60)
+        assert r.pods > 1500
+        assert sh.sched.stats()["bound"] == r.pods
+    finally:
+        sh.close()
