@@ -1,6 +1,7 @@
 #include "common/parallel.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 
 namespace xsched {
@@ -18,15 +19,31 @@ Parallelizer::~Parallelizer() {
   for (auto& t : threads_) t.join();
 }
 
-void Parallelizer::run_job(Job& job) {
+namespace {
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+void observe(ParallelSite* site, int64_t ns, int items) {
+  if (!site || items <= 0) return;
+  int64_t sample = ns * 16 / items;
+  int64_t cur = site->ns_per_item_x16.load(std::memory_order_relaxed);
+  // EMA with alpha 1/8; the first sample seeds it.
+  site->ns_per_item_x16.store(cur == 0 ? sample : cur + (sample - cur) / 8, std::memory_order_relaxed);
+}
+}  // namespace
+
+int Parallelizer::run_job(Job& job) {
+  int done = 0;
   for (;;) {
-    if (job.stop && job.stop->load(std::memory_order_relaxed)) return;
+    if (job.stop && job.stop->load(std::memory_order_relaxed)) return done;
     int start = job.next.fetch_add(job.chunk, std::memory_order_relaxed);
-    if (start >= job.n) return;
+    if (start >= job.n) return done;
     int end = std::min(job.n, start + job.chunk);
     for (int i = start; i < end; ++i) {
-      if (job.stop && job.stop->load(std::memory_order_relaxed)) return;
+      if (job.stop && job.stop->load(std::memory_order_relaxed)) return done;
       (*job.fn)(i);
+      ++done;
     }
   }
 }
@@ -52,17 +69,23 @@ void Parallelizer::worker_loop() {
   }
 }
 
-void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop) {
+void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop,
+                         ParallelSite* site) {
   if (n <= 0) return;
   // Helpers only pay off when each gets >= inline_below_/2 items: a fork/join
   // round costs a few microseconds of wake-ups, more than filtering dozens of
   // nodes with the allocation-free plugins.
   int helpers = std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1);
-  if (n < inline_below_ || helpers <= 0) {
+  const bool cheap = site && site->ns_per_item_x16.load(std::memory_order_relaxed) / 16 * n < kMinParallelWorkNs;
+  if (n < inline_below_ || helpers <= 0 || cheap) {
+    int64_t t0 = site ? now_ns() : 0;
+    int done = 0;
     for (int i = 0; i < n; ++i) {
-      if (stop && stop->load(std::memory_order_relaxed)) return;
+      if (stop && stop->load(std::memory_order_relaxed)) break;
       fn(i);
+      ++done;
     }
+    if (site) observe(site, now_ns() - t0, done);
     return;
   }
   std::lock_guard<std::mutex> call(call_mu_);
@@ -83,7 +106,9 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
     cv_.notify_all();
   else
     for (int i = 0; i < helpers; ++i) cv_.notify_one();
-  run_job(job);
+  int64_t t0 = site ? now_ns() : 0;
+  int mine = run_job(job);
+  if (site) observe(site, now_ns() - t0, mine);
   std::unique_lock<std::mutex> lk(mu_);
   job_ = nullptr;  // no new worker can join after this point
   job.active.fetch_sub(1);

@@ -18,6 +18,17 @@
 
 namespace xsched {
 
+// Cost model of one call site (Filter, Score): an exponential moving average
+// of the per-item time measured on the calling thread. Above `inline_below`
+// items the site still runs inline while the estimated serial time is under
+// Parallelizer::kMinParallelWorkNs: a fork/join round (waking helpers and
+// joining them) costs ~15-25 us on the MI355X hosts, more than filtering a
+// thousand nodes whose verdicts come from the equivalence cache
+// (profiles/r1h_inline_ab.txt).
+struct ParallelSite {
+  std::atomic<int64_t> ns_per_item_x16{0};  // fixed point, 1/16 ns
+};
+
 class Parallelizer {
  public:
   explicit Parallelizer(int workers = 16, int inline_below = 128);
@@ -27,8 +38,10 @@ class Parallelizer {
 
   // Runs fn(i) for i in [0, n). `stop` (optional) is polled between items to
   // allow early exit (e.g. enough feasible nodes found).
-  void until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop = nullptr);
+  void until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop = nullptr,
+             ParallelSite* site = nullptr);
   int workers() const { return workers_; }
+  static constexpr int64_t kMinParallelWorkNs = 60'000;
 
  private:
   struct Job {
@@ -41,7 +54,7 @@ class Parallelizer {
     std::atomic<int> active{0};
   };
   void worker_loop();
-  void run_job(Job& job);
+  int run_job(Job& job);  // items processed by this thread
 
   int workers_;
   int inline_below_;

@@ -349,7 +349,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
       for (size_t k = 0; k < scorers_.size(); ++k) slot->raw[k] = per[k][i].score;
       slot->score_gen = nodes[i]->generation;
     }
-  }, &failed);
+  }, &failed, &score_site_);
   if (failed.load()) return Status(Code::Error, err);
   for (size_t k = 0; k < scorers_.size(); ++k) {
     auto& pl = scorers_[k].first;

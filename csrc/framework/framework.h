@@ -90,6 +90,7 @@ class Framework {
   static constexpr int64_t kMaxPermitTimeoutUs = 15LL * 60 * 1000000;  // framework.go:46
 
  private:
+  ParallelSite score_site_;  // inline-vs-parallel cost model of Score
   void record(const char* point, const Status& st, int64_t start_us, CycleState& s);
   ProfileConfig cfg_;
   Handle handle_;

@@ -698,7 +698,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       has_err = true;
       stop.store(true);
     }
-  }, &stop);
+  }, &stop, &filter_site_);
   if (eq_filter) {
     uint64_t h = hits.load();
     std::lock_guard<std::mutex> g(stats_mu_);

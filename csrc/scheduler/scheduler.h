@@ -162,6 +162,7 @@ class Scheduler {
   std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
   std::vector<const Status*> fail_ptr_;
   static constexpr size_t kInformerWindow = 64;
+  ParallelSite filter_site_;  // inline-vs-parallel cost model of Filter
   // Per-profile metric cells of the scheduling cycle, cached per metrics
   // epoch (scheduling thread / sched_mu_ only).
   struct CycleMetrics {
