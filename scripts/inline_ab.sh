@@ -12,7 +12,7 @@ from flex_gpu_scheduler_amd.utils.cpuaffinity import apply
 apply('l3')
 from flex_gpu_scheduler_amd.tools.phase_profile import profile
 r = profile($n, 2, warmup=1, options={'parallelInlineBelow': $inl})
-print(json.dumps({'nodes': $n, 'inline_below': $inl, 'pods_per_s': r['pods_per_s'], 'filter_us': r['phases_us_per_pod']['filter'], 'schedule_us': r['phases_us_per_pod']['schedule']}))" >>> "$OUT/inline_ab2.txt" || exit $?
+print(json.dumps({'nodes': $n, 'inline_below': $inl, 'pods_per_s': r['pods_per_s'], 'filter_us': r['phases_us_per_pod']['filter'], 'schedule_us': r['phases_us_per_pod']['schedule']}))" >> "$OUT/inline_ab2.txt" || exit $?
   done
 done
 cat "$OUT/inline_ab2.txt"
