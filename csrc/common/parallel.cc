@@ -24,12 +24,17 @@ int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
+void ema(std::atomic<int64_t>& v, int64_t sample, bool seed) {
+  int64_t cur = v.load(std::memory_order_relaxed);
+  v.store(seed ? sample : cur + (sample - cur) / 8, std::memory_order_relaxed);  // alpha 1/8
+}
 void observe(ParallelSite* site, int64_t ns, int items) {
   if (!site || items <= 0) return;
-  int64_t sample = ns * 16 / items;
-  int64_t cur = site->ns_per_item_x16.load(std::memory_order_relaxed);
-  // EMA with alpha 1/8; the first sample seeds it.
-  site->ns_per_item_x16.store(cur == 0 ? sample : cur + (sample - cur) / 8, std::memory_order_relaxed);
+  ema(site->ns_per_item_x16, ns * 16 / items, site->ns_per_item_x16.load(std::memory_order_relaxed) == 0);
+}
+void observe_done(ParallelSite* site, int done, int n) {
+  if (!site || n <= 0) return;
+  ema(site->done_frac_x1024, static_cast<int64_t>(done) * 1024 / n, false);
 }
 }  // namespace
 
@@ -76,7 +81,13 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
   // round costs a few microseconds of wake-ups, more than filtering dozens of
   // nodes with the allocation-free plugins.
   int helpers = std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1);
-  const bool cheap = site && site->ns_per_item_x16.load(std::memory_order_relaxed) / 16 * n < kMinParallelWorkNs;
+  bool cheap = false;
+  if (site) {
+    int64_t est = site->ns_per_item_x16.load(std::memory_order_relaxed) * n / 16 *
+                  site->done_frac_x1024.load(std::memory_order_relaxed) / 1024;
+    bool probe = site->calls.fetch_add(1, std::memory_order_relaxed) % ParallelSite::kProbeEvery == 0;
+    cheap = probe || est < kMinParallelWorkNs;
+  }
   if (n < inline_below_ || helpers <= 0 || cheap) {
     int64_t t0 = site ? now_ns() : 0;
     int done = 0;
@@ -85,7 +96,10 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
       fn(i);
       ++done;
     }
-    if (site) observe(site, now_ns() - t0, done);
+    if (site) {
+      observe(site, now_ns() - t0, done);
+      observe_done(site, done, n);
+    }
     return;
   }
   std::lock_guard<std::mutex> call(call_mu_);
@@ -106,13 +120,14 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
     cv_.notify_all();
   else
     for (int i = 0; i < helpers; ++i) cv_.notify_one();
-  int64_t t0 = site ? now_ns() : 0;
-  int mine = run_job(job);
-  if (site) observe(site, now_ns() - t0, mine);
+  // Per-item cost is learned from inline runs only (the periodic probes):
+  // the caller's items in a parallel run are inflated by contention.
+  run_job(job);
   std::unique_lock<std::mutex> lk(mu_);
   job_ = nullptr;  // no new worker can join after this point
   job.active.fetch_sub(1);
   done_cv_.wait(lk, [&] { return job.active.load() == 0; });
+  if (site) observe_done(site, std::min(job.n, job.next.load(std::memory_order_relaxed)), job.n);
 }
 
 }  // namespace xsched

@@ -27,6 +27,13 @@ namespace xsched {
 // (profiles/r1h_inline_ab.txt).
 struct ParallelSite {
   std::atomic<int64_t> ns_per_item_x16{0};  // fixed point, 1/16 ns
+  // Fraction of the n items a call actually runs before `stop` (Filter stops
+  // at numFeasibleNodesToFind), fixed point 1/1024.
+  std::atomic<int64_t> done_frac_x1024{1024};
+  // Every kProbeEvery-th call runs inline to re-measure the serial cost, so
+  // an estimate inflated by contention in parallel runs cannot lock it in.
+  std::atomic<uint32_t> calls{0};
+  static constexpr uint32_t kProbeEvery = 32;
 };
 
 class Parallelizer {
