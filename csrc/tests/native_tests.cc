@@ -2,12 +2,17 @@
 // the GPU ledger's incremental aggregates (checked against a brute-force
 // recomputation over random assignment sequences), the pod heap and
 // scheduling-queue backoff under a fake clock, the timer service, CycleState
-// memo invalidation and store watch replay/expiry.
+// memo invalidation, store watch replay/expiry, PodGroup-aligned chunked
+// creates and the parallelizer's inline-vs-parallel cost model.
 //
 // Built by `python -m flex_gpu_scheduler_amd.build_ext --tests` into
 // build/xsched_native_tests and run by tests/test_native_unit.py.
 #include <cstdio>
+#include <chrono>
 #include <functional>
+#include <mutex>
+#include <set>
+#include <thread>
 #include <random>
 #include <string>
 #include <vector>
@@ -15,6 +20,7 @@
 #include "api/types.h"
 #include "common/clock.h"
 #include "common/json.h"
+#include "common/parallel.h"
 #include "common/quantity.h"
 #include "framework/types.h"
 #include "scheduler/queue.h"
@@ -354,6 +360,34 @@ TEST(store_create_chunked_keeps_gangs_whole) {
     bad_array = true;
   }
   CHECK(bad_array);
+}
+
+TEST(parallelizer_cost_model_inline_vs_parallel) {
+  // Cheap items above inline_below stay on the caller once measured; items
+  // whose serial work is far above kMinParallelWorkNs fan out to helpers.
+  Parallelizer par(8, 16);
+  ParallelSite cheap_site, heavy_site;
+  auto threads_used = [&](int n, ParallelSite* site, bool heavy) {
+    std::mutex mu;
+    std::set<std::thread::id> ids;
+    par.until(n, [&](int) {
+      if (heavy) {
+        auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(2);
+        while (std::chrono::steady_clock::now() < end) {
+        }
+      }
+      std::lock_guard<std::mutex> g(mu);
+      ids.insert(std::this_thread::get_id());
+    }, nullptr, site);
+    return ids.size();
+  };
+  for (int i = 0; i < 3; ++i) threads_used(512, &cheap_site, false);
+  CHECK_EQ(threads_used(512, &cheap_site, false), 1u);
+  threads_used(512, &heavy_site, true);  // first call is an inline probe
+  size_t most = 0;
+  for (int i = 0; i < 4; ++i) most = std::max(most, threads_used(512, &heavy_site, true));
+  CHECK(most > 1);  // 512 x 2 us = 1 ms of serial work
+  CHECK(heavy_site.ns_per_item_x16.load() / 16 >= 1000);
 }
 
 }  // namespace
