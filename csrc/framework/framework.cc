@@ -321,6 +321,14 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
   std::vector<std::vector<NodeScore>>& per = per_rows;
   if (per.size() < scorers_.size()) per.resize(scorers_.size());
   for (size_t k = 0; k < scorers_.size(); ++k) per[k].resize(n);
+  // Plugins whose raw score is 0 on every node for this pod are skipped
+  // (Plugin::score_all_zero); their rows are zero-filled so equivalence-cache
+  // slots stay exact.
+  thread_local std::vector<char> skip_rows;
+  std::vector<char>& skip = skip_rows;
+  skip.assign(scorers_.size(), 0);
+  if (!breakdown && handle_.snapshot)
+    for (size_t k = 0; k < scorers_.size(); ++k) skip[k] = scorers_[k].first->score_all_zero(p, *handle_.snapshot);
   std::atomic<bool> failed{false};
   std::string err;
   std::mutex err_mu;
@@ -331,6 +339,10 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
     EqSlot* slot = eq ? eq->slots[i] : nullptr;
     const bool hit = slot && slot->score_gen == nodes[i]->generation && slot->raw.size() == scorers_.size();
     for (size_t k = 0; k < scorers_.size(); ++k) {
+      if (skip[k]) {
+        per[k][i].score = 0;
+        continue;
+      }
       if (hit && eq->local[k]) {
         per[k][i].score = slot->raw[k];
         continue;
@@ -352,6 +364,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
   }, &failed, &score_site_);
   if (failed.load()) return Status(Code::Error, err);
   for (size_t k = 0; k < scorers_.size(); ++k) {
+    if (skip[k]) continue;
     auto& pl = scorers_[k].first;
     if (pl->has_normalize_score()) {
       Status st = pl->normalize_score(s, p, per[k]);

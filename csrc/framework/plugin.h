@@ -120,6 +120,12 @@ class Plugin {
   // cluster-wide, time-varying or cross-pod state for this pod return false.
   virtual bool filter_node_local(const Pod& p, const Snapshot& s) const { return false; }
   virtual bool score_node_local(const Pod& p, const Snapshot& s) const { return false; }
+  // True when this plugin's raw Score is 0 on every node for this pod (e.g.
+  // NodeAffinity without preferred terms). The framework then skips the
+  // plugin's Score and NormalizeScore for the cycle: its normalized output is
+  // the same on every node, so node ranking and selectHost are unchanged.
+  // Not applied when a per-plugin breakdown is requested (explain).
+  virtual bool score_all_zero(const Pod& p, const Snapshot& s) const { return false; }
   // EnqueueExtensions
   virtual std::vector<ClusterEvent> events_to_register() const { return {}; }
   // Informer hooks (plugins that maintain their own state from watch events,

@@ -270,6 +270,7 @@ class NodeAffinity : public Plugin {
  public:
   bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
   bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
+  bool score_all_zero(const Pod& p, const Snapshot&) const override { return p.preferred_node_terms.empty(); }
   explicit NodeAffinity(const Json& args) : Plugin("NodeAffinity", kPreFilter | kFilter | kPreScore | kScore) {
     if (const Json* aa = args.get("addedAffinity")) {
       if (const Json* req = aa->path({"requiredDuringSchedulingIgnoredDuringExecution", "nodeSelectorTerms"})) {

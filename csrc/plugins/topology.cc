@@ -99,6 +99,11 @@ class PodTopologySpread : public Plugin {
   // Without constraints the pod's Filter/Score ignore other pods entirely.
   bool filter_node_local(const Pod& p, const Snapshot&) const override { return p.spread_constraints.empty(); }
   bool score_node_local(const Pod& p, const Snapshot&) const override { return p.spread_constraints.empty(); }
+  bool score_all_zero(const Pod& p, const Snapshot&) const override {
+    for (const auto& c : p.spread_constraints)
+      if (!c.hard) return false;
+    return true;
+  }
   explicit PodTopologySpread(Handle& h)
       : Plugin("PodTopologySpread", kPreFilter | kFilter | kPreScore | kScore), h_(h) {}
 
@@ -297,6 +302,7 @@ class InterPodAffinity : public Plugin {
   }
   bool filter_node_local(const Pod& p, const Snapshot& s) const override { return no_terms(p, s); }
   bool score_node_local(const Pod& p, const Snapshot& s) const override { return no_terms(p, s); }
+  bool score_all_zero(const Pod& p, const Snapshot& s) const override { return no_terms(p, s); }
   InterPodAffinity(const Json& args, Handle& h)
       : Plugin("InterPodAffinity", kPreFilter | kFilter | kPreScore | kScore), h_(h) {
     hard_weight_ = static_cast<int32_t>(args["hardPodAffinityWeight"].as_int(1));
