@@ -230,6 +230,9 @@ class TaintToleration : public Plugin {
   bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
   bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   TaintToleration() : Plugin("TaintToleration", kFilter | kPreScore | kScore) {}
+  // Raw score counts untolerated PreferNoSchedule taints: with none in the
+  // cluster it is 0 everywhere and the reversed normalization is flat.
+  bool score_all_zero(const Pod&, const Snapshot& s) const override { return s.nodes_with_prefer_no_schedule == 0; }
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     if (!ni.node) return Status::error("invalid nodeInfo");
     for (const auto& t : ni.node->taints) {

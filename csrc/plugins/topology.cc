@@ -526,6 +526,16 @@ class ImageLocality : public Plugin {
     return has_tag ? image : image + ":latest";
   }
 
+  // No container image present on any node: sum is 0 on every node, which
+  // clamps to kMinThreshold and scores 0.
+  bool score_all_zero(const Pod& p, const Snapshot&) const override {
+    if (kMaxContainerThreshold * static_cast<int64_t>(p.containers.size()) <= kMinThreshold) return true;
+    std::shared_lock<std::shared_mutex> g(mu_);
+    for (const auto& c : p.containers)
+      if (image_nodes_.count(normalized(c.image))) return false;
+    return true;
+  }
+
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
     int64_t total_nodes = h_.snapshot ? static_cast<int64_t>(h_.snapshot->nodes.size()) : 1;
     int64_t sum = 0;

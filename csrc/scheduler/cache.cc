@@ -274,6 +274,18 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us) {
     }
   }
   s.generation = generation_;
+  if (s.node_epoch != node_epoch_) {
+    int64_t prefer = 0;
+    for (const auto& ni : s.nodes) {
+      if (!ni->node) continue;
+      for (const auto& t : ni->node->taints)
+        if (t.effect == "PreferNoSchedule") {
+          ++prefer;
+          break;
+        }
+    }
+    s.nodes_with_prefer_no_schedule = prefer;
+  }
   s.node_epoch = node_epoch_;
   return clones;
 }
