@@ -467,11 +467,13 @@ std::shared_ptr<Node> Node::from_json(const Json& obj) {
   n->unschedulable = spec["unschedulable"].as_bool(false);
   for (const auto& t : spec["taints"].items()) {
     n->taints.push_back(Taint{t["key"].as_string(), t["value"].as_string(), t["effect"].as_string()});
+    if (n->taints.back().effect == "PreferNoSchedule") n->has_prefer_no_schedule = true;
   }
   for (const auto& im : status["images"].items()) {
     ContainerImage ci;
     for (const auto& nm : im["names"].items()) ci.names.push_back(nm.as_string());
     ci.size_bytes = im["sizeBytes"].as_int(0);
+    for (const auto& nm : ci.names) n->image_sizes.emplace(nm, ci.size_bytes);
     n->images.push_back(std::move(ci));
   }
   const GpuNames& gn = gpu_names();

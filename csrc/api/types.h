@@ -194,6 +194,11 @@ struct Node {
   bool unschedulable = false;
   std::vector<Taint> taints;
   std::vector<ContainerImage> images;  // status.images (ImageLocality)
+  // Derived at parse time: every image name on the node -> size (first entry
+  // wins, as upstream NodeInfo.ImageStates), and whether any taint is
+  // PreferNoSchedule. The cache keeps cluster-wide counts of both.
+  std::unordered_map<std::string, int64_t> image_sizes;
+  bool has_prefer_no_schedule = false;
   // MI355X GPU topology as published by the node agent (see flexgpu.cc).
   int gpu_count = 0;
   std::vector<int> gpu_partitions;  // partitions per physical GPU (1 = SPX .. 8 = CPX)

@@ -364,9 +364,15 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
   }, &failed, &score_site_);
   if (failed.load()) return Status(Code::Error, err);
   for (size_t k = 0; k < scorers_.size(); ++k) {
-    if (skip[k]) continue;
+    if (skip[k]) {
+      if (int64_t c = scorers_[k].first->score_skip_value() * scorers_[k].second)
+        for (size_t i = 0; i < n; ++i) total[i].score += c;
+      continue;
+    }
     auto& pl = scorers_[k].first;
     if (pl->has_normalize_score()) {
+      if (pl->normalize_uses_names())
+        for (size_t i = 0; i < n; ++i) per[k][i].name = total[i].name;
       Status st = pl->normalize_score(s, p, per[k]);
       if (!st.is_success()) return Status(Code::Error, "running Normalize on Score plugin " + pl->name() + ": " + st.message());
     }

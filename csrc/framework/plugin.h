@@ -126,6 +126,15 @@ class Plugin {
   // the same on every node, so node ranking and selectHost are unchanged.
   // Not applied when a per-plugin breakdown is requested (explain).
   virtual bool score_all_zero(const Pod& p, const Snapshot& s) const { return false; }
+  // The normalized score every node gets when the raw scores are all 0: 0 for
+  // min-max/plain normalizers, kMaxNodeScore for reversed ones
+  // (TaintToleration's DefaultNormalizeScore(reverse), PodTopologySpread). A
+  // skipped plugin still adds this x weight to every total, so hot-path
+  // totals equal explain() totals.
+  virtual int64_t score_skip_value() const { return 0; }
+  // NormalizeScore reads NodeScore::name (not just scores). The framework's
+  // reused score rows carry names only for plugins that ask for them.
+  virtual bool normalize_uses_names() const { return false; }
   // EnqueueExtensions
   virtual std::vector<ClusterEvent> events_to_register() const { return {}; }
   // Informer hooks (plugins that maintain their own state from watch events,

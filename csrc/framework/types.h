@@ -211,9 +211,14 @@ struct Snapshot {
   std::vector<NodeInfoPtr> have_pods_with_required_anti_affinity;
   int64_t generation = 0;
   uint64_t node_epoch = 0;  // bumped on any Node object / node-set change (not on pod changes)
-  // Nodes carrying at least one PreferNoSchedule taint; recounted when
-  // node_epoch moves. Zero lets TaintToleration skip its Score pass.
+  // Nodes carrying at least one PreferNoSchedule taint, kept by the cache as
+  // Nodes change. Zero lets TaintToleration skip its Score pass.
   int64_t nodes_with_prefer_no_schedule = 0;
+  // Image name -> number of nodes listing it (upstream ImageStateSummary.
+  // NumNodes), published with the same refresh as `nodes`, so ImageLocality's
+  // score and its all-zero skip read one consistent view. Never null.
+  std::shared_ptr<const std::unordered_map<std::string, int64_t>> image_spread =
+      std::make_shared<const std::unordered_map<std::string, int64_t>>();
   // Versions replaced by the last refreshes. Dropping one can free deleted
   // pods, so the scheduler releases them off the scheduling thread.
   std::vector<NodeInfoPtr> retired;

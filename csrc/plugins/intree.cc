@@ -233,6 +233,7 @@ class TaintToleration : public Plugin {
   // Raw score counts untolerated PreferNoSchedule taints: with none in the
   // cluster it is 0 everywhere and the reversed normalization is flat.
   bool score_all_zero(const Pod&, const Snapshot& s) const override { return s.nodes_with_prefer_no_schedule == 0; }
+  int64_t score_skip_value() const override { return kMaxNodeScore; }  // reversed normalize of all-zero
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     if (!ni.node) return Status::error("invalid nodeInfo");
     for (const auto& t : ni.node->taints) {

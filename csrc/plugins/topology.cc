@@ -104,6 +104,9 @@ class PodTopologySpread : public Plugin {
       if (!c.hard) return false;
     return true;
   }
+  // NormalizeScore with no soft constraints: no ignored nodes and max 0, so
+  // every node gets kMaxNodeScore.
+  int64_t score_skip_value() const override { return kMaxNodeScore; }
   explicit PodTopologySpread(Handle& h)
       : Plugin("PodTopologySpread", kPreFilter | kFilter | kPreScore | kScore), h_(h) {}
 
@@ -239,6 +242,7 @@ class PodTopologySpread : public Plugin {
     return {static_cast<int64_t>(score), {}};
   }
   bool has_normalize_score() const override { return true; }
+  bool normalize_uses_names() const override { return true; }  // ignored nodes are keyed by name
   Status normalize_score(CycleState& s, const Pod&, std::vector<NodeScore>& scores) override {
     auto* st = s.read_as<SpreadScoreState>(kScoreKey);
     if (!st) return Status::error("PodTopologySpread: no PreScore state");
@@ -501,25 +505,6 @@ class ImageLocality : public Plugin {
   static constexpr int64_t kMinThreshold = 23 * kMB;
   static constexpr int64_t kMaxContainerThreshold = 1000 * kMB;
 
-  std::vector<std::string> watched_kinds() const override { return {"nodes"}; }
-  void on_object_event(const std::string&, int type, const JsonPtr& obj, const JsonPtr&) override {
-    auto n = Node::from_json(*obj);
-    std::unique_lock<std::shared_mutex> g(mu_);
-    auto old = node_images_.find(n->name());
-    if (old != node_images_.end()) {
-      for (const auto& [img, _] : old->second) {
-        auto it = image_nodes_.find(img);
-        if (it != image_nodes_.end() && --it->second == 0) image_nodes_.erase(it);
-      }
-      node_images_.erase(old);
-    }
-    if (static_cast<EventType>(type) == EventType::Deleted) return;
-    auto& mine = node_images_[n->name()];
-    for (const auto& im : n->images)
-      for (const auto& name : im.names)
-        if (mine.emplace(name, im.size_bytes).second) ++image_nodes_[name];
-  }
-
   static std::string normalized(const std::string& image) {
     size_t colon = image.rfind(':'), slash = image.rfind('/');
     bool has_tag = colon != std::string::npos && (slash == std::string::npos || colon > slash);
@@ -527,31 +512,33 @@ class ImageLocality : public Plugin {
   }
 
   // No container image present on any node: sum is 0 on every node, which
-  // clamps to kMinThreshold and scores 0.
-  bool score_all_zero(const Pod& p, const Snapshot&) const override {
+  // clamps to kMinThreshold and scores 0. Reads the Snapshot's image spread,
+  // the same view score() uses, so the skip and the score cannot disagree.
+  bool score_all_zero(const Pod& p, const Snapshot& s) const override {
     if (kMaxContainerThreshold * static_cast<int64_t>(p.containers.size()) <= kMinThreshold) return true;
-    std::shared_lock<std::shared_mutex> g(mu_);
+    if (s.image_spread->empty()) return true;
     for (const auto& c : p.containers)
-      if (image_nodes_.count(normalized(c.image))) return false;
+      if (s.image_spread->count(normalized(c.image))) return false;
     return true;
   }
 
+  // Upstream ImageLocality (vendor/.../plugins/imagelocality/image_locality.go):
+  // Σ size·(numNodes/totalNodes) over the pod's images present on the node,
+  // clamped to [23 MB, 1000 MB·containers] and scaled to [0, 100]. Node image
+  // sizes come from the immutable Node object and spreads from the Snapshot.
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
-    int64_t total_nodes = h_.snapshot ? static_cast<int64_t>(h_.snapshot->nodes.size()) : 1;
+    const Snapshot* snap = h_.snapshot;
+    int64_t total_nodes = snap ? static_cast<int64_t>(snap->nodes.size()) : 1;
     int64_t sum = 0;
-    {
-      std::shared_lock<std::shared_mutex> g(mu_);
-      auto nit = node_images_.find(ni.name());
-      if (nit != node_images_.end() && total_nodes > 0)
-        for (const auto& c : p.containers) {
-          auto it = nit->second.find(normalized(c.image));
-          if (it == nit->second.end()) continue;
-          auto cnt = image_nodes_.find(it->first);
-          int64_t spread = cnt == image_nodes_.end() ? 0 : cnt->second;
-          sum += static_cast<int64_t>(static_cast<double>(it->second) * static_cast<double>(spread) /
-                                      static_cast<double>(total_nodes));
-        }
-    }
+    if (ni.node && snap && total_nodes > 0 && !ni.node->image_sizes.empty())
+      for (const auto& c : p.containers) {
+        auto it = ni.node->image_sizes.find(normalized(c.image));
+        if (it == ni.node->image_sizes.end()) continue;
+        auto cnt = snap->image_spread->find(it->first);
+        int64_t spread = cnt == snap->image_spread->end() ? 0 : cnt->second;
+        sum += static_cast<int64_t>(static_cast<double>(it->second) * static_cast<double>(spread) /
+                                    static_cast<double>(total_nodes));
+      }
     int64_t max_threshold = kMaxContainerThreshold * static_cast<int64_t>(p.containers.size());
     if (max_threshold <= kMinThreshold) return {0, {}};
     sum = std::clamp(sum, kMinThreshold, max_threshold);
@@ -560,9 +547,6 @@ class ImageLocality : public Plugin {
 
  private:
   Handle& h_;
-  mutable std::shared_mutex mu_;
-  std::unordered_map<std::string, std::unordered_map<std::string, int64_t>> node_images_;  // node -> image -> size
-  std::unordered_map<std::string, int64_t> image_nodes_;                                   // image -> #nodes
 };
 
 PluginRegistrar r1("PodTopologySpread", [](const Json&, Handle& h) { return std::make_shared<PodTopologySpread>(h); });

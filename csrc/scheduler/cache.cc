@@ -37,11 +37,36 @@ void SchedulerCache::group_delta(const Pod& p, int d) {
   if (c <= 0) group_assigned_.erase(k);
 }
 
-void SchedulerCache::add_node(const NodePtr& n) {
-  std::lock_guard<std::mutex> g(mu_);
+void SchedulerCache::account_node(const Node* old_node, const Node* new_node) {
+  prefer_nodes_ += (new_node && new_node->has_prefer_no_schedule) - (old_node && old_node->has_prefer_no_schedule);
+  const bool old_imgs = old_node && !old_node->image_sizes.empty();
+  const bool new_imgs = new_node && !new_node->image_sizes.empty();
+  if (!old_imgs && !new_imgs) return;  // heartbeat-style updates of image-less nodes cost nothing
+  if (old_imgs && new_imgs && old_node->image_sizes.size() == new_node->image_sizes.size()) {
+    bool same = true;
+    for (const auto& kv : new_node->image_sizes)
+      if (!old_node->image_sizes.count(kv.first)) {
+        same = false;
+        break;
+      }
+    if (same) return;
+  }
+  if (image_spread_.use_count() > 1) image_spread_ = std::make_shared<std::unordered_map<std::string, int64_t>>(*image_spread_);
+  auto& spread = *image_spread_;
+  if (old_imgs)
+    for (const auto& kv : old_node->image_sizes) {
+      auto it = spread.find(kv.first);
+      if (it != spread.end() && --it->second <= 0) spread.erase(it);
+    }
+  if (new_imgs)
+    for (const auto& kv : new_node->image_sizes) ++spread[kv.first];
+}
+
+void SchedulerCache::set_node_locked(const NodePtr& n) {
   ++node_epoch_;
   auto& ni = info_for(n->name());
   bool was_ghost = ni->node == nullptr;
+  account_node(ni->node.get(), n.get());
   writable(ni).set_node(n);
   if (was_ghost) {
     order_.push_back(n->name());
@@ -50,17 +75,14 @@ void SchedulerCache::add_node(const NodePtr& n) {
   mark_dirty(n->name());
 }
 
+void SchedulerCache::add_node(const NodePtr& n) {
+  std::lock_guard<std::mutex> g(mu_);
+  set_node_locked(n);
+}
+
 void SchedulerCache::update_node(const NodePtr& n) {
   std::lock_guard<std::mutex> g(mu_);
-  ++node_epoch_;
-  auto& ni = info_for(n->name());
-  bool was_ghost = ni->node == nullptr;
-  writable(ni).set_node(n);
-  if (was_ghost) {
-    order_.push_back(n->name());
-    structure_changed_ = true;
-  }
-  mark_dirty(n->name());
+  set_node_locked(n);
 }
 
 void SchedulerCache::remove_node(const std::string& name) {
@@ -68,6 +90,7 @@ void SchedulerCache::remove_node(const std::string& name) {
   auto it = nodes_.find(name);
   if (it == nodes_.end()) return;
   ++node_epoch_;
+  account_node(it->second->node.get(), nullptr);
   order_.erase(std::remove(order_.begin(), order_.end(), name), order_.end());
   structure_changed_ = true;
   if (it->second->pods.empty()) {
@@ -274,18 +297,8 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us) {
     }
   }
   s.generation = generation_;
-  if (s.node_epoch != node_epoch_) {
-    int64_t prefer = 0;
-    for (const auto& ni : s.nodes) {
-      if (!ni->node) continue;
-      for (const auto& t : ni->node->taints)
-        if (t.effect == "PreferNoSchedule") {
-          ++prefer;
-          break;
-        }
-    }
-    s.nodes_with_prefer_no_schedule = prefer;
-  }
+  s.nodes_with_prefer_no_schedule = prefer_nodes_;
+  if (s.image_spread != image_spread_) s.image_spread = image_spread_;
   s.node_epoch = node_epoch_;
   return clones;
 }

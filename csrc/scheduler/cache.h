@@ -78,6 +78,10 @@ class SchedulerCache {
   void remove_pod_locked(const Pod& p);
   void mark_dirty(const std::string& node);
   void group_delta(const Pod& p, int d);
+  void set_node_locked(const NodePtr& n);
+  // Cluster-wide Node-derived counts, adjusted per Node change (old -> new)
+  // instead of rescanning every node on each snapshot refresh.
+  void account_node(const Node* old_node, const Node* new_node);
 
   std::shared_ptr<Clock> clock_;
   int64_t ttl_us_;
@@ -91,6 +95,10 @@ class SchedulerCache {
   bool structure_changed_ = true;
   int64_t generation_ = 0;
   uint64_t node_epoch_ = 1;
+  int64_t prefer_nodes_ = 0;
+  // Copied on write while a snapshot still shares it.
+  std::shared_ptr<std::unordered_map<std::string, int64_t>> image_spread_ =
+      std::make_shared<std::unordered_map<std::string, int64_t>>();
 };
 
 }  // namespace xsched

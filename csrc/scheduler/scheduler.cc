@@ -989,6 +989,14 @@ Json Scheduler::explain(const Json& pod_obj) {
       }
       out.set("scores", std::move(sc));
       out.set("selected", Json(select_host(scores)));
+      // The scheduling path's totals (all-zero plugins skipped, their
+      // normalized constant still added) for parity checks against "total".
+      std::vector<NodeScore> hot;
+      if (fw->run_score(*state, *pod, feasible, hot, nullptr).is_success()) {
+        Json h = Json::object();
+        for (size_t i = 0; i < feasible.size(); ++i) h.set(feasible[i]->name(), Json(hot[i].score));
+        out.set("hot_path_totals", std::move(h));
+      }
     } else {
       out.set("score_error", Json(ps.message()));
     }
