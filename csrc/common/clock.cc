@@ -3,7 +3,10 @@
 namespace xsched {
 
 TimerService::TimerService(std::shared_ptr<Clock> clock) : clock_(std::move(clock)) {
-  th_ = std::thread([this] { loop(); });
+  th_ = std::thread([this] {
+    name_this_thread("xs-timer");
+    loop();
+  });
 }
 
 TimerService::~TimerService() { stop(); }
@@ -20,16 +23,21 @@ void TimerService::stop() {
 
 uint64_t TimerService::schedule_at(int64_t deadline_us, Fn fn) {
   uint64_t id;
+  bool earliest;
   {
     std::lock_guard<std::mutex> g(mu_);
     id = next_id_++;
     Timer t;
     t.fn = std::move(fn);
     t.pos = heap_.emplace(deadline_us, id);
+    // The loop sleeps until the earliest deadline; a later one needs no
+    // wake-up (Permit timeouts arrive in deadline order, so this skips a
+    // futex wake per waiting gang member).
+    earliest = t.pos == heap_.begin();
     timers_.emplace(id, std::move(t));
-    ++change_gen_;
+    if (earliest) ++change_gen_;
   }
-  cv_.notify_one();
+  if (earliest) cv_.notify_one();
   return id;
 }
 

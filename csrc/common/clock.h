@@ -18,8 +18,13 @@
 #include <mutex>
 #include <thread>
 #include <unordered_map>
+#include <pthread.h>
 
 namespace xsched {
+
+// Names the calling thread (<= 15 chars) so per-thread CPU shows up by role
+// in top -H, /proc/<pid>/task/*/comm and the stress driver's sampler.
+inline void name_this_thread(const char* name) { pthread_setname_np(pthread_self(), name); }
 
 class Clock {
  public:

@@ -1,5 +1,7 @@
 #include "common/parallel.h"
 
+#include "common/clock.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -7,7 +9,10 @@
 namespace xsched {
 
 Parallelizer::Parallelizer(int workers, int inline_below) : workers_(std::max(1, workers)), inline_below_(inline_below) {
-  for (int i = 0; i < workers_ - 1; ++i) threads_.emplace_back([this] { worker_loop(); });
+  for (int i = 0; i < workers_ - 1; ++i) threads_.emplace_back([this] {
+    name_this_thread("xs-filter");
+    worker_loop();
+  });
 }
 
 Parallelizer::~Parallelizer() {
@@ -19,11 +24,12 @@ Parallelizer::~Parallelizer() {
   for (auto& t : threads_) t.join();
 }
 
-namespace {
-int64_t now_ns() {
+int64_t Parallelizer::now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
       .count();
 }
+
+namespace {
 void ema(std::atomic<int64_t>& v, int64_t sample, bool seed) {
   int64_t cur = v.load(std::memory_order_relaxed);
   v.store(seed ? sample : cur + (sample - cur) / 8, std::memory_order_relaxed);  // alpha 1/8
@@ -74,9 +80,7 @@ void Parallelizer::worker_loop() {
   }
 }
 
-void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop,
-                         ParallelSite* site) {
-  if (n <= 0) return;
+bool Parallelizer::plan_inline(int n, ParallelSite* site) {
   // Helpers only pay off when each gets >= inline_below_/2 items: a fork/join
   // round costs a few microseconds of wake-ups, more than filtering dozens of
   // nodes with the allocation-free plugins.
@@ -88,7 +92,19 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
     bool probe = site->calls.fetch_add(1, std::memory_order_relaxed) % ParallelSite::kProbeEvery == 0;
     cheap = probe || est < kMinParallelWorkNs;
   }
-  if (n < inline_below_ || helpers <= 0 || cheap) {
+  return n < inline_below_ || helpers <= 0 || cheap;
+}
+
+void Parallelizer::record_inline(ParallelSite* site, int64_t elapsed_ns, int done, int n) {
+  observe(site, elapsed_ns, done);
+  observe_done(site, done, n);
+}
+
+void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop,
+                         ParallelSite* site) {
+  if (n <= 0) return;
+  int helpers = std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1);
+  if (plan_inline(n, site)) {
     int64_t t0 = site ? now_ns() : 0;
     int done = 0;
     for (int i = 0; i < n; ++i) {
@@ -96,10 +112,7 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
       fn(i);
       ++done;
     }
-    if (site) {
-      observe(site, now_ns() - t0, done);
-      observe_done(site, done, n);
-    }
+    if (site) record_inline(site, now_ns() - t0, done, n);
     return;
   }
   std::lock_guard<std::mutex> call(call_mu_);

@@ -47,6 +47,13 @@ class Parallelizer {
   // allow early exit (e.g. enough feasible nodes found).
   void until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop = nullptr,
              ParallelSite* site = nullptr);
+  // The inline-vs-fork decision `until` makes for (n, site), exposed so a hot
+  // call site can run its own serial loop (plain counters instead of the
+  // atomics a parallel run needs) and report it with `record_inline`.
+  // Counts as a call of the site (advances its probe cadence).
+  bool plan_inline(int n, ParallelSite* site);
+  static void record_inline(ParallelSite* site, int64_t elapsed_ns, int done, int n);
+  static int64_t now_ns();
   int workers() const { return workers_; }
   static constexpr int64_t kMinParallelWorkNs = 60'000;
 

@@ -275,7 +275,7 @@ std::pair<PostFilterResult, Status> Framework::run_post_filter(CycleState& s, co
   return {PostFilterResult{}, last};
 }
 
-Status Framework::run_pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) {
+Status Framework::run_pre_score(CycleState& s, const Pod& p, const NodeList& nodes) {
   auto it = chain_.find(kPreScore);
   if (it == chain_.end()) return {};
   for (const auto& pl : it->second) {
@@ -304,12 +304,14 @@ std::vector<char> Framework::local_scorers(const Pod& p, const Snapshot& snap) c
   return out;
 }
 
-Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes,
+Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
                             std::vector<NodeScore>& total, ScoreBreakdown* breakdown, EqScoreCache* eq) {
   int64_t t0 = s.record_metrics ? handle_.clock->now_us() : 0;
   size_t n = nodes.size();
-  total.assign(n, NodeScore{});
-  for (size_t i = 0; i < n; ++i) total[i].name = nodes[i]->name();
+  total.resize(n);
+  for (size_t i = 0; i < n; ++i) total[i].score = 0;
+  if (breakdown)
+    for (size_t i = 0; i < n; ++i) total[i].name = nodes[i]->name();
   if (scorers_.empty()) return {};
   // Per-plugin score rows are reused across cycles (no allocation or string
   // construction per plugin x node in steady state); every cell is written
@@ -372,7 +374,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const std::vector<NodeI
     auto& pl = scorers_[k].first;
     if (pl->has_normalize_score()) {
       if (pl->normalize_uses_names())
-        for (size_t i = 0; i < n; ++i) per[k][i].name = total[i].name;
+        for (size_t i = 0; i < n; ++i) per[k][i].name = nodes[i]->name();
       Status st = pl->normalize_score(s, p, per[k]);
       if (!st.is_success()) return Status(Code::Error, "running Normalize on Score plugin " + pl->name() + ": " + st.message());
     }

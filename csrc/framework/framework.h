@@ -62,11 +62,13 @@ class Framework {
   Status run_filter(CycleState& s, const Pod& p, const NodeInfo& ni);
   Status run_filter_with_nominated_pods(CycleState& s, const Pod& p, const NodeInfo& ni);
   std::pair<PostFilterResult, Status> run_post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m);
-  Status run_pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes);
+  Status run_pre_score(CycleState& s, const Pod& p, const NodeList& nodes);
   // Weighted sum of all score plugins per node (same order as `nodes`).
   // `breakdown` (optional) receives ("Plugin*weight", normalized scores).
+  // Only scores are filled on the scheduling path; `total[i].name` is set
+  // when a breakdown is requested (explain), since callers index `nodes`.
   using ScoreBreakdown = std::vector<std::pair<std::string, std::vector<int64_t>>>;
-  Status run_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes, std::vector<NodeScore>& total,
+  Status run_score(CycleState& s, const Pod& p, const NodeList& nodes, std::vector<NodeScore>& total,
                    ScoreBreakdown* breakdown = nullptr, EqScoreCache* eq = nullptr);
   // Equivalence cache: every Filter plugin node-local for `p`?
   bool filters_node_local(const Pod& p, const Snapshot& s) const;

@@ -98,7 +98,7 @@ class Plugin {
     return {PostFilterResult{}, Status(Code::Unschedulable)};
   }
   // PreScore / Score
-  virtual Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) { return {}; }
+  virtual Status pre_score(CycleState& s, const Pod& p, const NodeList& nodes) { return {}; }
   virtual std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) { return {0, {}}; }
   virtual bool has_normalize_score() const { return false; }
   virtual Status normalize_score(CycleState& s, const Pod& p, std::vector<NodeScore>& scores) { return {}; }

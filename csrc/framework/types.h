@@ -201,6 +201,10 @@ struct NodeInfo {
   const PodPtr* find_pod(const std::string& uid) const;
 };
 using NodeInfoPtr = std::shared_ptr<NodeInfo>;
+// Nodes of one scheduling cycle (feasible set, score order). Borrowed from
+// the Snapshot, which holds every version for the whole cycle, so the hot
+// path passes raw pointers instead of bumping shared refcounts per node.
+using NodeList = std::vector<const NodeInfo*>;
 
 // ------------------------------------------------------------ Snapshot ----
 struct Snapshot {

@@ -64,6 +64,7 @@ WaitingPodPtr WaitingPods::add(const PodPtr& pod, const std::string& node, const
   {
     std::lock_guard<std::mutex> g(mu_);
     pods_[pod->uid()] = wp;
+    if (pod->pg_key) by_group_[pod->pg_key].push_back(wp);
   }
   // Arm timers after registration so a zero timeout cannot fire before the
   // pod is visible to IterateOverWaitingPods.
@@ -96,6 +97,17 @@ void WaitingPods::iterate(const std::function<void(const WaitingPodPtr&)>& fn) c
   for (const auto& wp : snap) fn(wp);
 }
 
+void WaitingPods::iterate_group(uint64_t pg_key, const std::function<void(const WaitingPodPtr&)>& fn) const {
+  std::vector<WaitingPodPtr> snap;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = by_group_.find(pg_key);
+    if (it == by_group_.end()) return;
+    snap = it->second;
+  }
+  for (const auto& wp : snap) fn(wp);
+}
+
 size_t WaitingPods::size() const {
   std::lock_guard<std::mutex> g(mu_);
   return pods_.size();
@@ -103,7 +115,22 @@ size_t WaitingPods::size() const {
 
 void WaitingPods::remove(const std::string& uid) {
   std::lock_guard<std::mutex> g(mu_);
-  pods_.erase(uid);
+  auto it = pods_.find(uid);
+  if (it == pods_.end()) return;
+  if (uint64_t key = it->second->pod()->pg_key) {
+    auto git = by_group_.find(key);
+    if (git != by_group_.end()) {
+      auto& v = git->second;
+      for (size_t i = 0; i < v.size(); ++i)
+        if (v[i] == it->second) {
+          v[i] = std::move(v.back());
+          v.pop_back();
+          break;
+        }
+      if (v.empty()) by_group_.erase(git);
+    }
+  }
+  pods_.erase(it);
 }
 
 void WaitingPods::reject_all(const std::string& msg) {

@@ -58,6 +58,9 @@ class WaitingPods {
                     WaitingPod::Done on_done);
   WaitingPodPtr get(const std::string& uid) const;
   void iterate(const std::function<void(const WaitingPodPtr&)>& fn) const;
+  // Waiting pods whose Pod::pg_key is `pg_key` (callers still compare the
+  // group name: the key is a 64-bit hash). O(group), not O(all waiting).
+  void iterate_group(uint64_t pg_key, const std::function<void(const WaitingPodPtr&)>& fn) const;
   size_t size() const;
   // Reject every waiting pod (shutdown).
   void reject_all(const std::string& msg);
@@ -68,6 +71,7 @@ class WaitingPods {
   TimerService* timers_;
   mutable std::mutex mu_;
   std::unordered_map<std::string, WaitingPodPtr> pods_;
+  std::unordered_map<uint64_t, std::vector<WaitingPodPtr>> by_group_;
 };
 
 }  // namespace xsched

@@ -190,11 +190,11 @@ class Coscheduling : public Plugin {
     if (!m.empty() && m.begin()->second.failed_plugin() == name())
       return {PostFilterResult{}, Status(Code::Unschedulable)};
     std::string full = p.pg_full_name();
-    int assigned = h_.cache->assigned_in_group(full);
+    int assigned = h_.cache->assigned_in_group(p.pg_key);
     if (assigned >= pg->min_member) return {PostFilterResult{}, Status(Code::Unschedulable)};
     float gap = static_cast<float>(pg->min_member - assigned) / static_cast<float>(std::max(1, pg->min_member));
     if (gap <= 0.1f) return {PostFilterResult{}, Status(Code::Unschedulable)};
-    reject_group(p.ns(), p.pod_group, "optimistic rejection in PostFilter");
+    reject_group(p, "optimistic rejection in PostFilter");
     denied_.add(full, denied_ttl_us_);
     permitted_.erase(full);
     return {PostFilterResult{},
@@ -202,10 +202,12 @@ class Coscheduling : public Plugin {
                                   " is unschedulable even after PostFilter")};
   }
 
-  void reject_group(const std::string& ns, const std::string& pg, const std::string& msg) {
-    h_.waiting_pods->iterate([&](const WaitingPodPtr& wp) {
+  // Rejects every waiting member of p's group (the group index visits only
+  // that group's waiting pods; names are still compared, as the key is a hash).
+  void reject_group(const Pod& p, const std::string& msg) {
+    h_.waiting_pods->iterate_group(p.pg_key, [&](const WaitingPodPtr& wp) {
       const Pod& wpod = *wp->pod();
-      if (wpod.ns() == ns && wpod.pod_group == pg) wp->reject(name(), msg);
+      if (wpod.ns() == p.ns() && wpod.pod_group == p.pod_group) wp->reject(name(), msg);
     });
   }
 
@@ -214,15 +216,14 @@ class Coscheduling : public Plugin {
     if (p->pod_group.empty()) return {Status(), 0};
     auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
     if (!pg) return {Status::unschedulable("PodGroup not found"), 0};
-    std::string full = p->pg_full_name();
     // The cache already holds this (assumed) pod, so `assigned` includes it:
     // equivalent to the reference's snapshot count + 1.
-    int assigned = h_.cache->assigned_in_group(full);
+    int assigned = h_.cache->assigned_in_group(p->pg_key);
     if (assigned < pg->min_member) {
       activate_siblings(*p, s);
       return {Status(Code::Wait), wait_time(*pg)};
     }
-    h_.waiting_pods->iterate([&](const WaitingPodPtr& wp) {
+    h_.waiting_pods->iterate_group(p->pg_key, [&](const WaitingPodPtr& wp) {
       const Pod& q = *wp->pod();  // flat group key first: no string build per waiting pod
       if (q.pg_key == p->pg_key && q.pod_group == p->pod_group && q.ns() == p->ns()) wp->allow(name());
     });
@@ -244,7 +245,7 @@ class Coscheduling : public Plugin {
     if (p->pod_group.empty()) return;
     auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
     if (!pg) return;
-    reject_group(p->ns(), p->pod_group, "rejection in Unreserve");
+    reject_group(*p, "rejection in Unreserve");
     denied_.add(p->pg_full_name(), denied_ttl_us_);
     permitted_.erase(p->pg_full_name());
   }
@@ -259,7 +260,7 @@ class Coscheduling : public Plugin {
     // count goes stale after the first member (a gang of 4 sticks at
     // Scheduling/1). We take the larger of that and the group's assigned
     // (assumed + bound) pods from the cache.
-    int32_t scheduled = std::max<int32_t>(pg->scheduled + 1, h_.cache->assigned_in_group(p->pg_full_name()));
+    int32_t scheduled = std::max<int32_t>(pg->scheduled + 1, h_.cache->assigned_in_group(p->pg_key));
     std::string phase;
     Json status = Json::object();
     if (scheduled >= pg->min_member) {

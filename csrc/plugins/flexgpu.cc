@@ -273,7 +273,7 @@ class FlexGPU : public Plugin {
     st->annotations.set(gn.index_annotation, Json(join_ints(pl.gpus)));
     if (!pl.parts.empty()) st->annotations.set(gn.partition_annotation, Json(join_parts(pl.parts)));
     const Json& ann = st->annotations;
-    h_.cache->mutate_assumed_pod(p->uid(), [&](Pod& cp) {
+    h_.cache->annotate_assumed_pod(p->uid(), [&](Pod& cp) {
       for (const auto& kv : ann.members()) {
         bool set = false;
         for (auto& a : cp.meta.annotations)

@@ -276,7 +276,7 @@ class TopologyMatch : public Plugin {
 
   // PreScore: gang facts shared by every node's Score (one PodGroup lookup
   // and one assigned-count read per cycle instead of per node).
-  Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>&) override {
+  Status pre_score(CycleState& s, const Pod& p, const NodeList&) override {
     if (strategy_ != Strategy::XGMI) return {};
     auto ctx = std::make_shared<GangCtx>();
     if (!p.pod_group.empty()) {
@@ -286,7 +286,7 @@ class TopologyMatch : public Plugin {
         ctx->gang = true;
         ctx->full = p.pg_full_name();
         ctx->key = p.pg_key;
-        ctx->remaining = std::max<int64_t>(1, pg->min_member - h_.cache->assigned_in_group(ctx->full));
+        ctx->remaining = std::max<int64_t>(1, pg->min_member - h_.cache->assigned_in_group(ctx->key));
         ctx->kind = d.kind == GpuDemand::Gpu ? GangCtx::kWhole : GangCtx::kXcd;
         ctx->amount = d.amount;
       }
@@ -329,7 +329,7 @@ class TopologyMatch : public Plugin {
       if (auto* c = s.read_as<GangCtx>(kGangKey)) return {gang_score(*c, ni), {}};
       // PreScore not enabled for this profile: derive the context per node.
       CycleState local;
-      std::vector<NodeInfoPtr> none;
+      NodeList none;
       pre_score(local, p, none);
       return {gang_score(*local.read_as<GangCtx>(kGangKey), ni), {}};
     }

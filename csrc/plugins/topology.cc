@@ -179,7 +179,7 @@ class PodTopologySpread : public Plugin {
     return {};
   }
 
-  Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) override {
+  Status pre_score(CycleState& s, const Pod& p, const NodeList& nodes) override {
     auto st = std::make_shared<SpreadScoreState>();
     for (const auto& c : p.spread_constraints)
       if (!c.hard) st->constraints.push_back(c);
@@ -434,7 +434,7 @@ class InterPodAffinity : public Plugin {
     if (const std::string* v = n.meta.label(t.topology_key)) st.topo_score[t.topology_key][*v] += w;
   }
 
-  Status pre_score(CycleState& s, const Pod& p, const std::vector<NodeInfoPtr>& nodes) override {
+  Status pre_score(CycleState& s, const Pod& p, const NodeList& nodes) override {
     auto st = std::make_shared<AffinityScoreState>();
     bool has_pref = !p.pod_affinity_preferred.empty() || !p.pod_anti_affinity_preferred.empty();
     if (h_.snapshot && !nodes.empty() && (has_pref || !h_.snapshot->have_pods_with_affinity.empty())) {

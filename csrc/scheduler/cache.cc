@@ -30,11 +30,10 @@ void SchedulerCache::mark_dirty(const std::string& node) {
 }
 
 void SchedulerCache::group_delta(const Pod& p, int d) {
-  if (p.pod_group.empty()) return;
-  std::string k = p.pg_full_name();
-  int& c = group_assigned_[k];
-  c += d;
-  if (c <= 0) group_assigned_.erase(k);
+  if (!p.pg_key) return;
+  auto it = group_assigned_.try_emplace(p.pg_key, 0).first;
+  it->second += d;
+  if (it->second <= 0) group_assigned_.erase(it);
 }
 
 void SchedulerCache::account_node(const Node* old_node, const Node* new_node) {
@@ -232,17 +231,20 @@ PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<vo
   return fresh;
 }
 
-PodPtr SchedulerCache::mutate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn) {
+PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn) {
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = pod_states_.find(uid);
     if (it == pod_states_.end()) return nullptr;
-    if (assumed_.count(uid) && !it->second.binding_finished) {
+    auto nit = nodes_.find(it->second.pod->node_name);
+    if (assumed_.count(uid) && !it->second.binding_finished && nit != nodes_.end()) {
       PodPtr pod = it->second.pod;
-      remove_pod_locked(*pod);
+      NodeInfo& ni = writable(nit->second);
+      ni.gpu.apply(pod->gpu, -1);
       fn(*pod);
       pod->recompute_gpu_assignment();
-      add_pod_locked(pod);
+      ni.gpu.apply(pod->gpu, +1);
+      mark_dirty(pod->node_name);
       return pod;
     }
   }
@@ -321,9 +323,9 @@ void SchedulerCache::cleanup_expired_assumed_pods() {
   }
 }
 
-int SchedulerCache::assigned_in_group(const std::string& pg_full_name) const {
+int SchedulerCache::assigned_in_group(uint64_t pg_key) const {
   std::lock_guard<std::mutex> g(mu_);
-  auto it = group_assigned_.find(pg_full_name);
+  auto it = group_assigned_.find(pg_key);
   return it == group_assigned_.end() ? 0 : it->second;
 }
 

@@ -48,10 +48,12 @@ class SchedulerCache {
   // Copy-on-write mutation of a cached (assumed or bound) pod; re-accounts
   // the pod on its node. Returns the new object (nullptr if not cached).
   PodPtr mutate_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
-  // In-place variant for a pod assumed in the current scheduling cycle
-  // (Reserve): no other thread holds that object yet, so the copy is skipped.
-  // Falls back to mutate_pod for pods that are not assumed.
-  PodPtr mutate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
+  // In-place annotation of a pod assumed in the current scheduling cycle
+  // (FlexGPU Reserve): no other thread holds that object yet, so there is no
+  // copy, and since `fn` may only change annotations, only the node's GPU
+  // ledger is re-accounted (Pod::recompute_gpu_assignment). Falls back to
+  // mutate_pod for pods that are not (or no longer) assumed.
+  PodPtr annotate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
 
   // Returns the number of NodeInfo versions refreshed (shared, not cloned:
   // the cache copies on write); replaced versions go to `s.retired`; `lock_wait_us` (optional)
@@ -59,7 +61,10 @@ class SchedulerCache {
   int update_snapshot(Snapshot& s, int64_t* lock_wait_us = nullptr);
   void cleanup_expired_assumed_pods();
 
-  int assigned_in_group(const std::string& pg_full_name) const;
+  // Pods of a PodGroup that are assumed or bound, keyed by Pod::pg_key (a
+  // 64-bit hash of "ns/name", as NodeInfo::pg_count).
+  int assigned_in_group(uint64_t pg_key) const;
+  int assigned_in_group(const std::string& pg_full_name) const { return assigned_in_group(pg_key_of(pg_full_name)); }
   size_t node_count() const;
   size_t pod_count() const;
   size_t assumed_count() const;
@@ -90,7 +95,7 @@ class SchedulerCache {
   std::vector<std::string> order_;  // node names with a Node object, insertion order
   std::unordered_map<std::string, PodState> pod_states_;
   std::unordered_set<std::string> assumed_;
-  std::unordered_map<std::string, int> group_assigned_;
+  std::unordered_map<uint64_t, int> group_assigned_;
   std::unordered_set<std::string> dirty_;
   bool structure_changed_ = true;
   int64_t generation_ = 0;

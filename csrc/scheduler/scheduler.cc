@@ -42,21 +42,41 @@ void StoreClient::record_event(const std::string& kind, const std::string& ns, c
 }
 
 // -------------------------------------------------------------- Executor ----
+bool Executor::try_pop(std::function<void()>& fn) {
+  if (q_.empty()) return false;
+  fn = std::move(q_.front());
+  q_.pop_front();
+  queued_.fetch_sub(1, std::memory_order_relaxed);
+  busy_.fetch_add(1);
+  return true;
+}
+
 Executor::Executor(int threads) {
   for (int i = 0; i < std::max(1, threads); ++i) {
     threads_.emplace_back([this] {
+      name_this_thread("xs-bind");
+      bool spin = false;  // just finished a task: poll before sleeping
       for (;;) {
         std::function<void()> fn;
+        if (spin && spinners_.fetch_add(1) < kMaxSpinners) {
+          const int64_t until = Parallelizer::now_ns() + kSpinNs;
+          while (queued_.load(std::memory_order_relaxed) == 0 && Parallelizer::now_ns() < until) __builtin_ia32_pause();
+          // Leave the spinner set before the locked check below: a submit
+          // that still saw this spinner finds its task taken here.
+          spinners_.fetch_sub(1);
+        } else if (spin) {
+          spinners_.fetch_sub(1);
+        }
         {
           std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-          if (q_.empty()) return;  // stop_ and drained
-          fn = std::move(q_.front());
-          q_.pop_front();
-          busy_.fetch_add(1);
+          if (!try_pop(fn)) {
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            if (!try_pop(fn)) return;  // stop_ and drained
+          }
         }
         fn();
         busy_.fetch_sub(1);
+        spin = true;
       }
     });
   }
@@ -68,8 +88,11 @@ void Executor::submit(std::function<void()> fn) {
   {
     std::lock_guard<std::mutex> g(mu_);
     q_.push_back(std::move(fn));
+    queued_.fetch_add(1, std::memory_order_relaxed);
   }
-  cv_.notify_one();
+  // Wake a sleeper unless a spinning worker is free for this task (a burst of
+  // k Allows from one gang still fans out over k workers).
+  if (queued_.load() > spinners_.load()) cv_.notify_one();
 }
 
 void Executor::stop() {
@@ -238,8 +261,14 @@ void Scheduler::start() {
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"backoff\"", static_cast<double>(c.backoff));
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"unschedulable\"", static_cast<double>(c.unschedulable));
   }));
-  informer_thread_ = std::thread([this] { informer_loop(); });
-  sched_thread_ = std::thread([this] { scheduling_loop(); });
+  informer_thread_ = std::thread([this] {
+    name_this_thread("xs-informer");
+    informer_loop();
+  });
+  sched_thread_ = std::thread([this] {
+    name_this_thread("xs-sched");
+    scheduling_loop();
+  });
 }
 
 void Scheduler::stop() {
@@ -603,12 +632,14 @@ Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
   return e.get();
 }
 
-Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d,
-                                      std::vector<NodeInfoPtr>& feasible, EqEntry* eq, bool full_diagnosis) {
+Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, NodeList& feasible,
+                                      EqEntry* eq, bool full_diagnosis, std::vector<int>* feasible_pos) {
   int64_t pf0 = tracer_.enabled() ? clock_->now_us() : 0;
   Status st = fw.run_pre_filter(s, p);
   if (tracer_.enabled()) tracer_.record(TraceEvent{"prefilter", p.key(), "", pf0, clock_->now_us() - pf0, 0});
   const auto& all = snapshot_.nodes;
+  feasible.clear();
+  if (feasible_pos) feasible_pos->clear();
   if (!st.is_success()) {
     if (!st.is_unschedulable()) return st;
     for (const auto& ni : all) d.node_to_status[ni->name()] = st;
@@ -617,10 +648,13 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   }
   // Prefer the nominated node (PreferNominatedNode, beta in 1.23).
   if (!p.nominated_node_name.empty()) {
-    if (auto ni = snapshot_.get(p.nominated_node_name)) {
+    auto it = snapshot_.index.find(p.nominated_node_name);
+    if (it != snapshot_.index.end()) {
+      const NodeInfo* ni = all[it->second].get();
       Status nst = fw.run_filter_with_nominated_pods(s, p, *ni);
       if (nst.is_success()) {
         feasible.push_back(ni);
+        if (feasible_pos) feasible_pos->push_back(static_cast<int>(it->second));
         return {};
       }
       if (!nst.is_unschedulable()) return nst;
@@ -630,22 +664,18 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   if (n == 0) return Status(Code::Unschedulable, "no nodes available to schedule pods");
   int to_find = num_feasible_nodes_to_find(fw, n);
   if (!fw.has(kFilter)) {
-    for (int i = 0; i < std::min(n, to_find); ++i) feasible.push_back(all[(next_start_node_ + i) % n]);
+    for (int i = 0; i < std::min(n, to_find); ++i) {
+      int pos = (next_start_node_ + i) % n;
+      feasible.push_back(all[pos].get());
+      if (feasible_pos) feasible_pos->push_back(pos);
+    }
     next_start_node_ = (next_start_node_ + static_cast<int>(feasible.size())) % n;
     return {};
   }
   // Filter verdicts are reused only when every Filter plugin is node-local for
   // this pod and no nominated pod can change a node's verdict.
   const bool eq_filter = eq && (!nominator_ || nominator_->empty()) && fw.filters_node_local(p, snapshot_);
-  std::vector<NodeInfoPtr> found(to_find);
-  std::atomic<int> count{0};
-  std::atomic<int> processed{0};
-  std::atomic<bool> stop{false};
-  std::mutex mu;
-  Status first_err;
-  bool has_err = false;
   int start = next_start_node_;
-  std::atomic<uint64_t> hits{0};
   // Per-node failures go to a position-indexed buffer (no lock, no map
   // insert per node); the NodeToStatusMap is only materialized when the
   // diagnosis is consumed: no feasible node (PostFilter / FitError) or explain.
@@ -654,61 +684,116 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   // workers doing that per node serialize on its cache line.
   if (static_cast<int>(fail_buf_.size()) < n) fail_buf_.resize(n);
   fail_ptr_.assign(n, nullptr);
-  parallelizer_->until(n, [&](int i) {
-    const int pos = (start + i) % n;
-    const NodeInfoPtr& ni = all[pos];
-    Status own;
-    const Status* fp = &own;
-    if (eq_filter) {
-      EqSlot& slot = eq->slots[pos];
-      if (slot.filter_gen == ni->generation) {
-        hits.fetch_add(1, std::memory_order_relaxed);
+  Status first_err;
+  bool has_err = false;
+  int c = 0, processed = 0;
+  uint64_t hits = 0;
+  if (static_cast<int>(found_buf_.size()) < to_find) found_buf_.resize(to_find);
+  if (static_cast<int>(found_pos_buf_.size()) < to_find) found_pos_buf_.resize(to_find);
+  if (parallelizer_->plan_inline(n, &filter_site_)) {
+    // Serial path (every cluster below the parallel threshold, and larger
+    // ones whose verdicts mostly come from the equivalence cache): plain
+    // counters, no std::function call or atomic per node.
+    const int64_t t0 = Parallelizer::now_ns();
+    for (int i = 0; i < n; ++i) {
+      int pos = start + i;
+      if (pos >= n) pos -= n;
+      const NodeInfo& ni = *all[pos];
+      const Status* fp;
+      if (eq_filter) {
+        EqSlot& slot = eq->slots[pos];
+        if (slot.filter_gen == ni.generation) {
+          ++hits;
+        } else {
+          slot.filter = fw.run_filter(s, p, ni);
+          slot.filter_gen = ni.generation;
+        }
+        fp = &slot.filter;
       } else {
-        slot.filter = fw.run_filter(s, p, *ni);
-        slot.filter_gen = ni->generation;
-      }
-      fp = &slot.filter;
-    } else {
-      own = fw.run_filter_with_nominated_pods(s, p, *ni);
-    }
-    const Status& fst = *fp;
-    processed.fetch_add(1, std::memory_order_relaxed);
-    if (fst.is_success()) {
-      int len = count.fetch_add(1) + 1;
-      if (len > to_find) {
-        stop.store(true);
-        count.fetch_sub(1);
-      } else {
-        found[len - 1] = ni;
-        if (len == to_find) stop.store(true);
-      }
-      return;
-    }
-    if (fst.is_unschedulable()) {
-      if (fp == &own) {
-        fail_buf_[pos] = std::move(own);
+        fail_buf_[pos] = fw.run_filter_with_nominated_pods(s, p, ni);
         fp = &fail_buf_[pos];
       }
-      fail_ptr_[pos] = fp;
-      return;
-    }
-    std::lock_guard<std::mutex> g(mu);
-    if (!has_err) {
-      first_err = fst;
+      ++processed;
+      if (fp->is_success()) {
+        found_buf_[c] = &ni;
+        found_pos_buf_[c] = pos;
+        if (++c == to_find) break;
+        continue;
+      }
+      if (fp->is_unschedulable()) {
+        fail_ptr_[pos] = fp;
+        continue;
+      }
+      first_err = *fp;
       has_err = true;
-      stop.store(true);
+      break;
     }
-  }, &stop, &filter_site_);
+    Parallelizer::record_inline(&filter_site_, Parallelizer::now_ns() - t0, processed, n);
+  } else {
+    std::atomic<int> count{0};
+    std::atomic<int> aprocessed{0};
+    std::atomic<bool> stop{false};
+    std::atomic<uint64_t> ahits{0};
+    std::mutex mu;
+    parallelizer_->until(n, [&](int i) {
+      const int pos = (start + i) % n;
+      const NodeInfo& ni = *all[pos];
+      Status own;
+      const Status* fp = &own;
+      if (eq_filter) {
+        EqSlot& slot = eq->slots[pos];
+        if (slot.filter_gen == ni.generation) {
+          ahits.fetch_add(1, std::memory_order_relaxed);
+        } else {
+          slot.filter = fw.run_filter(s, p, ni);
+          slot.filter_gen = ni.generation;
+        }
+        fp = &slot.filter;
+      } else {
+        own = fw.run_filter_with_nominated_pods(s, p, ni);
+      }
+      const Status& fst = *fp;
+      aprocessed.fetch_add(1, std::memory_order_relaxed);
+      if (fst.is_success()) {
+        int len = count.fetch_add(1) + 1;
+        if (len > to_find) {
+          stop.store(true);
+          count.fetch_sub(1);
+        } else {
+          found_buf_[len - 1] = &ni;
+          found_pos_buf_[len - 1] = pos;
+          if (len == to_find) stop.store(true);
+        }
+        return;
+      }
+      if (fst.is_unschedulable()) {
+        if (fp == &own) {
+          fail_buf_[pos] = std::move(own);
+          fp = &fail_buf_[pos];
+        }
+        fail_ptr_[pos] = fp;
+        return;
+      }
+      std::lock_guard<std::mutex> g(mu);
+      if (!has_err) {
+        first_err = fst;
+        has_err = true;
+        stop.store(true);
+      }
+    }, &stop, &filter_site_);
+    c = std::min(count.load(), to_find);
+    processed = aprocessed.load();
+    hits = ahits.load();
+  }
   if (eq_filter) {
-    uint64_t h = hits.load();
     std::lock_guard<std::mutex> g(stats_mu_);
-    stats_.eq_filter_hits += h;
-    stats_.eq_filter_misses += static_cast<uint64_t>(processed.load()) - h;
+    stats_.eq_filter_hits += hits;
+    stats_.eq_filter_misses += static_cast<uint64_t>(processed) - hits;
   }
   if (has_err) return first_err;
-  int c = std::min(count.load(), to_find);
-  next_start_node_ = (start + processed.load()) % n;
-  feasible.assign(found.begin(), found.begin() + c);
+  next_start_node_ = (start + processed) % n;
+  feasible.assign(found_buf_.begin(), found_buf_.begin() + c);
+  if (feasible_pos) feasible_pos->assign(found_pos_buf_.begin(), found_pos_buf_.begin() + c);
   if (feasible.empty() || full_diagnosis) {
     for (int pos = 0; pos < n; ++pos) {
       if (!fail_ptr_[pos]) continue;
@@ -733,8 +818,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   return {};
 }
 
-std::string Scheduler::select_host(const std::vector<NodeScore>& scores) {
-  if (scores.empty()) return {};
+size_t Scheduler::select_host(const std::vector<NodeScore>& scores) {
   int64_t best = scores[0].score;
   size_t sel = 0;
   int cnt = 1;
@@ -748,7 +832,7 @@ std::string Scheduler::select_host(const std::vector<NodeScore>& scores) {
       if (rng_() % static_cast<uint64_t>(cnt) == 0) sel = i;  // reservoir sampling
     }
   }
-  return scores[sel].name;
+  return sel;
 }
 
 Scheduler::CycleMetrics& Scheduler::cycle_metrics(const Framework& fw) {
@@ -804,9 +888,9 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   }
 
   Diagnosis diag;
-  std::vector<NodeInfoPtr> feasible;
+  NodeList& feasible = feasible_buf_;
   EqEntry* eq = eq_entry(*fw, *pod);
-  Status st = find_nodes_that_fit(*fw, *state, *pod, diag, feasible, eq);
+  Status st = find_nodes_that_fit(*fw, *state, *pod, diag, feasible, eq, false, &feasible_pos_buf_);
   if (tracer_.enabled())
     tracer_.record(TraceEvent{"filter", pod->key(), std::to_string(feasible.size()), snap_end,
                               clock_->now_us() - snap_end, 0});
@@ -815,10 +899,10 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     if (feasible.size() == 1) {
       host = feasible[0]->name();
     } else {
-      std::vector<NodeScore> scores;
+      std::vector<NodeScore>& scores = scores_buf_;
       if (!fw->has(kScore)) {
-        scores.reserve(feasible.size());
-        for (const auto& ni : feasible) scores.push_back(NodeScore{ni->name(), 1});
+        scores.assign(feasible.size(), NodeScore{});
+        for (auto& sc : scores) sc.score = 1;
         st = Status();
       } else {
         st = fw->run_pre_score(*state, *pod, feasible);
@@ -826,14 +910,11 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         if (eq) esc.local = fw->local_scorers(*pod, snapshot_);
         if (!esc.local.empty()) {
           esc.slots.resize(feasible.size());
-          for (size_t i = 0; i < feasible.size(); ++i) {
-            auto it = snapshot_.index.find(feasible[i]->name());
-            esc.slots[i] = it != snapshot_.index.end() ? &eq->slots[it->second] : nullptr;
-          }
+          for (size_t i = 0; i < feasible.size(); ++i) esc.slots[i] = &eq->slots[feasible_pos_buf_[i]];
         }
         if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores, nullptr, esc.local.empty() ? nullptr : &esc);
       }
-      if (st.is_success()) host = select_host(scores);
+      if (st.is_success()) host = feasible[select_host(scores)]->name();
     }
   }
   int64_t algo_end = clock_->now_us();
@@ -957,7 +1038,7 @@ Json Scheduler::explain(const Json& pod_obj) {
   auto state = std::make_shared<CycleState>();
   state->write(kPodsToActivateKey, std::make_shared<PodsToActivate>());
   Diagnosis d;
-  std::vector<NodeInfoPtr> feasible;
+  NodeList feasible;
   int saved_start = next_start_node_;
   Status st = find_nodes_that_fit(*fw, *state, *pod, d, feasible, nullptr, true);
   next_start_node_ = saved_start;
@@ -988,7 +1069,7 @@ Json Scheduler::explain(const Json& pod_obj) {
         sc.set(feasible[i]->name(), std::move(node));
       }
       out.set("scores", std::move(sc));
-      out.set("selected", Json(select_host(scores)));
+      out.set("selected", Json(feasible[select_host(scores)]->name()));
       // The scheduling path's totals (all-zero plugins skipped, their
       // normalized constant still added) for parity checks against "total".
       std::vector<NodeScore> hot;
@@ -1012,7 +1093,9 @@ double Scheduler::score_benchmark(const Json& pod_obj, int iterations, Json* out
   Framework* fw = framework_for(pod->scheduler_name);
   if (!fw) throw std::runtime_error("no profile for schedulerName " + pod->scheduler_name);
   cache_->update_snapshot(snapshot_);
-  const std::vector<NodeInfoPtr>& nodes = snapshot_.nodes;
+  NodeList nodes;
+  nodes.reserve(snapshot_.nodes.size());
+  for (const auto& ni : snapshot_.nodes) nodes.push_back(ni.get());
   int64_t checksum = 0;
   int64_t t0 = clock_->now_us();
   for (int it = 0; it < std::max(1, iterations); ++it) {

@@ -61,12 +61,21 @@ class Executor {
   size_t pending() const;
 
  private:
+  // A worker that finishes a task spins briefly on `queued_` before it
+  // sleeps, and submit() skips the futex wake while a spinning worker can
+  // take the task: under load the scheduling thread hands bindings over
+  // without a syscall.
+  static constexpr int64_t kSpinNs = 30'000;
+  static constexpr int kMaxSpinners = 2;
+  bool try_pop(std::function<void()>& fn);  // under mu_
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
   std::vector<std::thread> threads_;
   bool stop_ = false;
   std::atomic<int> busy_{0};
+  std::atomic<int> queued_{0};
+  std::atomic<int> spinners_{0};
 };
 
 struct SchedulerOptions {
@@ -195,10 +204,18 @@ class Scheduler {
   void handle_node_event(const WatchEvent& ev);
   void scheduling_loop();
   void schedule_cycle(const QueuedPodInfoPtr& qpi);
-  Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, std::vector<NodeInfoPtr>& feasible,
-                             EqEntry* eq = nullptr, bool full_diagnosis = false);
+  // `feasible_pos` (optional) receives each feasible node's snapshot position.
+  Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, NodeList& feasible,
+                             EqEntry* eq = nullptr, bool full_diagnosis = false, std::vector<int>* feasible_pos = nullptr);
   int num_feasible_nodes_to_find(Framework& fw, int n) const;
-  std::string select_host(const std::vector<NodeScore>& scores);
+  // Index of the highest total (reservoir-sampled among ties).
+  size_t select_host(const std::vector<NodeScore>& scores);
+  // Cycle scratch reused across cycles (scheduling thread only).
+  NodeList feasible_buf_;
+  std::vector<const NodeInfo*> found_buf_;
+  std::vector<int> found_pos_buf_;
+  std::vector<int> feasible_pos_buf_;
+  std::vector<NodeScore> scores_buf_;
   void binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
                      int64_t cycle, Status permit_status, int64_t wait_start_us,
                      std::shared_ptr<PodsToActivate> to_activate);

@@ -7,6 +7,7 @@
 // wave_<i>.json files {"podgroups":[...],"pods":[...]} written by
 // flex_gpu_scheduler_amd/tools/stress.py.
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <fstream>
 #include <sstream>
@@ -14,6 +15,7 @@
 #include <thread>
 
 #include "scheduler/scheduler.h"
+#include "tools/sampler.h"
 
 using namespace xsched;
 
@@ -46,6 +48,10 @@ int main(int argc, char** argv) {
   Json cfg = Json::parse(slurp(dir + "/config.json"));
   Scheduler sched(store, cfg);
   sched.start();
+  // XSCHED_SAMPLE=<file>: CPU-sample every thread during the waves
+  // (tools/sample_report.py symbolizes the dump).
+  const char* sample_path = std::getenv("XSCHED_SAMPLE");
+  if (sample_path) sampler::start(std::getenv("XSCHED_SAMPLE_HZ") ? std::atoi(std::getenv("XSCHED_SAMPLE_HZ")) : 4000);
   uint64_t bound = 0;
   double total_s = 0;
   size_t total_pods = 0;
@@ -80,6 +86,7 @@ int main(int argc, char** argv) {
     total_pods += n;
     std::printf("wave %d: %zu pods in %.4fs (%.0f pods/s)\n", w, n, s, n / s);
   }
+  if (sample_path) sampler::dump(sample_path);
   sched.stop();
   std::printf("total: %zu pods in %.4fs (%.0f pods/s)\n", total_pods, total_s, total_pods / total_s);
   return 0;

@@ -1,0 +1,158 @@
+"""Symbolize and summarize a CPU-sample dump of the native stress driver
+(csrc/tools/sampler.h; `XSCHED_SAMPLE=<file> build/xsched_stress <dir> N`).
+
+Samples are wall-clock (every thread, fixed rate). A sample whose stack is
+parked in a condition-variable wait or a sleep is idle; the rest are busy
+(lock contention counts as busy). Per thread role (xs-sched, xs-bind,
+xs-informer, xs-filter, xs-timer, main): busy fraction, and over busy samples
+the top functions by self time (leaf frame), by self time with library frames
+charged to their caller in our code, and by inclusive time.
+
+    python -m flex_gpu_scheduler_amd.tools.sample_report <dump> [--exe build/xsched_stress] [--top 25] [--json out]
+"""
+from __future__ import annotations
+
+import argparse
+import bisect
+import collections
+import json
+import re
+import subprocess
+import sys
+
+
+class SymbolTable:
+    def __init__(self, path: str, dynamic: bool = False):
+        args = ["nm", "-C", "-n", "--defined-only"] + (["-D"] if dynamic else []) + [path]
+        try:
+            out = subprocess.run(args, capture_output=True, text=True, check=False).stdout
+        except OSError:
+            out = ""
+        self.addrs: list[int] = []
+        self.names: list[str] = []
+        for line in out.splitlines():
+            parts = line.split(" ", 2)
+            if len(parts) < 3 or parts[1] not in "tTwW":
+                continue
+            self.addrs.append(int(parts[0], 16))
+            self.names.append(parts[2])
+
+    def lookup(self, off: int) -> str | None:
+        i = bisect.bisect_right(self.addrs, off) - 1
+        return self.names[i] if i >= 0 else None
+
+
+def short(name: str, width: int = 110) -> str:
+    name = re.sub(r"std::__cxx11::basic_string<char, std::char_traits<char>, std::allocator<char> >", "std::string", name)
+    name = re.sub(r"\(__gnu_cxx::_Lock_policy\)2", "2", name)
+    return name if len(name) <= width else name[: width - 3] + "..."
+
+
+def load(dump: str, exe: str):
+    base = 0
+    maps: list[tuple[int, int, int, str]] = []
+    samples: list[tuple[str, list[int]]] = []
+    with open(dump) as f:
+        for line in f:
+            if line.startswith("exe_base "):
+                base = int(line.split()[1], 16)
+            elif line.startswith("map "):
+                m = line.split()
+                lo, hi = (int(x, 16) for x in m[1].split("-"))
+                maps.append((lo, hi, int(m[3], 16), m[6] if len(m) > 6 else "?"))
+            else:
+                parts = line.split()
+                if len(parts) < 3:
+                    continue
+                samples.append((parts[1], [int(x, 16) for x in parts[2:]]))
+    exe_syms = SymbolTable(exe)
+    lib_syms: dict[str, SymbolTable] = {}
+    cache: dict[int, str] = {}
+
+    def resolve(pc: int) -> str:
+        if pc in cache:
+            return cache[pc]
+        name = None
+        for lo, hi, off, path in maps:
+            if lo <= pc < hi:
+                if path.endswith(exe.split("/")[-1]):
+                    name = exe_syms.lookup(pc - base)
+                else:
+                    tab = lib_syms.get(path)
+                    if tab is None:
+                        tab = lib_syms[path] = SymbolTable(path, dynamic=True)
+                    sym = tab.lookup(pc - lo + off)
+                    name = f"{sym or '?'} [{path.split('/')[-1]}]"
+                break
+        cache[pc] = name or f"?{pc:x}"
+        return cache[pc]
+
+    return samples, resolve
+
+
+IDLE_MARKERS = ("pthread_cond_wait", "pthread_cond_timedwait", "pthread_cond_clockwait",
+                "std::condition_variable::wait", "nanosleep", "clock_nanosleep", "std::this_thread::sleep")
+
+
+def is_idle(frames: list[str]) -> bool:
+    return any(f.startswith(IDLE_MARKERS) for f in frames[:6])
+
+
+def summarize(dump: str, exe: str, top: int = 25) -> dict:
+    samples, resolve = load(dump, exe)
+    by_thread: dict[str, list[list[str]]] = collections.defaultdict(list)
+    for tname, pcs in samples:
+        # frames[0] is the handler, [1] the signal trampoline; [2] is the interrupted pc.
+        frames = [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
+        role = re.sub(r"\d+$", "", tname)
+        by_thread[role].append(frames)
+    total = sum(len(v) for v in by_thread.values())
+    out: dict = {"samples": total, "threads": {}}
+    for role, all_stacks in sorted(by_thread.items(), key=lambda kv: -len(kv[1])):
+        stacks = [s for s in all_stacks if not is_idle(s)]
+        self_c = collections.Counter(s[0] for s in stacks if s)
+        # First frame in our own code: charges libc/libstdc++ time (malloc,
+        # locks, atomics) to the function that called into it.
+        own_c = collections.Counter(next((f for f in s if "[lib" not in f), "?") for s in stacks if s)
+        incl_c: collections.Counter = collections.Counter()
+        for s in stacks:
+            incl_c.update(set(s))
+        n = max(1, len(stacks))
+        out["threads"][role] = {
+            "samples": len(all_stacks),
+            "busy": round(len(stacks) / max(1, len(all_stacks)), 4),
+            "self": [[round(c / n, 4), short(f)] for f, c in self_c.most_common(top)],
+            "self_own_code": [[round(c / n, 4), short(f)] for f, c in own_c.most_common(top)],
+            "inclusive": [[round(c / n, 4), short(f)] for f, c in incl_c.most_common(top)],
+        }
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("dump")
+    ap.add_argument("--exe", default="build/xsched_stress")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    rep = summarize(a.dump, a.exe, a.top)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rep, f, indent=1)
+    print(f"samples: {rep['samples']}")
+    for role, t in rep["threads"].items():
+        print(f"\n== {role}: {t['samples']} samples, {100 * t['busy']:.1f}% busy (profiles below: busy samples)")
+        print("  self:")
+        for frac, f in t["self"]:
+            print(f"    {100 * frac:5.1f}%  {f}")
+        print("  self, library time charged to its caller in our code:")
+        for frac, f in t["self_own_code"]:
+            print(f"    {100 * frac:5.1f}%  {f}")
+        print("  inclusive:")
+        for frac, f in t["inclusive"]:
+            print(f"    {100 * frac:5.1f}%  {f}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
