@@ -11,11 +11,17 @@
 // publishes the WatcherMetrics document as a `loadwatchermetrics` object in
 // the API store; the plugins watch that kind, so Score never does I/O and a
 // refresh is one informer event. GPU metric types ("GPU" utilization %,
-// "GPUMemory" %) extend the CPU/Memory set:
+// "GPUMemory" %, and from amd-smi "GPUMemoryBandwidth" = HBM controller
+// activity % and "XGMI" = xGMI traffic % of link capacity) extend the
+// CPU/Memory set:
 //  * TargetLoadPacking arg `resourceType: GPU` packs on live MI355X busy %
 //    (capacity = amd.com/gpu, a pod's predicted use = its GPU limit);
-//  * LoadVariationRiskBalancing adds a GPU risk dimension when GPU metrics are
-//    present and the pod requests GPUs (score = min over valid dimensions).
+//    `resourceType: GPUMemoryBandwidth` packs on HBM bandwidth the same way
+//    (a GPU pod is predicted to drive its GPUs' HBM);
+//  * LoadVariationRiskBalancing adds risk dimensions for GPU busy and HBM
+//    bandwidth when the pod requests GPUs, and for xGMI when it is also a
+//    PodGroup member (gang ranks all-reduce over xGMI); score = min over the
+//    valid dimensions.
 // Fixed: the pod-assign cache drops fully-stale node entries (the reference's
 // cleanupCache keeps them when every entry is stale, handler.go:114-138).
 #include <array>
@@ -36,13 +42,15 @@ constexpr int64_t kCacheCleanupUs = 5LL * 60 * 1000000;
 
 // Metric types / operators are interned at parse time so Score compares
 // integers, not strings, per node.
-enum MType : uint8_t { kTCPU, kTMemory, kTGPU, kTGPUMemory, kTOther };
+enum MType : uint8_t { kTCPU, kTMemory, kTGPU, kTGPUMemory, kTGPUMemoryBandwidth, kTXGMI, kTOther };
 enum MOp : uint8_t { kOpAVG, kOpSTD, kOpLatest, kOpEmpty, kOpOther };
 MType mtype(const std::string& s) {
   if (s == "CPU") return kTCPU;
   if (s == "Memory") return kTMemory;
   if (s == "GPU") return kTGPU;
   if (s == "GPUMemory") return kTGPUMemory;
+  if (s == "GPUMemoryBandwidth") return kTGPUMemoryBandwidth;
+  if (s == "XGMI") return kTXGMI;
   return kTOther;
 }
 MOp mop(const std::string& s) {
@@ -229,7 +237,9 @@ class TargetLoadPacking : public TrimaranBase {
     if (multiplier_ <= 0) multiplier_ = 1.5;
     const Json& dr = args["defaultRequests"]["cpu"];
     default_milli_ = dr.is_string() ? Quantity::parse(dr.as_string()).milli_value() : 1000;
-    gpu_mode_ = args["resourceType"].str_or("CPU") == "GPU";
+    const std::string rt = args["resourceType"].str_or("CPU");
+    gpu_mode_ = rt == "GPU" || rt == "GPUMemoryBandwidth";
+    want_ = rt == "GPU" ? kTGPU : rt == "GPUMemoryBandwidth" ? kTGPUMemoryBandwidth : kTCPU;
   }
 
   // PredictUtilisation (targetloadpacking.go:286-294).
@@ -254,7 +264,7 @@ class TargetLoadPacking : public TrimaranBase {
     if (!m->present) return {kMinNodeScore, {}};
     auto it = m->nodes.find(ni.name());
     if (it == m->nodes.end()) return {kMinNodeScore, {}};
-    const MType want = gpu_mode_ ? kTGPU : kTCPU;
+    const MType want = want_;
     double util = 0;
     bool found = false;
     for (const auto& x : it->second)
@@ -281,6 +291,7 @@ class TargetLoadPacking : public TrimaranBase {
   double target_ = 40, multiplier_ = 1.5;
   int64_t default_milli_ = 1000;
   bool gpu_mode_ = false;
+  MType want_ = kTCPU;
 };
 
 // ------------------------------------------------ LoadVariationRiskBalancing ----
@@ -344,8 +355,9 @@ class LoadVariationRiskBalancing : public TrimaranBase {
     }
     req_cpu += p.overhead.get(kCPU);
     req_mem += p.overhead.get(kMemory);
-    double scores[3];
-    bool valid[3] = {false, false, false};
+    constexpr int kDims = 5;  // cpu, memory, GPU busy, HBM bandwidth, xGMI
+    double scores[kDims];
+    bool valid[kDims] = {false, false, false, false, false};
     double avg, sd;
     if (resource_data(it->second, kTCPU, &avg, &sd)) {
       ResourceStats rs;
@@ -366,24 +378,33 @@ class LoadVariationRiskBalancing : public TrimaranBase {
       scores[1] = rs.score(margin_, sensitivity_);
       valid[1] = true;
     }
+    // GPU dimensions: capacity = the node's GPUs, the pod's request = its
+    // GPUs (a GPU pod can drive its devices' engines, HBM and links fully).
     int gid = gpu_names().gpu_id();
-    if (p.limit_sum.get(gid) > 0 && resource_data(it->second, kTGPU, &avg, &sd)) {
+    auto gpu_dim = [&](MType type, int slot) {
+      if (!resource_data(it->second, type, &avg, &sd)) return;
       ResourceStats rs;
       rs.capacity = static_cast<double>(ni.node->allocatable.get(gid));
       rs.req = static_cast<double>(p.limit_sum.get(gid));
       rs.used_avg = avg * rs.capacity / 100;
       rs.used_std = sd * rs.capacity / 100;
-      scores[2] = rs.score(margin_, sensitivity_);
-      valid[2] = true;
+      scores[slot] = rs.score(margin_, sensitivity_);
+      valid[slot] = true;
+    };
+    if (p.limit_sum.get(gid) > 0) {
+      gpu_dim(kTGPU, 2);
+      gpu_dim(kTGPUMemoryBandwidth, 3);
+      if (!p.pod_group.empty()) gpu_dim(kTXGMI, 4);
     }
-    int n_valid = int(valid[0]) + int(valid[1]) + int(valid[2]);
+    int n_valid = 0;
+    for (int i = 0; i < kDims; ++i) n_valid += int(valid[i]);
     double total = 0;
     if (n_valid >= 2) {
       total = 1e300;
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < kDims; ++i)
         if (valid[i]) total = std::min(total, scores[i]);
     } else {
-      for (int i = 0; i < 3; ++i)
+      for (int i = 0; i < kDims; ++i)
         if (valid[i]) total = std::max(total, scores[i]);
     }
     return {static_cast<int64_t>(std::llround(total)), {}};

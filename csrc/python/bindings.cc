@@ -17,6 +17,7 @@
 #include "common/quantity.h"
 #include "scheduler/scheduler.h"
 #include "store/store.h"
+#include "telemetry/amdsmi_sampler.h"
 
 namespace py = pybind11;
 using namespace xsched;
@@ -230,6 +231,46 @@ PYBIND11_MODULE(_xsched, m) {
     return Registry::global().names();
   });
   m.def("json_roundtrip", [](const std::string& s) { return Json::parse(s).dump(); });
+  // ---- live MI355X telemetry (libamd_smi) ----
+  m.def("amdsmi_status", [] {
+    auto& smi = telemetry::AmdSmi::get();
+    py::gil_scoped_release nogil;
+    bool ok = smi.available();
+    py::gil_scoped_acquire gil;
+    return py::make_tuple(ok, smi.error());
+  });
+  m.def("amdsmi_sample", [] {
+    std::vector<telemetry::GpuSample> v;
+    {
+      py::gil_scoped_release nogil;
+      v = telemetry::AmdSmi::get().sample();
+    }
+    py::list out;
+    for (const auto& s : v) {
+      py::dict d;
+      d["index"] = s.index;
+      d["bdf"] = s.bdf;
+      d["gfx_activity"] = s.gfx_activity;
+      d["umc_activity"] = s.umc_activity;
+      d["mm_activity"] = s.mm_activity;
+      d["xcc_busy"] = s.xcc_busy;
+      d["vram_total_mb"] = s.vram_total_mb;
+      d["vram_used_mb"] = s.vram_used_mb;
+      d["socket_power_w"] = s.socket_power_w;
+      d["temp_hotspot_c"] = s.temp_hotspot_c;
+      d["temp_mem_c"] = s.temp_mem_c;
+      d["xgmi_read_kb"] = s.xgmi_read_kb;
+      d["xgmi_write_kb"] = s.xgmi_write_kb;
+      d["xgmi_link_up"] = s.xgmi_link_up;
+      d["xgmi_link_speed"] = s.xgmi_link_speed;
+      d["xgmi_link_width"] = s.xgmi_link_width;
+      d["vram_max_bandwidth_gbs"] = s.vram_max_bandwidth_gbs;
+      d["firmware_timestamp_10ns"] = s.firmware_timestamp_10ns;
+      d["num_partition"] = s.num_partition;
+      out.append(std::move(d));
+    }
+    return out;
+  });
   m.def("merge_patch", [](py::handle a, py::handle b) {
     Json x = json_arg(a);
     x.merge_patch(json_arg(b));

@@ -87,8 +87,11 @@ def build_core(verbose: bool = True) -> Path:
     import pybind11
 
     py_inc = sysconfig.get_paths()["include"]
-    includes = [str(CSRC), pybind11.get_include(), py_inc]
-    objs = build_objects(core_sources() + [CSRC / "python" / "bindings.cc"], BUILD / "core", [], includes)
+    # The amd-smi telemetry sampler compiles against the ROCm header and loads
+    # libamd_smi with dlopen at first use (no link-time dependency).
+    includes = [str(CSRC), pybind11.get_include(), py_inc, str(ROCM / "include")]
+    srcs = core_sources() + sorted((CSRC / "telemetry").glob("*.cc")) + [CSRC / "python" / "bindings.cc"]
+    objs = build_objects(srcs, BUILD / "core", [], includes)
     out = PKG / f"_xsched{_ext_suffix()}"
     newest = max(o.stat().st_mtime for o in objs)
     if not out.exists() or out.stat().st_mtime < newest:

@@ -149,8 +149,9 @@ def default_plugin_args(name: str, args: dict | None) -> dict:
                           "watcherAddress", "resourceType"})
         a.setdefault("defaultRequests", {"cpu": "1000m"})
         a["resourceType"] = a.get("resourceType") or "CPU"
-        if a["resourceType"] not in ("CPU", "GPU"):
-            raise ConfigError(f"{name}Args.resourceType must be CPU or GPU, got {a['resourceType']!r}")
+        if a["resourceType"] not in ("CPU", "GPU", "GPUMemoryBandwidth"):
+            raise ConfigError(f"{name}Args.resourceType must be CPU, GPU or GPUMemoryBandwidth, "
+                              f"got {a['resourceType']!r}")
         if a.get("defaultRequestsMultiplier") is None:
             a["defaultRequestsMultiplier"] = "1.5"
         if a.get("targetUtilization") is None or int(a["targetUtilization"]) <= 0:

@@ -7,12 +7,16 @@ AVG|STD|Latest, rollup, value %} over 15/10/5-minute windows, refreshed every
 minute from metrics-server/Prometheus/SignalFx, served at GET /watcher.
 
 Here each node agent samples its own host — CPU from /proc/stat, memory from
-/proc/meminfo, and per-GPU busy % and HBM used % from amdgpu sysfs
-(gpu_busy_percent, mem_info_vram_used/total) — keeps rolling windows, and
-publishes one WatcherMetrics document per node into the API store
+/proc/meminfo, and per-GPU counters from amd-smi (the native libamd_smi
+sampler, gpu/amdsmi.py: GFX and HBM-controller activity, VRAM, xGMI link
+traffic) or, without it, amdgpu sysfs (gpu_busy_percent,
+mem_info_vram_used/total) — keeps rolling windows, and publishes one
+WatcherMetrics document per node into the API store
 (`loadwatchermetrics/<node>`), which the C++ Trimaran plugins merge
-(csrc/plugins/trimaran.cc). GPU metric types extend the set: "GPU" (busy %)
-and "GPUMemory" (HBM used %). `LoadWatcherService` re-serves the cluster
+(csrc/plugins/trimaran.cc). GPU metric types extend the set: "GPU" (busy %),
+"GPUMemory" (HBM used %), and with amd-smi "GPUMemoryBandwidth" (HBM
+controller activity %) and "XGMI" (xGMI traffic as % of the up links'
+capacity). `LoadWatcherService` re-serves the cluster
 union at GET /watcher (+ ?host=, /watcher/health) for any consumer that
 speaks the original service mode, and `WatcherFetcher` does the reverse for a
 scheduler pointed at an external load-watcher (`watcherAddress`).
@@ -43,18 +47,38 @@ class Sample:
     memory: float | None = None
     gpu: float | None = None
     gpu_memory: float | None = None
+    hbm_bandwidth: float | None = None
+    xgmi: float | None = None
+
+
+def _mean(xs) -> float | None:
+    xs = [x for x in xs if x is not None]
+    return sum(xs) / len(xs) if xs else None
 
 
 class HostSampler:
-    """Reads utilisation percentages of the local host (or a sysfs root)."""
+    """Reads utilisation percentages of the local host (or a sysfs root).
 
-    def __init__(self, root: str = "/", cards: list[str] | None = None):
+    GPU counters come from amd-smi when it is usable on the live host
+    (`gpu_source="auto"` with root "/", or "amdsmi"; `smi` injects a sampler
+    for tests), else from amdgpu sysfs. `gpu_source` reports which."""
+
+    def __init__(self, root: str = "/", cards: list[str] | None = None, gpu_source: str = "auto", smi=None):
         self.root = root
         self._prev_cpu: tuple[int, int] | None = None
         if cards is None:
             from .discovery import discover_gpus
             cards = [g.card for g in discover_gpus(root)]
         self.cards = cards
+        self.smi = smi
+        if self.smi is None and (gpu_source == "amdsmi" or (gpu_source == "auto" and root == "/")):
+            from .amdsmi import AmdSmiSampler, native_status
+            ok, err = native_status()
+            if ok:
+                self.smi = AmdSmiSampler()
+            elif gpu_source == "amdsmi":
+                raise RuntimeError(f"amd-smi unavailable: {err}")
+        self.gpu_source = "amdsmi" if self.smi is not None else "sysfs"
 
     def _cpu(self) -> float | None:
         line = _read(os.path.join(self.root, "proc/stat")).splitlines()[:1]
@@ -90,11 +114,12 @@ class HostSampler:
         return out
 
     def sample(self) -> Sample:
+        if self.smi is not None:
+            cs = self.smi.sample()
+            return Sample(time.time(), self._cpu(), self._memory(), _mean(c.gfx for c in cs),
+                          _mean(c.vram_used_pct for c in cs), _mean(c.umc for c in cs), _mean(c.xgmi_pct for c in cs))
         gs = self.gpu_samples()
-        busy = [b for b, _ in gs if b is not None]
-        mem = [m for _, m in gs if m is not None]
-        return Sample(time.time(), self._cpu(), self._memory(), sum(busy) / len(busy) if busy else None,
-                      sum(mem) / len(mem) if mem else None)
+        return Sample(time.time(), self._cpu(), self._memory(), _mean(b for b, _ in gs), _mean(m for _, m in gs))
 
 
 class RollingWindow:
@@ -121,7 +146,8 @@ class RollingWindow:
         return mu, sd, vals[-1]
 
 
-_TYPES = (("cpu", "CPU"), ("memory", "Memory"), ("gpu", "GPU"), ("gpu_memory", "GPUMemory"))
+_TYPES = (("cpu", "CPU"), ("memory", "Memory"), ("gpu", "GPU"), ("gpu_memory", "GPUMemory"),
+          ("hbm_bandwidth", "GPUMemoryBandwidth"), ("xgmi", "XGMI"))
 
 
 class NodeTelemetry:

@@ -223,12 +223,21 @@ def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None) -> dict:
     from ..gpu.telemetry import HostSampler, NodeTelemetry, Sample, publish
     from ..control.client import LocalClient
 
-    live = []
+    live, hbm = [], []
+    source = "synthetic"
     try:
-        live = [b for b, _ in (sampler or HostSampler()).gpu_samples()]
-    except Exception:  # noqa: BLE001 - no amdgpu sysfs
+        hs = sampler or HostSampler()
+        if hs.smi is not None:
+            cs = hs.smi.sample()
+            live, hbm = [c.gfx for c in cs], [c.umc for c in cs]
+            source = "amd-smi (libamd_smi) gfx_activity / umc_activity"
+        else:
+            live = [b for b, _ in hs.gpu_samples()]
+            source = "amdgpu sysfs gpu_busy_percent"
+    except Exception:  # noqa: BLE001 - no amd-smi and no amdgpu sysfs
         live = []
-    source = "amdgpu sysfs gpu_busy_percent" if any(b is not None for b in live) else "synthetic"
+    if not any(b is not None for b in live):
+        source = "synthetic"
     busy = [(live[i % len(live)] if live and live[i % len(live)] is not None else (i * 13) % 100)
             for i in range(nodes)]
     store = Store()
@@ -236,7 +245,8 @@ def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None) -> dict:
     c = LocalClient(store)
     for i in range(nodes):
         t = NodeTelemetry(f"mi355x-{i}", source=source)
-        t.add(Sample(time.time(), None, None, float(busy[i]), None))
+        bw = hbm[i % len(hbm)] if hbm else None
+        t.add(Sample(time.time(), None, None, float(busy[i]), None, bw))
         publish(c, t.watcher_metrics())
     cfg = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
            "profiles": [{"schedulerName": "default-scheduler", "plugins": {
@@ -254,7 +264,7 @@ def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None) -> dict:
     finally:
         s.stop()
     return {"pods_per_s": round(pods / dt, 1) if ok else None, "metrics_source": source,
-            "node_gpu_busy_pct": busy, "first_gpu_pod_node": first.get("selected"),
+            "node_gpu_busy_pct": busy, "node_hbm_bandwidth_pct": [hbm[i % len(hbm)] for i in range(nodes)] if hbm else None, "first_gpu_pod_node": first.get("selected"),
             "tlp_scores": {n: v["TargetLoadPacking*1"] for n, v in (first.get("scores") or {}).items()}}
 
 

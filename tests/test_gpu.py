@@ -114,3 +114,28 @@ def test_mfma_peak_scales_with_xcds():
     # One XCD is an eighth of the chip (CPX partition budget).
     ratio = one["tflops"] / full["tflops"]
     assert 0.08 < ratio < 0.2, (one, full)
+
+
+def test_amdsmi_telemetry_sees_hbm_load():
+    """The native amd-smi sampler (csrc/telemetry/amdsmi_sampler.cc) reads the
+    live MI355X: 8 XCCs, 7 xGMI links up, idle near 0%, and a device copy
+    loop drives GFX and HBM-controller activity and power up."""
+    from flex_gpu_scheduler_amd.tools.amdsmi_probe import run
+
+    r = run(seconds=1.5)
+    assert r["available"], r
+    assert r["gpu0"]["xcc"] == 8 and r["gpu0"]["links_up"] >= 1, r
+    assert r["load"]["max_gfx"] >= 50 and r["load"]["max_umc"] >= 20, r
+    assert r["load"]["max_umc"] > r["idle"]["max_umc"] and r["load"]["max_power_w"] > r["idle"]["max_power_w"], r
+
+
+def test_node_agent_sampler_uses_amdsmi_on_the_box():
+    from flex_gpu_scheduler_amd.gpu.telemetry import HostSampler, NodeTelemetry
+
+    hs = HostSampler()
+    assert hs.gpu_source == "amdsmi"
+    nt = NodeTelemetry("box", hs)
+    nt.sample()
+    s = nt.sample()
+    assert s.gpu is not None and s.hbm_bandwidth is not None
+    assert {"GPU", "GPUMemory", "GPUMemoryBandwidth"} <= {m["type"] for m in nt.metrics()}
