@@ -294,14 +294,19 @@ bool Framework::filters_node_local(const Pod& p, const Snapshot& snap) const {
 }
 
 std::vector<char> Framework::local_scorers(const Pod& p, const Snapshot& snap) const {
-  std::vector<char> out(scorers_.size(), 0);
+  std::vector<char> out;
+  local_scorers(p, snap, out);
+  return out;
+}
+
+void Framework::local_scorers(const Pod& p, const Snapshot& snap, std::vector<char>& out) const {
+  out.assign(scorers_.size(), 0);
   bool any = false;
   for (size_t k = 0; k < scorers_.size(); ++k) {
     out[k] = scorers_[k].first->score_node_local(p, snap) ? 1 : 0;
     any = any || out[k];
   }
   if (!any) out.clear();
-  return out;
 }
 
 Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,

@@ -74,6 +74,7 @@ class Framework {
   bool filters_node_local(const Pod& p, const Snapshot& s) const;
   // Per scorer (scorer order): raw Score node-local for `p`? Empty if none is.
   std::vector<char> local_scorers(const Pod& p, const Snapshot& s) const;
+  void local_scorers(const Pod& p, const Snapshot& s, std::vector<char>& out) const;  // into a reused buffer
   Status run_reserve(CycleState& s, const PodPtr& p, const std::string& node);
   void run_unreserve(CycleState& s, const PodPtr& p, const std::string& node);
   // Returns Success, an unschedulable/error status, or Wait (then `on_done`

@@ -78,14 +78,15 @@ class StateData {
 // Pods the current cycle wants moved to activeQ (framework.PodsToActivate).
 struct PodsToActivate : StateData {
   std::mutex mu;
-  std::map<std::string, PodPtr> pods;  // "ns/name" -> pod
+  // Duplicates are harmless: activating a pod already in activeQ is a no-op.
+  std::vector<PodPtr> pods;
   std::shared_ptr<StateData> clone() const override { return nullptr; }  // shared, never cloned
 };
 inline constexpr const char* kPodsToActivateKey = "kubernetes.io/pods-to-activate";
 
 class CycleState {
  public:
-  CycleState() : version_(next_version()) {}
+  CycleState() : version_(next_version()) { kv_.reserve(8); }  // a cycle writes ~7 entries
   std::shared_ptr<StateData> read(std::string_view key) const;
   StateData* read_raw(std::string_view key) const;
   // Filter/Score run a plugin once per node on up to 16 threads against the

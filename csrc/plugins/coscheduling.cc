@@ -86,7 +86,7 @@ class Coscheduling : public Plugin {
   MicroTime creation(const QueuedPodInfo& q) const {
     if (q.sort_key_cache != INT64_MIN) return q.sort_key_cache;
     if (!q.pod->pod_group.empty())
-      if (auto pg = h_.informers->pod_group(q.pod->ns(), q.pod->pod_group)) {
+      if (auto pg = h_.informers->pod_group_of(*q.pod)) {
         q.sort_key_cache = pg->meta.creation;
         return q.sort_key_cache;
       }
@@ -117,7 +117,7 @@ class Coscheduling : public Plugin {
   // ---- PreFilter (core.go:149-196) ----
   Status pre_filter(CycleState&, const Pod& p) override {
     if (p.pod_group.empty()) return {};
-    auto pg = h_.informers->pod_group(p.ns(), p.pod_group);
+    auto pg = h_.informers->pod_group_of(p);
     if (!pg) return {};
     std::string full = p.pg_full_name();
     if (denied_.has(full))
@@ -181,7 +181,7 @@ class Coscheduling : public Plugin {
 
   // ---- PostFilter (coscheduling.go:140-176) ----
   std::pair<PostFilterResult, Status> post_filter(CycleState&, const Pod& p, const NodeStatusMap& m) override {
-    auto pg = p.pod_group.empty() ? nullptr : h_.informers->pod_group(p.ns(), p.pod_group);
+    auto pg = p.pod_group.empty() ? nullptr : h_.informers->pod_group_of(p);
     if (!pg) return {PostFilterResult{}, Status::unschedulable("can not find pod group")};
     // Deliberate deviation: when the cycle failed on this plugin's own
     // PreFilter (siblings not created yet, or group already denied) there is
@@ -214,7 +214,7 @@ class Coscheduling : public Plugin {
   // ---- Permit (coscheduling.go:184-216, core.go:199-216) ----
   std::pair<Status, int64_t> permit(CycleState& s, const PodPtr& p, const std::string&) override {
     if (p->pod_group.empty()) return {Status(), 0};
-    auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
+    auto pg = h_.informers->pod_group_of(*p);
     if (!pg) return {Status::unschedulable("PodGroup not found"), 0};
     // The cache already holds this (assumed) pod, so `assigned` includes it:
     // equivalent to the reference's snapshot count + 1.
@@ -236,14 +236,14 @@ class Coscheduling : public Plugin {
     auto pods = h_.informers->pods_in_group(p.ns(), p.pod_group);
     std::lock_guard<std::mutex> g(pta->mu);
     for (const auto& q : pods)
-      if (q->uid() != p.uid()) pta->pods[q->key()] = q;
+      if (q->uid() != p.uid()) pta->pods.push_back(q);
   }
 
   // ---- Reserve / Unreserve (coscheduling.go:219-237) ----
   Status reserve(CycleState&, const PodPtr&, const std::string&) override { return {}; }
   void unreserve(CycleState&, const PodPtr& p, const std::string&) override {
     if (p->pod_group.empty()) return;
-    auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
+    auto pg = h_.informers->pod_group_of(*p);
     if (!pg) return;
     reject_group(*p, "rejection in Unreserve");
     denied_.add(p->pg_full_name(), denied_ttl_us_);
@@ -253,7 +253,7 @@ class Coscheduling : public Plugin {
   // ---- PostBind (core.go:220-252) ----
   void post_bind(CycleState&, const PodPtr& p, const std::string&) override {
     if (p->pod_group.empty()) return;
-    auto pg = h_.informers->pod_group(p->ns(), p->pod_group);
+    auto pg = h_.informers->pod_group_of(*p);
     if (!pg) return;
     // Deliberate fix: the reference increments the lister's status.scheduled,
     // which is only written back on a phase change (core.go:220-252), so the

@@ -280,7 +280,7 @@ class TopologyMatch : public Plugin {
     if (strategy_ != Strategy::XGMI) return {};
     auto ctx = std::make_shared<GangCtx>();
     if (!p.pod_group.empty()) {
-      auto pg = h_.informers->pod_group(p.ns(), p.pod_group);
+      auto pg = h_.informers->pod_group_of(p);
       const GpuDemand& d = p.gpu_demand;
       if (pg && pg->min_member > 1 && d.amount > 0 && (d.kind == GpuDemand::Gpu || d.kind == GpuDemand::Xcd)) {
         ctx->gang = true;

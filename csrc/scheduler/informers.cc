@@ -4,46 +4,47 @@
 
 namespace xsched {
 
-namespace {
-std::string group_key(const std::string& ns, const std::string& pg) { return ns + "/" + pg; }
-}  // namespace
+void Informers::group_remove(const PodPtr& p) {
+  auto git = pods_by_group_.find(p->pg_key);
+  if (git == pods_by_group_.end()) return;
+  auto& v = git->second;
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i] == p) {
+      v[i] = std::move(v.back());
+      v.pop_back();
+      break;
+    }
+  if (v.empty()) pods_by_group_.erase(git);
+}
 
 void Informers::upsert_pod(const PodPtr& p) {
   std::unique_lock<std::shared_mutex> g(mu_);
-  std::string key = p->key();
-  auto it = pods_.find(key);
-  if (it != pods_.end() && !it->second->pod_group.empty() && it->second->pod_group != p->pod_group) {
-    auto git = pods_by_group_.find(group_key(p->ns(), it->second->pod_group));
-    if (git != pods_by_group_.end()) {
-      git->second.erase(key);
-      if (git->second.empty()) pods_by_group_.erase(git);
-    }
+  auto [it, fresh] = pods_.try_emplace(p->key(), p);
+  if (!fresh) {
+    if (it->second->pg_key) group_remove(it->second);
+    it->second = p;
   }
-  pods_[key] = p;
-  if (!p->pod_group.empty()) pods_by_group_[group_key(p->ns(), p->pod_group)].insert(key);
+  if (p->pg_key) pods_by_group_[p->pg_key].push_back(p);
 }
 
 void Informers::delete_pod(const Pod& p) {
   std::unique_lock<std::shared_mutex> g(mu_);
-  std::string key = p.key();
-  auto it = pods_.find(key);
+  auto it = pods_.find(p.key());
   if (it == pods_.end()) return;
-  if (!it->second->pod_group.empty()) {
-    auto git = pods_by_group_.find(group_key(p.ns(), it->second->pod_group));
-    if (git != pods_by_group_.end()) {
-      git->second.erase(key);
-      if (git->second.empty()) pods_by_group_.erase(git);
-    }
-  }
+  if (it->second->pg_key) group_remove(it->second);
   pods_.erase(it);
 }
 
 void Informers::upsert_pod_group(const PodGroupPtr& pg) {
   std::unique_lock<std::shared_mutex> g(mu_);
-  pgs_[pg->meta.key()] = pg;
+  std::string key = pg->meta.key();
+  pgs_by_key_[pg_key_of(key)] = pg;
+  pgs_[std::move(key)] = pg;
 }
 void Informers::delete_pod_group(const std::string& key) {
   std::unique_lock<std::shared_mutex> g(mu_);
+  auto it = pgs_by_key_.find(pg_key_of(key));
+  if (it != pgs_by_key_.end() && it->second->meta.key() == key) pgs_by_key_.erase(it);
   pgs_.erase(key);
 }
 void Informers::upsert_elastic_quota(const ElasticQuotaPtr& eq) {
@@ -85,23 +86,36 @@ PodPtr Informers::pod(const std::string& ns, const std::string& name) const {
   return it == pods_.end() ? nullptr : it->second;
 }
 
+namespace {
+uint64_t group_hash(const std::string& ns, const std::string& pg) {
+  std::string full;
+  full.reserve(ns.size() + 1 + pg.size());
+  full.append(ns).push_back('/');
+  full.append(pg);
+  return pg_key_of(full);
+}
+}  // namespace
+
 std::vector<PodPtr> Informers::pods_in_group(const std::string& ns, const std::string& pg) const {
   std::vector<PodPtr> out;
+  const uint64_t key = group_hash(ns, pg);
   std::shared_lock<std::shared_mutex> g(mu_);
-  auto git = pods_by_group_.find(group_key(ns, pg));
+  auto git = pods_by_group_.find(key);
   if (git == pods_by_group_.end()) return out;
   out.reserve(git->second.size());
-  for (const auto& k : git->second) {
-    auto it = pods_.find(k);
-    if (it != pods_.end()) out.push_back(it->second);
-  }
+  for (const auto& p : git->second)
+    if (p->pod_group == pg && p->ns() == ns) out.push_back(p);
   return out;
 }
 
 size_t Informers::count_pods_in_group(const std::string& ns, const std::string& pg) const {
+  const uint64_t key = group_hash(ns, pg);
   std::shared_lock<std::shared_mutex> g(mu_);
-  auto git = pods_by_group_.find(group_key(ns, pg));
-  return git == pods_by_group_.end() ? 0 : git->second.size();
+  auto git = pods_by_group_.find(key);
+  if (git == pods_by_group_.end()) return 0;
+  size_t n = 0;
+  for (const auto& p : git->second) n += p->pod_group == pg && p->ns() == ns;
+  return n;
 }
 
 std::vector<PodPtr> Informers::all_pods() const {
@@ -121,6 +135,18 @@ PodGroupPtr Informers::pod_group(const std::string& ns, const std::string& name)
   std::shared_lock<std::shared_mutex> g(mu_);
   auto it = pgs_.find(ns + "/" + name);
   return it == pgs_.end() ? nullptr : it->second;
+}
+
+PodGroupPtr Informers::pod_group_of(const Pod& p) const {
+  if (!p.pg_key) return nullptr;
+  {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    auto it = pgs_by_key_.find(p.pg_key);
+    if (it != pgs_by_key_.end() && it->second->meta.name == p.pod_group && it->second->meta.ns == p.ns())
+      return it->second;
+    if (it == pgs_by_key_.end()) return nullptr;
+  }
+  return pod_group(p.ns(), p.pod_group);  // hash collision: exact lookup
 }
 
 std::vector<PodGroupPtr> Informers::pod_groups() const {

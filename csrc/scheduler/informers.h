@@ -42,6 +42,9 @@ class Informers {
   size_t count_pods_in_group(const std::string& ns, const std::string& pg) const;
   std::vector<PodPtr> all_pods() const;
   PodGroupPtr pod_group(const std::string& ns, const std::string& name) const;
+  // The PodGroup named by p's group label, looked up by p.pg_key (no string
+  // building on the scheduling path).
+  PodGroupPtr pod_group_of(const Pod& p) const;
   std::vector<PodGroupPtr> pod_groups() const;
   ElasticQuotaPtr elastic_quota_for_namespace(const std::string& ns) const;
   std::vector<ElasticQuotaPtr> elastic_quotas() const;
@@ -53,8 +56,12 @@ class Informers {
  private:
   mutable std::shared_mutex mu_;
   std::unordered_map<std::string, PodPtr> pods_;  // ns/name
-  std::unordered_map<std::string, std::unordered_set<std::string>> pods_by_group_;  // ns/pg -> {ns/name}
+  // PodGroup members by Pod::pg_key (64-bit hash of "ns/pg"). Readers still
+  // compare namespace and group name, so a hash collision cannot mix groups.
+  std::unordered_map<uint64_t, std::vector<PodPtr>> pods_by_group_;
   std::unordered_map<std::string, PodGroupPtr> pgs_;
+  std::unordered_map<uint64_t, PodGroupPtr> pgs_by_key_;  // same objects, keyed by pg_key_of("ns/name")
+  void group_remove(const PodPtr& p);
   std::map<std::string, ElasticQuotaPtr> eqs_;  // ordered: "first listed wins"
   std::unordered_map<std::string, NRTPtr> nrts_;
   std::unordered_map<std::string, PDBPtr> pdbs_;

@@ -191,12 +191,12 @@ void SchedulingQueue::add(const PodPtr& p) {
   cv_.notify_one();
 }
 
-void SchedulingQueue::activate(const std::map<std::string, PodPtr>& pods) {
+void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
   bool moved = false;
   {
     std::lock_guard<std::mutex> g(mu_);
-    for (const auto& kv : pods) {
-      const std::string& uid = kv.second->uid();
+    for (const auto& pod : pods) {
+      const std::string& uid = pod->uid();
       if (active_.contains(uid)) continue;
       QueuedPodInfoPtr q;
       auto it = unschedulable_.find(uid);

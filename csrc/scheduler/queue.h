@@ -80,7 +80,7 @@ class SchedulingQueue {
   void set_cluster_event_map(std::vector<std::pair<ClusterEvent, std::set<std::string>>> m);
 
   void add(const PodPtr& p);
-  void activate(const std::map<std::string, PodPtr>& pods);
+  void activate(const std::vector<PodPtr>& pods);
   // Returns false if the pod is already queued (active/backoff).
   bool add_unschedulable_if_not_present(const QueuedPodInfoPtr& p, int64_t pod_scheduling_cycle);
   int64_t scheduling_cycle() const;

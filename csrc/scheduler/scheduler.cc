@@ -464,9 +464,10 @@ void Scheduler::apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr 
       // in unschedulableQ/backoffQ (targeted form of the Pod/Add cluster
       // event Coscheduling registers; O(group size), not O(queue)).
       if (!np->pod_group.empty()) {
-        std::map<std::string, PodPtr> sib;
-        for (const auto& q : informers_->pods_in_group(np->ns(), np->pod_group))
-          if (q->uid() != np->uid() && q->node_name.empty()) sib[q->key()] = q;
+        std::vector<PodPtr> sib = informers_->pods_in_group(np->ns(), np->pod_group);
+        sib.erase(std::remove_if(sib.begin(), sib.end(),
+                                 [&](const PodPtr& q) { return q->uid() == np->uid() || !q->node_name.empty(); }),
+                  sib.end());
         if (!sib.empty()) queue_->activate(sib);
       }
     }
@@ -530,7 +531,7 @@ void Scheduler::note_gang_enqueue(const Pod& p, int64_t t) {
 
 void Scheduler::note_gang_event(const Pod& p, bool bound) {
   if (p.pod_group.empty()) return;
-  auto pg = informers_->pod_group(p.ns(), p.pod_group);
+  auto pg = informers_->pod_group_of(p);
   if (!pg) return;
   int need = std::max(1, pg->min_member);
   std::lock_guard<std::mutex> g(stats_mu_);
@@ -841,6 +842,7 @@ Scheduler::CycleMetrics& Scheduler::cycle_metrics(const Framework& fw) {
   if (m.epoch != e) {
     static const char* kResults[3] = {"scheduled", "unschedulable", "error"};
     m.algo = &metrics_->histogram("scheduler_scheduling_algorithm_duration_seconds", "");
+    m.e2e = &metrics_->histogram("scheduler_e2e_scheduling_duration_seconds", "profile=\"" + fw.profile_name() + "\"");
     for (int i = 0; i < 3; ++i) {
       std::string labels = "profile=\"" + fw.profile_name() + "\",result=\"" + kResults[i] + "\"";
       m.attempt[i] = &metrics_->histogram("scheduler_scheduling_attempt_duration_seconds", labels);
@@ -906,8 +908,9 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         st = Status();
       } else {
         st = fw->run_pre_score(*state, *pod, feasible);
-        EqScoreCache esc;
-        if (eq) esc.local = fw->local_scorers(*pod, snapshot_);
+        EqScoreCache& esc = esc_buf_;
+        esc.local.clear();
+        if (eq) fw->local_scorers(*pod, snapshot_, esc.local);
         if (!esc.local.empty()) {
           esc.slots.resize(feasible.size());
           for (size_t i = 0; i < feasible.size(); ++i) esc.slots[i] = &eq->slots[feasible_pos_buf_[i]];
@@ -975,13 +978,20 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   // Permit.
   int64_t permit_start = clock_->now_us();
   inflight_.fetch_add(1);
-  auto self = this;
-  Status pst = fw->run_permit(*state, assumed, host,
-                              [self, fw, state, qpi, assumed, host, cycle, permit_start, to_activate](const Status& wst) {
-                                self->binder_->submit([=] {
-                                  self->binding_cycle(fw, state, qpi, assumed, host, cycle, wst, permit_start, to_activate);
-                                });
-                              });
+  auto task = std::make_shared<BindTask>();
+  task->self = this;
+  task->fw = fw;
+  task->state = state;
+  task->qpi = qpi;
+  task->assumed = assumed;
+  task->host = host;
+  task->cycle = cycle;
+  task->permit_start_us = permit_start;
+  task->to_activate = to_activate;
+  task->e2e = cycle_metrics(*fw).e2e;
+  Status pst = fw->run_permit(*state, assumed, host, [task](const Status& wst) {
+    task->self->binder_->submit([task, wst] { task->self->binding_cycle(*task, wst); });
+  });
   if (!pst.is_success() && !pst.is_wait()) {
     inflight_.fetch_sub(1);
     fw->run_unreserve(*state, assumed, host);
@@ -998,7 +1008,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   if (pst.is_success()) note_gang_event(*assumed, false);
   // Activate siblings stashed by plugins (scheduler.go:543-548).
   {
-    std::map<std::string, PodPtr> act;
+    std::vector<PodPtr> act;
     {
       std::lock_guard<std::mutex> g(to_activate->mu);
       act.swap(to_activate->pods);
@@ -1012,7 +1022,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     ++stats_.scheduled;
   }
   if (pst.is_success()) {
-    binder_->submit([=] { binding_cycle(fw, state, qpi, assumed, host, cycle, Status(), permit_start, to_activate); });
+    binder_->submit([task = std::move(task)] { task->self->binding_cycle(*task, Status()); });
   }
   if (tracer_.enabled()) {
     int64_t t_end = clock_->now_us();
@@ -1133,9 +1143,14 @@ Scheduler::BindMetrics& Scheduler::bind_metrics() {
   return m;
 }
 
-void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
-                              int64_t cycle, Status permit_status, int64_t wait_start_us,
-                              std::shared_ptr<PodsToActivate> to_activate) {
+void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
+  Framework* fw = t.fw;
+  const CycleStatePtr& s = t.state;
+  const QueuedPodInfoPtr& qpi = t.qpi;
+  const PodPtr& assumed = t.assumed;
+  const std::string& host = t.host;
+  const int64_t cycle = t.cycle, wait_start_us = t.permit_start_us;
+  const std::shared_ptr<PodsToActivate>& to_activate = t.to_activate;
   int64_t t0 = clock_->now_us();
   auto fail = [&](const Status& st, const std::string& reason) {
     fw->run_unreserve(*s, assumed, host);
@@ -1176,8 +1191,7 @@ void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr q
   cache_->finish_binding(*assumed);
   int64_t t1 = clock_->now_us();
   bm.binding.load(std::memory_order_relaxed)->observe(static_cast<double>(t1 - t0) / 1e6);
-  metrics_->histogram("scheduler_e2e_scheduling_duration_seconds", "profile=\"" + fw->profile_name() + "\"")
-      .observe(static_cast<double>(t1 - qpi->timestamp_us) / 1e6);
+  t.e2e->observe(static_cast<double>(t1 - qpi->timestamp_us) / 1e6);
   Histogram* pd = qpi->attempts >= 1 && qpi->attempts <= 8
                       ? bm.pod_duration[qpi->attempts - 1].load(std::memory_order_relaxed)
                       : &metrics_->histogram("scheduler_pod_scheduling_duration_seconds",
@@ -1192,7 +1206,7 @@ void Scheduler::binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr q
   }
   note_gang_event(*assumed, true);
   {
-    std::map<std::string, PodPtr> act;
+    std::vector<PodPtr> act;
     {
       std::lock_guard<std::mutex> g(to_activate->mu);
       act.swap(to_activate->pods);

@@ -177,6 +177,7 @@ class Scheduler {
   struct CycleMetrics {
     uint64_t epoch = ~0ULL;
     Histogram* algo = nullptr;
+    Histogram* e2e = nullptr;
     Histogram* attempt[3] = {};  // scheduled, unschedulable, error
     Counter* attempts[3] = {};
   };
@@ -216,9 +217,23 @@ class Scheduler {
   std::vector<int> found_pos_buf_;
   std::vector<int> feasible_pos_buf_;
   std::vector<NodeScore> scores_buf_;
-  void binding_cycle(Framework* fw, CycleStatePtr s, QueuedPodInfoPtr qpi, PodPtr assumed, std::string host,
-                     int64_t cycle, Status permit_status, int64_t wait_start_us,
-                     std::shared_ptr<PodsToActivate> to_activate);
+  EqScoreCache esc_buf_;
+  // Everything the binding cycle of one assumed pod needs, in one heap
+  // object: the Permit continuation and the binder task capture only this
+  // pointer (fits std::function's inline buffer, no per-closure allocation).
+  struct BindTask {
+    Scheduler* self = nullptr;
+    Framework* fw = nullptr;
+    CycleStatePtr state;
+    QueuedPodInfoPtr qpi;
+    PodPtr assumed;
+    std::string host;
+    int64_t cycle = 0;
+    int64_t permit_start_us = 0;
+    std::shared_ptr<PodsToActivate> to_activate;
+    Histogram* e2e = nullptr;  // scheduler_e2e_scheduling_duration_seconds{profile}
+  };
+  void binding_cycle(const BindTask& t, const Status& permit_status);
   void handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const Status& st, const std::string& reason,
                       const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins);
   void note_gang_enqueue(const Pod& p, int64_t t);
