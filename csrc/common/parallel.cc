@@ -103,7 +103,6 @@ void Parallelizer::record_inline(ParallelSite* site, int64_t elapsed_ns, int don
 void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop,
                          ParallelSite* site) {
   if (n <= 0) return;
-  int helpers = std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1);
   if (plan_inline(n, site)) {
     int64_t t0 = site ? now_ns() : 0;
     int done = 0;
@@ -115,6 +114,12 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
     if (site) record_inline(site, now_ns() - t0, done, n);
     return;
   }
+  until_forked(n, fn, stop, site);
+}
+
+void Parallelizer::until_forked(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop,
+                                ParallelSite* site) {
+  int helpers = std::max(1, std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1));
   std::lock_guard<std::mutex> call(call_mu_);
   Job job;
   job.fn = &fn;

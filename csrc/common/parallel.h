@@ -52,6 +52,9 @@ class Parallelizer {
   // atomics a parallel run needs) and report it with `record_inline`.
   // Counts as a call of the site (advances its probe cadence).
   bool plan_inline(int n, ParallelSite* site);
+  // The fork/join half of `until`, for a caller that already got
+  // plan_inline() == false (records the site's done fraction, no re-planning).
+  void until_forked(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop, ParallelSite* site);
   static void record_inline(ParallelSite* site, int64_t elapsed_ns, int done, int n);
   static int64_t now_ns();
   int workers() const { return workers_; }

@@ -316,7 +316,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
   total.resize(n);
   for (size_t i = 0; i < n; ++i) total[i].score = 0;
   if (breakdown)
-    for (size_t i = 0; i < n; ++i) total[i].name = nodes[i]->name();
+    for (size_t i = 0; i < n; ++i) total[i].name = &nodes[i]->name();
   if (scorers_.empty()) return {};
   // Per-plugin score rows are reused across cycles (no allocation or string
   // construction per plugin x node in steady state); every cell is written
@@ -339,13 +339,15 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
   std::atomic<bool> failed{false};
   std::string err;
   std::mutex err_mu;
-  // Node-parallel scoring: one task per node runs every score plugin.
-  handle_.parallelizer->until(static_cast<int>(n), [&](int i) {
+  const size_t ns = scorers_.size();
+  // One node: every score plugin (raw scores; normalizers read the rows).
+  auto score_node = [&](size_t i) {
     // Equivalence cache: node-local raw scores of this pod template on an
     // unchanged node are reused; the others are recomputed.
     EqSlot* slot = eq ? eq->slots[i] : nullptr;
-    const bool hit = slot && slot->score_gen == nodes[i]->generation && slot->raw.size() == scorers_.size();
-    for (size_t k = 0; k < scorers_.size(); ++k) {
+    const NodeInfo& ni = *nodes[i];
+    const bool hit = slot && slot->score_gen == ni.generation && slot->raw.size() == ns;
+    for (size_t k = 0; k < ns; ++k) {
       if (skip[k]) {
         per[k][i].score = 0;
         continue;
@@ -354,21 +356,30 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
         per[k][i].score = slot->raw[k];
         continue;
       }
-      auto [sc, st] = scorers_[k].first->score(s, p, *nodes[i]);
+      auto [sc, st] = scorers_[k].first->score(s, p, ni);
       if (!st.is_success()) {
         std::lock_guard<std::mutex> g(err_mu);
         err = "running Score plugin " + scorers_[k].first->name() + ": " + st.message();
         failed.store(true);
         return;
       }
-      per[k][i].score = sc;  // names live in `total` only (normalizers use scores)
+      per[k][i].score = sc;
     }
     if (slot && !hit) {
-      slot->raw.resize(scorers_.size());
-      for (size_t k = 0; k < scorers_.size(); ++k) slot->raw[k] = per[k][i].score;
-      slot->score_gen = nodes[i]->generation;
+      slot->raw.resize(ns);
+      for (size_t k = 0; k < ns; ++k) slot->raw[k] = per[k][i].score;
+      slot->score_gen = ni.generation;
     }
-  }, &failed, &score_site_);
+  };
+  if (handle_.parallelizer->plan_inline(static_cast<int>(n), &score_site_)) {
+    // Serial path: a plain loop, no std::function dispatch per node.
+    const int64_t s0 = Parallelizer::now_ns();
+    for (size_t i = 0; i < n && !failed.load(std::memory_order_relaxed); ++i) score_node(i);
+    Parallelizer::record_inline(&score_site_, Parallelizer::now_ns() - s0, static_cast<int>(n), static_cast<int>(n));
+  } else {
+    handle_.parallelizer->until_forked(static_cast<int>(n), [&](int i) { score_node(static_cast<size_t>(i)); },
+                                       &failed, &score_site_);
+  }
   if (failed.load()) return Status(Code::Error, err);
   for (size_t k = 0; k < scorers_.size(); ++k) {
     if (skip[k]) {
@@ -379,7 +390,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
     auto& pl = scorers_[k].first;
     if (pl->has_normalize_score()) {
       if (pl->normalize_uses_names())
-        for (size_t i = 0; i < n; ++i) per[k][i].name = nodes[i]->name();
+        for (size_t i = 0; i < n; ++i) per[k][i].name = &nodes[i]->name();
       Status st = pl->normalize_score(s, p, per[k]);
       if (!st.is_success()) return Status(Code::Error, "running Normalize on Score plugin " + pl->name() + ": " + st.message());
     }

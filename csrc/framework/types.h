@@ -266,8 +266,12 @@ struct ClusterEvent {
   }
 };
 
+// One node's score in a plugin row or the total row. `name` points at the
+// NodeInfo's node name (stable for the cycle) and is set only where a reader
+// needs it (explain, normalizers that declare normalize_uses_names), so a
+// row is 16 trivially-copyable bytes per node.
 struct NodeScore {
-  std::string name;
+  const std::string* name = nullptr;
   int64_t score = 0;
 };
 inline constexpr int64_t kMaxNodeScore = 100;

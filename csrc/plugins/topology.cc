@@ -249,7 +249,7 @@ class PodTopologySpread : public Plugin {
     int64_t lo = INT64_MAX, hi = 0;
     std::vector<char> invalid(scores.size(), 0);
     for (size_t i = 0; i < scores.size(); ++i) {
-      if (st->ignored.count(scores[i].name)) {
+      if (scores[i].name && st->ignored.count(*scores[i].name)) {
         invalid[i] = 1;
         continue;
       }

@@ -736,7 +736,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     std::atomic<bool> stop{false};
     std::atomic<uint64_t> ahits{0};
     std::mutex mu;
-    parallelizer_->until(n, [&](int i) {
+    parallelizer_->until_forked(n, [&](int i) {
       const int pos = (start + i) % n;
       const NodeInfo& ni = *all[pos];
       Status own;
