@@ -17,6 +17,8 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <atomic>
+
 #include "framework/plugin.h"
 #include "framework/waiting_pods.h"
 #include "scheduler/cache.h"
@@ -25,37 +27,47 @@
 namespace xsched {
 namespace {
 
+// go-cache style TTL set of PodGroups (core.go:103-104: lastDeniedPG,
+// permittedPG), keyed by Pod::pg_key. `has` on an empty set (the common case:
+// no group denied) is one atomic load, no lock.
 class TTLSet {
  public:
   explicit TTLSet(std::shared_ptr<Clock> c) : clock_(std::move(c)) {}
-  void add(const std::string& k, int64_t ttl_us) {
+  void add(uint64_t k, int64_t ttl_us) {
     std::lock_guard<std::mutex> g(mu_);
     m_[k] = clock_->now_us() + ttl_us;
+    size_.store(m_.size(), std::memory_order_release);
   }
-  bool has(const std::string& k) {
+  bool has(uint64_t k) {
+    if (size_.load(std::memory_order_acquire) == 0) return false;
     std::lock_guard<std::mutex> g(mu_);
     auto it = m_.find(k);
     if (it == m_.end()) return false;
     if (clock_->now_us() >= it->second) {
       m_.erase(it);
+      size_.store(m_.size(), std::memory_order_release);
       return false;
     }
     return true;
   }
-  void erase(const std::string& k) {
+  void erase(uint64_t k) {
+    if (size_.load(std::memory_order_acquire) == 0) return;
     std::lock_guard<std::mutex> g(mu_);
     m_.erase(k);
+    size_.store(m_.size(), std::memory_order_release);
   }
   void sweep() {
     std::lock_guard<std::mutex> g(mu_);
     int64_t now = clock_->now_us();
     for (auto it = m_.begin(); it != m_.end();) it = now >= it->second ? m_.erase(it) : std::next(it);
+    size_.store(m_.size(), std::memory_order_release);
   }
 
  private:
   std::shared_ptr<Clock> clock_;
   std::mutex mu_;
-  std::unordered_map<std::string, int64_t> m_;
+  std::unordered_map<uint64_t, int64_t> m_;
+  std::atomic<size_t> size_{0};
 };
 
 class Coscheduling : public Plugin {
@@ -119,29 +131,28 @@ class Coscheduling : public Plugin {
     if (p.pod_group.empty()) return {};
     auto pg = h_.informers->pod_group_of(p);
     if (!pg) return {};
-    std::string full = p.pg_full_name();
-    if (denied_.has(full))
-      return Status::unresolvable("pod with pgName: " + full + " last failed in " +
+    if (denied_.has(p.pg_key))
+      return Status::unresolvable("pod with pgName: " + p.pg_full_name() + " last failed in " +
                                   std::to_string(denied_ttl_us_ / 1000000) + "s, deny");
-    size_t n = h_.informers->count_pods_in_group(p.ns(), p.pod_group);
+    size_t n = h_.informers->count_pods_in_group_of(p);
     if (static_cast<int64_t>(n) < pg->min_member)
       return Status::unresolvable("pre-filter pod " + p.name() + " cannot find enough sibling pods, current pods number: " +
                                   std::to_string(n) + ", minMember of group: " + std::to_string(pg->min_member));
     if (!pg->has_min_resources) return {};
-    if (permitted_.has(full)) return {};
+    if (permitted_.has(p.pg_key)) return {};
     Res need = pg->min_resources;
     need.set(kPods, pg->min_member);
-    if (!check_cluster_resource(need, full)) {
-      denied_.add(full, denied_ttl_us_);
-      return Status::unresolvable("resource gap for PodGroup " + full);
+    if (!check_cluster_resource(need, p)) {
+      denied_.add(p.pg_key, denied_ttl_us_);
+      return Status::unresolvable("resource gap for PodGroup " + p.pg_full_name());
     }
-    permitted_.add(full, wait_time(*pg));
+    permitted_.add(p.pg_key, wait_time(*pg));
     return {};
   }
 
   // CheckClusterResource (core.go:322-382): greedily subtract each node's
   // free resources (with this group's own pods counted as free).
-  bool check_cluster_resource(Res need, const std::string& full) const {
+  bool check_cluster_resource(Res need, const Pod& member) const {
     if (!h_.snapshot) return false;
     for (const auto& ni : h_.snapshot->nodes) {
       if (!ni->node) continue;
@@ -149,7 +160,7 @@ class Coscheduling : public Plugin {
       Res requested = ni->requested;
       int64_t pods = ni->num_pods();
       for (const auto& q : ni->pods)
-        if (q->pg_full_name() == full) {
+        if (q->pg_key == member.pg_key && q->pod_group == member.pod_group && q->ns() == member.ns()) {
           requested -= q->request;
           --pods;
         }
@@ -195,8 +206,8 @@ class Coscheduling : public Plugin {
     float gap = static_cast<float>(pg->min_member - assigned) / static_cast<float>(std::max(1, pg->min_member));
     if (gap <= 0.1f) return {PostFilterResult{}, Status(Code::Unschedulable)};
     reject_group(p, "optimistic rejection in PostFilter");
-    denied_.add(full, denied_ttl_us_);
-    permitted_.erase(full);
+    denied_.add(p.pg_key, denied_ttl_us_);
+    permitted_.erase(p.pg_key);
     return {PostFilterResult{},
             Status::unschedulable("PodGroup " + full + " gets rejected due to Pod " + p.name() +
                                   " is unschedulable even after PostFilter")};
@@ -233,7 +244,7 @@ class Coscheduling : public Plugin {
   void activate_siblings(const Pod& p, CycleState& s) {
     auto* pta = s.read_as<PodsToActivate>(kPodsToActivateKey);
     if (!pta) return;
-    auto pods = h_.informers->pods_in_group(p.ns(), p.pod_group);
+    auto pods = h_.informers->pods_in_group_of(p);
     std::lock_guard<std::mutex> g(pta->mu);
     for (const auto& q : pods)
       if (q->uid() != p.uid()) pta->pods.push_back(q);
@@ -246,8 +257,8 @@ class Coscheduling : public Plugin {
     auto pg = h_.informers->pod_group_of(*p);
     if (!pg) return;
     reject_group(*p, "rejection in Unreserve");
-    denied_.add(p->pg_full_name(), denied_ttl_us_);
-    permitted_.erase(p->pg_full_name());
+    denied_.add(p->pg_key, denied_ttl_us_);
+    permitted_.erase(p->pg_key);
   }
 
   // ---- PostBind (core.go:220-252) ----

@@ -40,8 +40,7 @@ using NumaNode = NumaZone;
 // Per-cycle gang facts for XGMIGangAffinity, computed once in PreScore.
 struct GangCtx : StateData {
   bool gang = false;
-  std::string full;         // ns/pg
-  uint64_t key = 0;         // pg_key_of(full)
+  uint64_t key = 0;         // Pod::pg_key of the gang
   int64_t remaining = 0;    // members still to place (>= 1)
   enum { kWhole, kXcd } kind = kWhole;
   int64_t amount = 0;       // per member: GPUs or XCDs
@@ -284,7 +283,6 @@ class TopologyMatch : public Plugin {
       const GpuDemand& d = p.gpu_demand;
       if (pg && pg->min_member > 1 && d.amount > 0 && (d.kind == GpuDemand::Gpu || d.kind == GpuDemand::Xcd)) {
         ctx->gang = true;
-        ctx->full = p.pg_full_name();
         ctx->key = p.pg_key;
         ctx->remaining = std::max<int64_t>(1, pg->min_member - h_.cache->assigned_in_group(ctx->key));
         ctx->kind = d.kind == GpuDemand::Gpu ? GangCtx::kWhole : GangCtx::kXcd;

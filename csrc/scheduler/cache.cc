@@ -19,7 +19,7 @@ NodeInfoPtr& SchedulerCache::info_for(const std::string& node) {
 // copy happens on the mutating thread (informer, binder, assume) and never
 // while the scheduling thread refreshes its snapshot.
 NodeInfo& SchedulerCache::writable(NodeInfoPtr& slot) {
-  if (slot.use_count() > 1) slot = slot->clone();
+  if (!in_place_ && slot.use_count() > 1) slot = slot->clone();
   return *slot;
 }
 
@@ -31,6 +31,7 @@ void SchedulerCache::mark_dirty(const std::string& node) {
 
 void SchedulerCache::group_delta(const Pod& p, int d) {
   if (!p.pg_key) return;
+  std::lock_guard<std::mutex> g(group_mu_);
   auto it = group_assigned_.try_emplace(p.pg_key, 0).first;
   it->second += d;
   if (it->second <= 0) group_assigned_.erase(it);
@@ -130,7 +131,9 @@ void SchedulerCache::remove_pod_locked(const Pod& p) {
 Status SchedulerCache::assume_pod(const PodPtr& p) {
   std::lock_guard<std::mutex> g(mu_);
   if (pod_states_.count(p->uid())) return Status::error("pod " + p->key() + " is in the cache, so can't be assumed");
+  in_place_ = true;
   add_pod_locked(p);
+  in_place_ = false;
   pod_states_[p->uid()] = PodState{p, 0, false};
   assumed_.insert(p->uid());
   return {};
@@ -239,22 +242,26 @@ PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::f
     auto nit = nodes_.find(it->second.pod->node_name);
     if (assumed_.count(uid) && !it->second.binding_finished && nit != nodes_.end()) {
       PodPtr pod = it->second.pod;
+      in_place_ = true;  // scheduling thread, same cycle as assume_pod
       NodeInfo& ni = writable(nit->second);
       ni.gpu.apply(pod->gpu, -1);
       fn(*pod);
       pod->recompute_gpu_assignment();
       ni.gpu.apply(pod->gpu, +1);
       mark_dirty(pod->node_name);
+      in_place_ = false;
       return pod;
     }
   }
   return mutate_pod(uid, fn);
 }
 
-int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us) {
+int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const std::string* check_assumed,
+                                    bool* is_assumed) {
   int64_t t0 = lock_wait_us ? clock_->now_us() : 0;
   std::lock_guard<std::mutex> g(mu_);
   if (lock_wait_us) *lock_wait_us = clock_->now_us() - t0;
+  if (check_assumed && is_assumed) *is_assumed = assumed_.count(*check_assumed) > 0;
   int clones = 0;
   bool affinity_dirty = false;
   if (structure_changed_) {
@@ -281,7 +288,11 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us) {
       auto sit = s.by_name.find(name);
       if (sit == s.by_name.end()) continue;
       const NodeInfoPtr& cl = it->second;
-      if (sit->second == cl) continue;
+      if (sit->second == cl) {
+        // Updated in place (assume/Reserve): the Snapshot already sees it.
+        if (!cl->pods_with_affinity.empty() || !cl->pods_with_required_anti_affinity.empty()) affinity_dirty = true;
+        continue;
+      }
       ++clones;
       if (!sit->second->pods_with_affinity.empty() || !cl->pods_with_affinity.empty()) affinity_dirty = true;
       s.retired.push_back(s.nodes[s.index[name]]);
@@ -324,7 +335,7 @@ void SchedulerCache::cleanup_expired_assumed_pods() {
 }
 
 int SchedulerCache::assigned_in_group(uint64_t pg_key) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<std::mutex> g(group_mu_);
   auto it = group_assigned_.find(pg_key);
   return it == group_assigned_.end() ? 0 : it->second;
 }

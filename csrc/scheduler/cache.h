@@ -40,7 +40,13 @@ class SchedulerCache {
   void update_pod(const PodPtr& old_pod, const PodPtr& new_pod);
   void remove_pod(const Pod& p);
 
-  Status assume_pod(const PodPtr& p);  // p->node_name must be set
+  // p->node_name must be set. Called by the scheduling thread between cycles
+  // (Scheduler holds sched_mu_): the node's NodeInfo is updated in place even
+  // while the scheduler's own Snapshot shares it — no Filter/Score worker is
+  // running and no other thread reads snapshot NodeInfos — which saves a
+  // NodeInfo copy per scheduled pod (and its release on a binder thread).
+  // Every other writer (informer, binder) still copies on write.
+  Status assume_pod(const PodPtr& p);
   void finish_binding(const Pod& p);
   void forget_pod(const Pod& p);
   bool is_assumed(const std::string& uid) const;
@@ -49,7 +55,7 @@ class SchedulerCache {
   // the pod on its node. Returns the new object (nullptr if not cached).
   PodPtr mutate_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
   // In-place annotation of a pod assumed in the current scheduling cycle
-  // (FlexGPU Reserve): no other thread holds that object yet, so there is no
+  // (FlexGPU Reserve, scheduling thread): no other thread holds that object yet, so there is no
   // copy, and since `fn` may only change annotations, only the node's GPU
   // ledger is re-accounted (Pod::recompute_gpu_assignment). Falls back to
   // mutate_pod for pods that are not (or no longer) assumed.
@@ -58,7 +64,10 @@ class SchedulerCache {
   // Returns the number of NodeInfo versions refreshed (shared, not cloned:
   // the cache copies on write); replaced versions go to `s.retired`; `lock_wait_us` (optional)
   // receives the time spent waiting for the cache lock (trace diagnostics).
-  int update_snapshot(Snapshot& s, int64_t* lock_wait_us = nullptr);
+  // `check_assumed` (optional): also reports, under the same lock, whether
+  // that pod uid is assumed (the cycle's skipPodSchedule check).
+  int update_snapshot(Snapshot& s, int64_t* lock_wait_us = nullptr, const std::string* check_assumed = nullptr,
+                      bool* is_assumed = nullptr);
   void cleanup_expired_assumed_pods();
 
   // Pods of a PodGroup that are assumed or bound, keyed by Pod::pg_key (a
@@ -79,6 +88,7 @@ class SchedulerCache {
   };
   NodeInfoPtr& info_for(const std::string& node);  // creates a ghost entry
   NodeInfo& writable(NodeInfoPtr& slot);            // copy-on-write before mutating
+  bool in_place_ = false;  // assume/annotate on the scheduling thread (under mu_)
   void add_pod_locked(const PodPtr& p);
   void remove_pod_locked(const Pod& p);
   void mark_dirty(const std::string& node);
@@ -95,6 +105,9 @@ class SchedulerCache {
   std::vector<std::string> order_;  // node names with a Node object, insertion order
   std::unordered_map<std::string, PodState> pod_states_;
   std::unordered_set<std::string> assumed_;
+  // Written under mu_ + group_mu_, read under group_mu_ only: Permit and
+  // PreScore read a gang's count without waiting behind NodeInfo copies.
+  mutable std::mutex group_mu_;
   std::unordered_map<uint64_t, int> group_assigned_;
   std::unordered_set<std::string> dirty_;
   bool structure_changed_ = true;

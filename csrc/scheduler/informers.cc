@@ -118,6 +118,28 @@ size_t Informers::count_pods_in_group(const std::string& ns, const std::string& 
   return n;
 }
 
+std::vector<PodPtr> Informers::pods_in_group_of(const Pod& p) const {
+  std::vector<PodPtr> out;
+  if (!p.pg_key) return out;
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto git = pods_by_group_.find(p.pg_key);
+  if (git == pods_by_group_.end()) return out;
+  out.reserve(git->second.size());
+  for (const auto& q : git->second)
+    if (q->pod_group == p.pod_group && q->ns() == p.ns()) out.push_back(q);
+  return out;
+}
+
+size_t Informers::count_pods_in_group_of(const Pod& p) const {
+  if (!p.pg_key) return 0;
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto git = pods_by_group_.find(p.pg_key);
+  if (git == pods_by_group_.end()) return 0;
+  size_t n = 0;
+  for (const auto& q : git->second) n += q->pod_group == p.pod_group && q->ns() == p.ns();
+  return n;
+}
+
 std::vector<PodPtr> Informers::all_pods() const {
   std::shared_lock<std::shared_mutex> g(mu_);
   std::vector<PodPtr> out;

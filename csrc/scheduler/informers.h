@@ -40,6 +40,9 @@ class Informers {
   PodPtr pod(const std::string& ns, const std::string& name) const;
   std::vector<PodPtr> pods_in_group(const std::string& ns, const std::string& pg) const;
   size_t count_pods_in_group(const std::string& ns, const std::string& pg) const;
+  // Members of p's PodGroup, found by p.pg_key (no key string built).
+  std::vector<PodPtr> pods_in_group_of(const Pod& p) const;
+  size_t count_pods_in_group_of(const Pod& p) const;
   std::vector<PodPtr> all_pods() const;
   PodGroupPtr pod_group(const std::string& ns, const std::string& name) const;
   // The PodGroup named by p's group label, looked up by p.pg_key (no string

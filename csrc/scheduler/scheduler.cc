@@ -464,7 +464,7 @@ void Scheduler::apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr 
       // in unschedulableQ/backoffQ (targeted form of the Pod/Add cluster
       // event Coscheduling registers; O(group size), not O(queue)).
       if (!np->pod_group.empty()) {
-        std::vector<PodPtr> sib = informers_->pods_in_group(np->ns(), np->pod_group);
+        std::vector<PodPtr> sib = informers_->pods_in_group_of(*np);
         sib.erase(std::remove_if(sib.begin(), sib.end(),
                                  [&](const PodPtr& q) { return q->uid() == np->uid() || !q->node_name.empty(); }),
                   sib.end());
@@ -860,7 +860,6 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   // skipPodSchedule: deleted or already assumed.
   PodPtr latest = informers_->pod(pod->ns(), pod->name());
   if (!latest || latest->uid() != pod->uid() || latest->terminating() || !latest->node_name.empty()) return;
-  if (cache_->is_assumed(pod->uid())) return;
 
   int64_t cycle_start = clock_->now_us();
   auto state = std::make_shared<CycleState>();
@@ -873,7 +872,9 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
 
   int64_t lock_wait = 0;
   int64_t snap_start = tracer_.enabled() ? clock_->now_us() : 0;
-  int clones = cache_->update_snapshot(snapshot_, tracer_.enabled() ? &lock_wait : nullptr);
+  bool already_assumed = false;
+  int clones = cache_->update_snapshot(snapshot_, tracer_.enabled() ? &lock_wait : nullptr, &pod->uid(), &already_assumed);
+  if (already_assumed) return;  // skipPodSchedule: assumed by an earlier cycle
   release_retired();
   const std::string& profile = fw->profile_name();
   {
