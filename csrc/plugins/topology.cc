@@ -59,6 +59,17 @@ struct CriticalPath {
   int64_t num = INT32_MAX;
 };
 
+// The pre-filter/pre-score state of a pod that has nothing to track (no
+// constraints, no affinity terms in play) is one shared empty object handed
+// out as a non-owning shared_ptr (aliasing an empty owner): no allocation and
+// no refcount traffic per cycle. Filter/Score only read it; preemption dry
+// runs mutate clones (CycleState::clone), never the original.
+template <typename T>
+std::shared_ptr<StateData> empty_state() {
+  static T obj;
+  return std::shared_ptr<StateData>(std::shared_ptr<StateData>(), &obj);
+}
+
 struct SpreadFilterState : StateData {
   std::vector<TopologySpreadConstraint> constraints;
   std::unordered_map<std::string, int64_t> pair_num;                     // key\nvalue -> matching pods
@@ -114,6 +125,12 @@ class PodTopologySpread : public Plugin {
   static constexpr const char* kScoreKey = "PreScorePodTopologySpread";
 
   Status pre_filter(CycleState& s, const Pod& p) override {
+    bool any_hard = false;
+    for (const auto& c : p.spread_constraints) any_hard = any_hard || c.hard;
+    if (!any_hard) {
+      s.write(kFilterKey, empty_state<SpreadFilterState>());
+      return {};
+    }
     auto st = std::make_shared<SpreadFilterState>();
     for (const auto& c : p.spread_constraints)
       if (c.hard) st->constraints.push_back(c);
@@ -180,6 +197,12 @@ class PodTopologySpread : public Plugin {
   }
 
   Status pre_score(CycleState& s, const Pod& p, const NodeList& nodes) override {
+    bool any_soft = false;
+    for (const auto& c : p.spread_constraints) any_soft = any_soft || !c.hard;
+    if (!any_soft || nodes.empty()) {
+      s.write(kScoreKey, empty_state<SpreadScoreState>());
+      return {};
+    }
     auto st = std::make_shared<SpreadScoreState>();
     for (const auto& c : p.spread_constraints)
       if (!c.hard) st->constraints.push_back(c);
@@ -363,6 +386,11 @@ class InterPodAffinity : public Plugin {
   }
 
   Status pre_filter(CycleState& s, const Pod& p) override {
+    if (!h_.snapshot || (h_.snapshot->have_pods_with_required_anti_affinity.empty() &&
+                         p.pod_affinity_required.empty() && p.pod_anti_affinity_required.empty())) {
+      s.write(kFilterKey, empty_state<AffinityFilterState>());
+      return {};
+    }
     auto st = std::make_shared<AffinityFilterState>();
     if (h_.snapshot) {
       for (const auto& ni : h_.snapshot->have_pods_with_required_anti_affinity)
@@ -435,8 +463,12 @@ class InterPodAffinity : public Plugin {
   }
 
   Status pre_score(CycleState& s, const Pod& p, const NodeList& nodes) override {
-    auto st = std::make_shared<AffinityScoreState>();
     bool has_pref = !p.pod_affinity_preferred.empty() || !p.pod_anti_affinity_preferred.empty();
+    if (!h_.snapshot || nodes.empty() || (!has_pref && h_.snapshot->have_pods_with_affinity.empty())) {
+      s.write(kScoreKey, empty_state<AffinityScoreState>());
+      return {};
+    }
+    auto st = std::make_shared<AffinityScoreState>();
     if (h_.snapshot && !nodes.empty() && (has_pref || !h_.snapshot->have_pods_with_affinity.empty())) {
       const auto& scan = has_pref ? h_.snapshot->nodes : h_.snapshot->have_pods_with_affinity;
       for (const auto& ni : scan) {
