@@ -4,6 +4,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_set>
 
 namespace xsched {
 
@@ -315,6 +317,13 @@ void Pod::recompute_gpu_assignment() {
       i = j + 1;
     }
   }
+}
+
+const std::string& IStr::intern(std::string_view v) {
+  static std::mutex mu;
+  static auto* table = new std::unordered_set<std::string>();  // never freed: IStr pointers outlive statics
+  std::lock_guard<std::mutex> g(mu);
+  return *table->emplace(v).first;
 }
 
 uint64_t pg_key_of(std::string_view full) {

@@ -12,6 +12,7 @@
 #include <memory>
 #include <optional>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -136,11 +137,32 @@ struct GpuDemand {
   int64_t amount = 0;
 };
 
+// An interned string: values from a small set (scheduler names, preemption
+// policies) that every Pod copy would otherwise re-allocate (both exceed the
+// 15-character small-string buffer). Copying is a pointer copy; the table
+// lives for the process.
+class IStr {
+ public:
+  IStr() : s_(&intern("")) {}
+  IStr(std::string_view v) : s_(&intern(v)) {}  // NOLINT: implicit on purpose
+  IStr(const char* v) : s_(&intern(v)) {}       // NOLINT
+  IStr(const std::string& v) : s_(&intern(v)) {}  // NOLINT
+  const std::string& str() const { return *s_; }
+  operator const std::string&() const { return *s_; }  // NOLINT
+  bool operator==(std::string_view v) const { return *s_ == v; }
+  bool operator!=(std::string_view v) const { return *s_ != v; }
+  bool empty() const { return s_->empty(); }
+  static const std::string& intern(std::string_view v);
+
+ private:
+  const std::string* s_;
+};
+
 struct Pod {
   ObjectMeta meta;
-  std::string scheduler_name = kDefaultSchedulerName;
+  IStr scheduler_name = kDefaultSchedulerName;
   std::string node_name, nominated_node_name, priority_class_name, phase = "Pending";
-  std::string preemption_policy = "PreemptLowerPriority";
+  IStr preemption_policy = "PreemptLowerPriority";
   int32_t priority = 0;
   std::vector<Container> containers, init_containers;
   Res overhead;

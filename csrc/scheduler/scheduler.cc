@@ -1041,7 +1041,7 @@ Json Scheduler::explain(const Json& pod_obj) {
   auto pod = Pod::from_json(pod_obj);
   Framework* fw = framework_for(pod->scheduler_name);
   if (!fw) {
-    out.set("error", Json("no profile for schedulerName " + pod->scheduler_name));
+    out.set("error", Json("no profile for schedulerName " + pod->scheduler_name.str()));
     return out;
   }
   if (pod->uid().empty()) pod->meta.uid = "explain-" + pod->key();
@@ -1102,7 +1102,7 @@ double Scheduler::score_benchmark(const Json& pod_obj, int iterations, Json* out
   std::lock_guard<std::mutex> g(sched_mu_);
   auto pod = Pod::from_json(pod_obj);
   Framework* fw = framework_for(pod->scheduler_name);
-  if (!fw) throw std::runtime_error("no profile for schedulerName " + pod->scheduler_name);
+  if (!fw) throw std::runtime_error("no profile for schedulerName " + pod->scheduler_name.str());
   cache_->update_snapshot(snapshot_);
   NodeList nodes;
   nodes.reserve(snapshot_.nodes.size());
