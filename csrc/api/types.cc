@@ -34,8 +34,22 @@ void civil_from_days(int64_t z, int64_t* y, unsigned* m, unsigned* d) {
 
 MicroTime parse_rfc3339(const std::string& s) {
   if (s.size() < 19) return 0;
+  // Fixed-width "YYYY-MM-DDTHH:MM:SS" read digit by digit (every watched Pod
+  // carries a creationTimestamp; sscanf was a visible share of parsing).
+  auto num = [&](size_t at, size_t width, int* out) {
+    int v = 0;
+    for (size_t k = at; k < at + width; ++k) {
+      if (s[k] < '0' || s[k] > '9') return false;
+      v = v * 10 + (s[k] - '0');
+    }
+    *out = v;
+    return true;
+  };
   int Y, M, D, h, mi, sec;
-  if (std::sscanf(s.c_str(), "%4d-%2d-%2dT%2d:%2d:%2d", &Y, &M, &D, &h, &mi, &sec) != 6) return 0;
+  if (!num(0, 4, &Y) || s[4] != '-' || !num(5, 2, &M) || s[7] != '-' || !num(8, 2, &D) ||
+      (s[10] != 'T' && s[10] != 't' && s[10] != ' ') || !num(11, 2, &h) || s[13] != ':' || !num(14, 2, &mi) ||
+      s[16] != ':' || !num(17, 2, &sec))
+    return 0;
   size_t i = 19;
   int64_t frac_us = 0;
   if (i < s.size() && s[i] == '.') {
@@ -320,6 +334,11 @@ void Pod::recompute_gpu_assignment() {
 }
 
 const std::string& IStr::intern(std::string_view v) {
+  // The values almost every pod carries skip the table lock.
+  static const std::string* kCommon[] = {new std::string(kDefaultSchedulerName), new std::string("PreemptLowerPriority"),
+                                         new std::string("")};
+  for (const std::string* c : kCommon)
+    if (*c == v) return *c;
   static std::mutex mu;
   static auto* table = new std::unordered_set<std::string>();  // never freed: IStr pointers outlive statics
   std::lock_guard<std::mutex> g(mu);
@@ -340,10 +359,10 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
   p->meta = ObjectMeta::from_json(obj);
   const Json& spec = obj["spec"];
   const Json& status = obj["status"];
+  p->spec_hash = json_hash(spec, 1469598103934665603ULL, "nodeName");
   if (spec["nodeName"].as_string().empty()) {  // only pending pods are ever scheduled
     const Json& md = obj["metadata"];
-    uint64_t h = json_hash(spec, 1469598103934665603ULL, "nodeName");
-    h = json_hash(md["namespace"], h);
+    uint64_t h = json_hash(md["namespace"], p->spec_hash);
     p->template_hash = json_hash(md["annotations"], h);
   }
   if (spec["schedulerName"].is_string()) p->scheduler_name = spec["schedulerName"].as_string();

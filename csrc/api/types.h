@@ -8,6 +8,7 @@
 // scheduling/v1 PriorityClass.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <optional>
@@ -158,6 +159,24 @@ class IStr {
   const std::string* s_;
 };
 
+// An int64 field that one thread may update while others read it (relaxed:
+// a timestamp, no ordering implied). Copyable, unlike std::atomic.
+struct RelaxedI64 {
+  std::atomic<int64_t> v{0};
+  RelaxedI64() = default;
+  RelaxedI64(int64_t x) : v(x) {}  // NOLINT: implicit on purpose
+  RelaxedI64(const RelaxedI64& o) : v(o.v.load(std::memory_order_relaxed)) {}
+  RelaxedI64& operator=(const RelaxedI64& o) {
+    v.store(o.v.load(std::memory_order_relaxed), std::memory_order_relaxed);
+    return *this;
+  }
+  RelaxedI64& operator=(int64_t x) {
+    v.store(x, std::memory_order_relaxed);
+    return *this;
+  }
+  operator int64_t() const { return v.load(std::memory_order_relaxed); }  // NOLINT
+};
+
 struct Pod {
   ObjectMeta meta;
   IStr scheduler_name = kDefaultSchedulerName;
@@ -174,8 +193,11 @@ struct Pod {
   std::vector<PodAffinityTerm> pod_affinity_required, pod_anti_affinity_required;
   std::vector<WeightedPodAffinityTerm> pod_affinity_preferred, pod_anti_affinity_preferred;
   std::vector<TopologySpreadConstraint> spread_constraints;
-  MicroTime start_time = 0;
-  MicroTime scheduled_at = 0;  // PodScheduled=True lastTransitionTime (0 = not scheduled)
+  // status.startTime and the PodScheduled=True lastTransitionTime (0 = unset).
+  // Relaxed atomics: a bind confirmation copies them into the assumed object
+  // that NodeInfos (and Snapshot readers) already hold (cache.cc).
+  RelaxedI64 start_time = 0;
+  RelaxedI64 scheduled_at = 0;
 
   // ---- derived at parse time ----
   Res request;          // computePodResourceRequest: max(sum(containers), each init) + overhead
@@ -194,6 +216,10 @@ struct Pod {
   // (InterPodAffinity, PodTopologySpread, XGMIGangAffinity via the PodGroup)
   // declare themselves non-local whenever those labels can matter.
   uint64_t template_hash = 0;
+  // Hash of the spec minus nodeName: two objects of one pod with equal
+  // spec_hash, labels and GPU assignment account identically on a node (the
+  // cache keeps the assumed object when its bind is confirmed).
+  uint64_t spec_hash = 0;
 
   const std::string& ns() const { return meta.ns; }
   const std::string& name() const { return meta.name; }

@@ -158,11 +158,38 @@ void SchedulerCache::forget_pod(const Pod& p) {
   pod_states_.erase(it);
 }
 
+namespace {
+// The informer's bound object accounts on its node exactly like the assumed
+// copy: same node, spec, labels and GPU placement.
+bool same_accounting(const Pod& assumed, const Pod& bound) {
+  const GpuAssignment &a = assumed.gpu, &b = bound.gpu;
+  return assumed.node_name == bound.node_name && assumed.spec_hash == bound.spec_hash &&
+         assumed.meta.labels == bound.meta.labels && assumed.meta.deletion == bound.meta.deletion &&
+         assumed.priority == bound.priority && a.kind == b.kind && a.gpus == b.gpus && a.partitions == b.partitions &&
+         a.memory == b.memory;
+}
+}  // namespace
+
+bool SchedulerCache::confirm_assumed_locked(std::unordered_map<std::string, PodState>::iterator it, const PodPtr& p) {
+  if (!same_accounting(*it->second.pod, *p)) return false;
+  // The node's NodeInfo already holds an equivalent object: leave it (and its
+  // generation, so equivalence-cache verdicts for the node stay valid) and
+  // only record the informer's object as the pod's current state.
+  // Status timestamps the preemption paths read from NodeInfo pods
+  // (victim ordering, PreemptionToleration's toleration window).
+  it->second.pod->scheduled_at = p->scheduled_at;
+  it->second.pod->start_time = p->start_time;
+  assumed_.erase(p->uid());
+  it->second = PodState{p, 0, false};
+  return true;
+}
+
 void SchedulerCache::add_pod(const PodPtr& p) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = pod_states_.find(p->uid());
   if (it != pod_states_.end()) {
     if (assumed_.count(p->uid())) {
+      if (confirm_assumed_locked(it, p)) return;
       // Confirmation of an assumed pod: replace with the informer's object
       // (it carries the bound annotations) on the node it was bound to.
       remove_pod_locked(*it->second.pod);
@@ -190,6 +217,7 @@ void SchedulerCache::update_pod(const PodPtr& old_pod, const PodPtr& new_pod) {
   }
   if (assumed_.count(new_pod->uid())) {
     // An update for an assumed pod means it got bound: confirm it.
+    if (confirm_assumed_locked(it, new_pod)) return;
     remove_pod_locked(*it->second.pod);
     add_pod_locked(new_pod);
     assumed_.erase(new_pod->uid());

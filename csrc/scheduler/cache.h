@@ -86,6 +86,10 @@ class SchedulerCache {
     int64_t deadline_us = 0;
     bool binding_finished = false;
   };
+  // Bind confirmation of an assumed pod whose informer object accounts the
+  // same on its node: records it without touching the NodeInfo (no copy, no
+  // generation bump). False when the node must be re-accounted.
+  bool confirm_assumed_locked(std::unordered_map<std::string, PodState>::iterator it, const PodPtr& p);
   NodeInfoPtr& info_for(const std::string& node);  // creates a ghost entry
   NodeInfo& writable(NodeInfoPtr& slot);            // copy-on-write before mutating
   bool in_place_ = false;  // assume/annotate on the scheduling thread (under mu_)
