@@ -453,7 +453,10 @@ Status Framework::run_permit(CycleState& s, const PodPtr& p, const std::string& 
   }
   if (timeouts.empty()) return {};
   handle_.waiting_pods->add(p, node, timeouts, std::move(on_done));
-  return Status(Code::Wait, "one or more plugins asked to wait and no plugin rejected pod " + p->name());
+  // Prebuilt (the reference appends the pod name; the caller only tests
+  // is_wait(), so the message is not built per waiting gang member).
+  static const Status kWait(Code::Wait, "one or more plugins asked to wait and no plugin rejected the pod");
+  return kWait;
 }
 
 Status Framework::run_pre_bind(CycleState& s, const PodPtr& p, const std::string& node) {
