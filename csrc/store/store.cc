@@ -289,37 +289,56 @@ JsonPtr ObjectStore::update(const std::string& kind, Json obj, bool check_rv) {
   return ptr;
 }
 
+JsonPtr ObjectStore::update_optimistic(const std::string& kind, const std::string& key, const std::string& name,
+                                       const std::function<std::optional<Json>(const Json& cur)>& build) {
+  for (;;) {
+    JsonPtr base;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto& km = kinds_[kind];
+      auto it = km.find(key);
+      if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
+      base = it->second.obj;
+    }
+    std::optional<Json> next = build(*base);  // validation + copy + edit, unlocked
+    std::lock_guard<std::mutex> g(mu_);
+    auto& km = kinds_[kind];
+    auto it = km.find(key);
+    if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
+    if (it->second.obj != base) continue;  // a concurrent write won: rebuild from the new version
+    if (!next) return base;
+    int64_t rv = rv_.fetch_add(1) + 1;
+    stamp(*next, rv);
+    auto ptr = std::make_shared<const Json>(std::move(*next));
+    it->second.obj = ptr;
+    emit_locked(EventType::Modified, kind, ptr, base, rv);
+    return ptr;
+  }
+}
+
 JsonPtr ObjectStore::patch(const std::string& kind, const std::string& ns, const std::string& name,
                            const Json& merge_patch) {
   check_faults("patch", kind);
-  std::lock_guard<std::mutex> g(mu_);
-  auto& km = kinds_[kind];
-  auto it = km.find(key_of(namespaced(kind) ? ns : "", name));
-  if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
-  // A patch carrying metadata.resourceVersion is a precondition (optimistic
-  // concurrency, as kube-apiserver applies it to merge patches).
-  if (const Json* pmd = merge_patch.get("metadata")) {
-    const Json& prv = (*pmd)["resourceVersion"];
-    if (prv.is_string() && !prv.as_string().empty() &&
-        prv.as_string() != (*it->second.obj)["metadata"]["resourceVersion"].as_string())
-      throw StoreError(409, "Conflict",
-                       "Operation cannot be fulfilled on " + kind + " \"" + name +
-                           "\": the object has been modified; please apply your changes to the latest version and try again");
-  }
-  Json obj = *it->second.obj;
-  Json saved_md = obj["metadata"];
-  obj.merge_patch(merge_patch);
-  Json& md = obj.at_or_create("metadata");
-  for (const char* k : {"uid", "creationTimestamp", "name", "namespace"})
-    if (const Json* v = saved_md.get(k)) md.set(k, *v);
-  if (obj == *it->second.obj) return it->second.obj;  // no-op patch: no new version
-  int64_t rv = rv_.fetch_add(1) + 1;
-  stamp(obj, rv);
-  auto ptr = std::make_shared<const Json>(std::move(obj));
-  JsonPtr old = it->second.obj;
-  it->second.obj = ptr;
-  emit_locked(EventType::Modified, kind, ptr, old, rv);
-  return ptr;
+  return update_optimistic(kind, key_of(namespaced(kind) ? ns : "", name), name,
+                           [&](const Json& cur) -> std::optional<Json> {
+    // A patch carrying metadata.resourceVersion is a precondition (optimistic
+    // concurrency, as kube-apiserver applies it to merge patches).
+    if (const Json* pmd = merge_patch.get("metadata")) {
+      const Json& prv = (*pmd)["resourceVersion"];
+      if (prv.is_string() && !prv.as_string().empty() && prv.as_string() != cur["metadata"]["resourceVersion"].as_string())
+        throw StoreError(409, "Conflict",
+                         "Operation cannot be fulfilled on " + kind + " \"" + name +
+                             "\": the object has been modified; please apply your changes to the latest version and try again");
+    }
+    Json obj = cur;
+    Json saved_md = obj["metadata"];
+    obj.merge_patch(merge_patch);
+    Json& md = obj.at_or_create("metadata");
+    for (const char* k : {"uid", "creationTimestamp", "name", "namespace"})
+      if (const Json* v = saved_md.get(k)) md.set(k, *v);
+    if (obj == cur) return std::nullopt;  // no-op patch: no new version
+    return obj;
+  });
 }
 
 JsonPtr ObjectStore::remove(const std::string& kind, const std::string& ns, const std::string& name,
@@ -384,41 +403,33 @@ size_t ObjectStore::delete_all(const std::string& kind, const std::string& ns) {
 JsonPtr ObjectStore::bind(const std::string& ns, const std::string& name, const std::string& uid,
                           const std::string& node, const Json& annotations) {
   check_faults("bind", "pods");
-  std::lock_guard<std::mutex> g(mu_);
-  auto& km = kinds_["pods"];
-  auto it = km.find(key_of(ns, name));
-  if (it == km.end()) throw StoreError(404, "NotFound", "pods \"" + name + "\" not found");
-  const Json& cur = *it->second.obj;
-  if (!uid.empty() && cur["metadata"]["uid"].as_string() != uid)
-    throw StoreError(409, "Conflict", "Precondition failed: UID in precondition does not match");
-  if (!cur["spec"]["nodeName"].as_string().empty())
-    throw StoreError(409, "Conflict",
-                     "pod " + name + " is already assigned to node \"" + cur["spec"]["nodeName"].as_string() + "\"");
-  if (cur["metadata"]["deletionTimestamp"].is_string())
-    throw StoreError(409, "Conflict", "pod " + name + " is being deleted, cannot be assigned to a host");
-  Json obj = cur;
-  obj.at_or_create("spec").set("nodeName", Json(node));
-  if (annotations.is_object() && annotations.size()) {
-    Json& ann = obj.at_or_create("metadata").at_or_create("annotations");
-    for (const auto& kv : annotations.members()) ann.set(kv.first, kv.second);
-  }
-  Json& st = obj.at_or_create("status");
-  Json cond = Json::object();
-  cond.set("type", Json("PodScheduled"));
-  cond.set("status", Json("True"));
-  cond.set("lastTransitionTime", Json(format_rfc3339(wall_now_us())));
-  Json conds = Json::array();
-  for (const auto& c : st["conditions"].items())
-    if (c["type"].as_string() != "PodScheduled") conds.push_back(c);
-  conds.push_back(std::move(cond));
-  st.set("conditions", std::move(conds));
-  int64_t rv = rv_.fetch_add(1) + 1;
-  stamp(obj, rv);
-  auto ptr = std::make_shared<const Json>(std::move(obj));
-  JsonPtr old = it->second.obj;
-  it->second.obj = ptr;
-  emit_locked(EventType::Modified, "pods", ptr, old, rv);
-  return ptr;
+  const std::string now = format_rfc3339(wall_now_us());
+  return update_optimistic("pods", key_of(ns, name), name, [&](const Json& cur) -> std::optional<Json> {
+    if (!uid.empty() && cur["metadata"]["uid"].as_string() != uid)
+      throw StoreError(409, "Conflict", "Precondition failed: UID in precondition does not match");
+    if (!cur["spec"]["nodeName"].as_string().empty())
+      throw StoreError(409, "Conflict",
+                       "pod " + name + " is already assigned to node \"" + cur["spec"]["nodeName"].as_string() + "\"");
+    if (cur["metadata"]["deletionTimestamp"].is_string())
+      throw StoreError(409, "Conflict", "pod " + name + " is being deleted, cannot be assigned to a host");
+    Json obj = cur;
+    obj.at_or_create("spec").set("nodeName", Json(node));
+    if (annotations.is_object() && annotations.size()) {
+      Json& ann = obj.at_or_create("metadata").at_or_create("annotations");
+      for (const auto& kv : annotations.members()) ann.set(kv.first, kv.second);
+    }
+    Json& st = obj.at_or_create("status");
+    Json cond = Json::object();
+    cond.set("type", Json("PodScheduled"));
+    cond.set("status", Json("True"));
+    cond.set("lastTransitionTime", Json(now));
+    Json conds = Json::array();
+    for (const auto& c : st["conditions"].items())
+      if (c["type"].as_string() != "PodScheduled") conds.push_back(c);
+    conds.push_back(std::move(cond));
+    st.set("conditions", std::move(conds));
+    return obj;
+  });
 }
 
 WatcherPtr ObjectStore::watch(const std::set<std::string>& kinds, const std::string& ns, int64_t since_rv) {

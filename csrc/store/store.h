@@ -141,6 +141,14 @@ class ObjectStore {
   JsonPtr create_locked(const std::string& kind, Json obj);
   void flush_batch_locked(std::vector<WatchEvent>& batch);
   static void stamp(Json& obj, int64_t rv);
+  // Optimistic update of one object: `build(cur)` validates the current
+  // version and returns the new object (or nullopt for a no-op) outside the
+  // store lock; the result is committed only if the object is still the
+  // version `build` saw, else `build` reruns (the deep copy of a Pod no
+  // longer happens while 16 binder threads queue on mu_). Returns the
+  // committed (or, for a no-op, current) object.
+  JsonPtr update_optimistic(const std::string& kind, const std::string& key, const std::string& name,
+                            const std::function<std::optional<Json>(const Json& cur)>& build);
   std::vector<WatchEvent>* batch_ = nullptr;  // bulk ops collect events here (under mu_)
 
   mutable std::mutex mu_;

@@ -372,7 +372,7 @@ TEST(parallelizer_cost_model_inline_vs_parallel) {
     std::set<std::thread::id> ids;
     par.until(n, [&](int) {
       if (heavy) {
-        auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(2);
+        auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(4);
         while (std::chrono::steady_clock::now() < end) {
         }
       }
@@ -385,12 +385,52 @@ TEST(parallelizer_cost_model_inline_vs_parallel) {
   CHECK_EQ(threads_used(512, &cheap_site, false), 1u);
   threads_used(512, &heavy_site, true);  // first call is an inline probe
   size_t most = 0;
-  for (int i = 0; i < 4; ++i) most = std::max(most, threads_used(512, &heavy_site, true));
-  CHECK(most > 1);  // 512 x 2 us = 1 ms of serial work
+  // Helpers must win a wake-up race against the caller; on a loaded host
+  // (a parallel build) give them several rounds.
+  for (int i = 0; i < 12 && most <= 1; ++i) most = std::max(most, threads_used(512, &heavy_site, true));
+  CHECK(most > 1);  // 512 x 4 us = 2 ms of serial work
   CHECK(heavy_site.ns_per_item_x16.load() / 16 >= 1000);
 }
 
 }  // namespace
+
+TEST(store_optimistic_updates_lose_nothing) {
+  // 8 writers patch (and one binds) the same pod concurrently: each update
+  // is built outside the store lock and committed only on the version it was
+  // built from, so every patch lands and resourceVersions stay contiguous.
+  ObjectStore st;
+  st.create("pods", Json::parse(R"({"metadata":{"name":"p","namespace":"d","uid":"u1"},"spec":{}})"));
+  int64_t rv0 = st.resource_version();
+  constexpr int kThreads = 8, kEach = 150;
+  std::vector<std::thread> ts;
+  for (int t = 0; t < kThreads; ++t)
+    ts.emplace_back([&st, t] {
+      for (int i = 0; i < kEach; ++i) {
+        Json patch = Json::object();
+        Json labels = Json::object();
+        labels.set("k" + std::to_string(t) + "-" + std::to_string(i), Json("v"));
+        Json md = Json::object();
+        md.set("labels", std::move(labels));
+        patch.set("metadata", std::move(md));
+        st.patch("pods", "d", "p", patch);
+      }
+    });
+  bool bound = false;
+  std::thread binder([&] {
+    try {
+      st.bind("d", "p", "u1", "node-1", Json::object());
+      bound = true;
+    } catch (const StoreError&) {
+    }
+  });
+  for (auto& th : ts) th.join();
+  binder.join();
+  JsonPtr cur = st.get("pods", "d", "p");
+  CHECK_EQ(static_cast<int>((*cur)["metadata"]["labels"].size()), kThreads * kEach);
+  CHECK(bound);
+  CHECK_EQ((*cur)["spec"]["nodeName"].as_string(), "node-1");
+  CHECK_EQ(st.resource_version() - rv0, static_cast<int64_t>(kThreads * kEach + 1));
+}
 
 int main() {
   for (const auto& t : tests()) {
