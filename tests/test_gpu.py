@@ -120,9 +120,11 @@ def test_amdsmi_telemetry_sees_hbm_load():
     """The native amd-smi sampler (csrc/telemetry/amdsmi_sampler.cc) reads the
     live MI355X: 8 XCCs, 7 xGMI links up, idle near 0%, and a device copy
     loop drives GFX and HBM-controller activity and power up."""
-    from flex_gpu_scheduler_amd.tools.amdsmi_probe import run
-
-    r = run(seconds=1.5)
+    # Own process: this module's HIP probe runtime and torch's must not share one.
+    out = subprocess.run([sys.executable, "-m", "flex_gpu_scheduler_amd.tools.amdsmi_probe", "--seconds", "1.5"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["available"], r
     assert r["gpu0"]["xcc"] == 8 and r["gpu0"]["links_up"] >= 1, r
     assert r["load"]["max_gfx"] >= 50 and r["load"]["max_umc"] >= 20, r
