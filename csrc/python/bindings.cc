@@ -102,8 +102,14 @@ class PyApiClient : public ApiClient {
   }
 };
 
-py::dict pod_summary(const Json& obj) {
-  auto p = Pod::from_json(obj);
+py::dict pod_struct_summary(const Pod& pod);
+
+py::dict pod_summary(const Json& obj) { return pod_struct_summary(*Pod::from_json(obj)); }
+
+// The decoded fields of a Pod object (lister copies and parsed JSON compare
+// equal field by field when the informer's bind fast path is exact).
+py::dict pod_struct_summary(const Pod& pod) {
+  const Pod* p = &pod;
   py::dict d;
   d["key"] = p->key();
   d["request"] = to_py(p->request.to_json());
@@ -117,6 +123,18 @@ py::dict pod_summary(const Json& obj) {
   py::list parts;
   for (auto [g, pp] : p->gpu.partitions) parts.append(py::make_tuple(g, pp));
   d["partitions"] = parts;
+  d["node_name"] = p->node_name;
+  d["uid"] = p->uid();
+  d["resource_version"] = p->meta.resource_version;
+  d["labels"] = p->meta.labels;
+  d["annotations"] = p->meta.annotations;
+  d["phase"] = p->phase;
+  d["scheduled_at"] = static_cast<int64_t>(p->scheduled_at);
+  d["start_time"] = static_cast<int64_t>(p->start_time);
+  d["template_hash"] = p->template_hash;
+  d["spec_hash"] = p->spec_hash;
+  d["scheduler_name"] = p->scheduler_name.str();
+  d["host_ports"] = static_cast<int>(p->host_ports.size());
   return d;
 }
 
@@ -512,6 +530,12 @@ PYBIND11_MODULE(_xsched, m) {
              d["pods"] = s.cache().pod_count();
              d["assumed"] = s.cache().assumed_count();
              return d;
+           })
+      .def("lister_pod",
+           [](Scheduler& s, const std::string& ns, const std::string& name) -> py::object {
+             auto p = s.informers().pod(ns, name);
+             if (!p) return py::none();
+             return pod_struct_summary(*p);
            })
       .def("lister_counts",
            [](Scheduler& s) {

@@ -201,6 +201,7 @@ class Scheduler {
   void handle_event(const WatchEvent& ev);
   void handle_pod_event(const WatchEvent& ev);
   void handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, PodPtr old);
+  PodPtr bound_copy_of_assumed(const WatchEvent& ev);
   void apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr old);
   void handle_node_event(const WatchEvent& ev);
   void scheduling_loop();
