@@ -37,14 +37,6 @@ namespace {
 
 const char* kHostnameLabel = "kubernetes.io/hostname";
 
-inline std::string pair_key(const std::string& k, const std::string& v) {
-  std::string s;
-  s.reserve(k.size() + v.size() + 1);
-  s += k;
-  s += '\n';
-  s += v;
-  return s;
-}
 
 int64_t count_matching(const std::vector<PodPtr>& pods, const LabelSelector& sel, const std::string& ns) {
   int64_t n = 0;
@@ -70,9 +62,53 @@ std::shared_ptr<StateData> empty_state() {
   return std::shared_ptr<StateData>(std::shared_ptr<StateData>(), &obj);
 }
 
+// Topology key -> value -> count. Lookups take the node's own label strings,
+// so Filter and Score build no key per node.
+using TopoCounts = std::unordered_map<std::string, std::unordered_map<std::string, int64_t>>;
+
+// Adds d to (key, value), dropping entries that reach 0 (an empty map means
+// "no pair counted", which InterPodAffinity's Filter relies on).
+void topo_add(TopoCounts& m, const std::string& key, const std::string& value, int64_t d) {
+  auto& vals = m[key];
+  int64_t& c = vals[value];
+  c += d;
+  if (c == 0) {
+    vals.erase(value);
+    if (vals.empty()) m.erase(key);
+  }
+}
+int64_t topo_get(const TopoCounts& m, const std::string& key, const std::string& value) {
+  auto kit = m.find(key);
+  if (kit == m.end()) return 0;
+  auto it = kit->second.find(value);
+  return it == kit->second.end() ? 0 : it->second;
+}
+
+// Matching pods per (node, constraint) counted node-parallel on the
+// framework's Parallelizer (upstream's PreFilter/PreScore also fan out over
+// nodes): out[i * C + c] = count, or -1 where `eligible(node)` is false.
+// Counting walks every pod of every node (O(pods in the cluster)), the part
+// that dominates at thousands of nodes; the per-value sums stay serial.
+template <typename Eligible>
+void count_per_node(Parallelizer* par, const std::vector<NodeInfoPtr>& nodes,
+                    const std::vector<TopologySpreadConstraint>& cs, const std::string& ns, Eligible eligible,
+                    std::vector<int64_t>& out) {
+  const size_t C = cs.size();
+  out.assign(nodes.size() * C, -1);
+  auto one = [&](int i) {
+    const NodeInfo& ni = *nodes[i];
+    if (!eligible(ni)) return;
+    for (size_t c = 0; c < C; ++c) out[i * C + c] = count_matching(ni.pods, cs[c].selector, ns);
+  };
+  if (par && nodes.size() >= 256)
+    par->until(static_cast<int>(nodes.size()), one);
+  else
+    for (size_t i = 0; i < nodes.size(); ++i) one(static_cast<int>(i));
+}
+
 struct SpreadFilterState : StateData {
   std::vector<TopologySpreadConstraint> constraints;
-  std::unordered_map<std::string, int64_t> pair_num;                     // key\nvalue -> matching pods
+  TopoCounts pair_num;                                                    // key -> value -> matching pods
   std::unordered_map<std::string, std::array<CriticalPath, 2>> critical;  // topology key -> two smallest
   std::shared_ptr<StateData> clone() const override { return std::make_shared<SpreadFilterState>(*this); }
 
@@ -94,7 +130,7 @@ struct SpreadFilterState : StateData {
 struct SpreadScoreState : StateData {
   std::vector<TopologySpreadConstraint> constraints;
   std::unordered_set<std::string> ignored;
-  std::unordered_map<std::string, int64_t> pair_count;
+  TopoCounts pair_count;
   std::vector<double> weight;
   std::shared_ptr<StateData> clone() const override { return std::make_shared<SpreadScoreState>(*this); }
 };
@@ -135,18 +171,20 @@ class PodTopologySpread : public Plugin {
     for (const auto& c : p.spread_constraints)
       if (c.hard) st->constraints.push_back(c);
     if (!st->constraints.empty() && h_.snapshot) {
-      for (const auto& ni : h_.snapshot->nodes) {
-        const Node& n = *ni->node;
-        if (!pod_matches_node_selector_and_affinity(p, n) || !has_all_keys(n, st->constraints)) continue;
-        for (const auto& c : st->constraints)
-          st->pair_num[pair_key(c.topology_key, *n.meta.label(c.topology_key))] +=
-              count_matching(ni->pods, c.selector, p.ns());
+      const auto& nodes = h_.snapshot->nodes;
+      const size_t C = st->constraints.size();
+      thread_local std::vector<int64_t> counts;
+      count_per_node(h_.parallelizer, nodes, st->constraints, p.ns(), [&](const NodeInfo& ni) {
+        return pod_matches_node_selector_and_affinity(p, *ni.node) && has_all_keys(*ni.node, st->constraints);
+      }, counts);
+      for (size_t c = 0; c < C; ++c) {
+        auto& values = st->pair_num[st->constraints[c].topology_key];
+        for (size_t i = 0; i < nodes.size(); ++i)
+          if (counts[i * C + c] >= 0) values[*nodes[i]->node->meta.label(st->constraints[c].topology_key)] += counts[i * C + c];
       }
       for (const auto& c : st->constraints) st->critical[c.topology_key];
-      for (const auto& [pk, num] : st->pair_num) {
-        size_t nl = pk.find('\n');
-        st->update_critical(pk.substr(0, nl), pk.substr(nl + 1), num);
-      }
+      for (const auto& [key, values] : st->pair_num)
+        for (const auto& [value, num] : values) st->update_critical(key, value, num);
     }
     s.write(kFilterKey, st);
     return {};
@@ -162,7 +200,7 @@ class PodTopologySpread : public Plugin {
     for (const auto& c : st->constraints) {
       if (!c.selector.matches(q.meta.labels)) continue;
       const std::string& v = *n.meta.label(c.topology_key);
-      int64_t& num = st->pair_num[pair_key(c.topology_key, v)];
+      int64_t& num = st->pair_num[c.topology_key][v];
       num += delta;
       st->update_critical(c.topology_key, v, num);
     }
@@ -188,8 +226,12 @@ class PodTopologySpread : public Plugin {
       auto cit = st->critical.find(c.topology_key);
       if (cit == st->critical.end()) return Status::error("PodTopologySpread: internal error: no critical paths");
       int64_t min_num = cit->second[0].num;
-      auto it = st->pair_num.find(pair_key(c.topology_key, *v));
-      int64_t num = it == st->pair_num.end() ? 0 : it->second;
+      int64_t num = 0;
+      auto kit = st->pair_num.find(c.topology_key);
+      if (kit != st->pair_num.end()) {
+        auto it = kit->second.find(*v);
+        if (it != kit->second.end()) num = it->second;
+      }
       if (num + self - min_num > c.max_skew)
         return Status::unschedulable("node(s) didn't match pod topology spread constraints");
     }
@@ -210,33 +252,40 @@ class PodTopologySpread : public Plugin {
       s.write(kScoreKey, st);
       return {};
     }
-    std::vector<int64_t> size(st->constraints.size(), 0);
+    const size_t C = st->constraints.size();
+    std::vector<int64_t> size(C, 0);
     for (const auto& ni : nodes) {
       const Node& n = *ni->node;
       if (!has_all_keys(n, st->constraints)) {
         st->ignored.insert(n.name());
         continue;
       }
-      for (size_t i = 0; i < st->constraints.size(); ++i) {
+      for (size_t i = 0; i < C; ++i) {
         const auto& c = st->constraints[i];
         if (c.topology_key == kHostnameLabel) {
           ++size[i];
           continue;
         }
-        auto [it, fresh] = st->pair_count.emplace(pair_key(c.topology_key, *n.meta.label(c.topology_key)), 0);
+        auto [it, fresh] = st->pair_count[c.topology_key].emplace(*n.meta.label(c.topology_key), 0);
         if (fresh) ++size[i];
       }
     }
     for (int64_t sz : size) st->weight.push_back(std::log(static_cast<double>(sz + 2)));
     if (h_.snapshot) {
-      for (const auto& ni : h_.snapshot->nodes) {
-        const Node& n = *ni->node;
-        if (!pod_matches_node_selector_and_affinity(p, n) || !has_all_keys(n, st->constraints)) continue;
-        for (const auto& c : st->constraints) {
-          if (c.topology_key == kHostnameLabel) continue;
-          auto it = st->pair_count.find(pair_key(c.topology_key, *n.meta.label(c.topology_key)));
-          if (it == st->pair_count.end()) continue;
-          it->second += count_matching(ni->pods, c.selector, p.ns());
+      const auto& all = h_.snapshot->nodes;
+      thread_local std::vector<int64_t> counts;
+      count_per_node(h_.parallelizer, all, st->constraints, p.ns(), [&](const NodeInfo& ni) {
+        return pod_matches_node_selector_and_affinity(p, *ni.node) && has_all_keys(*ni.node, st->constraints);
+      }, counts);
+      for (size_t c = 0; c < C; ++c) {
+        const auto& key = st->constraints[c].topology_key;
+        if (key == kHostnameLabel) continue;
+        auto kit = st->pair_count.find(key);
+        if (kit == st->pair_count.end()) continue;
+        for (size_t i = 0; i < all.size(); ++i) {
+          if (counts[i * C + c] < 0) continue;
+          auto it = kit->second.find(*all[i]->node->meta.label(key));
+          if (it != kit->second.end()) it->second += counts[i * C + c];
         }
       }
     }
@@ -257,8 +306,12 @@ class PodTopologySpread : public Plugin {
       if (c.topology_key == kHostnameLabel) {
         cnt = count_matching(ni.pods, c.selector, p.ns());
       } else {
-        auto it = st->pair_count.find(pair_key(c.topology_key, *v));
-        cnt = it == st->pair_count.end() ? 0 : it->second;
+        cnt = 0;
+        auto kit = st->pair_count.find(c.topology_key);
+        if (kit != st->pair_count.end()) {
+          auto it = kit->second.find(*v);
+          if (it != kit->second.end()) cnt = it->second;
+        }
       }
       score += static_cast<double>(cnt) * st->weight[i] + static_cast<double>(c.max_skew - 1);
     }
@@ -299,24 +352,26 @@ class PodTopologySpread : public Plugin {
 };
 
 // ====================================================== InterPodAffinity ====
-using PairCounts = std::unordered_map<std::string, int64_t>;
-
 struct AffinityFilterState : StateData {
-  PairCounts existing_anti, affinity, anti;
+  TopoCounts existing_anti, affinity, anti;
   std::shared_ptr<StateData> clone() const override { return std::make_shared<AffinityFilterState>(*this); }
+  void merge(const AffinityFilterState& o) {
+    merge_into(existing_anti, o.existing_anti);
+    merge_into(affinity, o.affinity);
+    merge_into(anti, o.anti);
+  }
+  static void merge_into(TopoCounts& dst, const TopoCounts& src) {
+    for (const auto& [k, vals] : src)
+      for (const auto& [v, c] : vals) topo_add(dst, k, v, c);
+  }
 };
 struct AffinityScoreState : StateData {
   std::unordered_map<std::string, std::unordered_map<std::string, int64_t>> topo_score;  // key -> value -> score
   std::shared_ptr<StateData> clone() const override { return std::make_shared<AffinityScoreState>(*this); }
 };
 
-void bump(PairCounts& m, const Node& n, const std::string& key, int64_t v) {
-  const std::string* tv = n.meta.label(key);
-  if (!tv) return;
-  std::string k = pair_key(key, *tv);
-  int64_t& c = m[k];
-  c += v;
-  if (c == 0) m.erase(k);
+void bump(TopoCounts& m, const Node& n, const std::string& key, int64_t v) {
+  if (const std::string* tv = n.meta.label(key)) topo_add(m, key, *tv, v);
 }
 
 class InterPodAffinity : public Plugin {
@@ -392,21 +447,40 @@ class InterPodAffinity : public Plugin {
       return {};
     }
     auto st = std::make_shared<AffinityFilterState>();
-    if (h_.snapshot) {
-      for (const auto& ni : h_.snapshot->have_pods_with_required_anti_affinity)
-        for (const auto& q : ni->pods_with_required_anti_affinity)
+    // Existing pods' required anti-affinity against p, and p's own required
+    // terms against every existing pod: O(pods in the cluster) term matches,
+    // split into node chunks on the Parallelizer (as upstream's PreFilter
+    // fans out over nodes) and merged.
+    const auto& anti_nodes = h_.snapshot->have_pods_with_required_anti_affinity;
+    const auto& all = h_.snapshot->nodes;
+    const bool own = !p.pod_affinity_required.empty() || !p.pod_anti_affinity_required.empty();
+    const size_t work = anti_nodes.size() + (own ? all.size() : 0);
+    const int chunks = h_.parallelizer && work >= 512 ? 16 : 1;
+    std::vector<AffinityFilterState> part(chunks);
+    auto run = [&](int k) {
+      AffinityFilterState& ps = part[k];
+      for (size_t i = anti_nodes.size() * k / chunks; i < anti_nodes.size() * (k + 1) / chunks; ++i) {
+        const NodeInfo& ni = *anti_nodes[i];
+        for (const auto& q : ni.pods_with_required_anti_affinity)
           for (const auto& t : q->pod_anti_affinity_required)
-            if (term_matches(t, q->ns(), p)) bump(st->existing_anti, *ni->node, t.topology_key, 1);
-      if (!p.pod_affinity_required.empty() || !p.pod_anti_affinity_required.empty()) {
-        for (const auto& ni : h_.snapshot->nodes)
-          for (const auto& q : ni->pods) {
-            if (matches_all(p.pod_affinity_required, p.ns(), *q))
-              for (const auto& t : p.pod_affinity_required) bump(st->affinity, *ni->node, t.topology_key, 1);
-            for (const auto& t : p.pod_anti_affinity_required)
-              if (term_matches(t, p.ns(), *q)) bump(st->anti, *ni->node, t.topology_key, 1);
-          }
+            if (term_matches(t, q->ns(), p)) bump(ps.existing_anti, *ni.node, t.topology_key, 1);
       }
-    }
+      if (!own) return;
+      for (size_t i = all.size() * k / chunks; i < all.size() * (k + 1) / chunks; ++i) {
+        const NodeInfo& ni = *all[i];
+        for (const auto& q : ni.pods) {
+          if (matches_all(p.pod_affinity_required, p.ns(), *q))
+            for (const auto& t : p.pod_affinity_required) bump(ps.affinity, *ni.node, t.topology_key, 1);
+          for (const auto& t : p.pod_anti_affinity_required)
+            if (term_matches(t, p.ns(), *q)) bump(ps.anti, *ni.node, t.topology_key, 1);
+        }
+      }
+    };
+    if (chunks > 1)
+      h_.parallelizer->until(chunks, run);
+    else
+      run(0);
+    for (const auto& ps : part) st->merge(ps);
     s.write(kFilterKey, st);
     return {};
   }
@@ -430,8 +504,7 @@ class InterPodAffinity : public Plugin {
       for (const auto& t : p.pod_affinity_required) {
         const std::string* v = n.meta.label(t.topology_key);
         if (!v) return Status::unresolvable("node(s) didn't match pod affinity rules");
-        auto it = st->affinity.find(pair_key(t.topology_key, *v));
-        if (it == st->affinity.end() || it->second <= 0) exist = false;
+        if (topo_get(st->affinity, t.topology_key, *v) <= 0) exist = false;
       }
       // The first pod of a self-affine series may go anywhere.
       if (!exist && !(st->affinity.empty() && matches_all(p.pod_affinity_required, p.ns(), p)))
@@ -442,17 +515,18 @@ class InterPodAffinity : public Plugin {
       for (const auto& t : p.pod_anti_affinity_required) {
         const std::string* v = n.meta.label(t.topology_key);
         if (!v) continue;
-        auto it = st->anti.find(pair_key(t.topology_key, *v));
-        if (it != st->anti.end() && it->second > 0)
+        if (topo_get(st->anti, t.topology_key, *v) > 0)
           return Status::unschedulable("node(s) didn't match pod anti-affinity rules");
       }
     // satisfyExistingPodsAntiAffinity
-    if (!st->existing_anti.empty())
-      for (const auto& [k, v] : n.meta.labels) {
-        auto it = st->existing_anti.find(pair_key(k, v));
-        if (it != st->existing_anti.end() && it->second > 0)
-          return Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
-      }
+    // (per topology key counted, the node's value for it: no key strings built)
+    for (const auto& [key, values] : st->existing_anti) {
+      const std::string* v = n.meta.label(key);
+      if (!v) continue;
+      auto it = values.find(*v);
+      if (it != values.end() && it->second > 0)
+        return Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
+    }
     return {};
   }
 
