@@ -41,6 +41,19 @@ def _wait_bound(sched, target: int, timeout: float) -> bool:
     return True
 
 
+def _spec(name: str, nodes: list[dict], init_pods: list[dict], pods: list[dict], *, config=None, options=None,
+          extra_objects: dict | None = None) -> dict:
+    """A workload: everything needed to run it here or in the native stress
+    driver (tools/stress.py --workload)."""
+    return {"name": name, "nodes": nodes, "init_pods": init_pods, "pods": pods, "config": config,
+            "options": options or {}, "extra_objects": extra_objects or {}}
+
+
+def run_spec(w: dict, timeout: float = 120.0) -> dict:
+    return _run(w["name"], w["nodes"], w["init_pods"], w["pods"], config=w["config"], options=w["options"],
+                extra_objects=w["extra_objects"], timeout=timeout)
+
+
 def _run(name: str, nodes: list[dict], init_pods: list[dict], pods: list[dict], *, config=None, options=None,
          extra_objects: dict | None = None, expect_bound: int | None = None, timeout: float = 120.0) -> dict:
     store = Store()
@@ -75,7 +88,7 @@ def _run(name: str, nodes: list[dict], init_pods: list[dict], pods: list[dict], 
 def scheduling_basic(n_nodes: int, n_pods: int) -> dict:
     init = [make_pod(f"init-{i}", requests={"cpu": "100m", "memory": "100Mi"}) for i in range(n_nodes)]
     pods = [make_pod(f"p-{i}", requests={"cpu": "100m", "memory": "100Mi"}) for i in range(n_pods)]
-    return _run("SchedulingBasic", _nodes_plain(n_nodes), init, pods)
+    return _spec("SchedulingBasic", _nodes_plain(n_nodes), init, pods)
 
 
 def pod_anti_affinity(n_nodes: int, n_pods: int) -> dict:
@@ -84,7 +97,7 @@ def pod_anti_affinity(n_nodes: int, n_pods: int) -> dict:
         {"labelSelector": {"matchLabels": {"color": "green"}}, "topologyKey": "kubernetes.io/hostname"}]}}
     pods = [make_pod(f"aa-{i}", requests={"cpu": "100m", "memory": "100Mi"}, labels={"color": "green"}, affinity=aff)
             for i in range(n)]
-    return _run("SchedulingPodAntiAffinity", _nodes_plain(n_nodes), [], pods)
+    return _spec("SchedulingPodAntiAffinity", _nodes_plain(n_nodes), [], pods)
 
 
 def topology_spreading(n_nodes: int, n_pods: int) -> dict:
@@ -94,14 +107,14 @@ def topology_spreading(n_nodes: int, n_pods: int) -> dict:
                                                    "whenUnsatisfiable": "DoNotSchedule",
                                                    "labelSelector": {"matchLabels": {"app": "spread"}}}]
         return p
-    return _run("TopologySpreading", _nodes_plain(n_nodes), [], [pod(i) for i in range(n_pods)])
+    return _spec("TopologySpreading", _nodes_plain(n_nodes), [], [pod(i) for i in range(n_pods)])
 
 
 def node_affinity(n_nodes: int, n_pods: int) -> dict:
     aff = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
         {"matchExpressions": [{"key": "disktype", "operator": "In", "values": ["ssd"]}]}]}}}
     pods = [make_pod(f"na-{i}", requests={"cpu": "100m", "memory": "100Mi"}, affinity=aff) for i in range(n_pods)]
-    return _run("SchedulingNodeAffinity", _nodes_plain(n_nodes), [], pods)
+    return _spec("SchedulingNodeAffinity", _nodes_plain(n_nodes), [], pods)
 
 
 def preemption_basic(n_nodes: int, n_pods: int) -> dict:
@@ -110,7 +123,7 @@ def preemption_basic(n_nodes: int, n_pods: int) -> dict:
     n = min(n_pods, n_nodes)
     init = [make_pod(f"low-{i}", requests={"cpu": "8", "memory": "1Gi"}, priority=1) for i in range(4 * n_nodes)]
     pods = [make_pod(f"high-{i}", requests={"cpu": "8", "memory": "1Gi"}, priority=1000) for i in range(n)]
-    return _run("PreemptionBasic", _nodes_plain(n_nodes), init, pods,
+    return _spec("PreemptionBasic", _nodes_plain(n_nodes), init, pods,
                 options={"podInitialBackoffSeconds": 0.01, "podMaxBackoffSeconds": 0.1})
 
 
@@ -121,7 +134,7 @@ def mi355x_flexgpu_mix(n_nodes: int, n_pods: int) -> dict:
         k = i % 4
         lim = {GPU: "1"} if k == 0 else {GPU_XCD: "2"} if k == 1 else {GPU_MEMORY: "24"} if k == 2 else {}
         pods.append(make_pod(f"g-{i}", requests={"cpu": "1", "memory": "4Gi"}, limits=lim or None))
-    return _run("MI355X-FlexGPUMix", nodes, [], pods, config=flagship_config())
+    return _spec("MI355X-FlexGPUMix", nodes, [], pods, config=flagship_config())
 
 
 def mi355x_gangs(n_nodes: int, n_pods: int) -> dict:
@@ -131,7 +144,7 @@ def mi355x_gangs(n_nodes: int, n_pods: int) -> dict:
     pgs = [make_pod_group(f"gang-{g}", "default", size) for g in range(groups)]
     pods = [make_pod(f"r-{g}-{r}", pod_group=f"gang-{g}", requests={"cpu": "8", "memory": "64Gi"}, limits={GPU: "1"})
             for g in range(groups) for r in range(size)]
-    return _run("MI355X-Gang8", nodes, [], pods, config=flagship_config(), extra_objects={"podgroups": pgs})
+    return _spec("MI355X-Gang8", nodes, [], pods, config=flagship_config(), extra_objects={"podgroups": pgs})
 
 
 WORKLOADS = {
@@ -159,7 +172,7 @@ def main() -> int:
         if a.only and name not in a.only:
             continue
         try:
-            r = fn(a.nodes, a.pods)
+            r = run_spec(fn(a.nodes, a.pods))
         except Exception as e:  # noqa: BLE001 - one workload failing must not hide the others
             r = {"workload": name, "error": f"{type(e).__name__}: {e}"}
         print(json.dumps(r), flush=True)

@@ -24,13 +24,37 @@ def write_inputs(out: str | Path, nodes: int = 64, seed: int = 0, options: dict 
     return d
 
 
+def write_workload(out: str | Path, name: str, nodes: int, pods: int, options: dict | None = None) -> Path:
+    """A tools/sched_perf.py workload as stress-driver input: the measured
+    pods form every wave (init pods are not replayed)."""
+    from .sched_perf import WORKLOADS
+
+    w = WORKLOADS[name](nodes, pods)
+    d = Path(out)
+    d.mkdir(parents=True, exist_ok=True)
+    (d / "nodes.json").write_text(json.dumps(w["nodes"]))
+    (d / "nrts.json").write_text("[]")
+    cfg = load_config(w["config"]).to_native(**{**w["options"], **(options or {})})
+    (d / "config.json").write_text(json.dumps(cfg))
+    ns = w["pods"][0]["metadata"].get("namespace", "default")
+    for i in range(4):
+        (d / f"wave_{i}.json").write_text(json.dumps({"namespace": ns, "podgroups": w["extra_objects"].get("podgroups", []),
+                                                      "pods": w["pods"]}))
+    return d
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
     ap.add_argument("--nodes", type=int, default=64)
+    ap.add_argument("--pods", type=int, default=1000, help="pods per wave (--workload only)")
+    ap.add_argument("--workload", default="", help="a tools/sched_perf.py workload instead of the bench waves")
     ap.add_argument("--parallelism", type=int, default=16)
     a = ap.parse_args()
-    write_inputs(a.out, a.nodes, options={"parallelism": a.parallelism})
+    if a.workload:
+        write_workload(a.out, a.workload, a.nodes, a.pods, options={"parallelism": a.parallelism})
+    else:
+        write_inputs(a.out, a.nodes, options={"parallelism": a.parallelism})
 
 
 if __name__ == "__main__":
