@@ -497,6 +497,7 @@ std::shared_ptr<Node> Node::from_json(const Json& obj) {
     n->taints.push_back(Taint{t["key"].as_string(), t["value"].as_string(), t["effect"].as_string()});
     if (n->taints.back().effect == "PreferNoSchedule") n->has_prefer_no_schedule = true;
   }
+  if (const std::string* h = n->meta.label(kHostnameLabel)) n->foreign_hostname = *h != n->meta.name;
   for (const auto& im : status["images"].items()) {
     ContainerImage ci;
     for (const auto& nm : im["names"].items()) ci.names.push_back(nm.as_string());

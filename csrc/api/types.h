@@ -36,6 +36,8 @@ using StrMap = std::vector<std::pair<std::string, std::string>>;  // small, orde
 const std::string* strmap_get(const StrMap& m, std::string_view k);
 StrMap strmap_from_json(const Json& j);
 
+inline constexpr const char* kHostnameLabel = "kubernetes.io/hostname";
+
 struct ObjectMeta {
   std::string ns, name, uid;
   int64_t resource_version = 0;
@@ -247,6 +249,9 @@ struct Node {
   // PreferNoSchedule. The cache keeps cluster-wide counts of both.
   std::unordered_map<std::string, int64_t> image_sizes;
   bool has_prefer_no_schedule = false;
+  // kubernetes.io/hostname label present and different from the node name:
+  // then hostname topology domains may span nodes (see Snapshot).
+  bool foreign_hostname = false;
   // MI355X GPU topology as published by the node agent (see flexgpu.cc).
   int gpu_count = 0;
   std::vector<int> gpu_partitions;  // partitions per physical GPU (1 = SPX .. 8 = CPX)

@@ -19,6 +19,7 @@ Parallelizer::~Parallelizer() {
   {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;
+    pub_gen_.fetch_add(1, std::memory_order_release);  // ends spins
   }
   cv_.notify_all();
   for (auto& t : threads_) t.join();
@@ -30,6 +31,7 @@ int64_t Parallelizer::now_ns() {
 }
 
 namespace {
+inline void cpu_relax() { __builtin_ia32_pause(); }
 void ema(std::atomic<int64_t>& v, int64_t sample, bool seed) {
   int64_t cur = v.load(std::memory_order_relaxed);
   v.store(seed ? sample : cur + (sample - cur) / 8, std::memory_order_relaxed);  // alpha 1/8
@@ -62,20 +64,30 @@ int Parallelizer::run_job(Job& job) {
 void Parallelizer::worker_loop() {
   uint64_t seen = 0;
   for (;;) {
+    if (spinners_.fetch_add(1, std::memory_order_relaxed) < kMaxSpinners) {
+      int64_t end = now_ns() + kSpinNs;
+      while (pub_gen_.load(std::memory_order_acquire) == seen && now_ns() < end) cpu_relax();
+    }
+    spinners_.fetch_sub(1, std::memory_order_relaxed);
     Job* job = nullptr;
+    bool wake_next = false;
     {
       std::unique_lock<std::mutex> lk(mu_);
+      ++sleepers_;
       cv_.wait(lk, [&] { return stop_ || (job_ != nullptr && job_gen_ != seen && job_->seats > 0); });
+      --sleepers_;
       if (stop_) return;
       seen = job_gen_;
       job = job_;
       --job->seats;
       job->active.fetch_add(1);
+      wake_next = job->seats > 0 && sleepers_ > 0;
     }
+    if (wake_next) cv_.notify_one();
     run_job(*job);
     if (job->active.fetch_sub(1) == 1) {
       std::lock_guard<std::mutex> g(mu_);
-      done_cv_.notify_all();
+      if (caller_waiting_) done_cv_.notify_one();
     }
   }
 }
@@ -129,22 +141,33 @@ void Parallelizer::until_forked(int n, const std::function<void(int)>& fn, const
   // chunkSizeFor: sqrt(n), capped so every participant gets work.
   job.chunk = std::max(1, std::min(static_cast<int>(std::sqrt(static_cast<double>(n))), n / (helpers + 1)));
   job.active.store(1);  // the caller
+  int wake = 0;
   {
     std::lock_guard<std::mutex> g(mu_);
     job_ = &job;
     ++job_gen_;
+    pub_gen_.store(job_gen_, std::memory_order_release);
+    int spinning = static_cast<int>(threads_.size()) - sleepers_;
+    if (helpers > spinning) wake = std::min({2, helpers - spinning, sleepers_});
   }
-  if (helpers >= static_cast<int>(threads_.size()))
-    cv_.notify_all();
-  else
-    for (int i = 0; i < helpers; ++i) cv_.notify_one();
+  for (int i = 0; i < wake; ++i) cv_.notify_one();
   // Per-item cost is learned from inline runs only (the periodic probes):
   // the caller's items in a parallel run are inflated by contention.
   run_job(job);
-  std::unique_lock<std::mutex> lk(mu_);
-  job_ = nullptr;  // no new worker can join after this point
-  job.active.fetch_sub(1);
-  done_cv_.wait(lk, [&] { return job.active.load() == 0; });
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    job_ = nullptr;  // no new worker can join after this point
+  }
+  if (job.active.fetch_sub(1, std::memory_order_acq_rel) != 1) {
+    int64_t end = now_ns() + kSpinNs;
+    while (job.active.load(std::memory_order_acquire) != 0 && now_ns() < end) cpu_relax();
+    if (job.active.load(std::memory_order_acquire) != 0) {
+      std::unique_lock<std::mutex> lk(mu_);
+      caller_waiting_ = true;
+      done_cv_.wait(lk, [&] { return job.active.load() == 0; });
+      caller_waiting_ = false;
+    }
+  }
   if (site) observe_done(site, std::min(job.n, job.next.load(std::memory_order_relaxed)), job.n);
 }
 

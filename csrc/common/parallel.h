@@ -82,6 +82,17 @@ class Parallelizer {
   uint64_t job_gen_ = 0;
   bool stop_ = false;
   std::mutex call_mu_;  // one job at a time
+  // The fork/join phases of one scheduling cycle (PreFilter, Filter, Score)
+  // come back to back, so a few workers spin briefly for the next job and the
+  // caller spins briefly for the join: both skip a futex round trip. Sleepers
+  // are woken in a chain (each helper that takes a seat wakes the next), so
+  // the caller pays at most two wake-ups per fork.
+  static constexpr int64_t kSpinNs = 30'000;
+  static constexpr int kMaxSpinners = 4;
+  std::atomic<uint64_t> pub_gen_{0};  // job_gen_, readable without mu_
+  std::atomic<int> spinners_{0};
+  int sleepers_ = 0;             // guarded by mu_
+  bool caller_waiting_ = false;  // guarded by mu_
 };
 
 }  // namespace xsched

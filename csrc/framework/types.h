@@ -212,13 +212,24 @@ struct Snapshot {
   std::vector<NodeInfoPtr> nodes;  // in cache order
   std::unordered_map<std::string, NodeInfoPtr> by_name;
   std::unordered_map<std::string, size_t> index;  // name -> position in `nodes`
+  // Nodes with affinity / required anti-affinity pods, in no particular
+  // order. Kept incrementally by the cache: *_pos[i] is node i's slot in the
+  // list (-1 if absent) and *_idx the reverse, so a refresh touches only the
+  // nodes that changed instead of rescanning every node.
   std::vector<NodeInfoPtr> have_pods_with_affinity;
   std::vector<NodeInfoPtr> have_pods_with_required_anti_affinity;
+  std::vector<int32_t> affinity_pos, anti_pos;
+  std::vector<uint32_t> affinity_idx, anti_idx;
   int64_t generation = 0;
   uint64_t node_epoch = 0;  // bumped on any Node object / node-set change (not on pod changes)
   // Nodes carrying at least one PreferNoSchedule taint, kept by the cache as
   // Nodes change. Zero lets TaintToleration skip its Score pass.
   int64_t nodes_with_prefer_no_schedule = 0;
+  // No node carries a kubernetes.io/hostname label other than its own name,
+  // so a hostname topology domain is exactly one node: InterPodAffinity then
+  // evaluates hostname-keyed anti-affinity on the node's own pods instead of
+  // counting them cluster-wide in PreFilter.
+  bool hostname_domains_are_nodes = true;
   // Image name -> number of nodes listing it (upstream ImageStateSummary.
   // NumNodes), published with the same refresh as `nodes`, so ImageLocality's
   // score and its all-zero skip read one consistent view. Never null.

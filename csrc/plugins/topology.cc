@@ -35,9 +35,6 @@
 namespace xsched {
 namespace {
 
-const char* kHostnameLabel = "kubernetes.io/hostname";
-
-
 int64_t count_matching(const std::vector<PodPtr>& pods, const LabelSelector& sel, const std::string& ns) {
   int64_t n = 0;
   for (const auto& q : pods)
@@ -430,14 +427,23 @@ class InterPodAffinity : public Plugin {
     return true;
   }
 
+  // Required anti-affinity terms whose topology domain is a single node
+  // (hostname key, Snapshot::hostname_domains_are_nodes) are not counted in
+  // the PreFilter state: Filter checks them against the node's own pods, so
+  // PreFilter does no per-pod map work for the common "one per node" rule.
+  bool counted(const PodAffinityTerm& t) const {
+    return !(h_.snapshot && h_.snapshot->hostname_domains_are_nodes && t.topology_key == kHostnameLabel);
+  }
+
   // updateWithPod: `q` (existing) entering/leaving node `n` for incoming `p`.
+  // Callers add/remove q on the NodeInfo too, which node-local terms read.
   void update(AffinityFilterState& st, const Pod& p, const Pod& q, const Node& n, int64_t d) const {
     for (const auto& t : q.pod_anti_affinity_required)
-      if (term_matches(t, q.ns(), p)) bump(st.existing_anti, n, t.topology_key, d);
+      if (counted(t) && term_matches(t, q.ns(), p)) bump(st.existing_anti, n, t.topology_key, d);
     if (matches_all(p.pod_affinity_required, p.ns(), q))
       for (const auto& t : p.pod_affinity_required) bump(st.affinity, n, t.topology_key, d);
     for (const auto& t : p.pod_anti_affinity_required)
-      if (term_matches(t, p.ns(), q)) bump(st.anti, n, t.topology_key, d);
+      if (counted(t) && term_matches(t, p.ns(), q)) bump(st.anti, n, t.topology_key, d);
   }
 
   Status pre_filter(CycleState& s, const Pod& p) override {
@@ -453,7 +459,8 @@ class InterPodAffinity : public Plugin {
     // fans out over nodes) and merged.
     const auto& anti_nodes = h_.snapshot->have_pods_with_required_anti_affinity;
     const auto& all = h_.snapshot->nodes;
-    const bool own = !p.pod_affinity_required.empty() || !p.pod_anti_affinity_required.empty();
+    bool own = !p.pod_affinity_required.empty();
+    for (const auto& t : p.pod_anti_affinity_required) own = own || counted(t);
     const size_t work = anti_nodes.size() + (own ? all.size() : 0);
     const int chunks = h_.parallelizer && work >= 512 ? 16 : 1;
     std::vector<AffinityFilterState> part(chunks);
@@ -463,7 +470,7 @@ class InterPodAffinity : public Plugin {
         const NodeInfo& ni = *anti_nodes[i];
         for (const auto& q : ni.pods_with_required_anti_affinity)
           for (const auto& t : q->pod_anti_affinity_required)
-            if (term_matches(t, q->ns(), p)) bump(ps.existing_anti, *ni.node, t.topology_key, 1);
+            if (counted(t) && term_matches(t, q->ns(), p)) bump(ps.existing_anti, *ni.node, t.topology_key, 1);
       }
       if (!own) return;
       for (size_t i = all.size() * k / chunks; i < all.size() * (k + 1) / chunks; ++i) {
@@ -472,7 +479,7 @@ class InterPodAffinity : public Plugin {
           if (matches_all(p.pod_affinity_required, p.ns(), *q))
             for (const auto& t : p.pod_affinity_required) bump(ps.affinity, *ni.node, t.topology_key, 1);
           for (const auto& t : p.pod_anti_affinity_required)
-            if (term_matches(t, p.ns(), *q)) bump(ps.anti, *ni.node, t.topology_key, 1);
+            if (counted(t) && term_matches(t, p.ns(), *q)) bump(ps.anti, *ni.node, t.topology_key, 1);
         }
       }
     };
@@ -511,15 +518,26 @@ class InterPodAffinity : public Plugin {
         return Status::unresolvable("node(s) didn't match pod affinity rules");
     }
     // satisfyPodAntiAffinity
-    if (!st->anti.empty())
-      for (const auto& t : p.pod_anti_affinity_required) {
+    for (const auto& t : p.pod_anti_affinity_required) {
+      if (counted(t)) {
+        if (st->anti.empty()) continue;
         const std::string* v = n.meta.label(t.topology_key);
-        if (!v) continue;
-        if (topo_get(st->anti, t.topology_key, *v) > 0)
+        if (v && topo_get(st->anti, t.topology_key, *v) > 0)
           return Status::unschedulable("node(s) didn't match pod anti-affinity rules");
+      } else if (n.meta.label(kHostnameLabel)) {
+        for (const auto& q : ni.pods)
+          if (term_matches(t, p.ns(), *q))
+            return Status::unschedulable("node(s) didn't match pod anti-affinity rules");
       }
-    // satisfyExistingPodsAntiAffinity
-    // (per topology key counted, the node's value for it: no key strings built)
+    }
+    // satisfyExistingPodsAntiAffinity: node-local terms of the node's own pods,
+    // then per counted topology key the node's value (no key strings built).
+    if (!ni.pods_with_required_anti_affinity.empty() && h_.snapshot && h_.snapshot->hostname_domains_are_nodes &&
+        n.meta.label(kHostnameLabel))
+      for (const auto& q : ni.pods_with_required_anti_affinity)
+        for (const auto& t : q->pod_anti_affinity_required)
+          if (!counted(t) && term_matches(t, q->ns(), p))
+            return Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
     for (const auto& [key, values] : st->existing_anti) {
       const std::string* v = n.meta.label(key);
       if (!v) continue;

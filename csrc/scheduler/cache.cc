@@ -39,6 +39,7 @@ void SchedulerCache::group_delta(const Pod& p, int d) {
 
 void SchedulerCache::account_node(const Node* old_node, const Node* new_node) {
   prefer_nodes_ += (new_node && new_node->has_prefer_no_schedule) - (old_node && old_node->has_prefer_no_schedule);
+  foreign_hostnames_ += (new_node && new_node->foreign_hostname) - (old_node && old_node->foreign_hostname);
   const bool old_imgs = old_node && !old_node->image_sizes.empty();
   const bool new_imgs = new_node && !new_node->image_sizes.empty();
   if (!old_imgs && !new_imgs) return;  // heartbeat-style updates of image-less nodes cost nothing
@@ -284,6 +285,41 @@ PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::f
   return mutate_pod(uid, fn);
 }
 
+namespace {
+// Keeps node i's membership in one of the Snapshot's affinity lists in step
+// with its current NodeInfo version (swap-remove on leave).
+void sync_member(std::vector<NodeInfoPtr>& list, std::vector<int32_t>& pos, std::vector<uint32_t>& idx, size_t i,
+                 const NodeInfoPtr& ni, bool want) {
+  int32_t p = pos[i];
+  if (want) {
+    if (p >= 0) {
+      if (list[p] != ni) list[p] = ni;
+    } else {
+      pos[i] = static_cast<int32_t>(list.size());
+      list.push_back(ni);
+      idx.push_back(static_cast<uint32_t>(i));
+    }
+  } else if (p >= 0) {
+    size_t last = list.size() - 1;
+    if (static_cast<size_t>(p) != last) {
+      list[p] = std::move(list[last]);
+      idx[p] = idx[last];
+      pos[idx[p]] = p;
+    }
+    list.pop_back();
+    idx.pop_back();
+    pos[i] = -1;
+  }
+}
+
+void sync_affinity_lists(Snapshot& s, size_t i) {
+  const NodeInfoPtr& ni = s.nodes[i];
+  sync_member(s.have_pods_with_affinity, s.affinity_pos, s.affinity_idx, i, ni, !ni->pods_with_affinity.empty());
+  sync_member(s.have_pods_with_required_anti_affinity, s.anti_pos, s.anti_idx, i, ni,
+              !ni->pods_with_required_anti_affinity.empty());
+}
+}  // namespace
+
 int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const std::string* check_assumed,
                                     bool* is_assumed) {
   int64_t t0 = lock_wait_us ? clock_->now_us() : 0;
@@ -291,7 +327,6 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
   if (lock_wait_us) *lock_wait_us = clock_->now_us() - t0;
   if (check_assumed && is_assumed) *is_assumed = assumed_.count(*check_assumed) > 0;
   int clones = 0;
-  bool affinity_dirty = false;
   if (structure_changed_) {
     for (auto& ni : s.nodes) s.retired.push_back(std::move(ni));
     s.nodes.clear();
@@ -308,7 +343,13 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
       s.by_name[name] = cl;
     }
     structure_changed_ = false;
-    affinity_dirty = true;
+    s.have_pods_with_affinity.clear();
+    s.have_pods_with_required_anti_affinity.clear();
+    s.affinity_idx.clear();
+    s.anti_idx.clear();
+    s.affinity_pos.assign(s.nodes.size(), -1);
+    s.anti_pos.assign(s.nodes.size(), -1);
+    for (size_t i = 0; i < s.nodes.size(); ++i) sync_affinity_lists(s, i);
   } else {
     for (const auto& name : dirty_) {
       auto it = nodes_.find(name);
@@ -316,29 +357,22 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
       auto sit = s.by_name.find(name);
       if (sit == s.by_name.end()) continue;
       const NodeInfoPtr& cl = it->second;
-      if (sit->second == cl) {
-        // Updated in place (assume/Reserve): the Snapshot already sees it.
-        if (!cl->pods_with_affinity.empty() || !cl->pods_with_required_anti_affinity.empty()) affinity_dirty = true;
-        continue;
+      size_t i = s.index[name];
+      // Same pointer: updated in place (assume/Reserve), the Snapshot
+      // already sees it; only its list membership may have changed.
+      if (sit->second != cl) {
+        ++clones;
+        s.retired.push_back(s.nodes[i]);
+        s.nodes[i] = cl;
+        sit->second = cl;
       }
-      ++clones;
-      if (!sit->second->pods_with_affinity.empty() || !cl->pods_with_affinity.empty()) affinity_dirty = true;
-      s.retired.push_back(s.nodes[s.index[name]]);
-      s.nodes[s.index[name]] = cl;
-      sit->second = cl;
+      sync_affinity_lists(s, i);
     }
   }
   dirty_.clear();
-  if (affinity_dirty) {
-    s.have_pods_with_affinity.clear();
-    s.have_pods_with_required_anti_affinity.clear();
-    for (const auto& ni : s.nodes) {
-      if (!ni->pods_with_affinity.empty()) s.have_pods_with_affinity.push_back(ni);
-      if (!ni->pods_with_required_anti_affinity.empty()) s.have_pods_with_required_anti_affinity.push_back(ni);
-    }
-  }
   s.generation = generation_;
   s.nodes_with_prefer_no_schedule = prefer_nodes_;
+  s.hostname_domains_are_nodes = foreign_hostnames_ == 0;
   if (s.image_spread != image_spread_) s.image_spread = image_spread_;
   s.node_epoch = node_epoch_;
   return clones;

@@ -118,6 +118,7 @@ class SchedulerCache {
   int64_t generation_ = 0;
   uint64_t node_epoch_ = 1;
   int64_t prefer_nodes_ = 0;
+  int64_t foreign_hostnames_ = 0;  // nodes whose hostname label is not their name
   // Copied on write while a snapshot still shares it.
   std::shared_ptr<std::unordered_map<std::string, int64_t>> image_spread_ =
       std::make_shared<std::unordered_map<std::string, int64_t>>();

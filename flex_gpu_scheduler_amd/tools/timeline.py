@@ -32,15 +32,18 @@ def timeline(nodes: int = 64, warmup: int = 4) -> dict:
             by[e["name"]].append(e)
         t0 = min(e["ts"] for e in ev)
         sched = sorted(by["schedule"], key=lambda e: e["ts"])
-        busy = sum(e["dur"] for e in by["schedule"]) + sum(e["dur"] for e in by["assume_reserve_permit"])
         first = sched[0]["ts"] - t0
         last_end = max(e["ts"] + e["dur"] for e in by["schedule"] + by["assume_reserve_permit"]) - t0
         ends = sorted((e["ts"], e["ts"] + e["dur"]) for e in by["schedule"] + by["assume_reserve_permit"])
+        # Busy = union of the spans (trace timestamps are rounded to 1 us, so
+        # adjacent spans can overlap by a tick and must not count twice).
         gaps = []
         cur = ends[0][1]
+        busy = ends[0][1] - ends[0][0]
         for s, e in ends[1:]:
             if s > cur:
                 gaps.append((s - cur, round((cur - t0) / 1e3, 3)))
+            busy += max(0, e - max(s, cur))
             cur = max(cur, e)
         gaps.sort(reverse=True)
         span = last_end - first

@@ -208,3 +208,30 @@ def test_image_locality(store):
     # 800 MiB present on 1 of 3 nodes: 800*1/3 = 266 MiB -> 100*(266-23)/(1000-23) = 24
     assert sc == {"warm": 24, "cold": 0, "warm2": 0}
     s.stop()
+
+
+def test_hostname_anti_affinity_node_local_and_shared_hostnames(store):
+    """Hostname-keyed anti-affinity is checked on the node's own pods while
+    every hostname label equals its node's name; once two nodes share a
+    hostname value the term is counted per domain again, as upstream does."""
+    for n in ("n1", "n2", "n3"):
+        store.create("nodes", node(n))
+    store.create("pods", pod("web", {"app": "web"}, "n1"))
+    store.create("pods", pod("guard", {"app": "guard"}, "n3", affinity={"podAntiAffinity": {
+        "requiredDuringSchedulingIgnoredDuringExecution": [term(HOST, app="noisy")]}}))
+    s = sched(store)
+    anti = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [term(HOST, app="web")]}}
+    assert sorted(s.explain(pod("p", {"app": "web"}, affinity=anti))["feasible"]) == ["n2", "n3"]
+    assert sorted(s.explain(pod("q", {"app": "noisy"}))["feasible"]) == ["n1", "n2"]
+    s.stop()
+    # n2 now reports n1's hostname: both form one domain.
+    shared = node("n2")
+    shared["metadata"]["labels"][HOST] = "n1"
+    store.update("nodes", shared)
+    shared3 = node("n3")
+    shared3["metadata"]["labels"][HOST] = "n1"
+    store.update("nodes", shared3)
+    s = sched(store)
+    assert s.explain(pod("p", {"app": "web"}, affinity=anti))["feasible"] == []
+    assert s.explain(pod("q", {"app": "noisy"}))["feasible"] == []
+    s.stop()
