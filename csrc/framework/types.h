@@ -8,6 +8,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -207,6 +208,17 @@ using NodeInfoPtr = std::shared_ptr<NodeInfo>;
 // path passes raw pointers instead of bumping shared refcounts per node.
 using NodeList = std::vector<const NodeInfo*>;
 
+// One pod entering (+1) or leaving (-1) a node's NodeInfo, as the cache
+// applied it, with the Node object of that moment. Plugins that count pods
+// cluster-wide in PreFilter (PodTopologySpread, InterPodAffinity) replay the
+// events since an earlier cycle to bring that cycle's state up to date
+// instead of recounting every pod of every node.
+struct PodDelta {
+  PodPtr pod;
+  NodePtr node;
+  int d = 0;
+};
+
 // ------------------------------------------------------------ Snapshot ----
 struct Snapshot {
   std::vector<NodeInfoPtr> nodes;  // in cache order
@@ -235,9 +247,28 @@ struct Snapshot {
   // score and its all-zero skip read one consistent view. Never null.
   std::shared_ptr<const std::unordered_map<std::string, int64_t>> image_spread =
       std::make_shared<const std::unordered_map<std::string, int64_t>>();
-  // Versions replaced by the last refreshes. Dropping one can free deleted
-  // pods, so the scheduler releases them off the scheduling thread.
+  // Bumped when a node joins or leaves or its labels change: pod counts per
+  // topology domain stay comparable across cycles while it holds.
+  uint64_t topology_epoch = 0;
+  // The most recent pod events (oldest first); delta_end is the sequence
+  // number one past deltas.back().
+  static constexpr size_t kMaxDeltas = 16384;
+  std::deque<PodDelta> deltas;
+  uint64_t delta_end = 0;
+  // Calls fn(delta) for each pod event after sequence `from` (a delta_end
+  // seen in an earlier cycle) and returns true, or returns false without
+  // calling fn when some of them have been trimmed.
+  template <typename Fn>
+  bool replay_since(uint64_t from, Fn&& fn) const {
+    if (from > delta_end || delta_end - from > deltas.size()) return false;
+    for (size_t i = deltas.size() - static_cast<size_t>(delta_end - from); i < deltas.size(); ++i) fn(deltas[i]);
+    return true;
+  }
+  // Versions replaced by the last refreshes (and trimmed pod events). Dropping
+  // one can free deleted pods, so the scheduler releases them off the
+  // scheduling thread.
   std::vector<NodeInfoPtr> retired;
+  std::vector<PodDelta> retired_deltas;
   NodeInfoPtr get(const std::string& name) const {
     auto it = by_name.find(name);
     return it == by_name.end() ? nullptr : it->second;

@@ -23,6 +23,7 @@
 // emptiness check per cycle (no per-node work).
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <shared_mutex>
@@ -57,6 +58,51 @@ template <typename T>
 std::shared_ptr<StateData> empty_state() {
   static T obj;
   return std::shared_ptr<StateData>(std::shared_ptr<StateData>(), &obj);
+}
+
+// PreFilter states kept across cycles (PodTopologySpread, InterPodAffinity).
+// Counting the pods that match a pod's terms walks every pod of the cluster;
+// a later pod with the same spec (and, where it matters, labels) in the same
+// namespace gets the earlier state brought up to date by replaying the pod
+// events since (Snapshot::replay_since), while the topology epoch (node set,
+// node labels) and `aux` (InterPodAffinity: namespace labels) are unchanged.
+//
+// Used only by PreFilter, which runs on the scheduling thread (cycle or
+// explain(), both under the scheduler's cycle lock). The reused object is the
+// one the previous cycle's CycleState points at: that cycle's Filter/Score
+// are over, binding cycles hold its CycleState but none of their plugins read
+// these states, and preemption / nominated-pod checks mutate clones.
+template <typename State>
+class StateMemo {
+ public:
+  struct Entry {
+    uint64_t key = 0, aux = 0, epoch = 0, seq = 0;
+    std::string ns;
+    std::shared_ptr<State> st;
+  };
+  Entry* find(uint64_t key, const std::string& ns, uint64_t aux, uint64_t epoch) {
+    for (auto& x : e_)
+      if (x.st && x.key == key && x.aux == aux && x.epoch == epoch && x.ns == ns) return &x;
+    return nullptr;
+  }
+  void put(uint64_t key, const std::string& ns, uint64_t aux, uint64_t epoch, uint64_t seq, std::shared_ptr<State> st) {
+    Entry* slot = nullptr;
+    for (auto& x : e_)
+      if (x.st && x.key == key && x.ns == ns) slot = &x;
+    if (!slot) slot = &e_[next_++ % e_.size()];
+    *slot = Entry{key, aux, epoch, seq, ns, std::move(st)};
+  }
+
+ private:
+  std::array<Entry, 8> e_;
+  size_t next_ = 0;
+};
+
+uint64_t labels_hash(const StrMap& m) {
+  uint64_t h = 1469598103934665603ULL;
+  std::hash<std::string> hs;
+  for (const auto& [k, v] : m) h = (h ^ hs(k)) * 1099511628211ULL ^ (hs(v) * 0x9E3779B97F4A7C15ULL);
+  return h;
 }
 
 // Topology key -> value -> count. Lookups take the node's own label strings,
@@ -109,6 +155,11 @@ struct SpreadFilterState : StateData {
   std::unordered_map<std::string, std::array<CriticalPath, 2>> critical;  // topology key -> two smallest
   std::shared_ptr<StateData> clone() const override { return std::make_shared<SpreadFilterState>(*this); }
 
+  void recompute_critical() {
+    for (auto& [key, p] : critical) p = {CriticalPath{}, CriticalPath{}};
+    for (const auto& [key, values] : pair_num)
+      for (const auto& [value, num] : values) update_critical(key, value, num);
+  }
   void update_critical(const std::string& key, const std::string& value, int64_t num) {
     auto& p = critical[key];
     int i = value == p[0].value ? 0 : value == p[1].value ? 1 : -1;
@@ -164,6 +215,18 @@ class PodTopologySpread : public Plugin {
       s.write(kFilterKey, empty_state<SpreadFilterState>());
       return {};
     }
+    if (h_.snapshot) {
+      const Snapshot& snap = *h_.snapshot;
+      if (auto* m = memo_.find(p.spec_hash, p.ns(), 0, snap.topology_epoch)) {
+        SpreadFilterState& ms = *m->st;
+        if (snap.replay_since(m->seq, [&](const PodDelta& d) { count_delta(ms, p, *d.pod, *d.node, d.d); })) {
+          m->seq = snap.delta_end;
+          ms.recompute_critical();
+          s.write(kFilterKey, m->st);
+          return {};
+        }
+      }
+    }
     auto st = std::make_shared<SpreadFilterState>();
     for (const auto& c : p.spread_constraints)
       if (c.hard) st->constraints.push_back(c);
@@ -182,11 +245,21 @@ class PodTopologySpread : public Plugin {
       for (const auto& c : st->constraints) st->critical[c.topology_key];
       for (const auto& [key, values] : st->pair_num)
         for (const auto& [value, num] : values) st->update_critical(key, value, num);
+      memo_.put(p.spec_hash, p.ns(), 0, h_.snapshot->topology_epoch, h_.snapshot->delta_end, st);
     }
     s.write(kFilterKey, st);
     return {};
   }
   bool has_pre_filter_extensions() const override { return true; }
+
+  // One pod event replayed into a memoized state: exactly what PreFilter's
+  // count would have added for it (count_matching on eligible nodes).
+  static void count_delta(SpreadFilterState& st, const Pod& p, const Pod& q, const Node& n, int d) {
+    if (q.terminating() || q.ns() != p.ns()) return;
+    if (!pod_matches_node_selector_and_affinity(p, n) || !has_all_keys(n, st.constraints)) return;
+    for (const auto& c : st.constraints)
+      if (c.selector.matches(q.meta.labels)) st.pair_num[c.topology_key][*n.meta.label(c.topology_key)] += d;
+  }
 
   void update_with_pod(CycleState& s, const Pod& preemptor, const Pod& q, const NodeInfo& ni, int64_t delta) {
     auto* st = s.read_as<SpreadFilterState>(kFilterKey);
@@ -346,6 +419,7 @@ class PodTopologySpread : public Plugin {
 
  private:
   Handle& h_;
+  StateMemo<SpreadFilterState> memo_;
 };
 
 // ====================================================== InterPodAffinity ====
@@ -397,6 +471,7 @@ class InterPodAffinity : public Plugin {
       ns_labels_.erase(md.name);
     else
       ns_labels_[md.name] = md.labels;
+    ns_version_.fetch_add(1, std::memory_order_release);
   }
   StrMap ns_labels(const std::string& ns) const {
     std::shared_lock<std::shared_mutex> g(ns_mu_);
@@ -452,6 +527,17 @@ class InterPodAffinity : public Plugin {
       s.write(kFilterKey, empty_state<AffinityFilterState>());
       return {};
     }
+    const Snapshot& snap = *h_.snapshot;
+    const uint64_t key = p.spec_hash ^ labels_hash(p.meta.labels);
+    const uint64_t nsv = ns_version_.load(std::memory_order_acquire);
+    if (auto* m = memo_.find(key, p.ns(), nsv, snap.topology_epoch)) {
+      AffinityFilterState& ms = *m->st;
+      if (snap.replay_since(m->seq, [&](const PodDelta& d) { update(ms, p, *d.pod, *d.node, d.d); })) {
+        m->seq = snap.delta_end;
+        s.write(kFilterKey, m->st);
+        return {};
+      }
+    }
     auto st = std::make_shared<AffinityFilterState>();
     // Existing pods' required anti-affinity against p, and p's own required
     // terms against every existing pod: O(pods in the cluster) term matches,
@@ -488,6 +574,7 @@ class InterPodAffinity : public Plugin {
     else
       run(0);
     for (const auto& ps : part) st->merge(ps);
+    memo_.put(key, p.ns(), nsv, snap.topology_epoch, snap.delta_end, st);
     s.write(kFilterKey, st);
     return {};
   }
@@ -616,6 +703,8 @@ class InterPodAffinity : public Plugin {
   int32_t hard_weight_ = 1;
   mutable std::shared_mutex ns_mu_;
   std::unordered_map<std::string, StrMap> ns_labels_;
+  std::atomic<uint64_t> ns_version_{0};  // memoized states depend on namespace labels
+  StateMemo<AffinityFilterState> memo_;
 };
 
 // ========================================================= ImageLocality ====

@@ -67,6 +67,7 @@ void SchedulerCache::set_node_locked(const NodePtr& n) {
   ++node_epoch_;
   auto& ni = info_for(n->name());
   bool was_ghost = ni->node == nullptr;
+  if (was_ghost || ni->node->meta.labels != n->meta.labels) ++topology_epoch_;
   account_node(ni->node.get(), n.get());
   writable(ni).set_node(n);
   if (was_ghost) {
@@ -91,6 +92,7 @@ void SchedulerCache::remove_node(const std::string& name) {
   auto it = nodes_.find(name);
   if (it == nodes_.end()) return;
   ++node_epoch_;
+  ++topology_epoch_;
   account_node(it->second->node.get(), nullptr);
   order_.erase(std::remove(order_.begin(), order_.end(), name), order_.end());
   structure_changed_ = true;
@@ -114,18 +116,31 @@ void SchedulerCache::set_nrt(const std::string& node, const NRTPtr& nrt) {
   mark_dirty(node);
 }
 
+// Pods on a ghost node (no Node object) are in no Snapshot and never
+// counted, so they need no event either: the Node's arrival bumps the
+// topology epoch.
+void SchedulerCache::record_delta(const PodPtr& p, const NodeInfo& ni, int d) {
+  if (!ni.node) return;
+  pending_deltas_.push_back(PodDelta{p, ni.node, d});
+  ++delta_seq_;
+}
+
 void SchedulerCache::add_pod_locked(const PodPtr& p) {
   auto& ni = info_for(p->node_name);
   writable(ni).add_pod(p);
   group_delta(*p, +1);
+  record_delta(p, *ni, +1);
   mark_dirty(p->node_name);
 }
 
-void SchedulerCache::remove_pod_locked(const Pod& p) {
-  auto it = nodes_.find(p.node_name);
+void SchedulerCache::remove_pod_locked(const PodPtr& p) {
+  auto it = nodes_.find(p->node_name);
   if (it == nodes_.end()) return;
-  if (writable(it->second).remove_pod(p.uid())) group_delta(p, -1);
-  mark_dirty(p.node_name);
+  if (writable(it->second).remove_pod(p->uid())) {
+    group_delta(*p, -1);
+    record_delta(p, *it->second, -1);
+  }
+  mark_dirty(p->node_name);
   if (it->second->node == nullptr && it->second->pods.empty()) nodes_.erase(it);
 }
 
@@ -154,7 +169,7 @@ void SchedulerCache::forget_pod(const Pod& p) {
   if (it == pod_states_.end()) return;
   if (!assumed_.count(p.uid())) return;  // only assumed pods can be forgotten
   PodPtr cur = it->second.pod;
-  remove_pod_locked(*cur);
+  remove_pod_locked(cur);
   assumed_.erase(p.uid());
   pod_states_.erase(it);
 }
@@ -193,12 +208,12 @@ void SchedulerCache::add_pod(const PodPtr& p) {
       if (confirm_assumed_locked(it, p)) return;
       // Confirmation of an assumed pod: replace with the informer's object
       // (it carries the bound annotations) on the node it was bound to.
-      remove_pod_locked(*it->second.pod);
+      remove_pod_locked(it->second.pod);
       add_pod_locked(p);
       assumed_.erase(p->uid());
       it->second = PodState{p, 0, false};
     } else {
-      remove_pod_locked(*it->second.pod);
+      remove_pod_locked(it->second.pod);
       add_pod_locked(p);
       it->second.pod = p;
     }
@@ -219,13 +234,13 @@ void SchedulerCache::update_pod(const PodPtr& old_pod, const PodPtr& new_pod) {
   if (assumed_.count(new_pod->uid())) {
     // An update for an assumed pod means it got bound: confirm it.
     if (confirm_assumed_locked(it, new_pod)) return;
-    remove_pod_locked(*it->second.pod);
+    remove_pod_locked(it->second.pod);
     add_pod_locked(new_pod);
     assumed_.erase(new_pod->uid());
     it->second = PodState{new_pod, 0, false};
     return;
   }
-  remove_pod_locked(*it->second.pod);
+  remove_pod_locked(it->second.pod);
   add_pod_locked(new_pod);
   it->second.pod = new_pod;
 }
@@ -234,7 +249,7 @@ void SchedulerCache::remove_pod(const Pod& p) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = pod_states_.find(p.uid());
   if (it == pod_states_.end()) return;
-  remove_pod_locked(*it->second.pod);
+  remove_pod_locked(it->second.pod);
   assumed_.erase(p.uid());
   pod_states_.erase(it);
 }
@@ -257,7 +272,7 @@ PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<vo
   auto fresh = std::make_shared<Pod>(*it->second.pod);
   fn(*fresh);
   fresh->recompute_gpu_assignment();
-  remove_pod_locked(*it->second.pod);
+  remove_pod_locked(it->second.pod);
   add_pod_locked(fresh);
   it->second.pod = fresh;
   return fresh;
@@ -370,6 +385,14 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
     }
   }
   dirty_.clear();
+  for (auto& d : pending_deltas_) s.deltas.push_back(std::move(d));
+  pending_deltas_.clear();
+  while (s.deltas.size() > Snapshot::kMaxDeltas) {
+    s.retired_deltas.push_back(std::move(s.deltas.front()));
+    s.deltas.pop_front();
+  }
+  s.delta_end = delta_seq_;
+  s.topology_epoch = topology_epoch_;
   s.generation = generation_;
   s.nodes_with_prefer_no_schedule = prefer_nodes_;
   s.hostname_domains_are_nodes = foreign_hostnames_ == 0;
@@ -390,7 +413,7 @@ void SchedulerCache::cleanup_expired_assumed_pods() {
   }
   for (const auto& uid : expired) {
     auto it = pod_states_.find(uid);
-    remove_pod_locked(*it->second.pod);
+    remove_pod_locked(it->second.pod);
     assumed_.erase(uid);
     pod_states_.erase(it);
   }

@@ -94,7 +94,8 @@ class SchedulerCache {
   NodeInfo& writable(NodeInfoPtr& slot);            // copy-on-write before mutating
   bool in_place_ = false;  // assume/annotate on the scheduling thread (under mu_)
   void add_pod_locked(const PodPtr& p);
-  void remove_pod_locked(const Pod& p);
+  void remove_pod_locked(const PodPtr& p);
+  void record_delta(const PodPtr& p, const NodeInfo& ni, int d);
   void mark_dirty(const std::string& node);
   void group_delta(const Pod& p, int d);
   void set_node_locked(const NodePtr& n);
@@ -119,6 +120,9 @@ class SchedulerCache {
   uint64_t node_epoch_ = 1;
   int64_t prefer_nodes_ = 0;
   int64_t foreign_hostnames_ = 0;  // nodes whose hostname label is not their name
+  uint64_t topology_epoch_ = 1;     // Snapshot::topology_epoch
+  std::vector<PodDelta> pending_deltas_;  // since the last snapshot refresh
+  uint64_t delta_seq_ = 0;
   // Copied on write while a snapshot still shares it.
   std::shared_ptr<std::unordered_map<std::string, int64_t>> image_spread_ =
       std::make_shared<std::unordered_map<std::string, int64_t>>();

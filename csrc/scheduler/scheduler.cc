@@ -645,10 +645,16 @@ int Scheduler::num_feasible_nodes_to_find(Framework& fw, int n) const {
 // Replaced snapshot versions may hold the last reference to deleted pods;
 // free them in batches on a binder thread instead of in the scheduling cycle.
 void Scheduler::release_retired() {
-  if (snapshot_.retired.size() < 32) return;
-  auto batch = std::make_shared<std::vector<NodeInfoPtr>>(std::move(snapshot_.retired));
-  snapshot_.retired.clear();
-  binder_->submit([batch] { batch->clear(); });
+  if (snapshot_.retired.size() >= 32) {
+    auto batch = std::make_shared<std::vector<NodeInfoPtr>>(std::move(snapshot_.retired));
+    snapshot_.retired.clear();
+    binder_->submit([batch] { batch->clear(); });
+  }
+  if (snapshot_.retired_deltas.size() >= 256) {
+    auto batch = std::make_shared<std::vector<PodDelta>>(std::move(snapshot_.retired_deltas));
+    snapshot_.retired_deltas.clear();
+    binder_->submit([batch] { batch->clear(); });
+  }
 }
 
 Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
