@@ -225,10 +225,16 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
     std::shared_ptr<CycleState> state_out;
     std::shared_ptr<NodeInfo> ni_out;
     if (i == 0) {
-      std::vector<PodPtr> nominated;
-      if (handle_.nominator && ni.node && !handle_.nominator->empty())
-        nominated = handle_.nominator->nominated_pods_for_node(ni.name());
-      for (const auto& np : nominated) {
+      std::vector<PodPtr> live;
+      const std::vector<PodPtr>* nominated = &live;
+      if (!ni.node) {
+      } else if (s.nominated) {
+        auto it = s.nominated->find(ni.name());
+        if (it != s.nominated->end()) nominated = &it->second;
+      } else if (handle_.nominator && !handle_.nominator->empty()) {
+        live = handle_.nominator->nominated_pods_for_node(ni.name());
+      }
+      for (const auto& np : *nominated) {
         if (np->priority < p.priority || np->uid() == p.uid()) continue;
         if (!ni_out) {
           ni_out = ni.clone();

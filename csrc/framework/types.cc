@@ -43,45 +43,46 @@ uint64_t CycleState::next_version() {
 }
 
 std::shared_ptr<StateData> CycleState::read(std::string_view key) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::shared_lock<std::shared_mutex> g(mu_);
   for (const auto& kv : kv_)
-    if (kv.first == key) return kv.second;
+    if (*kv.first == key) return kv.second;
   return nullptr;
 }
 
 StateData* CycleState::read_raw(std::string_view key) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::shared_lock<std::shared_mutex> g(mu_);
   for (const auto& kv : kv_)
-    if (kv.first == key) return kv.second.get();
+    if (*kv.first == key) return kv.second.get();
   return nullptr;
 }
 
 void CycleState::write(std::string_view key, std::shared_ptr<StateData> v) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::shared_mutex> g(mu_);
   version_.store(next_version(), std::memory_order_release);
   for (auto& kv : kv_)
-    if (kv.first == key) {
+    if (*kv.first == key) {
       kv.second = std::move(v);
       return;
     }
-  kv_.emplace_back(std::string(key), std::move(v));
+  kv_.emplace_back(&IStr::intern(key), std::move(v));
 }
 
 void CycleState::erase(std::string_view key) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::shared_mutex> g(mu_);
   version_.store(next_version(), std::memory_order_release);
-  kv_.erase(std::remove_if(kv_.begin(), kv_.end(), [&](const auto& kv) { return kv.first == key; }), kv_.end());
+  kv_.erase(std::remove_if(kv_.begin(), kv_.end(), [&](const auto& kv) { return *kv.first == key; }), kv_.end());
 }
 
 std::shared_ptr<CycleState> CycleState::clone() const {
   auto c = std::make_shared<CycleState>();
-  std::lock_guard<std::mutex> g(mu_);
+  std::shared_lock<std::shared_mutex> g(mu_);
   for (const auto& kv : kv_) {
     if (!kv.second) continue;
     auto cl = kv.second->clone();
     c->kv_.emplace_back(kv.first, cl ? cl : kv.second);
   }
   c->record_metrics = record_metrics;
+  c->nominated = nominated;
   return c;
 }
 

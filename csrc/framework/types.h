@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -52,6 +53,10 @@ class Status {
     return code_ == Code::Unschedulable || code_ == Code::UnschedulableAndUnresolvable;
   }
   const std::vector<std::string>& reasons() const;
+  // Identity of the shared reasons list: statuses copied from one another
+  // (e.g. a plugin's per-thread memo of a failure) compare equal here.
+  const void* reasons_id() const { return reasons_.get(); }
+  const void* plugin_id() const { return plugin_.get(); }
   std::string message() const;
   const std::string& failed_plugin() const;
   Status& with_plugin(std::string p) {
@@ -85,6 +90,9 @@ struct PodsToActivate : StateData {
 };
 inline constexpr const char* kPodsToActivateKey = "kubernetes.io/pods-to-activate";
 
+// Node name -> pods nominated to it (Nominator::view()).
+using NominatedMap = std::unordered_map<std::string, std::vector<PodPtr>>;
+
 class CycleState {
  public:
   CycleState() : version_(next_version()) { kv_.reserve(8); }  // a cycle writes ~7 entries
@@ -112,12 +120,19 @@ class CycleState {
   std::shared_ptr<CycleState> clone() const;
   bool record_metrics = false;
   bool skip_filter_plugins_mark = false;
+  // Nominated pods as of the cycle's start, shared read-only by the Filter
+  // workers (null: ask the Nominator). Saves a lock and a vector copy per
+  // node while preemptions keep nominations outstanding.
+  std::shared_ptr<const NominatedMap> nominated;
 
  private:
   static uint64_t next_version();
-  mutable std::mutex mu_;
+  // Readers (Filter workers, preemption dry runs cloning the state per
+  // candidate node on every worker) share the lock; only writes are exclusive.
+  mutable std::shared_mutex mu_;
   std::atomic<uint64_t> version_;
-  std::vector<std::pair<std::string, std::shared_ptr<StateData>>> kv_;
+  // Keys are interned (IStr): a clone copies pointers, not strings.
+  std::vector<std::pair<const std::string*, std::shared_ptr<StateData>>> kv_;
 };
 using CycleStatePtr = std::shared_ptr<CycleState>;
 

@@ -90,13 +90,16 @@ void Nominator::add(const PodPtr& p, const std::string& node) {
     auto& vec = by_node_[it->second];
     vec.erase(std::remove_if(vec.begin(), vec.end(), [&](const PodPtr& x) { return x->uid() == p->uid(); }), vec.end());
     if (vec.empty()) by_node_.erase(it->second);
+    log_remove(it->second, p);
     node_of_.erase(it);
   }
   if (!n.empty()) {
     node_of_[p->uid()] = n;
     by_node_[n].push_back(p);
+    log_.push_back(Change{n, p, true});
   }
   count_.store(node_of_.size(), std::memory_order_relaxed);
+  if (node_of_.empty()) reset_mirror();
 }
 
 void Nominator::remove(const Pod& p) {
@@ -104,10 +107,15 @@ void Nominator::remove(const Pod& p) {
   auto it = node_of_.find(p.uid());
   if (it == node_of_.end()) return;
   auto& vec = by_node_[it->second];
+  PodPtr gone;
+  for (const auto& x : vec)
+    if (x->uid() == p.uid()) gone = x;
   vec.erase(std::remove_if(vec.begin(), vec.end(), [&](const PodPtr& x) { return x->uid() == p.uid(); }), vec.end());
   if (vec.empty()) by_node_.erase(it->second);
+  if (gone) log_remove(it->second, gone);
   node_of_.erase(it);
   count_.store(node_of_.size(), std::memory_order_relaxed);
+  if (node_of_.empty()) reset_mirror();
 }
 
 void Nominator::update(const PodPtr& old_p, const PodPtr& new_p) {
@@ -127,6 +135,25 @@ std::vector<PodPtr> Nominator::nominated_pods_for_node(const std::string& node) 
   std::lock_guard<std::mutex> g(mu_);
   auto it = by_node_.find(node);
   return it == by_node_.end() ? std::vector<PodPtr>{} : it->second;
+}
+
+std::shared_ptr<const NominatedMap> Nominator::view() const {
+  std::lock_guard<std::mutex> g(mu_);
+  NominatedMap& m = *mirror_;
+  for (auto& c : log_) {
+    if (c.add) {
+      m[c.node].push_back(std::move(c.pod));
+      continue;
+    }
+    auto it = m.find(c.node);
+    if (it == m.end()) continue;
+    auto& vec = it->second;
+    const std::string& uid = c.pod->uid();
+    vec.erase(std::remove_if(vec.begin(), vec.end(), [&](const PodPtr& x) { return x->uid() == uid; }), vec.end());
+    if (vec.empty()) m.erase(it);
+  }
+  log_.clear();
+  return mirror_;
 }
 
 std::string Nominator::nominated_node(const std::string& uid) const {

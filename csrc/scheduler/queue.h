@@ -55,6 +55,11 @@ class Nominator {
   void remove(const Pod& p);
   void update(const PodPtr& old_p, const PodPtr& new_p);
   std::vector<PodPtr> nominated_pods_for_node(const std::string& node) const;
+  // Every node's nominated pods for the cycle about to start. Single
+  // consumer: the scheduling thread, between cycles. The view is a mirror
+  // that the changes since the last call are applied to (O(changes), not a
+  // copy of the map); the previous cycle's Filter workers are done with it.
+  std::shared_ptr<const NominatedMap> view() const;
   std::string nominated_node(const std::string& uid) const;
   size_t size() const;
   bool empty() const { return count_.load(std::memory_order_relaxed) == 0; }  // lock-free fast path
@@ -62,8 +67,22 @@ class Nominator {
  private:
   std::atomic<size_t> count_{0};
   mutable std::mutex mu_;
-  std::unordered_map<std::string, std::vector<PodPtr>> by_node_;
+  NominatedMap by_node_;
   std::unordered_map<std::string, std::string> node_of_;
+  struct Change {
+    std::string node;
+    PodPtr pod;
+    bool add;
+  };
+  void log_remove(const std::string& node, const PodPtr& p) { log_.push_back(Change{node, p, false}); }
+  // Nothing nominated: start an empty mirror (a cycle may still hold the old
+  // one) and drop the log, which would otherwise grow while no cycle asks.
+  void reset_mirror() {
+    log_.clear();
+    if (!mirror_->empty()) mirror_ = std::make_shared<NominatedMap>();
+  }
+  mutable std::vector<Change> log_;  // since the last view()
+  mutable std::shared_ptr<NominatedMap> mirror_ = std::make_shared<NominatedMap>();
 };
 
 struct QueueOptions {

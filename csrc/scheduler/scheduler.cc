@@ -837,18 +837,45 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   next_start_node_ = (start + processed) % n;
   feasible.assign(found_buf_.begin(), found_buf_.begin() + c);
   if (feasible_pos) feasible_pos->assign(found_pos_buf_.begin(), found_pos_buf_.begin() + c);
+  // Failed nodes mostly share a few Status objects (plugins memoize their
+  // failures), so plugins and reasons are tallied per distinct Status first.
+  std::vector<std::pair<const Status*, int>> distinct;
   if (feasible.empty() || full_diagnosis) {
+    d.node_to_status.reserve(d.node_to_status.size() + static_cast<size_t>(n));
+    std::unordered_map<const void*, std::unordered_map<const void*, size_t>> index;  // past 32 distinct
     for (int pos = 0; pos < n; ++pos) {
-      if (!fail_ptr_[pos]) continue;
-      d.unschedulable_plugins.insert(fail_ptr_[pos]->failed_plugin());
-      d.node_to_status[all[pos]->name()] = *fail_ptr_[pos];
+      const Status* fs = fail_ptr_[pos];
+      if (!fs) continue;
+      d.node_to_status.emplace(all[pos]->name(), *fs);
+      size_t k = distinct.size();
+      if (distinct.size() <= 32) {
+        for (size_t j = 0; j < distinct.size(); ++j)
+          if (distinct[j].first->reasons_id() == fs->reasons_id() && distinct[j].first->plugin_id() == fs->plugin_id()) {
+            k = j;
+            break;
+          }
+      } else {
+        auto& by_plugin = index[fs->reasons_id()];
+        auto it = by_plugin.find(fs->plugin_id());
+        if (it != by_plugin.end()) k = it->second;
+      }
+      if (k == distinct.size()) {
+        distinct.emplace_back(fs, 0);
+        if (distinct.size() == 33)  // switch to the index
+          for (size_t j = 0; j < distinct.size(); ++j)
+            index[distinct[j].first->reasons_id()][distinct[j].first->plugin_id()] = j;
+        else if (distinct.size() > 33)
+          index[fs->reasons_id()][fs->plugin_id()] = k;
+      }
+      ++distinct[k].second;
     }
+    for (const auto& [s0, cnt] : distinct) d.unschedulable_plugins.insert(s0->failed_plugin());
   }
   if (feasible.empty()) {
     // FitError message: "0/N nodes are available: k reason, ..."
     std::map<std::string, int> reasons;
-    for (const auto& kv : d.node_to_status)
-      for (const auto& r : kv.second.reasons()) ++reasons[r];
+    for (const auto& [s0, cnt] : distinct)
+      for (const auto& r : s0->reasons()) reasons[r] += cnt;
     std::string msg = "0/" + std::to_string(n) + " nodes are available:";
     bool first = true;
     for (const auto& kv : reasons) {
@@ -906,6 +933,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   int64_t cycle_start = clock_->now_us();
   auto state = std::make_shared<CycleState>();
   state->record_metrics = std::uniform_real_distribution<double>(0, 1)(rng_) < opts_.metrics_sample_rate;
+  if (!nominator_->empty()) state->nominated = nominator_->view();
   auto to_activate = std::make_shared<PodsToActivate>();
   state->write(kPodsToActivateKey, to_activate);
   int64_t cycle = queue_->scheduling_cycle();

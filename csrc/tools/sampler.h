@@ -69,6 +69,12 @@ inline std::atomic<bool>& running() {
   static std::atomic<bool> r{false};
   return r;
 }
+// While paused (e.g. a driver's untimed setup phase) no samples are taken.
+inline std::atomic<bool>& paused() {
+  static std::atomic<bool> p{false};
+  return p;
+}
+inline void pause(bool on) { paused().store(on, std::memory_order_relaxed); }
 inline std::thread& sampler_thread() {
   static std::thread t;
   return t;
@@ -104,7 +110,8 @@ inline void start(int hz, size_t max_samples = 1 << 21) {
     auto next_list = std::chrono::steady_clock::now() + std::chrono::milliseconds(50);
     auto tick = std::chrono::steady_clock::now();
     while (running().load(std::memory_order_relaxed) && next().load(std::memory_order_relaxed) < buffer().size()) {
-      for (int t : tids) syscall(SYS_tgkill, pid, t, SIGPROF);
+      if (!paused().load(std::memory_order_relaxed))
+        for (int t : tids) syscall(SYS_tgkill, pid, t, SIGPROF);
       tick += period;
       std::this_thread::sleep_until(tick);
       if (std::chrono::steady_clock::now() > next_list) {

@@ -5,10 +5,13 @@
 //   xsched_stress <dir> [waves]
 // <dir> holds nodes.json, nrts.json, config.json (native profile config) and
 // wave_<i>.json files {"podgroups":[...],"pods":[...]} written by
-// flex_gpu_scheduler_amd/tools/stress.py.
+// flex_gpu_scheduler_amd/tools/stress.py, and optionally init.json (pods
+// created and bound before every wave, untimed: e.g. PreemptionBasic's
+// low-priority victims).
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
+#include <filesystem>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -55,7 +58,33 @@ int main(int argc, char** argv) {
   uint64_t bound = 0;
   double total_s = 0;
   size_t total_pods = 0;
+  const bool has_init = std::filesystem::exists(dir + "/init.json");
+  auto wait_bound = [&](uint64_t target, const char* what, int w) {
+    auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+    while (sched.stats().bound < target) {
+      if (std::chrono::steady_clock::now() > deadline) {
+        std::fprintf(stderr, "%s %d timed out: bound %llu/%llu\n", what, w,
+                     static_cast<unsigned long long>(sched.stats().bound), static_cast<unsigned long long>(target));
+        return false;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    return true;
+  };
   for (int w = 0; w < waves; ++w) {
+    if (has_init) {
+      if (sample_path) sampler::pause(true);
+      Json init = Json::parse(slurp(dir + "/init.json"));
+      std::vector<Json> ip(init.items().begin(), init.items().end());
+      size_t in = ip.size();
+      store->create_many("pods", std::move(ip));
+      if (!wait_bound(bound + in, "init", w)) {
+        sched.stop();
+        return 1;
+      }
+      bound += in;
+      if (sample_path) sampler::pause(false);
+    }
     Json wave = Json::parse(slurp(dir + "/wave_" + std::to_string(w % 4) + ".json"));
     std::vector<Json> pgs(wave["podgroups"].items().begin(), wave["podgroups"].items().end());
     std::vector<Json> pods(wave["pods"].items().begin(), wave["pods"].items().end());
@@ -66,15 +95,9 @@ int main(int argc, char** argv) {
     store->create_chunked("pods", [&](const std::function<void(Json&&)>& emit) {
       for (auto& p : pods) emit(std::move(p));
     });
-    auto deadline = t0 + std::chrono::seconds(60);
-    while (sched.stats().bound < bound + n) {
-      if (std::chrono::steady_clock::now() > deadline) {
-        std::fprintf(stderr, "wave %d timed out: bound %llu/%zu\n", w,
-                     static_cast<unsigned long long>(sched.stats().bound - bound), n);
-        sched.stop();
-        return 1;
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    if (!wait_bound(bound + n, "wave", w)) {
+      sched.stop();
+      return 1;
     }
     bound += n;
     std::string ns = wave["namespace"].str_or("bench");

@@ -26,7 +26,8 @@ def write_inputs(out: str | Path, nodes: int = 64, seed: int = 0, options: dict 
 
 def write_workload(out: str | Path, name: str, nodes: int, pods: int, options: dict | None = None) -> Path:
     """A tools/sched_perf.py workload as stress-driver input: the measured
-    pods form every wave (init pods are not replayed)."""
+    pods form every wave; init pods (init.json) are created and bound before
+    each wave, untimed."""
     from .sched_perf import WORKLOADS
 
     w = WORKLOADS[name](nodes, pods)
@@ -36,6 +37,10 @@ def write_workload(out: str | Path, name: str, nodes: int, pods: int, options: d
     (d / "nrts.json").write_text("[]")
     cfg = load_config(w["config"]).to_native(**{**w["options"], **(options or {})})
     (d / "config.json").write_text(json.dumps(cfg))
+    if w["init_pods"]:
+        (d / "init.json").write_text(json.dumps(w["init_pods"]))
+    elif (d / "init.json").exists():
+        (d / "init.json").unlink()
     ns = w["pods"][0]["metadata"].get("namespace", "default")
     for i in range(4):
         (d / f"wave_{i}.json").write_text(json.dumps({"namespace": ns, "podgroups": w["extra_objects"].get("podgroups", []),
