@@ -43,6 +43,29 @@ int64_t count_matching(const std::vector<PodPtr>& pods, const LabelSelector& sel
   return n;
 }
 
+// Filter failures, built once: a failing node costs a Status copy (two
+// refcount increments), not a string, vector and control block per node.
+const Status& kSpreadMissingLabel() {
+  static const Status st = Status::unresolvable("node(s) didn't match pod topology spread constraints (missing required label)");
+  return st;
+}
+const Status& kSpreadSkew() {
+  static const Status st = Status::unschedulable("node(s) didn't match pod topology spread constraints");
+  return st;
+}
+const Status& kAffinityUnmet() {
+  static const Status st = Status::unresolvable("node(s) didn't match pod affinity rules");
+  return st;
+}
+const Status& kAntiAffinityUnmet() {
+  static const Status st = Status::unschedulable("node(s) didn't match pod anti-affinity rules");
+  return st;
+}
+const Status& kExistingAntiAffinityUnmet() {
+  static const Status st = Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
+  return st;
+}
+
 // ===================================================== PodTopologySpread ====
 struct CriticalPath {
   std::string value;
@@ -291,7 +314,7 @@ class PodTopologySpread : public Plugin {
     const Node& n = *ni.node;
     for (const auto& c : st->constraints) {
       const std::string* v = n.meta.label(c.topology_key);
-      if (!v) return Status::unresolvable("node(s) didn't match pod topology spread constraints (missing required label)");
+      if (!v) return kSpreadMissingLabel();
       int64_t self = c.selector.matches(p.meta.labels) ? 1 : 0;
       auto cit = st->critical.find(c.topology_key);
       if (cit == st->critical.end()) return Status::error("PodTopologySpread: internal error: no critical paths");
@@ -303,7 +326,7 @@ class PodTopologySpread : public Plugin {
         if (it != kit->second.end()) num = it->second;
       }
       if (num + self - min_num > c.max_skew)
-        return Status::unschedulable("node(s) didn't match pod topology spread constraints");
+        return kSpreadSkew();
     }
     return {};
   }
@@ -597,12 +620,12 @@ class InterPodAffinity : public Plugin {
       bool exist = true;
       for (const auto& t : p.pod_affinity_required) {
         const std::string* v = n.meta.label(t.topology_key);
-        if (!v) return Status::unresolvable("node(s) didn't match pod affinity rules");
+        if (!v) return kAffinityUnmet();
         if (topo_get(st->affinity, t.topology_key, *v) <= 0) exist = false;
       }
       // The first pod of a self-affine series may go anywhere.
       if (!exist && !(st->affinity.empty() && matches_all(p.pod_affinity_required, p.ns(), p)))
-        return Status::unresolvable("node(s) didn't match pod affinity rules");
+        return kAffinityUnmet();
     }
     // satisfyPodAntiAffinity
     for (const auto& t : p.pod_anti_affinity_required) {
@@ -610,11 +633,11 @@ class InterPodAffinity : public Plugin {
         if (st->anti.empty()) continue;
         const std::string* v = n.meta.label(t.topology_key);
         if (v && topo_get(st->anti, t.topology_key, *v) > 0)
-          return Status::unschedulable("node(s) didn't match pod anti-affinity rules");
+          return kAntiAffinityUnmet();
       } else if (n.meta.label(kHostnameLabel)) {
         for (const auto& q : ni.pods)
           if (term_matches(t, p.ns(), *q))
-            return Status::unschedulable("node(s) didn't match pod anti-affinity rules");
+            return kAntiAffinityUnmet();
       }
     }
     // satisfyExistingPodsAntiAffinity: node-local terms of the node's own pods,
@@ -624,13 +647,13 @@ class InterPodAffinity : public Plugin {
       for (const auto& q : ni.pods_with_required_anti_affinity)
         for (const auto& t : q->pod_anti_affinity_required)
           if (!counted(t) && term_matches(t, q->ns(), p))
-            return Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
+            return kExistingAntiAffinityUnmet();
     for (const auto& [key, values] : st->existing_anti) {
       const std::string* v = n.meta.label(key);
       if (!v) continue;
       auto it = values.find(*v);
       if (it != values.end() && it->second > 0)
-        return Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
+        return kExistingAntiAffinityUnmet();
     }
     return {};
   }
