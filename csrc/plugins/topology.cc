@@ -460,7 +460,7 @@ struct AffinityFilterState : StateData {
   }
 };
 struct AffinityScoreState : StateData {
-  std::unordered_map<std::string, std::unordered_map<std::string, int64_t>> topo_score;  // key -> value -> score
+  TopoCounts topo_score;  // key -> value -> score (zero entries dropped)
   std::shared_ptr<StateData> clone() const override { return std::make_shared<AffinityScoreState>(*this); }
 };
 
@@ -661,7 +661,18 @@ class InterPodAffinity : public Plugin {
   void add_term(AffinityScoreState& st, const PodAffinityTerm& t, int64_t w, const std::string& owner_ns,
                 const Pod& q, const Node& n) const {
     if (w == 0 || !term_matches(t, owner_ns, q)) return;
-    if (const std::string* v = n.meta.label(t.topology_key)) st.topo_score[t.topology_key][*v] += w;
+    if (const std::string* v = n.meta.label(t.topology_key)) topo_add(st.topo_score, t.topology_key, *v, w);
+  }
+  // Everything existing pod `q` on node `n` adds to p's topology scores,
+  // times d (+1 entering, -1 leaving): PreScore's per-pod body, and the
+  // replay step of a memoized score state.
+  void score_pod(AffinityScoreState& st, const Pod& p, const Pod& q, const Node& n, int64_t d) const {
+    for (const auto& wt : p.pod_affinity_preferred) add_term(st, wt.term, d * wt.weight, p.ns(), q, n);
+    for (const auto& wt : p.pod_anti_affinity_preferred) add_term(st, wt.term, -d * wt.weight, p.ns(), q, n);
+    if (hard_weight_ > 0)
+      for (const auto& t : q.pod_affinity_required) add_term(st, t, d * hard_weight_, q.ns(), p, n);
+    for (const auto& wt : q.pod_affinity_preferred) add_term(st, wt.term, d * wt.weight, q.ns(), p, n);
+    for (const auto& wt : q.pod_anti_affinity_preferred) add_term(st, wt.term, -d * wt.weight, q.ns(), p, n);
   }
 
   Status pre_score(CycleState& s, const Pod& p, const NodeList& nodes) override {
@@ -670,22 +681,26 @@ class InterPodAffinity : public Plugin {
       s.write(kScoreKey, empty_state<AffinityScoreState>());
       return {};
     }
-    auto st = std::make_shared<AffinityScoreState>();
-    if (h_.snapshot && !nodes.empty() && (has_pref || !h_.snapshot->have_pods_with_affinity.empty())) {
-      const auto& scan = has_pref ? h_.snapshot->nodes : h_.snapshot->have_pods_with_affinity;
-      for (const auto& ni : scan) {
-        const Node& n = *ni->node;
-        const auto& pods = has_pref ? ni->pods : ni->pods_with_affinity;
-        for (const auto& q : pods) {
-          for (const auto& wt : p.pod_affinity_preferred) add_term(*st, wt.term, wt.weight, p.ns(), *q, n);
-          for (const auto& wt : p.pod_anti_affinity_preferred) add_term(*st, wt.term, -wt.weight, p.ns(), *q, n);
-          if (hard_weight_ > 0)
-            for (const auto& t : q->pod_affinity_required) add_term(*st, t, hard_weight_, q->ns(), p, n);
-          for (const auto& wt : q->pod_affinity_preferred) add_term(*st, wt.term, wt.weight, q->ns(), p, n);
-          for (const auto& wt : q->pod_anti_affinity_preferred) add_term(*st, wt.term, -wt.weight, q->ns(), p, n);
-        }
+    // The scores do not depend on the feasible `nodes`, only on the pods of
+    // the cluster: memoized like the Filter state (same key and validity).
+    const Snapshot& snap = *h_.snapshot;
+    const uint64_t key = p.spec_hash ^ labels_hash(p.meta.labels);
+    const uint64_t nsv = ns_version_.load(std::memory_order_acquire);
+    if (auto* m = score_memo_.find(key, p.ns(), nsv, snap.topology_epoch)) {
+      AffinityScoreState& ms = *m->st;
+      if (snap.replay_since(m->seq, [&](const PodDelta& d) { score_pod(ms, p, *d.pod, *d.node, d.d); })) {
+        m->seq = snap.delta_end;
+        s.write(kScoreKey, m->st);
+        return {};
       }
     }
+    auto st = std::make_shared<AffinityScoreState>();
+    const auto& scan = has_pref ? snap.nodes : snap.have_pods_with_affinity;
+    for (const auto& ni : scan) {
+      const auto& pods = has_pref ? ni->pods : ni->pods_with_affinity;
+      for (const auto& q : pods) score_pod(*st, p, *q, *ni->node, 1);
+    }
+    score_memo_.put(key, p.ns(), nsv, snap.topology_epoch, snap.delta_end, st);
     s.write(kScoreKey, st);
     return {};
   }
@@ -728,6 +743,7 @@ class InterPodAffinity : public Plugin {
   std::unordered_map<std::string, StrMap> ns_labels_;
   std::atomic<uint64_t> ns_version_{0};  // memoized states depend on namespace labels
   StateMemo<AffinityFilterState> memo_;
+  StateMemo<AffinityScoreState> score_memo_;
 };
 
 // ========================================================= ImageLocality ====

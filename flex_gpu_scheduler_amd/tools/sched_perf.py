@@ -2,7 +2,8 @@
 
 Upstream kube-scheduler measures its plugins with a matrix of workloads
 (test/integration/scheduler_perf: SchedulingBasic, SchedulingPodAntiAffinity,
-TopologySpreading, SchedulingNodeAffinity, PreemptionBasic, ...) on 500 and
+SchedulingPodAffinity, the Preferred* variants, TopologySpreading,
+SchedulingNodeAffinity, PreemptionBasic, Unschedulable, ...) on 500 and
 5,000 fake nodes. The reference suite inherits that harness through its
 vendored scheduler but publishes no results. This tool runs the
 same shapes against our scheduler — in-process store, default plugin set
@@ -42,16 +43,16 @@ def _wait_bound(sched, target: int, timeout: float) -> bool:
 
 
 def _spec(name: str, nodes: list[dict], init_pods: list[dict], pods: list[dict], *, config=None, options=None,
-          extra_objects: dict | None = None) -> dict:
+          extra_objects: dict | None = None, expect_bound: int | None = None) -> dict:
     """A workload: everything needed to run it here or in the native stress
     driver (tools/stress.py --workload)."""
     return {"name": name, "nodes": nodes, "init_pods": init_pods, "pods": pods, "config": config,
-            "options": options or {}, "extra_objects": extra_objects or {}}
+            "options": options or {}, "extra_objects": extra_objects or {}, "expect_bound": expect_bound}
 
 
 def run_spec(w: dict, timeout: float = 120.0) -> dict:
     return _run(w["name"], w["nodes"], w["init_pods"], w["pods"], config=w["config"], options=w["options"],
-                extra_objects=w["extra_objects"], timeout=timeout)
+                extra_objects=w["extra_objects"], expect_bound=w.get("expect_bound"), timeout=timeout)
 
 
 def _run(name: str, nodes: list[dict], init_pods: list[dict], pods: list[dict], *, config=None, options=None,
@@ -110,6 +111,53 @@ def topology_spreading(n_nodes: int, n_pods: int) -> dict:
     return _spec("TopologySpreading", _nodes_plain(n_nodes), [], [pod(i) for i in range(n_pods)])
 
 
+def pod_affinity(n_nodes: int, n_pods: int) -> dict:
+    # Required affinity (zone) to a group of seed pods that all live in zone-0.
+    init = [make_pod(f"seed-{i}", requests={"cpu": "100m", "memory": "100Mi"}, labels={"color": "blue"},
+                     node_selector={ZONE: "zone-0"}) for i in range(max(1, n_nodes // 30))]
+    aff = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": {"color": "blue"}}, "topologyKey": ZONE}]}}
+    pods = [make_pod(f"pa-{i}", requests={"cpu": "100m", "memory": "100Mi"}, labels={"color": "blue"}, affinity=aff)
+            for i in range(n_pods)]
+    return _spec("SchedulingPodAffinity", _nodes_plain(n_nodes), init, pods)
+
+
+def preferred_pod_affinity(n_nodes: int, n_pods: int) -> dict:
+    aff = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+        {"weight": 1, "podAffinityTerm": {"labelSelector": {"matchLabels": {"color": "red"}},
+                                          "topologyKey": "kubernetes.io/hostname"}}]}}
+    pods = [make_pod(f"ppa-{i}", requests={"cpu": "100m", "memory": "100Mi"}, labels={"color": "red"}, affinity=aff)
+            for i in range(n_pods)]
+    return _spec("SchedulingPreferredPodAffinity", _nodes_plain(n_nodes), [], pods)
+
+
+def preferred_pod_anti_affinity(n_nodes: int, n_pods: int) -> dict:
+    aff = {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+        {"weight": 1, "podAffinityTerm": {"labelSelector": {"matchLabels": {"color": "yellow"}},
+                                          "topologyKey": "kubernetes.io/hostname"}}]}}
+    pods = [make_pod(f"ppaa-{i}", requests={"cpu": "100m", "memory": "100Mi"}, labels={"color": "yellow"},
+                     affinity=aff) for i in range(n_pods)]
+    return _spec("SchedulingPreferredPodAntiAffinity", _nodes_plain(n_nodes), [], pods)
+
+
+def preferred_topology_spreading(n_nodes: int, n_pods: int) -> dict:
+    def pod(i):
+        p = make_pod(f"pts-{i}", requests={"cpu": "100m", "memory": "100Mi"}, labels={"app": "soft"})
+        p["spec"]["topologySpreadConstraints"] = [{"maxSkew": 1, "topologyKey": ZONE,
+                                                   "whenUnsatisfiable": "ScheduleAnyway",
+                                                   "labelSelector": {"matchLabels": {"app": "soft"}}}]
+        return p
+    return _spec("PreferredTopologySpreading", _nodes_plain(n_nodes), [], [pod(i) for i in range(n_pods)])
+
+
+def unschedulable(n_nodes: int, n_pods: int) -> dict:
+    # 200 pods that fit nowhere sit in the unschedulable queue while the
+    # measured pods schedule (upstream "Unschedulable" shape).
+    stuck = [make_pod(f"huge-{i}", requests={"cpu": "9000", "memory": "1Gi"}) for i in range(200)]
+    pods = [make_pod(f"u-{i}", requests={"cpu": "100m", "memory": "100Mi"}) for i in range(n_pods)]
+    return _spec("Unschedulable", _nodes_plain(n_nodes), [], stuck + pods, expect_bound=n_pods)
+
+
 def node_affinity(n_nodes: int, n_pods: int) -> dict:
     aff = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
         {"matchExpressions": [{"key": "disktype", "operator": "In", "values": ["ssd"]}]}]}}}
@@ -151,6 +199,11 @@ WORKLOADS = {
     "SchedulingBasic": scheduling_basic,
     "SchedulingPodAntiAffinity": pod_anti_affinity,
     "TopologySpreading": topology_spreading,
+    "SchedulingPodAffinity": pod_affinity,
+    "SchedulingPreferredPodAffinity": preferred_pod_affinity,
+    "SchedulingPreferredPodAntiAffinity": preferred_pod_anti_affinity,
+    "PreferredTopologySpreading": preferred_topology_spreading,
+    "Unschedulable": unschedulable,
     "SchedulingNodeAffinity": node_affinity,
     "PreemptionBasic": preemption_basic,
     "MI355X-FlexGPUMix": mi355x_flexgpu_mix,

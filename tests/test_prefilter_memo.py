@@ -27,11 +27,23 @@ def template(name, app, ns="default"):
     return p
 
 
+def preferred(name, app):
+    p = make_pod(name, labels={"app": app, "tier": "web"})
+    p["spec"]["affinity"] = {
+        "podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": 7, "podAffinityTerm": {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": ZONE}}]},
+        "podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": 3, "podAffinityTerm": {"labelSelector": {"matchLabels": {"app": app}},
+                                              "topologyKey": HOST}}]}}
+    return p
+
+
 def verdicts(s, pods):
     out = []
     for p in pods:
         e = s.explain(p)
-        out.append((sorted(e["feasible"]), sorted((n, v.get("plugin")) for n, v in e["filtered"].items())))
+        scores = sorted((n, v.get("InterPodAffinity*1")) for n, v in e.get("scores", {}).items())
+        out.append((sorted(e["feasible"]), sorted((n, v.get("plugin")) for n, v in e["filtered"].items()), scores))
     return out
 
 
@@ -46,7 +58,7 @@ def test_memoized_prefilter_matches_fresh_count(store):
     guard["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
         {"labelSelector": {"matchLabels": {"tier": "web"}}, "topologyKey": HOST}]}}
     store.create("pods", guard)
-    probes = [template("probe-a", "a"), template("probe-b", "b")]
+    probes = [template("probe-a", "a"), template("probe-b", "b"), preferred("probe-c", "a")]
     live = new_scheduler(store, load_config(None))
     live.sync_informers(50)
     existing = []
@@ -56,8 +68,16 @@ def test_memoized_prefilter_matches_fresh_count(store):
             name = f"e{step}"
             ns = "team" if rng.random() < 0.2 else "default"
             app = rng.choice(["a", "b", "db"])
-            store.create("pods", make_pod(name, ns, labels={"app": app, "tier": rng.choice(["web", "batch"])},
-                                          node_name=rng.choice(nodes)))
+            q = make_pod(name, ns, labels={"app": app, "tier": rng.choice(["web", "batch"])},
+                         node_name=rng.choice(nodes))
+            if rng.random() < 0.25:  # existing pods' own preferred / required affinity score the probes too
+                q["spec"]["affinity"] = {"podAffinity": {
+                    "preferredDuringSchedulingIgnoredDuringExecution": [
+                        {"weight": 5, "podAffinityTerm": {"labelSelector": {"matchLabels": {"tier": "web"}},
+                                                          "topologyKey": ZONE}}],
+                    "requiredDuringSchedulingIgnoredDuringExecution": [
+                        {"labelSelector": {"matchLabels": {"app": "a"}}, "topologyKey": HOST}]}}
+            store.create("pods", q)
             existing.append((ns, name))
         elif op < 0.75:
             ns, name = existing.pop(rng.randrange(len(existing)))

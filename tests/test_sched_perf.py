@@ -8,7 +8,9 @@ from flex_gpu_scheduler_amd.tools import sched_perf
 
 @pytest.mark.parametrize("name", list(sched_perf.WORKLOADS))
 def test_workload_binds_everything(name):
-    r = sched_perf.run_spec(sched_perf.WORKLOADS[name](24, 48))
+    w = sched_perf.WORKLOADS[name](24, 48)
+    r = sched_perf.run_spec(w)
     assert "error" not in r, r
-    assert r["bound"] == r["pods"] or (name in ("SchedulingPodAntiAffinity", "PreemptionBasic") and r["bound"] == 24), r
+    want = w["expect_bound"] if w["expect_bound"] is not None else len(w["pods"])
+    assert r["bound"] == want, r
     assert r["pods_per_s"] > 0
