@@ -364,26 +364,55 @@ class PodTopologySpread : public Plugin {
       }
     }
     for (int64_t sz : size) st->weight.push_back(std::log(static_cast<double>(sz + 2)));
-    if (h_.snapshot) {
-      const auto& all = h_.snapshot->nodes;
-      thread_local std::vector<int64_t> counts;
-      count_per_node(h_.parallelizer, all, st->constraints, p.ns(), [&](const NodeInfo& ni) {
-        return pod_matches_node_selector_and_affinity(p, *ni.node) && has_all_keys(*ni.node, st->constraints);
-      }, counts);
-      for (size_t c = 0; c < C; ++c) {
-        const auto& key = st->constraints[c].topology_key;
-        if (key == kHostnameLabel) continue;
-        auto kit = st->pair_count.find(key);
-        if (kit == st->pair_count.end()) continue;
-        for (size_t i = 0; i < all.size(); ++i) {
-          if (counts[i * C + c] < 0) continue;
-          auto it = kit->second.find(*all[i]->node->meta.label(key));
-          if (it != kit->second.end()) it->second += counts[i * C + c];
-        }
-      }
+    // Hostname domains are counted per node in Score; the other domains take
+    // their cluster-wide counts from the memoized per-value totals.
+    if (h_.snapshot && !st->pair_count.empty()) {
+      const TopoCounts& totals = soft_totals(p, st->constraints);
+      for (auto& [key, values] : st->pair_count)
+        for (auto& [value, cnt] : values) cnt = topo_get(totals, key, value);
     }
     s.write(kScoreKey, st);
     return {};
+  }
+
+  // Matching pods per (non-hostname topology key, value) over every node
+  // eligible for p (node selector / affinity, all soft keys present): the
+  // O(pods) part of PreScore, kept across cycles like the Filter state.
+  struct SoftTotals {
+    TopoCounts counts;  // zero entries dropped
+  };
+  static void count_soft(SoftTotals& t, const std::vector<TopologySpreadConstraint>& cs, const Pod& p, const Pod& q,
+                         const Node& n, int64_t d) {
+    if (q.terminating() || q.ns() != p.ns()) return;
+    if (!pod_matches_node_selector_and_affinity(p, n) || !has_all_keys(n, cs)) return;
+    for (const auto& c : cs)
+      if (c.topology_key != kHostnameLabel && c.selector.matches(q.meta.labels))
+        topo_add(t.counts, c.topology_key, *n.meta.label(c.topology_key), d);
+  }
+  const TopoCounts& soft_totals(const Pod& p, const std::vector<TopologySpreadConstraint>& cs) {
+    const Snapshot& snap = *h_.snapshot;
+    if (auto* m = soft_memo_.find(p.spec_hash, p.ns(), 0, snap.topology_epoch)) {
+      SoftTotals& ms = *m->st;
+      if (snap.replay_since(m->seq, [&](const PodDelta& d) { count_soft(ms, cs, p, *d.pod, *d.node, d.d); })) {
+        m->seq = snap.delta_end;
+        return ms.counts;
+      }
+    }
+    auto t = std::make_shared<SoftTotals>();
+    const auto& all = snap.nodes;
+    const size_t C = cs.size();
+    thread_local std::vector<int64_t> counts;
+    count_per_node(h_.parallelizer, all, cs, p.ns(), [&](const NodeInfo& ni) {
+      return pod_matches_node_selector_and_affinity(p, *ni.node) && has_all_keys(*ni.node, cs);
+    }, counts);
+    for (size_t c = 0; c < C; ++c) {
+      const auto& key = cs[c].topology_key;
+      if (key == kHostnameLabel) continue;
+      for (size_t i = 0; i < all.size(); ++i)
+        if (counts[i * C + c] > 0) topo_add(t->counts, key, *all[i]->node->meta.label(key), counts[i * C + c]);
+    }
+    soft_memo_.put(p.spec_hash, p.ns(), 0, snap.topology_epoch, snap.delta_end, t);
+    return t->counts;
   }
 
   std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) override {
@@ -443,6 +472,7 @@ class PodTopologySpread : public Plugin {
  private:
   Handle& h_;
   StateMemo<SpreadFilterState> memo_;
+  StateMemo<SoftTotals> soft_memo_;
 };
 
 // ====================================================== InterPodAffinity ====

@@ -1,5 +1,5 @@
-"""PodTopologySpread and InterPodAffinity keep their PreFilter states across
-cycles and replay the cache's pod events into them (csrc/plugins/topology.cc
+"""PodTopologySpread and InterPodAffinity keep their PreFilter / PreScore
+states across cycles and replay the cache's pod events into them (csrc/plugins/topology.cc
 StateMemo, Snapshot::replay_since). Parity: after random pod creations,
 deletions, label changes, terminations and namespace label changes, a
 long-lived scheduler (memoized, replayed states) must give exactly the
@@ -38,11 +38,22 @@ def preferred(name, app):
     return p
 
 
+def soft_spread(name, app):
+    p = make_pod(name, labels={"app": app, "tier": "web"})
+    p["spec"]["topologySpreadConstraints"] = [
+        {"maxSkew": 1, "topologyKey": ZONE, "whenUnsatisfiable": "ScheduleAnyway",
+         "labelSelector": {"matchLabels": {"tier": "web"}}},
+        {"maxSkew": 1, "topologyKey": HOST, "whenUnsatisfiable": "ScheduleAnyway",
+         "labelSelector": {"matchLabels": {"app": app}}}]
+    return p
+
+
 def verdicts(s, pods):
     out = []
     for p in pods:
         e = s.explain(p)
-        scores = sorted((n, v.get("InterPodAffinity*1")) for n, v in e.get("scores", {}).items())
+        scores = sorted((n, v.get("InterPodAffinity*1"), v.get("PodTopologySpread*2"))
+                        for n, v in e.get("scores", {}).items())
         out.append((sorted(e["feasible"]), sorted((n, v.get("plugin")) for n, v in e["filtered"].items()), scores))
     return out
 
@@ -58,7 +69,7 @@ def test_memoized_prefilter_matches_fresh_count(store):
     guard["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
         {"labelSelector": {"matchLabels": {"tier": "web"}}, "topologyKey": HOST}]}}
     store.create("pods", guard)
-    probes = [template("probe-a", "a"), template("probe-b", "b"), preferred("probe-c", "a")]
+    probes = [template("probe-a", "a"), template("probe-b", "b"), preferred("probe-c", "a"), soft_spread("probe-d", "b")]
     live = new_scheduler(store, load_config(None))
     live.sync_informers(50)
     existing = []
