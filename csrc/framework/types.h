@@ -270,6 +270,9 @@ struct Snapshot {
   static constexpr size_t kMaxDeltas = 16384;
   std::deque<PodDelta> deltas;
   uint64_t delta_end = 0;
+  // Set by a plugin that memoizes a state against delta_end (scheduling
+  // thread); the cache records pod events only from the next refresh on.
+  mutable bool deltas_wanted = false;
   // Calls fn(delta) for each pod event after sequence `from` (a delta_end
   // seen in an earlier cycle) and returns true, or returns false without
   // calling fn when some of them have been trimmed.

@@ -108,12 +108,15 @@ class StateMemo {
       if (x.st && x.key == key && x.aux == aux && x.epoch == epoch && x.ns == ns) return &x;
     return nullptr;
   }
-  void put(uint64_t key, const std::string& ns, uint64_t aux, uint64_t epoch, uint64_t seq, std::shared_ptr<State> st) {
+  // Records `st` as computed from `snap` and asks the cache to log pod
+  // events from now on (Snapshot::deltas_wanted).
+  void put(uint64_t key, const std::string& ns, uint64_t aux, const Snapshot& snap, std::shared_ptr<State> st) {
+    snap.deltas_wanted = true;
     Entry* slot = nullptr;
     for (auto& x : e_)
       if (x.st && x.key == key && x.ns == ns) slot = &x;
     if (!slot) slot = &e_[next_++ % e_.size()];
-    *slot = Entry{key, aux, epoch, seq, ns, std::move(st)};
+    *slot = Entry{key, aux, snap.topology_epoch, snap.delta_end, ns, std::move(st)};
   }
 
  private:
@@ -268,7 +271,7 @@ class PodTopologySpread : public Plugin {
       for (const auto& c : st->constraints) st->critical[c.topology_key];
       for (const auto& [key, values] : st->pair_num)
         for (const auto& [value, num] : values) st->update_critical(key, value, num);
-      memo_.put(p.spec_hash, p.ns(), 0, h_.snapshot->topology_epoch, h_.snapshot->delta_end, st);
+      memo_.put(p.spec_hash, p.ns(), 0, *h_.snapshot, st);
     }
     s.write(kFilterKey, st);
     return {};
@@ -411,7 +414,7 @@ class PodTopologySpread : public Plugin {
       for (size_t i = 0; i < all.size(); ++i)
         if (counts[i * C + c] > 0) topo_add(t->counts, key, *all[i]->node->meta.label(key), counts[i * C + c]);
     }
-    soft_memo_.put(p.spec_hash, p.ns(), 0, snap.topology_epoch, snap.delta_end, t);
+    soft_memo_.put(p.spec_hash, p.ns(), 0, snap, t);
     return t->counts;
   }
 
@@ -627,7 +630,7 @@ class InterPodAffinity : public Plugin {
     else
       run(0);
     for (const auto& ps : part) st->merge(ps);
-    memo_.put(key, p.ns(), nsv, snap.topology_epoch, snap.delta_end, st);
+    memo_.put(key, p.ns(), nsv, snap, st);
     s.write(kFilterKey, st);
     return {};
   }
@@ -730,7 +733,7 @@ class InterPodAffinity : public Plugin {
       const auto& pods = has_pref ? ni->pods : ni->pods_with_affinity;
       for (const auto& q : pods) score_pod(*st, p, *q, *ni->node, 1);
     }
-    score_memo_.put(key, p.ns(), nsv, snap.topology_epoch, snap.delta_end, st);
+    score_memo_.put(key, p.ns(), nsv, snap, st);
     s.write(kScoreKey, st);
     return {};
   }

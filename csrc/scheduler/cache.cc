@@ -120,7 +120,7 @@ void SchedulerCache::set_nrt(const std::string& node, const NRTPtr& nrt) {
 // counted, so they need no event either: the Node's arrival bumps the
 // topology epoch.
 void SchedulerCache::record_delta(const PodPtr& p, const NodeInfo& ni, int d) {
-  if (!ni.node) return;
+  if (!track_deltas_ || !ni.node) return;
   pending_deltas_.push_back(PodDelta{p, ni.node, d});
   ++delta_seq_;
 }
@@ -385,6 +385,12 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
     }
   }
   dirty_.clear();
+  if (s.deltas_wanted && !track_deltas_) {
+    // Events were not recorded so far: jump the sequence past the log so
+    // no state memoized before now can be replayed.
+    track_deltas_ = true;
+    delta_seq_ += Snapshot::kMaxDeltas + 1;
+  }
   for (auto& d : pending_deltas_) s.deltas.push_back(std::move(d));
   pending_deltas_.clear();
   while (s.deltas.size() > Snapshot::kMaxDeltas) {

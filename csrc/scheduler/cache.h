@@ -123,6 +123,7 @@ class SchedulerCache {
   uint64_t topology_epoch_ = 1;     // Snapshot::topology_epoch
   std::vector<PodDelta> pending_deltas_;  // since the last snapshot refresh
   uint64_t delta_seq_ = 0;
+  bool track_deltas_ = false;  // once a plugin asked (Snapshot::deltas_wanted)
   // Copied on write while a snapshot still shares it.
   std::shared_ptr<std::unordered_map<std::string, int64_t>> image_spread_ =
       std::make_shared<std::unordered_map<std::string, int64_t>>();
