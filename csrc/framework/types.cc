@@ -56,6 +56,19 @@ StateData* CycleState::read_raw(std::string_view key) const {
   return nullptr;
 }
 
+namespace {
+// Plugins write a handful of constant keys every cycle: a per-thread list of
+// the keys seen so far skips the intern table's lock and hash.
+const std::string* intern_key(std::string_view key) {
+  thread_local std::vector<const std::string*> seen;
+  for (const std::string* k : seen)
+    if (*k == key) return k;
+  const std::string* k = &IStr::intern(key);
+  if (seen.size() < 64) seen.push_back(k);
+  return k;
+}
+}  // namespace
+
 void CycleState::write(std::string_view key, std::shared_ptr<StateData> v) {
   std::unique_lock<std::shared_mutex> g(mu_);
   version_.store(next_version(), std::memory_order_release);
@@ -64,7 +77,7 @@ void CycleState::write(std::string_view key, std::shared_ptr<StateData> v) {
       kv.second = std::move(v);
       return;
     }
-  kv_.emplace_back(&IStr::intern(key), std::move(v));
+  kv_.emplace_back(intern_key(key), std::move(v));
 }
 
 void CycleState::erase(std::string_view key) {

@@ -5,7 +5,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 tag=${1:-latest}
 mkdir -p profiles
-for db in gpurun_out/rocprof_*/*.db; do
+for db in gpurun_out/${tag}_rocprof_*/*.db gpurun_out/rocprof_*/*.db; do
   [ -f "$db" ] || continue
   name=$(basename "$(dirname "$db")")
   tmp=$(mktemp -d)
