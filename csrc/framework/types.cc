@@ -293,3 +293,62 @@ const PodPtr* NodeInfo::find_pod(const std::string& uid) const {
 }
 
 }  // namespace xsched
+
+namespace xsched {
+
+// ------------------------------------------------------- cache debugger ----
+std::vector<std::string> GpuLedger::diff(const GpuLedger& o) const {
+  std::vector<std::string> out;
+  if (gpu_count != o.gpu_count || parts != o.parts) out.push_back("gpu.partitions");
+  if (monopoly != o.monopoly) out.push_back("gpu.monopoly");
+  if (slots.size() != o.slots.size()) {
+    out.push_back("gpu.slots");
+  } else {
+    for (size_t i = 0; i < slots.size(); ++i)
+      if (slots[i].exclusive != o.slots[i].exclusive || slots[i].used_mem != o.slots[i].used_mem ||
+          slots[i].mem_pods != o.slots[i].mem_pods) {
+        out.push_back("gpu.slots[" + std::to_string(i) + "]");
+        break;
+      }
+  }
+  if (tot_whole != o.tot_whole) out.push_back("gpu.free_whole");
+  if (tot_xcds != o.tot_xcds) out.push_back("gpu.free_xcds");
+  if (tot_mem != o.tot_mem) out.push_back("gpu.free_memory");
+  for (int z = 0; z < kMaxZones; ++z)
+    if (zone_gpus[z] != o.zone_gpus[z] || zone_whole[z] != o.zone_whole[z] || zone_xcds[z] != o.zone_xcds[z] ||
+        zone_mem[z] != o.zone_mem[z]) {
+      out.push_back("gpu.zone[" + std::to_string(z) + "]");
+      break;
+    }
+  return out;
+}
+
+std::vector<std::string> NodeInfo::verify() const {
+  std::vector<std::string> out;
+  if (!node) return out;
+  NodeInfo fresh;
+  fresh.set_node(node);
+  fresh.nrt = nrt;
+  for (const auto& p : pods) fresh.add_pod(p);
+  auto same_res = [](const Res& a, const Res& b) {
+    for (int i = 0; i < kMaxRes; ++i)
+      if (a.v[i] != b.v[i]) return false;
+    return true;
+  };
+  if (!same_res(requested, fresh.requested)) out.push_back("requested");
+  if (!same_res(nonzero_requested, fresh.nonzero_requested)) out.push_back("nonzero_requested");
+  if (!same_res(allocatable, fresh.allocatable)) out.push_back("allocatable");
+  if (used_ports != fresh.used_ports) out.push_back("used_ports");
+  if (pods_with_affinity.size() != fresh.pods_with_affinity.size()) out.push_back("pods_with_affinity");
+  if (pods_with_required_anti_affinity.size() != fresh.pods_with_required_anti_affinity.size())
+    out.push_back("pods_with_required_anti_affinity");
+  auto a = pg_count, b = fresh.pg_count;
+  a.erase(std::remove_if(a.begin(), a.end(), [](const auto& kv) { return kv.second == 0; }), a.end());
+  std::sort(a.begin(), a.end());
+  std::sort(b.begin(), b.end());
+  if (a != b) out.push_back("pg_count");
+  for (auto& d : gpu.diff(fresh.gpu)) out.push_back(std::move(d));
+  return out;
+}
+
+}  // namespace xsched

@@ -173,6 +173,9 @@ struct GpuLedger {
 
   void init(const Node& n);
   void apply(const GpuAssignment& a, int sign);
+  // Fields (by name) where this ledger's usage and derived availability
+  // differ from `o` (cache debugger: incremental vs re-derived).
+  std::vector<std::string> diff(const GpuLedger& o) const;
   int64_t part_mem(int g) const { return parts[g] > 0 ? mem_per_gpu / parts[g] : 0; }
   int xcds_per_part(int g) const { return parts[g] > 0 ? 8 / parts[g] : 0; }
   bool gpu_untouched(int g) const;      // no owner and no memory use on any partition
@@ -216,6 +219,9 @@ struct NodeInfo {
   int num_pods() const { return static_cast<int>(pods.size()); }
   std::shared_ptr<NodeInfo> clone() const { return std::make_shared<NodeInfo>(*this); }
   const PodPtr* find_pod(const std::string& uid) const;
+  // Fields where this NodeInfo's incremental accounting differs from one
+  // rebuilt from scratch out of its Node and pods (cache debugger).
+  std::vector<std::string> verify() const;
 };
 using NodeInfoPtr = std::shared_ptr<NodeInfo>;
 // Nodes of one scheduling cycle (feasible set, score order). Borrowed from

@@ -565,6 +565,24 @@ PYBIND11_MODULE(_xsched, m) {
              }
              return to_py(out);
            })
+      .def("check_cache",
+           [](Scheduler& s) {
+             Json out;
+             {
+               py::gil_scoped_release r;
+               out = s.check_cache();
+             }
+             return to_py(out);
+           })
+      .def("dump_cache",
+           [](Scheduler& s) {
+             Json out;
+             {
+               py::gil_scoped_release r;
+               out = s.dump_cache();
+             }
+             return to_py(out);
+           })
       .def("score_benchmark",
            [](Scheduler& s, py::handle pod, int iterations) {
              Json j = json_arg(pod);

@@ -1,6 +1,7 @@
 #include "scheduler/cache.h"
 
 #include <algorithm>
+#include <set>
 
 namespace xsched {
 
@@ -455,6 +456,124 @@ NodeInfoPtr SchedulerCache::node_info_copy(const std::string& name) const {
 std::vector<std::string> SchedulerCache::node_names() const {
   std::lock_guard<std::mutex> g(mu_);
   return order_;
+}
+
+}  // namespace xsched
+
+namespace xsched {
+
+Json SchedulerCache::check(const std::vector<PodPtr>& assigned, const std::vector<std::string>& nodes) const {
+  std::lock_guard<std::mutex> g(mu_);
+  Json out = Json::object();
+  auto list = [](const std::vector<std::string>& v) {
+    Json a = Json::array();
+    for (const auto& x : v) a.push_back(Json(x));
+    return a;
+  };
+  // Pods: the listers' assigned pods vs the cache's non-assumed pods.
+  std::vector<std::string> missing, redundant, wrong;
+  std::unordered_map<std::string, const Pod*> truth;
+  for (const auto& p : assigned) truth[p->uid()] = p.get();
+  size_t assumed_n = 0;
+  for (const auto& [uid, st] : pod_states_) {
+    auto it = truth.find(uid);
+    if (assumed_.count(uid)) {
+      ++assumed_n;  // not bound yet, or bound and not confirmed: either is fine
+      if (it != truth.end() && it->second->node_name != st.pod->node_name)
+        wrong.push_back(st.pod->key() + ": cache " + st.pod->node_name + ", listers " + it->second->node_name);
+      continue;
+    }
+    if (it == truth.end()) {
+      redundant.push_back(st.pod->key());
+    } else if (it->second->node_name != st.pod->node_name) {
+      wrong.push_back(st.pod->key() + ": cache " + st.pod->node_name + ", listers " + it->second->node_name);
+    }
+  }
+  for (const auto& p : assigned)
+    if (!pod_states_.count(p->uid())) missing.push_back(p->key());
+  // Nodes.
+  std::set<std::string> want(nodes.begin(), nodes.end()), have;
+  for (const auto& [name, ni] : nodes_)
+    if (ni->node) have.insert(name);
+  std::vector<std::string> missing_nodes, redundant_nodes;
+  std::set_difference(want.begin(), want.end(), have.begin(), have.end(), std::back_inserter(missing_nodes));
+  std::set_difference(have.begin(), have.end(), want.begin(), want.end(), std::back_inserter(redundant_nodes));
+  // Accounting: every NodeInfo against one rebuilt from its pods; each pod's
+  // NodeInfo is the one of its node.
+  Json acct = Json::array();
+  for (const auto& [name, ni] : nodes_) {
+    std::vector<std::string> bad = ni->verify();
+    for (const auto& p : ni->pods)
+      if (p->node_name != name) bad.push_back("pod " + p->key() + " names node " + p->node_name);
+    if (bad.empty()) continue;
+    Json e = Json::object();
+    e.set("node", Json(name));
+    e.set("fields", list(bad));
+    acct.push_back(std::move(e));
+  }
+  // PodGroup counts: the O(1) counters against a recount of cached pods.
+  std::unordered_map<uint64_t, int> recount;
+  for (const auto& [uid, st] : pod_states_)
+    if (st.pod->pg_key) ++recount[st.pod->pg_key];
+  std::vector<std::string> groups;
+  {
+    std::lock_guard<std::mutex> gg(group_mu_);
+    for (const auto& [k, c] : recount) {
+      auto it = group_assigned_.find(k);
+      int have_c = it == group_assigned_.end() ? 0 : it->second;
+      if (have_c != c) groups.push_back(std::to_string(k) + ": counter " + std::to_string(have_c) + ", pods " + std::to_string(c));
+    }
+    for (const auto& [k, c] : group_assigned_)
+      if (c != 0 && !recount.count(k)) groups.push_back(std::to_string(k) + ": counter " + std::to_string(c) + ", pods 0");
+  }
+  bool clean = missing.empty() && redundant.empty() && wrong.empty() && missing_nodes.empty() &&
+               redundant_nodes.empty() && acct.size() == 0 && groups.empty();
+  out.set("clean", Json(clean));
+  out.set("missing_pods", list(missing));
+  out.set("redundant_pods", list(redundant));
+  out.set("wrong_node", list(wrong));
+  out.set("missing_nodes", list(missing_nodes));
+  out.set("redundant_nodes", list(redundant_nodes));
+  out.set("accounting", std::move(acct));
+  out.set("group_counts", list(groups));
+  out.set("assumed", Json(static_cast<int64_t>(assumed_n)));
+  return out;
+}
+
+Json SchedulerCache::dump() const {
+  std::lock_guard<std::mutex> g(mu_);
+  Json out = Json::object();
+  Json ns = Json::array();
+  for (const auto& name : order_) {
+    auto it = nodes_.find(name);
+    if (it == nodes_.end()) continue;
+    const NodeInfo& ni = *it->second;
+    Json n = Json::object();
+    n.set("name", Json(name));
+    Json pods = Json::array();
+    for (const auto& p : ni.pods) pods.push_back(Json(p->key() + (assumed_.count(p->uid()) ? " (assumed)" : "")));
+    n.set("pods", std::move(pods));
+    Json req = Json::object();
+    for (uint64_t m = ni.requested.mask; m; m &= m - 1) {
+      int id = __builtin_ctzll(m);
+      req.set(ResourceRegistry::get().name(id), Json(ni.requested.v[id]));
+    }
+    n.set("requested", std::move(req));
+    if (ni.gpu.gpu_count > 0) {
+      Json gj = Json::object();
+      gj.set("gpus", Json(ni.gpu.gpu_count));
+      gj.set("free_whole", Json(ni.gpu.free_gpus()));
+      gj.set("free_xcds", Json(ni.gpu.free_xcds()));
+      gj.set("free_memory", Json(ni.gpu.free_memory()));
+      n.set("gpu", std::move(gj));
+    }
+    n.set("generation", Json(ni.generation));
+    ns.push_back(std::move(n));
+  }
+  out.set("nodes", std::move(ns));
+  out.set("pods", Json(static_cast<int64_t>(pod_states_.size())));
+  out.set("assumed", Json(static_cast<int64_t>(assumed_.size())));
+  return out;
 }
 
 }  // namespace xsched

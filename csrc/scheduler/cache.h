@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "common/clock.h"
+#include "common/json.h"
 #include "framework/types.h"
 
 namespace xsched {
@@ -74,6 +75,17 @@ class SchedulerCache {
   // 64-bit hash of "ns/name", as NodeInfo::pg_count).
   int assigned_in_group(uint64_t pg_key) const;
   int assigned_in_group(const std::string& pg_full_name) const { return assigned_in_group(pg_key_of(pg_full_name)); }
+  // Cache debugger (upstream internal/cache/debugger): compares the cache
+  // with the listers' view — `assigned` pods (nodeName set) and Node names —
+  // and re-derives every NodeInfo's accounting and the PodGroup counts from
+  // the pods. Returns {"clean": bool, "missing_pods", "redundant_pods",
+  // "wrong_node", "missing_nodes", "redundant_nodes", "accounting",
+  // "group_counts", "assumed"}. Transient differences are expected while
+  // events are in flight.
+  Json check(const std::vector<PodPtr>& assigned, const std::vector<std::string>& nodes) const;
+  // Per node: pods, requested resources and GPU availability (upstream
+  // CacheDumper), plus assumed pods.
+  Json dump() const;
   size_t node_count() const;
   size_t pod_count() const;
   size_t assumed_count() const;

@@ -1105,6 +1105,33 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   }
 }
 
+Json Scheduler::check_cache() const {
+  std::vector<PodPtr> assigned;
+  for (auto& p : informers_->all_pods())
+    if (!p->node_name.empty()) assigned.push_back(std::move(p));
+  std::vector<std::string> nodes;
+  for (const auto& n : store_->list("nodes", "")) nodes.push_back((*n)["metadata"]["name"].as_string());
+  return cache_->check(assigned, nodes);
+}
+
+Json Scheduler::dump_cache() const {
+  Json out = cache_->dump();
+  auto c = queue_->counts();
+  Json q = Json::object();
+  q.set("active", Json(static_cast<int64_t>(c.active)));
+  q.set("backoff", Json(static_cast<int64_t>(c.backoff)));
+  q.set("unschedulable", Json(static_cast<int64_t>(c.unschedulable)));
+  Json pending = Json::array();
+  for (const auto& qpi : queue_->pending_pods()) pending.push_back(Json(qpi->pod->key()));
+  q.set("pods", std::move(pending));
+  out.set("queue", std::move(q));
+  int64_t waiting = 0;
+  for (const auto& w : waiting_) waiting += static_cast<int64_t>(w->size());
+  out.set("waiting_pods", Json(waiting));
+  out.set("nominated_pods", Json(static_cast<int64_t>(nominator_->size())));
+  return out;
+}
+
 Json Scheduler::explain(const Json& pod_obj) {
   std::lock_guard<std::mutex> g(sched_mu_);
   Json out = Json::object();

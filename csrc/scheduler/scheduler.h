@@ -124,6 +124,11 @@ class Scheduler {
   // Dry-run one scheduling cycle for `pod` (no assume/bind): filter verdicts
   // per node, per-plugin normalized scores and the host that would be chosen.
   Json explain(const Json& pod);
+  // Cache debugger (upstream internal/cache/debugger, SIGUSR2 in
+  // kube-scheduler): the cache against the listers and the store's Nodes,
+  // and a dump of cache, queue and waiting pods.
+  Json check_cache() const;
+  Json dump_cache() const;
   // Score micro-benchmark (the reference's BenchmarkTargetLoadPackingPlugin,
   // pkg/trimaran/targetloadpacking/targetloadpacking_test.go:267-360):
   // PreScore + node-parallel Score + NormalizeScore of `pod` over every node

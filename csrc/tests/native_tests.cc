@@ -23,6 +23,7 @@
 #include "common/parallel.h"
 #include "common/quantity.h"
 #include "framework/types.h"
+#include "scheduler/cache.h"
 #include "scheduler/queue.h"
 #include "store/store.h"
 
@@ -430,6 +431,45 @@ TEST(store_optimistic_updates_lose_nothing) {
   CHECK(bound);
   CHECK_EQ((*cur)["spec"]["nodeName"].as_string(), "node-1");
   CHECK_EQ(st.resource_version() - rv0, static_cast<int64_t>(kThreads * kEach + 1));
+}
+
+TEST(cache_debugger_reports_drift) {
+  auto node = [](const std::string& name) {
+    return Node::from_json(Json::parse(R"({"metadata":{"name":")" + name +
+                                       R"("},"status":{"allocatable":{"cpu":"8","memory":"16Gi","pods":"10"}}})"));
+  };
+  auto pod = [](const std::string& name, const std::string& on) {
+    return Pod::from_json(Json::parse(R"({"metadata":{"namespace":"d","name":")" + name + R"(","uid":"u-)" + name +
+                                      R"("},"spec":{"nodeName":")" + on +
+                                      R"(","containers":[{"name":"c","resources":{"requests":{"cpu":"1"}}}]}})"));
+  };
+  SchedulerCache cache(std::make_shared<FakeClock>(0), 1'000'000);
+  cache.add_node(node("a"));
+  cache.add_node(node("b"));
+  auto p1 = pod("p1", "a"), p2 = pod("p2", "b");
+  cache.add_pod(p1);
+  cache.add_pod(p2);
+  Json ok = cache.check({p1, p2}, {"a", "b"});
+  CHECK(ok["clean"].as_bool());
+  // Listers with a pod the cache lacks, without one it has, a moved pod and
+  // an extra Node.
+  auto p3 = pod("p3", "a"), p2b = pod("p2", "a");
+  Json bad = cache.check({p2b, p3}, {"a", "b", "c"});
+  CHECK(!bad["clean"].as_bool());
+  CHECK_EQ(bad["missing_pods"].items().size(), 1u);
+  CHECK_EQ(bad["missing_pods"].items()[0].as_string(), "d/p3");
+  CHECK_EQ(bad["redundant_pods"].items()[0].as_string(), "d/p1");
+  CHECK_EQ(bad["wrong_node"].items().size(), 1u);
+  CHECK_EQ(bad["missing_nodes"].items()[0].as_string(), "c");
+  // A NodeInfo whose incremental totals drifted from its pods.
+  NodeInfo ni;
+  ni.set_node(node("x"));
+  ni.add_pod(pod("q", "x"));
+  CHECK(ni.verify().empty());
+  ni.requested.v[kCPU] += 500;
+  auto fields = ni.verify();
+  CHECK_EQ(fields.size(), 1u);
+  CHECK_EQ(fields[0], "requested");
 }
 
 int main() {

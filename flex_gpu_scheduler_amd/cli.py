@@ -169,6 +169,16 @@ def _library_watchers(cfg, remote, store_client) -> list:
     return out
 
 
+def _on_sigusr2(sched) -> None:
+    """kube-scheduler's cache debugger signal: SIGUSR2 logs the cache
+    comparison and the cache dump (one JSON line each) to stderr."""
+    def handler(signum, frame):  # noqa: ARG001
+        print(json.dumps({"cache_compare": sched.check_cache()}), file=sys.stderr, flush=True)
+        print(json.dumps({"cache_dump": sched.dump_cache()}), file=sys.stderr, flush=True)
+    if threading.current_thread() is threading.main_thread():
+        signal.signal(signal.SIGUSR2, handler)
+
+
 def cmd_scheduler(args) -> int:
     from .config import load_config
     from .control.client import LocalClient
@@ -196,6 +206,9 @@ def cmd_scheduler(args) -> int:
     http.add_route("POST", "/debug/explain", lambda q, b: (200, "application/json", rs.scheduler.explain(b)))
     http.add_route("GET", "/debug/stats", lambda q, b: (200, "application/json", {
         "stats": rs.scheduler.stats(), "queue": rs.scheduler.queue_counts(), "mirror_applied": rs.mirror.applied}))
+    http.add_route("GET", "/debug/cache/compare", lambda q, b: (200, "application/json", rs.scheduler.check_cache()))
+    http.add_route("GET", "/debug/cache/dump", lambda q, b: (200, "application/json", rs.scheduler.dump_cache()))
+    _on_sigusr2(rs.scheduler)
     http.start()
     print(json.dumps({"scheduler": [p.scheduler_name for p in cfg.profiles], "metrics": http.url}), flush=True)
     stop = threading.Event()
