@@ -84,7 +84,7 @@ def main() -> int:
     shard = Shard(spec, namespace=f"bench-r{ctx.rank}", seed=args.seed + 7919 * ctx.rank,
                   options=json.loads(args.sched_options))
     # Pre-render every wave's JSON (data preparation, outside the timed region).
-    waves = [shard.wave(i) for i in range(args.warmup + args.steps)]
+    waves = [shard.wave(i) for i in range(args.warmup + args.steps + 1)]  # +1: the untimed check wave
     prepared = [(w.groups_json(), w.pods_json()) for w in waves]
 
     for i in range(args.warmup):
@@ -108,6 +108,13 @@ def main() -> int:
         with open(args.trace, "w") as f:
             f.write(shard.sched.trace_json())
 
+    # Untimed: one more wave, and once it is bound the cache debugger
+    # compares the cache with the listers and re-derives every node's
+    # accounting (resources, GPU ledger, gang counts) from its pods.
+    check: dict = {}
+    shard.run(waves[-1], prepared=prepared[-1], check_cache=check)
+    extras["cache_check"] = {"clean": bool(check.get("clean")), "assumed": check.get("assumed"),
+                             "accounting_mismatches": len(check.get("accounting", []))}
     t_max = ctx.all_max(elapsed)
     pods_total = ctx.all_sum(float(pods))
     all_gangs = [g for part in ctx.gather(gangs) for g in part]

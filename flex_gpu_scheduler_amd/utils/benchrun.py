@@ -48,7 +48,12 @@ class Shard:
     def wave(self, step: int) -> Wave:
         return make_wave(self.spec, step, namespace=self.ns, seed=self.seed)
 
-    def run(self, wave: Wave, timeout_s: float = 120.0, *, prepared: tuple[str, str] | None = None) -> StepResult:
+    def run(self, wave: Wave, timeout_s: float = 120.0, *, prepared: tuple[str, str] | None = None,
+            check_cache: dict | None = None) -> StepResult:
+        """One wave: create, wait until bound, delete, wait until the cache
+        drained. With `check_cache` (a dict, filled in), the cache debugger
+        runs once the wave is bound and no binding is in flight, before the
+        deletion (untimed callers only)."""
         groups_js, pods_js = prepared if prepared else (wave.groups_json(), wave.pods_json())
         n = len(wave.pods)
         target = self._bound + n
@@ -68,6 +73,10 @@ class Shard:
             time.sleep(0.0002)
         self._bound = target
         t_bound = time.perf_counter()
+        if check_cache is not None:
+            while sched.stats()["inflight_bindings"] > 0 and time.perf_counter() < deadline:
+                time.sleep(0.0002)
+            check_cache.update(sched.check_cache())
         gangs = sched.gang_records(True)
         self.store.delete_all("pods", self.ns)
         self.store.delete_all("podgroups", self.ns)
