@@ -370,8 +370,13 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
   p->priority_class_name = spec["priorityClassName"].as_string();
   p->priority = static_cast<int32_t>(spec["priority"].as_int(0));
   if (spec["preemptionPolicy"].is_string()) p->preemption_policy = spec["preemptionPolicy"].as_string();
-  for (const auto& c : spec["containers"].items()) p->containers.push_back(parse_container(c));
-  for (const auto& c : spec["initContainers"].items()) p->init_containers.push_back(parse_container(c));
+  {
+    std::vector<Container> cs, ics;
+    for (const auto& c : spec["containers"].items()) cs.push_back(parse_container(c));
+    for (const auto& c : spec["initContainers"].items()) ics.push_back(parse_container(c));
+    p->containers = std::move(cs);
+    p->init_containers = std::move(ics);
+  }
   p->overhead = Res::from_json(spec["overhead"]);
   p->node_selector = strmap_from_json(spec["nodeSelector"]);
   if (const Json* na = spec.path({"affinity", "nodeAffinity"})) {

@@ -96,6 +96,30 @@ struct Container {
   std::vector<ContainerPort> ports;
 };
 
+// A vector fixed at parse time and shared by every copy of its object: the
+// scheduler copies a Pod per scheduled pod (the assumed pod, the informer's
+// bound object), and those copies then share the containers instead of
+// duplicating their names, images and resource vectors.
+template <typename T>
+class SharedVec {
+ public:
+  SharedVec() = default;
+  SharedVec(std::vector<T> v)  // NOLINT: implicit on purpose
+      : p_(v.empty() ? nullptr : std::make_shared<const std::vector<T>>(std::move(v))) {}
+  const std::vector<T>& get() const {
+    static const std::vector<T> kEmpty;
+    return p_ ? *p_ : kEmpty;
+  }
+  typename std::vector<T>::const_iterator begin() const { return get().begin(); }
+  typename std::vector<T>::const_iterator end() const { return get().end(); }
+  size_t size() const { return p_ ? p_->size() : 0; }
+  bool empty() const { return !p_; }
+  const T& operator[](size_t i) const { return (*p_)[i]; }
+
+ private:
+  std::shared_ptr<const std::vector<T>> p_;
+};
+
 enum class QoS : uint8_t { BestEffort = 0, Burstable = 1, Guaranteed = 2 };
 
 struct PodAffinityTerm {
@@ -185,7 +209,7 @@ struct Pod {
   std::string node_name, nominated_node_name, priority_class_name, phase = "Pending";
   IStr preemption_policy = "PreemptLowerPriority";
   int32_t priority = 0;
-  std::vector<Container> containers, init_containers;
+  SharedVec<Container> containers, init_containers;
   Res overhead;
   StrMap node_selector;
   std::vector<NodeSelectorTerm> required_node_terms;  // OR of terms
