@@ -20,6 +20,14 @@
 #include "common/parallel.h"
 #include "framework/types.h"
 
+// A Filter verdict with a fixed message, built once per call site for the
+// life of the process (Status::immortal): returning it costs a plain copy.
+#define XS_FIXED_STATUS(code, msg)                                 \
+  ([]() -> const ::xsched::Status& {                               \
+    static const ::xsched::Status fixed_status = ::xsched::Status::immortal(code, msg); \
+    return fixed_status;                                          \
+  }())
+
 namespace xsched {
 
 class Framework;
@@ -74,10 +82,10 @@ struct Handle {
 class Plugin {
  public:
   explicit Plugin(std::string name, uint32_t points)
-      : name_(std::move(name)), name_ptr_(std::make_shared<const std::string>(name_)), points_(points) {}
+      : name_(std::move(name)), name_ptr_(&Status::intern_plugin(name_)), points_(points) {}
   virtual ~Plugin() = default;
   const std::string& name() const { return name_; }
-  const std::shared_ptr<const std::string>& name_ptr() const { return name_ptr_; }
+  const std::string* name_ptr() const { return name_ptr_; }  // interned
   uint32_t points() const { return points_; }
 
   // QueueSort
@@ -147,7 +155,7 @@ class Plugin {
 
  protected:
   std::string name_;
-  std::shared_ptr<const std::string> name_ptr_;
+  const std::string* name_ptr_;
   uint32_t points_;
 };
 using PluginPtr = std::shared_ptr<Plugin>;

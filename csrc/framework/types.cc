@@ -21,6 +21,8 @@ const std::vector<std::string>& Status::reasons() const {
   return reasons_ ? *reasons_ : kNone;
 }
 
+const std::string& Status::intern_plugin(std::string_view p) { return IStr::intern(p); }
+
 const std::string& Status::failed_plugin() const {
   static const std::string kNone;
   return plugin_ ? *plugin_ : kNone;

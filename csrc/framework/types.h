@@ -35,15 +35,28 @@ const char* code_name(Code c);
 class Status {
  public:
   Status() = default;
+  // Copies only: a moved-from Status would keep a raw view of reasons its
+  // owner took along, so moves copy (one reference count).
+  Status(const Status&) = default;
+  Status& operator=(const Status&) = default;
   explicit Status(Code c) : code_(c) {}
   Status(Code c, std::string reason)
-      : code_(c), reasons_(std::make_shared<const std::vector<std::string>>(1, std::move(reason))) {}
+      : code_(c), owner_(std::make_shared<const std::vector<std::string>>(1, std::move(reason))), reasons_(owner_.get()) {}
   Status(Code c, std::vector<std::string> reasons)
-      : code_(c), reasons_(std::make_shared<const std::vector<std::string>>(std::move(reasons))) {}
+      : code_(c), owner_(std::make_shared<const std::vector<std::string>>(std::move(reasons))), reasons_(owner_.get()) {}
   static Status ok() { return Status(); }
   static Status error(std::string r) { return Status(Code::Error, std::move(r)); }
   static Status unschedulable(std::string r) { return Status(Code::Unschedulable, std::move(r)); }
   static Status unresolvable(std::string r) { return Status(Code::UnschedulableAndUnresolvable, std::move(r)); }
+  // A failure built once for the life of the process (a plugin's fixed
+  // Filter verdicts): copies share its reasons without a reference count, so
+  // 16 Filter workers returning it for thousands of nodes never contend on
+  // one atomic counter.
+  static Status immortal(Code c, std::string reason) {
+    Status s(c);
+    s.reasons_ = new std::vector<std::string>(1, std::move(reason));  // never freed
+    return s;
+  }
 
   Code code() const { return code_; }
   bool is_success() const { return code_ == Code::Success; }
@@ -55,23 +68,26 @@ class Status {
   const std::vector<std::string>& reasons() const;
   // Identity of the shared reasons list: statuses copied from one another
   // (e.g. a plugin's per-thread memo of a failure) compare equal here.
-  const void* reasons_id() const { return reasons_.get(); }
-  const void* plugin_id() const { return plugin_.get(); }
+  const void* reasons_id() const { return reasons_; }
+  const void* plugin_id() const { return plugin_; }
   std::string message() const;
   const std::string& failed_plugin() const;
-  Status& with_plugin(std::string p) {
-    plugin_ = std::make_shared<const std::string>(std::move(p));
+  // Plugin names are interned (immortal), so a Status carries a plain pointer.
+  Status& with_plugin(std::string_view p) {
+    plugin_ = &intern_plugin(p);
     return *this;
   }
-  Status& with_plugin(std::shared_ptr<const std::string> p) {
-    plugin_ = std::move(p);
+  Status& with_plugin(const std::string* interned) {
+    plugin_ = interned;
     return *this;
   }
+  static const std::string& intern_plugin(std::string_view p);
 
  private:
   Code code_ = Code::Success;
-  std::shared_ptr<const std::vector<std::string>> reasons_;
-  std::shared_ptr<const std::string> plugin_;
+  std::shared_ptr<const std::vector<std::string>> owner_;  // empty for immortal statuses
+  const std::vector<std::string>* reasons_ = nullptr;
+  const std::string* plugin_ = nullptr;
 };
 
 // --------------------------------------------------------- CycleState ----

@@ -35,7 +35,7 @@ class NodeUnschedulable : public Plugin {
     Taint t{"node.kubernetes.io/unschedulable", "", "NoSchedule"};
     for (const auto& tol : p.tolerations)
       if (tol.tolerates(t)) return {};
-    return Status::unresolvable("node(s) were unschedulable");
+    return XS_FIXED_STATUS(Code::UnschedulableAndUnresolvable, "node(s) were unschedulable");
   }
   std::vector<ClusterEvent> events_to_register() const override {
     return {{"Node", kAdd | kUpdateNodeTaint, ""}};
@@ -50,7 +50,7 @@ class NodeName : public Plugin {
   NodeName() : Plugin("NodeName", kFilter) {}
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     if (p.node_name.empty() || p.node_name == ni.name()) return {};
-    return Status::unresolvable("node(s) didn't match the requested node name");
+    return XS_FIXED_STATUS(Code::UnschedulableAndUnresolvable, "node(s) didn't match the requested node name");
   }
   std::vector<ClusterEvent> events_to_register() const override { return {{"Node", kAdd, ""}}; }
 };
@@ -66,7 +66,7 @@ class NodePorts : public Plugin {
       for (const auto& [ip, proto, hp] : ni.used_ports) {
         if (hp != port.host_port || proto != port.protocol) continue;
         if (ip == "0.0.0.0" || port.host_ip == "0.0.0.0" || ip == port.host_ip)
-          return Status::unschedulable("node(s) didn't have free ports for the requested pod ports");
+          return XS_FIXED_STATUS(Code::Unschedulable, "node(s) didn't have free ports for the requested pod ports");
       }
     }
     return {};
@@ -300,9 +300,10 @@ class NodeAffinity : public Plugin {
       bool ok = false;
       for (const auto& t : added_)
         if (term_matches(t, *ni.node)) ok = true;
-      if (!ok) return Status::unresolvable("node(s) didn't match scheduler-enforced node affinity");
+      if (!ok) return XS_FIXED_STATUS(Code::UnschedulableAndUnresolvable, "node(s) didn't match scheduler-enforced node affinity");
     }
-    if (!required_matches(p, *ni.node)) return Status::unresolvable("node(s) didn't match Pod's node affinity/selector");
+    if (!required_matches(p, *ni.node))
+      return XS_FIXED_STATUS(Code::UnschedulableAndUnresolvable, "node(s) didn't match Pod's node affinity/selector");
     return {};
   }
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {

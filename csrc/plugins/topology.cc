@@ -46,23 +46,23 @@ int64_t count_matching(const std::vector<PodPtr>& pods, const LabelSelector& sel
 // Filter failures, built once: a failing node costs a Status copy (two
 // refcount increments), not a string, vector and control block per node.
 const Status& kSpreadMissingLabel() {
-  static const Status st = Status::unresolvable("node(s) didn't match pod topology spread constraints (missing required label)");
+  static const Status st = Status::immortal(Code::UnschedulableAndUnresolvable, "node(s) didn't match pod topology spread constraints (missing required label)");
   return st;
 }
 const Status& kSpreadSkew() {
-  static const Status st = Status::unschedulable("node(s) didn't match pod topology spread constraints");
+  static const Status st = Status::immortal(Code::Unschedulable, "node(s) didn't match pod topology spread constraints");
   return st;
 }
 const Status& kAffinityUnmet() {
-  static const Status st = Status::unresolvable("node(s) didn't match pod affinity rules");
+  static const Status st = Status::immortal(Code::UnschedulableAndUnresolvable, "node(s) didn't match pod affinity rules");
   return st;
 }
 const Status& kAntiAffinityUnmet() {
-  static const Status st = Status::unschedulable("node(s) didn't match pod anti-affinity rules");
+  static const Status st = Status::immortal(Code::Unschedulable, "node(s) didn't match pod anti-affinity rules");
   return st;
 }
 const Status& kExistingAntiAffinityUnmet() {
-  static const Status st = Status::unschedulable("node(s) didn't satisfy existing pods anti-affinity rules");
+  static const Status st = Status::immortal(Code::Unschedulable, "node(s) didn't satisfy existing pods anti-affinity rules");
   return st;
 }
 
