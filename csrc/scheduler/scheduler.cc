@@ -774,7 +774,6 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     Parallelizer::record_inline(&filter_site_, Parallelizer::now_ns() - t0, processed, n);
   } else {
     std::atomic<int> count{0};
-    std::atomic<int> aprocessed{0};
     std::atomic<bool> stop{false};
     std::atomic<uint64_t> ahits{0};
     std::mutex mu;
@@ -796,7 +795,6 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
         own = fw.run_filter_with_nominated_pods(s, p, ni);
       }
       const Status& fst = *fp;
-      aprocessed.fetch_add(1, std::memory_order_relaxed);
       if (fst.is_success()) {
         int len = count.fetch_add(1) + 1;
         if (len > to_find) {
@@ -825,7 +823,11 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       }
     }, &stop, &filter_site_);
     c = std::min(count.load(), to_find);
-    processed = aprocessed.load();
+    // Processed = feasible kept + failed (upstream's feasible +
+    // len(NodeToStatusMap)); counted here instead of by a shared atomic
+    // that every worker would bump per node.
+    processed = c;
+    for (int pos = 0; pos < n; ++pos) processed += fail_ptr_[pos] != nullptr;
     hits = ahits.load();
   }
   if (eq_filter) {
