@@ -179,7 +179,31 @@ struct SpreadFilterState : StateData {
   std::vector<TopologySpreadConstraint> constraints;
   TopoCounts pair_num;                                                    // key -> value -> matching pods
   std::unordered_map<std::string, std::array<CriticalPath, 2>> critical;  // topology key -> two smallest
-  std::shared_ptr<StateData> clone() const override { return std::make_shared<SpreadFilterState>(*this); }
+  // Per constraint (index()): its value counts, the current minimum
+  // (INT64_MIN: no critical paths) and whether the incoming pod matches its
+  // own selector, so Filter does one hash lookup per constraint and node.
+  std::vector<const std::unordered_map<std::string, int64_t>*> counts_c;
+  std::vector<int64_t> min_c;
+  std::vector<int64_t> self_c;
+  std::shared_ptr<StateData> clone() const override {
+    auto c = std::make_shared<SpreadFilterState>(*this);
+    c->index();  // the copied pointers still point into this state's maps
+    return c;
+  }
+  void index() {
+    counts_c.clear();
+    min_c.clear();
+    for (const auto& c : constraints) {
+      auto kit = pair_num.find(c.topology_key);
+      counts_c.push_back(kit == pair_num.end() ? nullptr : &kit->second);
+      auto cit = critical.find(c.topology_key);
+      min_c.push_back(cit == critical.end() ? INT64_MIN : cit->second[0].num);
+    }
+  }
+  void set_pod(const Pod& p) {
+    self_c.clear();
+    for (const auto& c : constraints) self_c.push_back(c.selector.matches(p.meta.labels) ? 1 : 0);
+  }
 
   void recompute_critical() {
     for (auto& [key, p] : critical) p = {CriticalPath{}, CriticalPath{}};
@@ -248,6 +272,8 @@ class PodTopologySpread : public Plugin {
         if (snap.replay_since(m->seq, [&](const PodDelta& d) { count_delta(ms, p, *d.pod, *d.node, d.d); })) {
           m->seq = snap.delta_end;
           ms.recompute_critical();
+          ms.index();
+          ms.set_pod(p);
           s.write(kFilterKey, m->st);
           return {};
         }
@@ -273,6 +299,8 @@ class PodTopologySpread : public Plugin {
         for (const auto& [value, num] : values) st->update_critical(key, value, num);
       memo_.put(p.spec_hash, p.ns(), 0, *h_.snapshot, st);
     }
+    st->index();
+    st->set_pod(p);
     s.write(kFilterKey, st);
     return {};
   }
@@ -300,6 +328,7 @@ class PodTopologySpread : public Plugin {
       num += delta;
       st->update_critical(c.topology_key, v, num);
     }
+    st->index();
   }
   Status add_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
     update_with_pod(s, p, *q, ni, 1);
@@ -315,21 +344,17 @@ class PodTopologySpread : public Plugin {
     if (!st) return Status::error("PodTopologySpread: no PreFilter state");
     if (st->constraints.empty()) return {};
     const Node& n = *ni.node;
-    for (const auto& c : st->constraints) {
+    for (size_t i = 0; i < st->constraints.size(); ++i) {
+      const auto& c = st->constraints[i];
       const std::string* v = n.meta.label(c.topology_key);
       if (!v) return kSpreadMissingLabel();
-      int64_t self = c.selector.matches(p.meta.labels) ? 1 : 0;
-      auto cit = st->critical.find(c.topology_key);
-      if (cit == st->critical.end()) return Status::error("PodTopologySpread: internal error: no critical paths");
-      int64_t min_num = cit->second[0].num;
+      if (st->min_c[i] == INT64_MIN) return Status::error("PodTopologySpread: internal error: no critical paths");
       int64_t num = 0;
-      auto kit = st->pair_num.find(c.topology_key);
-      if (kit != st->pair_num.end()) {
-        auto it = kit->second.find(*v);
-        if (it != kit->second.end()) num = it->second;
+      if (const auto* counts = st->counts_c[i]) {
+        auto it = counts->find(*v);
+        if (it != counts->end()) num = it->second;
       }
-      if (num + self - min_num > c.max_skew)
-        return kSpreadSkew();
+      if (num + st->self_c[i] - st->min_c[i] > c.max_skew) return kSpreadSkew();
     }
     return {};
   }
