@@ -506,7 +506,35 @@ class PodTopologySpread : public Plugin {
 // ====================================================== InterPodAffinity ====
 struct AffinityFilterState : StateData {
   TopoCounts existing_anti, affinity, anti;
-  std::shared_ptr<StateData> clone() const override { return std::make_shared<AffinityFilterState>(*this); }
+  // The incoming pod's required (anti-)affinity term keys and, per term,
+  // its value counts (nullptr: none), resolved once per cycle (index()) so
+  // Filter does one hash lookup per term and node.
+  std::vector<std::string> aff_keys, anti_keys;
+  std::vector<const std::unordered_map<std::string, int64_t>*> aff_c, anti_c;
+  std::shared_ptr<StateData> clone() const override {
+    auto c = std::make_shared<AffinityFilterState>(*this);
+    c->index();  // the copied pointers still point into this state's maps
+    return c;
+  }
+  void set_pod(const Pod& p) {
+    aff_keys.clear();
+    anti_keys.clear();
+    for (const auto& t : p.pod_affinity_required) aff_keys.push_back(t.topology_key);
+    for (const auto& t : p.pod_anti_affinity_required) anti_keys.push_back(t.topology_key);
+    index();
+  }
+  void index() {
+    auto resolve = [](const TopoCounts& m, const std::vector<std::string>& keys,
+                      std::vector<const std::unordered_map<std::string, int64_t>*>& out) {
+      out.clear();
+      for (const auto& k : keys) {
+        auto it = m.find(k);
+        out.push_back(it == m.end() ? nullptr : &it->second);
+      }
+    };
+    resolve(affinity, aff_keys, aff_c);
+    resolve(anti, anti_keys, anti_c);
+  }
   void merge(const AffinityFilterState& o) {
     merge_into(existing_anti, o.existing_anti);
     merge_into(affinity, o.affinity);
@@ -603,9 +631,15 @@ class InterPodAffinity : public Plugin {
   }
 
   Status pre_filter(CycleState& s, const Pod& p) override {
-    if (!h_.snapshot || (h_.snapshot->have_pods_with_required_anti_affinity.empty() &&
-                         p.pod_affinity_required.empty() && p.pod_anti_affinity_required.empty())) {
-      s.write(kFilterKey, empty_state<AffinityFilterState>());
+    const bool own_terms = !p.pod_affinity_required.empty() || !p.pod_anti_affinity_required.empty();
+    if (!h_.snapshot || (h_.snapshot->have_pods_with_required_anti_affinity.empty() && !own_terms)) {
+      if (!own_terms) {
+        s.write(kFilterKey, empty_state<AffinityFilterState>());
+      } else {  // no snapshot: nothing counted, but Filter indexes p's terms
+        auto st = std::make_shared<AffinityFilterState>();
+        st->set_pod(p);
+        s.write(kFilterKey, st);
+      }
       return {};
     }
     const Snapshot& snap = *h_.snapshot;
@@ -615,6 +649,7 @@ class InterPodAffinity : public Plugin {
       AffinityFilterState& ms = *m->st;
       if (snap.replay_since(m->seq, [&](const PodDelta& d) { update(ms, p, *d.pod, *d.node, d.d); })) {
         m->seq = snap.delta_end;
+        ms.set_pod(p);
         s.write(kFilterKey, m->st);
         return {};
       }
@@ -655,17 +690,24 @@ class InterPodAffinity : public Plugin {
     else
       run(0);
     for (const auto& ps : part) st->merge(ps);
+    st->set_pod(p);
     memo_.put(key, p.ns(), nsv, snap, st);
     s.write(kFilterKey, st);
     return {};
   }
   bool has_pre_filter_extensions() const override { return true; }
   Status add_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
-    if (auto* st = s.read_as<AffinityFilterState>(kFilterKey)) update(*st, p, *q, *ni.node, 1);
+    if (auto* st = s.read_as<AffinityFilterState>(kFilterKey)) {
+      update(*st, p, *q, *ni.node, 1);
+      st->set_pod(p);  // a count map may have appeared or gone
+    }
     return {};
   }
   Status remove_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
-    if (auto* st = s.read_as<AffinityFilterState>(kFilterKey)) update(*st, p, *q, *ni.node, -1);
+    if (auto* st = s.read_as<AffinityFilterState>(kFilterKey)) {
+      update(*st, p, *q, *ni.node, -1);
+      st->set_pod(p);
+    }
     return {};
   }
 
@@ -676,22 +718,27 @@ class InterPodAffinity : public Plugin {
     // satisfyPodAffinity
     if (!p.pod_affinity_required.empty()) {
       bool exist = true;
-      for (const auto& t : p.pod_affinity_required) {
-        const std::string* v = n.meta.label(t.topology_key);
+      for (size_t i = 0; i < p.pod_affinity_required.size(); ++i) {
+        const std::string* v = n.meta.label(p.pod_affinity_required[i].topology_key);
         if (!v) return kAffinityUnmet();
-        if (topo_get(st->affinity, t.topology_key, *v) <= 0) exist = false;
+        const auto* counts = st->aff_c[i];
+        auto it = counts ? counts->find(*v) : decltype(counts->end()){};
+        if (!counts || it == counts->end() || it->second <= 0) exist = false;
       }
       // The first pod of a self-affine series may go anywhere.
       if (!exist && !(st->affinity.empty() && matches_all(p.pod_affinity_required, p.ns(), p)))
         return kAffinityUnmet();
     }
     // satisfyPodAntiAffinity
-    for (const auto& t : p.pod_anti_affinity_required) {
+    for (size_t i = 0; i < p.pod_anti_affinity_required.size(); ++i) {
+      const auto& t = p.pod_anti_affinity_required[i];
       if (counted(t)) {
-        if (st->anti.empty()) continue;
+        const auto* counts = st->anti_c[i];
+        if (!counts) continue;
         const std::string* v = n.meta.label(t.topology_key);
-        if (v && topo_get(st->anti, t.topology_key, *v) > 0)
-          return kAntiAffinityUnmet();
+        if (!v) continue;
+        auto it = counts->find(*v);
+        if (it != counts->end() && it->second > 0) return kAntiAffinityUnmet();
       } else if (n.meta.label(kHostnameLabel)) {
         for (const auto& q : ni.pods)
           if (term_matches(t, p.ns(), *q))
