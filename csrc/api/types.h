@@ -300,6 +300,9 @@ struct PodGroup {
   std::string phase, occupied_by;
   int32_t scheduled = 0, running = 0, succeeded = 0, failed = 0;
   MicroTime schedule_start_time = 0;
+  // Set by the informer when a newer version replaces this object (or the
+  // PodGroup is deleted): per-thread lookup caches drop it then.
+  mutable RelaxedI64 superseded = 0;
   static std::shared_ptr<PodGroup> from_json(const Json& obj);
 };
 using PodGroupPtr = std::shared_ptr<PodGroup>;

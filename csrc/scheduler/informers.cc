@@ -39,13 +39,19 @@ void Informers::upsert_pod_group(const PodGroupPtr& pg) {
   std::unique_lock<std::shared_mutex> g(mu_);
   std::string key = pg->meta.key();
   pgs_by_key_[pg_key_of(key)] = pg;
-  pgs_[std::move(key)] = pg;
+  auto& slot = pgs_[std::move(key)];
+  if (slot && slot != pg) slot->superseded = 1;
+  slot = pg;
 }
 void Informers::delete_pod_group(const std::string& key) {
   std::unique_lock<std::shared_mutex> g(mu_);
   auto it = pgs_by_key_.find(pg_key_of(key));
   if (it != pgs_by_key_.end() && it->second->meta.key() == key) pgs_by_key_.erase(it);
-  pgs_.erase(key);
+  auto pit = pgs_.find(key);
+  if (pit != pgs_.end()) {
+    pit->second->superseded = 1;
+    pgs_.erase(pit);
+  }
 }
 void Informers::upsert_elastic_quota(const ElasticQuotaPtr& eq) {
   std::unique_lock<std::shared_mutex> g(mu_);
@@ -161,14 +167,29 @@ PodGroupPtr Informers::pod_group(const std::string& ns, const std::string& name)
 
 PodGroupPtr Informers::pod_group_of(const Pod& p) const {
   if (!p.pg_key) return nullptr;
+  // Consecutive cycles schedule the members of one gang, and every cycle
+  // looks its PodGroup up several times (PreFilter, PreScore, Permit, gang
+  // metrics): a per-thread last-hit entry, valid until the informer
+  // supersedes the object, skips the shared lock and the map.
+  struct Last {
+    uint64_t owner = 0;
+    uint64_t key = 0;
+    PodGroupPtr pg;
+  };
+  thread_local Last last;
+  if (last.owner == instance_ && last.key == p.pg_key && last.pg && last.pg->superseded.v.load(std::memory_order_relaxed) == 0 &&
+      last.pg->meta.name == p.pod_group && last.pg->meta.ns == p.ns())
+    return last.pg;
+  PodGroupPtr found;
   {
     std::shared_lock<std::shared_mutex> g(mu_);
     auto it = pgs_by_key_.find(p.pg_key);
-    if (it != pgs_by_key_.end() && it->second->meta.name == p.pod_group && it->second->meta.ns == p.ns())
-      return it->second;
     if (it == pgs_by_key_.end()) return nullptr;
+    if (it->second->meta.name == p.pod_group && it->second->meta.ns == p.ns()) found = it->second;
   }
-  return pod_group(p.ns(), p.pod_group);  // hash collision: exact lookup
+  if (!found) found = pod_group(p.ns(), p.pod_group);  // hash collision: exact lookup
+  if (found) last = Last{instance_, p.pg_key, found};
+  return found;
 }
 
 std::vector<PodGroupPtr> Informers::pod_groups() const {

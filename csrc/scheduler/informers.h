@@ -8,6 +8,8 @@
 // and ElasticQuotas by namespace (pkg/capacityscheduling/capacity_scheduling.go:703-708).
 #pragma once
 
+#include <atomic>
+
 #include <map>
 #include <memory>
 #include <shared_mutex>
@@ -58,6 +60,12 @@ class Informers {
 
  private:
   mutable std::shared_mutex mu_;
+  // Distinguishes instances for per-thread caches (an address can be reused).
+  const uint64_t instance_ = next_instance();
+  static uint64_t next_instance() {
+    static std::atomic<uint64_t> n{0};
+    return ++n;
+  }
   std::unordered_map<std::string, PodPtr> pods_;  // ns/name
   // PodGroup members by Pod::pg_key (64-bit hash of "ns/pg"). Readers still
   // compare namespace and group name, so a hash collision cannot mix groups.
