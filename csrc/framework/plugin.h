@@ -77,6 +77,9 @@ struct Handle {
   TimerService* timers = nullptr;
   Metrics* metrics = nullptr;
   const Snapshot* snapshot = nullptr;  // the scheduling cycle's snapshot
+  // Moves these pods (when queued as unschedulable or backing off) to the
+  // active queue; callable from any thread (e.g. a plugin's timer).
+  std::function<void(const std::vector<PodPtr>&)> activate;
 };
 
 class Plugin {

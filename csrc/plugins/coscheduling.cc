@@ -143,7 +143,7 @@ class Coscheduling : public Plugin {
     Res need = pg->min_resources;
     need.set(kPods, pg->min_member);
     if (!check_cluster_resource(need, p)) {
-      denied_.add(p.pg_key, denied_ttl_us_);
+      deny(p);
       return Status::unresolvable("resource gap for PodGroup " + p.pg_full_name());
     }
     permitted_.add(p.pg_key, wait_time(*pg));
@@ -206,11 +206,32 @@ class Coscheduling : public Plugin {
     float gap = static_cast<float>(pg->min_member - assigned) / static_cast<float>(std::max(1, pg->min_member));
     if (gap <= 0.1f) return {PostFilterResult{}, Status(Code::Unschedulable)};
     reject_group(p, "optimistic rejection in PostFilter");
-    denied_.add(p.pg_key, denied_ttl_us_);
+    deny(p);
     permitted_.erase(p.pg_key);
     return {PostFilterResult{},
             Status::unschedulable("PodGroup " + full + " gets rejected due to Pod " + p.name() +
                                   " is unschedulable even after PostFilter")};
+  }
+
+  // Denies p's group for the TTL and, when the TTL runs out, moves its
+  // unschedulable members back to the active queue. Without that, a group
+  // denied after its last member arrived (e.g. a Permit timeout breaking a
+  // gang deadlock at full capacity) waits for the unschedulable-queue flush
+  // (60 s): no cluster event is left to requeue it.
+  void deny(const Pod& p) {
+    denied_.add(p.pg_key, denied_ttl_us_);
+    if (!h_.timers || !h_.activate) return;
+    auto member = std::make_shared<Pod>();
+    member->meta.ns = p.ns();
+    member->pod_group = p.pod_group;
+    member->pg_key = p.pg_key;
+    h_.timers->schedule_after(denied_ttl_us_ + 1000, [this, member] {
+      if (denied_.has(member->pg_key)) return;  // denied again since: that denial's timer retries
+      std::vector<PodPtr> pods;
+      for (auto& q : h_.informers->pods_in_group_of(*member))
+        if (q->node_name.empty()) pods.push_back(std::move(q));
+      if (!pods.empty()) h_.activate(pods);
+    });
   }
 
   // Rejects every waiting member of p's group (the group index visits only
@@ -257,7 +278,7 @@ class Coscheduling : public Plugin {
     auto pg = h_.informers->pod_group_of(*p);
     if (!pg) return;
     reject_group(*p, "rejection in Unreserve");
-    denied_.add(p->pg_key, denied_ttl_us_);
+    deny(*p);
     permitted_.erase(p->pg_key);
   }
 

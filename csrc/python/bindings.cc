@@ -15,6 +15,7 @@
 #include "api/types.h"
 #include "common/json.h"
 #include "common/quantity.h"
+#include "rest/kube.h"
 #include "scheduler/scheduler.h"
 #include "store/store.h"
 #include "telemetry/amdsmi_sampler.h"
@@ -445,6 +446,42 @@ PYBIND11_MODULE(_xsched, m) {
 
   // ---- API client trampoline ----
   py::class_<ApiClient, PyApiClient, std::shared_ptr<ApiClient>>(m, "ApiClient").def(py::init<>());
+
+  // Native service mode (rest/kube.h): REST writes and the LIST/WATCH mirror.
+  auto endpoint = [](const std::string& host, int port, const std::string& token, bool tls, const std::string& ca_file,
+                     const std::string& ca_pem, const std::string& cert_file, const std::string& key_file,
+                     const std::string& cert_pem, const std::string& key_pem, bool insecure, int timeout_ms) {
+    rest::Endpoint ep;
+    ep.host = host;
+    ep.port = port;
+    ep.token = token;
+    ep.timeout_ms = timeout_ms;
+    ep.tls.enabled = tls;
+    ep.tls.ca_file = ca_file;
+    ep.tls.ca_pem = ca_pem;
+    ep.tls.cert_file = cert_file;
+    ep.tls.key_file = key_file;
+    ep.tls.cert_pem = cert_pem;
+    ep.tls.key_pem = key_pem;
+    ep.tls.insecure = insecure;
+    return ep;
+  };
+  py::class_<rest::Endpoint>(m, "RestEndpoint")
+      .def(py::init(endpoint), py::arg("host"), py::arg("port"), py::arg("token") = "", py::arg("tls") = false,
+           py::arg("ca_file") = "", py::arg("ca_pem") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
+           py::arg("cert_pem") = "", py::arg("key_pem") = "", py::arg("insecure") = false,
+           py::arg("timeout_ms") = 30000);
+  py::class_<rest::RestApiClient, ApiClient, std::shared_ptr<rest::RestApiClient>>(m, "RestApiClient")
+      .def(py::init<rest::Endpoint>())
+      .def("requests", &rest::RestApiClient::requests);
+  py::class_<rest::RemoteMirror, std::shared_ptr<rest::RemoteMirror>>(m, "RemoteMirror")
+      .def(py::init<rest::Endpoint, std::shared_ptr<ObjectStore>, std::vector<std::string>>())
+      .def("start", &rest::RemoteMirror::start)
+      .def("wait_synced", &rest::RemoteMirror::wait_synced, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &rest::RemoteMirror::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("applied", &rest::RemoteMirror::applied)
+      .def_property_readonly("relists", &rest::RemoteMirror::relists)
+      .def("last_error", &rest::RemoteMirror::last_error);
 
   // ---- scheduler ----
   py::class_<Scheduler, std::shared_ptr<Scheduler>>(m, "Scheduler")

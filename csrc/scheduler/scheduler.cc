@@ -192,6 +192,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.nominator = nominator_.get();
     h.clock = clock_;
     h.timers = timers_.get();
+    h.activate = [this](const std::vector<PodPtr>& pods) { queue_->activate(pods); };
     h.metrics = metrics_.get();
     h.snapshot = &snapshot_;
     frameworks_.push_back(std::make_unique<Framework>(pc, h));

@@ -29,7 +29,9 @@ BUILD = ROOT / "build"
 HIP_ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
-CORE_DIRS = ["common", "api", "store", "framework", "scheduler", "plugins"]
+CORE_DIRS = ["common", "api", "store", "framework", "scheduler", "plugins", "rest"]
+# OpenSSL for the native REST client's TLS (rest/http.cc).
+LINK_LIBS = ["-lssl", "-lcrypto"]
 CXXFLAGS = ["-std=c++20", "-O3", "-fPIC", "-Wall", "-Wno-unused-variable", "-Wno-unused-parameter",
             "-Wno-sign-compare", "-fvisibility=hidden", "-pthread"]
 
@@ -95,7 +97,7 @@ def build_core(verbose: bool = True) -> Path:
     out = PKG / f"_xsched{_ext_suffix()}"
     newest = max(o.stat().st_mtime for o in objs)
     if not out.exists() or out.stat().st_mtime < newest:
-        cmd = ["g++", "-shared", "-pthread", *[str(o) for o in objs], "-o", str(out)]
+        cmd = ["g++", "-shared", "-pthread", *[str(o) for o in objs], *LINK_LIBS, "-o", str(out)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
@@ -131,7 +133,7 @@ def build_tsan(verbose: bool = True) -> Path:
     extra = ["-fsanitize=thread", "-g", "-O1", "-include", str(CSRC / "tools" / "tsan_compat.h")]
     objs = build_objects(core_sources() + [CSRC / "tools" / "stress_main.cc"], BUILD / "tsan", extra, includes)
     out = BUILD / "xsched_stress_tsan"
-    cmd = ["g++", "-fsanitize=thread", "-pthread", *[str(o) for o in objs], "-o", str(out)]
+    cmd = ["g++", "-fsanitize=thread", "-pthread", *[str(o) for o in objs], *LINK_LIBS, "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"tsan link failed:\n{r.stderr[-8000:]}")
@@ -147,7 +149,7 @@ def build_asan(verbose: bool = True) -> Path:
     objs = build_objects(core_sources() + [CSRC / "tools" / "stress_main.cc"], BUILD / "asan", [*flags, "-g", "-O1"],
                          includes)
     out = BUILD / "xsched_stress_asan"
-    cmd = ["g++", *flags, "-pthread", *[str(o) for o in objs], "-o", str(out)]
+    cmd = ["g++", *flags, "-pthread", *[str(o) for o in objs], *LINK_LIBS, "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"asan link failed:\n{r.stderr[-8000:]}")
@@ -165,7 +167,7 @@ def build_prof(verbose: bool = True, gprof: bool = True) -> Path:
     sub = "prof" if gprof else "stress"
     objs = build_objects(core_sources() + [CSRC / "tools" / "stress_main.cc"], BUILD / sub, extra, includes)
     out = BUILD / ("xsched_stress_prof" if gprof else "xsched_stress")
-    cmd = ["g++", *(["-pg"] if gprof else []), "-pthread", *[str(o) for o in objs], "-o", str(out)]
+    cmd = ["g++", *(["-pg"] if gprof else []), "-pthread", *[str(o) for o in objs], *LINK_LIBS, "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"prof link failed:\n{r.stderr[-8000:]}")
@@ -184,7 +186,7 @@ def build_tests(verbose: bool = True) -> Path:
     newest = max(o.stat().st_mtime for o in objs)
     if out.exists() and out.stat().st_mtime >= newest:
         return out
-    cmd = ["g++", "-pthread", *[str(o) for o in objs], "-o", str(out)]
+    cmd = ["g++", "-pthread", *[str(o) for o in objs], *LINK_LIBS, "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"native tests link failed:\n{r.stderr[-8000:]}")

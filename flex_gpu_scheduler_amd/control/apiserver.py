@@ -135,7 +135,7 @@ class ApiServer:
         self._active_lock = threading.Lock()
         self.requests = 0
         handler = type("Handler", (_Handler,), {"api": self})
-        self.httpd = ThreadingHTTPServer((host, port), handler)
+        self.httpd = _Server((host, port), handler)
         self.httpd.daemon_threads = True
         self._thread: threading.Thread | None = None
         _lifecycle.register(self)
@@ -185,6 +185,13 @@ class ApiServer:
         self.stop()
 
 
+class _Server(ThreadingHTTPServer):
+    # A scheduler opens one watch per kind at once (and binder pools several
+    # keep-alive connections): socketserver's default backlog of 5 drops the
+    # surplus SYNs, which clients only retry after a second.
+    request_queue_size = 128
+
+
 def _store_error(e: Exception) -> ApiError:
     return ApiError(getattr(e, "code", 500), getattr(e, "reason", "InternalError"), str(e))
 
@@ -193,6 +200,9 @@ class _Handler(BaseHTTPRequestHandler):
     api: ApiServer
     protocol_version = "HTTP/1.1"
     server_version = "xsched-apiserver/1"
+    # TCP_NODELAY: keep-alive request/response pairs must not wait on the
+    # peer's delayed ACK (Nagle holds a small second segment ~40 ms).
+    disable_nagle_algorithm = True
 
     def log_message(self, fmt, *args):  # quiet
         pass
@@ -204,8 +214,10 @@ class _Handler(BaseHTTPRequestHandler):
         self.send_response(code)
         self.send_header("Content-Type", content_type)
         self.send_header("Content-Length", str(len(data)))
-        self.end_headers()
-        self.wfile.write(data)
+        # Headers and body in one write (one segment for small responses).
+        self._headers_buffer.append(b"\r\n")
+        self._headers_buffer.append(data)
+        self.flush_headers()
 
     def _error(self, e: ApiError) -> None:
         self._send(e.code, status_obj(e.code, e.reason, e.message))

@@ -64,6 +64,7 @@ class ServiceHTTP:
 class _Handler(BaseHTTPRequestHandler):
     svc: ServiceHTTP
     protocol_version = "HTTP/1.1"
+    disable_nagle_algorithm = True  # keep-alive scrapes: no delayed-ACK stalls
 
     def log_message(self, fmt, *args):
         pass

@@ -102,15 +102,71 @@ def remote_api_client(remote: Client):
     return RemoteApiClient()
 
 
-class RemoteScheduler:
-    """Native scheduler + mirror + remote writer, as one service."""
+def rest_endpoint(remote: Client):
+    """The native REST endpoint (host, port, bearer token, TLS settings) of a
+    RestClient, or None for clients that are not plain REST endpoints."""
+    from .client import RestClient
 
-    def __init__(self, remote: Client, config=None, **options):
+    if not isinstance(remote, RestClient):
+        return None
+    t = remote.tls
+    return native().RestEndpoint(
+        remote.host, remote.port, remote.token or "", remote.https, ca_file=t.ca_file or "",
+        ca_pem=t.ca_data.decode() if t.ca_data else "", cert_file=t.cert_file or "", key_file=t.key_file or "",
+        cert_pem=t.cert_data.decode() if t.cert_data else "", key_pem=t.key_data.decode() if t.key_data else "",
+        insecure=t.insecure, timeout_ms=int(remote.timeout * 1000))
+
+
+class NativeMirror:
+    """StoreMirror's interface over the native LIST/WATCH mirror (rest/kube.h):
+    one native thread per kind, no Python per event."""
+
+    def __init__(self, endpoint, local_store, kinds=SCHEDULER_KINDS):
+        self._m = native().RemoteMirror(endpoint, local_store, list(kinds))
+
+    @property
+    def applied(self) -> int:
+        return self._m.applied
+
+    @property
+    def relists(self) -> int:
+        return self._m.relists
+
+    def start(self) -> "NativeMirror":
+        self._m.start()
+        return self
+
+    def wait_for_sync(self, timeout: float = 30.0) -> bool:
+        ok = self._m.wait_synced(int(timeout * 1000))
+        if not ok and self._m.last_error():
+            log.warning("native mirror not synced: %s", self._m.last_error())
+        return ok
+
+    def stop(self) -> None:
+        self._m.stop()
+
+
+class RemoteScheduler:
+    """Native scheduler + mirror + remote writer, as one service.
+
+    Against a REST endpoint (RestClient: our API server or kube-apiserver)
+    the mirror and the writes are native (`native_io`, the default): bindings,
+    patches, deletes and events go out from the binder threads over pooled
+    keep-alive connections, and every watched kind is mirrored by a native
+    thread. Other clients (e.g. LocalClient) use the Python mirror/writer."""
+
+    def __init__(self, remote: Client, config=None, *, native_io: bool = True, **options):
         from ..scheduler import new_scheduler
 
         self.store = native().Store()
-        self.mirror = StoreMirror(remote, self.store)
-        self.client = remote_api_client(remote)
+        ep = rest_endpoint(remote) if native_io else None
+        if ep is not None:
+            self.mirror = NativeMirror(ep, self.store)
+            self.client = native().RestApiClient(ep)
+        else:
+            self.mirror = StoreMirror(remote, self.store)
+            self.client = remote_api_client(remote)
+        self.native_io = ep is not None
         self.scheduler = new_scheduler(self.store, config, client=self.client, **options)
 
     def start(self, sync_timeout: float = 30.0) -> "RemoteScheduler":

@@ -1,4 +1,5 @@
 import os
+import subprocess
 import sys
 
 import pytest
@@ -22,3 +23,26 @@ def store():
     from flex_gpu_scheduler_amd import Store
 
     return Store()
+
+
+def _openssl(*args, cwd):
+    subprocess.run(["openssl", *args], cwd=cwd, check=True, capture_output=True)
+
+
+@pytest.fixture(scope="session")
+def pki(tmp_path_factory):
+    """CA, server (SAN 127.0.0.1) and client certificates from the openssl CLI,
+    plus an unrelated CA (TLS tests)."""
+    d = tmp_path_factory.mktemp("pki")
+    _openssl("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.crt", "-days", "2",
+             "-subj", "/CN=test-ca", cwd=d)
+    (d / "san.cnf").write_text("subjectAltName=IP:127.0.0.1,DNS:localhost\n")
+    for name, cn in (("server", "127.0.0.1"), ("client", "system:kube-scheduler")):
+        _openssl("req", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{name}.key", "-out", f"{name}.csr",
+                 "-subj", f"/CN={cn}", cwd=d)
+        extra = ["-extfile", "san.cnf"] if name == "server" else []
+        _openssl("x509", "-req", "-in", f"{name}.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial",
+                 "-out", f"{name}.crt", "-days", "2", *extra, cwd=d)
+    _openssl("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "other.key", "-out", "other.crt",
+             "-days", "2", "-subj", "/CN=other-ca", cwd=d)
+    return d

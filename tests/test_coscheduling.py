@@ -118,3 +118,25 @@ def test_gang_latency_records(store):
         assert "xsched_gang_admit_seconds_bucket" in sched.metrics_text()
     finally:
         sched.stop()
+
+
+def test_denied_group_retries_when_the_denial_expires(store):
+    """A gang denied after all its members exist (here: a Permit timeout
+    while a blocker holds the room) is requeued when the denial runs out —
+    not by the 60 s unschedulable flush. Freeing the room while it is still
+    denied moves it once (rejected: denied); nothing else is left to move it."""
+    store.create("nodes", make_node("n", {"pods": "32", "memory": "100"}))
+    store.create("pods", make_pod("blocker", requests={"memory": "40"}, node_name="n", priority=10 ** 6))
+    sched = start(store, coscheduling_config(permit_wait=1, denied=2),
+                  podInitialBackoffSeconds=0.05, podMaxBackoffSeconds=0.1)
+    try:
+        store.create("podgroups", make_pod_group("g", "default", 2))
+        create_all(store, "pods", [pod("g1", 40, "g"), pod("g2", 40, "g")])
+        time.sleep(1.5)  # g1 waited at Permit, timed out; the group is denied
+        assert all(not n for name, n in placements(store).items() if name != "blocker")
+        store.delete("pods", "default", "blocker")
+        t0 = time.time()
+        wait_bound(sched, 2, timeout=10.0)
+        assert time.time() - t0 < 6.0
+    finally:
+        sched.stop()

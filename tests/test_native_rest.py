@@ -1,0 +1,126 @@
+"""Native service mode (csrc/rest/): the REST writer and the LIST/WATCH
+mirror RemoteScheduler uses against a REST endpoint. Bindings carry the
+FlexGPU annotations, a relist drops objects deleted while not watching, and
+TLS (server-verified and mutual) works end to end."""
+import shutil
+import ssl
+import time
+
+import pytest
+
+from flex_gpu_scheduler_amd import load_config
+from flex_gpu_scheduler_amd._native import native
+from flex_gpu_scheduler_amd.control import ApiServer, RestClient
+from flex_gpu_scheduler_amd.control.client import TLSConfig
+from flex_gpu_scheduler_amd.control.remote import RemoteScheduler, rest_endpoint
+from flex_gpu_scheduler_amd.models import GPU, INDEX_ANNOTATION, make_pod, make_pod_group, mi355x_node
+
+from helpers import FLEXGPU_PLUGINS, coscheduling_config
+
+
+def wait_for(fn, timeout=10.0):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        if fn():
+            return True
+        time.sleep(0.02)
+    return bool(fn())
+
+
+def test_native_io_binds_gang_with_annotations(store):
+    srv = ApiServer(store).start()
+    try:
+        client = RestClient(srv.url)
+        client.create("nodes", mi355x_node("n0"))
+        rs = RemoteScheduler(RestClient(srv.url), load_config(coscheduling_config(FLEXGPU_PLUGINS))).start()
+        try:
+            assert rs.native_io
+            client.create("podgroups", make_pod_group("g", min_member=4))
+            for i in range(4):
+                client.create("pods", make_pod(f"w{i}", pod_group="g", limits={GPU: "1"}, requests={GPU: "1"}))
+            assert wait_for(lambda: all(p["spec"].get("nodeName") for p in client.list("pods", "default")[0]))
+            pods = client.list("pods", "default")[0]
+            assert len({p["metadata"]["annotations"][INDEX_ANNOTATION] for p in pods}) == 4
+            # PostBind's PodGroup status patch went out natively too.
+            assert wait_for(lambda: client.get("podgroups", "default", "g")["status"].get("phase") == "Scheduled")
+            assert rs.client.requests() >= 5 and rs.mirror.applied > 0
+        finally:
+            rs.stop()
+    finally:
+        srv.stop()
+
+
+def test_native_mirror_relist_drops_objects_deleted_meanwhile(store):
+    srv = ApiServer(store).start()
+    try:
+        client = RestClient(srv.url)
+        for name in ("a", "b"):
+            client.create("pods", make_pod(name))
+        local = native().Store()
+        ep = rest_endpoint(client)
+        m = native().RemoteMirror(ep, local, ["pods"])
+        m.start()
+        assert m.wait_synced(5000)
+        assert wait_for(lambda: local.count("pods") == 2)
+        m.stop()
+        client.delete("pods", "default", "a")
+        client.create("pods", make_pod("c"))
+        m2 = native().RemoteMirror(ep, local, ["pods"])
+        m2.start()
+        assert m2.wait_synced(5000)
+        names = {p["metadata"]["name"] for p in local.list("pods", "default")[0]}
+        assert names == {"b", "c"}
+        # and it keeps watching
+        client.create("pods", make_pod("d"))
+        assert wait_for(lambda: local.count("pods") == 3)
+        m2.stop()
+    finally:
+        srv.stop()
+
+
+@pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
+@pytest.mark.parametrize("mutual", [False, True], ids=["server-tls", "mtls"])
+def test_native_io_over_tls(store, pki, mutual):
+    srv = ApiServer(store)
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.load_cert_chain(pki / "server.crt", pki / "server.key")
+    if mutual:
+        ctx.verify_mode = ssl.CERT_REQUIRED
+        ctx.load_verify_locations(pki / "ca.crt")
+    srv.httpd.socket = ctx.wrap_socket(srv.httpd.socket, server_side=True)
+    srv.start()
+    try:
+        url = srv.url.replace("http://", "https://")
+        tls = TLSConfig(ca_file=str(pki / "ca.crt"),
+                        cert_file=str(pki / "client.crt") if mutual else None,
+                        key_file=str(pki / "client.key") if mutual else None)
+        client = RestClient(url, tls=tls)
+        client.create("nodes", mi355x_node("n0"))
+        rs = RemoteScheduler(RestClient(url, tls=tls), load_config(coscheduling_config(FLEXGPU_PLUGINS))).start()
+        try:
+            assert rs.native_io
+            client.create("pods", make_pod("p", limits={GPU: "1"}, requests={GPU: "1"}))
+            assert wait_for(lambda: client.get("pods", "default", "p")["spec"].get("nodeName") == "n0")
+        finally:
+            rs.stop()
+    finally:
+        srv.stop()
+
+
+@pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
+def test_native_io_refuses_unknown_ca(store, pki):
+    srv = ApiServer(store)
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.load_cert_chain(pki / "server.crt", pki / "server.key")
+    srv.httpd.socket = ctx.wrap_socket(srv.httpd.socket, server_side=True)
+    srv.start()
+    try:
+        url = srv.url.replace("http://", "https://")
+        ep = rest_endpoint(RestClient(url, tls=TLSConfig(ca_file=str(pki / "other.crt"))))
+        m = native().RemoteMirror(ep, native().Store(), ["pods"])
+        m.start()
+        assert not m.wait_synced(1500)
+        assert "TLS handshake" in m.last_error()
+        m.stop()
+    finally:
+        srv.stop()
