@@ -268,17 +268,33 @@ void RemoteMirror::run(const std::string& kind) {
   int64_t rv = 0;
   int failures = 0;
   std::string line;
+  auto mark_synced = [&] {
+    if (!first) return;
+    first = false;
+    std::lock_guard<std::mutex> g(mu_);
+    ++synced_;
+    synced_cv_.notify_all();
+  };
   while (!stop_.load()) {
     try {
       if (need_list) {
-        rv = relist(kind, pool);
-        need_list = false;
-        if (first) {
-          first = false;
-          std::lock_guard<std::mutex> g(mu_);
-          ++synced_;
-          synced_cv_.notify_all();
+        try {
+          rv = relist(kind, pool);
+        } catch (const StoreError& e) {
+          if (e.code() != 404) throw;
+          // The API does not serve this kind (e.g. a CRD that is not
+          // installed): it mirrors as empty, and the list is retried
+          // now and then in case the CRD appears.
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            last_error_ = kind + ": " + e.what();
+          }
+          mark_synced();
+          for (int i = 0; i < 300 && !stop_.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+          continue;
         }
+        need_list = false;
+        mark_synced();
       }
       HttpConn conn(ep_, pool.tls(), /*streaming=*/true);
       {

@@ -176,7 +176,14 @@ class Informer:
                         last_resync = time.monotonic()
                         for o in self.list():
                             self._fire(1, o, o)
-            except Exception:  # noqa: BLE001
+            except Exception as e:  # noqa: BLE001
+                if getattr(e, "code", 0) == 404 and not self._synced.is_set():
+                    # The API does not serve this kind (a CRD that is not
+                    # installed): sync as empty, retry the list now and then.
+                    log.warning("informer %s: kind not served (%s); treating it as empty", self.kind, e)
+                    self._synced.set()
+                    self._stop.wait(30.0)
+                    continue
                 log.exception("informer %s list/watch failed; retrying", self.kind)
                 time.sleep(backoff)
                 backoff = min(backoff * 2, 5.0)

@@ -124,3 +124,40 @@ def test_native_io_refuses_unknown_ca(store, pki):
         m.stop()
     finally:
         srv.stop()
+
+
+def test_native_mirror_treats_unserved_kind_as_empty():
+    """A kind the API does not serve (a CRD that is not installed, e.g. NRT
+    on a plain kube-apiserver) syncs as empty instead of blocking startup."""
+    import http.server
+    import threading
+
+    class NotFound(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def do_GET(self):  # noqa: N802
+            body = b'{"kind":"Status","apiVersion":"v1","status":"Failure","reason":"NotFound","code":404,' \
+                   b'"message":"the server could not find the requested resource"}'
+            self.send_response(404)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    httpd = http.server.ThreadingHTTPServer(("127.0.0.1", 0), NotFound)
+    threading.Thread(target=httpd.serve_forever, daemon=True).start()
+    try:
+        ep = native().RestEndpoint("127.0.0.1", httpd.server_address[1])
+        local = native().Store()
+        m = native().RemoteMirror(ep, local, ["noderesourcetopologies"])
+        m.start()
+        assert m.wait_synced(3000)
+        assert "could not find the requested resource" in m.last_error()
+        assert local.count("noderesourcetopologies") == 0
+        m.stop()
+    finally:
+        httpd.shutdown()
+        httpd.server_close()
