@@ -200,7 +200,8 @@ class BalancedAllocation : public Plugin {
     weights_ = parse_weights(args["resources"], {{kCPU, 1}, {kMemory, 1}});
   }
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {
-    std::vector<double> fr;
+    double fr[kMaxRes];  // one fraction per weighted resource (no allocation per node)
+    size_t n = 0;
     for (const auto& w : weights_) {
       int64_t alloc = ni.allocatable.get(w.id);
       if (alloc == 0) continue;
@@ -208,15 +209,15 @@ class BalancedAllocation : public Plugin {
                                                        : ni.requested.get(w.id) + p.request.get(w.id);
       double f = static_cast<double>(req) / static_cast<double>(alloc);
       if (f >= 1) return {0, {}};  // over-committed
-      fr.push_back(f);
+      if (n < static_cast<size_t>(kMaxRes)) fr[n++] = f;
     }
-    if (fr.size() < 2) return {kMaxNodeScore, {}};
+    if (n < 2) return {kMaxNodeScore, {}};
     double mean = 0;
-    for (double f : fr) mean += f;
-    mean /= fr.size();
+    for (size_t i = 0; i < n; ++i) mean += fr[i];
+    mean /= static_cast<double>(n);
     double var = 0;
-    for (double f : fr) var += (f - mean) * (f - mean);
-    double sd = fr.size() == 2 ? std::fabs(fr[0] - fr[1]) / 2 : std::sqrt(var / fr.size());
+    for (size_t i = 0; i < n; ++i) var += (fr[i] - mean) * (fr[i] - mean);
+    double sd = n == 2 ? std::fabs(fr[0] - fr[1]) / 2 : std::sqrt(var / static_cast<double>(n));
     return {static_cast<int64_t>((1 - sd) * kMaxNodeScore), {}};
   }
 

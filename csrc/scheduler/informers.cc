@@ -87,8 +87,12 @@ void Informers::delete_priority_class(const std::string& name) {
 }
 
 PodPtr Informers::pod(const std::string& ns, const std::string& name) const {
+  thread_local std::string key;  // no key allocation per lookup
+  key.assign(ns);
+  key.push_back('/');
+  key.append(name);
   std::shared_lock<std::shared_mutex> g(mu_);
-  auto it = pods_.find(ns + "/" + name);
+  auto it = pods_.find(key);
   return it == pods_.end() ? nullptr : it->second;
 }
 

@@ -556,14 +556,27 @@ void Scheduler::handle_node_event(const WatchEvent& ev) {
 }
 
 // -------------------------------------------------------- gang tracking ----
+namespace {
+// "ns/group" in a per-thread buffer: gang bookkeeping runs per pod and a
+// lookup must not allocate a key string.
+const std::string& gang_key(const Pod& p) {
+  thread_local std::string k;
+  k.assign(p.ns());
+  k.push_back('/');
+  k.append(p.pod_group);
+  return k;
+}
+}  // namespace
+
 void Scheduler::note_gang_enqueue(const Pod& p, int64_t t) {
   if (p.pod_group.empty()) return;
+  const std::string& key = gang_key(p);
   std::lock_guard<std::mutex> g(stats_mu_);
-  auto& r = gangs_[p.pg_full_name()];
-  if (r.pg.empty()) {
-    r.pg = p.pg_full_name();
-    r.first_enqueue_us = t;
-  }
+  auto it = gangs_.find(key);
+  if (it != gangs_.end()) return;
+  GangRecord& r = gangs_[key];
+  r.pg = key;
+  r.first_enqueue_us = t;
 }
 
 void Scheduler::note_gang_event(const Pod& p, bool bound) {
@@ -571,8 +584,9 @@ void Scheduler::note_gang_event(const Pod& p, bool bound) {
   auto pg = informers_->pod_group_of(p);
   if (!pg) return;
   int need = std::max(1, pg->min_member);
+  const std::string& key = gang_key(p);
   std::lock_guard<std::mutex> g(stats_mu_);
-  auto it = gangs_.find(p.pg_full_name());
+  auto it = gangs_.find(key);
   if (it == gangs_.end()) return;
   GangRecord& r = it->second;
   r.size = need;
