@@ -91,3 +91,38 @@ def test_compare_reports_a_node_only_the_store_has(store):
     s.sync_informers(50)
     assert s.check_cache()["clean"]
     s.stop()
+
+
+def test_bind_failures_recover_and_leave_cache_consistent(store):
+    """Fault injection (ObjectStore.add_fault): a third of the bindings fail
+    with a server error. Failed binds are unreserved and the pods retried;
+    every pod ends up bound exactly once and the cache matches the listers
+    (upstream handleBindingCycleError: ForgetPod + requeue)."""
+    for i in range(4):
+        store.create("nodes", mi355x_node(f"mi-{i}"))
+    s = new_scheduler(store, load_config(flagship_config(permit_wait_s=2, denied_s=1)),
+                      podInitialBackoffSeconds=0.01, podMaxBackoffSeconds=0.05)
+    store.add_fault("bind", "pods", fail_prob=0.33)
+    s.start()
+    try:
+        for g in range(4):
+            store.create("podgroups", make_pod_group(f"g{g}", "default", 4))
+            for r in range(4):
+                store.create("pods", make_pod(f"g{g}-{r}", pod_group=f"g{g}", requests={"cpu": "2"},
+                                              limits={GPU: "1"}))
+        for i in range(16):
+            store.create("pods", make_pod(f"x{i}", requests={"cpu": "1"}, limits={GPU_XCD: "2"}))
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            pods = store.list("pods", "default")[0]
+            if all(p["spec"].get("nodeName") for p in pods):
+                break
+            time.sleep(0.05)
+        store.clear_faults()
+        assert all(p["spec"].get("nodeName") for p in store.list("pods", "default")[0])
+        assert s.stats()["bind_failures"] > 0
+        quiesce(s)
+        report = s.check_cache()
+        assert report["clean"], report
+    finally:
+        s.stop()
