@@ -560,6 +560,16 @@ PYBIND11_MODULE(_xsched, m) {
              return node_info_dict(*ni);
            })
       .def("node_names", [](Scheduler& s) { return s.cache().node_names(); })
+      .def("wait_bound",
+           [](Scheduler& s, uint64_t target, double timeout_s) {
+             py::gil_scoped_release r;
+             return s.wait_bound(target, static_cast<int64_t>(timeout_s * 1e6));
+           })
+      .def("wait_cache_empty",
+           [](Scheduler& s, double timeout_s) {
+             py::gil_scoped_release r;
+             return s.wait_cache_empty(static_cast<int64_t>(timeout_s * 1e6));
+           })
       .def("cache_counts",
            [](Scheduler& s) {
              py::dict d;

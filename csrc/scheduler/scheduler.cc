@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <map>
 #include <stdexcept>
 
@@ -1122,6 +1123,28 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   }
 }
 
+bool Scheduler::wait_bound(uint64_t target, int64_t timeout_us) const {
+  // Polls a counter instead of a condition variable: the binder threads
+  // then pay nothing per bind, and the waiter (a benchmark harness) wakes
+  // within ~50 us of the last binding.
+  // Wall time, not clock_ (a fake clock in tests does not advance).
+  const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+  while (bound_total_.load(std::memory_order_acquire) < target) {
+    if (std::chrono::steady_clock::now() > end) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  return true;
+}
+
+bool Scheduler::wait_cache_empty(int64_t timeout_us) const {
+  const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+  while (cache_->pod_count() > 0) {
+    if (std::chrono::steady_clock::now() > end) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  return true;
+}
+
 Json Scheduler::check_cache() const {
   std::vector<PodPtr> assigned;
   for (auto& p : informers_->all_pods())
@@ -1319,6 +1342,7 @@ void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
     std::lock_guard<std::mutex> g(stats_mu_);
     ++stats_.bound;
   }
+  bound_total_.fetch_add(1, std::memory_order_release);
   note_gang_event(*assumed, true);
   {
     std::vector<PodPtr> act;

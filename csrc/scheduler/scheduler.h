@@ -153,6 +153,10 @@ class Scheduler {
     uint64_t eq_filter_hits = 0, eq_filter_misses = 0;  // equivalence-cache Filter lookups
   };
   Stats stats() const;
+  // Blocks (without the Python lock, from the bindings) until `target`
+  // pods have been bound in total / the cache holds no pod; false on timeout.
+  bool wait_bound(uint64_t target, int64_t timeout_us) const;
+  bool wait_cache_empty(int64_t timeout_us) const;
   std::vector<GangRecord> gang_records(bool clear = false);
   size_t inflight_bindings() const { return inflight_.load(); }
 
@@ -278,6 +282,7 @@ class Scheduler {
 
   mutable std::mutex stats_mu_;
   Stats stats_;
+  std::atomic<uint64_t> bound_total_{0};  // stats_.bound, readable without stats_mu_
   std::unordered_map<std::string, GangRecord> gangs_;  // open groups
   std::vector<GangRecord> gang_done_;
   std::unordered_map<std::string, std::string> last_condition_;  // uid -> last failure message

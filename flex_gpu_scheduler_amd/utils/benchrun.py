@@ -63,14 +63,12 @@ class Shard:
         t_created = time.perf_counter()
         deadline = t0 + timeout_s
         sched = self.sched
-        while True:
+        # Waits natively (no Python per poll, no stats lock): wait_bound polls
+        # the scheduler's bound counter every 50 us with the GIL released.
+        if not sched.wait_bound(target, max(0.0, deadline - time.perf_counter())):
             b = sched.stats()["bound"]
-            if b >= target:
-                break
-            if time.perf_counter() > deadline:
-                raise WaveTimeout(f"wave not bound after {timeout_s}s: {b - self._bound}/{n} "
-                                  f"queue={sched.queue_counts()} stats={sched.stats()}")
-            time.sleep(0.0002)
+            raise WaveTimeout(f"wave not bound after {timeout_s}s: {b - self._bound}/{n} "
+                              f"queue={sched.queue_counts()} stats={sched.stats()}")
         self._bound = target
         t_bound = time.perf_counter()
         if check_cache is not None:
@@ -80,10 +78,8 @@ class Shard:
         gangs = sched.gang_records(True)
         self.store.delete_all("pods", self.ns)
         self.store.delete_all("podgroups", self.ns)
-        while sched.cache_counts()["pods"] > 0:
-            if time.perf_counter() > deadline:
-                raise WaveTimeout("wave deletion not observed by the scheduler cache")
-            time.sleep(0.0002)
+        if not sched.wait_cache_empty(max(0.0, deadline - time.perf_counter())):
+            raise WaveTimeout("wave deletion not observed by the scheduler cache")
         t_end = time.perf_counter()
         return StepResult(n, t_end - t0, gangs, {"create": (t_created - t0) * 1e3, "to_bound": (t_bound - t_created) * 1e3,
                                                  "delete_drain": (t_end - t_bound) * 1e3})
