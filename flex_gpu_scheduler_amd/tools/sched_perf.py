@@ -34,12 +34,7 @@ def _nodes_plain(n: int) -> list[dict]:
 
 
 def _wait_bound(sched, target: int, timeout: float) -> bool:
-    end = time.perf_counter() + timeout
-    while sched.stats()["bound"] < target:
-        if time.perf_counter() > end:
-            return False
-        time.sleep(0.0005)
-    return True
+    return sched.wait_bound(target, timeout)  # native wait, GIL released
 
 
 def _spec(name: str, nodes: list[dict], init_pods: list[dict], pods: list[dict], *, config=None, options=None,
