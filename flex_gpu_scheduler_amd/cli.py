@@ -113,7 +113,8 @@ def cmd_apiserver(args) -> int:
         n = restore(store, json.loads(Path(args.load).read_text()))
         log.info("restored %d objects from %s", n, args.load)
     host, port = _hostport(args.bind_address, args.port)
-    srv = ApiServer(store, host, port, token=args.token).start()
+    srv = ApiServer(store, host, port, token=args.token, tls_cert=args.tls_cert_file,
+                    tls_key=args.tls_private_key_file, client_ca=args.client_ca_file).start()
     print(json.dumps({"apiserver": srv.url}), flush=True)
     stop = threading.Event()
     if args.save and args.save_period > 0:
@@ -404,6 +405,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bind-address", default="127.0.0.1")
     p.add_argument("--port", type=int, default=6443)
     p.add_argument("--token")
+    p.add_argument("--tls-cert-file", help="serve HTTPS with this certificate (PEM)")
+    p.add_argument("--tls-private-key-file", help="key of --tls-cert-file (PEM)")
+    p.add_argument("--client-ca-file", help="require client certificates signed by this CA (mutual TLS)")
     p.add_argument("--load", help="restore objects from a JSON snapshot at start")
     p.add_argument("--save", help="write a JSON snapshot on exit (and every --save-period s)")
     p.add_argument("--save-period", type=float, default=0.0)

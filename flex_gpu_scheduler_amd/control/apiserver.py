@@ -126,7 +126,8 @@ class ApiServer:
     """Owns a native Store and serves it over HTTP on a background thread."""
 
     def __init__(self, store=None, host: str = "127.0.0.1", port: int = 0, *, token: str | None = None,
-                 bookmark_interval: float = 10.0):
+                 bookmark_interval: float = 10.0, tls_cert: str | None = None, tls_key: str | None = None,
+                 client_ca: str | None = None):
         self.store = store if store is not None else native().Store()
         self.token = token
         self.bookmark_interval = bookmark_interval
@@ -137,6 +138,20 @@ class ApiServer:
         handler = type("Handler", (_Handler,), {"api": self})
         self.httpd = _Server((host, port), handler)
         self.httpd.daemon_threads = True
+        self.tls = bool(tls_cert)
+        if tls_cert:
+            # kube-apiserver's --tls-cert-file/--tls-private-key-file, and
+            # --client-ca-file for client-certificate (mutual TLS) auth.
+            import ssl
+
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(tls_cert, tls_key or tls_cert)
+            if client_ca:
+                ctx.verify_mode = ssl.CERT_REQUIRED
+                ctx.load_verify_locations(client_ca)
+            # Handshakes run in each connection's handler thread, not in the
+            # accept loop (a slow client must not stall every other one).
+            self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True, do_handshake_on_connect=False)
         self._thread: threading.Thread | None = None
         _lifecycle.register(self)
 
@@ -147,7 +162,7 @@ class ApiServer:
     @property
     def url(self) -> str:
         h, p = self.address
-        return f"http://{h}:{p}"
+        return f"{'https' if self.tls else 'http'}://{h}:{p}"
 
     def start(self) -> "ApiServer":
         self._thread = threading.Thread(target=self.httpd.serve_forever, kwargs={"poll_interval": 0.05},

@@ -3,7 +3,6 @@ mirror RemoteScheduler uses against a REST endpoint. Bindings carry the
 FlexGPU annotations, a relist drops objects deleted while not watching, and
 TLS (server-verified and mutual) works end to end."""
 import shutil
-import ssl
 import time
 
 import pytest
@@ -81,16 +80,11 @@ def test_native_mirror_relist_drops_objects_deleted_meanwhile(store):
 @pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
 @pytest.mark.parametrize("mutual", [False, True], ids=["server-tls", "mtls"])
 def test_native_io_over_tls(store, pki, mutual):
-    srv = ApiServer(store)
-    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
-    ctx.load_cert_chain(pki / "server.crt", pki / "server.key")
-    if mutual:
-        ctx.verify_mode = ssl.CERT_REQUIRED
-        ctx.load_verify_locations(pki / "ca.crt")
-    srv.httpd.socket = ctx.wrap_socket(srv.httpd.socket, server_side=True)
-    srv.start()
+    srv = ApiServer(store, tls_cert=str(pki / "server.crt"), tls_key=str(pki / "server.key"),
+                    client_ca=str(pki / "ca.crt") if mutual else None).start()
     try:
-        url = srv.url.replace("http://", "https://")
+        url = srv.url
+        assert url.startswith("https://")
         tls = TLSConfig(ca_file=str(pki / "ca.crt"),
                         cert_file=str(pki / "client.crt") if mutual else None,
                         key_file=str(pki / "client.key") if mutual else None)
@@ -109,13 +103,9 @@ def test_native_io_over_tls(store, pki, mutual):
 
 @pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
 def test_native_io_refuses_unknown_ca(store, pki):
-    srv = ApiServer(store)
-    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
-    ctx.load_cert_chain(pki / "server.crt", pki / "server.key")
-    srv.httpd.socket = ctx.wrap_socket(srv.httpd.socket, server_side=True)
-    srv.start()
+    srv = ApiServer(store, tls_cert=str(pki / "server.crt"), tls_key=str(pki / "server.key")).start()
     try:
-        url = srv.url.replace("http://", "https://")
+        url = srv.url
         ep = rest_endpoint(RestClient(url, tls=TLSConfig(ca_file=str(pki / "other.crt"))))
         m = native().RemoteMirror(ep, native().Store(), ["pods"])
         m.start()
