@@ -450,7 +450,8 @@ PYBIND11_MODULE(_xsched, m) {
   // Native service mode (rest/kube.h): REST writes and the LIST/WATCH mirror.
   auto endpoint = [](const std::string& host, int port, const std::string& token, bool tls, const std::string& ca_file,
                      const std::string& ca_pem, const std::string& cert_file, const std::string& key_file,
-                     const std::string& cert_pem, const std::string& key_pem, bool insecure, int timeout_ms) {
+                     const std::string& cert_pem, const std::string& key_pem, bool insecure, int timeout_ms,
+                     double qps, int burst) {
     rest::Endpoint ep;
     ep.host = host;
     ep.port = port;
@@ -464,13 +465,15 @@ PYBIND11_MODULE(_xsched, m) {
     ep.tls.cert_pem = cert_pem;
     ep.tls.key_pem = key_pem;
     ep.tls.insecure = insecure;
+    ep.qps = qps;
+    ep.burst = burst;
     return ep;
   };
   py::class_<rest::Endpoint>(m, "RestEndpoint")
       .def(py::init(endpoint), py::arg("host"), py::arg("port"), py::arg("token") = "", py::arg("tls") = false,
            py::arg("ca_file") = "", py::arg("ca_pem") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
            py::arg("cert_pem") = "", py::arg("key_pem") = "", py::arg("insecure") = false,
-           py::arg("timeout_ms") = 30000);
+           py::arg("timeout_ms") = 30000, py::arg("qps") = 0.0, py::arg("burst") = 0);
   py::class_<rest::RestApiClient, ApiClient, std::shared_ptr<rest::RestApiClient>>(m, "RestApiClient")
       .def(py::init<rest::Endpoint>())
       .def("requests", &rest::RestApiClient::requests);

@@ -31,6 +31,10 @@ struct Endpoint {
   std::string token;  // bearer token ("" = none)
   TlsOptions tls;
   int timeout_ms = 30'000;  // connect and per-request I/O (not watch streams)
+  // client-go's token bucket (KubeSchedulerConfiguration clientConnection):
+  // at most `qps` requests per second with bursts of `burst`; 0 = unlimited.
+  double qps = 0;
+  int burst = 0;
 };
 
 struct Response {

@@ -1,5 +1,6 @@
 #include "rest/kube.h"
 
+#include <algorithm>
 #include <chrono>
 #include <ctime>
 #include <stdexcept>
@@ -73,10 +74,35 @@ std::string object_path(const std::string& kind, const std::string& ns, const st
 }
 
 // ------------------------------------------------------------ ConnPool ----
-ConnPool::ConnPool(Endpoint ep) : ep_(std::move(ep)), tls_(make_tls_context(ep_.tls)) {}
+ConnPool::ConnPool(Endpoint ep) : ep_(std::move(ep)), tls_(make_tls_context(ep_.tls)) {
+  tokens_ = std::max(1, ep_.burst);
+}
+
+void ConnPool::throttle() {
+  if (ep_.qps <= 0) return;
+  const double burst = std::max(1, ep_.burst);
+  for (;;) {
+    int64_t wait_ns;
+    {
+      std::lock_guard<std::mutex> g(rate_mu_);
+      int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count();
+      if (last_refill_ns_ == 0) last_refill_ns_ = now;
+      tokens_ = std::min(burst, tokens_ + static_cast<double>(now - last_refill_ns_) * 1e-9 * ep_.qps);
+      last_refill_ns_ = now;
+      if (tokens_ >= 1) {
+        tokens_ -= 1;
+        return;
+      }
+      wait_ns = static_cast<int64_t>((1 - tokens_) / ep_.qps * 1e9);
+    }
+    std::this_thread::sleep_for(std::chrono::nanoseconds(wait_ns));
+  }
+}
 
 Response ConnPool::call(const std::string& method, const std::string& path, const std::string& body,
                         const std::string& content_type) {
+  throttle();
   for (int attempt = 0;; ++attempt) {
     std::unique_ptr<HttpConn> c;
     bool pooled = false;

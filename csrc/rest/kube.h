@@ -47,10 +47,15 @@ class ConnPool {
   std::shared_ptr<TlsContext> tls() const { return tls_; }
 
  private:
+  void throttle();  // token bucket (Endpoint::qps / burst)
+
   Endpoint ep_;
   std::shared_ptr<TlsContext> tls_;
   std::mutex mu_;
   std::vector<std::unique_ptr<HttpConn>> idle_;
+  std::mutex rate_mu_;
+  double tokens_ = 0;
+  int64_t last_refill_ns_ = 0;
 };
 
 class RestApiClient : public ApiClient {

@@ -272,6 +272,8 @@ class SchedulerConfiguration:
     pod_initial_backoff_seconds: float = 1.0
     pod_max_backoff_seconds: float = 10.0
     leader_elect: bool = False
+    client_qps: float = 0.0   # clientConnection.qps (0 = unthrottled)
+    client_burst: int = 0     # clientConnection.burst
     bind_workers: int = 16
     status_updates: bool = True
     trace: bool = False
@@ -458,6 +460,13 @@ def load_config(src: str | Path | dict | None = None, *, restrict_to_native: boo
     if doc.get("podMaxBackoffSeconds") is not None:
         cfg.pod_max_backoff_seconds = float(doc["podMaxBackoffSeconds"])
     cfg.leader_elect = bool((doc.get("leaderElection") or {}).get("leaderElect", False))
+    cc = doc.get("clientConnection") or {}
+    # Upstream defaults qps 50 / burst 100 (a 1.23 kube-scheduler then binds at
+    # most 50 pods/s); here the writer is unthrottled unless configured.
+    cfg.client_qps = float(cc.get("qps") or 0)
+    cfg.client_burst = int(cc.get("burst") or 0)
+    if cfg.client_qps < 0 or cfg.client_burst < 0:
+        raise ConfigError("clientConnection.qps and .burst must be >= 0")
     return cfg
 
 

@@ -102,7 +102,7 @@ def remote_api_client(remote: Client):
     return RemoteApiClient()
 
 
-def rest_endpoint(remote: Client):
+def rest_endpoint(remote: Client, qps: float = 0.0, burst: int = 0):
     """The native REST endpoint (host, port, bearer token, TLS settings) of a
     RestClient, or None for clients that are not plain REST endpoints."""
     from .client import RestClient
@@ -114,7 +114,7 @@ def rest_endpoint(remote: Client):
         remote.host, remote.port, remote.token or "", remote.https, ca_file=t.ca_file or "",
         ca_pem=t.ca_data.decode() if t.ca_data else "", cert_file=t.cert_file or "", key_file=t.key_file or "",
         cert_pem=t.cert_data.decode() if t.cert_data else "", key_pem=t.key_data.decode() if t.key_data else "",
-        insecure=t.insecure, timeout_ms=int(remote.timeout * 1000))
+        insecure=t.insecure, timeout_ms=int(remote.timeout * 1000), qps=float(qps), burst=int(burst))
 
 
 class NativeMirror:
@@ -158,16 +158,21 @@ class RemoteScheduler:
     def __init__(self, remote: Client, config=None, *, native_io: bool = True, **options):
         from ..scheduler import new_scheduler
 
+        from ..config import SchedulerConfiguration, load_config
+
+        cfg = config if isinstance(config, SchedulerConfiguration) else load_config(config)
         self.store = native().Store()
         ep = rest_endpoint(remote) if native_io else None
         if ep is not None:
             self.mirror = NativeMirror(ep, self.store)
-            self.client = native().RestApiClient(ep)
+            # Writes are throttled per clientConnection; LIST/WATCH are not
+            # (a watch is one request).
+            self.client = native().RestApiClient(rest_endpoint(remote, cfg.client_qps, cfg.client_burst))
         else:
             self.mirror = StoreMirror(remote, self.store)
             self.client = remote_api_client(remote)
         self.native_io = ep is not None
-        self.scheduler = new_scheduler(self.store, config, client=self.client, **options)
+        self.scheduler = new_scheduler(self.store, cfg, client=self.client, **options)
 
     def start(self, sync_timeout: float = 30.0) -> "RemoteScheduler":
         self.mirror.start()

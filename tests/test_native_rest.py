@@ -151,3 +151,28 @@ def test_native_mirror_treats_unserved_kind_as_empty():
     finally:
         httpd.shutdown()
         httpd.server_close()
+
+
+def test_native_writer_honours_client_connection_qps(store):
+    """clientConnection.qps/burst (client-go's token bucket) throttle the
+    native writer: 25 bindings at qps 20 with a burst of 5 take >= 1 s."""
+    from flex_gpu_scheduler_amd.control import ApiServer as _Api
+
+    srv = _Api(store).start()
+    try:
+        client = RestClient(srv.url)
+        client.create("nodes", mi355x_node("n0"))
+        cfg = load_config({"apiVersion": "kubescheduler.config.k8s.io/v1beta3", "kind": "KubeSchedulerConfiguration",
+                           "clientConnection": {"qps": 20, "burst": 5}})
+        assert cfg.client_qps == 20 and cfg.client_burst == 5
+        rs = RemoteScheduler(RestClient(srv.url), cfg).start()
+        try:
+            t0 = time.time()
+            for i in range(25):
+                client.create("pods", make_pod(f"p{i}", requests={"cpu": "100m"}))
+            assert wait_for(lambda: all(p["spec"].get("nodeName") for p in client.list("pods", "default")[0]), 20)
+            assert time.time() - t0 >= 0.95
+        finally:
+            rs.stop()
+    finally:
+        srv.stop()
