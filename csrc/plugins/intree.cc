@@ -120,6 +120,8 @@ class NodeResourcesFit : public Plugin {
     return false;
   }
 
+  static constexpr uint64_t kBeyondAllocatable = 1ull << 63;  // above every resource id
+  static_assert(kMaxRes < 63);
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     // Failures are encoded as a resource bitmask (bit kPods = "Too many
     // pods") and their Status is built once per distinct mask per thread.
@@ -133,7 +135,13 @@ class NodeResourcesFit : public Plugin {
       if (want == 0) continue;
       if (i > kPods && ignored(i)) continue;
       int64_t free = ni.allocatable.get(i) - ni.requested.get(i);
-      if (want > free) fail |= 1ull << i;
+      if (want > free) {
+        fail |= 1ull << i;
+        // More than the node has at all: evicting pods cannot help, so the
+        // verdict is unresolvable and preemption skips the node (newer
+        // upstream NodeResourcesFit does the same).
+        if (want > ni.allocatable.get(i)) fail |= kBeyondAllocatable;
+      }
     }
     if (!fail) return {};
     thread_local std::unordered_map<uint64_t, Status> memo;
@@ -141,9 +149,10 @@ class NodeResourcesFit : public Plugin {
     if (it != memo.end()) return it->second;
     std::vector<std::string> reasons;
     if (fail & (1ull << kPods)) reasons.push_back("Too many pods");
-    for (uint64_t m = fail & ~(1ull << kPods); m; m &= m - 1)
+    for (uint64_t m = fail & ~((1ull << kPods) | kBeyondAllocatable); m; m &= m - 1)
       reasons.push_back("Insufficient " + ResourceRegistry::get().name(__builtin_ctzll(m)));
-    return memo.emplace(fail, Status(Code::Unschedulable, std::move(reasons))).first->second;
+    Code code = (fail & kBeyondAllocatable) ? Code::UnschedulableAndUnresolvable : Code::Unschedulable;
+    return memo.emplace(fail, Status(code, std::move(reasons))).first->second;
   }
 
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {

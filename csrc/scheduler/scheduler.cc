@@ -1197,6 +1197,7 @@ Json Scheduler::explain(const Json& pod_obj) {
     Json e = Json::object();
     e.set("plugin", Json(s.failed_plugin()));
     e.set("reason", Json(s.message()));
+    e.set("code", Json(code_name(s.code())));
     filt.set(node, std::move(e));
   }
   out.set("filtered", std::move(filt));

@@ -118,3 +118,23 @@ def test_preemption_toleration_seconds_window(store):
         wait_for(lambda: store.get("pods", "default", "victim") is None)
     finally:
         s.stop()
+
+
+def test_request_beyond_allocatable_is_unresolvable(store):
+    """A request larger than a node's allocatable cannot be met by evicting
+    pods: NodeResourcesFit says UnschedulableAndUnresolvable there, so
+    preemption does not dry-run that node; a node that is merely full stays
+    Unschedulable (a preemption candidate)."""
+    from flex_gpu_scheduler_amd import load_config, new_scheduler
+    from flex_gpu_scheduler_amd.models import make_node, make_pod
+
+    store.create("nodes", make_node("small", {"cpu": "4", "memory": "8Gi", "pods": "10"}))
+    store.create("nodes", make_node("big", {"cpu": "16", "memory": "8Gi", "pods": "10"}))
+    store.create("pods", make_pod("filler", requests={"cpu": "12"}, node_name="big"))
+    s = new_scheduler(store, load_config(None))
+    s.sync_informers(50)
+    out = s.explain(make_pod("p", requests={"cpu": "8"}))
+    assert out["filtered"]["small"]["code"] == "UnschedulableAndUnresolvable"
+    assert out["filtered"]["big"]["code"] == "Unschedulable"
+    assert "Insufficient cpu" in out["filtered"]["small"]["reason"]
+    s.stop()
