@@ -5,10 +5,12 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 
 namespace xsched {
 
 Parallelizer::Parallelizer(int workers, int inline_below) : workers_(std::max(1, workers)), inline_below_(inline_below) {
+  if (const char* e = std::getenv("XSCHED_MIN_PARALLEL_NS")) min_parallel_work_ns_ = std::max<int64_t>(0, std::atoll(e));
   for (int i = 0; i < workers_ - 1; ++i) threads_.emplace_back([this] {
     name_this_thread("xs-filter");
     worker_loop();
@@ -102,7 +104,7 @@ bool Parallelizer::plan_inline(int n, ParallelSite* site) {
     int64_t est = site->ns_per_item_x16.load(std::memory_order_relaxed) * n / 16 *
                   site->done_frac_x1024.load(std::memory_order_relaxed) / 1024;
     bool probe = site->calls.fetch_add(1, std::memory_order_relaxed) % ParallelSite::kProbeEvery == 0;
-    cheap = probe || est < kMinParallelWorkNs;
+    cheap = probe || est < min_parallel_work_ns_;
   }
   return n < inline_below_ || helpers <= 0 || cheap;
 }

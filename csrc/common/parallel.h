@@ -21,7 +21,7 @@ namespace xsched {
 // Cost model of one call site (Filter, Score): an exponential moving average
 // of the per-item time measured on the calling thread. Above `inline_below`
 // items the site still runs inline while the estimated serial time is under
-// Parallelizer::kMinParallelWorkNs: a fork/join round (waking helpers and
+// Parallelizer::min_parallel_work_ns(): a fork/join round (waking helpers and
 // joining them) costs ~15-25 us on the MI355X hosts, more than filtering a
 // thousand nodes whose verdicts come from the equivalence cache
 // (profiles/r1h_inline_ab.txt).
@@ -58,7 +58,10 @@ class Parallelizer {
   static void record_inline(ParallelSite* site, int64_t elapsed_ns, int done, int n);
   static int64_t now_ns();
   int workers() const { return workers_; }
+  // Serial-time estimate above which a site forks (XSCHED_MIN_PARALLEL_NS
+  // overrides the default, for A/B runs).
   static constexpr int64_t kMinParallelWorkNs = 60'000;
+  int64_t min_parallel_work_ns() const { return min_parallel_work_ns_; }
 
  private:
   struct Job {
@@ -75,6 +78,7 @@ class Parallelizer {
 
   int workers_;
   int inline_below_;
+  int64_t min_parallel_work_ns_ = kMinParallelWorkNs;
   std::vector<std::thread> threads_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
