@@ -52,8 +52,15 @@ def test_gang_scenarios(store, name, pods, groups, expected):
         create_all(store, "podgroups", [make_pod_group(g, "default", m) for g, m in groups])
         create_all(store, "pods", pods)
         wait_bound(sched, len(expected))
-        time.sleep(0.3)
-        got = sorted(n for n, node_ in placements(store).items() if node_)
+        # The bound counter can reach len(expected) on a group that is later
+        # preempted (the higher-priority scenario), so poll the placements
+        # themselves as the reference does (coscheduling_test.go:365).
+        t0 = time.time()
+        while True:
+            time.sleep(0.3)
+            got = sorted(n for n, node_ in placements(store).items() if node_)
+            if got == sorted(expected) or time.time() - t0 > 20:
+                break
         assert got == sorted(expected)
     finally:
         sched.stop()
