@@ -173,7 +173,7 @@ Status Framework::run_pre_filter_add_pod(CycleState& s, const Pod& to_schedule, 
   auto it = chain_.find(kPreFilter);
   if (it == chain_.end()) return {};
   for (const auto& pl : it->second) {
-    if (!pl->has_pre_filter_extensions()) continue;
+    if (!pl->has_pre_filter_extensions() || !pl->pre_filter_extension_affects(s, to_schedule, *to_add)) continue;
     Status st = pl->add_pod(s, to_schedule, to_add, ni);
     if (!st.is_success()) return Status(Code::Error, "running AddPod on PreFilter plugin " + pl->name() + ": " + st.message());
   }
@@ -185,12 +185,20 @@ Status Framework::run_pre_filter_remove_pod(CycleState& s, const Pod& to_schedul
   auto it = chain_.find(kPreFilter);
   if (it == chain_.end()) return {};
   for (const auto& pl : it->second) {
-    if (!pl->has_pre_filter_extensions()) continue;
+    if (!pl->has_pre_filter_extensions() || !pl->pre_filter_extension_affects(s, to_schedule, *to_remove)) continue;
     Status st = pl->remove_pod(s, to_schedule, to_remove, ni);
     if (!st.is_success())
       return Status(Code::Error, "running RemovePod on PreFilter plugin " + pl->name() + ": " + st.message());
   }
   return {};
+}
+
+bool Framework::pre_filter_extensions_affected(const CycleState& s, const Pod& to_schedule, const Pod& other) const {
+  auto it = chain_.find(kPreFilter);
+  if (it == chain_.end()) return false;
+  for (const auto& pl : it->second)
+    if (pl->has_pre_filter_extensions() && pl->pre_filter_extension_affects(s, to_schedule, other)) return true;
+  return false;
 }
 
 Status Framework::run_filter(CycleState& s, const Pod& p, const NodeInfo& ni) {
@@ -236,17 +244,20 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
       }
       for (const auto& np : *nominated) {
         if (np->priority < p.priority || np->uid() == p.uid()) continue;
-        if (!ni_out) {
-          ni_out = ni.clone();
-          state_out = s.clone();
-        }
+        if (!ni_out) ni_out = ni.clone();
         ni_out->add_pod(np);
+        pods_added = true;
+        // addNominatedPods clones the CycleState for the PreFilter AddPod
+        // extensions; a nominated pod none of them reacts to leaves the state
+        // as it is, so the clone waits for the first one that does (the
+        // skipped pods changed nothing it would have carried).
+        if (!pre_filter_extensions_affected(s, p, *np)) continue;
+        if (!state_out) state_out = s.clone();
         Status ast = run_pre_filter_add_pod(*state_out, p, np, *ni_out);
         if (!ast.is_success()) return ast;
-        pods_added = true;
       }
       if (pods_added) {
-        state_to_use = state_out.get();
+        if (state_out) state_to_use = state_out.get();
         ni_to_use = ni_out.get();
       }
     } else if (!pods_added || !st.is_success()) {

@@ -102,6 +102,14 @@ class Plugin {
   virtual Status remove_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_remove, const NodeInfo& ni) {
     return {};
   }
+  // False when AddPod/RemovePod of `other` leaves this plugin's PreFilter
+  // state for `to_schedule` unchanged. The framework then skips the call, and
+  // when no plugin is affected it evaluates nominated pods and preemption
+  // dry runs against the cycle's own state instead of a deep clone of it.
+  // Must only read `s`.
+  virtual bool pre_filter_extension_affects(const CycleState& s, const Pod& to_schedule, const Pod& other) const {
+    return true;
+  }
   // Filter
   virtual Status filter(CycleState& s, const Pod& p, const NodeInfo& ni) { return {}; }
   // PostFilter

@@ -200,6 +200,11 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
   }
 
   bool has_pre_filter_extensions() const override { return true; }
+  // AddPod/RemovePod touch only the quota of the other pod's namespace.
+  bool pre_filter_extension_affects(const CycleState& s, const Pod&, const Pod& other) const override {
+    auto* snap = s.read_as<EQSnapshot>(kSnapKey);
+    return snap && snap->infos.count(other.ns());
+  }
   Status add_pod(CycleState& s, const Pod&, const PodPtr& to_add, const NodeInfo&) override {
     if (auto* snap = s.read_as<EQSnapshot>(kSnapKey)) {
       auto it = snap->infos.find(to_add->ns());

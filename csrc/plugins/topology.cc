@@ -330,6 +330,11 @@ class PodTopologySpread : public Plugin {
     }
     st->index();
   }
+  // update_with_pod changes nothing without hard constraints or across namespaces.
+  bool pre_filter_extension_affects(const CycleState& s, const Pod& p, const Pod& q) const override {
+    auto* st = s.read_as<SpreadFilterState>(kFilterKey);
+    return st && !st->constraints.empty() && q.ns() == p.ns();
+  }
   Status add_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
     update_with_pod(s, p, *q, ni, 1);
     return {};
@@ -696,6 +701,12 @@ class InterPodAffinity : public Plugin {
     return {};
   }
   bool has_pre_filter_extensions() const override { return true; }
+  // update() bumps counts only through q's required anti-affinity terms or
+  // p's own required (anti-)affinity terms.
+  bool pre_filter_extension_affects(const CycleState&, const Pod& p, const Pod& q) const override {
+    return !q.pod_anti_affinity_required.empty() || !p.pod_affinity_required.empty() ||
+           !p.pod_anti_affinity_required.empty();
+  }
   Status add_pod(CycleState& s, const Pod& p, const PodPtr& q, const NodeInfo& ni) override {
     if (auto* st = s.read_as<AffinityFilterState>(kFilterKey)) {
       update(*st, p, *q, *ni.node, 1);

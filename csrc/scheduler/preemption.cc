@@ -125,7 +125,18 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
   h_.parallelizer->until(n, [&](int i) {
     const NodeInfoPtr& src = potential[(offset + i) % n];
     auto ni = src->clone();
-    auto st = s.clone();
+    // Victims leave and re-enter the node through the PreFilter extensions.
+    // When none of them reacts to any pod here, those calls are skipped and
+    // the candidate reads the cycle's state as every Filter worker does,
+    // instead of deep-cloning it per node.
+    std::shared_ptr<CycleState> cloned;
+    CycleState* st = &s;
+    for (const auto& q : ni->pods)
+      if (h_.framework->pre_filter_extensions_affected(s, pod, *q)) {
+        cloned = s.clone();
+        st = cloned.get();
+        break;
+      }
     Candidate c;
     c.node = ni->name();
     Status vs = policy_->select_victims_on_node(*st, pod, *ni, pdbs, c.victims, c.num_pdb_violations);

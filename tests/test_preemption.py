@@ -138,3 +138,53 @@ def test_request_beyond_allocatable_is_unresolvable(store):
     assert out["filtered"]["big"]["code"] == "Unschedulable"
     assert "Insufficient cpu" in out["filtered"]["small"]["reason"]
     s.stop()
+
+
+def _nominated(name, node, **kw):
+    """A pending pod nominated to `node` that cannot itself be placed (its
+    node selector matches nothing), so the nomination stays outstanding."""
+    p = make_pod(name, node_selector={"never": "matches"}, **kw)
+    p["status"] = {"phase": "Pending", "nominatedNodeName": node}
+    return p
+
+
+ANTI_WEB = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+    {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "topology.kubernetes.io/zone"}]}}
+
+
+def test_nominated_pod_resources_count_for_equal_or_lower_priority(store):
+    """addNominatedPods (vendor/.../runtime/framework.go): a nominated pod of
+    priority >= the incoming pod's is counted on its node. It has no
+    PreFilter-extension effect here, so the cycle's state is used as is."""
+    store.create("nodes", make_node("n", {"cpu": "4", "memory": "100", "pods": "10"},
+                                    labels={"kubernetes.io/hostname": "n"}))
+    store.create("pods", _nominated("nom", "n", requests={"memory": "60"}, priority=100))
+    s = new_scheduler(store, load_config(DEFAULT), start=True)
+    try:
+        store.create("pods", make_pod("same", requests={"memory": "50"}, priority=100))
+        store.create("pods", make_pod("higher", requests={"memory": "50"}, priority=200))
+        wait_bound(s, 1)
+        time.sleep(0.3)
+        assert placements(store) == {"nom": "", "same": "", "higher": "n"}
+    finally:
+        s.stop()
+
+
+def test_nominated_pod_anti_affinity_applies_through_prefilter_extension(store):
+    """A nominated pod with required anti-affinity changes InterPodAffinity's
+    PreFilter state (AddPod), so that state is cloned and the incoming pod
+    it repels stays off the node although its resources would fit. The
+    zone key keeps Filter on the counted state (a hostname key is decided on
+    the node's own pods)."""
+    store.create("nodes", make_node("n", {"cpu": "4", "memory": "100", "pods": "10"},
+                                    labels={"kubernetes.io/hostname": "n", "topology.kubernetes.io/zone": "z1"}))
+    store.create("pods", _nominated("nom", "n", requests={"memory": "10"}, priority=100, affinity=ANTI_WEB))
+    s = new_scheduler(store, load_config(DEFAULT), start=True)
+    try:
+        store.create("pods", make_pod("web", requests={"memory": "10"}, priority=100, labels={"app": "web"}))
+        store.create("pods", make_pod("db", requests={"memory": "10"}, priority=100, labels={"app": "db"}))
+        wait_bound(s, 1)
+        time.sleep(0.3)
+        assert placements(store) == {"nom": "", "web": "", "db": "n"}
+    finally:
+        s.stop()
