@@ -5,6 +5,8 @@
 #include <climits>
 #include <map>
 #include <mutex>
+#include <string_view>
+#include <unordered_set>
 
 #include "framework/framework.h"
 #include "framework/waiting_pods.h"
@@ -114,6 +116,18 @@ int calculate_num_candidates(int num_nodes, int pct, int min_abs) {
   if (n < min_abs) n = min_abs;
   if (n > num_nodes) n = num_nodes;
   return n;
+}
+
+std::vector<NodeInfoPtr> nodes_where_preemption_might_help(const Snapshot& snap, const NodeStatusMap& m) {
+  std::unordered_set<std::string_view> unresolvable;
+  for (const auto& [name, st] : m)
+    if (st.code() == Code::UnschedulableAndUnresolvable) unresolvable.insert(name);
+  if (unresolvable.empty()) return snap.nodes;
+  std::vector<NodeInfoPtr> out;
+  out.reserve(snap.nodes.size());
+  for (const auto& ni : snap.nodes)
+    if (!unresolvable.count(ni->name())) out.push_back(ni);
+  return out;
 }
 
 std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
@@ -243,12 +257,7 @@ std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod&
     return {PostFilterResult{}, Status::unschedulable("Pod is not eligible for preemption")};
   // 2) candidates: nodes where preemption might help
   if (!h_.snapshot || h_.snapshot->nodes.empty()) return {PostFilterResult{}, Status::error("no nodes available")};
-  std::vector<NodeInfoPtr> potential;
-  for (const auto& ni : h_.snapshot->nodes) {
-    auto it = m.find(ni->name());
-    if (it != m.end() && it->second.code() == Code::UnschedulableAndUnresolvable) continue;
-    potential.push_back(ni);
-  }
+  std::vector<NodeInfoPtr> potential = nodes_where_preemption_might_help(*h_.snapshot, m);
   if (potential.empty())
     return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +
                                                       " nodes are available: preemption is not helpful for scheduling.")};

@@ -73,5 +73,10 @@ Status select_victims_default(Handle& h, CycleState& s, const Pod& preemptor, No
                               std::vector<PodPtr>& victims, int& num_violating);
 bool default_eligible(Handle& h, const Pod& pod, const Status* nominated_status);
 int calculate_num_candidates(int num_nodes, int pct, int min_abs);
+// Snapshot nodes preemption might help on: all but those whose Filter status
+// is UnschedulableAndUnresolvable (nodesWherePreemptionMightHelp). One pass
+// over the diagnosis instead of a name lookup per node; usually no node is
+// unresolvable and the snapshot's list is returned whole.
+std::vector<NodeInfoPtr> nodes_where_preemption_might_help(const Snapshot& snap, const NodeStatusMap& m);
 
 }  // namespace xsched
