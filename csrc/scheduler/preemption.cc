@@ -5,8 +5,6 @@
 #include <climits>
 #include <map>
 #include <mutex>
-#include <string_view>
-#include <unordered_set>
 
 #include "framework/framework.h"
 #include "framework/waiting_pods.h"
@@ -119,14 +117,19 @@ int calculate_num_candidates(int num_nodes, int pct, int min_abs) {
 }
 
 std::vector<NodeInfoPtr> nodes_where_preemption_might_help(const Snapshot& snap, const NodeStatusMap& m) {
-  std::unordered_set<std::string_view> unresolvable;
-  for (const auto& [name, st] : m)
-    if (st.code() == Code::UnschedulableAndUnresolvable) unresolvable.insert(name);
-  if (unresolvable.empty()) return snap.nodes;
+  size_t unresolvable = 0;
+  for (const auto& kv : m)
+    if (kv.second.code() == Code::UnschedulableAndUnresolvable) ++unresolvable;
+  if (unresolvable == 0) return snap.nodes;
+  // Every node of the snapshot failed unresolvably (m holds one entry per
+  // failed node): nothing to try.
+  if (unresolvable == m.size() && m.size() >= snap.nodes.size()) return {};
   std::vector<NodeInfoPtr> out;
   out.reserve(snap.nodes.size());
-  for (const auto& ni : snap.nodes)
-    if (!unresolvable.count(ni->name())) out.push_back(ni);
+  for (const auto& ni : snap.nodes) {
+    auto it = m.find(ni->name());
+    if (it == m.end() || it->second.code() != Code::UnschedulableAndUnresolvable) out.push_back(ni);
+  }
   return out;
 }
 
