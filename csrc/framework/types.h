@@ -6,6 +6,7 @@
 // QueuedPodInfo, ClusterEvent)} as used by the reference's plugins.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <deque>
@@ -359,7 +360,76 @@ struct NodeScore {
 inline constexpr int64_t kMaxNodeScore = 100;
 inline constexpr int64_t kMinNodeScore = 0;
 
-using NodeStatusMap = std::unordered_map<std::string, Status>;
+// Node name -> Filter status of one failed cycle (framework.NodeToStatusMap).
+// A cycle that finds no node fills it with every node of the cluster before
+// PostFilter, so it is a flat map: entries in one vector (insertion order)
+// and an open-addressing index of positions, i.e. no allocation per node.
+// The subset of the std::unordered_map interface the scheduler and the
+// plugins use: find / count / emplace / operator[] / iteration / reserve.
+class NodeStatusMap {
+ public:
+  using value_type = std::pair<std::string, Status>;
+  using const_iterator = std::vector<value_type>::const_iterator;
+  using iterator = std::vector<value_type>::iterator;
+
+  size_t size() const { return entries_.size(); }
+  bool empty() const { return entries_.empty(); }
+  const_iterator begin() const { return entries_.begin(); }
+  const_iterator end() const { return entries_.end(); }
+  iterator begin() { return entries_.begin(); }
+  iterator end() { return entries_.end(); }
+  void clear() {
+    entries_.clear();
+    slots_.clear();
+  }
+  void reserve(size_t n) {
+    entries_.reserve(n);
+    if (n * 2 > slots_.size()) rehash(n * 2);
+  }
+  const_iterator find(std::string_view k) const {
+    int32_t i = lookup(k);
+    return i < 0 ? entries_.end() : entries_.begin() + i;
+  }
+  iterator find(std::string_view k) {
+    int32_t i = lookup(k);
+    return i < 0 ? entries_.end() : entries_.begin() + i;
+  }
+  size_t count(std::string_view k) const { return lookup(k) < 0 ? 0 : 1; }
+  std::pair<iterator, bool> emplace(std::string_view k, const Status& v) {
+    if (int32_t i = lookup(k); i >= 0) return {entries_.begin() + i, false};
+    if ((entries_.size() + 1) * 2 > slots_.size()) rehash(std::max<size_t>(16, slots_.size() * 2));
+    entries_.emplace_back(std::string(k), v);
+    place(static_cast<int32_t>(entries_.size() - 1));
+    return {entries_.end() - 1, true};
+  }
+  Status& operator[](std::string_view k) { return emplace(k, Status()).first->second; }
+
+ private:
+  static size_t hash(std::string_view k) { return std::hash<std::string_view>{}(k); }
+  int32_t lookup(std::string_view k) const {
+    if (slots_.empty()) return -1;
+    size_t mask = slots_.size() - 1;
+    for (size_t h = hash(k) & mask;; h = (h + 1) & mask) {
+      int32_t i = slots_[h];
+      if (i < 0) return -1;
+      if (entries_[i].first == k) return i;
+    }
+  }
+  void place(int32_t i) {
+    size_t mask = slots_.size() - 1;
+    size_t h = hash(entries_[i].first) & mask;
+    while (slots_[h] >= 0) h = (h + 1) & mask;
+    slots_[h] = i;
+  }
+  void rehash(size_t want) {
+    size_t cap = 16;
+    while (cap < want) cap <<= 1;
+    slots_.assign(cap, -1);
+    for (int32_t i = 0; i < static_cast<int32_t>(entries_.size()); ++i) place(i);
+  }
+  std::vector<value_type> entries_;
+  std::vector<int32_t> slots_;  // power of two, at most half full; -1 = empty
+};
 
 struct Victims {
   std::vector<PodPtr> pods;

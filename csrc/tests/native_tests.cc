@@ -75,6 +75,35 @@ TEST(quantity_parse_format) {
   CHECK(!Quantity::try_parse("1.2.3", &bad));
 }
 
+// ------------------------------------------------------------- NodeStatusMap
+TEST(node_status_map_matches_unordered_map) {
+  NodeStatusMap m;
+  std::unordered_map<std::string, Code> ref;
+  m.reserve(3);  // grows past the reservation below
+  for (int i = 0; i < 5000; ++i) {
+    std::string n = "node-" + std::to_string(i * 7 % 5003);
+    Code c = i % 3 ? Code::Unschedulable : Code::UnschedulableAndUnresolvable;
+    bool fresh = m.emplace(n, Status(c, "r")).second;
+    CHECK_EQ(fresh, ref.emplace(n, c).second);
+  }
+  CHECK_EQ(m.size(), ref.size());
+  for (const auto& [n, c] : ref) {
+    auto it = m.find(n);
+    CHECK(it != m.end() && it->first == n && it->second.code() == c);
+  }
+  CHECK(m.find("node-missing") == m.end());
+  CHECK_EQ(m.count("node-missing"), 0u);
+  m["node-0"] = Status(Code::Error, "e");  // overwrite through operator[]
+  CHECK(m.find("node-0")->second.code() == Code::Error);
+  m["brand-new"] = Status(Code::Unschedulable, "u");
+  CHECK_EQ(m.size(), ref.size() + 1);
+  size_t seen = 0;
+  for (const auto& [n, st] : m) seen += !n.empty();
+  CHECK_EQ(seen, m.size());
+  m.clear();
+  CHECK(m.empty() && m.find("node-0") == m.end());
+}
+
 // ---------------------------------------------------------------------- JSON
 TEST(json_roundtrip_and_merge_patch) {
   Json j = Json::parse(R"({"a":[1,2,{"b":null}],"c":"x\"y","d":{"e":1.5,"f":true}})");
