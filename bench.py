@@ -9,11 +9,20 @@ so per-GPU work is fixed as N grows (weak scaling) and `value` is the sum of
 pods/s over ranks divided by the slowest rank's time.
 
 GPU use: each rank discovers its MI355X with the HIP probe (device props +
-checksum health test, untimed) and sizes the synthetic nodes' HBM from it;
-after the timed steps, N>1 runs an RCCL all-reduce sweep over the ranks to
-report xGMI bus bandwidth for the placement (untimed).
+checksum health test, untimed) and sizes the synthetic nodes' HBM from it.
+After the timed steps (untimed) the ranks validate placement end to end
+(parallel/placement.py): the live node from discovery, PodGroups of 1/2/4/8
+ranks scheduled, each rank resolved through the device plugin's Allocate, and
+an RCCL all-reduce on exactly the allocated GPUs next to deliberately bad
+placements -> `config.rccl_placement`.
 
     python bench.py --gpus N --steps K --warmup W
+
+Launch: under torch.distributed.run (WORLD_SIZE set) each process is one
+rank. A bare `python bench.py --gpus N` with N > 1 starts its N ranks itself
+(one child process per GPU, before anything touches the GPU) and exits with
+their status; WORLD_SIZE != --gpus is refused, and `n_gpus` is always the
+real world size.
 """
 from __future__ import annotations
 
@@ -27,6 +36,53 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "pods/sec sched throughput + p99 PodGroup gang-admit latency, 1/2/4/8-GPU groups"
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Start ranks 0..n-1 of this script as child processes (the parent never
+    initialises the GPU: it only counts devices) and wait for them. If one
+    rank fails the others are stopped, so a broken rank cannot leave its peers
+    blocked in a collective."""
+    import signal
+    import subprocess
+
+    try:
+        import torch
+
+        have = torch.cuda.device_count()  # does not initialise HIP on this image
+    except Exception:  # noqa: BLE001
+        have = 0
+    if have and have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) are visible", file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
 
 
 def main() -> int:
@@ -44,7 +100,16 @@ def main() -> int:
                     help="skip the per-BASELINE-config scenarios (untimed, reported under config.scenarios)")
     ap.add_argument("--cpus", default=os.environ.get("XSCHED_CPUS", "l3"),
                     help="shard CPU placement: none | l3 | l3xK | explicit list (utils/cpuaffinity.py)")
+    ap.add_argument("--no-placement", action="store_true",
+                    help="skip the end-to-end placement validation (discovery -> scheduler -> Allocate -> RCCL)")
     args = ap.parse_args()
+
+    world = os.environ.get("WORLD_SIZE")
+    if world is None and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    if world is not None and int(world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; one rank per GPU is required", file=sys.stderr)
+        return 2
 
     from flex_gpu_scheduler_amd.parallel.dist import init_distributed
     from flex_gpu_scheduler_amd.utils.benchrun import Shard, gang_latency_summary
@@ -121,14 +186,12 @@ def main() -> int:
     stats = shard.sched.stats()
     shard.close()
 
-    if ctx.distributed and ctx.cuda:
-        from flex_gpu_scheduler_amd.parallel.rccl_probe import allreduce_sweep
+    if not args.no_placement and (ctx.distributed or ctx.cuda):
+        # Untimed: gangs placed on the live node, resolved by the device
+        # plugin, all-reduced on exactly those GPUs (parallel/placement.py).
+        from flex_gpu_scheduler_amd.parallel.placement import validate_placement
 
-        try:
-            res = allreduce_sweep()
-            extras["rccl_allreduce"] = [{"MiB": r.bytes >> 20, "busbw_GBps": round(r.busbw_gbps, 1)} for r in res]
-        except Exception as e:  # noqa: BLE001 - the probe is informational, never fatal
-            extras["rccl_allreduce_error"] = f"{type(e).__name__}: {e}"
+        extras["rccl_placement"] = validate_placement(ctx)
 
     value = pods_total / t_max if t_max > 0 else 0.0
     if ctx.rank == 0 and not args.no_scenarios:
@@ -143,7 +206,7 @@ def main() -> int:
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "pods/s",
-            "n_gpus": args.gpus,
+            "n_gpus": ctx.world_size,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_max * 1000.0 / max(1, args.steps), 3),
@@ -156,7 +219,8 @@ def main() -> int:
                 "model": "FlexGPU(MI355X SPX/CPX/HBM) + Coscheduling + NRT xGMI gang placement",
                 "global_batch": int(round(pods_total / max(1, args.steps))),
                 "seq_len": None,
-                "parallelism": f"{ctx.world_size} scheduler shard(s), one per GPU",
+                "parallelism": f"{ctx.world_size} rank(s) x 1 scheduler shard, one rank per GPU "
+                               f"({ctx.backend if ctx.distributed else 'single process'})",
                 "nodes_per_shard": args.nodes,
                 "gpus_per_shard": args.nodes * 8,
                 "p99_gang_admit_ms": {k: v["p99_ms"] for k, v in lat.items()},

@@ -31,6 +31,9 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <vector>
+
+#include "hip/device_raii.h"
 
 #define XS_CHECK(x)                                                            \
   do {                                                                         \
@@ -44,6 +47,10 @@
 namespace {
 
 char g_err[512];
+
+using xsprobe::DevMem;
+using xsprobe::Event;
+using xsprobe::Stream;
 
 constexpr int kBlock = 256;  // 4 waves of 64 lanes
 
@@ -244,28 +251,45 @@ Variant decode(int v) {
   return o;
 }
 
+constexpr uint32_t kWriteSeed = 7;
+constexpr float kTriadScale = 3.0f;
+
+// mode 0 read(a), 1 write(a <- pattern(seed)), 2 copy(b <- a), 3 triad(a <- b + scale*c).
 template <int U, bool NT>
-void launch_t(int mode, int grid, hipStream_t s, void* a, void* b, void* c, size_t n, uint32_t* sink) {
+void launch_t(int mode, int grid, hipStream_t s, void* a, void* b, void* c, size_t n, uint32_t* sink, uint32_t seed,
+              float scale) {
   switch (mode) {
     case 0: k_read<U, NT><<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), n, sink); break;
-    case 1: k_write<U, NT><<<grid, kBlock, 0, s>>>(static_cast<vec4*>(a), n, 7); break;
+    case 1: k_write<U, NT><<<grid, kBlock, 0, s>>>(static_cast<vec4*>(a), n, seed); break;
     case 2: k_copy<U, NT><<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), static_cast<vec4*>(b), n); break;
     default:
       k_triad<U, NT><<<grid, kBlock, 0, s>>>(static_cast<f32x4*>(a), static_cast<const f32x4*>(b),
-                                            static_cast<const f32x4*>(c), 3.0f, n);
+                                            static_cast<const f32x4*>(c), scale, n);
   }
 }
 
-void launch(const Variant& v, int mode, int grid, hipStream_t s, void* a, void* b, void* c, size_t n, uint32_t* sink) {
+void launch(const Variant& v, int mode, int grid, hipStream_t s, void* a, void* b, void* c, size_t n, uint32_t* sink,
+            uint32_t seed = kWriteSeed, float scale = kTriadScale) {
   if (v.nt) {
-    if (v.unroll == 1) launch_t<1, true>(mode, grid, s, a, b, c, n, sink);
-    else if (v.unroll == 8) launch_t<8, true>(mode, grid, s, a, b, c, n, sink);
-    else launch_t<4, true>(mode, grid, s, a, b, c, n, sink);
+    if (v.unroll == 1) launch_t<1, true>(mode, grid, s, a, b, c, n, sink, seed, scale);
+    else if (v.unroll == 8) launch_t<8, true>(mode, grid, s, a, b, c, n, sink, seed, scale);
+    else launch_t<4, true>(mode, grid, s, a, b, c, n, sink, seed, scale);
   } else {
-    if (v.unroll == 1) launch_t<1, false>(mode, grid, s, a, b, c, n, sink);
-    else if (v.unroll == 8) launch_t<8, false>(mode, grid, s, a, b, c, n, sink);
-    else launch_t<4, false>(mode, grid, s, a, b, c, n, sink);
+    if (v.unroll == 1) launch_t<1, false>(mode, grid, s, a, b, c, n, sink, seed, scale);
+    else if (v.unroll == 8) launch_t<8, false>(mode, grid, s, a, b, c, n, sink, seed, scale);
+    else launch_t<4, false>(mode, grid, s, a, b, c, n, sink, seed, scale);
   }
+}
+
+Variant default_variant(int mode) {
+  // Measured optimum per mode on MI355X (profiles/r1b_probe_sweep.json):
+  // one 16-B access per lane per iteration wins; non-temporal loads help,
+  // plain stores beat nt stores for pure writes; 4-8 workgroups per CU.
+  Variant v;
+  v.unroll = 1;
+  v.nt = mode != 1;
+  v.bpc = mode == 0 ? 8 : 4;
+  return v;
 }
 
 }  // namespace
@@ -307,54 +331,79 @@ int xs_hbm_bandwidth_v(int dev, size_t bytes, int iters, int cu_limit, int mode,
   size_t n = bytes / sizeof(vec4);
   if (n == 0 || mode < 0 || mode > 3) return -1000;
   bytes = n * sizeof(vec4);
-  Variant v = decode(variant);
-  if (variant == 0) {
-    // Measured optimum per mode on MI355X (profiles/r1b_probe_sweep.json):
-    // one 16-B access per lane per iteration wins; non-temporal loads help,
-    // plain stores beat nt stores for pure writes; 4-8 workgroups per CU.
-    v.unroll = 1;
-    v.nt = mode != 1;
-    v.bpc = mode == 0 ? 8 : 4;
-  }
-  void *a = nullptr, *b = nullptr, *c = nullptr;
-  uint32_t* sink = nullptr;
-  XS_CHECK(hipMalloc(&a, bytes));
-  XS_CHECK(hipMalloc(&b, bytes));
-  if (mode == 3) XS_CHECK(hipMalloc(&c, bytes));
-  XS_CHECK(hipMalloc(&sink, sizeof(uint32_t)));
+  Variant v = variant == 0 ? default_variant(mode) : decode(variant);
+  DevMem a, b, c, sink;
+  XS_CHECK(hipMalloc(&a.p, bytes));
+  XS_CHECK(hipMalloc(&b.p, bytes));
+  if (mode == 3) XS_CHECK(hipMalloc(&c.p, bytes));
+  XS_CHECK(hipMalloc(&sink.p, sizeof(uint32_t)));
   int cus = cu_count(dev);
   if (cu_limit > 0 && cu_limit < cus) cus = cu_limit;
   int grid = cus * v.bpc;
-  hipStream_t s;
-  XS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  Stream s;
+  XS_CHECK(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
   // Page everything in and warm the launch path.
-  launch(Variant{}, 1, grid, s, a, nullptr, nullptr, n, sink);
-  launch(Variant{}, 1, grid, s, b, nullptr, nullptr, n, sink);
-  if (c) launch(Variant{}, 1, grid, s, c, nullptr, nullptr, n, sink);
+  launch(Variant{}, 1, grid, s.s, a.p, nullptr, nullptr, n, sink.as<uint32_t>());
+  launch(Variant{}, 1, grid, s.s, b.p, nullptr, nullptr, n, sink.as<uint32_t>());
+  if (c.p) launch(Variant{}, 1, grid, s.s, c.p, nullptr, nullptr, n, sink.as<uint32_t>());
   XS_CHECK(hipGetLastError());
-  launch(v, mode, grid, s, a, b, c, n, sink);
-  XS_CHECK(hipStreamSynchronize(s));
-  hipEvent_t e0, e1;
-  XS_CHECK(hipEventCreate(&e0));
-  XS_CHECK(hipEventCreate(&e1));
-  XS_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) launch(v, mode, grid, s, a, b, c, n, sink);
-  XS_CHECK(hipEventRecord(e1, s));
-  XS_CHECK(hipEventSynchronize(e1));
+  launch(v, mode, grid, s.s, a.p, b.p, c.p, n, sink.as<uint32_t>());
+  XS_CHECK(hipStreamSynchronize(s.s));
+  Event e0, e1;
+  XS_CHECK(hipEventCreate(&e0.e));
+  XS_CHECK(hipEventCreate(&e1.e));
+  XS_CHECK(hipEventRecord(e0.e, s.s));
+  for (int i = 0; i < iters; ++i) launch(v, mode, grid, s.s, a.p, b.p, c.p, n, sink.as<uint32_t>());
+  XS_CHECK(hipEventRecord(e1.e, s.s));
+  XS_CHECK(hipEventSynchronize(e1.e));
   XS_CHECK(hipGetLastError());
   float ms = 0;
-  XS_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  XS_CHECK(hipEventElapsedTime(&ms, e0.e, e1.e));
   double per = ms / iters;
   double moved = static_cast<double>(bytes) * (mode == 2 ? 2.0 : mode == 3 ? 3.0 : 1.0);
   if (gbps) *gbps = moved / (per * 1e-3) / 1e9;
   if (ms_per_iter) *ms_per_iter = per;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipStreamDestroy(s);
-  (void)hipFree(a);
-  (void)hipFree(b);
-  if (c) (void)hipFree(c);
-  (void)hipFree(sink);
+  return 0;
+}
+
+// One streaming kernel over caller-owned device buffers (e.g. torch tensors),
+// run to completion: the GPU tier checks the kernels' results against a plain
+// PyTorch fp32 reference. mode 1: a <- pattern(seed); 2: b <- a; 3: a <- b +
+// scale*c (float4 lanes). bytes must be a multiple of 16 and every pointer
+// 16-byte aligned. variant as in xs_hbm_bandwidth_v (0 = the tuned default).
+int xs_stream_op(int dev, int mode, void* a, void* b, void* c, size_t bytes, uint32_t seed, float scale,
+                 int variant) {
+  XS_CHECK(hipSetDevice(dev));
+  if (mode < 1 || mode > 3 || bytes == 0 || bytes % sizeof(vec4) != 0) return -1000;
+  const uintptr_t align = reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+                          reinterpret_cast<uintptr_t>(c);
+  if (!a || (mode >= 2 && !b) || (mode == 3 && !c) || (align & (sizeof(vec4) - 1))) return -1001;
+  Variant v = variant == 0 ? default_variant(mode) : decode(variant);
+  int grid = cu_count(dev) * v.bpc;
+  launch(v, mode, grid, nullptr, a, b, c, bytes / sizeof(vec4), nullptr, seed, scale);
+  XS_CHECK(hipGetLastError());
+  XS_CHECK(hipDeviceSynchronize());
+  return 0;
+}
+
+// XCD-pinned streaming over caller-owned buffers (mode 1 write dst, 2 copy
+// src -> dst): only workgroups on the XCDs in xcd_mask do the work.
+int xs_pinned_op(int dev, int mode, const void* src, void* dst, size_t bytes, uint32_t xcd_mask) {
+  XS_CHECK(hipSetDevice(dev));
+  if (mode < 1 || mode > 2 || xcd_mask == 0 || bytes == 0 || bytes % sizeof(vec4) != 0) return -1000;
+  const size_t n = bytes / sizeof(vec4);
+  if (n / 4096 >= 0xffffff00ull) return -1000;
+  if (!dst || (mode == 2 && !src) ||
+      ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & (sizeof(vec4) - 1)))
+    return -1001;
+  DevMem counter, sink;
+  XS_CHECK(hipMalloc(&counter.p, sizeof(unsigned)));
+  XS_CHECK(hipMalloc(&sink.p, sizeof(uint32_t)));
+  XS_CHECK(hipMemset(counter.p, 0, sizeof(unsigned)));
+  k_pinned<<<cu_count(dev) * 8, kBlock>>>(static_cast<const vec4*>(src), static_cast<vec4*>(dst), n, xcd_mask,
+                                         counter.as<unsigned>(), mode, sink.as<uint32_t>());
+  XS_CHECK(hipGetLastError());
+  XS_CHECK(hipDeviceSynchronize());
   return 0;
 }
 
@@ -372,45 +421,37 @@ int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, in
   size_t n = bytes / sizeof(vec4);
   if (n == 0 || n / 4096 >= 0xffffff00ull) return -1000;
   bytes = n * sizeof(vec4);
-  void *a = nullptr, *b = nullptr;
-  unsigned* counters = nullptr;
-  uint32_t* sink = nullptr;
-  XS_CHECK(hipMalloc(&a, bytes));
-  XS_CHECK(hipMalloc(&b, bytes));
-  XS_CHECK(hipMalloc(&counters, sizeof(unsigned) * (iters + 1)));
-  XS_CHECK(hipMalloc(&sink, sizeof(uint32_t)));
-  XS_CHECK(hipMemset(counters, 0, sizeof(unsigned) * (iters + 1)));
+  DevMem a, b, counters, sink;
+  XS_CHECK(hipMalloc(&a.p, bytes));
+  XS_CHECK(hipMalloc(&b.p, bytes));
+  XS_CHECK(hipMalloc(&counters.p, sizeof(unsigned) * (iters + 1)));
+  XS_CHECK(hipMalloc(&sink.p, sizeof(uint32_t)));
+  XS_CHECK(hipMemset(counters.p, 0, sizeof(unsigned) * (iters + 1)));
+  unsigned* ctr = counters.as<unsigned>();
   int grid = cu_count(dev) * 8;  // every CU gets 8 workgroups; only masked XCDs work
-  hipStream_t s;
-  XS_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  k_write<4, true><<<grid, kBlock, 0, s>>>(static_cast<vec4*>(a), n, 1);
-  k_pinned<<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), static_cast<vec4*>(b), n, xcd_mask, &counters[iters],
-                                   mode, sink);
+  Stream s;
+  XS_CHECK(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
+  k_write<4, true><<<grid, kBlock, 0, s.s>>>(a.as<vec4>(), n, 1);
+  k_pinned<<<grid, kBlock, 0, s.s>>>(a.as<const vec4>(), b.as<vec4>(), n, xcd_mask, &ctr[iters], mode,
+                                     sink.as<uint32_t>());
   XS_CHECK(hipGetLastError());
-  XS_CHECK(hipStreamSynchronize(s));
-  hipEvent_t e0, e1;
-  XS_CHECK(hipEventCreate(&e0));
-  XS_CHECK(hipEventCreate(&e1));
-  XS_CHECK(hipEventRecord(e0, s));
+  XS_CHECK(hipStreamSynchronize(s.s));
+  Event e0, e1;
+  XS_CHECK(hipEventCreate(&e0.e));
+  XS_CHECK(hipEventCreate(&e1.e));
+  XS_CHECK(hipEventRecord(e0.e, s.s));
   for (int i = 0; i < iters; ++i)
-    k_pinned<<<grid, kBlock, 0, s>>>(static_cast<const vec4*>(a), static_cast<vec4*>(b), n, xcd_mask, &counters[i],
-                                     mode, sink);
-  XS_CHECK(hipEventRecord(e1, s));
-  XS_CHECK(hipEventSynchronize(e1));
+    k_pinned<<<grid, kBlock, 0, s.s>>>(a.as<const vec4>(), b.as<vec4>(), n, xcd_mask, &ctr[i], mode,
+                                       sink.as<uint32_t>());
+  XS_CHECK(hipEventRecord(e1.e, s.s));
+  XS_CHECK(hipEventSynchronize(e1.e));
   XS_CHECK(hipGetLastError());
   float ms = 0;
-  XS_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  XS_CHECK(hipEventElapsedTime(&ms, e0.e, e1.e));
   double per = ms / iters;
   double moved = static_cast<double>(bytes) * (mode == 2 ? 2.0 : 1.0);
   if (gbps) *gbps = moved / (per * 1e-3) / 1e9;
   if (ms_per_iter) *ms_per_iter = per;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipStreamDestroy(s);
-  (void)hipFree(a);
-  (void)hipFree(b);
-  (void)hipFree(counters);
-  (void)hipFree(sink);
   return 0;
 }
 
@@ -419,16 +460,15 @@ int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, in
 int xs_xcd_census(int dev, int blocks, int* xcd_hist8, int* distinct_cus) {
   XS_CHECK(hipSetDevice(dev));
   if (blocks <= 0) blocks = 2048;
-  uint32_t *dx = nullptr, *dh = nullptr;
-  XS_CHECK(hipMalloc(&dx, blocks * sizeof(uint32_t)));
-  XS_CHECK(hipMalloc(&dh, blocks * sizeof(uint32_t)));
-  k_census<<<blocks, 64>>>(dx, dh);
+  DevMem dx, dh;
+  XS_CHECK(hipMalloc(&dx.p, blocks * sizeof(uint32_t)));
+  XS_CHECK(hipMalloc(&dh.p, blocks * sizeof(uint32_t)));
+  k_census<<<blocks, 64>>>(dx.as<uint32_t>(), dh.as<uint32_t>());
   XS_CHECK(hipGetLastError());
   XS_CHECK(hipDeviceSynchronize());
-  uint32_t* hx = new uint32_t[blocks];
-  uint32_t* hh = new uint32_t[blocks];
-  XS_CHECK(hipMemcpy(hx, dx, blocks * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  XS_CHECK(hipMemcpy(hh, dh, blocks * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::vector<uint32_t> hx(blocks), hh(blocks);
+  XS_CHECK(hipMemcpy(hx.data(), dx.p, blocks * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  XS_CHECK(hipMemcpy(hh.data(), dh.p, blocks * sizeof(uint32_t), hipMemcpyDeviceToHost));
   int hist[16] = {0};
   for (int i = 0; i < blocks; ++i) hist[hx[i] & 0xf]++;
   int distinct = 0;
@@ -446,10 +486,6 @@ int xs_xcd_census(int dev, int blocks, int* xcd_hist8, int* distinct_cus) {
     }
     *distinct_cus = uniq;
   }
-  delete[] hx;
-  delete[] hh;
-  (void)hipFree(dx);
-  (void)hipFree(dh);
   return distinct;
 }
 
@@ -459,23 +495,20 @@ int xs_health_check(int dev, size_t bytes, unsigned long long* device_sum, unsig
   XS_CHECK(hipSetDevice(dev));
   size_t n = bytes / sizeof(uint32_t);
   if (n == 0) n = 1 << 20;
-  uint32_t* buf = nullptr;
-  unsigned long long* out = nullptr;
-  XS_CHECK(hipMalloc(&buf, n * sizeof(uint32_t)));
-  XS_CHECK(hipMalloc(&out, sizeof(unsigned long long)));
-  XS_CHECK(hipMemset(out, 0, sizeof(unsigned long long)));
+  DevMem buf, out;
+  XS_CHECK(hipMalloc(&buf.p, n * sizeof(uint32_t)));
+  XS_CHECK(hipMalloc(&out.p, sizeof(unsigned long long)));
+  XS_CHECK(hipMemset(out.p, 0, sizeof(unsigned long long)));
   int grid = cu_count(dev) * 8;
-  k_pattern<<<grid, kBlock>>>(buf, n);
-  k_checksum<<<grid, kBlock>>>(buf, n, out);
+  k_pattern<<<grid, kBlock>>>(buf.as<uint32_t>(), n);
+  k_checksum<<<grid, kBlock>>>(buf.as<uint32_t>(), n, out.as<unsigned long long>());
   XS_CHECK(hipGetLastError());
   unsigned long long d = 0;
-  XS_CHECK(hipMemcpy(&d, out, sizeof d, hipMemcpyDeviceToHost));
+  XS_CHECK(hipMemcpy(&d, out.p, sizeof d, hipMemcpyDeviceToHost));
   unsigned long long h = 0;
   for (size_t i = 0; i < n; ++i) h += static_cast<uint32_t>(static_cast<uint32_t>(i * 2654435761u) ^ 0xa5a5a5a5u);
   if (device_sum) *device_sum = d;
   if (host_sum) *host_sum = h;
-  (void)hipFree(buf);
-  (void)hipFree(out);
   return d == h ? 0 : 1;
 }
 

@@ -21,6 +21,8 @@
 #include <cstdio>
 #include <vector>
 
+#include "hip/device_raii.h"
+
 namespace {
 
 char g_mfma_err[512];
@@ -114,20 +116,17 @@ int xs_mfma_check(int dev, int K) {
       bi[k * 32 + j] = (k * 5 + j * 11 + (j > k ? 3 : 0)) % 13 - 6;  // asymmetric
       b[k * 32 + j] = to_bf16(static_cast<float>(bi[k * 32 + j]));
     }
-  __bf16 *da = nullptr, *db = nullptr;
-  float* dc = nullptr;
-  XS_MCHECK(hipMalloc(&da, a.size() * sizeof(__bf16)));
-  XS_MCHECK(hipMalloc(&db, b.size() * sizeof(__bf16)));
-  XS_MCHECK(hipMalloc(&dc, 32 * 32 * sizeof(float)));
-  XS_MCHECK(hipMemcpy(da, a.data(), a.size() * sizeof(__bf16), hipMemcpyHostToDevice));
-  XS_MCHECK(hipMemcpy(db, b.data(), b.size() * sizeof(__bf16), hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_mfma_tile, dim3(1), dim3(64), 0, 0, da, db, dc, K);
+  xsprobe::DevMem da, db, dc;
+  XS_MCHECK(hipMalloc(&da.p, a.size() * sizeof(__bf16)));
+  XS_MCHECK(hipMalloc(&db.p, b.size() * sizeof(__bf16)));
+  XS_MCHECK(hipMalloc(&dc.p, 32 * 32 * sizeof(float)));
+  XS_MCHECK(hipMemcpy(da.p, a.data(), a.size() * sizeof(__bf16), hipMemcpyHostToDevice));
+  XS_MCHECK(hipMemcpy(db.p, b.data(), b.size() * sizeof(__bf16), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_mfma_tile, dim3(1), dim3(64), 0, 0, da.as<const __bf16>(), db.as<const __bf16>(),
+                     dc.as<float>(), K);
   XS_MCHECK(hipGetLastError());
   std::vector<float> c(32 * 32);
-  XS_MCHECK(hipMemcpy(c.data(), dc, c.size() * sizeof(float), hipMemcpyDeviceToHost));
-  (void)hipFree(da);
-  (void)hipFree(db);
-  (void)hipFree(dc);
+  XS_MCHECK(hipMemcpy(c.data(), dc.p, c.size() * sizeof(float), hipMemcpyDeviceToHost));
   int bad = 0;
   for (int i = 0; i < 32; ++i)
     for (int j = 0; j < 32; ++j) {
@@ -148,20 +147,23 @@ int xs_mfma_peak(int dev, int iters, uint32_t xcd_mask, int blocks, double* tflo
   XS_MCHECK(hipGetDeviceProperties(&p, dev));
   if (blocks <= 0) blocks = 2 * p.multiProcessorCount;
   if (iters <= 0) iters = 4096;
-  unsigned* d_active = nullptr;
-  float* d_sink = nullptr;
-  XS_MCHECK(hipMalloc(&d_active, sizeof(unsigned)));
-  XS_MCHECK(hipMalloc(&d_sink, blocks * sizeof(float)));
-  hipStream_t s;
-  XS_MCHECK(hipStreamCreate(&s));
+  xsprobe::DevMem active_mem, sink_mem;
+  XS_MCHECK(hipMalloc(&active_mem.p, sizeof(unsigned)));
+  XS_MCHECK(hipMalloc(&sink_mem.p, blocks * sizeof(float)));
+  unsigned* d_active = active_mem.as<unsigned>();
+  float* d_sink = sink_mem.as<float>();
+  xsprobe::Stream stream;
+  XS_MCHECK(hipStreamCreate(&stream.s));
+  hipStream_t s = stream.s;
   // Warm-up (clocks up, code resident).
   XS_MCHECK(hipMemsetAsync(d_active, 0, sizeof(unsigned), s));
   hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters / 4 + 1, xcd_mask, d_active, d_sink);
   XS_MCHECK(hipGetLastError());
   XS_MCHECK(hipMemsetAsync(d_active, 0, sizeof(unsigned), s));
-  hipEvent_t e0, e1;
-  XS_MCHECK(hipEventCreate(&e0));
-  XS_MCHECK(hipEventCreate(&e1));
+  xsprobe::Event ev0, ev1;
+  XS_MCHECK(hipEventCreate(&ev0.e));
+  XS_MCHECK(hipEventCreate(&ev1.e));
+  hipEvent_t e0 = ev0.e, e1 = ev1.e;
   XS_MCHECK(hipEventRecord(e0, s));
   hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters, xcd_mask, d_active, d_sink);
   XS_MCHECK(hipGetLastError());
@@ -171,11 +173,6 @@ int xs_mfma_peak(int dev, int iters, uint32_t xcd_mask, int blocks, double* tflo
   XS_MCHECK(hipEventElapsedTime(&ms, e0, e1));
   unsigned active = 0;
   XS_MCHECK(hipMemcpy(&active, d_active, sizeof(unsigned), hipMemcpyDeviceToHost));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipStreamDestroy(s);
-  (void)hipFree(d_active);
-  (void)hipFree(d_sink);
   const double flop_per_mfma = 2.0 * 32 * 32 * 16;
   double flops = static_cast<double>(active) * (kPeakBlock / 64) * kAcc * static_cast<double>(iters) * flop_per_mfma;
   *tflops = ms > 0 ? flops / (ms * 1e-3) / 1e12 : 0.0;

@@ -36,6 +36,14 @@ class HipProbe:
     def __init__(self, path: str | Path = _LIB):
         if not Path(path).exists():
             raise ProbeError(f"{path} not built; run `python -m flex_gpu_scheduler_amd.build_ext --hip`")
+        try:
+            # torch's bundled libamdhip64.so.7 first, whatever the import order
+            # of the caller: the probe library then resolves the same soname to
+            # that copy, so one HIP runtime owns every device pointer and
+            # stream in the process (tensors handed to the kernels included).
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         self.lib = ctypes.CDLL(str(path))
         L = self.lib
         L.xs_last_error.restype = ctypes.c_char_p
@@ -51,6 +59,10 @@ class HipProbe:
                                     ctypes.POINTER(ctypes.c_int)]
         L.xs_health_check.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_ulonglong),
                                       ctypes.POINTER(ctypes.c_ulonglong)]
+        L.xs_stream_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_size_t, ctypes.c_uint32, ctypes.c_float, ctypes.c_int]
+        L.xs_pinned_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.c_uint32]
         L.xs_mfma_last_error.restype = ctypes.c_char_p
         L.xs_mfma_check.argtypes = [ctypes.c_int, ctypes.c_int]
         L.xs_mfma_peak.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
@@ -102,6 +114,65 @@ class HipProbe:
                                     "GBps": round(bw.gbps, 1)})
         best = max(results, key=lambda r: r["GBps"])
         return {"mode": mode, "best": best, "all": results}
+
+    # ------------------------------------------------ kernels on torch tensors
+    # The streaming kernels run on caller-owned device buffers so the GPU tier
+    # can check their output against a plain PyTorch fp32 reference. torch
+    # must be imported before this library is loaded (one HIP runtime: both
+    # resolve the soname libamdhip64.so.7 to the same copy).
+    @staticmethod
+    def _dev_buf(t, what: str) -> tuple[int, int]:
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError(f"{what} must be a contiguous device tensor")
+        nbytes = t.numel() * t.element_size()
+        if nbytes % 16 or t.data_ptr() % 16:
+            raise ValueError(f"{what}: {nbytes} bytes at {t.data_ptr():#x} is not 16-byte granular")
+        return t.data_ptr(), nbytes
+
+    def _stream(self, dev: int, mode: int, a, b, c, nbytes: int, seed: int = 7, scale: float = 3.0,
+                variant: int = 0) -> None:
+        rc = self.lib.xs_stream_op(dev, mode, a, b, c, nbytes, seed, scale, variant)
+        if rc != 0:
+            raise self._err(rc, "stream_op")
+
+    def write_pattern(self, dst, seed: int = 7, variant: int = 0) -> None:
+        """k_write: every 16-B lane of `dst` <- (seed, seed^0x55555555, seed+1, ~seed) as uint32."""
+        p, n = self._dev_buf(dst, "dst")
+        self._stream(dst.device.index or 0, MODES["write"], p, None, None, n, seed=seed, variant=variant)
+
+    def copy(self, dst, src, variant: int = 0) -> None:
+        """k_copy: dst <- src (byte copy; equal sizes)."""
+        pd, n = self._dev_buf(dst, "dst")
+        ps, ns = self._dev_buf(src, "src")
+        if n != ns:
+            raise ValueError("copy: size mismatch")
+        self._stream(dst.device.index or 0, MODES["copy"], ps, pd, None, n, variant=variant)
+
+    def triad(self, a, b, c, scale: float = 3.0, variant: int = 0) -> None:
+        """k_triad (STREAM): a <- b + scale*c on fp32 tensors."""
+        import torch
+
+        if not (a.dtype == b.dtype == c.dtype == torch.float32):
+            raise ValueError("triad: fp32 tensors only")
+        pa, n = self._dev_buf(a, "a")
+        pb_, nb = self._dev_buf(b, "b")
+        pc, nc = self._dev_buf(c, "c")
+        if not n == nb == nc:
+            raise ValueError("triad: size mismatch")
+        self._stream(a.device.index or 0, MODES["triad"], pa, pb_, pc, n, scale=scale, variant=variant)
+
+    def pinned(self, dst, src=None, xcd_mask: int = 0x1) -> None:
+        """k_pinned on the XCDs of `xcd_mask`: copy src -> dst, or write the
+        fill pattern (1, 2, 3, 4) into dst when src is None."""
+        pd, n = self._dev_buf(dst, "dst")
+        ps = 0
+        if src is not None:
+            ps, ns = self._dev_buf(src, "src")
+            if ns != n:
+                raise ValueError("pinned: size mismatch")
+        rc = self.lib.xs_pinned_op(dst.device.index or 0, 2 if src is not None else 1, ps or None, pd, n, xcd_mask)
+        if rc != 0:
+            raise self._err(rc, "pinned_op")
 
     def hbm_bandwidth_xcd(self, dev: int = 0, xcd_mask: int = 0x1, nbytes: int = 1 << 30, iters: int = 10,
                           mode: str = "read") -> Bandwidth:

@@ -1,6 +1,10 @@
 """Run one HIP probe kernel family in isolation (for rocprofv3 --pmc passes).
 
-    python -m flex_gpu_scheduler_amd.tools.probe_kernels mfma|hbm-read|hbm-copy [device]
+    python -m flex_gpu_scheduler_amd.tools.probe_kernels PROBE [device]
+
+    PROBE: mfma | hbm-read | hbm-copy | hbm-triad | hbm-write
+           | xcd-read-K | xcd-copy-K   (k_pinned on the first K XCDs: K=1 is
+             one CPX partition's CUs, 2 QPX, 4 DPX, 8 the whole GPU)
 
 Prints the probe's own measurement as one JSON line, so a counter pass can be
 cross-checked against the timing the probe reports.
@@ -20,9 +24,17 @@ def main() -> int:
     if what == "mfma":
         r = pr.mfma_peak(dev, 0xFF, iters=8192)
         out = {"kernel": "k_mfma_peak", "TFLOPs": round(r["tflops"], 1), "ms": round(r["ms"], 3)}
-    elif what in ("hbm-read", "hbm-copy"):
+    elif what in ("hbm-read", "hbm-copy", "hbm-triad", "hbm-write"):
         bw = pr.hbm_bandwidth(dev, 2 << 30, iters=5, mode=what.split("-")[1])
-        out = {"kernel": what, "bytes": 2 << 30, "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4)}
+        arrays = {"read": 1, "write": 1, "copy": 2, "triad": 3}[what.split("-")[1]]
+        out = {"kernel": what, "bytes_per_array": 2 << 30, "arrays": arrays, "GBps": round(bw.gbps, 1),
+               "ms": round(bw.ms_per_iter, 4), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
+    elif what.startswith("xcd-"):
+        _, mode, k = what.split("-")
+        mask = (1 << int(k)) - 1
+        bw = pr.hbm_bandwidth_xcd(dev, mask, 1 << 30, iters=5, mode=mode)
+        out = {"kernel": f"k_pinned[{mode}]", "xcds": int(k), "xcd_mask": mask, "bytes": 1 << 30,
+               "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
     else:
         raise SystemExit(f"unknown probe {what!r}")
     print(json.dumps(out))

@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out
+OUT=${OUTDIR:-gpurun_out}
 mkdir -p "$OUT"
 run() {  # name probe counters...
   local name=$1 probe=$2; shift 2
@@ -18,5 +18,12 @@ run() {  # name probe counters...
 timeout -s KILL 60 rocprofv3 --list-avail > "$OUT/pmc_list_avail.txt" 2>&1 || true
 run mfma mfma SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE &&
 run hbm_read hbm-read FETCH_SIZE GRBM_GUI_ACTIVE &&
-run hbm_copy hbm-copy WRITE_SIZE GRBM_GUI_ACTIVE
+run hbm_copy hbm-copy WRITE_SIZE GRBM_GUI_ACTIVE &&
+run triad_fetch hbm-triad FETCH_SIZE GRBM_GUI_ACTIVE &&
+run triad_write hbm-triad WRITE_SIZE GRBM_GUI_ACTIVE &&
+run xcd1_read xcd-read-1 FETCH_SIZE GRBM_GUI_ACTIVE &&
+run xcd2_read xcd-read-2 FETCH_SIZE GRBM_GUI_ACTIVE &&
+run xcd4_read xcd-read-4 FETCH_SIZE GRBM_GUI_ACTIVE &&
+run xcd8_read xcd-read-8 FETCH_SIZE GRBM_GUI_ACTIVE &&
+run xcd1_copy xcd-copy-1 WRITE_SIZE GRBM_GUI_ACTIVE
 echo "[pmc] done" | tee -a "$OUT/pmc_steps.log"

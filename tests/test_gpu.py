@@ -90,6 +90,33 @@ def test_bench_one_gpu_json_contract():
               "vs_baseline", "dtype", "data", "config"):
         assert k in line
     assert line["value"] > 0 and line["config"]["gpu"]["name"].startswith("gfx950")
+    assert line["n_gpus"] == 1
+    pl = line["config"]["rccl_placement"]
+    assert pl["source"] == "live sysfs/KFD", pl
+    assert pl["gangs"][0]["gang"] == 1 and pl["gangs"][0]["ordinals"] == [0], pl
+
+
+def test_placement_resolves_to_the_visible_gpu():
+    """Live discovery -> scheduler -> device-plugin Allocate -> HIP ordinal:
+    the 1-rank gang lands on the GPU this process holds (every other GPU of
+    the box is occupied by tenant pods), and the render node Allocate returns
+    is that GPU's, matched by PCI address."""
+    import torch
+
+    from flex_gpu_scheduler_amd.gpu.discovery import discover_host
+    from flex_gpu_scheduler_amd.parallel.dist import DistContext
+    from flex_gpu_scheduler_amd.parallel.placement import validate_placement
+
+    host = discover_host()
+    assert host.gpus, "no amdgpu devices in sysfs"
+    r = validate_placement(DistContext(rank=0, local_rank=0, world_size=1, backend="none", cuda=True))
+    assert "error" not in r, r
+    g = r["gangs"][0]
+    assert g["gang"] == 1 and g["ordinals"] == [0]
+    p = torch.cuda.get_device_properties(0)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    assert host.gpus[g["gpus"][0]].bdf == bdf, (g, bdf)
+    assert g["xsched_gpu_index"] == [str(g["gpus"][0])]
 
 
 @pytest.mark.gpu
