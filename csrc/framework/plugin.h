@@ -65,6 +65,8 @@ class ApiClient {
 };
 
 // Everything a plugin can reach (framework.Handle).
+class Extender;  // scheduler/extender.h
+
 struct Handle {
   Framework* framework = nullptr;
   SchedulerCache* cache = nullptr;
@@ -80,6 +82,10 @@ struct Handle {
   // Moves these pods (when queued as unschedulable or backing off) to the
   // active queue; callable from any thread (e.g. a plugin's timer).
   std::function<void(const std::vector<PodPtr>&)> activate;
+  // HTTP extenders of the configuration (preemption's callExtenders) and the
+  // informer store's objects they are sent.
+  const std::vector<std::shared_ptr<Extender>>* extenders = nullptr;
+  std::function<JsonPtr(const std::string& kind, const std::string& ns, const std::string& name)> lookup;
 };
 
 class Plugin {

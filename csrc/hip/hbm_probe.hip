@@ -146,23 +146,38 @@ __device__ __forceinline__ uint32_t hw_cu_id() {
   return v;
 }
 
-// XCD-pinned streaming: workgroups off the selected XCDs exit at once; the
-// rest pull 64 KiB chunks from an atomic counter until the buffer is done, so
-// the launch always drains. mode 0 read, 1 write, 2 copy.
+// XCD-pinned streaming: workgroups off the selected XCDs exit at once. The
+// selected XCDs split the buffer into equal contiguous slices (by their rank
+// in xcd_mask) and the workgroups of each XCD pull 256 KiB chunks of their
+// slice from that XCD's own counter, so the launch always drains and no
+// atomic is shared across XCDs (one counter per 128-B line: a single
+// device-wide counter serialized the 8-XCD case at ~2 TB/s, round-3 pmc
+// run). mode 0 read, 1 write, 2 copy.
+constexpr int kCounterStride = 32;  // unsigned per XCD counter (128 B)
+constexpr int kMaxXcds = 8;
+
 __global__ __launch_bounds__(kBlock) void k_pinned(const vec4* __restrict__ src, vec4* __restrict__ dst, size_t n,
-                                                   uint32_t xcd_mask, unsigned* __restrict__ counter, int mode,
+                                                   uint32_t xcd_mask, unsigned* __restrict__ counters, int mode,
                                                    uint32_t* __restrict__ sink) {
-  if (!((xcd_mask >> xcc_id()) & 1u)) return;
-  constexpr size_t kChunk = 4096;  // vec4s = 64 KiB
+  const uint32_t x = xcc_id();
+  if (x >= kMaxXcds || !((xcd_mask >> x) & 1u)) return;
+  constexpr size_t kChunk = 16384;  // vec4s = 256 KiB
+  const uint32_t sel = xcd_mask & 0xffu;
+  const size_t nsel = static_cast<size_t>(__popc(sel));
+  const size_t rank = static_cast<size_t>(__popc(sel & ((1u << x) - 1u)));
+  const size_t nchunks = (n + kChunk - 1) / kChunk;
+  const size_t c0 = nchunks * rank / nsel, c1 = nchunks * (rank + 1) / nsel;
+  unsigned* ctr = counters + x * kCounterStride;
   __shared__ unsigned chunk;
   uint32_t acc = 0;
   const vec4 fill = {1u, 2u, 3u, 4u};
   for (;;) {
-    if (threadIdx.x == 0) chunk = atomicAdd(counter, 1u);
+    if (threadIdx.x == 0) chunk = atomicAdd(ctr, 1u);
     __syncthreads();
-    size_t base = static_cast<size_t>(chunk) * kChunk;
+    const size_t c = c0 + chunk;
     __syncthreads();
-    if (base >= n) break;
+    if (c >= c1) break;
+    size_t base = c * kChunk;
     size_t end = base + kChunk < n ? base + kChunk : n;
     size_t i = base + threadIdx.x;
     for (; i + 3 * kBlock < end; i += 4 * kBlock) {
@@ -392,14 +407,15 @@ int xs_pinned_op(int dev, int mode, const void* src, void* dst, size_t bytes, ui
   XS_CHECK(hipSetDevice(dev));
   if (mode < 1 || mode > 2 || xcd_mask == 0 || bytes == 0 || bytes % sizeof(vec4) != 0) return -1000;
   const size_t n = bytes / sizeof(vec4);
-  if (n / 4096 >= 0xffffff00ull) return -1000;
+  if (n / 16384 >= 0xffffff00ull) return -1000;
   if (!dst || (mode == 2 && !src) ||
       ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & (sizeof(vec4) - 1)))
     return -1001;
   DevMem counter, sink;
-  XS_CHECK(hipMalloc(&counter.p, sizeof(unsigned)));
+  const size_t ctr_bytes = sizeof(unsigned) * kMaxXcds * kCounterStride;
+  XS_CHECK(hipMalloc(&counter.p, ctr_bytes));
   XS_CHECK(hipMalloc(&sink.p, sizeof(uint32_t)));
-  XS_CHECK(hipMemset(counter.p, 0, sizeof(unsigned)));
+  XS_CHECK(hipMemset(counter.p, 0, ctr_bytes));
   k_pinned<<<cu_count(dev) * 8, kBlock>>>(static_cast<const vec4*>(src), static_cast<vec4*>(dst), n, xcd_mask,
                                          counter.as<unsigned>(), mode, sink.as<uint32_t>());
   XS_CHECK(hipGetLastError());
@@ -419,20 +435,21 @@ int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, in
   if (iters <= 0) iters = 10;
   if (mode < 0 || mode > 2 || xcd_mask == 0) return -1000;
   size_t n = bytes / sizeof(vec4);
-  if (n == 0 || n / 4096 >= 0xffffff00ull) return -1000;
+  if (n == 0 || n / 16384 >= 0xffffff00ull) return -1000;
   bytes = n * sizeof(vec4);
   DevMem a, b, counters, sink;
   XS_CHECK(hipMalloc(&a.p, bytes));
   XS_CHECK(hipMalloc(&b.p, bytes));
-  XS_CHECK(hipMalloc(&counters.p, sizeof(unsigned) * (iters + 1)));
+  const size_t per_launch = static_cast<size_t>(kMaxXcds) * kCounterStride;  // fresh counters per launch
+  XS_CHECK(hipMalloc(&counters.p, sizeof(unsigned) * per_launch * (iters + 1)));
   XS_CHECK(hipMalloc(&sink.p, sizeof(uint32_t)));
-  XS_CHECK(hipMemset(counters.p, 0, sizeof(unsigned) * (iters + 1)));
+  XS_CHECK(hipMemset(counters.p, 0, sizeof(unsigned) * per_launch * (iters + 1)));
   unsigned* ctr = counters.as<unsigned>();
   int grid = cu_count(dev) * 8;  // every CU gets 8 workgroups; only masked XCDs work
   Stream s;
   XS_CHECK(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
   k_write<4, true><<<grid, kBlock, 0, s.s>>>(a.as<vec4>(), n, 1);
-  k_pinned<<<grid, kBlock, 0, s.s>>>(a.as<const vec4>(), b.as<vec4>(), n, xcd_mask, &ctr[iters], mode,
+  k_pinned<<<grid, kBlock, 0, s.s>>>(a.as<const vec4>(), b.as<vec4>(), n, xcd_mask, &ctr[iters * per_launch], mode,
                                      sink.as<uint32_t>());
   XS_CHECK(hipGetLastError());
   XS_CHECK(hipStreamSynchronize(s.s));
@@ -441,7 +458,7 @@ int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, in
   XS_CHECK(hipEventCreate(&e1.e));
   XS_CHECK(hipEventRecord(e0.e, s.s));
   for (int i = 0; i < iters; ++i)
-    k_pinned<<<grid, kBlock, 0, s.s>>>(a.as<const vec4>(), b.as<vec4>(), n, xcd_mask, &ctr[i], mode,
+    k_pinned<<<grid, kBlock, 0, s.s>>>(a.as<const vec4>(), b.as<vec4>(), n, xcd_mask, &ctr[i * per_launch], mode,
                                        sink.as<uint32_t>());
   XS_CHECK(hipEventRecord(e1.e, s.s));
   XS_CHECK(hipEventSynchronize(e1.e));

@@ -476,7 +476,16 @@ PYBIND11_MODULE(_xsched, m) {
            py::arg("timeout_ms") = 30000, py::arg("qps") = 0.0, py::arg("burst") = 0);
   py::class_<rest::RestApiClient, ApiClient, std::shared_ptr<rest::RestApiClient>>(m, "RestApiClient")
       .def(py::init<rest::Endpoint>())
-      .def("requests", &rest::RestApiClient::requests);
+      .def("requests", &rest::RestApiClient::requests)
+      .def(
+          "bind_json",
+          [](rest::RestApiClient& c, py::handle pod, const std::string& node, py::handle ann) {
+            auto p = Pod::from_json(json_arg(pod));
+            Json a = json_arg(ann);
+            py::gil_scoped_release r;
+            c.bind(*p, node, a);
+          },
+          py::arg("pod"), py::arg("node"), py::arg("annotations") = py::dict());
   py::class_<rest::RemoteMirror, std::shared_ptr<rest::RemoteMirror>>(m, "RemoteMirror")
       .def(py::init<rest::Endpoint, std::shared_ptr<ObjectStore>, std::vector<std::string>>())
       .def("start", &rest::RemoteMirror::start)

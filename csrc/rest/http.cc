@@ -21,6 +21,8 @@ namespace xsched::rest {
 
 namespace {
 
+constexpr int kWatchRecvTimeoutS = 330;  // > the watches' timeoutSeconds=300
+
 std::string ssl_error(const std::string& what) {
   unsigned long e = ERR_get_error();
   char buf[256];
@@ -133,9 +135,22 @@ HttpConn::HttpConn(const Endpoint& ep, std::shared_ptr<TlsContext> tls, bool str
     if (fd < 0) continue;
     timeval tv{ep.timeout_ms / 1000, (ep.timeout_ms % 1000) * 1000};
     setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
-    // A watch stream idles between events (the server's own timeout and
-    // bookmarks end it): no receive timeout there.
-    if (!streaming) setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    if (!streaming) {
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    } else {
+      // A watch idles between events until the server's timeoutSeconds
+      // (300 s) ends it. A half-open connection (API server host lost, an
+      // idle-dropping load balancer) would block recv forever: TCP keepalive
+      // probes find a dead peer within ~1 min, and a receive timeout above
+      // the watch timeout ends the stream regardless, so the mirror re-watches.
+      timeval rtv{kWatchRecvTimeoutS, 0};
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &rtv, sizeof(rtv));
+      int on = 1, idle = 30, intvl = 10, cnt = 3;
+      setsockopt(fd, SOL_SOCKET, SO_KEEPALIVE, &on, sizeof(on));
+      setsockopt(fd, IPPROTO_TCP, TCP_KEEPIDLE, &idle, sizeof(idle));
+      setsockopt(fd, IPPROTO_TCP, TCP_KEEPINTVL, &intvl, sizeof(intvl));
+      setsockopt(fd, IPPROTO_TCP, TCP_KEEPCNT, &cnt, sizeof(cnt));
+    }
     if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) {
       int one = 1;
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));  // small keep-alive requests
@@ -206,6 +221,7 @@ void HttpConn::send_request(std::string_view method, std::string_view path, std:
     if (n <= 0) {
       if (!ssl_ && n < 0 && errno == EINTR) continue;
       reusable_ = false;
+      note_io_failure(n);
       throw std::runtime_error(std::string("send: ") + (ssl_ ? "TLS write failed" : std::strerror(errno)));
     }
     off += static_cast<size_t>(n);
@@ -230,12 +246,26 @@ bool HttpConn::fill() {
     }
     if (n > 0) {
       buf_.append(tmp, static_cast<size_t>(n));
+      rx_bytes_ += static_cast<size_t>(n);
       return true;
     }
     if (!ssl_ && n < 0 && errno == EINTR) continue;
     reusable_ = false;
+    note_io_failure(n);
     return false;
   }
+}
+
+void HttpConn::note_io_failure(ssize_t n) {
+  const int e = errno;
+  if (e == EAGAIN || e == EWOULDBLOCK || e == ETIMEDOUT)
+    fail_ = Fail::kTimeout;  // SO_RCVTIMEO/SO_SNDTIMEO expired: the server may be working on it
+  else if (e == ECONNRESET || e == EPIPE || e == ECONNABORTED)
+    fail_ = Fail::kReset;
+  else if (n == 0)
+    fail_ = Fail::kEof;
+  else
+    fail_ = Fail::kOther;
 }
 
 bool HttpConn::read_line_raw(std::string& out) {
@@ -311,6 +341,9 @@ bool HttpConn::read_chunked_body(std::string& out) {
 
 Response HttpConn::roundtrip(std::string_view method, std::string_view path, std::string_view body,
                              std::string_view content_type) {
+  fail_ = Fail::kNone;
+  rx_bytes_ = 0;
+  errno = 0;
   send_request(method, path, body, content_type);
   bool chunked;
   int64_t len;

@@ -8,6 +8,8 @@
 // no interpreter lock on the path (rest/kube.h).
 #pragma once
 
+#include <sys/types.h>
+
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -64,6 +66,10 @@ class HttpConn {
   bool next_line(std::string& line);
   // The server asked to close, or an error happened: do not reuse.
   bool reusable() const { return reusable_; }
+  // The last roundtrip failed the way a keep-alive connection the server
+  // closed while idle fails: EOF or a reset before any response byte, never
+  // a receive timeout. Only then may a pooled request be sent again.
+  bool failed_stale() const { return (fail_ == Fail::kEof || fail_ == Fail::kReset) && rx_bytes_ == 0; }
   // Unblocks a reader blocked in next_line() (from another thread).
   void shutdown();
 
@@ -84,6 +90,10 @@ class HttpConn {
   std::string buf_;      // received, not yet consumed
   size_t pos_ = 0;
   bool reusable_ = true;
+  enum class Fail { kNone, kEof, kReset, kTimeout, kOther };
+  Fail fail_ = Fail::kNone;
+  size_t rx_bytes_ = 0;  // bytes received since the current request was sent
+  void note_io_failure(ssize_t n);
   // streaming state
   bool stream_chunked_ = false;
   int64_t stream_left_ = -1;  // Content-Length stream: bytes left (-1: until close)

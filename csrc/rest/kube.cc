@@ -101,8 +101,9 @@ void ConnPool::throttle() {
 }
 
 Response ConnPool::call(const std::string& method, const std::string& path, const std::string& body,
-                        const std::string& content_type) {
+                        const std::string& content_type, bool* retried) {
   throttle();
+  if (retried) *retried = false;
   for (int attempt = 0;; ++attempt) {
     std::unique_ptr<HttpConn> c;
     bool pooled = false;
@@ -123,9 +124,11 @@ Response ConnPool::call(const std::string& method, const std::string& path, cons
       }
       return r;
     } catch (const std::runtime_error&) {
-      // A keep-alive connection the server closed while idle: retry once on
-      // a fresh one. A fresh connection failing is a real error.
-      if (!pooled || attempt > 0) throw;
+      // Only a keep-alive connection the server closed while idle is retried,
+      // once, on a fresh connection; anything else (a fresh connection, a
+      // timeout, bytes of a response already read) is the caller's error.
+      if (!pooled || attempt > 0 || !c->failed_stale()) throw;
+      if (retried) *retried = true;
     }
   }
 }
@@ -148,7 +151,23 @@ void RestApiClient::bind(const Pod& pod, const std::string& node, const Json& an
   b.set("metadata", std::move(md));
   b.set("target", std::move(target));
   requests_.fetch_add(1, std::memory_order_relaxed);
-  Response r = pool_.call("POST", object_path("pods", pod.ns(), pod.name(), "binding"), b.dump());
+  bool retried = false;
+  Response r = pool_.call("POST", object_path("pods", pod.ns(), pod.name(), "binding"), b.dump(), "application/json",
+                          &retried);
+  if (r.status == 409 && retried) {
+    // The first attempt may have been applied before its connection died:
+    // a pod already bound to this very node is this binding's success.
+    Response g = pool_.call("GET", object_path("pods", pod.ns(), pod.name()));
+    if (g.status == 200) {
+      try {
+        Json cur = Json::parse(g.body);
+        if (cur["spec"]["nodeName"].as_string() == node &&
+            (pod.uid().empty() || cur["metadata"]["uid"].as_string() == pod.uid()))
+          return;
+      } catch (const std::exception&) {
+      }
+    }
+  }
   if (r.status != 200 && r.status != 201) throw_status(r, "binding " + pod.ns() + "/" + pod.name());
 }
 

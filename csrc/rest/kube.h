@@ -39,10 +39,13 @@ std::string object_path(const std::string& kind, const std::string& ns, const st
 class ConnPool {
  public:
   explicit ConnPool(Endpoint ep);
-  // One request; a broken pooled connection is replaced and the request
-  // retried once (idempotence is the caller's concern, as with client-go).
+  // One request. A pooled connection that turns out to have been closed by
+  // the server while idle (EOF or reset before any response byte) is
+  // replaced and the request sent once more; `*retried` reports that. A
+  // receive timeout or a partial response is never retried: the server may
+  // have applied the request (a POST /binding must not be sent twice).
   Response call(const std::string& method, const std::string& path, const std::string& body = "",
-                const std::string& content_type = "application/json");
+                const std::string& content_type = "application/json", bool* retried = nullptr);
   const Endpoint& endpoint() const { return ep_; }
   std::shared_ptr<TlsContext> tls() const { return tls_; }
 

@@ -8,6 +8,7 @@
 
 #include "framework/framework.h"
 #include "framework/waiting_pods.h"
+#include "scheduler/extender.h"
 #include "scheduler/informers.h"
 #include "scheduler/metrics.h"
 #include "scheduler/queue.h"
@@ -247,6 +248,62 @@ Status Evaluator::prepare_candidate(const Candidate& c, const Pod& pod) {
   return {};
 }
 
+Status Evaluator::call_extenders(const Pod& pod, std::vector<Candidate>& cands) {
+  // preemption.go callExtenders: each interested extender with a preempt verb
+  // gets the current node -> victims map and returns the subset it accepts;
+  // the next extender sees that subset.
+  std::map<std::string, Extender::NodeVictims> victims;
+  for (const auto& c : cands) victims[c.node] = Extender::NodeVictims{c.victims, c.num_pdb_violations};
+  if (victims.empty()) return {};
+  Json pod_obj;
+  bool have_pod = false;
+  for (const auto& e : *h_.extenders) {
+    if (!e->supports_preemption() || !e->interested(pod)) continue;
+    if (!have_pod) {
+      JsonPtr obj = h_.lookup ? h_.lookup("pods", pod.ns(), pod.name()) : nullptr;
+      if (obj) {
+        pod_obj = *obj;
+      } else {
+        Json md = Json::object();
+        md.set("name", Json(pod.name()));
+        md.set("namespace", Json(pod.ns()));
+        md.set("uid", Json(pod.uid()));
+        pod_obj = Json::object();
+        pod_obj.set("metadata", std::move(md));
+      }
+      have_pod = true;
+    }
+    std::map<std::string, Extender::NodeVictims> got;
+    try {
+      got = e->process_preemption(pod_obj, victims, h_.lookup);
+    } catch (const std::exception& ex) {
+      if (e->ignorable()) continue;
+      return Status::error(ex.what());
+    }
+    for (auto it = got.begin(); it != got.end();) {
+      if (it->second.pods.empty()) {
+        if (!e->ignorable()) return Status::error("expected at least one victim pod on node " + it->first);
+        it = got.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    victims = std::move(got);
+    if (victims.empty()) break;
+  }
+  std::vector<Candidate> out;
+  out.reserve(victims.size());
+  for (auto& [node, v] : victims) {
+    Candidate c;
+    c.node = node;
+    c.victims = std::move(v.pods);
+    c.num_pdb_violations = static_cast<int>(v.num_pdb_violations);
+    out.push_back(std::move(c));
+  }
+  cands = std::move(out);
+  return {};
+}
+
 std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod& pod_in, const NodeStatusMap& m) {
   if (h_.metrics) h_.metrics->inc("scheduler_preemption_attempts_total", "");
   // 0) latest version of the pod
@@ -270,6 +327,12 @@ std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod&
   if (cands.empty())
     return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +
                                                       " nodes are available: no preemption victims found.")};
+  // 3) extenders with a preempt verb narrow the candidates
+  if (h_.extenders && !h_.extenders->empty()) {
+    Status est = call_extenders(pod, cands);
+    if (!est.is_success()) return {PostFilterResult{}, est};
+    if (cands.empty()) return {PostFilterResult{}, Status::unschedulable("no candidate node for preemption")};
+  }
   // 4) best candidate
   std::string node = pick_one_node(cands);
   const Candidate* best = nullptr;

@@ -53,6 +53,8 @@ class Evaluator {
   // prepareCandidate: reject waiting victims, delete the others, clear
   // lower-priority nominations on the node (also used by CrossNodePreemption).
   Status prepare_candidate(const Candidate& c, const Pod& pod);
+  // callExtenders: the configured preempt-verb extenders filter `cands`.
+  Status call_extenders(const Pod& pod, std::vector<Candidate>& cands);
 
  private:
   std::string plugin_;

@@ -177,6 +177,8 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     client_ = std::move(sc);
   }
 
+  for (const auto& ej : config["extenders"].items())
+    extenders_.push_back(std::make_shared<Extender>(ExtenderConfig::from_json(ej)));
   const auto& profiles = config["profiles"].items();
   if (profiles.empty()) throw std::runtime_error("scheduler config has no profiles");
   for (const auto& pj : profiles) {
@@ -196,6 +198,10 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.activate = [this](const std::vector<PodPtr>& pods) { queue_->activate(pods); };
     h.metrics = metrics_.get();
     h.snapshot = &snapshot_;
+    h.extenders = &extenders_;
+    h.lookup = [this](const std::string& kind, const std::string& ns, const std::string& name) {
+      return store_->get(kind, ns, name);
+    };
     frameworks_.push_back(std::make_unique<Framework>(pc, h));
     by_name_[pc.scheduler_name] = frameworks_.back().get();
   }
@@ -691,8 +697,30 @@ Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
   return e.get();
 }
 
+namespace {
+
+// "0/N nodes are available: k reason, ..." over a complete diagnosis.
+std::string fit_error_message(int n, const NodeStatusMap& m) {
+  std::map<std::string, int> reasons;
+  for (const auto& [node, st] : m)
+    for (const auto& r : st.reasons()) ++reasons[r];
+  std::string msg = "0/" + std::to_string(n) + " nodes are available:";
+  bool first = true;
+  for (const auto& kv : reasons) {
+    msg += (first ? " " : ", ") + std::to_string(kv.second) + " " + kv.first;
+    first = false;
+  }
+  return msg + ".";
+}
+
+}  // namespace
+
 Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, NodeList& feasible,
                                       EqEntry* eq, bool full_diagnosis, std::vector<int>* feasible_pos) {
+  // Extenders filter after the plugins; the diagnosis must then be complete,
+  // since the FitError may come from nodes only an extender rejected.
+  const bool ext = extenders_interested(p);
+  full_diagnosis = full_diagnosis || ext;
   int64_t pf0 = tracer_.enabled() ? clock_->now_us() : 0;
   Status st = fw.run_pre_filter(s, p);
   if (tracer_.enabled()) tracer_.record(TraceEvent{"prefilter", p.key(), "", pf0, clock_->now_us() - pf0, 0});
@@ -714,9 +742,14 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       if (nst.is_success()) {
         feasible.push_back(ni);
         if (feasible_pos) feasible_pos->push_back(static_cast<int>(it->second));
-        return {};
+        if (!ext) return {};
+        // evaluateNominatedNode: the extenders see the nominated node too;
+        // when they reject it the full search below runs.
+        Status es = run_extender_filters(p, feasible, feasible_pos, d);
+        if (!es.is_success() || !feasible.empty()) return es;
+      } else if (!nst.is_unschedulable()) {
+        return nst;
       }
-      if (!nst.is_unschedulable()) return nst;
     }
   }
   int n = static_cast<int>(all.size());
@@ -729,7 +762,10 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       if (feasible_pos) feasible_pos->push_back(pos);
     }
     next_start_node_ = (next_start_node_ + static_cast<int>(feasible.size())) % n;
-    return {};
+    if (!ext) return {};
+    Status es = run_extender_filters(p, feasible, feasible_pos, d);
+    if (!es.is_success() || !feasible.empty()) return es;
+    return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status));
   }
   // Filter verdicts are reused only when every Filter plugin is node-local for
   // this pod and no nominated pod can change a node's verdict.
@@ -903,7 +939,123 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     msg += ".";
     return Status(Code::Unschedulable, msg);
   }
+  if (!ext) return {};
+  Status es = run_extender_filters(p, feasible, feasible_pos, d);
+  if (!es.is_success() || !feasible.empty()) return es;
+  return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status));
+}
+
+bool Scheduler::extenders_interested(const Pod& p) const {
+  for (const auto& e : extenders_)
+    if (e->interested(p)) return true;
+  return false;
+}
+
+Json Scheduler::pod_object(const Pod& p) const {
+  if (JsonPtr obj = store_->get("pods", p.ns(), p.name())) return *obj;
+  Json md = Json::object();
+  md.set("name", Json(p.name()));
+  md.set("namespace", Json(p.ns()));
+  md.set("uid", Json(p.uid()));
+  Json o = Json::object();
+  o.set("apiVersion", Json("v1"));
+  o.set("kind", Json("Pod"));
+  o.set("metadata", std::move(md));
+  return o;
+}
+
+Status Scheduler::run_extender_filters(const Pod& p, NodeList& feasible, std::vector<int>* pos, Diagnosis& d) {
+  Json pod;
+  bool have_pod = false;
+  ObjectLookup lookup = [this](const std::string& kind, const std::string& ns, const std::string& name) {
+    return store_->get(kind, ns, name);
+  };
+  for (const auto& e : extenders_) {
+    if (feasible.empty()) break;
+    if (!e->interested(p) || !e->is_filter()) continue;
+    if (!have_pod) {
+      pod = pod_object(p);
+      have_pod = true;
+    }
+    std::vector<std::string> names;
+    names.reserve(feasible.size());
+    for (const auto* ni : feasible) names.push_back(ni->name());
+    Extender::FilterResult r;
+    try {
+      r = e->filter(pod, names, lookup);
+    } catch (const std::exception& ex) {
+      if (e->ignorable()) continue;  // "Skipping extender as it returned error and has ignorable flag set"
+      return Status::error(ex.what());
+    }
+    for (const auto& [node, msg] : r.unresolvable) {
+      std::vector<std::string> reasons;
+      auto it = d.node_to_status.find(node);
+      if (it != d.node_to_status.end()) reasons = it->second.reasons();
+      reasons.push_back(msg);
+      d.node_to_status[node] = Status(Code::UnschedulableAndUnresolvable, std::move(reasons));
+    }
+    for (const auto& [node, msg] : r.failed) {
+      if (r.unresolvable.count(node)) continue;  // unresolvable takes precedence
+      auto it = d.node_to_status.find(node);
+      if (it == d.node_to_status.end()) {
+        d.node_to_status[node] = Status(Code::Unschedulable, msg);
+      } else {
+        std::vector<std::string> reasons = it->second.reasons();
+        reasons.push_back(msg);
+        Status ns(it->second.code(), std::move(reasons));
+        if (!it->second.failed_plugin().empty()) ns.with_plugin(it->second.failed_plugin());
+        it->second = std::move(ns);
+      }
+    }
+    std::set<std::string> keep(r.nodes.begin(), r.nodes.end());
+    size_t w = 0;
+    for (size_t i = 0; i < feasible.size(); ++i) {
+      if (!keep.count(feasible[i]->name())) continue;
+      feasible[w] = feasible[i];
+      if (pos) (*pos)[w] = (*pos)[i];
+      ++w;
+    }
+    feasible.resize(w);
+    if (pos) pos->resize(w);
+  }
   return {};
+}
+
+void Scheduler::add_extender_scores(const Pod& p, const NodeList& feasible, std::vector<NodeScore>& scores,
+                                    Json* breakdown) {
+  std::vector<std::string> names;
+  std::unordered_map<std::string, int64_t> combined;
+  Json pod;
+  bool any = false;
+  ObjectLookup lookup = [this](const std::string& kind, const std::string& ns, const std::string& name) {
+    return store_->get(kind, ns, name);
+  };
+  for (const auto& e : extenders_) {
+    if (!e->interested(p) || !e->is_prioritizer()) continue;
+    if (!any) {
+      pod = pod_object(p);
+      names.reserve(feasible.size());
+      for (const auto* ni : feasible) names.push_back(ni->name());
+      any = true;
+    }
+    try {
+      for (const auto& [host, score] : e->prioritize(pod, names, lookup)) {
+        combined[host] += score * e->config().weight;
+        if (breakdown) {
+          Json& node = breakdown->at_or_create(host);
+          node.set(e->name(), Json(score));
+        }
+      }
+    } catch (const std::exception&) {
+      // "Prioritization errors from extender can be ignored, let k8s/other
+      // extenders determine the priorities" (generic_scheduler.go:460-463)
+    }
+  }
+  if (!any) return;
+  for (size_t i = 0; i < feasible.size(); ++i) {
+    auto it = combined.find(feasible[i]->name());
+    if (it != combined.end()) scores[i].score += it->second * (kMaxNodeScore / kMaxExtenderPriority);
+  }
 }
 
 size_t Scheduler::select_host(const std::vector<NodeScore>& scores) {
@@ -992,8 +1144,11 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     } else {
       std::vector<NodeScore>& scores = scores_buf_;
       if (!fw->has(kScore)) {
+        // No score plugins: every node 1, unless extenders score (then 0 +
+        // their priorities, generic_scheduler.go:408-416).
+        const bool ext_scores = extenders_interested(*pod);
         scores.assign(feasible.size(), NodeScore{});
-        for (auto& sc : scores) sc.score = 1;
+        for (auto& sc : scores) sc.score = ext_scores ? 0 : 1;
         st = Status();
       } else {
         st = fw->run_pre_score(*state, *pod, feasible);
@@ -1006,6 +1161,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         }
         if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores, nullptr, esc.local.empty() ? nullptr : &esc);
       }
+      if (st.is_success() && !extenders_.empty()) add_extender_scores(*pod, feasible, scores);
       if (st.is_success()) host = feasible[select_host(scores)]->name();
     }
   }
@@ -1210,10 +1366,13 @@ Json Scheduler::explain(const Json& pod_obj) {
     Status ps = fw->run_pre_score(*state, *pod, feasible);
     if (ps.is_success()) ps = fw->run_score(*state, *pod, feasible, scores, &bd);
     if (ps.is_success()) {
+      Json ext = Json::object();
+      if (!extenders_.empty()) add_extender_scores(*pod, feasible, scores, &ext);
       Json sc = Json::object();
       for (size_t i = 0; i < feasible.size(); ++i) {
         Json node = Json::object();
         for (const auto& [plugin, vals] : bd) node.set(plugin, Json(vals[i]));
+        if (const Json* e = ext.get(feasible[i]->name())) node.set("extenders", *e);
         node.set("total", Json(scores[i].score));
         sc.set(feasible[i]->name(), std::move(node));
       }
@@ -1321,7 +1480,24 @@ void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
     fail(st, "SchedulerError");
     return;
   }
-  st = fw->run_bind(*s, assumed, host);
+  // extendersBinding (scheduler.go bind()): the first interested binder
+  // extender binds instead of the Bind plugins.
+  Extender* binder = nullptr;
+  for (const auto& e : extenders_)
+    if (e->is_binder() && e->interested(*assumed)) {
+      binder = e.get();
+      break;
+    }
+  if (binder) {
+    try {
+      binder->bind(assumed->ns(), assumed->name(), assumed->uid(), host);
+      st = Status();
+    } catch (const std::exception& ex) {
+      st = Status::error(std::string("extender ") + binder->name() + " bind: " + ex.what());
+    }
+  } else {
+    st = fw->run_bind(*s, assumed, host);
+  }
   if (st.is_skip()) st = Status(Code::Error, "no bind plugin bound the pod");
   if (!st.is_success()) {
     fail(st, "SchedulerError");

@@ -28,6 +28,7 @@
 #include "common/parallel.h"
 #include "framework/framework.h"
 #include "scheduler/cache.h"
+#include "scheduler/extender.h"
 #include "scheduler/informers.h"
 #include "scheduler/metrics.h"
 #include "scheduler/queue.h"
@@ -219,6 +220,15 @@ class Scheduler {
   Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, NodeList& feasible,
                              EqEntry* eq = nullptr, bool full_diagnosis = false, std::vector<int>* feasible_pos = nullptr);
   int num_feasible_nodes_to_find(Framework& fw, int n) const;
+  // findNodesThatPassExtenders: interested filter extenders narrow
+  // `feasible` (and `pos`) in order; their failures join the diagnosis.
+  Status run_extender_filters(const Pod& p, NodeList& feasible, std::vector<int>* pos, Diagnosis& d);
+  // Extender priorities x weight x (MaxNodeScore / MaxExtenderPriority)
+  // added to the plugin totals; errors are ignored as upstream does.
+  void add_extender_scores(const Pod& p, const NodeList& feasible, std::vector<NodeScore>& scores,
+                           Json* breakdown = nullptr);
+  bool extenders_interested(const Pod& p) const;
+  Json pod_object(const Pod& p) const;  // the informer store's Pod (what extenders receive)
   // Index of the highest total (reservoir-sampled among ties).
   size_t select_host(const std::vector<NodeScore>& scores);
   // Cycle scratch reused across cycles (scheduling thread only).
@@ -261,6 +271,7 @@ class Scheduler {
   std::unique_ptr<Nominator> nominator_;
   std::unique_ptr<SchedulingQueue> queue_;
   std::shared_ptr<ApiClient> client_;
+  ExtenderList extenders_;
   std::vector<std::unique_ptr<WaitingPods>> waiting_;
   std::vector<std::unique_ptr<Framework>> frameworks_;
   std::unordered_map<std::string, Framework*> by_name_;

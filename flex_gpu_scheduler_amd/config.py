@@ -15,13 +15,22 @@ Semantics reproduced:
     point plugins first, then the multiPoint plugins implementing it);
   * plugin args defaults of apis/config/v1beta2/defaults.go:28-157
     (identical in v1beta3) and upstream DefaultPreemptionArgs;
-  * strict decoding: unknown args fields are errors (scheme.go:35 uses the
-    strict codec).
+  * strict decoding: unknown fields are errors, at the top level, in
+    leaderElection / clientConnection / profiles / plugin sets / extenders
+    and in every plugin's args (apis/config/scheme/scheme.go:35 uses the
+    strict codec);
+  * extenders (kube-scheduler/config/v1beta{2,3} Extender): validated as
+    validation.go validateExtenders does (positive weight with a prioritize
+    verb, at most one binder, unique extended managedResources), ignorable
+    extenders moved to the tail and ignoredByScheduler resources written into
+    every profile's NodeResourcesFit ignoredResources (factory.go:90-130).
 """
 from __future__ import annotations
 
+import base64
 import copy
 import json
+import re
 from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Any
@@ -99,6 +108,150 @@ V1BETA3_MULTIPOINT: list[tuple[str, int]] = [
 
 class ConfigError(ValueError):
     pass
+
+
+# Top-level fields of KubeSchedulerConfiguration (kube-scheduler/config/
+# v1beta{2,3}/types.go; DebuggingConfiguration is inlined). v1beta3 dropped
+# the two bind addresses.
+_TOP_FIELDS = {"apiVersion", "kind", "parallelism", "leaderElection", "clientConnection", "enableProfiling",
+               "enableContentionProfiling", "percentageOfNodesToScore", "podInitialBackoffSeconds",
+               "podMaxBackoffSeconds", "profiles", "extenders"}
+_V1BETA2_ONLY = {"healthzBindAddress", "metricsBindAddress"}
+_LEADER_FIELDS = {"leaderElect", "leaseDuration", "renewDeadline", "retryPeriod", "resourceLock", "resourceName",
+                  "resourceNamespace"}
+_CLIENT_FIELDS = {"kubeconfig", "acceptContentTypes", "contentType", "qps", "burst"}
+# percentageOfNodesToScore per profile is an extension of this scheduler
+# (upstream added it in v1); the rest is KubeSchedulerProfile.
+_PROFILE_FIELDS = {"schedulerName", "plugins", "pluginConfig", "percentageOfNodesToScore"}
+_EXTENDER_FIELDS = {"urlPrefix", "filterVerb", "preemptVerb", "prioritizeVerb", "weight", "bindVerb", "enableHTTPS",
+                    "tlsConfig", "httpTimeout", "nodeCacheCapable", "managedResources", "ignorable"}
+_EXTENDER_TLS_FIELDS = {"insecure", "serverName", "certFile", "keyFile", "caFile", "certData", "keyData", "caData"}
+
+
+def _strict_fields(where: str, obj: Any, allowed: set[str]) -> None:
+    if obj is None:
+        return
+    if not isinstance(obj, dict):
+        raise ConfigError(f"{where}: expected an object, got {type(obj).__name__}")
+    extra = set(obj) - allowed
+    if extra:
+        raise ConfigError("strict decoding error: " + ", ".join(
+            f'unknown field "{where + "." if where else ""}{f}"' for f in sorted(extra)))
+
+
+_DURATION = re.compile(r"(\d+(?:\.\d*)?|\.\d+)(ns|us|µs|ms|s|m|h)")
+
+
+def parse_duration_ms(v: Any, where: str) -> int:
+    """metav1.Duration (Go time.ParseDuration syntax, e.g. "30s", "1m30s",
+    "250ms") -> milliseconds. A bare number is taken as seconds."""
+    if v is None or v == "":
+        return 0
+    if isinstance(v, (int, float)):
+        return int(float(v) * 1000)
+    s = str(v).strip()
+    if s in ("0", "0s"):
+        return 0
+    scale = {"ns": 1e-6, "us": 1e-3, "µs": 1e-3, "ms": 1.0, "s": 1e3, "m": 60e3, "h": 3600e3}
+    pos, total = 0, 0.0
+    for m in _DURATION.finditer(s):
+        if m.start() != pos:
+            break
+        total += float(m.group(1)) * scale[m.group(2)]
+        pos = m.end()
+    if pos != len(s) or pos == 0:
+        raise ConfigError(f"{where}: invalid duration {v!r}")
+    return int(round(total))
+
+
+_QUALIFIED = re.compile(r"^([a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*)/"
+                        r"([A-Za-z0-9]([-A-Za-z0-9_.]*[A-Za-z0-9])?)$")
+
+
+def _extended_resource_name(name: str) -> bool:
+    """validateExtendedResourceName: a domain-prefixed name outside
+    kubernetes.io that is not a requests.* quota name."""
+    m = _QUALIFIED.match(name or "")
+    if not m:
+        return False
+    domain = m.group(1)
+    if domain == "kubernetes.io" or domain.endswith(".kubernetes.io"):
+        return False
+    return not name.startswith("requests.")
+
+
+def _pem(v: Any, where: str) -> str:
+    """[]byte fields arrive base64-encoded (JSON/YAML of a Go byte slice)."""
+    if not v:
+        return ""
+    try:
+        return base64.b64decode(str(v), validate=True).decode()
+    except Exception as e:  # noqa: BLE001
+        raise ConfigError(f"{where}: not base64 data: {e}") from None
+
+
+def resolve_extenders(raw: Any) -> tuple[list[dict], list[str]]:
+    """Validated, defaulted extenders (non-ignorable first) and the resources
+    they ask the scheduler to ignore."""
+    if raw is None:
+        return [], []
+    if not isinstance(raw, list):
+        raise ConfigError("extenders must be a list")
+    out, ignorable, ignored, seen = [], [], [], set()
+    binders = 0
+    for i, e in enumerate(raw):
+        where = f"extenders[{i}]"
+        _strict_fields(where, e, _EXTENDER_FIELDS)
+        if not isinstance(e, dict) or not e.get("urlPrefix"):
+            raise ConfigError(f"{where}.urlPrefix: required")
+        url = str(e["urlPrefix"])
+        if not (url.startswith("http://") or url.startswith("https://")):
+            raise ConfigError(f"{where}.urlPrefix: must be an http:// or https:// URL, got {url!r}")
+        weight = int(e.get("weight") or 0)
+        if e.get("prioritizeVerb") and weight <= 0:
+            raise ConfigError(f"{where}.weight: Invalid value: {weight}: must have a positive weight applied to it")
+        if e.get("bindVerb"):
+            binders += 1
+        managed = []
+        for j, r in enumerate(e.get("managedResources") or []):
+            _strict_fields(f"{where}.managedResources[{j}]", r, {"name", "ignoredByScheduler"})
+            name = str((r or {}).get("name", ""))
+            if not _extended_resource_name(name):
+                raise ConfigError(f"{where}.managedResources[{j}].name: Invalid value: {name!r}: "
+                                  "must be a fully qualified extended resource name")
+            if name in seen:
+                raise ConfigError(f"{where}.managedResources[{j}].name: Invalid value: {name!r}: "
+                                  "duplicate extender managed resource name")
+            seen.add(name)
+            managed.append({"name": name, "ignoredByScheduler": bool(r.get("ignoredByScheduler", False))})
+            if r.get("ignoredByScheduler"):
+                ignored.append(name)
+        tls = e.get("tlsConfig") or {}
+        _strict_fields(f"{where}.tlsConfig", tls, _EXTENDER_TLS_FIELDS)
+        ext = {
+            "urlPrefix": url,
+            "filterVerb": str(e.get("filterVerb") or ""),
+            "preemptVerb": str(e.get("preemptVerb") or ""),
+            "prioritizeVerb": str(e.get("prioritizeVerb") or ""),
+            "bindVerb": str(e.get("bindVerb") or ""),
+            "weight": weight,
+            "enableHTTPS": bool(e.get("enableHTTPS", False)),
+            "nodeCacheCapable": bool(e.get("nodeCacheCapable", False)),
+            "ignorable": bool(e.get("ignorable", False)),
+            "managedResources": managed,
+            "httpTimeoutMs": parse_duration_ms(e.get("httpTimeout"), f"{where}.httpTimeout"),
+            "tlsConfig": {"insecure": bool(tls.get("insecure", False)), "serverName": str(tls.get("serverName") or ""),
+                          "certFile": str(tls.get("certFile") or ""), "keyFile": str(tls.get("keyFile") or ""),
+                          "caFile": str(tls.get("caFile") or ""),
+                          "certData": _pem(tls.get("certData"), f"{where}.tlsConfig.certData"),
+                          "keyData": _pem(tls.get("keyData"), f"{where}.tlsConfig.keyData"),
+                          "caData": _pem(tls.get("caData"), f"{where}.tlsConfig.caData")},
+        }
+        (ignorable if ext["ignorable"] else out).append(ext)
+    if binders > 1:
+        raise ConfigError(f"extenders: Invalid value: \"found {binders} extenders implementing bind\": "
+                          "only one extender can implement bind")
+    return out + ignorable, ignored
 
 
 # ----------------------------------------------------------------- args ----
@@ -278,6 +431,7 @@ class SchedulerConfiguration:
     status_updates: bool = True
     trace: bool = False
     api_version: str = API_VERSIONS[0]
+    extenders: list[dict] = field(default_factory=list)
     raw: dict = field(default_factory=dict)
 
     def to_native(self, **overrides) -> dict:
@@ -291,7 +445,7 @@ class SchedulerConfiguration:
             "trace": self.trace,
         }
         opts.update(overrides)
-        return {"profiles": [p.to_native() for p in self.profiles], "options": opts}
+        return {"profiles": [p.to_native() for p in self.profiles], "options": opts, "extenders": self.extenders}
 
     def profile(self, name: str) -> Profile:
         for p in self.profiles:
@@ -351,6 +505,7 @@ def _resolve_profile(p: dict, api_version: str, available: set[str] | None, inde
     point with "*" disabled gets no multiPoint plugins. Score weights: an
     explicit score entry wins, else the multiPoint weight, 0 meaning 1.
     """
+    _strict_fields(f"profiles[{index}]", p, _PROFILE_FIELDS)
     prof = Profile(scheduler_name=p.get("schedulerName") or "default-scheduler")
     if "percentageOfNodesToScore" in p and p["percentageOfNodesToScore"] is not None:
         prof.percentage_of_nodes_to_score = int(p["percentageOfNodesToScore"])
@@ -358,6 +513,12 @@ def _resolve_profile(p: dict, api_version: str, available: set[str] | None, inde
     unknown = set(spec) - set(EXT_POINTS) - {"multiPoint"}
     if unknown:
         raise ConfigError(f"unknown extension point(s) {sorted(unknown)}")
+    for pt, ps in spec.items():
+        _strict_fields(f"profiles[{index}].plugins.{pt}", ps, {"enabled", "disabled"})
+        for k in ("enabled", "disabled"):
+            for j, e in enumerate((ps or {}).get(k) or []):
+                if isinstance(e, dict):
+                    _strict_fields(f"profiles[{index}].plugins.{pt}.{k}[{j}]", e, {"name", "weight"})
     v1beta3 = api_version.endswith("v1beta3")
     if "multiPoint" in spec and not v1beta3:
         raise ConfigError("multiPoint requires kubescheduler.config.k8s.io/v1beta3")
@@ -399,6 +560,7 @@ def _resolve_profile(p: dict, api_version: str, available: set[str] | None, inde
     prof.plugins = resolved
     prof.score_weights = weights
     for j, pc in enumerate(p.get("pluginConfig") or []):
+        _strict_fields(f"profiles[{index}].pluginConfig[{j}]", pc, {"name", "args"})
         name = pc.get("name")
         if not name:
             raise ConfigError("pluginConfig entry without name")
@@ -439,6 +601,10 @@ def load_config(src: str | Path | dict | None = None, *, restrict_to_native: boo
         raise ConfigError(f"unsupported apiVersion {api!r}")
     if doc.get("kind", "KubeSchedulerConfiguration") != "KubeSchedulerConfiguration":
         raise ConfigError(f"unsupported kind {doc.get('kind')!r}")
+    _strict_fields("", doc, _TOP_FIELDS | (_V1BETA2_ONLY if api.endswith("v1beta2") else set()))
+    _strict_fields("leaderElection", doc.get("leaderElection"), _LEADER_FIELDS)
+    _strict_fields("clientConnection", doc.get("clientConnection"), _CLIENT_FIELDS)
+    extenders, ignored = resolve_extenders(doc.get("extenders"))
     available = _available_plugins() if restrict_to_native else None
     profiles_raw = doc.get("profiles") or [{"schedulerName": "default-scheduler"}]
     profiles = [_resolve_profile(p, api, available, i) for i, p in enumerate(profiles_raw)]
@@ -448,7 +614,13 @@ def load_config(src: str | Path | dict | None = None, *, restrict_to_native: boo
     qs = {tuple(p.plugins.get("queueSort", [])) for p in profiles}
     if len(qs) > 1:
         raise ConfigError("all profiles must use the same queueSort plugin")
-    cfg = SchedulerConfiguration(profiles=profiles, api_version=api, raw=doc)
+    if ignored:
+        # factory.go:112-130: the extenders' ignoredByScheduler resources
+        # replace every profile's NodeResourcesFit ignoredResources.
+        for prof in profiles:
+            if "NodeResourcesFit" in prof.plugin_config:
+                prof.plugin_config["NodeResourcesFit"]["ignoredResources"] = list(ignored)
+    cfg = SchedulerConfiguration(profiles=profiles, api_version=api, extenders=extenders, raw=doc)
     if doc.get("parallelism") is not None:
         cfg.parallelism = int(doc["parallelism"])
         if cfg.parallelism <= 0:

@@ -1,6 +1,6 @@
 """Run one HIP probe kernel family in isolation (for rocprofv3 --pmc passes).
 
-    python -m flex_gpu_scheduler_amd.tools.probe_kernels PROBE [device]
+    python -m flex_gpu_scheduler_amd.tools.probe_kernels PROBE [device] [iters]
 
     PROBE: mfma | hbm-read | hbm-copy | hbm-triad | hbm-write
            | xcd-read-K | xcd-copy-K   (k_pinned on the first K XCDs: K=1 is
@@ -20,20 +20,21 @@ from ..ops.hip_probe import probe
 def main() -> int:
     what = sys.argv[1] if len(sys.argv) > 1 else "mfma"
     dev = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     pr = probe()
     if what == "mfma":
         r = pr.mfma_peak(dev, 0xFF, iters=8192)
         out = {"kernel": "k_mfma_peak", "TFLOPs": round(r["tflops"], 1), "ms": round(r["ms"], 3)}
     elif what in ("hbm-read", "hbm-copy", "hbm-triad", "hbm-write"):
-        bw = pr.hbm_bandwidth(dev, 2 << 30, iters=5, mode=what.split("-")[1])
+        bw = pr.hbm_bandwidth(dev, 2 << 30, iters=iters, mode=what.split("-")[1])
         arrays = {"read": 1, "write": 1, "copy": 2, "triad": 3}[what.split("-")[1]]
-        out = {"kernel": what, "bytes_per_array": 2 << 30, "arrays": arrays, "GBps": round(bw.gbps, 1),
+        out = {"kernel": what, "iters": iters, "bytes_per_array": 2 << 30, "arrays": arrays, "GBps": round(bw.gbps, 1),
                "ms": round(bw.ms_per_iter, 4), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
     elif what.startswith("xcd-"):
         _, mode, k = what.split("-")
         mask = (1 << int(k)) - 1
-        bw = pr.hbm_bandwidth_xcd(dev, mask, 1 << 30, iters=5, mode=mode)
-        out = {"kernel": f"k_pinned[{mode}]", "xcds": int(k), "xcd_mask": mask, "bytes": 1 << 30,
+        bw = pr.hbm_bandwidth_xcd(dev, mask, 1 << 30, iters=iters, mode=mode)
+        out = {"kernel": f"k_pinned[{mode}]", "iters": iters, "xcds": int(k), "xcd_mask": mask, "bytes": 1 << 30,
                "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
     else:
         raise SystemExit(f"unknown probe {what!r}")
