@@ -218,15 +218,42 @@ class Coscheduling : public Plugin {
   // denied after its last member arrived (e.g. a Permit timeout breaking a
   // gang deadlock at full capacity) waits for the unschedulable-queue flush
   // (60 s): no cluster event is left to requeue it.
+  // One requeue timer per group at a time: Unreserve runs once per rejected
+  // member, so a gang denial calls deny() k times; later calls only push the
+  // pending timer's deadline (it re-arms itself for the remainder).
   void deny(const Pod& p) {
     denied_.add(p.pg_key, denied_ttl_us_);
     if (!h_.timers || !h_.activate) return;
+    const int64_t due = h_.clock->now_us() + denied_ttl_us_ + 1000;
+    {
+      std::lock_guard<std::mutex> g(requeue_mu_);
+      auto [it, fresh] = requeue_due_.try_emplace(p.pg_key, due);
+      if (!fresh) {
+        it->second = std::max(it->second, due);
+        return;
+      }
+    }
     auto member = std::make_shared<Pod>();
     member->meta.ns = p.ns();
     member->pod_group = p.pod_group;
     member->pg_key = p.pg_key;
-    h_.timers->schedule_after(denied_ttl_us_ + 1000, [this, member] {
-      if (denied_.has(member->pg_key)) return;  // denied again since: that denial's timer retries
+    arm_requeue(member, denied_ttl_us_ + 1000);
+  }
+
+  void arm_requeue(const std::shared_ptr<Pod>& member, int64_t after_us) {
+    h_.timers->schedule_after(after_us, [this, member] {
+      {
+        std::lock_guard<std::mutex> g(requeue_mu_);
+        auto it = requeue_due_.find(member->pg_key);
+        if (it == requeue_due_.end()) return;
+        int64_t left = it->second - h_.clock->now_us();
+        if (left > 0) {  // denied again meanwhile: wait out the newest denial
+          arm_requeue(member, left);
+          return;
+        }
+        requeue_due_.erase(it);
+      }
+      if (denied_.has(member->pg_key)) return;
       std::vector<PodPtr> pods;
       for (auto& q : h_.informers->pods_in_group_of(*member))
         if (q->node_name.empty()) pods.push_back(std::move(q));
@@ -319,6 +346,8 @@ class Coscheduling : public Plugin {
  private:
   Handle& h_;
   TTLSet denied_, permitted_;
+  std::mutex requeue_mu_;
+  std::unordered_map<uint64_t, int64_t> requeue_due_;  // pg_key -> when its pending requeue timer fires
   int64_t permit_wait_us_ = 60'000'000;
   int64_t denied_ttl_us_ = 20'000'000;
   uint64_t sweep_id_ = 0;

@@ -104,6 +104,7 @@ class NodeResourcesFit : public Plugin {
     weights_ = parse_weights(ss["resources"], {{kCPU, 1}, {kMemory, 1}});
     for (const auto& pt : ss["requestedToCapacityRatio"]["shape"].items())
       shape_.emplace_back(pt["utilization"].as_int(), pt["score"].as_int());
+    unresolvable_beyond_allocatable_ = args["unresolvableBeyondAllocatable"].as_bool(false);
   }
 
   bool ignored(int id) const {
@@ -137,10 +138,11 @@ class NodeResourcesFit : public Plugin {
       int64_t free = ni.allocatable.get(i) - ni.requested.get(i);
       if (want > free) {
         fail |= 1ull << i;
-        // More than the node has at all: evicting pods cannot help, so the
-        // verdict is unresolvable and preemption skips the node (newer
-        // upstream NodeResourcesFit does the same).
-        if (want > ni.allocatable.get(i)) fail |= kBeyondAllocatable;
+        // More than the node has at all: evicting pods cannot help. Opt-in
+        // (unresolvableBeyondAllocatable), the verdict is then unresolvable
+        // and preemption skips the node, as newer upstream does; k8s 1.23,
+        // the reference's version, always says Unschedulable.
+        if (unresolvable_beyond_allocatable_ && want > ni.allocatable.get(i)) fail |= kBeyondAllocatable;
       }
     }
     if (!fail) return {};
@@ -195,6 +197,7 @@ class NodeResourcesFit : public Plugin {
   }
   std::vector<int> ignored_;
   std::vector<std::string> ignored_groups_;
+  bool unresolvable_beyond_allocatable_ = false;
   std::string strategy_;
   std::vector<ResourceWeight> weights_;
   std::vector<std::pair<int64_t, int64_t>> shape_;

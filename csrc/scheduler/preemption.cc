@@ -122,9 +122,8 @@ std::vector<NodeInfoPtr> nodes_where_preemption_might_help(const Snapshot& snap,
   for (const auto& kv : m)
     if (kv.second.code() == Code::UnschedulableAndUnresolvable) ++unresolvable;
   if (unresolvable == 0) return snap.nodes;
-  // Every node of the snapshot failed unresolvably (m holds one entry per
-  // failed node): nothing to try.
-  if (unresolvable == m.size() && m.size() >= snap.nodes.size()) return {};
+  // The map may carry names outside this snapshot (a PostFilter handed a map
+  // built elsewhere), so a node is only skipped on its own unresolvable entry.
   std::vector<NodeInfoPtr> out;
   out.reserve(snap.nodes.size());
   for (const auto& ni : snap.nodes) {

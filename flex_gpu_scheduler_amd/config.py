@@ -368,7 +368,11 @@ def default_plugin_args(name: str, args: dict | None) -> dict:
         a.setdefault("indexAnnotationKey", "amd.com/gpu-index")
         a.setdefault("partitionAnnotationKey", "amd.com/gpu-partitions")
     elif name == "NodeResourcesFit":
-        _strict(name, a, {"ignoredResources", "ignoredResourceGroups", "scoringStrategy"})
+        # unresolvableBeyondAllocatable is an extension (default off = k8s
+        # 1.23): a request above the node's allocatable fails the node as
+        # UnschedulableAndUnresolvable, so preemption does not try it.
+        _strict(name, a, {"ignoredResources", "ignoredResourceGroups", "scoringStrategy",
+                          "unresolvableBeyondAllocatable"})
         ss = dict(a.get("scoringStrategy") or {})
         ss.setdefault("type", "LeastAllocated")
         ss["resources"] = _resource_specs(ss.get("resources"), name) or [

@@ -2,6 +2,7 @@
 mirror RemoteScheduler uses against a REST endpoint. Bindings carry the
 FlexGPU annotations, a relist drops objects deleted while not watching, and
 TLS (server-verified and mutual) works end to end."""
+import json
 import shutil
 import time
 
@@ -176,3 +177,124 @@ def test_native_writer_honours_client_connection_qps(store):
             rs.stop()
     finally:
         srv.stop()
+
+
+class _BindServer:
+    """A scripted API server for POST .../binding: `script` lists, per
+    binding request, "ok", "stall" (no answer past the client's timeout),
+    "ok_close" (answer, then drop the keep-alive connection without saying
+    so), "apply_drop" (apply the binding, drop the connection unanswered) or
+    "conflict" (409, the pod is already bound)."""
+
+    def __init__(self, script):
+        import http.server
+        import threading
+
+        self.script = list(script)
+        self.posts = 0
+        self.bound: dict[str, str] = {}
+        srv = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def _send(self, code, obj):
+                data = json.dumps(obj).encode()
+                self.send_response(code)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(data)))
+                self.end_headers()
+                self.wfile.write(data)
+
+            def do_POST(self):  # noqa: N802
+                body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+                srv.posts += 1
+                step = srv.script.pop(0) if srv.script else "ok"
+                name, node = body["metadata"]["name"], body["target"]["name"]
+                if step == "stall":
+                    time.sleep(1.5)
+                    self.close_connection = True
+                    return
+                if step == "apply_drop":
+                    srv.bound[name] = node
+                    self.close_connection = True
+                    return
+                if step == "conflict" or name in srv.bound:
+                    self._send(409, {"kind": "Status", "code": 409, "reason": "Conflict",
+                                     "message": f"pod {name} is already assigned to node {srv.bound.get(name)}"})
+                    return
+                srv.bound[name] = node
+                self._send(201, {"kind": "Status", "status": "Success"})
+                if step == "ok_close":
+                    self.close_connection = True
+
+            def do_GET(self):  # noqa: N802
+                name = self.path.rsplit("/", 1)[-1]
+                self._send(200, {"metadata": {"name": name, "namespace": "default", "uid": f"uid-{name}"},
+                                 "spec": {"nodeName": srv.bound.get(name, "")}})
+
+            def log_message(self, *a):
+                pass
+
+        import http.server as hs
+
+        self.httpd = hs.ThreadingHTTPServer(("127.0.0.1", 0), H)
+        threading.Thread(target=self.httpd.serve_forever, daemon=True).start()
+        self.port = self.httpd.server_address[1]
+
+    def client(self, timeout_ms=30000):
+        return native().RestApiClient(native().RestEndpoint("127.0.0.1", self.port, timeout_ms=timeout_ms))
+
+    def close(self):
+        self.httpd.shutdown()
+        self.httpd.server_close()
+
+
+def _pod(name):
+    return {"metadata": {"name": name, "namespace": "default", "uid": f"uid-{name}"}, "spec": {}}
+
+
+def test_binding_is_not_resent_after_a_receive_timeout():
+    """A binding whose answer does not arrive in time may have been applied:
+    it is reported as failed, never sent again on another connection
+    (ConnPool retried any error of a pooled connection)."""
+    srv = _BindServer(["ok", "stall"])
+    try:
+        c = srv.client(timeout_ms=300)
+        c.bind_json(_pod("a"), "n0")  # leaves a pooled keep-alive connection
+        with pytest.raises(Exception):
+            c.bind_json(_pod("b"), "n0")
+        time.sleep(1.6)
+        assert srv.posts == 2  # no retry of "b"
+    finally:
+        srv.close()
+
+
+def test_stale_keepalive_connection_is_retried_once():
+    srv = _BindServer(["ok_close", "ok"])
+    try:
+        c = srv.client()
+        c.bind_json(_pod("a"), "n0")
+        time.sleep(0.1)  # the server has closed the pooled connection
+        c.bind_json(_pod("b"), "n1")
+        assert srv.bound == {"a": "n0", "b": "n1"} and srv.posts == 2
+    finally:
+        srv.close()
+
+
+def test_retried_binding_conflict_on_same_node_is_success():
+    """The first attempt was applied but its connection died unanswered: the
+    retry gets 409 'already assigned', and the pod bound to the same node
+    makes that binding a success."""
+    srv = _BindServer(["ok", "apply_drop"])
+    try:
+        c = srv.client()
+        c.bind_json(_pod("a"), "n0")
+        c.bind_json(_pod("b"), "n1")  # apply_drop, then the retry conflicts
+        assert srv.bound["b"] == "n1" and srv.posts == 3
+        # A conflict with another node is still an error.
+        srv.script = ["conflict"]
+        with pytest.raises(Exception):
+            c.bind_json(_pod("c"), "n2")
+    finally:
+        srv.close()

@@ -120,24 +120,31 @@ def test_preemption_toleration_seconds_window(store):
         s.stop()
 
 
-def test_request_beyond_allocatable_is_unresolvable(store):
-    """A request larger than a node's allocatable cannot be met by evicting
-    pods: NodeResourcesFit says UnschedulableAndUnresolvable there, so
-    preemption does not dry-run that node; a node that is merely full stays
-    Unschedulable (a preemption candidate)."""
+def test_request_beyond_allocatable_verdict(store):
+    """k8s 1.23 (the reference's version) reports a request larger than a
+    node's allocatable as plain Unschedulable, so that node stays a
+    preemption candidate. The opt-in NodeResourcesFit extension
+    unresolvableBeyondAllocatable makes it UnschedulableAndUnresolvable
+    (evicting pods cannot help; newer upstream does this); a node that is
+    merely full stays Unschedulable either way."""
     from flex_gpu_scheduler_amd import load_config, new_scheduler
     from flex_gpu_scheduler_amd.models import make_node, make_pod
 
     store.create("nodes", make_node("small", {"cpu": "4", "memory": "8Gi", "pods": "10"}))
     store.create("nodes", make_node("big", {"cpu": "16", "memory": "8Gi", "pods": "10"}))
     store.create("pods", make_pod("filler", requests={"cpu": "12"}, node_name="big"))
-    s = new_scheduler(store, load_config(None))
-    s.sync_informers(50)
-    out = s.explain(make_pod("p", requests={"cpu": "8"}))
-    assert out["filtered"]["small"]["code"] == "UnschedulableAndUnresolvable"
-    assert out["filtered"]["big"]["code"] == "Unschedulable"
-    assert "Insufficient cpu" in out["filtered"]["small"]["reason"]
-    s.stop()
+    for opt_in, small_code in ((False, "Unschedulable"), (True, "UnschedulableAndUnresolvable")):
+        cfg = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration"}
+        if opt_in:
+            cfg["profiles"] = [{"pluginConfig": [{"name": "NodeResourcesFit",
+                                                  "args": {"unresolvableBeyondAllocatable": True}}]}]
+        s = new_scheduler(store, load_config(cfg))
+        s.sync_informers(50)
+        out = s.explain(make_pod("p", requests={"cpu": "8"}))
+        assert out["filtered"]["small"]["code"] == small_code
+        assert out["filtered"]["big"]["code"] == "Unschedulable"
+        assert "Insufficient cpu" in out["filtered"]["small"]["reason"]
+        s.stop()
 
 
 def _nominated(name, node, **kw):
