@@ -7,6 +7,8 @@
 #include <mutex>
 #include <unordered_set>
 
+#include "api/storage.h"
+
 namespace xsched {
 
 // ---------------------------------------------------------------- time ----
@@ -377,6 +379,7 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
     p->containers = std::move(cs);
     p->init_containers = std::move(ics);
   }
+  p->volumes = parse_pod_volumes(spec, p->meta.name);
   p->overhead = Res::from_json(spec["overhead"]);
   p->node_selector = strmap_from_json(spec["nodeSelector"]);
   if (const Json* na = spec.path({"affinity", "nodeAffinity"})) {

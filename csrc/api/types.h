@@ -96,6 +96,23 @@ struct Container {
   std::vector<ContainerPort> ports;
 };
 
+// In-tree volume sources that count against per-node attach limits or can
+// conflict between pods (VolumeRestrictions, the non-CSI limits plugins).
+enum class InTree : uint8_t { None, AWSEBS, GCEPD, AzureDisk, Cinder, ISCSI, RBD };
+const char* intree_plugin_name(InTree k);  // "kubernetes.io/aws-ebs", ... (api/storage.cc)
+
+struct PodVolume {
+  enum class Kind : uint8_t { Other, PVC, Ephemeral, InTree };
+  std::string name;
+  Kind kind = Kind::Other;
+  std::string claim;  // PVC name (Ephemeral: "<pod>-<volume>")
+  InTree intree = InTree::None;
+  std::string id;     // EBS volumeID, GCE pdName, Azure diskName, Cinder volumeID, iSCSI IQN, RBD image
+  bool read_only = false;
+  std::vector<std::string> rbd_monitors;
+  std::string rbd_pool;
+};
+
 // A vector fixed at parse time and shared by every copy of its object: the
 // scheduler copies a Pod per scheduled pod (the assumed pod, the informer's
 // bound object), and those copies then share the containers instead of
@@ -210,6 +227,7 @@ struct Pod {
   IStr preemption_policy = "PreemptLowerPriority";
   int32_t priority = 0;
   SharedVec<Container> containers, init_containers;
+  SharedVec<PodVolume> volumes;  // PVC / ephemeral / in-tree disk volumes (others are not parsed)
   Res overhead;
   StrMap node_selector;
   std::vector<NodeSelectorTerm> required_node_terms;  // OR of terms

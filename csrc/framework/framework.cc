@@ -147,6 +147,10 @@ void Framework::record(const char* point, const Status& st, int64_t start_us, Cy
 
 Status Framework::run_pre_filter(CycleState& s, const Pod& p) {
   int64_t t0 = s.record_metrics ? handle_.clock->now_us() : 0;
+  s.filter_skip = 0;
+  if (auto fit = chain_.find(kFilter); fit != chain_.end() && fit->second.size() <= 64)
+    for (size_t k = 0; k < fit->second.size(); ++k)
+      if (fit->second[k]->skip_filter(p)) s.filter_skip |= uint64_t{1} << k;
   auto it = chain_.find(kPreFilter);
   if (it != chain_.end()) {
     for (const auto& pl : it->second) {
@@ -206,7 +210,10 @@ Status Framework::run_filter(CycleState& s, const Pod& p, const NodeInfo& ni) {
   if (it == chain_.end()) return {};
   Status merged;
   bool failed = false;
-  for (const auto& pl : it->second) {
+  const uint64_t skip = s.filter_skip;
+  for (size_t k = 0; k < it->second.size(); ++k) {
+    if ((skip >> k) & 1u) continue;
+    const auto& pl = it->second[k];
     Status st = pl->filter(s, p, ni);
     if (st.is_success()) continue;
     if (!st.is_unschedulable()) {
@@ -306,7 +313,7 @@ bool Framework::filters_node_local(const Pod& p, const Snapshot& snap) const {
   auto it = chain_.find(kFilter);
   if (it == chain_.end()) return true;
   for (const auto& pl : it->second)
-    if (!pl->filter_node_local(p, snap)) return false;
+    if (!pl->skip_filter(p) && !pl->filter_node_local(p, snap)) return false;
   return true;
 }
 

@@ -118,6 +118,10 @@ class Plugin {
   }
   // Filter
   virtual Status filter(CycleState& s, const Pod& p, const NodeInfo& ni) { return {}; }
+  // True when this plugin's Filter passes every node for p (e.g. a volume
+  // plugin and a pod without volumes): the framework then skips the call for
+  // the whole cycle (the PreFilterResult "Skip" of later upstream).
+  virtual bool skip_filter(const Pod& p) const { return false; }
   // PostFilter
   virtual std::pair<PostFilterResult, Status> post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m) {
     return {PostFilterResult{}, Status(Code::Unschedulable)};

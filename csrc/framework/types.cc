@@ -98,6 +98,7 @@ std::shared_ptr<CycleState> CycleState::clone() const {
   }
   c->record_metrics = record_metrics;
   c->nominated = nominated;
+  c->filter_skip = filter_skip;
   return c;
 }
 

@@ -137,6 +137,10 @@ class CycleState {
   std::shared_ptr<CycleState> clone() const;
   bool record_metrics = false;
   bool skip_filter_plugins_mark = false;
+  // Filter plugins (by position in the profile's Filter chain) that pass
+  // every node for this cycle's pod (Plugin::skip_filter, evaluated once in
+  // PreFilter): run_filter does not call them.
+  uint64_t filter_skip = 0;
   // Nominated pods as of the cycle's start, shared read-only by the Filter
   // workers (null: ask the Nominator). Saves a lock and a vector copy per
   // node while preemptions keep nominations outstanding.

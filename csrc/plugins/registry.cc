@@ -15,6 +15,7 @@ void link_trimaran_plugins();
 void link_sample_plugins();
 void link_topology_plugins();
 void link_crossnode_plugin();
+void link_volume_plugins();
 
 void register_builtin_plugins() {
   link_intree_plugins();
@@ -28,6 +29,7 @@ void register_builtin_plugins() {
   link_sample_plugins();
   link_topology_plugins();
   link_crossnode_plugin();
+  link_volume_plugins();
 }
 
 }  // namespace xsched

@@ -44,6 +44,10 @@ const ResourcePath& resource_path(const std::string& kind) {
       {"nodes", {"/api/v1", false, "v1", "Node"}},
       {"namespaces", {"/api/v1", false, "v1", "Namespace"}},
       {"events", {"/api/v1", true, "v1", "Event"}},
+      {"persistentvolumes", {"/api/v1", false, "v1", "PersistentVolume"}},
+      {"persistentvolumeclaims", {"/api/v1", true, "v1", "PersistentVolumeClaim"}},
+      {"storageclasses", {"/apis/storage.k8s.io/v1", false, "storage.k8s.io/v1", "StorageClass"}},
+      {"csinodes", {"/apis/storage.k8s.io/v1", false, "storage.k8s.io/v1", "CSINode"}},
       {"priorityclasses", {"/apis/scheduling.k8s.io/v1", false, "scheduling.k8s.io/v1", "PriorityClass"}},
       {"poddisruptionbudgets", {"/apis/policy/v1", true, "policy/v1", "PodDisruptionBudget"}},
       {"leases", {"/apis/coordination.k8s.io/v1", true, "coordination.k8s.io/v1", "Lease"}},

@@ -236,4 +236,86 @@ PriorityClassPtr Informers::priority_class(const std::string& name) const {
   return it == pcs_.end() ? nullptr : it->second;
 }
 
+// ------------------------------------------------------------- storage ----
+void Informers::upsert_pv(const PVPtr& pv) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  auto it = pvs_.find(pv->meta.name);
+  if (it != pvs_.end()) {
+    auto& old = pvs_by_class_[it->second->storage_class];
+    std::erase(old, it->second);
+    it->second = pv;
+  } else {
+    pvs_.emplace(pv->meta.name, pv);
+  }
+  pvs_by_class_[pv->storage_class].push_back(pv);
+}
+
+void Informers::delete_pv(const std::string& name) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  auto it = pvs_.find(name);
+  if (it == pvs_.end()) return;
+  std::erase(pvs_by_class_[it->second->storage_class], it->second);
+  pvs_.erase(it);
+}
+
+void Informers::upsert_pvc(const PVCPtr& pvc) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  pvcs_[pvc->meta.key()] = pvc;
+}
+
+void Informers::delete_pvc(const std::string& key) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  pvcs_.erase(key);
+}
+
+void Informers::upsert_storage_class(const StorageClassPtr& sc) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  scs_[sc->meta.name] = sc;
+}
+
+void Informers::delete_storage_class(const std::string& name) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  scs_.erase(name);
+}
+
+void Informers::upsert_csinode(const CSINodePtr& n) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  csinodes_[n->meta.name] = n;
+}
+
+void Informers::delete_csinode(const std::string& name) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  csinodes_.erase(name);
+}
+
+PVPtr Informers::pv(const std::string& name) const {
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = pvs_.find(name);
+  return it == pvs_.end() ? nullptr : it->second;
+}
+
+PVCPtr Informers::pvc(const std::string& ns, const std::string& name) const {
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = pvcs_.find(ns + "/" + name);
+  return it == pvcs_.end() ? nullptr : it->second;
+}
+
+StorageClassPtr Informers::storage_class(const std::string& name) const {
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = scs_.find(name);
+  return it == scs_.end() ? nullptr : it->second;
+}
+
+CSINodePtr Informers::csinode(const std::string& name) const {
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = csinodes_.find(name);
+  return it == csinodes_.end() ? nullptr : it->second;
+}
+
+std::vector<PVPtr> Informers::pvs_of_class(const std::string& cls) const {
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = pvs_by_class_.find(cls);
+  return it == pvs_by_class_.end() ? std::vector<PVPtr>{} : it->second;
+}
+
 }  // namespace xsched

@@ -18,6 +18,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "api/storage.h"
 #include "api/types.h"
 
 namespace xsched {
@@ -37,6 +38,15 @@ class Informers {
   void delete_pdb(const std::string& key);
   void upsert_priority_class(const PriorityClassPtr& pc);
   void delete_priority_class(const std::string& name);
+  // storage (core/v1 PV/PVC, storage.k8s.io/v1 StorageClass/CSINode)
+  void upsert_pv(const PVPtr& pv);
+  void delete_pv(const std::string& name);
+  void upsert_pvc(const PVCPtr& pvc);
+  void delete_pvc(const std::string& key);
+  void upsert_storage_class(const StorageClassPtr& sc);
+  void delete_storage_class(const std::string& name);
+  void upsert_csinode(const CSINodePtr& n);
+  void delete_csinode(const std::string& name);
 
   // ---- listers ----
   PodPtr pod(const std::string& ns, const std::string& name) const;
@@ -57,6 +67,12 @@ class Informers {
   std::vector<PDBPtr> pdbs() const;
   PriorityClassPtr priority_class(const std::string& name) const;
   size_t pod_count() const;
+  PVPtr pv(const std::string& name) const;
+  PVCPtr pvc(const std::string& ns, const std::string& name) const;
+  StorageClassPtr storage_class(const std::string& name) const;
+  CSINodePtr csinode(const std::string& name) const;
+  // PVs of one storage class ("" = no class), as pvCache.ListPVs(class).
+  std::vector<PVPtr> pvs_of_class(const std::string& cls) const;
 
  private:
   mutable std::shared_mutex mu_;
@@ -77,6 +93,11 @@ class Informers {
   std::unordered_map<std::string, NRTPtr> nrts_;
   std::unordered_map<std::string, PDBPtr> pdbs_;
   std::unordered_map<std::string, PriorityClassPtr> pcs_;
+  std::unordered_map<std::string, PVPtr> pvs_;
+  std::unordered_map<std::string, std::vector<PVPtr>> pvs_by_class_;
+  std::unordered_map<std::string, PVCPtr> pvcs_;  // ns/name
+  std::unordered_map<std::string, StorageClassPtr> scs_;
+  std::unordered_map<std::string, CSINodePtr> csinodes_;
 };
 
 }  // namespace xsched

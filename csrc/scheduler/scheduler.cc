@@ -145,6 +145,10 @@ std::string resource_for_kind(const std::string& kind) {
   if (kind == "noderesourcetopologies") return "NodeResourceTopology";
   if (kind == "poddisruptionbudgets") return "PodDisruptionBudget";
   if (kind == "priorityclasses") return "PriorityClass";
+  if (kind == "persistentvolumes") return "PersistentVolume";
+  if (kind == "persistentvolumeclaims") return "PersistentVolumeClaim";
+  if (kind == "storageclasses") return "StorageClass";
+  if (kind == "csinodes") return "CSINode";
   return kind;
 }
 uint32_t action_for(EventType t) {
@@ -407,6 +411,18 @@ void Scheduler::handle_event(const WatchEvent& ev) {
       } else if (ev.kind == "priorityclasses") {
         auto pc = PriorityClass::from_json(o);
         if (del) informers_->delete_priority_class(pc->meta.name); else informers_->upsert_priority_class(pc);
+      } else if (ev.kind == "persistentvolumes") {
+        auto pv = PersistentVolume::from_json(o);
+        if (del) informers_->delete_pv(pv->meta.name); else informers_->upsert_pv(pv);
+      } else if (ev.kind == "persistentvolumeclaims") {
+        auto pvc = PersistentVolumeClaim::from_json(o);
+        if (del) informers_->delete_pvc(pvc->meta.key()); else informers_->upsert_pvc(pvc);
+      } else if (ev.kind == "storageclasses") {
+        auto sc = StorageClass::from_json(o);
+        if (del) informers_->delete_storage_class(sc->meta.name); else informers_->upsert_storage_class(sc);
+      } else if (ev.kind == "csinodes") {
+        auto n = CSINode::from_json(o);
+        if (del) informers_->delete_csinode(n->meta.name); else informers_->upsert_csinode(n);
       }
       for (auto& fw : frameworks_) fw->dispatch_object_event(ev.kind, static_cast<int>(ev.type), ev.obj, ev.old);
       queue_->move_all_to_active_or_backoff(ClusterEvent{resource_for_kind(ev.kind), action_for(ev.type), ""});

@@ -73,7 +73,8 @@ ObjectStore::ObjectStore() {
 
 bool ObjectStore::namespaced(const std::string& kind) {
   return !(kind == "nodes" || kind == "priorityclasses" || kind == "noderesourcetopologies" || kind == "namespaces" ||
-           kind == "loadwatchermetrics");
+           kind == "loadwatchermetrics" || kind == "persistentvolumes" || kind == "storageclasses" ||
+           kind == "csinodes");
 }
 
 void ObjectStore::stamp(Json& obj, int64_t rv) {

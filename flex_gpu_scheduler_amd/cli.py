@@ -242,7 +242,8 @@ def cmd_controller(args) -> int:
 
     client = _client(args)
     stop = threading.Event()
-    mgr = ControllerManager(client, workers=args.workers)
+    provisioners = set(args.provisioners.split(",")) if args.provisioners else None
+    mgr = ControllerManager(client, workers=args.workers, pv_controller=args.pv_controller, provisioners=provisioners)
     if args.enableLeaderElection:
         identity = f"{socket.gethostname()}_{os.getpid()}"
         le = LeaderElector(client, "sched-plugins-controller", "kube-system", identity,
@@ -429,6 +430,11 @@ def build_parser() -> argparse.ArgumentParser:
     conn(p, reference_flags=True)
     p.add_argument("--workers", type=int, default=1)
     p.add_argument("--enableLeaderElection", action="store_true")
+    p.add_argument("--pv-controller", action="store_true",
+                   help="also bind PVs/PVCs and provision claims (clusters without kube-controller-manager)")
+    p.add_argument("--provisioners", default="",
+                   help="comma-separated StorageClass provisioners to provision for (default: all but "
+                        "kubernetes.io/no-provisioner)")
     p.set_defaults(fn=cmd_controller)
 
     p = sub.add_parser("node-agent", help="MI355X node agent")

@@ -57,6 +57,16 @@ PLUGIN_POINTS: dict[str, tuple[str, ...]] = {
     "ImageLocality": ("score",),
     "DefaultPreemption": ("postFilter",),
     "DefaultBinder": ("bind",),
+    "VolumeRestrictions": ("preFilter", "filter"),
+    # Score: 0 everywhere without the alpha VolumeCapacityPriority gate, but
+    # listed, as upstream's multiPoint expansion lists it.
+    "VolumeBinding": ("preFilter", "filter", "score", "reserve", "preBind"),
+    "VolumeZone": ("filter",),
+    "NodeVolumeLimits": ("filter",),
+    "EBSLimits": ("filter",),
+    "GCEPDLimits": ("filter",),
+    "AzureDiskLimits": ("filter",),
+    "CinderLimits": ("filter",),
     # out-of-tree (the reference's pkg/*)
     "FlexGPU": ("filter", "score", "reserve", "bind"),
     "Coscheduling": ("queueSort", "preFilter", "postFilter", "reserve", "permit", "postBind"),
@@ -71,38 +81,39 @@ PLUGIN_POINTS: dict[str, tuple[str, ...]] = {
     "QOSSort": ("queueSort",),
 }
 
-# Volume plugins are part of upstream's default set but have no meaning for a
-# store without PersistentVolumes; accepted in configs and ignored.
-NOT_APPLICABLE = {"VolumeRestrictions", "EBSLimits", "GCEPDLimits", "NodeVolumeLimits", "AzureDiskLimits",
-                  "VolumeBinding", "VolumeZone", "CinderLimits", "SelectorSpread"}
+# SelectorSpread (deprecated, not in 1.23's default set) is accepted in configs
+# and ignored.
+NOT_APPLICABLE = {"SelectorSpread"}
 
-# kube-scheduler 1.23 v1beta2 default plugin set (default_plugins.go:34-106),
-# minus NOT_APPLICABLE.
+# kube-scheduler 1.23 v1beta2 default plugin set (default_plugins.go:34-106).
 DEFAULT_PLUGINS: dict[str, list[tuple[str, int]]] = {
     "queueSort": [("PrioritySort", 0)],
-    "preFilter": [("NodeResourcesFit", 0), ("NodePorts", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0),
-                  ("NodeAffinity", 0)],
+    "preFilter": [("NodeResourcesFit", 0), ("NodePorts", 0), ("VolumeRestrictions", 0), ("PodTopologySpread", 0),
+                  ("InterPodAffinity", 0), ("VolumeBinding", 0), ("NodeAffinity", 0)],
     "filter": [("NodeUnschedulable", 0), ("NodeName", 0), ("TaintToleration", 0), ("NodeAffinity", 0),
-               ("NodePorts", 0), ("NodeResourcesFit", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
+               ("NodePorts", 0), ("NodeResourcesFit", 0), ("VolumeRestrictions", 0), ("EBSLimits", 0),
+               ("GCEPDLimits", 0), ("NodeVolumeLimits", 0), ("AzureDiskLimits", 0), ("VolumeBinding", 0),
+               ("VolumeZone", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
     "postFilter": [("DefaultPreemption", 0)],
     "preScore": [("InterPodAffinity", 0), ("PodTopologySpread", 0), ("TaintToleration", 0), ("NodeAffinity", 0)],
     "score": [("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1), ("InterPodAffinity", 1),
               ("NodeResourcesFit", 1), ("NodeAffinity", 1), ("PodTopologySpread", 2), ("TaintToleration", 1)],
-    "reserve": [],
+    "reserve": [("VolumeBinding", 0)],
     "permit": [],
-    "preBind": [],
+    "preBind": [("VolumeBinding", 0)],
     "bind": [("DefaultBinder", 0)],
     "postBind": [],
 }
 
 
 # kube-scheduler 1.23 v1beta3 defaults: every default plugin in multiPoint,
-# with v1beta3's own score weights (v1beta3/default_plugins.go:30-56), minus
-# NOT_APPLICABLE.
+# with v1beta3's own score weights (v1beta3/default_plugins.go:30-56).
 V1BETA3_MULTIPOINT: list[tuple[str, int]] = [
     ("PrioritySort", 0), ("NodeUnschedulable", 0), ("NodeName", 0), ("TaintToleration", 3), ("NodeAffinity", 2),
-    ("NodePorts", 0), ("NodeResourcesFit", 1), ("PodTopologySpread", 2), ("InterPodAffinity", 2),
-    ("DefaultPreemption", 0), ("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1), ("DefaultBinder", 0),
+    ("NodePorts", 0), ("NodeResourcesFit", 1), ("VolumeRestrictions", 0), ("EBSLimits", 0), ("GCEPDLimits", 0),
+    ("NodeVolumeLimits", 0), ("AzureDiskLimits", 0), ("VolumeBinding", 0), ("VolumeZone", 0),
+    ("PodTopologySpread", 2), ("InterPodAffinity", 2), ("DefaultPreemption", 0),
+    ("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1), ("DefaultBinder", 0),
 ]
 
 
@@ -390,6 +401,20 @@ def default_plugin_args(name: str, args: dict | None) -> dict:
         a.setdefault("hardPodAffinityWeight", 1)
     elif name == "NodeAffinity":
         _strict(name, a, {"addedAffinity"})
+    elif name == "VolumeBinding":
+        # VolumeBindingArgs (v1beta2/types.go); `shape` needs the alpha
+        # VolumeCapacityPriority gate, off in 1.23. pollIntervalMillis is an
+        # extension (the reference polls every second).
+        _strict(name, a, {"bindTimeoutSeconds", "shape", "pollIntervalMillis"})
+        if a.get("shape"):
+            raise ConfigError(f"{name}Args.shape: Invalid value: feature gate VolumeCapacityPriority is not enabled")
+        a.setdefault("bindTimeoutSeconds", 600)
+        if int(a["bindTimeoutSeconds"]) < 0:
+            raise ConfigError(f"{name}Args.bindTimeoutSeconds: Invalid value: must be >= 0")
+        a.setdefault("pollIntervalMillis", 100)
+    elif name in ("VolumeRestrictions", "VolumeZone", "NodeVolumeLimits", "EBSLimits", "GCEPDLimits",
+                  "AzureDiskLimits", "CinderLimits"):
+        _strict(name, a, set())
     return a
 
 

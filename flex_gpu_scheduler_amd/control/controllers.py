@@ -304,22 +304,31 @@ class ControllerManager:
     """Runs both controllers over one informer factory (cmd/controller/app/
     server.go:55-122), optionally only while holding the leader lease."""
 
-    def __init__(self, client: Client, workers: int = 1, record_events: bool = True):
+    def __init__(self, client: Client, workers: int = 1, record_events: bool = True,
+                 pv_controller: bool = False, provisioners: set[str] | None = None):
         self.client = client
         self.factory = InformerFactory(client)
         self.podgroup = PodGroupController(client, workers, self.factory)
         self.elasticquota = ElasticQuotaController(client, workers, self.factory, record_events)
+        self.controllers: list[_Controller] = [self.podgroup, self.elasticquota]
+        if pv_controller:
+            # Only for clusters without kube-controller-manager (this
+            # framework's own API server): it completes the volume binding
+            # the scheduler's VolumeBinding plugin starts.
+            from .pv_controller import PersistentVolumeController
+
+            self.controllers.append(PersistentVolumeController(client, workers, self.factory, provisioners))
 
     def run(self) -> "ControllerManager":
         self.factory.start()
-        self.podgroup.run(start_informers=False)
-        self.elasticquota.run(start_informers=False)
+        for c in self.controllers:
+            c.run(start_informers=False)
         return self
 
     def stop(self) -> None:
-        self.podgroup.stop()
-        self.elasticquota.stop()
+        for c in self.controllers:
+            c.stop()
         self.factory.stop()
 
     def wait_idle(self, timeout: float = 10.0) -> bool:
-        return self.podgroup.wait_idle(timeout) and self.elasticquota.wait_idle(timeout)
+        return all(c.wait_idle(timeout) for c in self.controllers)

@@ -24,7 +24,8 @@ log = logging.getLogger(__name__)
 # Kinds the scheduler and its plugins watch (scheduler informers + plugin
 # watched_kinds()).
 SCHEDULER_KINDS = ("nodes", "pods", "podgroups", "elasticquotas", "noderesourcetopologies", "priorityclasses",
-                   "poddisruptionbudgets", "namespaces", "loadwatchermetrics")
+                   "poddisruptionbudgets", "namespaces", "loadwatchermetrics", "persistentvolumes",
+                   "persistentvolumeclaims", "storageclasses", "csinodes")
 
 
 class StoreMirror:

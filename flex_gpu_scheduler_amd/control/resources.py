@@ -3,7 +3,8 @@
 The native ObjectStore keys objects by plural kind ("pods", "podgroups", ...).
 The HTTP API server and the REST client map those kinds onto the Kubernetes
 URL layout so the wire format matches kube-apiserver for every kind the
-reference touches (core pods/nodes/events, scheduling.k8s.io PriorityClass,
+reference touches (core pods/nodes/events/PV/PVC, storage.k8s.io StorageClass
+and CSINode, scheduling.k8s.io PriorityClass,
 policy PDB, coordination Lease, the scheduling.sigs.k8s.io CRDs from
 apis/scheduling/v1alpha1/types.go:30-193, topology.node.k8s.io NRT) plus the
 load-watcher document (vendor/github.com/paypal/load-watcher/pkg/watcher/
@@ -50,6 +51,10 @@ RESOURCES: dict[str, Resource] = {r.kind_plural: r for r in [
     Resource("nodes", "", "v1", "Node", False, ("no",)),
     Resource("namespaces", "", "v1", "Namespace", False, ("ns",)),
     Resource("events", "", "v1", "Event", True, ("ev",)),
+    Resource("persistentvolumes", "", "v1", "PersistentVolume", False, ("pv",)),
+    Resource("persistentvolumeclaims", "", "v1", "PersistentVolumeClaim", True, ("pvc",)),
+    Resource("storageclasses", "storage.k8s.io", "v1", "StorageClass", False, ("sc",)),
+    Resource("csinodes", "storage.k8s.io", "v1", "CSINode", False),
     Resource("priorityclasses", "scheduling.k8s.io", "v1", "PriorityClass", False, ("pc",)),
     Resource("poddisruptionbudgets", "policy", "v1", "PodDisruptionBudget", True, ("pdb",)),
     Resource("leases", "coordination.k8s.io", "v1", "Lease", True),

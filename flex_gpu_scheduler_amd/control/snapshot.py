@@ -15,7 +15,8 @@ import tempfile
 from .resources import RESOURCES
 
 # Restore order: namespaces and cluster objects first, pods last.
-ORDER = ("namespaces", "priorityclasses", "nodes", "noderesourcetopologies", "podgroups", "elasticquotas",
+ORDER = ("namespaces", "priorityclasses", "storageclasses", "nodes", "csinodes", "noderesourcetopologies",
+         "persistentvolumes", "persistentvolumeclaims", "podgroups", "elasticquotas",
          "poddisruptionbudgets", "leases", "loadwatchermetrics", "events", "pods")
 
 

@@ -10,8 +10,7 @@ Mirrors the reference's config tests:
     point for each per-plugin config file, v1beta2 and v1beta3 (multiPoint),
     against upstream's defaults.PluginsV1beta2 / ExpandedPluginsV1beta3
     (vendor/k8s.io/kubernetes/pkg/scheduler/apis/config/testing/defaults/
-    defaults.go:183-274) minus the volume plugins, which have no meaning
-    without PersistentVolumes.
+    defaults.go:183-274), volume plugins included.
 """
 import pytest
 
@@ -20,32 +19,39 @@ from flex_gpu_scheduler_amd.config import ConfigError, default_plugin_args, load
 V2 = "kubescheduler.config.k8s.io/v1beta2"
 V3 = "kubescheduler.config.k8s.io/v1beta3"
 
-# defaults.PluginsV1beta2 minus volume plugins: point -> [(name, weight)]
+# defaults.PluginsV1beta2: point -> [(name, weight)]
 PLUGINS_V1BETA2 = {
     "queueSort": [("PrioritySort", 0)],
-    "preFilter": [("NodeResourcesFit", 0), ("NodePorts", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0),
-                  ("NodeAffinity", 0)],
+    "preFilter": [("NodeResourcesFit", 0), ("NodePorts", 0), ("VolumeRestrictions", 0), ("PodTopologySpread", 0),
+                  ("InterPodAffinity", 0), ("VolumeBinding", 0), ("NodeAffinity", 0)],
     "filter": [("NodeUnschedulable", 0), ("NodeName", 0), ("TaintToleration", 0), ("NodeAffinity", 0),
-               ("NodePorts", 0), ("NodeResourcesFit", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
+               ("NodePorts", 0), ("NodeResourcesFit", 0), ("VolumeRestrictions", 0), ("EBSLimits", 0),
+               ("GCEPDLimits", 0), ("NodeVolumeLimits", 0), ("AzureDiskLimits", 0), ("VolumeBinding", 0),
+               ("VolumeZone", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
     "postFilter": [("DefaultPreemption", 0)],
     "preScore": [("InterPodAffinity", 0), ("PodTopologySpread", 0), ("TaintToleration", 0), ("NodeAffinity", 0)],
     "score": [("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1), ("InterPodAffinity", 1),
               ("NodeResourcesFit", 1), ("NodeAffinity", 1), ("PodTopologySpread", 2), ("TaintToleration", 1)],
-    "reserve": [], "permit": [], "preBind": [], "bind": [("DefaultBinder", 0)], "postBind": [],
+    "reserve": [("VolumeBinding", 0)], "permit": [], "preBind": [("VolumeBinding", 0)],
+    "bind": [("DefaultBinder", 0)], "postBind": [],
 }
 
-# defaults.ExpandedPluginsV1beta3 minus volume plugins
+# defaults.ExpandedPluginsV1beta3
 EXPANDED_V1BETA3 = {
     "queueSort": [("PrioritySort", 0)],
-    "preFilter": [("NodeAffinity", 0), ("NodePorts", 0), ("NodeResourcesFit", 0), ("PodTopologySpread", 0),
-                  ("InterPodAffinity", 0)],
+    "preFilter": [("NodeAffinity", 0), ("NodePorts", 0), ("NodeResourcesFit", 0), ("VolumeRestrictions", 0),
+                  ("VolumeBinding", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
     "filter": [("NodeUnschedulable", 0), ("NodeName", 0), ("TaintToleration", 0), ("NodeAffinity", 0),
-               ("NodePorts", 0), ("NodeResourcesFit", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
+               ("NodePorts", 0), ("NodeResourcesFit", 0), ("VolumeRestrictions", 0), ("EBSLimits", 0),
+               ("GCEPDLimits", 0), ("NodeVolumeLimits", 0), ("AzureDiskLimits", 0), ("VolumeBinding", 0),
+               ("VolumeZone", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
     "postFilter": [("DefaultPreemption", 0)],
     "preScore": [("TaintToleration", 0), ("NodeAffinity", 0), ("PodTopologySpread", 0), ("InterPodAffinity", 0)],
-    "score": [("TaintToleration", 3), ("NodeAffinity", 2), ("NodeResourcesFit", 1), ("PodTopologySpread", 2),
-              ("InterPodAffinity", 2), ("NodeResourcesBalancedAllocation", 1), ("ImageLocality", 1)],
-    "reserve": [], "permit": [], "preBind": [], "bind": [("DefaultBinder", 0)], "postBind": [],
+    "score": [("TaintToleration", 3), ("NodeAffinity", 2), ("NodeResourcesFit", 1), ("VolumeBinding", 1),
+              ("PodTopologySpread", 2), ("InterPodAffinity", 2), ("NodeResourcesBalancedAllocation", 1),
+              ("ImageLocality", 1)],
+    "reserve": [("VolumeBinding", 0)], "permit": [], "preBind": [("VolumeBinding", 0)],
+    "bind": [("DefaultBinder", 0)], "postBind": [],
 }
 
 
@@ -94,7 +100,8 @@ MAIN_CASES = [
      with_points(EXPANDED_V1BETA3, queueSort=[("Coscheduling", 0)],
                  preFilter=EXPANDED_V1BETA3["preFilter"] + [("Coscheduling", 0)], filter=[],
                  postFilter=[("DefaultPreemption", 0), ("Coscheduling", 0)], preScore=[], score=[],
-                 reserve=[("Coscheduling", 0)], permit=[("Coscheduling", 0)], postBind=[("Coscheduling", 0)])),
+                 reserve=[("VolumeBinding", 0), ("Coscheduling", 0)], permit=[("Coscheduling", 0)],
+                 postBind=[("Coscheduling", 0)])),
     ("single profile config - Node Resources Allocatable with args",
      cfg(V3, {"score": {"enabled": [{"name": "NodeResourcesAllocatable"}], "disabled": ALL}},
          [{"name": "NodeResourcesAllocatable", "args": {"mode": "Least", "resources": [
@@ -105,7 +112,7 @@ MAIN_CASES = [
               "postFilter": {"enabled": [{"name": "CapacityScheduling"}], "disabled": ALL},
               "reserve": {"enabled": [{"name": "CapacityScheduling"}]}}, name="default-scheduler"),
      with_points(PLUGINS_V1BETA2, preFilter=PLUGINS_V1BETA2["preFilter"] + [("CapacityScheduling", 0)],
-                 postFilter=[("CapacityScheduling", 0)], reserve=[("CapacityScheduling", 0)])),
+                 postFilter=[("CapacityScheduling", 0)], reserve=[("VolumeBinding", 0), ("CapacityScheduling", 0)])),
     # Commented out upstream (k/k#108083); expandMultiPointPlugins puts the
     # point's explicit plugins first.
     ("single profile config - Capacityscheduling - v1beta3",
@@ -113,7 +120,7 @@ MAIN_CASES = [
               "postFilter": {"enabled": [{"name": "CapacityScheduling"}], "disabled": ALL},
               "reserve": {"enabled": [{"name": "CapacityScheduling"}]}}, name="default-scheduler"),
      with_points(EXPANDED_V1BETA3, preFilter=[("CapacityScheduling", 0)] + EXPANDED_V1BETA3["preFilter"],
-                 postFilter=[("CapacityScheduling", 0)], reserve=[("CapacityScheduling", 0)])),
+                 postFilter=[("CapacityScheduling", 0)], reserve=[("CapacityScheduling", 0), ("VolumeBinding", 0)])),
     ("single profile config - TargetLoadPacking with args",
      cfg(V3, {"score": {"enabled": [{"name": "TargetLoadPacking"}], "disabled": ALL}},
          [{"name": "TargetLoadPacking", "args": {"targetUtilization": 60, "defaultRequests": {"cpu": "1000m"},

@@ -53,7 +53,8 @@ def test_flexgpu_chart_reference_profile():
                                                                       "xgmiPlacement": {"enabled": False}},
                                                         "nodeAgent": {"enabled": False}})
     prof = _config_from(objs).profile("flex-gpu-scheduler")
-    assert prof.plugins["reserve"] == ["FlexGPU"] and prof.plugins["score"][-1] == "FlexGPU"
+    # v1beta2 defaults keep VolumeBinding at Reserve ahead of FlexGPU, as upstream.
+    assert prof.plugins["reserve"] == ["VolumeBinding", "FlexGPU"] and prof.plugins["score"][-1] == "FlexGPU"
     assert "Coscheduling" not in prof.plugins.get("permit", [])
     assert not any(o["kind"] == "DaemonSet" for o in objs)
 
