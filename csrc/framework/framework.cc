@@ -238,7 +238,10 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
     CycleState* state_to_use = &s;
     const NodeInfo* ni_to_use = &ni;
     std::shared_ptr<CycleState> state_out;
-    std::shared_ptr<NodeInfo> ni_out;
+    // addNominatedPods works on a copy of the node: this thread's scratch,
+    // whose storage is reused from call to call (no allocation per node).
+    thread_local NodeInfo scratch;
+    NodeInfo* ni_out = nullptr;
     if (i == 0) {
       std::vector<PodPtr> live;
       const std::vector<PodPtr>* nominated = &live;
@@ -251,7 +254,10 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
       }
       for (const auto& np : *nominated) {
         if (np->priority < p.priority || np->uid() == p.uid()) continue;
-        if (!ni_out) ni_out = ni.clone();
+        if (!ni_out) {
+          scratch = ni;
+          ni_out = &scratch;
+        }
         ni_out->add_pod(np);
         pods_added = true;
         // addNominatedPods clones the CycleState for the PreFilter AddPod
@@ -265,7 +271,7 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
       }
       if (pods_added) {
         if (state_out) state_to_use = state_out.get();
-        ni_to_use = ni_out.get();
+        ni_to_use = ni_out;
       }
     } else if (!pods_added || !st.is_success()) {
       break;

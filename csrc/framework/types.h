@@ -264,6 +264,10 @@ struct PodDelta {
 // ------------------------------------------------------------ Snapshot ----
 struct Snapshot {
   std::vector<NodeInfoPtr> nodes;  // in cache order
+  // nodes[i]'s name, contiguous: the per-node loops of a failed cycle (the
+  // FitError diagnosis over every node) read names without touching each
+  // NodeInfo and Node.
+  std::vector<std::string> names;
   std::unordered_map<std::string, NodeInfoPtr> by_name;
   std::unordered_map<std::string, size_t> index;  // name -> position in `nodes`
   // Nodes with affinity / required anti-affinity pods, in no particular
@@ -384,55 +388,62 @@ class NodeStatusMap {
   iterator end() { return entries_.end(); }
   void clear() {
     entries_.clear();
+    hashes_.clear();
     slots_.clear();
   }
   void reserve(size_t n) {
     entries_.reserve(n);
+    hashes_.reserve(n);
     if (n * 2 > slots_.size()) rehash(n * 2);
   }
   const_iterator find(std::string_view k) const {
-    int32_t i = lookup(k);
+    int32_t i = lookup(k, hash(k));
     return i < 0 ? entries_.end() : entries_.begin() + i;
   }
   iterator find(std::string_view k) {
-    int32_t i = lookup(k);
+    int32_t i = lookup(k, hash(k));
     return i < 0 ? entries_.end() : entries_.begin() + i;
   }
-  size_t count(std::string_view k) const { return lookup(k) < 0 ? 0 : 1; }
+  size_t count(std::string_view k) const { return lookup(k, hash(k)) < 0 ? 0 : 1; }
   std::pair<iterator, bool> emplace(std::string_view k, const Status& v) {
-    if (int32_t i = lookup(k); i >= 0) return {entries_.begin() + i, false};
+    const size_t h = hash(k);
+    if (int32_t i = lookup(k, h); i >= 0) return {entries_.begin() + i, false};
     if ((entries_.size() + 1) * 2 > slots_.size()) rehash(std::max<size_t>(16, slots_.size() * 2));
     entries_.emplace_back(std::string(k), v);
-    place(static_cast<int32_t>(entries_.size() - 1));
+    hashes_.push_back(h);
+    place(static_cast<int32_t>(entries_.size() - 1), h);
     return {entries_.end() - 1, true};
   }
   Status& operator[](std::string_view k) { return emplace(k, Status()).first->second; }
 
  private:
+  // Each key is hashed once: the hash is kept beside the entry, so probing
+  // compares hashes before strings and a rehash never rehashes a string.
   static size_t hash(std::string_view k) { return std::hash<std::string_view>{}(k); }
-  int32_t lookup(std::string_view k) const {
+  int32_t lookup(std::string_view k, size_t h) const {
     if (slots_.empty()) return -1;
     size_t mask = slots_.size() - 1;
-    for (size_t h = hash(k) & mask;; h = (h + 1) & mask) {
-      int32_t i = slots_[h];
+    for (size_t j = h & mask;; j = (j + 1) & mask) {
+      int32_t i = slots_[j];
       if (i < 0) return -1;
-      if (entries_[i].first == k) return i;
+      if (hashes_[i] == h && entries_[i].first == k) return i;
     }
   }
-  void place(int32_t i) {
+  void place(int32_t i, size_t h) {
     size_t mask = slots_.size() - 1;
-    size_t h = hash(entries_[i].first) & mask;
-    while (slots_[h] >= 0) h = (h + 1) & mask;
-    slots_[h] = i;
+    size_t j = h & mask;
+    while (slots_[j] >= 0) j = (j + 1) & mask;
+    slots_[j] = i;
   }
   void rehash(size_t want) {
     size_t cap = 16;
     while (cap < want) cap <<= 1;
     slots_.assign(cap, -1);
-    for (int32_t i = 0; i < static_cast<int32_t>(entries_.size()); ++i) place(i);
+    for (int32_t i = 0; i < static_cast<int32_t>(entries_.size()); ++i) place(i, hashes_[i]);
   }
   std::vector<value_type> entries_;
-  std::vector<int32_t> slots_;  // power of two, at most half full; -1 = empty
+  std::vector<size_t> hashes_;   // hash of entries_[i].first
+  std::vector<int32_t> slots_;   // power of two, at most half full; -1 = empty
 };
 
 struct Victims {

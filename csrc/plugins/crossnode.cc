@@ -87,7 +87,8 @@ class CrossNodePreemption : public Plugin, public PreemptionPolicy {
   // Exposed through the plugin for tests (bindings call post_filter).
   std::vector<Candidate> find_candidates(CycleState& s, const Pod& pod, const NodeStatusMap& m,
                                          const std::vector<PDBPtr>& pdbs) {
-    std::vector<NodeInfoPtr> potential = nodes_where_preemption_might_help(*h_.snapshot, m);
+    std::vector<NodeInfoPtr> filtered;
+    const std::vector<NodeInfoPtr>& potential = nodes_where_preemption_might_help(*h_.snapshot, m, filtered);
     if (potential.empty()) return {};
     // Victim pool: lower-priority, not already terminating pods that sit on a
     // potential node or can constrain the preemptor from elsewhere (they

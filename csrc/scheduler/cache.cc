@@ -346,9 +346,11 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
   if (structure_changed_) {
     for (auto& ni : s.nodes) s.retired.push_back(std::move(ni));
     s.nodes.clear();
+    s.names.clear();
     s.by_name.clear();
     s.index.clear();
     s.nodes.reserve(order_.size());
+    s.names.reserve(order_.size());
     for (const auto& name : order_) {
       auto it = nodes_.find(name);
       if (it == nodes_.end() || !it->second->node) continue;
@@ -356,6 +358,7 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
       ++clones;
       s.index[name] = s.nodes.size();
       s.nodes.push_back(cl);
+      s.names.push_back(name);
       s.by_name[name] = cl;
     }
     structure_changed_ = false;

@@ -79,6 +79,8 @@ int calculate_num_candidates(int num_nodes, int pct, int min_abs);
 // is UnschedulableAndUnresolvable (nodesWherePreemptionMightHelp). One pass
 // over the diagnosis instead of a name lookup per node; usually no node is
 // unresolvable and the snapshot's list is returned whole.
-std::vector<NodeInfoPtr> nodes_where_preemption_might_help(const Snapshot& snap, const NodeStatusMap& m);
+// Returns the snapshot's own list when no node is unresolvable, else `out`.
+const std::vector<NodeInfoPtr>& nodes_where_preemption_might_help(const Snapshot& snap, const NodeStatusMap& m,
+                                                                  std::vector<NodeInfoPtr>& out);
 
 }  // namespace xsched

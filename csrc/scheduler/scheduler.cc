@@ -745,7 +745,8 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   if (feasible_pos) feasible_pos->clear();
   if (!st.is_success()) {
     if (!st.is_unschedulable()) return st;
-    for (const auto& ni : all) d.node_to_status[ni->name()] = st;
+    d.node_to_status.reserve(all.size());
+    for (const auto& name : snapshot_.names) d.node_to_status.emplace(name, st);
     d.unschedulable_plugins.insert(st.failed_plugin());
     return Status(Code::Unschedulable, st.message()).with_plugin(st.failed_plugin());
   }
@@ -916,7 +917,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     for (int pos = 0; pos < n; ++pos) {
       const Status* fs = fail_ptr_[pos];
       if (!fs) continue;
-      d.node_to_status.emplace(all[pos]->name(), *fs);
+      d.node_to_status.emplace(snapshot_.names[pos], *fs);
       size_t k = distinct.size();
       if (distinct.size() <= 32) {
         for (size_t j = 0; j < distinct.size(); ++j)

@@ -1,0 +1,36 @@
+#!/usr/bin/env bash
+# Round-3 box session. Usage: bash scripts/gpu_r3.sh TAG step [step ...]
+# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote
+# Every GPU step runs under its own time limit; the script stops at the first
+# failure (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+tag=$1; shift
+OUT=gpurun_out/$tag
+mkdir -p "$OUT"
+for step in "$@"; do
+  echo "[$tag] $step $(date +%T)"
+  case $step in
+    pytest) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+              > "$OUT/pytest_gpu.txt" 2>&1 ;;
+    smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 ;;
+    bench) timeout -k 10 300 python bench.py > "$OUT/bench1.json" 2> "$OUT/bench1.err" ;;
+    bench3) for i in 1 2 3; do
+              timeout -k 10 200 python bench.py --no-scenarios --no-placement > "$OUT/bench64_$i.json" \
+                2> "$OUT/bench64_$i.err" || exit $?
+            done ;;
+    pmc) OUTDIR="$OUT" bash scripts/pmc_round.sh ;;
+    sched500) timeout -k 10 400 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 500 --pods 1000 \
+                --cpus l3 > "$OUT/sched_perf_500.jsonl" 2>&1 ;;
+    sched5000) timeout -k 10 700 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 5000 --pods 5000 \
+                --cpus l3 > "$OUT/sched_perf_5000.jsonl" 2>&1 ;;
+    remote) timeout -k 10 600 python -u -m flex_gpu_scheduler_amd.tools.remote_bench > "$OUT/remote_bench.jsonl" \
+              2>&1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  echo "[$tag] $step rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
+echo "[$tag] done"
