@@ -232,8 +232,31 @@ Status Framework::run_filter(CycleState& s, const Pod& p, const NodeInfo& ni) {
 }
 
 Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, const NodeInfo& ni) {
+  return filter_with_nominated(s, p, ni, nullptr);
+}
+
+Status Framework::run_filter_with_nominated_pods_inplace(CycleState& s, const Pod& p, NodeInfo& ni) {
+  return filter_with_nominated(s, p, ni, &ni);
+}
+
+Status Framework::filter_with_nominated(CycleState& s, const Pod& p, const NodeInfo& ni, NodeInfo* inplace) {
   Status st;
   bool pods_added = false;
+  // In place: the nominated pods join `inplace` for the first pass and leave
+  // it before the second (and on every return), instead of a copy of it.
+  thread_local std::vector<PodPtr> added_here;
+  struct Undo {
+    NodeInfo* ni;
+    size_t base;  // re-entrancy safe: only this call's tail is undone
+    void operator()() {
+      if (!ni) return;
+      while (added_here.size() > base) {
+        ni->remove_pod(added_here.back()->uid());
+        added_here.pop_back();
+      }
+    }
+    ~Undo() { (*this)(); }
+  } undo{inplace, added_here.size()};
   for (int i = 0; i < 2; ++i) {
     CycleState* state_to_use = &s;
     const NodeInfo* ni_to_use = &ni;
@@ -255,10 +278,15 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
       for (const auto& np : *nominated) {
         if (np->priority < p.priority || np->uid() == p.uid()) continue;
         if (!ni_out) {
-          scratch = ni;
-          ni_out = &scratch;
+          if (inplace) {
+            ni_out = inplace;
+          } else {
+            scratch = ni;
+            ni_out = &scratch;
+          }
         }
         ni_out->add_pod(np);
+        if (inplace) added_here.push_back(np);
         pods_added = true;
         // addNominatedPods clones the CycleState for the PreFilter AddPod
         // extensions; a nominated pod none of them reacts to leaves the state
@@ -278,6 +306,7 @@ Status Framework::run_filter_with_nominated_pods(CycleState& s, const Pod& p, co
     }
     st = run_filter(*state_to_use, p, *ni_to_use);
     if (!st.is_success() && !st.is_unschedulable()) return st;
+    if (inplace) undo();  // the second pass sees the node without them
   }
   return st;
 }

@@ -64,6 +64,9 @@ class Framework {
   bool pre_filter_extensions_affected(const CycleState& s, const Pod& to_schedule, const Pod& other) const;
   Status run_filter(CycleState& s, const Pod& p, const NodeInfo& ni);
   Status run_filter_with_nominated_pods(CycleState& s, const Pod& p, const NodeInfo& ni);
+  // The same on a NodeInfo the caller owns (a preemption dry run's scratch):
+  // nominated pods are added to it and removed again, no copy is made.
+  Status run_filter_with_nominated_pods_inplace(CycleState& s, const Pod& p, NodeInfo& ni);
   std::pair<PostFilterResult, Status> run_post_filter(CycleState& s, const Pod& p, const NodeStatusMap& m);
   Status run_pre_score(CycleState& s, const Pod& p, const NodeList& nodes);
   // Weighted sum of all score plugins per node (same order as `nodes`).
@@ -96,6 +99,7 @@ class Framework {
   static constexpr int64_t kMaxPermitTimeoutUs = 15LL * 60 * 1000000;  // framework.go:46
 
  private:
+  Status filter_with_nominated(CycleState& s, const Pod& p, const NodeInfo& ni, NodeInfo* inplace);
   ParallelSite score_site_;  // inline-vs-parallel cost model of Score
   void record(const char* point, const Status& st, int64_t start_us, CycleState& s);
   ProfileConfig cfg_;

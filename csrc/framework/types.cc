@@ -121,8 +121,12 @@ void GpuLedger::init(const Node& n) {
   std::fill(std::begin(zone_whole), std::end(zone_whole), 0);
   std::fill(std::begin(zone_xcds), std::end(zone_xcds), 0);
   std::fill(std::begin(zone_mem), std::end(zone_mem), 0);
+  zone_n = 0;
   for (int g = 0; g < gpu_count; ++g) {
-    if (numa[g] >= 0 && numa[g] < kMaxZones) ++zone_gpus[numa[g]];
+    if (numa[g] >= 0 && numa[g] < kMaxZones) {
+      ++zone_gpus[numa[g]];
+      zone_n = std::max(zone_n, numa[g] + 1);
+    }
     refresh(g);
   }
 }

@@ -163,7 +163,7 @@ using CycleStatePtr = std::shared_ptr<CycleState>;
 // CPX=8; each partition owns 8/parts XCDs and mem_per_gpu/parts memory
 // units). The ledger is updated incrementally as pods enter/leave the node,
 // replacing the reference's per-call O(pods) rebuild (gpu_node.go:30-120).
-struct GpuLedger {
+struct GpuLedgerState {
   struct Slot {
     int exclusive = 0;     // whole-GPU or partition owners (expected 0/1)
     int64_t used_mem = 0;  // Σ memory-slice pods on this partition
@@ -189,8 +189,26 @@ struct GpuLedger {
   std::vector<GpuFree> free;
   int tot_whole = 0, tot_xcds = 0;
   int64_t tot_mem = 0;
+};
+
+// Per-zone totals live in fixed arrays sized for the largest NUMA id; only
+// the first zone_n entries (1 + the largest NUMA id of a GPU) are ever
+// non-zero, so copies (every NodeInfo clone and preemption dry run) move
+// those and not the 1.3 KB of the full arrays.
+struct GpuLedger : GpuLedgerState {
+  int zone_n = 0;
   int zone_gpus[kMaxZones] = {}, zone_whole[kMaxZones] = {}, zone_xcds[kMaxZones] = {};
   int64_t zone_mem[kMaxZones] = {};
+
+  GpuLedger() = default;
+  GpuLedger(const GpuLedger& o) : GpuLedgerState(o) { copy_zones(o); }
+  GpuLedger& operator=(const GpuLedger& o) {
+    if (this != &o) {
+      GpuLedgerState::operator=(o);
+      copy_zones(o);
+    }
+    return *this;
+  }
 
   void init(const Node& n);
   void apply(const GpuAssignment& a, int sign);
@@ -204,6 +222,14 @@ struct GpuLedger {
   // GPU the container would see 2/4/8 separate devices, not one MI355X.
   bool whole_gpu_free(int g) const { return free[g].whole != 0; }
   bool slot_free(int g, int p) const;   // exclusive-free and no memory use
+  void copy_zones(const GpuLedger& o) {
+    const int n = std::max(zone_n, o.zone_n);
+    std::copy_n(o.zone_gpus, n, zone_gpus);
+    std::copy_n(o.zone_whole, n, zone_whole);
+    std::copy_n(o.zone_xcds, n, zone_xcds);
+    std::copy_n(o.zone_mem, n, zone_mem);
+    zone_n = o.zone_n;
+  }
   int free_gpus() const { return tot_whole; }  // GPUScore (gpu_node.go:179-187): free whole (SPX) GPUs
   int64_t free_memory() const { return tot_mem; }  // MemScore (gpu_node.go:189-199)
   int free_xcds() const { return tot_xcds; }

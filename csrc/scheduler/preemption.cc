@@ -67,7 +67,7 @@ Status select_victims_default(Handle& h, CycleState& s, const Pod& preemptor, No
   }
   if (potential.empty())
     return Status::unresolvable("No victims found on node " + ni.name() + " for preemptor pod " + preemptor.name());
-  Status st = fw.run_filter_with_nominated_pods(s, preemptor, ni);
+  Status st = fw.run_filter_with_nominated_pods_inplace(s, preemptor, ni);
   if (!st.is_success()) return st;
   std::stable_sort(potential.begin(), potential.end(),
             [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*a, *b); });
@@ -77,7 +77,7 @@ Status select_victims_default(Handle& h, CycleState& s, const Pod& preemptor, No
     ni.add_pod(p);
     Status ast = fw.run_pre_filter_add_pod(s, preemptor, p, ni);
     if (!ast.is_success()) return {false, ast};
-    bool fits = fw.run_filter_with_nominated_pods(s, preemptor, ni).is_success();
+    bool fits = fw.run_filter_with_nominated_pods_inplace(s, preemptor, ni).is_success();
     if (!fits) {
       ni.remove_pod(p->uid());
       Status rst = fw.run_pre_filter_remove_pod(s, preemptor, p, ni);
