@@ -100,6 +100,8 @@ def main() -> int:
                     help="skip the per-BASELINE-config scenarios (untimed, reported under config.scenarios)")
     ap.add_argument("--cpus", default=os.environ.get("XSCHED_CPUS", "l3"),
                     help="shard CPU placement: none | l3 | l3xK | explicit list (utils/cpuaffinity.py)")
+    ap.add_argument("--no-open-loop", action="store_true",
+                    help="skip the untimed open-loop (Poisson arrivals) gang admission latency run")
     ap.add_argument("--no-placement", action="store_true",
                     help="skip the end-to-end placement validation (discovery -> scheduler -> Allocate -> RCCL)")
     args = ap.parse_args()
@@ -184,6 +186,17 @@ def main() -> int:
     pods_total = ctx.all_sum(float(pods))
     all_gangs = [g for part in ctx.gather(gangs) for g in part]
     stats = shard.sched.stats()
+    if ctx.rank == 0 and not args.no_open_loop:
+        # Untimed: Poisson gang arrivals at 50% / 90% of this shard's measured
+        # throughput, gang types interleaved, held then deleted
+        # (utils/openloop.py) — admission latency rather than burst queueing.
+        from flex_gpu_scheduler_amd.utils.openloop import run_open_loop
+
+        cap = pods / elapsed if elapsed > 0 else 0.0
+        extras["gang_admit_open_loop"] = {
+            "capacity_pods_per_s": round(cap, 1),
+            **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed)
+               for f in (0.5, 0.9)}} if cap > 0 else {}
     shard.close()
 
     if not args.no_placement and (ctx.distributed or ctx.cuda):
@@ -225,6 +238,7 @@ def main() -> int:
                 "gpus_per_shard": args.nodes * 8,
                 "p99_gang_admit_ms": {k: v["p99_ms"] for k, v in lat.items()},
                 "gang_admit": lat,
+                "gang_admit_by_type": gang_latency_summary(all_gangs, by_type=True),
                 "attempts": stats["attempts"],
                 "unschedulable_attempts": stats["unschedulable"],
                 "eq_cache_filter_hit_rate": round(stats["eq_filter_hits"] / max(1, stats["eq_filter_hits"] +

@@ -16,6 +16,7 @@
 #include "common/json.h"
 #include "common/quantity.h"
 #include "rest/kube.h"
+#include "scheduler/openloop.h"
 #include "scheduler/scheduler.h"
 #include "store/store.h"
 #include "telemetry/amdsmi_sampler.h"
@@ -496,6 +497,47 @@ PYBIND11_MODULE(_xsched, m) {
       .def("last_error", &rest::RemoteMirror::last_error);
 
   // ---- scheduler ----
+  // Open-loop gang arrivals (scheduler/openloop.h): gangs_json = [{"podgroup":
+  // {...}, "pods": [...]}, ...]; returns per-gang timelines in microseconds.
+  m.def(
+      "run_open_loop",
+      [](ObjectStore& store, Scheduler& sched, const std::string& gangs_json, std::vector<int64_t> offsets_us,
+         int64_t hold_us, int64_t timeout_us) {
+        std::vector<OpenLoopGang> gangs;
+        {
+          Json arr = Json::parse(gangs_json);
+          gangs.reserve(arr.size());
+          for (const auto& g : arr.items()) {
+            OpenLoopGang og;
+            og.pod_group = g["podgroup"];
+            og.pods.assign(g["pods"].items().begin(), g["pods"].items().end());
+            gangs.push_back(std::move(og));
+          }
+        }
+        OpenLoopResult r;
+        {
+          py::gil_scoped_release rel;
+          r = run_open_loop(store, sched, std::move(gangs), offsets_us, hold_us, timeout_us);
+        }
+        py::list out;
+        for (const auto& g : r.gangs) {
+          py::dict d;
+          d["size"] = g.size;
+          d["create_us"] = g.create_us;
+          d["first_enqueue_us"] = g.first_enqueue_us;
+          d["admit_us"] = g.admit_us;
+          d["bound_us"] = g.bound_us;
+          out.append(d);
+        }
+        py::dict res;
+        res["gangs"] = out;
+        res["wall_us"] = r.wall_us;
+        res["late_us"] = r.late_us;
+        return res;
+      },
+      py::arg("store"), py::arg("sched"), py::arg("gangs_json"), py::arg("offsets_us"), py::arg("hold_us"),
+      py::arg("timeout_us") = 10'000'000);
+
   py::class_<Scheduler, std::shared_ptr<Scheduler>>(m, "Scheduler")
       .def(py::init([](std::shared_ptr<ObjectStore> store, py::handle config, std::shared_ptr<FakeClock> clock,
                        std::shared_ptr<ApiClient> client) {

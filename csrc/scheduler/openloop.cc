@@ -1,0 +1,108 @@
+#include "scheduler/openloop.h"
+
+#include <algorithm>
+#include <queue>
+#include <string>
+#include <thread>
+#include <unordered_map>
+
+#include "scheduler/scheduler.h"
+#include "store/store.h"
+
+namespace xsched {
+
+OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<OpenLoopGang> gangs,
+                             const std::vector<int64_t>& offsets_us, int64_t hold_us, int64_t timeout_us) {
+  const size_t n = std::min(gangs.size(), offsets_us.size());
+  OpenLoopResult out;
+  out.gangs.resize(n);
+  std::unordered_map<std::string, size_t> by_key;  // "ns/pg" -> gang
+  std::vector<std::string> ns(n), pg(n);
+  for (size_t i = 0; i < n; ++i) {
+    const Json& md = gangs[i].pod_group["metadata"];
+    ns[i] = md["namespace"].str_or("default");
+    pg[i] = md["name"].as_string();
+    by_key[ns[i] + "/" + pg[i]] = i;
+    out.gangs[i].size = static_cast<int>(gangs[i].pods.size());
+  }
+  (void)sched.gang_records(true);  // start from a clean slate
+  using Due = std::pair<int64_t, size_t>;
+  std::priority_queue<Due, std::vector<Due>, std::greater<Due>> deletions;
+  std::vector<char> deleted(n, 0);
+  auto remove_gang = [&](size_t i) {
+    if (deleted[i]) return;
+    deleted[i] = 1;
+    for (const auto& p : gangs[i].pods) {
+      try {
+        store.remove("pods", ns[i], p["metadata"]["name"].as_string());
+      } catch (const std::exception&) {
+      }
+    }
+    try {
+      store.remove("podgroups", ns[i], pg[i]);
+    } catch (const std::exception&) {
+    }
+  };
+
+  auto clock = sched.clock();
+  const int64_t t0 = clock->now_us();
+  size_t next = 0, done = 0;
+  int64_t last_arrival = t0;
+  for (;;) {
+    int64_t now = clock->now_us();
+    bool busy = false;
+    // Arrivals due now.
+    while (next < n && now >= t0 + offsets_us[next]) {
+      out.late_us += now - (t0 + offsets_us[next]);
+      OpenLoopGang& g = gangs[next];
+      out.gangs[next].create_us = clock->now_us();
+      store.create("podgroups", g.pod_group);
+      store.create_many("pods", g.pods);  // copies: the objects are needed again for deletion names
+      last_arrival = now;
+      ++next;
+      busy = true;
+      now = clock->now_us();
+    }
+    // Gangs that completed since the last poll.
+    for (const auto& r : sched.gang_records(true)) {
+      auto it = by_key.find(r.pg);
+      if (it == by_key.end()) continue;
+      auto& g = out.gangs[it->second];
+      if (g.bound_us) continue;
+      g.first_enqueue_us = r.first_enqueue_us;
+      g.admit_us = r.admit_us;
+      g.bound_us = r.bound_us;
+      deletions.push({r.bound_us + hold_us, it->second});
+      ++done;
+      busy = true;
+    }
+    // Departures due now.
+    while (!deletions.empty() && deletions.top().first <= now) {
+      remove_gang(deletions.top().second);
+      deletions.pop();
+      busy = true;
+    }
+    if (next == n && (done == n || now - last_arrival > timeout_us)) break;
+    if (!busy) {
+      int64_t wake = INT64_MAX;
+      if (next < n) wake = std::min(wake, t0 + offsets_us[next]);
+      if (!deletions.empty()) wake = std::min(wake, deletions.top().first);
+      // Completions are polled every ~50 us while gangs are in flight; the
+      // recorded timestamps come from the scheduler, so the poll period only
+      // delays deletions. Sleeping (not spinning) keeps the driver off the
+      // cores the scheduler's threads use.
+      if (done < next) wake = std::min(wake, now + 50);
+      int64_t d = std::clamp<int64_t>(wake - now, 10, 2000);
+      std::this_thread::sleep_for(std::chrono::microseconds(d));
+    }
+  }
+  out.wall_us = clock->now_us() - t0;
+  while (!deletions.empty()) {
+    remove_gang(deletions.top().second);
+    deletions.pop();
+  }
+  for (size_t i = 0; i < n; ++i) remove_gang(i);
+  return out;
+}
+
+}  // namespace xsched

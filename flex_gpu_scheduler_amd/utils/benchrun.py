@@ -88,14 +88,21 @@ class Shard:
         self.sched.stop()
 
 
-def gang_latency_summary(gangs: list[dict], sizes: dict[str, int] | None = None) -> dict:
-    """p50/p99 first-member-enqueue -> last-member-bound (ms) per group size."""
-    by: dict[int, list[float]] = {}
+def gang_latency_summary(gangs: list[dict], sizes: dict[str, int] | None = None, *, by_type: bool = False) -> dict:
+    """p50/p99 first-member-enqueue -> last-member-bound (ms) per group size.
+
+    With `by_type`, CPX quarter-GPU gangs (workload.make_wave names them
+    "<step>-q<i>") are keyed "cpx4" apart from whole-GPU gangs of 4: the wave
+    appends them after every whole-GPU gang, so in a burst they queue longest
+    and dominate the mixed size-4 p99."""
+    by: dict[str, list[float]] = {}
     for g in gangs:
-        sz = g["size"]
-        by.setdefault(sz, []).append((g["bound_us"] - g["first_enqueue_us"]) / 1000.0)
+        key = str(g["size"])
+        if by_type and "-q" in g.get("pod_group", "").rsplit("/", 1)[-1]:
+            key = "cpx4"
+        by.setdefault(key, []).append((g["bound_us"] - g["first_enqueue_us"]) / 1000.0)
     out = {}
-    for sz in sorted(by):
-        xs = by[sz]
-        out[str(sz)] = {"n": len(xs), "p50_ms": round(percentile(xs, 50), 3), "p99_ms": round(percentile(xs, 99), 3)}
+    for key in sorted(by, key=lambda k: (k.startswith("cpx"), int(k.lstrip("cpx")))):
+        xs = by[key]
+        out[key] = {"n": len(xs), "p50_ms": round(percentile(xs, 50), 3), "p99_ms": round(percentile(xs, 99), 3)}
     return out

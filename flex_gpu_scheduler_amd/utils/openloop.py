@@ -1,0 +1,98 @@
+"""Open-loop gang admission latency (bench.py `config.gang_admit_open_loop`).
+
+The headline step is a burst: a whole wave of gangs created at once, so the
+p99 gang-admit latency it reports is mostly the time a gang queues behind the
+rest of the burst (and the CPX quarter gangs, appended after the whole-GPU
+gangs in a wave, always queue longest: the "size-4 anomaly" of the burst
+numbers). This mode measures admission instead: gangs arrive one by one as a
+Poisson process at a fixed fraction of the shard's measured throughput, gang
+types interleaved at random (whole-GPU gangs of 1/2/4/8 ranks and CPX quarter
+gangs of 4 x 0.25 MI355X), and each gang is deleted a hold time after it is
+bound so the cluster stays at a steady occupancy. The native driver
+(csrc/scheduler/openloop.cc) paces arrivals and records, per gang:
+
+  enqueue_to_allow   first member enters the queue -> last member allowed at
+                     Permit (scheduler-internal; the reference's
+                     scheduler_permit_wait_duration_seconds family,
+                     vendor/.../scheduler/metrics/metrics.go:158-166)
+  create_to_bound    PodGroup + pods written -> last member bound (end to end)
+
+both as p50/p99 per gang type.
+"""
+from __future__ import annotations
+
+import json
+import random
+
+from ..models.mi355x import GPU, GPU_XCD
+from ..models.objects import make_container, make_pod, make_pod_group
+from .workload import ClusterSpec, percentile
+
+GANG_TYPES = ("1", "2", "4", "8", "cpx4")  # whole-GPU ranks, or a CPX quarter-GPU gang of 4
+
+
+def gang_objects(kind: str, name: str, ns: str, rng: random.Random) -> dict:
+    req = {"cpu": f"{rng.choice([500, 1000, 2000, 4000])}m", "memory": f"{rng.choice([2, 4, 8, 16])}Gi"}
+    if kind == "cpx4":
+        size, limits, cname = 4, {GPU_XCD: "2"}, "shard"
+    else:
+        size, limits, cname = int(kind), {GPU: "1"}, "trainer"
+    pods = [make_pod(f"{name}-r{r}", ns, containers=[make_container(cname, requests=req, limits=limits)],
+                     pod_group=name) for r in range(size)]
+    return {"podgroup": make_pod_group(name, ns, size), "pods": pods}
+
+
+def plan(spec: ClusterSpec, rate_pods_per_s: float, duration_s: float, seed: int = 0, ns: str = "openloop",
+         occupancy: float = 0.5) -> tuple[list[dict], list[str], list[int], int]:
+    """Gangs, their types, Poisson arrival offsets (us) and the hold time (us)
+    that keeps ~`occupancy` of the SPX GPUs busy at this arrival rate."""
+    rng = random.Random(seed)
+    mean_pods = sum(4 if t == "cpx4" else int(t) for t in GANG_TYPES) / len(GANG_TYPES)
+    gang_rate = rate_pods_per_s / mean_pods
+    n = max(1, int(gang_rate * duration_s))
+    kinds = [rng.choice(GANG_TYPES) for _ in range(n)]
+    t, offsets = 0.0, []
+    for _ in range(n):
+        t += rng.expovariate(gang_rate)
+        offsets.append(int(t * 1e6))
+    gangs = [gang_objects(k, f"ol{i}-{k}", ns, rng) for i, k in enumerate(kinds)]
+    # Whole-GPU GPU-seconds arriving per second on the SPX side.
+    whole = [int(k) for k in GANG_TYPES if k != "cpx4"]
+    spx_gpu_rate = gang_rate * (len(whole) / len(GANG_TYPES)) * (sum(whole) / len(whole))
+    hold_us = int(1e6 * occupancy * max(1, spec.spx_gpus) / max(spx_gpu_rate, 1e-9))
+    return gangs, kinds, offsets, max(100, hold_us)
+
+
+def _pct(xs: list[float]) -> dict:
+    if not xs:
+        return {"p50": None, "p99": None}
+    return {"p50": round(percentile(xs, 50), 3), "p99": round(percentile(xs, 99), 3)}
+
+
+def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -> dict:
+    out: dict = {}
+    for k in GANG_TYPES:
+        rows = [g for kk, g in zip(kinds, gangs) if kk == k]
+        ok = [g for g in rows if g["bound_us"]]
+        if not rows:
+            continue
+        e2a = [(g["admit_us"] - g["first_enqueue_us"]) / 1e3 for g in ok]
+        c2b = [(g["bound_us"] - g["create_us"]) / 1e3 for g in ok]
+        out[k] = {"n": len(rows), "unbound": len(rows) - len(ok),
+                  "enqueue_to_allow_ms": _pct(e2a), "create_to_bound_ms": _pct(c2b)}
+    n = len(gangs)
+    return {"by_gang": out, "gangs": n, "wall_s": round(wall_us / 1e6, 3),
+            "mean_arrival_lag_us": round(late_us / max(1, n), 1)}
+
+
+def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: int = 0,
+                  occupancy: float = 0.5) -> dict:
+    """One load level on `shard` (utils/benchrun.py Shard, idle)."""
+    from .._native import native
+
+    gangs, kinds, offsets, hold_us = plan(shard.spec, rate_pods_per_s, duration_s, seed, occupancy=occupancy)
+    res = native().run_open_loop(shard.store, shard.sched, json.dumps(gangs), offsets, hold_us, 10_000_000)
+    shard.sched.wait_idle(10_000)
+    out = summarize(kinds, res["gangs"], res["wall_us"], res["late_us"])
+    out.update({"offered_pods_per_s": round(rate_pods_per_s, 1), "hold_ms": round(hold_us / 1e3, 3)})
+    return out

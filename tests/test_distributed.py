@@ -62,6 +62,12 @@ def test_bench_launches_its_own_ranks():
     assert sorted(g2["gpus"]) == [0, 1] and sorted(g2["ordinals"]) == [0, 1]
     assert g2["placed"]["ranks"] == [0, 1] and all(x["correct"] for x in g2["placed"]["results"])
     assert pl["summary"]["2"]["all_correct"]
+    # Untimed open-loop admission latency, by interleaved gang type.
+    ol = d["config"]["gang_admit_open_loop"]
+    assert ol["capacity_pods_per_s"] > 0
+    for load in ("load_50", "load_90"):
+        assert set(ol[load]["by_gang"]) <= {"1", "2", "4", "8", "cpx4"} and ol[load]["gangs"] > 0
+    assert "cpx4" in d["config"]["gang_admit_by_type"]
 
 
 def test_bench_refuses_world_size_mismatch():

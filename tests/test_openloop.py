@@ -1,0 +1,59 @@
+"""Open-loop gang admission (utils/openloop.py, csrc/scheduler/openloop.cc)."""
+import json
+
+from flex_gpu_scheduler_amd.utils.benchrun import Shard, gang_latency_summary
+from flex_gpu_scheduler_amd.utils.openloop import GANG_TYPES, plan, run_open_loop
+from flex_gpu_scheduler_amd.utils.workload import ClusterSpec
+
+
+def test_plan_interleaves_types_and_sizes_hold():
+    spec = ClusterSpec(nodes=16)
+    gangs, kinds, offsets, hold_us = plan(spec, 4000.0, 1.0, seed=3)
+    assert len(gangs) == len(kinds) == len(offsets) > 500
+    assert offsets == sorted(offsets) and offsets[-1] < 1.5e6
+    assert set(kinds) == set(GANG_TYPES)
+    # Interleaved: CPX gangs are not all at the tail.
+    first_cpx = kinds.index("cpx4")
+    assert first_cpx < len(kinds) // 10
+    names = [g["podgroup"]["metadata"]["name"] for g in gangs]
+    assert len(set(names)) == len(names)
+    for g, k in zip(gangs, kinds):
+        assert len(g["pods"]) == (4 if k == "cpx4" else int(k)) == g["podgroup"]["spec"]["minMember"]
+    # Occupancy 0.5 of 96 SPX GPUs at the whole-GPU GPU-seconds arrival rate.
+    gang_rate = 4000.0 / 3.8
+    assert abs(hold_us - 0.5 * 96 / (gang_rate * 0.8 * 3.75) * 1e6) < 1000
+
+
+def test_open_loop_admits_every_gang_with_ordered_timeline():
+    sh = Shard(ClusterSpec(nodes=16), namespace="b")
+    try:
+        gangs, kinds, offsets, hold_us = plan(sh.spec, 2000.0, 0.3, seed=1)
+        from flex_gpu_scheduler_amd._native import native
+
+        res = native().run_open_loop(sh.store, sh.sched, json.dumps(gangs), offsets, hold_us, 5_000_000)
+        assert len(res["gangs"]) == len(gangs)
+        for g, k in zip(res["gangs"], kinds):
+            assert g["bound_us"] > 0, g
+            assert g["create_us"] <= g["first_enqueue_us"] <= g["admit_us"] <= g["bound_us"]
+            assert g["size"] == (4 if k == "cpx4" else int(k))
+        # Every gang was deleted again: the cluster is empty afterwards.
+        sh.sched.wait_idle(10_000)
+        assert sh.sched.wait_cache_empty(10.0)
+        assert sh.store.count("pods") == 0 and sh.store.count("podgroups") == 0
+        out = run_open_loop(sh, 1500.0, duration_s=0.2, seed=2)
+        assert out["gangs"] > 0 and all(v["unbound"] == 0 for v in out["by_gang"].values())
+        for v in out["by_gang"].values():
+            assert v["create_to_bound_ms"]["p99"] >= v["create_to_bound_ms"]["p50"] > 0
+    finally:
+        sh.close()
+
+
+def test_burst_summary_splits_cpx_gangs():
+    recs = [{"pod_group": "ns/s1-g3-x4", "size": 4, "first_enqueue_us": 0, "bound_us": 1000},
+            {"pod_group": "ns/s1-q1", "size": 4, "first_enqueue_us": 0, "bound_us": 9000},
+            {"pod_group": "ns/s1-g1-x1", "size": 1, "first_enqueue_us": 0, "bound_us": 500}]
+    mixed = gang_latency_summary(recs)
+    assert mixed["4"]["n"] == 2
+    typed = gang_latency_summary(recs, by_type=True)
+    assert list(typed) == ["1", "4", "cpx4"]
+    assert typed["4"]["p99_ms"] == 1.0 and typed["cpx4"]["p99_ms"] == 9.0
