@@ -300,9 +300,8 @@ std::vector<int> parse_int_list(const std::string& s) {
 }
 }  // namespace
 
-void Pod::recompute_gpu_assignment() {
+void Pod::recompute_gpu_assignment(const GpuNames& gn) {
   gpu = GpuAssignment{};
-  const GpuNames& gn = gpu_names();
   const std::string* idx = meta.annotation(gn.index_annotation);
   if (!idx) return;
   std::vector<int> gpus = parse_int_list(*idx);
@@ -356,7 +355,7 @@ uint64_t pg_key_of(std::string_view full) {
   return h ? h : 1;
 }
 
-std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
+std::shared_ptr<Pod> Pod::from_json(const Json& obj, const GpuNames& gn) {
   auto p = std::make_shared<Pod>();
   p->meta = ObjectMeta::from_json(obj);
   const Json& spec = obj["spec"];
@@ -453,8 +452,8 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj) {
     p->pod_group = *pg;
     p->pg_key = pg_key_of(p->pg_full_name());
   }
-  p->gpu_demand = compute_gpu_demand(*p);
-  p->recompute_gpu_assignment();
+  p->gpu_demand = compute_gpu_demand(*p, gn);
+  p->recompute_gpu_assignment(gn);
   return p;
 }
 
@@ -492,7 +491,7 @@ bool pod_matches_node_selector_and_affinity(const Pod& p, const Node& n) {
   return false;
 }
 
-std::shared_ptr<Node> Node::from_json(const Json& obj) {
+std::shared_ptr<Node> Node::from_json(const Json& obj, const GpuNames& gn) {
   auto n = std::make_shared<Node>();
   n->meta = ObjectMeta::from_json(obj);
   const Json& spec = obj["spec"];
@@ -513,7 +512,6 @@ std::shared_ptr<Node> Node::from_json(const Json& obj) {
     for (const auto& nm : ci.names) n->image_sizes.emplace(nm, ci.size_bytes);
     n->images.push_back(std::move(ci));
   }
-  const GpuNames& gn = gpu_names();
   int gid = gn.gpu_id();
   n->gpu_count = n->allocatable.has(gid) ? static_cast<int>(n->allocatable.get(gid)) : 0;
   int parts = 1;
@@ -643,19 +641,34 @@ std::shared_ptr<PriorityClass> PriorityClass::from_json(const Json& obj) {
 }
 
 // ------------------------------------------------------------ GPU names ----
-GpuNames& gpu_names() {
-  static GpuNames* g = new GpuNames();
+const GpuNames& default_gpu_names() {
+  static const GpuNames* g = new GpuNames();
   return *g;
 }
-void GpuNames::refresh() const {
+void GpuNames::intern() {
   gpu_rid_ = res_id(gpu);
   mem_rid_ = res_id(memory);
   xcd_rid_ = res_id(xcd);
-  ids_ready_ = true;
+}
+std::shared_ptr<const GpuNames> GpuNames::from_args(const Json& args) {
+  auto g = std::make_shared<GpuNames>();
+  auto take = [&](const char* key, std::string& field) {
+    if (args[key].is_string() && !args[key].as_string().empty()) field = args[key].as_string();
+  };
+  take("gpuResourceName", g->gpu);
+  take("memoryResourceName", g->memory);
+  take("xcdResourceName", g->xcd);
+  take("indexAnnotationKey", g->index_annotation);
+  take("partitionAnnotationKey", g->partition_annotation);
+  g->intern();
+  return g;
+}
+std::string GpuNames::describe() const {
+  return "gpu=" + gpu + " memory=" + memory + " xcd=" + xcd + " index=" + index_annotation +
+         " partitions=" + partition_annotation;
 }
 
-GpuDemand compute_gpu_demand(const Pod& p) {
-  const GpuNames& gn = gpu_names();
+GpuDemand compute_gpu_demand(const Pod& p, const GpuNames& gn) {
   int gid = gn.gpu_id(), mid = gn.memory_id(), xid = gn.xcd_id();
   bool has_g = false, has_m = false, has_x = false;
   for (const auto& c : p.containers) {  // presence per container limit (podResourceLimit)

@@ -220,6 +220,9 @@ struct RelaxedI64 {
   operator int64_t() const { return v.load(std::memory_order_relaxed); }  // NOLINT
 };
 
+struct GpuNames;
+const GpuNames& default_gpu_names();
+
 struct Pod {
   ObjectMeta meta;
   IStr scheduler_name = kDefaultSchedulerName;
@@ -272,8 +275,8 @@ struct Pod {
   bool terminating() const { return meta.deletion != 0; }
   std::string pg_full_name() const { return pod_group.empty() ? std::string() : meta.ns + "/" + pod_group; }
 
-  static std::shared_ptr<Pod> from_json(const Json& obj);
-  void recompute_gpu_assignment();
+  static std::shared_ptr<Pod> from_json(const Json& obj, const GpuNames& gn = default_gpu_names());
+  void recompute_gpu_assignment(const GpuNames& gn = default_gpu_names());
 };
 using PodPtr = std::shared_ptr<Pod>;
 
@@ -300,7 +303,7 @@ struct Node {
   std::vector<int> gpu_numa;        // NUMA node per GPU (-1 unknown)
   int64_t gpu_memory_per_gpu = 0;   // memory slice units per physical GPU
   const std::string& name() const { return meta.name; }
-  static std::shared_ptr<Node> from_json(const Json& obj);
+  static std::shared_ptr<Node> from_json(const Json& obj, const GpuNames& gn = default_gpu_names());
 };
 using NodePtr = std::shared_ptr<Node>;
 
@@ -381,7 +384,13 @@ struct PriorityClass {
 };
 using PriorityClassPtr = std::shared_ptr<PriorityClass>;
 
-// Global GPU naming used by pod/node parsing (configured by FlexGPU args).
+// GPU resource and annotation names used by pod/node parsing and the GPU
+// plugins. Immutable once built; each Scheduler owns one, built from its
+// profiles' FlexGPU args (the reference's package constants,
+// pkg/flexgpu/flex_gpu.go:18-19, made configurable), and hands it to its
+// informers, cache and plugins through the Handle. Two schedulers in one
+// process may use different names; profiles of one scheduler share a cache
+// (one GPU ledger per node), so they must agree.
 struct GpuNames {
   std::string gpu = "amd.com/gpu";
   std::string memory = "amd.com/gpu-memory";
@@ -390,29 +399,27 @@ struct GpuNames {
   std::string partition_annotation = "amd.com/gpu-partitions";
   std::string partition_label = "amd.com/gpu.compute-partition";     // spx|dpx|qpx|cpx
   std::string topology_annotation = "amd.com/gpu-topology";          // JSON, per-GPU detail
-  // Resource ids are interned once per name change (hot paths call these
-  // per node per pod).
-  int gpu_id() const {
-    if (!ids_ready_) refresh();
-    return gpu_rid_;
+
+  GpuNames() { intern(); }
+  // FlexGPU args (gpuResourceName, memoryResourceName, xcdResourceName,
+  // indexAnnotationKey, partitionAnnotationKey) over the defaults.
+  static std::shared_ptr<const GpuNames> from_args(const Json& args);
+  bool operator==(const GpuNames& o) const {
+    return gpu == o.gpu && memory == o.memory && xcd == o.xcd && index_annotation == o.index_annotation &&
+           partition_annotation == o.partition_annotation;
   }
-  int memory_id() const {
-    if (!ids_ready_) refresh();
-    return mem_rid_;
-  }
-  int xcd_id() const {
-    if (!ids_ready_) refresh();
-    return xcd_rid_;
-  }
-  void invalidate() { ids_ready_ = false; }
+  std::string describe() const;
+  // Interned resource ids (hot paths use these per node per pod).
+  int gpu_id() const { return gpu_rid_; }
+  int memory_id() const { return mem_rid_; }
+  int xcd_id() const { return xcd_rid_; }
 
  private:
-  void refresh() const;
-  mutable int gpu_rid_ = -1, mem_rid_ = -1, xcd_rid_ = -1;
-  mutable bool ids_ready_ = false;
+  void intern();
+  int gpu_rid_ = -1, mem_rid_ = -1, xcd_rid_ = -1;
 };
-GpuNames& gpu_names();
-GpuDemand compute_gpu_demand(const Pod& p);
+const GpuNames& default_gpu_names();
+GpuDemand compute_gpu_demand(const Pod& p, const GpuNames& gn = default_gpu_names());
 int partitions_for_mode(const std::string& mode);  // spx=1 dpx=2 qpx=4 cpx=8 (0 unknown)
 
 }  // namespace xsched

@@ -79,6 +79,7 @@ struct Handle {
   TimerService* timers = nullptr;
   Metrics* metrics = nullptr;
   const Snapshot* snapshot = nullptr;  // the scheduling cycle's snapshot
+  const GpuNames* gpu_names = &default_gpu_names();  // the scheduler's (types.h)
   // Moves these pods (when queued as unschedulable or backing off) to the
   // active queue; callable from any thread (e.g. a plugin's timer).
   std::function<void(const std::vector<PodPtr>&)> activate;

@@ -118,9 +118,9 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       return;
     }
     // pods: FilteringResourceEventHandler over assigned pods.
-    auto np = Pod::from_json(*obj);
+    auto np = Pod::from_json(*obj, *h_.gpu_names);
     bool now_assigned = !np->node_name.empty();
-    PodPtr op = old ? Pod::from_json(*old) : nullptr;
+    PodPtr op = old ? Pod::from_json(*old, *h_.gpu_names) : nullptr;
     bool was_assigned = op && !op->node_name.empty();
     std::lock_guard<std::mutex> g(mu_);
     if (t == EventType::Deleted) {

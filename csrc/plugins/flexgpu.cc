@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <string>
 
+#include "common/log.h"
 #include "framework/plugin.h"
 #include "scheduler/cache.h"
 
@@ -173,21 +174,16 @@ class FlexGPU : public Plugin {
   // Filter/Score read only the node's GPU ledger, allocatable and the pod's demand.
   bool filter_node_local(const Pod&, const Snapshot&) const override { return true; }
   bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
-  FlexGPU(const Json& args, Handle& h) : Plugin("FlexGPU", kFilter | kScore | kReserve | kBind), h_(h) {
-    GpuNames& gn = gpu_names();
-    if (args["gpuResourceName"].is_string()) gn.gpu = args["gpuResourceName"].as_string();
-    if (args["memoryResourceName"].is_string()) gn.memory = args["memoryResourceName"].as_string();
-    if (args["xcdResourceName"].is_string()) gn.xcd = args["xcdResourceName"].as_string();
-    if (args["indexAnnotationKey"].is_string()) gn.index_annotation = args["indexAnnotationKey"].as_string();
-    if (args["partitionAnnotationKey"].is_string()) gn.partition_annotation = args["partitionAnnotationKey"].as_string();
-    gn.invalidate();
-  }
+  // Resource/annotation names come from the scheduler (GpuNames::from_args
+  // of this plugin's args, checked equal across profiles in Scheduler()).
+  FlexGPU(const Json&, Handle& h) : Plugin("FlexGPU", kFilter | kScore | kReserve | kBind), h_(h), gn_(*h.gpu_names) {}
 
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
     const Demand& d = p.gpu_demand;
+    if (XS_V(6)) log_filter(p, ni);
     if (d.kind == Demand::None) return {};
     if (d.kind == Demand::Conflict) return Status::unresolvable("pod conflict resources");
-    const GpuNames& gn = gpu_names();
+    const GpuNames& gn = gn_;
     int gid = gn.gpu_id();
     int kid = d.kind == Demand::Gpu ? gid : d.kind == Demand::Xcd ? gn.xcd_id() : gn.memory_id();
     if (!ni.allocatable.has(gid) || !ni.allocatable.has(kid)) return Status::unresolvable("unknown resource type");
@@ -195,6 +191,23 @@ class FlexGPU : public Plugin {
     if (ni.requested.get(kid) + d.amount > ni.allocatable.get(kid)) return failure(kid, false);
     if (!fits(ni.gpu, d)) return failure(kid, true);
     return {};
+  }
+
+  // V(6) dump of the pod's limits and the node's GPU ledger, as the
+  // reference's Filter does (pkg/flexgpu/flex_gpu.go:42-50,103-107).
+  void log_filter(const Pod& p, const NodeInfo& ni) const {
+    XS_LOGV(6, "pod info").kv("point", "filter").kv("pod", p.key()).kv("node", ni.name());
+    for (const auto& c : p.containers)
+      for (int id : {gn_.gpu_id(), gn_.xcd_id(), gn_.memory_id()})
+        if (c.limits.has(id))
+          XS_LOGV(6, "resource limit").kv("container", c.name).kv(ResourceRegistry::get().name(id), c.limits.get(id));
+    const GpuLedger& L = ni.gpu;
+    for (int g = 0; g < L.gpu_count; ++g) {
+      const auto& f = L.free[g];
+      XS_LOGV(6, "node gpu usages").kv("node", ni.name()).kv("gpu", g).kv("partitions", L.parts[g])
+          .kv("wholeFree", f.whole).kv("freeSlots", f.free_slots).kv("freeXcds", f.xcds).kv("freeMemory", f.mem)
+          .kv("numa", g < static_cast<int>(L.numa.size()) ? L.numa[g] : -1);
+    }
   }
 
   // Prebuilt per resource id (Filter fails on most nodes of a busy cluster).
@@ -268,7 +281,9 @@ class FlexGPU : public Plugin {
     if (!ni) return Status::error("getting node \"" + node + "\" from Snapshot");
     Placement pl = place(ni->gpu, d);
     if (!pl.ok()) return Status::unschedulable("allocate index fail");
-    const GpuNames& gn = gpu_names();
+    XS_LOGV(6, "assigned gpu indexes").kv("pod", p->key()).kv("node", node).kv("indexes", join_ints(pl.gpus))
+        .kv("partitions", join_parts(pl.parts));
+    const GpuNames& gn = gn_;
     auto st = std::make_shared<AssignmentState>();
     st->annotations.set(gn.index_annotation, Json(join_ints(pl.gpus)));
     if (!pl.parts.empty()) st->annotations.set(gn.partition_annotation, Json(join_parts(pl.parts)));
@@ -289,7 +304,7 @@ class FlexGPU : public Plugin {
   }
 
   void unreserve(CycleState& s, const PodPtr& p, const std::string&) override {
-    const GpuNames& gn = gpu_names();
+    const GpuNames& gn = gn_;
     s.erase(kFlexGPUStateKey);
     if (!h_.cache->is_assumed(p->uid())) return;
     h_.cache->mutate_pod(p->uid(), [&](Pod& cp) {
@@ -317,6 +332,7 @@ class FlexGPU : public Plugin {
 
  private:
   Handle& h_;
+  const GpuNames& gn_;
 };
 
 PluginRegistrar reg("FlexGPU", [](const Json& a, Handle& h) { return std::make_shared<FlexGPU>(a, h); });

@@ -28,6 +28,7 @@
 #include <cmath>
 #include <map>
 
+#include "common/log.h"
 #include "framework/plugin.h"
 #include "scheduler/cache.h"
 #include "scheduler/informers.h"
@@ -82,7 +83,7 @@ class TopologyMatch : public Plugin {
 
   std::vector<NumaNode> numa_list(const NodeResourceTopology& nrt, const NodeInfo& ni) const {
     std::vector<NumaNode> out = nrt.numa;  // precomputed at parse time
-    const GpuNames& gn = gpu_names();
+    const GpuNames& gn = *h_.gpu_names;
     int gid = gn.gpu_id(), xid = gn.xcd_id(), mid = gn.memory_id();
     const GpuLedger& L = ni.gpu;
     for (auto& n : out) {
@@ -147,9 +148,9 @@ class TopologyMatch : public Plugin {
   }
 
   // Allocation-free resourcesAvailableInAnyNUMANodes for one request vector.
-  static bool fits_fast(const NodeResourceTopology& nrt, const NodeInfo& ni, const Res& req, QoS qos) {
+  bool fits_fast(const NodeResourceTopology& nrt, const NodeInfo& ni, const Res& req, QoS qos) const {
     if (nrt.numa.size() > 64) return true;
-    const GpuNames& gn = gpu_names();
+    const GpuNames& gn = *h_.gpu_names;
     int gid = gn.gpu_id(), xid = gn.xcd_id(), mid = gn.memory_id();
     LiveGpu live;
     bool live_ready = false;
@@ -185,6 +186,27 @@ class TopologyMatch : public Plugin {
   }
 
   Status filter(CycleState&, const Pod& p, const NodeInfo& ni) override {
+    Status st = filter_impl(p, ni);
+    if (XS_V(6)) log_filter(p, ni, st);
+    return st;
+  }
+
+  // V(6): the node's NUMA zones with live GPU availability and the verdict
+  // (the reference logs the same at V(6), pkg/noderesourcetopology/filter.go).
+  void log_filter(const Pod& p, const NodeInfo& ni, const Status& st) const {
+    if (ni.nrt) {
+      const auto& reg = ResourceRegistry::get();
+      for (const auto& n : numa_list(*ni.nrt, ni)) {
+        Json avail = Json::object();
+        for (const auto& [id, v] : n.res) avail.set(reg.name(id), Json(v));
+        XS_LOGV(6, "numa zone").kv("node", ni.name()).kv("numa", n.id).kv("available", std::move(avail));
+      }
+    }
+    XS_LOGV(6, "topology filter").kv("pod", p.key()).kv("node", ni.name()).kv("fits", st.is_success())
+        .kv("reason", st.is_success() ? std::string() : st.message());
+  }
+
+  Status filter_impl(const Pod& p, const NodeInfo& ni) const {
     if (!ni.node) return Status::error("node not found");
     if (p.qos == QoS::BestEffort) return {};
     const NodeResourceTopology* nrt = ni.nrt.get();

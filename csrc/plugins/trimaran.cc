@@ -130,7 +130,7 @@ class TrimaranBase : public Plugin {
       return;
     }
     // Pod-assign cache over assigned pods (handler.go:68-101).
-    auto np = Pod::from_json(*obj);
+    auto np = Pod::from_json(*obj, *h_.gpu_names);
     if (np->node_name.empty()) return;
     Shard& sh = shard(np->node_name);
     std::unique_lock<std::shared_mutex> g(sh.mu);
@@ -245,7 +245,7 @@ class TargetLoadPacking : public TrimaranBase {
   // PredictUtilisation (targetloadpacking.go:286-294).
   int64_t predict(const Container& c) const {
     if (gpu_mode_) {
-      int gid = gpu_names().gpu_id();
+      int gid = h_.gpu_names->gpu_id();
       return c.limits.has(gid) ? c.limits.get(gid) * 1000 : 0;  // milli-GPUs
     }
     if (c.limits.has(kCPU)) return c.limits.get(kCPU);
@@ -273,7 +273,7 @@ class TargetLoadPacking : public TrimaranBase {
         found = true;
       }
     if (!found) return {kMinNodeScore, {}};
-    double cap = gpu_mode_ ? static_cast<double>(ni.node->capacity.get(gpu_names().gpu_id()) * 1000)
+    double cap = gpu_mode_ ? static_cast<double>(ni.node->capacity.get(h_.gpu_names->gpu_id()) * 1000)
                            : static_cast<double>(ni.node->capacity.get(kCPU));
     double used = util / 100.0 * cap;
     int64_t missing = 0;
@@ -380,7 +380,7 @@ class LoadVariationRiskBalancing : public TrimaranBase {
     }
     // GPU dimensions: capacity = the node's GPUs, the pod's request = its
     // GPUs (a GPU pod can drive its devices' engines, HBM and links fully).
-    int gid = gpu_names().gpu_id();
+    int gid = h_.gpu_names->gpu_id();
     auto gpu_dim = [&](MType type, int slot) {
       if (!resource_data(it->second, type, &avg, &sd)) return;
       ResourceStats rs;

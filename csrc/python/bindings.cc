@@ -17,6 +17,7 @@
 #include "common/quantity.h"
 #include "rest/kube.h"
 #include "scheduler/openloop.h"
+#include "common/log.h"
 #include "scheduler/scheduler.h"
 #include "store/store.h"
 #include "telemetry/amdsmi_sampler.h"
@@ -299,15 +300,12 @@ PYBIND11_MODULE(_xsched, m) {
   m.def("rfc3339", [](int64_t us) { return format_rfc3339(us); });
   m.def("native_waiters", [] { return g_native_waiters.load(); });
   m.def("parse_rfc3339", [](const std::string& s) { return parse_rfc3339(s); });
-  m.def("set_gpu_names", [](py::dict d) {
-    GpuNames& g = gpu_names();
-    if (d.contains("gpu")) g.gpu = d["gpu"].cast<std::string>();
-    if (d.contains("memory")) g.memory = d["memory"].cast<std::string>();
-    if (d.contains("xcd")) g.xcd = d["xcd"].cast<std::string>();
-    if (d.contains("index_annotation")) g.index_annotation = d["index_annotation"].cast<std::string>();
-    if (d.contains("partition_annotation")) g.partition_annotation = d["partition_annotation"].cast<std::string>();
-    g.invalidate();
-  });
+  // ---- native logging (common/log.h) ----
+  m.def("set_log_verbosity", &xsched::log::set_verbosity, py::arg("v"));
+  m.def("log_verbosity", &xsched::log::verbosity);
+  m.def("set_log_json", &xsched::log::set_json, py::arg("json"));
+  m.def("set_log_capture", &xsched::log::set_capture, py::arg("max_lines"));
+  m.def("drain_log", &xsched::log::drain_captured);
 
   // ---- clock ----
   py::class_<FakeClock, std::shared_ptr<FakeClock>>(m, "FakeClock")

@@ -272,7 +272,7 @@ PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<vo
   if (it == pod_states_.end()) return nullptr;
   auto fresh = std::make_shared<Pod>(*it->second.pod);
   fn(*fresh);
-  fresh->recompute_gpu_assignment();
+  fresh->recompute_gpu_assignment(*gpu_names_);
   remove_pod_locked(it->second.pod);
   add_pod_locked(fresh);
   it->second.pod = fresh;
@@ -291,7 +291,7 @@ PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::f
       NodeInfo& ni = writable(nit->second);
       ni.gpu.apply(pod->gpu, -1);
       fn(*pod);
-      pod->recompute_gpu_assignment();
+      pod->recompute_gpu_assignment(*gpu_names_);
       ni.gpu.apply(pod->gpu, +1);
       mark_dirty(pod->node_name);
       in_place_ = false;

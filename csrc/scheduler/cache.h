@@ -31,6 +31,9 @@ namespace xsched {
 class SchedulerCache {
  public:
   SchedulerCache(std::shared_ptr<Clock> clock, int64_t assumed_ttl_us);
+  // The owning scheduler's GPU names (re-deriving a mutated pod's GPU
+  // assignment); must outlive the cache.
+  void set_gpu_names(const GpuNames* gn) { gpu_names_ = gn; }
 
   void add_node(const NodePtr& n);
   void update_node(const NodePtr& n);
@@ -117,6 +120,7 @@ class SchedulerCache {
 
   std::shared_ptr<Clock> clock_;
   int64_t ttl_us_;
+  const GpuNames* gpu_names_ = &default_gpu_names();
   mutable std::mutex mu_;
   std::unordered_map<std::string, NodeInfoPtr> nodes_;
   std::vector<std::string> order_;  // node names with a Node object, insertion order

@@ -1,5 +1,7 @@
 #include "scheduler/scheduler.h"
 
+#include "common/log.h"
+
 #include <algorithm>
 #include <chrono>
 #include <thread>
@@ -185,6 +187,19 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     extenders_.push_back(std::make_shared<Extender>(ExtenderConfig::from_json(ej)));
   const auto& profiles = config["profiles"].items();
   if (profiles.empty()) throw std::runtime_error("scheduler config has no profiles");
+  // GPU names: every profile's FlexGPU args must agree (one cache, one GPU
+  // ledger per node); other schedulers in the process are unaffected.
+  for (const auto& pj : profiles) {
+    const Json* args = pj["pluginConfig"].get("FlexGPU");
+    if (!args) continue;
+    auto gn = GpuNames::from_args(*args);
+    if (!gpu_names_) gpu_names_ = gn;
+    else if (!(*gn == *gpu_names_))
+      throw std::runtime_error("FlexGPU resource names differ between profiles of one scheduler (" +
+                               gpu_names_->describe() + " vs " + gn->describe() + ")");
+  }
+  if (!gpu_names_) gpu_names_ = std::make_shared<GpuNames>();
+  cache_->set_gpu_names(gpu_names_.get());
   for (const auto& pj : profiles) {
     ProfileConfig pc = ProfileConfig::from_json(pj);
     if (pc.percentage_of_nodes_to_score == 0) pc.percentage_of_nodes_to_score = opts_.percentage_of_nodes_to_score;
@@ -203,6 +218,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.metrics = metrics_.get();
     h.snapshot = &snapshot_;
     h.extenders = &extenders_;
+    h.gpu_names = gpu_names_.get();
     h.lookup = [this](const std::string& kind, const std::string& ns, const std::string& name) {
       return store_->get(kind, ns, name);
     };
@@ -352,7 +368,7 @@ void Scheduler::informer_loop() {
         if (ev.kind != "pods" || ev.type == EventType::Deleted) continue;
         try {
           if (ev.type == EventType::Modified) parsed[hi - 1] = bound_copy_of_assumed(ev);
-          if (!parsed[hi - 1]) parsed[hi - 1] = Pod::from_json(*ev.obj);
+          if (!parsed[hi - 1]) parsed[hi - 1] = Pod::from_json(*ev.obj, *gpu_names_);
         } catch (const std::exception&) {
           continue;
         }
@@ -429,7 +445,29 @@ void Scheduler::handle_event(const WatchEvent& ev) {
     }
   } catch (const std::exception& e) {
     // A malformed object must not kill the informer thread.
-    metrics_->inc("xsched_informer_errors_total", "kind=\"" + ev.kind + "\"");
+    report_informer_error(ev, e.what());
+  }
+}
+
+// The object is dropped from the scheduler's view: say so (log line and, for
+// pods and nodes, a Warning event on the object) so that, e.g., a pod naming
+// a 65th distinct resource does not just silently stay Pending.
+void Scheduler::report_informer_error(const WatchEvent& ev, const char* what) {
+  metrics_->inc("xsched_informer_errors_total", "kind=\"" + ev.kind + "\"");
+  std::string ns, name;
+  if (ev.obj) {
+    const Json& md = (*ev.obj)["metadata"];
+    ns = md["namespace"].str_or("");
+    name = md["name"].str_or("");
+  }
+  XS_WARN("informer dropped object").kv("kind", ev.kind).kv("namespace", ns).kv("name", name).kv("err", what);
+  if (name.empty() || ev.type == EventType::Deleted) return;
+  if (ev.kind == "pods" || ev.kind == "nodes") {
+    try {
+      client_->record_event(ev.kind == "pods" ? "Pod" : "Node", ns, name, "Warning", "FailedToDecode",
+                            std::string("scheduler cannot use this object: ") + what);
+    } catch (const std::exception&) {
+    }
   }
 }
 
@@ -441,7 +479,7 @@ void Scheduler::handle_pod_event(const WatchEvent& ev) {
     const Json& md = (*ev.obj)["metadata"];
     PodPtr p = informers_->pod(md["namespace"].as_string(), md["name"].as_string());
     if (!p || p->uid() != md["uid"].as_string() || p->node_name != (*ev.obj)["spec"]["nodeName"].as_string())
-      p = Pod::from_json(*ev.obj);
+      p = Pod::from_json(*ev.obj, *gpu_names_);
     informers_->delete_pod(*p);
     if (!p->node_name.empty()) {
       cache_->remove_pod(*p);
@@ -461,7 +499,7 @@ void Scheduler::handle_pod_event(const WatchEvent& ev) {
     return;
   }
   PodPtr np = ev.type == EventType::Modified ? bound_copy_of_assumed(ev) : nullptr;
-  if (!np) np = Pod::from_json(*ev.obj);
+  if (!np) np = Pod::from_json(*ev.obj, *gpu_names_);
   PodPtr old = informers_->pod(np->ns(), np->name());
   informers_->upsert_pod(np);
   apply_pod_update(ev, np, old);
@@ -505,8 +543,8 @@ void Scheduler::handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, 
   try {
     for (auto& fw : frameworks_) fw->dispatch_object_event("pods", static_cast<int>(ev.type), ev.obj, ev.old);
     apply_pod_update(ev, np, std::move(old));
-  } catch (const std::exception&) {
-    metrics_->inc("xsched_informer_errors_total", "kind=\"pods\"");
+  } catch (const std::exception& e) {
+    report_informer_error(ev, e.what());
   }
 }
 
@@ -553,17 +591,17 @@ void Scheduler::apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr 
 void Scheduler::handle_node_event(const WatchEvent& ev) {
   for (auto& fw : frameworks_) fw->dispatch_object_event("nodes", static_cast<int>(ev.type), ev.obj, ev.old);
   if (ev.type == EventType::Deleted) {
-    auto n = Node::from_json(*ev.obj);
+    auto n = Node::from_json(*ev.obj, *gpu_names_);
     cache_->remove_node(n->name());
     return;
   }
-  auto n = Node::from_json(*ev.obj);
+  auto n = Node::from_json(*ev.obj, *gpu_names_);
   if (ev.type == EventType::Added || !ev.old) {
     cache_->add_node(n);
     queue_->move_all_to_active_or_backoff(ClusterEvent{"Node", kAdd, "NodeAdd"});
     return;
   }
-  auto o = Node::from_json(*ev.old);
+  auto o = Node::from_json(*ev.old, *gpu_names_);
   cache_->update_node(n);
   uint32_t action = 0;
   if (!(o->allocatable == n->allocatable)) action |= kUpdateNodeAllocatable;
@@ -1348,7 +1386,7 @@ Json Scheduler::dump_cache() const {
 Json Scheduler::explain(const Json& pod_obj) {
   std::lock_guard<std::mutex> g(sched_mu_);
   Json out = Json::object();
-  auto pod = Pod::from_json(pod_obj);
+  auto pod = Pod::from_json(pod_obj, *gpu_names_);
   Framework* fw = framework_for(pod->scheduler_name);
   if (!fw) {
     out.set("error", Json("no profile for schedulerName " + pod->scheduler_name.str()));
@@ -1414,7 +1452,7 @@ Json Scheduler::explain(const Json& pod_obj) {
 
 double Scheduler::score_benchmark(const Json& pod_obj, int iterations, Json* out) {
   std::lock_guard<std::mutex> g(sched_mu_);
-  auto pod = Pod::from_json(pod_obj);
+  auto pod = Pod::from_json(pod_obj, *gpu_names_);
   Framework* fw = framework_for(pod->scheduler_name);
   if (!fw) throw std::runtime_error("no profile for schedulerName " + pod->scheduler_name.str());
   cache_->update_snapshot(snapshot_);

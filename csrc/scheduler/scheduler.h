@@ -210,6 +210,7 @@ class Scheduler {
   void informer_loop();
   void handle_event(const WatchEvent& ev);
   void handle_pod_event(const WatchEvent& ev);
+  void report_informer_error(const WatchEvent& ev, const char* what);
   void handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, PodPtr old);
   PodPtr bound_copy_of_assumed(const WatchEvent& ev);
   void apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr old);
@@ -272,6 +273,7 @@ class Scheduler {
   std::unique_ptr<SchedulingQueue> queue_;
   std::shared_ptr<ApiClient> client_;
   ExtenderList extenders_;
+  std::shared_ptr<const GpuNames> gpu_names_;  // from the profiles' FlexGPU args
   std::vector<std::unique_ptr<WaitingPods>> waiting_;
   std::vector<std::unique_ptr<Framework>> frameworks_;
   std::unordered_map<std::string, Framework*> by_name_;

@@ -33,10 +33,35 @@ log = logging.getLogger("xsched")
 
 
 # ------------------------------------------------------------------ helpers
-def _setup_logging(v: int) -> None:
+class JsonLogFormatter(logging.Formatter):
+    """One JSON object per line, every field escaped by json.dumps (the
+    native core writes the same shape, csrc/common/log.cc)."""
+
+    def format(self, record: logging.LogRecord) -> str:
+        d = {"ts": self.formatTime(record), "level": record.levelname, "logger": record.name,
+             "caller": f"{record.filename}:{record.lineno}", "msg": record.getMessage()}
+        if record.exc_info:
+            d["exc"] = self.formatException(record.exc_info)
+        return json.dumps(d)
+
+
+def _setup_logging(v: int, fmt: str = "json") -> None:
+    """--v for both halves: Python logging level, and the native core's klog
+    verbosity (V(6) dumps FlexGPU/NRT ledgers and chosen GPU indexes)."""
     level = logging.WARNING if v <= 0 else logging.INFO if v < 5 else logging.DEBUG
-    logging.basicConfig(level=level, format='{"ts":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s",'
-                                            '"msg":"%(message)s"}')
+    handler = logging.StreamHandler()
+    handler.setFormatter(JsonLogFormatter() if fmt == "json" else
+                         logging.Formatter("%(levelname).1s%(asctime)s %(filename)s:%(lineno)d] %(message)s"))
+    root = logging.getLogger()
+    root.handlers[:] = [handler]
+    root.setLevel(level)
+    try:
+        from ._native import native
+
+        native().set_log_verbosity(int(v))
+        native().set_log_json(fmt == "json")
+    except ImportError:  # native core not built (CPU-only tooling)
+        pass
 
 
 def master_from_kubeconfig(path: str) -> tuple[str, str | None]:
@@ -387,6 +412,8 @@ def cmd_apply(args) -> int:
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="xsched", description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     ap.add_argument("-v", "--v", type=int, default=2, dest="verbosity", help="log verbosity (klog-style)")
+    ap.add_argument("--logging-format", default="json", choices=["json", "text"],
+                    help="log line format of both the Python and the native logger")
     sub = ap.add_subparsers(dest="cmd", required=True)
 
     def conn(p, reference_flags=False):
@@ -494,7 +521,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv: list[str] | None = None) -> int:
     args = build_parser().parse_args(argv)
-    _setup_logging(args.verbosity)
+    _setup_logging(args.verbosity, args.logging_format)
     return int(args.fn(args) or 0)
 
 

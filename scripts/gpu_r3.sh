@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Round-3 box session. Usage: bash scripts/gpu_r3.sh TAG step [step ...]
-# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote
+# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote sample_pre sample_sched
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure (no retries).
 set -u
@@ -27,6 +27,16 @@ for step in "$@"; do
                 --cpus l3 > "$OUT/sched_perf_5000.jsonl" 2>&1 ;;
     remote) timeout -k 10 600 python -u -m flex_gpu_scheduler_amd.tools.remote_bench > "$OUT/remote_bench.jsonl" \
               2>&1 ;;
+    sample_pre|sample_sched)
+      # Wall-clock thread sampler of the native stress driver
+      # (abbin/xsched_stress_prof = build_ext.build_prof output; symbolized
+      # here with tools/sample_report.py against the same binary).
+      wl=PreemptionBasic; pods=2000
+      [ "$step" = sample_sched ] && { wl=SchedulingBasic; pods=5000; }
+      python -m flex_gpu_scheduler_amd.tools.stress "/tmp/s_$wl" --workload "$wl" --nodes 5000 --pods "$pods" &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      XSCHED_SAMPLE_HZ=2000 XSCHED_SAMPLE="$OUT/$wl.samples" timeout -k 5 300 taskset -c "$cpus" \
+        abbin/xsched_stress_prof "/tmp/s_$wl" 1 > "$OUT/$wl.sample_run.txt" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?

@@ -165,3 +165,49 @@ def test_gang_ranks_colocate_on_one_node(store):
         assert len(nodes) == 1, nodes  # all 8 ranks share one node's xGMI mesh
     finally:
         s.stop()
+
+
+def _named_cfg(names: dict, scheduler_name="default-scheduler"):
+    c = coscheduling_config(FLEXGPU_PLUGINS)
+    c["profiles"][0]["schedulerName"] = scheduler_name
+    c["profiles"][0]["pluginConfig"].append({"name": "FlexGPU", "args": names})
+    return c
+
+
+def test_gpu_resource_names_are_per_scheduler():
+    """Two schedulers in one process with different FlexGPU resource names:
+    each parses pods/nodes and writes index annotations with its own names
+    (no process-global state; the second does not rename the first's)."""
+    from flex_gpu_scheduler_amd.models import make_node
+    from flex_gpu_scheduler_amd.scheduler import Store
+
+    sa, sb = Store(), Store()
+    sa.create("nodes", mi355x_node("n0"))
+    sb.create("nodes", make_node("m0", {"cpu": "32", "memory": "64Gi", "pods": "110", "example.com/accel": "4"}))
+    a = start(sa, cfg())
+    b = start(sb, _named_cfg({"gpuResourceName": "example.com/accel", "indexAnnotationKey": "example.com/accel-index"}))
+    try:
+        create_all(sb, "pods", [make_pod(f"q{i}", limits={"example.com/accel": "1"}) for i in range(4)])
+        wait_bound(b, 4)
+        assert sorted(int(annotations(sb, f"q{i}")["example.com/accel-index"]) for i in range(4)) == [0, 1, 2, 3]
+        sb.create("pods", make_pod("q4", limits={"example.com/accel": "1"}))
+        create_all(sa, "pods", [make_pod(f"p{i}", limits={GPU: "1"}) for i in range(3)])
+        wait_bound(a, 3)
+        for i in range(3):
+            ann = annotations(sa, f"p{i}")
+            assert "amd.com/gpu-index" in ann and "example.com/accel-index" not in ann
+        time.sleep(0.3)
+        assert placements(sb)["q4"] == ""  # the 5th accel does not exist: B's ledger counts its own resource
+    finally:
+        a.stop()
+        b.stop()
+
+
+def test_profiles_of_one_scheduler_must_agree_on_gpu_names(store):
+    from flex_gpu_scheduler_amd.scheduler import new_scheduler
+
+    c = _named_cfg({"gpuResourceName": "example.com/accel"})
+    other = _named_cfg({"gpuResourceName": "amd.com/gpu"}, scheduler_name="second")["profiles"][0]
+    c["profiles"].append(other)
+    with pytest.raises(Exception, match="FlexGPU resource names differ"):
+        new_scheduler(store, c)
