@@ -329,6 +329,10 @@ class Coscheduling : public Plugin {
       if (pg->schedule_start_time == 0) status.set("scheduleStartTime", Json(format_rfc3339(wall_now_us())));
     }
     if (phase == pg->phase) return;  // the reference PATCHes only on phase change
+    // The gang's members bind concurrently and the PodGroup in the informer
+    // lags our own PATCH, so every member would see the old phase and send
+    // the same PATCH (8 per 8-rank gang): one PATCH per group and phase.
+    if (!note_patched(p->pg_key, pg->meta.uid, phase)) return;
     status.set("phase", Json(phase));
     status.set("scheduled", Json(static_cast<int64_t>(scheduled)));
     Json patch = Json::object();
@@ -344,6 +348,27 @@ class Coscheduling : public Plugin {
   }
 
  private:
+  // True the first time (group uid, phase) is seen within kPatchMemoUs.
+  static constexpr int64_t kPatchMemoUs = 60'000'000;
+  bool note_patched(uint64_t key, const std::string& uid, const std::string& phase) {
+    const int64_t now = h_.clock->now_us();
+    std::lock_guard<std::mutex> g(patched_mu_);
+    auto& e = patched_[key];
+    if (e.uid == uid && e.phase == phase && now - e.at_us < kPatchMemoUs) return false;
+    e = {uid, phase, now};
+    if (patched_.size() > 8192) {
+      for (auto it = patched_.begin(); it != patched_.end();)
+        it = now - it->second.at_us >= kPatchMemoUs ? patched_.erase(it) : std::next(it);
+    }
+    return true;
+  }
+  struct Patched {
+    std::string uid, phase;
+    int64_t at_us = 0;
+  };
+  std::mutex patched_mu_;
+  std::unordered_map<uint64_t, Patched> patched_;
+
   Handle& h_;
   TTLSet denied_, permitted_;
   std::mutex requeue_mu_;

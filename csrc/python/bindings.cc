@@ -18,6 +18,7 @@
 #include "rest/kube.h"
 #include "scheduler/openloop.h"
 #include "common/log.h"
+#include "apiserver/apiserver.h"
 #include "scheduler/scheduler.h"
 #include "store/store.h"
 #include "telemetry/amdsmi_sampler.h"
@@ -300,6 +301,28 @@ PYBIND11_MODULE(_xsched, m) {
   m.def("rfc3339", [](int64_t us) { return format_rfc3339(us); });
   m.def("native_waiters", [] { return g_native_waiters.load(); });
   m.def("parse_rfc3339", [](const std::string& s) { return parse_rfc3339(s); });
+  // ---- native API server (apiserver/apiserver.h) ----
+  py::class_<apiserver::Server, std::shared_ptr<apiserver::Server>>(m, "NativeApiServer")
+      .def(py::init([](std::shared_ptr<ObjectStore> store, const std::string& host, int port, const std::string& token,
+                       int bookmark_interval_ms) {
+             apiserver::Options o;
+             o.host = host;
+             o.port = port;
+             o.token = token;
+             o.bookmark_interval_ms = bookmark_interval_ms;
+             return std::make_shared<apiserver::Server>(std::move(store), o);
+           }),
+           py::arg("store"), py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("token") = "",
+           py::arg("bookmark_interval_ms") = 10000)
+      .def("start", &apiserver::Server::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &apiserver::Server::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &apiserver::Server::port)
+      .def("requests", &apiserver::Server::requests)
+      .def("connections", &apiserver::Server::connections);
+  m.def("apply_json_patch", [](py::handle doc, py::handle ops) {
+    return to_py(apiserver::apply_json_patch(json_arg(doc), json_arg(ops)));
+  });
+
   // ---- native logging (common/log.h) ----
   m.def("set_log_verbosity", &xsched::log::set_verbosity, py::arg("v"));
   m.def("log_verbosity", &xsched::log::verbosity);

@@ -38,7 +38,7 @@ int64_t rv_of(const Json& obj) {
 
 }  // namespace
 
-const ResourcePath& resource_path(const std::string& kind) {
+const std::unordered_map<std::string, ResourcePath>& resource_table() {
   static const std::unordered_map<std::string, ResourcePath> kTable = {
       {"pods", {"/api/v1", true, "v1", "Pod"}},
       {"nodes", {"/api/v1", false, "v1", "Node"}},
@@ -58,8 +58,13 @@ const ResourcePath& resource_path(const std::string& kind) {
        {"/apis/topology.node.k8s.io/v1alpha1", false, "topology.node.k8s.io/v1alpha1", "NodeResourceTopology"}},
       {"loadwatchermetrics", {"/apis/xsched.amd.com/v1alpha1", false, "xsched.amd.com/v1alpha1", "WatcherMetrics"}},
   };
-  auto it = kTable.find(kind);
-  if (it == kTable.end()) throw std::invalid_argument("unknown resource kind " + kind);
+  return kTable;
+}
+
+const ResourcePath& resource_path(const std::string& kind) {
+  const auto& table = resource_table();
+  auto it = table.find(kind);
+  if (it == table.end()) throw std::invalid_argument("unknown resource kind " + kind);
   return it->second;
 }
 

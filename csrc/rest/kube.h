@@ -16,6 +16,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "framework/plugin.h"
@@ -31,6 +32,7 @@ struct ResourcePath {
   std::string api_version, kind;
 };
 const ResourcePath& resource_path(const std::string& kind);  // throws for unknown kinds
+const std::unordered_map<std::string, ResourcePath>& resource_table();
 std::string collection_path(const std::string& kind, const std::string& ns);
 std::string object_path(const std::string& kind, const std::string& ns, const std::string& name,
                         const std::string& sub = "");

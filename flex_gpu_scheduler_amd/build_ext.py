@@ -29,7 +29,7 @@ BUILD = ROOT / "build"
 HIP_ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
-CORE_DIRS = ["common", "api", "store", "framework", "scheduler", "plugins", "rest"]
+CORE_DIRS = ["common", "api", "store", "framework", "scheduler", "plugins", "rest", "apiserver"]
 # OpenSSL for the native REST client's TLS (rest/http.cc).
 LINK_LIBS = ["-lssl", "-lcrypto"]
 CXXFLAGS = ["-std=c++20", "-O3", "-fPIC", "-Wall", "-Wno-unused-variable", "-Wno-unused-parameter",

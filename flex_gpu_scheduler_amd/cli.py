@@ -139,7 +139,8 @@ def cmd_apiserver(args) -> int:
         log.info("restored %d objects from %s", n, args.load)
     host, port = _hostport(args.bind_address, args.port)
     srv = ApiServer(store, host, port, token=args.token, tls_cert=args.tls_cert_file,
-                    tls_key=args.tls_private_key_file, client_ca=args.client_ca_file).start()
+                    tls_key=args.tls_private_key_file, client_ca=args.client_ca_file,
+                    native_http=False if args.python_http else None).start()
     print(json.dumps({"apiserver": srv.url}), flush=True)
     stop = threading.Event()
     if args.save and args.save_period > 0:
@@ -439,6 +440,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--load", help="restore objects from a JSON snapshot at start")
     p.add_argument("--save", help="write a JSON snapshot on exit (and every --save-period s)")
     p.add_argument("--save-period", type=float, default=0.0)
+    p.add_argument("--python-http", action="store_true",
+                   help="serve with the Python http.server front end instead of the native one (TLS always uses it)")
     p.set_defaults(fn=cmd_apiserver)
 
     p = sub.add_parser("scheduler", help="the scheduler service")

@@ -123,40 +123,65 @@ def apply_json_patch(doc: Any, ops: list) -> Any:
 
 
 class ApiServer:
-    """Owns a native Store and serves it over HTTP on a background thread."""
+    """Owns a native Store and serves it over HTTP on background threads.
+
+    By default the HTTP layer is native (csrc/apiserver/apiserver.cc: same
+    REST surface, no interpreter on the request path); with TLS certificates
+    (or `native_http=False`) it is this module's http.server handler."""
 
     def __init__(self, store=None, host: str = "127.0.0.1", port: int = 0, *, token: str | None = None,
                  bookmark_interval: float = 10.0, tls_cert: str | None = None, tls_key: str | None = None,
-                 client_ca: str | None = None):
+                 client_ca: str | None = None, native_http: bool | None = None):
         self.store = store if store is not None else native().Store()
         self.token = token
         self.bookmark_interval = bookmark_interval
         self._stopping = threading.Event()
         self._active: set = set()
         self._active_lock = threading.Lock()
-        self.requests = 0
-        handler = type("Handler", (_Handler,), {"api": self})
-        self.httpd = _Server((host, port), handler)
-        self.httpd.daemon_threads = True
+        self._py_requests = 0
         self.tls = bool(tls_cert)
-        if tls_cert:
-            # kube-apiserver's --tls-cert-file/--tls-private-key-file, and
-            # --client-ca-file for client-certificate (mutual TLS) auth.
-            import ssl
-
-            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
-            ctx.load_cert_chain(tls_cert, tls_key or tls_cert)
-            if client_ca:
-                ctx.verify_mode = ssl.CERT_REQUIRED
-                ctx.load_verify_locations(client_ca)
-            # Handshakes run in each connection's handler thread, not in the
-            # accept loop (a slow client must not stall every other one).
-            self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True, do_handshake_on_connect=False)
+        if native_http is None:
+            native_http = not self.tls
+        if native_http and self.tls:
+            raise ValueError("the native HTTP server does not terminate TLS; use native_http=False")
+        self._native = None
+        self.httpd = None
         self._thread: threading.Thread | None = None
+        if native_http:
+            self._native = native().NativeApiServer(self.store, host, port, token or "",
+                                                    int(bookmark_interval * 1000))
+            self._host = host
+        else:
+            handler = type("Handler", (_Handler,), {"api": self})
+            self.httpd = _Server((host, port), handler)
+            self.httpd.daemon_threads = True
+            if tls_cert:
+                # kube-apiserver's --tls-cert-file/--tls-private-key-file, and
+                # --client-ca-file for client-certificate (mutual TLS) auth.
+                import ssl
+
+                ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+                ctx.load_cert_chain(tls_cert, tls_key or tls_cert)
+                if client_ca:
+                    ctx.verify_mode = ssl.CERT_REQUIRED
+                    ctx.load_verify_locations(client_ca)
+                # Handshakes run in each connection's handler thread, not in the
+                # accept loop (a slow client must not stall every other one).
+                self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True, do_handshake_on_connect=False)
         _lifecycle.register(self)
 
     @property
+    def native_http(self) -> bool:
+        return self._native is not None
+
+    @property
+    def requests(self) -> int:
+        return self._native.requests() if self._native is not None else self._py_requests
+
+    @property
     def address(self) -> tuple[str, int]:
+        if self._native is not None:
+            return self._host, self._native.port
         return self.httpd.server_address[:2]
 
     @property
@@ -165,6 +190,9 @@ class ApiServer:
         return f"{'https' if self.tls else 'http'}://{h}:{p}"
 
     def start(self) -> "ApiServer":
+        if self._native is not None:
+            self._native.start()
+            return self
         self._thread = threading.Thread(target=self.httpd.serve_forever, kwargs={"poll_interval": 0.05},
                                         name="apiserver", daemon=True)
         self._thread.start()
@@ -178,9 +206,15 @@ class ApiServer:
             self.store.unwatch(w)
 
     def shutdown_for_exit(self) -> None:
+        if self._native is not None:
+            self._native.stop()
+            return
         self._wake_watches()
 
     def stop(self) -> None:
+        if self._native is not None:
+            self._native.stop()
+            return
         self._wake_watches()
         self.httpd.shutdown()
         self.httpd.server_close()
@@ -252,7 +286,7 @@ class _Handler(BaseHTTPRequestHandler):
             raise ApiError(401, "Unauthorized", "Unauthorized")
 
     def _dispatch(self, verb: str) -> None:
-        self.api.requests += 1
+        self.api._py_requests += 1
         url = urlsplit(self.path)
         q = {k: v[-1] for k, v in parse_qs(url.query).items()}
         try:

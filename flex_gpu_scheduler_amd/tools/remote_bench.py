@@ -5,9 +5,12 @@ API, bindings and PodGroup patches go back as REST calls).
 Starts `flex_gpu_scheduler_amd.cli apiserver` as a child process, loads
 MI355X nodes and the pods (plain, or 8-rank gangs within the GPU capacity),
 then starts RemoteScheduler in this process and reports pods/s from its start
-(LIST/WATCH sync included) to the last binding seen by the API.
+(LIST/WATCH sync included) to the last binding the API server acknowledged,
+the rate after the initial sync, and a per-phase timeline (first/half/all of
+the pods mirrored, attempted, bound). The API server's HTTP front end is the
+native one (csrc/apiserver) unless --python-http.
 
-    python -m flex_gpu_scheduler_amd.tools.remote_bench [--nodes 64] [--pods 2000] [--gangs]
+    python -m flex_gpu_scheduler_amd.tools.remote_bench [--nodes 128] [--pods 8000] [--gangs] [--matrix]
 """
 from __future__ import annotations
 
@@ -20,7 +23,25 @@ import time
 from concurrent.futures import ThreadPoolExecutor
 
 
-def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, native_io: bool = True) -> dict:
+def _phases(timeline: list[tuple], n_pods: int, bound: int, t_bound: float) -> dict:
+    """Seconds from the scheduler's start until the first/half/all of the
+    pods were mirrored, attempted and bound, and the REST requests sent."""
+    def first(col: int, target: float):
+        for row in timeline:
+            if row[col] >= target:
+                return round(row[0], 4)
+        return None
+
+    out = {}
+    for name, col in (("mirrored", 1), ("attempted", 2), ("bound", 3)):
+        out[name] = {"first": first(col, 1), "half": first(col, n_pods / 2), "all": first(col, n_pods)}
+    out["bound"]["all"] = round(t_bound, 4) if bound >= n_pods else None
+    out["rest_requests"] = timeline[-1][4] if timeline else 0
+    return out
+
+
+def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, native_io: bool = True,
+        native_http: bool = True) -> dict:
     from ..config import load_config
     from ..control import RestClient
     from ..control.remote import RemoteScheduler
@@ -28,7 +49,8 @@ def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, nat
     from ..utils.workload import flagship_config
 
     srv = subprocess.Popen([sys.executable, "-m", "flex_gpu_scheduler_amd.cli", "apiserver", "--port", "0",
-                            "--bind-address", "127.0.0.1"], stdout=subprocess.PIPE, text=True)
+                            "--bind-address", "127.0.0.1"] + ([] if native_http else ["--python-http"]),
+                           stdout=subprocess.PIPE, text=True)
     try:
         url = json.loads(srv.stdout.readline())["apiserver"]
         admin = RestClient(url)
@@ -60,7 +82,14 @@ def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, nat
             t_synced = time.perf_counter()
             deadline = t0 + 300
             diag = None
+            # Per-phase timeline (sampled every ~1 ms): pods mirrored into the
+            # scheduler's store, scheduling attempts, bindings confirmed by
+            # the scheduler, REST requests sent.
+            timeline = []
             while rs.scheduler.stats()["bound"] < n_pods and time.perf_counter() < deadline:
+                st = rs.scheduler.stats()
+                timeline.append((time.perf_counter() - t0, rs.mirror.applied, st["attempts"], st["bound"],
+                                 rs.client.requests() if hasattr(rs.client, "requests") else 0))
                 if diag is None and time.perf_counter() - t0 > 5:  # stalled: record why
                     diag = {"stats": rs.scheduler.stats(), "queue": rs.scheduler.queue_counts(),
                             "cache": rs.scheduler.cache_counts(), "local_pods": rs.store.count("pods"),
@@ -74,19 +103,23 @@ def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, nat
                         diag["stuck"] = stuck[:8]
                         diag["explain"] = {k: e.get(k) for k in ("code", "message", "feasible")}
                         diag["filtered"] = dict(list((e.get("filtered") or {}).items())[:3])
-                time.sleep(0.005)
+                time.sleep(0.001)
             bound = rs.scheduler.stats()["bound"]
             t_bound = time.perf_counter()
-            while time.perf_counter() < deadline:
-                items = admin.list("pods", "default")[0]
-                if sum(1 for p in items if p["spec"].get("nodeName")) >= n_pods:
-                    break
-                time.sleep(0.01)
-            t_api = time.perf_counter()
+            # A binding counts once the API server answered the POST (the
+            # scheduler's bound counter); one LIST afterwards (untimed)
+            # checks that every pod carries its nodeName on the server.
+            api_bound = sum(1 for p in admin.list("pods", "default")[0] if p["spec"].get("nodeName"))
+            phases = _phases(timeline, n_pods, bound, t_bound - t0)
             return {"nodes": nodes, "pods": n_pods, "gangs": gangs, "bind_workers": bind_workers, "native_io": rs.native_io,
-                    "bound": bound, "create_s": round(create_s, 3), "sync_s": round(t_synced - t0, 3),
-                    "bound_s": round(t_bound - t0, 3), "api_visible_s": round(t_api - t0, 3),
-                    "pods_per_s": round(n_pods / (t_api - t0), 1), **({"stall": diag} if diag else {})}
+                    "apiserver": "native" if native_http else "python", "phases": phases,
+                    "bound": bound, "api_bound": api_bound, "create_s": round(create_s, 3),
+                    "sync_s": round(t_synced - t0, 3), "bound_s": round(t_bound - t0, 3),
+                    # from the scheduler's start (LIST+WATCH sync included)
+                    "pods_per_s": round(n_pods / (t_bound - t0), 1),
+                    # after the initial sync: the steady binding rate
+                    "pods_per_s_after_sync": round(n_pods / max(1e-9, t_bound - t_synced), 1),
+                    **({"stall": diag} if diag else {})}
         finally:
             rs.stop()
     finally:
@@ -96,14 +129,23 @@ def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, nat
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--nodes", type=int, default=64)
-    ap.add_argument("--pods", type=int, default=2000)
+    ap.add_argument("--nodes", type=int, default=128)
+    ap.add_argument("--pods", type=int, default=8000)
     ap.add_argument("--gangs", action="store_true")
     ap.add_argument("--bind-workers", type=int, default=16)
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--python-io", action="store_true", help="Python mirror and writer instead of the native ones")
+    ap.add_argument("--python-http", action="store_true", help="the API server's http.server front end")
+    ap.add_argument("--matrix", action="store_true",
+                    help="plain and 8-rank gang runs, native and Python API server front ends")
     a = ap.parse_args()
-    print(json.dumps(run(a.nodes, a.pods, a.gangs, a.bind_workers, a.clients, native_io=not a.python_io)), flush=True)
+    if a.matrix:
+        for native_http in (True, False):
+            for g, n in ((False, a.pods), (True, min(a.pods, a.nodes * 8))):
+                print(json.dumps(run(a.nodes, n, g, a.bind_workers, a.clients, native_http=native_http)), flush=True)
+        return 0
+    print(json.dumps(run(a.nodes, a.pods, a.gangs, a.bind_workers, a.clients, native_io=not a.python_io,
+                         native_http=not a.python_http)), flush=True)
     return 0
 
 

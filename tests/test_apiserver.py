@@ -15,9 +15,12 @@ from flex_gpu_scheduler_amd.control.selectors import label_matcher, parse_select
 from flex_gpu_scheduler_amd.models import make_node, make_pod, make_pod_group
 
 
-@pytest.fixture
-def server(store):
-    srv = ApiServer(store).start()
+@pytest.fixture(params=[True, False], ids=["native-http", "python-http"])
+def server(request, store):
+    """Both HTTP front ends over the same store: the native one
+    (csrc/apiserver, the default) and http.server (the TLS path)."""
+    srv = ApiServer(store, native_http=request.param).start()
+    assert srv.native_http is request.param
     yield srv
     srv.stop()
 
