@@ -111,7 +111,9 @@ const std::unordered_map<std::string, std::string>& routes() {
   return *m;
 }
 
-bool valid_key_char(char c) { return std::isalnum(static_cast<unsigned char>(c)) || c == '_' || c == '.' || c == '/' || c == '-'; }
+bool valid_key_char(char c) {
+  return std::isalnum(static_cast<unsigned char>(c)) || c == '_' || c == '.' || c == '/' || c == '-';
+}
 
 std::string field_string(const Json& obj, std::string_view path) {
   const Json* cur = &obj;

@@ -310,7 +310,9 @@ class FlexGPU : public Plugin {
     h_.cache->mutate_pod(p->uid(), [&](Pod& cp) {
       auto& a = cp.meta.annotations;
       a.erase(std::remove_if(a.begin(), a.end(),
-                             [&](const auto& kv) { return kv.first == gn.index_annotation || kv.first == gn.partition_annotation; }),
+                             [&](const auto& kv) {
+                               return kv.first == gn.index_annotation || kv.first == gn.partition_annotation;
+                             }),
               a.end());
     });
   }

@@ -313,7 +313,9 @@ class NodeAffinity : public Plugin {
       bool ok = false;
       for (const auto& t : added_)
         if (term_matches(t, *ni.node)) ok = true;
-      if (!ok) return XS_FIXED_STATUS(Code::UnschedulableAndUnresolvable, "node(s) didn't match scheduler-enforced node affinity");
+      if (!ok)
+        return XS_FIXED_STATUS(Code::UnschedulableAndUnresolvable,
+                               "node(s) didn't match scheduler-enforced node affinity");
     }
     if (!required_matches(p, *ni.node))
       return XS_FIXED_STATUS(Code::UnschedulableAndUnresolvable, "node(s) didn't match Pod's node affinity/selector");

@@ -279,7 +279,8 @@ class TopologyMatch : public Plugin {
       int64_t cap = have ? value_units(id, *have) : 0;
       int64_t want = value_units(id, req.v[id]);
       int64_t s = 0;
-      if (cap != 0 && want <= cap) s = strategy_ == Strategy::Most ? want * kMaxNodeScore / cap : (cap - want) * kMaxNodeScore / cap;
+      if (cap != 0 && want <= cap)
+        s = strategy_ == Strategy::Most ? want * kMaxNodeScore / cap : (cap - want) * kMaxNodeScore / cap;
       num += s * weight(id);
       wsum += weight(id);
     }

@@ -46,7 +46,9 @@ int64_t count_matching(const std::vector<PodPtr>& pods, const LabelSelector& sel
 // Filter failures, built once: a failing node costs a Status copy (two
 // refcount increments), not a string, vector and control block per node.
 const Status& kSpreadMissingLabel() {
-  static const Status st = Status::immortal(Code::UnschedulableAndUnresolvable, "node(s) didn't match pod topology spread constraints (missing required label)");
+  static const Status st = Status::immortal(
+      Code::UnschedulableAndUnresolvable,
+      "node(s) didn't match pod topology spread constraints (missing required label)");
   return st;
 }
 const Status& kSpreadSkew() {

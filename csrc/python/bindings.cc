@@ -374,7 +374,8 @@ PYBIND11_MODULE(_xsched, m) {
 
   py::class_<ObjectStore, std::shared_ptr<ObjectStore>>(m, "Store")
       .def(py::init<>())
-      .def("create", [](ObjectStore& s, const std::string& kind, py::handle obj) { return ptr_to_py(s.create(kind, json_arg(obj))); })
+      .def("create",
+           [](ObjectStore& s, const std::string& kind, py::handle obj) { return ptr_to_py(s.create(kind, json_arg(obj))); })
       .def("create_many",
            [](ObjectStore& s, const std::string& kind, py::handle objs) {
              // A JSON string is parsed element by element with the GIL

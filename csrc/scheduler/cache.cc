@@ -524,7 +524,8 @@ Json SchedulerCache::check(const std::vector<PodPtr>& assigned, const std::vecto
     for (const auto& [k, c] : recount) {
       auto it = group_assigned_.find(k);
       int have_c = it == group_assigned_.end() ? 0 : it->second;
-      if (have_c != c) groups.push_back(std::to_string(k) + ": counter " + std::to_string(have_c) + ", pods " + std::to_string(c));
+      if (have_c != c)
+        groups.push_back(std::to_string(k) + ": counter " + std::to_string(have_c) + ", pods " + std::to_string(c));
     }
     for (const auto& [k, c] : group_assigned_)
       if (c != 0 && !recount.count(k)) groups.push_back(std::to_string(k) + ": counter " + std::to_string(c) + ", pods 0");

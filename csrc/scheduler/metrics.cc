@@ -63,19 +63,25 @@ struct Def {
 };
 const Def kDefs[] = {
     {"scheduler_schedule_attempts_total", "counter", "Number of attempts to schedule pods, by the result.", 0, 0, 0},
-    {"scheduler_e2e_scheduling_duration_seconds", "histogram", "E2e scheduling latency in seconds (scheduling algorithm + binding)", 0.001, 2, 15},
+    {"scheduler_e2e_scheduling_duration_seconds", "histogram",
+     "E2e scheduling latency in seconds (scheduling algorithm + binding)", 0.001, 2, 15},
     {"scheduler_scheduling_attempt_duration_seconds", "histogram", "Scheduling attempt latency in seconds", 0.001, 2, 15},
     {"scheduler_scheduling_algorithm_duration_seconds", "histogram", "Scheduling algorithm latency in seconds", 0.001, 2, 15},
-    {"scheduler_pod_scheduling_duration_seconds", "histogram", "E2e latency for a pod being scheduled which may include multiple scheduling attempts.", 0.01, 2, 20},
+    {"scheduler_pod_scheduling_duration_seconds", "histogram",
+     "E2e latency for a pod being scheduled which may include multiple scheduling attempts.", 0.01, 2, 20},
     {"scheduler_pod_scheduling_attempts", "histogram", "Number of attempts to successfully schedule a pod.", 1, 2, 5},
-    {"scheduler_framework_extension_point_duration_seconds", "histogram", "Latency for running all plugins of a specific extension point.", 0.0001, 2, 12},
-    {"scheduler_plugin_execution_duration_seconds", "histogram", "Duration for running a plugin at a specific extension point.", 0.00001, 1.5, 20},
+    {"scheduler_framework_extension_point_duration_seconds", "histogram",
+     "Latency for running all plugins of a specific extension point.", 0.0001, 2, 12},
+    {"scheduler_plugin_execution_duration_seconds", "histogram",
+     "Duration for running a plugin at a specific extension point.", 0.00001, 1.5, 20},
     {"scheduler_permit_wait_duration_seconds", "histogram", "Duration of waiting on permit.", 0.001, 2, 15},
     {"scheduler_preemption_victims", "histogram", "Number of selected preemption victims", 1, 2, 7},
     {"scheduler_preemption_attempts_total", "counter", "Total preemption attempts in the cluster till now", 0, 0, 0},
     {"scheduler_pending_pods", "gauge", "Number of pending pods, by the queue type.", 0, 0, 0},
-    {"scheduler_queue_incoming_pods_total", "counter", "Number of pods added to scheduling queues by event and queue type.", 0, 0, 0},
-    {"xsched_gang_admit_seconds", "histogram", "PodGroup gang-admit latency: first member enqueued to last member bound.", 0.0001, 2, 22},
+    {"scheduler_queue_incoming_pods_total", "counter",
+     "Number of pods added to scheduling queues by event and queue type.", 0, 0, 0},
+    {"xsched_gang_admit_seconds", "histogram",
+     "PodGroup gang-admit latency: first member enqueued to last member bound.", 0.0001, 2, 22},
     {"xsched_binding_duration_seconds", "histogram", "Binding cycle latency (PreBind+Bind+PostBind).", 0.00001, 2, 20},
 };
 }  // namespace

@@ -26,7 +26,6 @@ import signal
 import socket
 import sys
 import threading
-import time
 from pathlib import Path
 
 log = logging.getLogger("xsched")

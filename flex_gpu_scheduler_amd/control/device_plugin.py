@@ -26,7 +26,6 @@ from __future__ import annotations
 import logging
 import os
 import threading
-import time
 from concurrent import futures
 
 import grpc

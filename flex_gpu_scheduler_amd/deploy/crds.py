@@ -18,7 +18,8 @@ import sys
 import yaml
 
 QUANTITY = {"anyOf": [{"type": "integer"}, {"type": "string"}],
-            "pattern": r"^(\+|-)?(([0-9]+(\.[0-9]*)?)|(\.[0-9]+))(([KMGTPE]i)|[numkMGTPE]|([eE](\+|-)?(([0-9]+(\.[0-9]*)?)|(\.[0-9]+))))?$",
+            "pattern": (r"^(\+|-)?(([0-9]+(\.[0-9]*)?)|(\.[0-9]+))"
+                        r"(([KMGTPE]i)|[numkMGTPE]|([eE](\+|-)?(([0-9]+(\.[0-9]*)?)|(\.[0-9]+))))?$"),
             "x-kubernetes-int-or-string": True}
 RESOURCE_LIST = {"type": "object", "additionalProperties": QUANTITY}
 
@@ -50,7 +51,8 @@ def _crd(group: str, kind: str, plural: str, scope: str, short: list[str], spec_
         names["shortNames"] = short
     return {"apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition",
             "metadata": {"name": f"{plural}.{group}",
-                         "annotations": {"api-approved.kubernetes.io": "https://github.com/kubernetes-sigs/scheduler-plugins/pull/50"}
+                         "annotations": {"api-approved.kubernetes.io":
+                                         "https://github.com/kubernetes-sigs/scheduler-plugins/pull/50"}
                          if group.endswith(".k8s.io") or group == "scheduling.sigs.k8s.io" else {}},
             "spec": {"group": group, "names": names, "scope": scope, "versions": [ver]}}
 

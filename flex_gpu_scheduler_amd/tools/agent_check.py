@@ -16,7 +16,6 @@ def main() -> int:
     from .. import Store
     from ..control.client import LocalClient
     from ..control.node_agent import NodeAgent, hip_health_fn
-    from ..gpu.discovery import discover_host
 
     store = Store()
     health = None

@@ -264,7 +264,9 @@ def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None) -> dict:
     finally:
         s.stop()
     return {"pods_per_s": round(pods / dt, 1) if ok else None, "metrics_source": source,
-            "node_gpu_busy_pct": busy, "node_hbm_bandwidth_pct": [hbm[i % len(hbm)] for i in range(nodes)] if hbm else None, "first_gpu_pod_node": first.get("selected"),
+            "node_gpu_busy_pct": busy,
+            "node_hbm_bandwidth_pct": [hbm[i % len(hbm)] for i in range(nodes)] if hbm else None,
+            "first_gpu_pod_node": first.get("selected"),
             "tlp_scores": {n: v["TargetLoadPacking*1"] for n, v in (first.get("scores") or {}).items()}}
 
 

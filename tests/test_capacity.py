@@ -37,8 +37,9 @@ def wait_for(pred, timeout=10.0):
 
 def test_cross_namespace_preemption_reclaims_min(store):
     store.create("nodes", gpu_node())
-    create_all(store, "elasticquotas", [make_elastic_quota("eq1", "ns1", min={GPU: "4", "cpu": "100"}, max={GPU: "8", "cpu": "100"}),
-                                        make_elastic_quota("eq2", "ns2", min={GPU: "4", "cpu": "100"}, max={GPU: "8", "cpu": "100"})])
+    create_all(store, "elasticquotas",
+               [make_elastic_quota("eq1", "ns1", min={GPU: "4", "cpu": "100"}, max={GPU: "8", "cpu": "100"}),
+                make_elastic_quota("eq2", "ns2", min={GPU: "4", "cpu": "100"}, max={GPU: "8", "cpu": "100"})])
     s = new_scheduler(store, load_config(CONFIG), start=True)
     try:
         create_all(store, "pods", [gpod(f"a{i}", "ns1") for i in range(8)])  # ns1 borrows ns2's min
@@ -110,8 +111,9 @@ def test_regular_preemption_without_quota(store):
 
 def test_overused_quota_cannot_preempt_other_quota(store):
     store.create("nodes", gpu_node(gpus=4))
-    create_all(store, "elasticquotas", [make_elastic_quota("eq1", "ns1", min={GPU: "1", "cpu": "50"}, max={GPU: "4", "cpu": "100"}),
-                                        make_elastic_quota("eq2", "ns2", min={GPU: "3", "cpu": "50"}, max={GPU: "4", "cpu": "100"})])
+    create_all(store, "elasticquotas",
+               [make_elastic_quota("eq1", "ns1", min={GPU: "1", "cpu": "50"}, max={GPU: "4", "cpu": "100"}),
+                make_elastic_quota("eq2", "ns2", min={GPU: "3", "cpu": "50"}, max={GPU: "4", "cpu": "100"})])
     s = new_scheduler(store, load_config(CONFIG), start=True)
     try:
         create_all(store, "pods", [gpod(f"b{i}", "ns2", 1) for i in range(3)])

@@ -129,7 +129,7 @@ def test_crds_written_match_generator(tmp_path):
 
 
 def test_examples_validate_against_crds():
-    from flex_gpu_scheduler_amd.models import make_nrt, mi355x_nrt
+    from flex_gpu_scheduler_amd.models import mi355x_nrt
     schemas = {}
     for make in crds.ALL.values():
         c = make()

@@ -144,7 +144,6 @@ def test_gpu_freed_on_delete_is_reused(store):
 
 
 def test_gang_ranks_colocate_on_one_node(store):
-    import json
 
     from flex_gpu_scheduler_amd import load_config, new_scheduler
     from flex_gpu_scheduler_amd.models import mi355x_nrt

@@ -158,6 +158,24 @@ def test_amdsmi_telemetry_sees_hbm_load():
     assert r["load"]["max_umc"] > r["idle"]["max_umc"] and r["load"]["max_power_w"] > r["idle"]["max_power_w"], r
 
 
+def test_trimaran_tlp_on_live_gpu_load():
+    """TargetLoadPacking scores nodes from live amd-smi telemetry: a GPU kept
+    >50% busy by a device copy loop scores differently from the same GPU
+    sampled idle, and the first GPU pod lands where explain() predicts
+    (tools/tlp_live.py; TLP target 40%, so the busy node scores 0)."""
+    out = subprocess.run([sys.executable, "-m", "flex_gpu_scheduler_amd.tools.tlp_live", "--seconds", "2"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    from flex_gpu_scheduler_amd.tools.tlp_live import BUSY, IDLE
+
+    assert r["gpu_source"] == "amdsmi", r
+    assert r["gpu_busy_avg"][BUSY] > 50 and r["gpu_busy_avg"][IDLE] < 20, r
+    assert r["tlp_scores"][IDLE] != r["tlp_scores"][BUSY], r
+    assert r["tlp_scores"][IDLE] > r["tlp_scores"][BUSY], r
+    assert r["predicted"] == r["landed"] == IDLE, r
+
+
 def test_node_agent_sampler_uses_amdsmi_on_the_box():
     from flex_gpu_scheduler_amd.gpu.telemetry import HostSampler, NodeTelemetry
 

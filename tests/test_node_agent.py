@@ -3,7 +3,6 @@ a real 8x MI355X box (tests/fixtures/mi355x_box, taken with
 `python -m flex_gpu_scheduler_amd.tools.capture_hw` through gpurun)."""
 import json
 import os
-import threading
 import time
 import urllib.request
 

@@ -119,7 +119,8 @@ NAMED = [
      [nrt("fake-node-1", PODL, [("cpu", "2", "2"), ("memory", "8Gi", "8Gi")], [("cpu", "2", "2"), ("memory", "8Gi", "8Gi")]),
       nrt("fake-node-2", PODL, [("cpu", "4", "4"), ("memory", "8Gi", "8Gi")], [("cpu", "4", "4"), ("memory", "8Gi", "8Gi")])],
      ["fake-node-2"]),
-    ("SingleNUMANodeContainerLevel: Filtering out nodes that cannot fit resources in case of Guaranteed pod with multi containers",
+    ("SingleNUMANodeContainerLevel: Filtering out nodes that cannot fit resources in case of Guaranteed pod "
+     "with multi containers",
      pod([cm("3", "5Gi"), cm("3", "5Gi")]),
      [nrt("fake-node-1", CNT, [("cpu", "8", "6"), ("memory", "8Gi", "8Gi")], [("cpu", "2", "2"), ("memory", "8Gi", "8Gi")]),
       nrt("fake-node-2", CNT, [("cpu", "4", "4"), ("memory", "8Gi", "8Gi")], [("cpu", "4", "4"), ("memory", "8Gi", "8Gi")])],

@@ -7,7 +7,7 @@ import time
 from flex_gpu_scheduler_amd import load_config, new_scheduler
 from flex_gpu_scheduler_amd.models import make_node, make_pod
 
-from helpers import placements, wait_bound
+from helpers import placements
 
 
 def node(name, zone=None, images=None, **labels):

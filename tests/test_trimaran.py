@@ -90,3 +90,29 @@ def test_lvrb_min_of_cpu_and_memory(store):
     sc = explain_scores(store, s, make_pod("p"))
     assert sc["a"]["LoadVariationRiskBalancing*1"] == 70  # min(90, 70)
     s.stop()
+
+
+def test_tlp_live_tool_logic_with_injected_load():
+    """tools/tlp_live.py end to end with a stand-in sampler (the GPU tier
+    runs it on the real MI355X through amd-smi)."""
+    import time as _t
+
+    from flex_gpu_scheduler_amd.gpu.telemetry import Sample
+    from flex_gpu_scheduler_amd.tools import tlp_live
+
+    state = {"busy": False}
+
+    class FakeSampler:
+        def sample(self):
+            return Sample(_t.time(), 10.0, 20.0, 92.0 if state["busy"] else 3.0, 5.0)
+
+    def start_load():
+        state["busy"] = True
+        return lambda: state.update(busy=False)
+
+    r = tlp_live.run(0.2, 0.01, sampler=FakeSampler(), start_load=start_load)
+    assert r["gpu_busy_avg"][tlp_live.BUSY] == 92.0 and r["gpu_busy_avg"][tlp_live.IDLE] == 3.0
+    sc = r["tlp_scores"]
+    # idle: 3% + 1/8 GPU = 15.5% -> round(60*15.5/40+40) = 63; busy: 104.5% -> 0
+    assert sc[tlp_live.IDLE] == 63 and sc[tlp_live.BUSY] == 0
+    assert r["predicted"] == r["landed"] == tlp_live.IDLE
