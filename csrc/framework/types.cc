@@ -23,6 +23,21 @@ const std::vector<std::string>& Status::reasons() const {
 
 const std::string& Status::intern_plugin(std::string_view p) { return IStr::intern(p); }
 
+Status Status::interned(Code c, std::vector<std::string> reasons) {
+  static std::mutex mu;
+  static auto* table = new std::map<std::pair<int, std::vector<std::string>>, const std::vector<std::string>*>();
+  std::lock_guard<std::mutex> g(mu);
+  auto key = std::make_pair(static_cast<int>(c), std::move(reasons));
+  auto it = table->find(key);
+  if (it == table->end()) {
+    auto* r = new std::vector<std::string>(key.second);  // never freed (bounded by distinct verdicts)
+    it = table->emplace(std::move(key), r).first;
+  }
+  Status s(c);
+  s.reasons_ = it->second;
+  return s;
+}
+
 const std::string& Status::failed_plugin() const {
   static const std::string kNone;
   return plugin_ ? *plugin_ : kNone;

@@ -58,6 +58,12 @@ class Status {
     s.reasons_ = new std::vector<std::string>(1, std::move(reason));  // never freed
     return s;
   }
+  // An immortal failure shared process-wide per distinct (code, reasons):
+  // plugins whose verdicts come from a small set (NodeResourcesFit's
+  // "Insufficient <resource>" combinations, FlexGPU's per-resource failures)
+  // memoize these, so the thousands of copies a failed cycle makes (one per
+  // node into the diagnosis) never touch a reference count.
+  static Status interned(Code c, std::vector<std::string> reasons);
 
   Code code() const { return code_; }
   bool is_success() const { return code_ == Code::Success; }
@@ -406,6 +412,19 @@ class NodeStatusMap {
   using const_iterator = std::vector<value_type>::const_iterator;
   using iterator = std::vector<value_type>::iterator;
 
+  NodeStatusMap() = default;
+  NodeStatusMap(const NodeStatusMap& o) { *this = o; }
+  NodeStatusMap& operator=(const NodeStatusMap& o) {
+    if (this != &o) {
+      o.ensure_index();
+      entries_ = o.entries_;
+      hashes_ = o.hashes_;
+      slots_ = o.slots_;
+      indexed_.store(o.indexed_.load(std::memory_order_acquire), std::memory_order_relaxed);
+    }
+    return *this;
+  }
+
   size_t size() const { return entries_.size(); }
   bool empty() const { return entries_.empty(); }
   const_iterator begin() const { return entries_.begin(); }
@@ -416,36 +435,67 @@ class NodeStatusMap {
     entries_.clear();
     hashes_.clear();
     slots_.clear();
+    indexed_.store(0, std::memory_order_relaxed);
   }
-  void reserve(size_t n) {
-    entries_.reserve(n);
-    hashes_.reserve(n);
-    if (n * 2 > slots_.size()) rehash(n * 2);
-  }
+  void reserve(size_t n) { entries_.reserve(n); }
   const_iterator find(std::string_view k) const {
+    ensure_index();
     int32_t i = lookup(k, hash(k));
     return i < 0 ? entries_.end() : entries_.begin() + i;
   }
   iterator find(std::string_view k) {
+    ensure_index();
     int32_t i = lookup(k, hash(k));
     return i < 0 ? entries_.end() : entries_.begin() + i;
   }
-  size_t count(std::string_view k) const { return lookup(k, hash(k)) < 0 ? 0 : 1; }
+  size_t count(std::string_view k) const { return find(k) == end() ? 0 : 1; }
   std::pair<iterator, bool> emplace(std::string_view k, const Status& v) {
+    ensure_index();
     const size_t h = hash(k);
     if (int32_t i = lookup(k, h); i >= 0) return {entries_.begin() + i, false};
-    if ((entries_.size() + 1) * 2 > slots_.size()) rehash(std::max<size_t>(16, slots_.size() * 2));
     entries_.emplace_back(std::string(k), v);
-    hashes_.push_back(h);
-    place(static_cast<int32_t>(entries_.size() - 1), h);
+    index_tail();
     return {entries_.end() - 1, true};
   }
+  // Appends a node the caller knows is not in the map yet (a diagnosis built
+  // from one pass over distinct snapshot nodes). Nothing is hashed: the
+  // index is built on the first lookup, which most failed cycles (FitError
+  // message, preemption over the whole list) never make.
+  void append_unique(std::string_view k, const Status& v) { entries_.emplace_back(std::string(k), v); }
   Status& operator[](std::string_view k) { return emplace(k, Status()).first->second; }
 
  private:
-  // Each key is hashed once: the hash is kept beside the entry, so probing
-  // compares hashes before strings and a rehash never rehashes a string.
   static size_t hash(std::string_view k) { return std::hash<std::string_view>{}(k); }
+  // Indexes entries appended since the last lookup. Lookups on a shared map
+  // from several threads are safe: the first one to arrive builds the index
+  // under a lock, the others see it complete.
+  void ensure_index() const {
+    if (indexed_.load(std::memory_order_acquire) == entries_.size()) return;
+    std::lock_guard<std::mutex> g(index_mu());
+    if (indexed_.load(std::memory_order_relaxed) == entries_.size()) return;
+    index_tail();
+  }
+  void index_tail() const {
+    size_t from = indexed_.load(std::memory_order_relaxed);
+    if (entries_.size() * 2 > slots_.size()) {
+      size_t cap = 16;
+      while (cap < entries_.size() * 2) cap <<= 1;
+      hashes_.resize(from);
+      for (size_t i = from; i < entries_.size(); ++i) hashes_.push_back(hash(entries_[i].first));
+      slots_.assign(cap, -1);
+      for (int32_t i = 0; i < static_cast<int32_t>(entries_.size()); ++i) place(i, hashes_[i]);
+    } else {
+      for (size_t i = from; i < entries_.size(); ++i) {
+        hashes_.push_back(hash(entries_[i].first));
+        place(static_cast<int32_t>(i), hashes_[i]);
+      }
+    }
+    indexed_.store(entries_.size(), std::memory_order_release);
+  }
+  static std::mutex& index_mu() {
+    static std::mutex m;
+    return m;
+  }
   int32_t lookup(std::string_view k, size_t h) const {
     if (slots_.empty()) return -1;
     size_t mask = slots_.size() - 1;
@@ -455,21 +505,18 @@ class NodeStatusMap {
       if (hashes_[i] == h && entries_[i].first == k) return i;
     }
   }
-  void place(int32_t i, size_t h) {
+  void place(int32_t i, size_t h) const {
     size_t mask = slots_.size() - 1;
     size_t j = h & mask;
     while (slots_[j] >= 0) j = (j + 1) & mask;
     slots_[j] = i;
   }
-  void rehash(size_t want) {
-    size_t cap = 16;
-    while (cap < want) cap <<= 1;
-    slots_.assign(cap, -1);
-    for (int32_t i = 0; i < static_cast<int32_t>(entries_.size()); ++i) place(i, hashes_[i]);
-  }
   std::vector<value_type> entries_;
-  std::vector<size_t> hashes_;   // hash of entries_[i].first
-  std::vector<int32_t> slots_;   // power of two, at most half full; -1 = empty
+  // Index over entries_[0, indexed_): each key hashed once, kept beside the
+  // entry, so probing compares hashes before strings.
+  mutable std::vector<size_t> hashes_;
+  mutable std::vector<int32_t> slots_;  // power of two, at most half full; -1 = empty
+  mutable std::atomic<size_t> indexed_{0};
 };
 
 struct Victims {

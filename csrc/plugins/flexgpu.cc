@@ -216,8 +216,9 @@ class FlexGPU : public Plugin {
     auto it = memo.find(kid);
     if (it == memo.end()) {
       const std::string n = ResourceRegistry::get().name(kid);
-      it = memo.emplace(kid, std::make_pair(Status::unschedulable("insufficient resource " + n),
-                                            Status::unschedulable("no fit indexes resource " + n))).first;
+      it = memo.emplace(kid, std::make_pair(Status::interned(Code::Unschedulable, {"insufficient resource " + n}),
+                                            Status::interned(Code::Unschedulable, {"no fit indexes resource " + n})))
+               .first;
     }
     return no_fit ? it->second.second : it->second.first;
   }

@@ -154,7 +154,7 @@ class NodeResourcesFit : public Plugin {
     for (uint64_t m = fail & ~((1ull << kPods) | kBeyondAllocatable); m; m &= m - 1)
       reasons.push_back("Insufficient " + ResourceRegistry::get().name(__builtin_ctzll(m)));
     Code code = (fail & kBeyondAllocatable) ? Code::UnschedulableAndUnresolvable : Code::Unschedulable;
-    return memo.emplace(fail, Status(code, std::move(reasons))).first->second;
+    return memo.emplace(fail, Status::interned(code, std::move(reasons))).first->second;
   }
 
   std::pair<int64_t, Status> score(CycleState&, const Pod& p, const NodeInfo& ni) override {

@@ -46,8 +46,13 @@ class DefaultPreemption : public Plugin, public PreemptionPolicy {
     return select_victims_default(h_, s, preemptor, ni, pdbs, [&](const Pod& p) { return p.priority < prio; }, victims,
                                  num_violating);
   }
+  // Victims = lower-priority pods, kept or reprieved by node-local Filters:
+  // a function of the node and the preemptor alone. Subclasses with their
+  // own victim rules (PreemptionToleration: clock-dependent) opt out.
+  bool victims_depend_only_on_node() const override { return !overrides_victims_; }
 
  protected:
+  bool overrides_victims_ = false;  // set by subclasses that replace select_victims_on_node
   Handle& h_;
   Evaluator ev_;
   int pct_ = 10, abs_ = 100;
@@ -80,7 +85,9 @@ bool parse_policy(const PriorityClass& pc, TolerationPolicy* out) {
 
 class PreemptionToleration : public DefaultPreemption {
  public:
-  PreemptionToleration(const Json& args, Handle& h) : DefaultPreemption(args, h, "PreemptionToleration") {}
+  PreemptionToleration(const Json& args, Handle& h) : DefaultPreemption(args, h, "PreemptionToleration") {
+    overrides_victims_ = true;
+  }
 
   // ExemptedFromPreemption (preemption_toleration.go:125-175).
   bool exempted(const Pod& victim, const Pod& preemptor, MicroTime now) const {

@@ -1,5 +1,7 @@
 #include "scheduler/preemption.h"
 
+#include "common/log.h"
+
 #include <algorithm>
 #include <atomic>
 #include <climits>
@@ -142,8 +144,49 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
   std::mutex mu;
   std::atomic<bool> stop{false};
   int n = static_cast<int>(potential.size());
+  // Reuse is sound when the policy's victims depend on the node alone, no
+  // PDB can change the violation count, and every Filter is node-local for
+  // this pod (the equivalence cache's condition); nodes with nominated pods
+  // and nodes where a PreFilter extension reacts to a victim are recomputed.
+  const bool memo_ok = policy_->victims_depend_only_on_node() && pdbs.empty() && pod.template_hash != 0 &&
+                       h_.snapshot && h_.framework && h_.framework->filters_node_local(pod, *h_.snapshot) &&
+                       (s.nominated || !h_.nominator || h_.nominator->empty());
+  auto add_candidate = [&](Candidate&& c) {
+    std::lock_guard<std::mutex> g(mu);
+    if (c.num_pdb_violations == 0)
+      non_violating.push_back(std::move(c));
+    else
+      violating.push_back(std::move(c));
+    int nv = static_cast<int>(non_violating.size());
+    if (nv > 0 && nv + static_cast<int>(violating.size()) >= num_candidates) stop.store(true);
+  };
   h_.parallelizer->until(n, [&](int i) {
     const NodeInfoPtr& src = potential[(offset + i) % n];
+    Memo::Shard* shard = nullptr;
+    if (memo_ok) {
+      bool nominated_here = false;
+      if (s.nominated) {
+        auto it = s.nominated->find(src->name());
+        nominated_here = it != s.nominated->end() && !it->second.empty();
+      }
+      if (!nominated_here) {
+        shard = &memo_->shards[std::hash<std::string>{}(src->name()) % Memo::kShards];
+        std::unique_lock<std::mutex> g(shard->mu);
+        auto it = shard->m.find(src->name());
+        if (it != shard->m.end() && it->second.gen == src->generation && it->second.tmpl == pod.template_hash) {
+          memo_->hits.fetch_add(1, std::memory_order_relaxed);
+          if (!it->second.candidate) return;
+          Candidate c;
+          c.node = src->name();
+          c.victims = it->second.victims;
+          c.num_pdb_violations = it->second.num_pdb_violations;
+          g.unlock();
+          add_candidate(std::move(c));
+          return;
+        }
+        memo_->misses.fetch_add(1, std::memory_order_relaxed);
+      }
+    }
     // The candidate is evaluated on this worker's scratch NodeInfo: copy
     // assignment reuses its vectors' storage, so a dry run allocates nothing
     // per node (a fresh clone per candidate made the 16 workers contend on
@@ -166,17 +209,25 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
     Candidate c;
     c.node = ni->name();
     Status vs = policy_->select_victims_on_node(*st, pod, *ni, pdbs, c.victims, c.num_pdb_violations);
-    if (!vs.is_success() || c.victims.empty()) return;
-    std::lock_guard<std::mutex> g(mu);
-    if (c.num_pdb_violations == 0)
-      non_violating.push_back(std::move(c));
-    else
-      violating.push_back(std::move(c));
-    int nv = static_cast<int>(non_violating.size());
-    if (nv > 0 && nv + static_cast<int>(violating.size()) >= num_candidates) stop.store(true);
+    // An Error is not a property of the node: never remembered.
+    const bool candidate = vs.is_success() && !c.victims.empty();
+    if (shard && !cloned && (candidate || vs.is_unschedulable())) {
+      std::lock_guard<std::mutex> g(shard->mu);
+      if (shard->m.size() > 8192) shard->m.clear();  // bounded (nodes that left the cluster)
+      MemoEntry& e = shard->m[c.node];
+      e.gen = src->generation;
+      e.tmpl = pod.template_hash;
+      e.candidate = candidate;
+      e.victims = c.victims;
+      e.num_pdb_violations = c.num_pdb_violations;
+    }
+    if (!candidate) return;
+    add_candidate(std::move(c));
   }, &stop);
   std::vector<Candidate> out = std::move(non_violating);
   for (auto& c : violating) out.push_back(std::move(c));
+  XS_LOGV(5, "preemption dry run").kv("pod", pod.key()).kv("potentialNodes", n).kv("candidates", out.size())
+      .kv("memo", memo_ok).kv("memoHits", memo_->hits.load()).kv("memoMisses", memo_->misses.load());
   return out;
 }
 

@@ -12,10 +12,14 @@
 // order (util.MoreImportantPod).
 #pragma once
 
+#include <array>
+#include <atomic>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <random>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "framework/plugin.h"
@@ -32,6 +36,11 @@ class PreemptionPolicy {
   virtual Status select_victims_on_node(CycleState& s, const Pod& preemptor, NodeInfo& ni,
                                         const std::vector<PDBPtr>& pdbs, std::vector<PodPtr>& victims,
                                         int& num_violating) = 0;
+  // True when select_victims_on_node's outcome is a function of the node's
+  // version, the preemptor's template and the node's nominated pods only
+  // (no clock, no quota or other cluster-wide state): the evaluator may then
+  // reuse a node's dry-run result across preemptors (Evaluator::dry_run).
+  virtual bool victims_depend_only_on_node() const { return false; }
 };
 
 struct Candidate {
@@ -43,7 +52,7 @@ struct Candidate {
 class Evaluator {
  public:
   Evaluator(std::string plugin_name, Handle& h, PreemptionPolicy* policy)
-      : plugin_(std::move(plugin_name)), h_(h), policy_(policy) {}
+      : plugin_(std::move(plugin_name)), h_(h), policy_(policy), memo_(std::make_unique<Memo>()) {}
   std::pair<PostFilterResult, Status> preempt(CycleState& s, const Pod& pod, const NodeStatusMap& m);
 
   // Exposed for tests / other plugins.
@@ -56,10 +65,35 @@ class Evaluator {
   // callExtenders: the configured preempt-verb extenders filter `cands`.
   Status call_extenders(const Pod& pod, std::vector<Candidate>& cands);
 
+  uint64_t memo_hits() const { return memo_->hits.load(std::memory_order_relaxed); }
+  uint64_t memo_misses() const { return memo_->misses.load(std::memory_order_relaxed); }
+
  private:
+  // Dry-run results per node, valid while (node generation, preemptor
+  // template) match and the node has no nominated pods. PreemptionBasic-like
+  // waves evaluate the same unchanged nodes for every preemptor of one
+  // template: the reference recomputes each (cloning the NodeInfo and
+  // re-running every Filter per reprieved victim), here the result is reused.
+  struct MemoEntry {
+    int64_t gen = -1;
+    uint64_t tmpl = 0;
+    bool candidate = false;
+    std::vector<PodPtr> victims;
+    int num_pdb_violations = 0;
+  };
+  struct Memo {
+    static constexpr size_t kShards = 32;
+    struct Shard {
+      std::mutex mu;
+      std::unordered_map<std::string, MemoEntry> m;
+    };
+    std::array<Shard, kShards> shards;
+    std::atomic<uint64_t> hits{0}, misses{0};
+  };
   std::string plugin_;
   Handle& h_;
   PreemptionPolicy* policy_;
+  std::unique_ptr<Memo> memo_;
 };
 
 // ---- helpers shared by policies ----

@@ -784,7 +784,11 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   if (!st.is_success()) {
     if (!st.is_unschedulable()) return st;
     d.node_to_status.reserve(all.size());
-    for (const auto& name : snapshot_.names) d.node_to_status.emplace(name, st);
+    const bool fresh = d.node_to_status.empty();
+    for (const auto& name : snapshot_.names) {
+      if (fresh) d.node_to_status.append_unique(name, st);
+      else d.node_to_status.emplace(name, st);
+    }
     d.unschedulable_plugins.insert(st.failed_plugin());
     return Status(Code::Unschedulable, st.message()).with_plugin(st.failed_plugin());
   }
@@ -823,8 +827,25 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status));
   }
   // Filter verdicts are reused only when every Filter plugin is node-local for
-  // this pod and no nominated pod can change a node's verdict.
-  const bool eq_filter = eq && (!nominator_ || nominator_->empty()) && fw.filters_node_local(p, snapshot_);
+  // this pod; a node with nominated pods is always evaluated with them added
+  // (uncached), every other node reads and fills the cache. (While any pod
+  // is nominated somewhere, e.g. during a preemption wave, the nodes without
+  // nominations keep their cached verdicts.)
+  bool eq_filter = eq && fw.filters_node_local(p, snapshot_);
+  const char* nom_mark = nullptr;
+  if (eq_filter && s.nominated && !s.nominated->empty()) {
+    nom_mark_.assign(n, 0);
+    for (const auto& [node, pods] : *s.nominated) {
+      if (pods.empty()) continue;
+      auto it = snapshot_.index.find(node);
+      if (it != snapshot_.index.end()) nom_mark_[it->second] = 1;
+    }
+    nom_mark = nom_mark_.data();
+  } else if (eq_filter && nominator_ && !nominator_->empty()) {
+    // Nominations without this cycle's view (explain, or a caller that did
+    // not snapshot them): no per-node knowledge, so no reuse.
+    eq_filter = false;
+  }
   int start = next_start_node_;
   // Per-node failures go to a position-indexed buffer (no lock, no map
   // insert per node); the NodeToStatusMap is only materialized when the
@@ -850,7 +871,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       if (pos >= n) pos -= n;
       const NodeInfo& ni = *all[pos];
       const Status* fp;
-      if (eq_filter) {
+      if (eq_filter && !(nom_mark && nom_mark[pos])) {
         EqSlot& slot = eq->slots[pos];
         if (slot.filter_gen == ni.generation) {
           ++hits;
@@ -889,7 +910,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       const NodeInfo& ni = *all[pos];
       Status own;
       const Status* fp = &own;
-      if (eq_filter) {
+      if (eq_filter && !(nom_mark && nom_mark[pos])) {
         EqSlot& slot = eq->slots[pos];
         if (slot.filter_gen == ni.generation) {
           ahits.fetch_add(1, std::memory_order_relaxed);
@@ -952,10 +973,12 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   if (feasible.empty() || full_diagnosis) {
     d.node_to_status.reserve(d.node_to_status.size() + static_cast<size_t>(n));
     std::unordered_map<const void*, std::unordered_map<const void*, size_t>> index;  // past 32 distinct
+    const bool fresh = d.node_to_status.empty();  // positions are distinct nodes: no duplicate check
     for (int pos = 0; pos < n; ++pos) {
       const Status* fs = fail_ptr_[pos];
       if (!fs) continue;
-      d.node_to_status.emplace(snapshot_.names[pos], *fs);
+      if (fresh) d.node_to_status.append_unique(snapshot_.names[pos], *fs);
+      else d.node_to_status.emplace(snapshot_.names[pos], *fs);
       size_t k = distinct.size();
       if (distinct.size() <= 32) {
         for (size_t j = 0; j < distinct.size(); ++j)

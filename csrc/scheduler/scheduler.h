@@ -179,6 +179,7 @@ class Scheduler {
   EqEntry* eq_entry(Framework& fw, const Pod& p);
   void release_retired();
   std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
+  std::vector<char> nom_mark_;    // ... and its nodes with nominated pods, per position
   std::vector<const Status*> fail_ptr_;
   static constexpr size_t kInformerWindow = 64;
   ParallelSite filter_site_;  // inline-vs-parallel cost model of Filter
