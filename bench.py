@@ -190,12 +190,14 @@ def main() -> int:
         # Untimed: Poisson gang arrivals at 50% / 90% of this shard's measured
         # throughput, gang types interleaved, held then deleted
         # (utils/openloop.py) — admission latency rather than burst queueing.
-        from flex_gpu_scheduler_amd.utils.openloop import run_open_loop
+        from flex_gpu_scheduler_amd.utils.openloop import open_loop_capacity, run_open_loop
 
-        cap = pods / elapsed if elapsed > 0 else 0.0
+        burst = pods / elapsed if elapsed > 0 else 0.0
+        cap = open_loop_capacity(shard, burst, seed=args.seed) if burst > 0 else 0.0
         extras["gang_admit_open_loop"] = {
+            "burst_capacity_pods_per_s": round(burst, 1),
             "capacity_pods_per_s": round(cap, 1),
-            **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed)
+            **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed + 1)
                for f in (0.5, 0.9)}} if cap > 0 else {}
     shard.close()
 

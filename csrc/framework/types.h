@@ -421,21 +421,35 @@ class NodeStatusMap {
       hashes_ = o.hashes_;
       slots_ = o.slots_;
       indexed_.store(o.indexed_.load(std::memory_order_acquire), std::memory_order_relaxed);
+      clear_deferred();
     }
     return *this;
   }
 
-  size_t size() const { return entries_.size(); }
-  bool empty() const { return entries_.empty(); }
-  const_iterator begin() const { return entries_.begin(); }
-  const_iterator end() const { return entries_.end(); }
-  iterator begin() { return entries_.begin(); }
-  iterator end() { return entries_.end(); }
+  size_t size() const { return deferred() ? deferred_.size() : entries_.size(); }
+  bool empty() const { return size() == 0; }
+  const_iterator begin() const {
+    materialize();
+    return entries_.begin();
+  }
+  const_iterator end() const {
+    materialize();
+    return entries_.end();
+  }
+  iterator begin() {
+    materialize();
+    return entries_.begin();
+  }
+  iterator end() {
+    materialize();
+    return entries_.end();
+  }
   void clear() {
     entries_.clear();
     hashes_.clear();
     slots_.clear();
     indexed_.store(0, std::memory_order_relaxed);
+    clear_deferred();
   }
   void reserve(size_t n) { entries_.reserve(n); }
   const_iterator find(std::string_view k) const {
@@ -448,7 +462,7 @@ class NodeStatusMap {
     int32_t i = lookup(k, hash(k));
     return i < 0 ? entries_.end() : entries_.begin() + i;
   }
-  size_t count(std::string_view k) const { return find(k) == end() ? 0 : 1; }
+  size_t count(std::string_view k) const { return status_of(k) ? 1 : 0; }
   std::pair<iterator, bool> emplace(std::string_view k, const Status& v) {
     ensure_index();
     const size_t h = hash(k);
@@ -457,19 +471,80 @@ class NodeStatusMap {
     index_tail();
     return {entries_.end() - 1, true};
   }
-  // Appends a node the caller knows is not in the map yet (a diagnosis built
-  // from one pass over distinct snapshot nodes). Nothing is hashed: the
-  // index is built on the first lookup, which most failed cycles (FitError
-  // message, preemption over the whole list) never make.
-  void append_unique(std::string_view k, const Status& v) { entries_.emplace_back(std::string(k), v); }
+  // Appends a node the caller knows is not in the map yet. Nothing is
+  // hashed: the index is built on the first lookup by key.
+  void append_unique(std::string_view k, const Status& v) {
+    materialize();
+    entries_.emplace_back(std::string(k), v);
+  }
   Status& operator[](std::string_view k) { return emplace(k, Status()).first->second; }
 
+  // ---- deferred form: what a failed scheduling cycle builds ----
+  // (snapshot position, status) pairs naming the snapshot's nodes, with no
+  // string or Status copied. Valid for the cycle that built them: `names`
+  // and `pos_index` are the Snapshot's, the statuses live in the cycle's
+  // Filter buffers. The first iteration, key lookup by iterator or copy
+  // materializes owned entries; status_of / count_code / for_each do not,
+  // and a PostFilter that only asks those (DefaultPreemption over 5,000
+  // nodes) never pays the copy.
+  void defer(const std::vector<std::string>* names, const std::unordered_map<std::string, size_t>* pos_index) {
+    clear();
+    def_names_ = names;
+    def_index_ = pos_index;
+    pos_to_def_.assign(names->size(), -1);
+  }
+  void append_deferred(int32_t pos, const Status* st) {
+    pos_to_def_[pos] = static_cast<int32_t>(deferred_.size());
+    deferred_.emplace_back(pos, st);
+  }
+  // The status recorded for node `k`, nullptr if none.
+  const Status* status_of(std::string_view k) const {
+    if (deferred()) {
+      auto it = def_index_->find(std::string(k));
+      if (it == def_index_->end() || it->second >= pos_to_def_.size()) return nullptr;
+      int32_t i = pos_to_def_[it->second];
+      return i < 0 ? nullptr : deferred_[i].second;
+    }
+    auto it = find(k);
+    return it == entries_.end() ? nullptr : &it->second;
+  }
+  size_t count_code(Code c) const {
+    size_t n = 0;
+    for_each([&](std::string_view, const Status& st) { n += st.code() == c; });
+    return n;
+  }
+  template <class F>
+  void for_each(F&& f) const {
+    if (deferred()) {
+      for (const auto& [pos, st] : deferred_) f(std::string_view((*def_names_)[pos]), *st);
+      return;
+    }
+    for (const auto& [k, st] : entries_) f(std::string_view(k), st);
+  }
+
  private:
+  bool deferred() const { return def_names_ != nullptr && !materialized_.load(std::memory_order_acquire); }
+  void clear_deferred() {
+    def_names_ = nullptr;
+    def_index_ = nullptr;
+    deferred_.clear();
+    pos_to_def_.clear();
+    materialized_.store(false, std::memory_order_relaxed);
+  }
+  void materialize() const {
+    if (!deferred()) return;
+    std::lock_guard<std::mutex> g(index_mu());
+    if (!deferred()) return;
+    entries_.reserve(entries_.size() + deferred_.size());
+    for (const auto& [pos, st] : deferred_) entries_.emplace_back((*def_names_)[pos], *st);
+    materialized_.store(true, std::memory_order_release);
+  }
   static size_t hash(std::string_view k) { return std::hash<std::string_view>{}(k); }
   // Indexes entries appended since the last lookup. Lookups on a shared map
   // from several threads are safe: the first one to arrive builds the index
   // under a lock, the others see it complete.
   void ensure_index() const {
+    materialize();
     if (indexed_.load(std::memory_order_acquire) == entries_.size()) return;
     std::lock_guard<std::mutex> g(index_mu());
     if (indexed_.load(std::memory_order_relaxed) == entries_.size()) return;
@@ -511,12 +586,18 @@ class NodeStatusMap {
     while (slots_[j] >= 0) j = (j + 1) & mask;
     slots_[j] = i;
   }
-  std::vector<value_type> entries_;
+  mutable std::vector<value_type> entries_;
   // Index over entries_[0, indexed_): each key hashed once, kept beside the
   // entry, so probing compares hashes before strings.
   mutable std::vector<size_t> hashes_;
   mutable std::vector<int32_t> slots_;  // power of two, at most half full; -1 = empty
   mutable std::atomic<size_t> indexed_{0};
+  // deferred form
+  const std::vector<std::string>* def_names_ = nullptr;
+  const std::unordered_map<std::string, size_t>* def_index_ = nullptr;
+  std::vector<std::pair<int32_t, const Status*>> deferred_;
+  std::vector<int32_t> pos_to_def_;
+  mutable std::atomic<bool> materialized_{false};
 };
 
 struct Victims {

@@ -64,8 +64,7 @@ class CrossNodePreemption : public Plugin, public PreemptionPolicy {
     PodPtr latest = h_.informers ? h_.informers->pod(pod_in.ns(), pod_in.name()) : nullptr;
     const Pod& pod = latest ? *latest : pod_in;
     const Status* nom = nullptr;
-    auto nit = m.find(pod.nominated_node_name);
-    if (nit != m.end()) nom = &nit->second;
+    if (!pod.nominated_node_name.empty()) nom = m.status_of(pod.nominated_node_name);
     if (!eligible(pod, nom)) return {PostFilterResult{}, Status::unschedulable("Pod is not eligible for preemption")};
     if (!h_.snapshot || h_.snapshot->nodes.empty()) return {PostFilterResult{}, Status::error("no nodes available")};
 

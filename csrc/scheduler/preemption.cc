@@ -123,17 +123,14 @@ int calculate_num_candidates(int num_nodes, int pct, int min_abs) {
 
 const std::vector<NodeInfoPtr>& nodes_where_preemption_might_help(const Snapshot& snap, const NodeStatusMap& m,
                                                                   std::vector<NodeInfoPtr>& out) {
-  size_t unresolvable = 0;
-  for (const auto& kv : m)
-    if (kv.second.code() == Code::UnschedulableAndUnresolvable) ++unresolvable;
-  if (unresolvable == 0) return snap.nodes;  // no copy of the node list
+  if (m.count_code(Code::UnschedulableAndUnresolvable) == 0) return snap.nodes;  // no copy of the node list
   // The map may carry names outside this snapshot (a PostFilter handed a map
   // built elsewhere), so a node is only skipped on its own unresolvable entry.
   out.clear();
   out.reserve(snap.nodes.size());
   for (const auto& ni : snap.nodes) {
-    auto it = m.find(ni->name());
-    if (it == m.end() || it->second.code() != Code::UnschedulableAndUnresolvable) out.push_back(ni);
+    const Status* st = m.status_of(ni->name());
+    if (!st || st->code() != Code::UnschedulableAndUnresolvable) out.push_back(ni);
   }
   return out;
 }
@@ -370,8 +367,7 @@ std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod&
   const Pod& pod = latest ? *latest : pod_in;
   // 1) eligibility
   const Status* nom = nullptr;
-  auto nit = m.find(pod.nominated_node_name);
-  if (nit != m.end()) nom = &nit->second;
+  if (!pod.nominated_node_name.empty()) nom = m.status_of(pod.nominated_node_name);
   if (!policy_->eligible(pod, nom))
     return {PostFilterResult{}, Status::unschedulable("Pod is not eligible for preemption")};
   // 2) candidates: nodes where preemption might help

@@ -82,7 +82,7 @@ class Evaluator {
     int num_pdb_violations = 0;
   };
   struct Memo {
-    static constexpr size_t kShards = 32;
+    static constexpr size_t kShards = 256;  // 16 dry-run workers rarely meet on one
     struct Shard {
       std::mutex mu;
       std::unordered_map<std::string, MemoEntry> m;

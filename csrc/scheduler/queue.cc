@@ -137,10 +137,11 @@ std::vector<PodPtr> Nominator::nominated_pods_for_node(const std::string& node) 
   return it == by_node_.end() ? std::vector<PodPtr>{} : it->second;
 }
 
-std::shared_ptr<const NominatedMap> Nominator::view() const {
+std::shared_ptr<const NominatedMap> Nominator::view(std::vector<std::string>* changed) const {
   std::lock_guard<std::mutex> g(mu_);
   NominatedMap& m = *mirror_;
   for (auto& c : log_) {
+    if (changed) changed->push_back(c.node);
     if (c.add) {
       m[c.node].push_back(std::move(c.pod));
       continue;

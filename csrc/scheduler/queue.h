@@ -59,7 +59,8 @@ class Nominator {
   // consumer: the scheduling thread, between cycles. The view is a mirror
   // that the changes since the last call are applied to (O(changes), not a
   // copy of the map); the previous cycle's Filter workers are done with it.
-  std::shared_ptr<const NominatedMap> view() const;
+  // `changed` (optional) receives the nodes whose entries this call updated.
+  std::shared_ptr<const NominatedMap> view(std::vector<std::string>* changed = nullptr) const;
   std::string nominated_node(const std::string& uid) const;
   size_t size() const;
   bool empty() const { return count_.load(std::memory_order_relaxed) == 0; }  // lock-free fast path

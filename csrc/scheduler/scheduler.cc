@@ -733,6 +733,37 @@ void Scheduler::release_retired() {
   }
 }
 
+// Which snapshot positions carry nominated pods: rebuilt from the view when
+// the view object or the node set changed, else updated for the nodes the
+// view's change log touched (a preemption wave keeps hundreds of pods
+// nominated; re-deriving every position per cycle was a hash lookup each).
+// Stale marks only send a node down the exact (uncached) path; every node
+// nominated in the view is always marked.
+void Scheduler::refresh_nom_mark(const NominatedMap* view) {
+  if (!view || view->empty()) {
+    nom_mark_valid_ = false;
+    return;
+  }
+  const size_t n = snapshot_.nodes.size();
+  auto mark = [&](const std::string& node) {
+    auto it = snapshot_.index.find(node);
+    if (it == snapshot_.index.end()) return;
+    auto vit = view->find(node);
+    nom_mark_[it->second] = vit != view->end() && !vit->second.empty();
+  };
+  if (!nom_mark_valid_ || view != nom_src_ || snapshot_.node_epoch != nom_epoch_ || nom_mark_.size() != n) {
+    nom_mark_.assign(n, 0);
+    for (const auto& [node, pods] : *view)
+      if (!pods.empty()) mark(node);
+  } else {
+    for (const auto& node : nom_changed_) mark(node);
+  }
+  nom_changed_.clear();
+  nom_src_ = view;
+  nom_epoch_ = snapshot_.node_epoch;
+  nom_mark_valid_ = true;
+}
+
 Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
   if (!opts_.equivalence_cache || p.template_hash == 0) return nullptr;
   auto& per_fw = eq_[&fw];
@@ -756,8 +787,9 @@ namespace {
 // "0/N nodes are available: k reason, ..." over a complete diagnosis.
 std::string fit_error_message(int n, const NodeStatusMap& m) {
   std::map<std::string, int> reasons;
-  for (const auto& [node, st] : m)
+  m.for_each([&](std::string_view, const Status& st) {
     for (const auto& r : st.reasons()) ++reasons[r];
+  });
   std::string msg = "0/" + std::to_string(n) + " nodes are available:";
   bool first = true;
   for (const auto& kv : reasons) {
@@ -834,12 +866,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   bool eq_filter = eq && fw.filters_node_local(p, snapshot_);
   const char* nom_mark = nullptr;
   if (eq_filter && s.nominated && !s.nominated->empty()) {
-    nom_mark_.assign(n, 0);
-    for (const auto& [node, pods] : *s.nominated) {
-      if (pods.empty()) continue;
-      auto it = snapshot_.index.find(node);
-      if (it != snapshot_.index.end()) nom_mark_[it->second] = 1;
-    }
+    if (!nom_mark_valid_ || s.nominated.get() != nom_src_) refresh_nom_mark(s.nominated.get());
     nom_mark = nom_mark_.data();
   } else if (eq_filter && nominator_ && !nominator_->empty()) {
     // Nominations without this cycle's view (explain, or a caller that did
@@ -971,13 +998,17 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   // failures), so plugins and reasons are tallied per distinct Status first.
   std::vector<std::pair<const Status*, int>> distinct;
   if (feasible.empty() || full_diagnosis) {
-    d.node_to_status.reserve(d.node_to_status.size() + static_cast<size_t>(n));
     std::unordered_map<const void*, std::unordered_map<const void*, size_t>> index;  // past 32 distinct
-    const bool fresh = d.node_to_status.empty();  // positions are distinct nodes: no duplicate check
+    // A fresh diagnosis is recorded in deferred form: (position, status)
+    // pairs over the snapshot's names and this cycle's Filter buffers, which
+    // outlive every consumer of the diagnosis (PostFilter, FitError).
+    const bool fresh = d.node_to_status.empty();
+    if (fresh) d.node_to_status.defer(&snapshot_.names, &snapshot_.index);
+    else d.node_to_status.reserve(d.node_to_status.size() + static_cast<size_t>(n));
     for (int pos = 0; pos < n; ++pos) {
       const Status* fs = fail_ptr_[pos];
       if (!fs) continue;
-      if (fresh) d.node_to_status.append_unique(snapshot_.names[pos], *fs);
+      if (fresh) d.node_to_status.append_deferred(pos, fs);
       else d.node_to_status.emplace(snapshot_.names[pos], *fs);
       size_t k = distinct.size();
       if (distinct.size() <= 32) {
@@ -1181,7 +1212,8 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   int64_t cycle_start = clock_->now_us();
   auto state = std::make_shared<CycleState>();
   state->record_metrics = std::uniform_real_distribution<double>(0, 1)(rng_) < opts_.metrics_sample_rate;
-  if (!nominator_->empty()) state->nominated = nominator_->view();
+  nom_changed_.clear();
+  if (!nominator_->empty()) state->nominated = nominator_->view(&nom_changed_);
   auto to_activate = std::make_shared<PodsToActivate>();
   state->write(kPodsToActivateKey, to_activate);
   int64_t cycle = queue_->scheduling_cycle();
@@ -1194,6 +1226,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   int clones = cache_->update_snapshot(snapshot_, tracer_.enabled() ? &lock_wait : nullptr, &pod->uid(), &already_assumed);
   if (already_assumed) return;  // skipPodSchedule: assumed by an earlier cycle
   release_retired();
+  refresh_nom_mark(state->nominated.get());
   const std::string& profile = fw->profile_name();
   {
     std::lock_guard<std::mutex> g(stats_mu_);

@@ -179,7 +179,12 @@ class Scheduler {
   EqEntry* eq_entry(Framework& fw, const Pod& p);
   void release_retired();
   std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
-  std::vector<char> nom_mark_;    // ... and its nodes with nominated pods, per position
+  std::vector<char> nom_mark_;    // nodes with nominated pods, per snapshot position (refresh_nom_mark)
+  std::vector<std::string> nom_changed_;
+  const NominatedMap* nom_src_ = nullptr;  // the view nom_mark_ describes
+  uint64_t nom_epoch_ = UINT64_MAX;
+  bool nom_mark_valid_ = false;
+  void refresh_nom_mark(const NominatedMap* view);
   std::vector<const Status*> fail_ptr_;
   static constexpr size_t kInformerWindow = 64;
   ParallelSite filter_site_;  // inline-vs-parallel cost model of Filter
