@@ -137,8 +137,6 @@ const std::vector<NodeInfoPtr>& nodes_where_preemption_might_help(const Snapshot
 
 std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
                                           const std::vector<PDBPtr>& pdbs, int offset, int num_candidates) {
-  std::vector<Candidate> violating, non_violating;
-  std::mutex mu;
   std::atomic<bool> stop{false};
   int n = static_cast<int>(potential.size());
   // Reuse is sound when the policy's victims depend on the node alone, no
@@ -148,14 +146,35 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
   const bool memo_ok = policy_->victims_depend_only_on_node() && pdbs.empty() && pod.template_hash != 0 &&
                        h_.snapshot && h_.framework && h_.framework->filters_node_local(pod, *h_.snapshot) &&
                        (s.nominated || !h_.nominator || h_.nominator->empty());
-  auto add_candidate = [&](Candidate&& c) {
-    std::lock_guard<std::mutex> g(mu);
-    if (c.num_pdb_violations == 0)
-      non_violating.push_back(std::move(c));
-    else
-      violating.push_back(std::move(c));
-    int nv = static_cast<int>(non_violating.size());
-    if (nv > 0 && nv + static_cast<int>(violating.size()) >= num_candidates) stop.store(true);
+  if (memo_ok) {
+    // Bounded: entries of nodes that left the cluster are dropped here,
+    // single-threaded, never while workers hold pointers into a shard.
+    const size_t limit = 2 * (static_cast<size_t>(n) / Memo::kShards + 64);
+    for (auto& sh : memo_->shards)
+      if (sh.m.size() > limit) sh.m.clear();
+  }
+  // Candidates land in preallocated slots claimed with one atomic add: the
+  // 16 workers never share a lock, and a remembered result is only a
+  // pointer here (its victims are copied on this thread afterwards, so the
+  // workers allocate nothing for it). Workers overshoot the stop by at most
+  // one node each.
+  struct Slot {
+    const MemoEntry* memo = nullptr;
+    const NodeInfo* node = nullptr;
+    Candidate c;
+  };
+  const int cap = num_candidates + 64;
+  std::vector<Slot> slots(static_cast<size_t>(cap));
+  std::atomic<int> used{0}, non_violating{0};
+  auto claim = [&](int num_pdb_violations) -> Slot* {
+    int k = used.fetch_add(1, std::memory_order_relaxed);
+    if (k >= cap) {
+      stop.store(true);
+      return nullptr;
+    }
+    int nv = num_pdb_violations == 0 ? non_violating.fetch_add(1) + 1 : non_violating.load();
+    if (nv > 0 && k + 1 >= num_candidates) stop.store(true);
+    return &slots[static_cast<size_t>(k)];
   };
   h_.parallelizer->until(n, [&](int i) {
     const NodeInfoPtr& src = potential[(offset + i) % n];
@@ -168,17 +187,20 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
       }
       if (!nominated_here) {
         shard = &memo_->shards[std::hash<std::string>{}(src->name()) % Memo::kShards];
-        std::unique_lock<std::mutex> g(shard->mu);
-        auto it = shard->m.find(src->name());
-        if (it != shard->m.end() && it->second.gen == src->generation && it->second.tmpl == pod.template_hash) {
+        const MemoEntry* hit = nullptr;
+        {
+          std::lock_guard<std::mutex> g(shard->mu);
+          auto it = shard->m.find(src->name());
+          if (it != shard->m.end() && it->second.gen == src->generation && it->second.tmpl == pod.template_hash)
+            hit = &it->second;  // stable: only this worker writes this node's entry during the run
+        }
+        if (hit) {
           memo_->hits.fetch_add(1, std::memory_order_relaxed);
-          if (!it->second.candidate) return;
-          Candidate c;
-          c.node = src->name();
-          c.victims = it->second.victims;
-          c.num_pdb_violations = it->second.num_pdb_violations;
-          g.unlock();
-          add_candidate(std::move(c));
+          if (!hit->candidate) return;
+          if (Slot* sl = claim(hit->num_pdb_violations)) {
+            sl->memo = hit;
+            sl->node = src.get();
+          }
           return;
         }
         memo_->misses.fetch_add(1, std::memory_order_relaxed);
@@ -210,7 +232,6 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
     const bool candidate = vs.is_success() && !c.victims.empty();
     if (shard && !cloned && (candidate || vs.is_unschedulable())) {
       std::lock_guard<std::mutex> g(shard->mu);
-      if (shard->m.size() > 8192) shard->m.clear();  // bounded (nodes that left the cluster)
       MemoEntry& e = shard->m[c.node];
       e.gen = src->generation;
       e.tmpl = pod.template_hash;
@@ -219,10 +240,28 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
       e.num_pdb_violations = c.num_pdb_violations;
     }
     if (!candidate) return;
-    add_candidate(std::move(c));
+    if (Slot* sl = claim(c.num_pdb_violations)) sl->c = std::move(c);
   }, &stop);
-  std::vector<Candidate> out = std::move(non_violating);
-  for (auto& c : violating) out.push_back(std::move(c));
+  // Non-violating candidates first, then the violating ones (upstream order).
+  const int k = std::min(used.load(), cap);
+  std::vector<Candidate> out;
+  out.reserve(static_cast<size_t>(k));
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int j = 0; j < k; ++j) {
+      Slot& sl = slots[static_cast<size_t>(j)];
+      const int npv = sl.memo ? sl.memo->num_pdb_violations : sl.c.num_pdb_violations;
+      if ((npv == 0) != (pass == 0)) continue;
+      if (sl.memo) {
+        Candidate c;
+        c.node = sl.node->name();
+        c.victims = sl.memo->victims;
+        c.num_pdb_violations = npv;
+        out.push_back(std::move(c));
+      } else if (!sl.c.node.empty()) {
+        out.push_back(std::move(sl.c));
+      }
+    }
+  }
   XS_LOGV(5, "preemption dry run").kv("pod", pod.key()).kv("potentialNodes", n).kv("candidates", out.size())
       .kv("memo", memo_ok).kv("memoHits", memo_->hits.load()).kv("memoMisses", memo_->misses.load());
   return out;

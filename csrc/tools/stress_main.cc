@@ -89,17 +89,19 @@ int main(int argc, char** argv) {
     std::vector<Json> pgs(wave["podgroups"].items().begin(), wave["podgroups"].items().end());
     std::vector<Json> pods(wave["pods"].items().begin(), wave["pods"].items().end());
     size_t n = pods.size();
+    // Workloads with pods that fit nowhere (Unschedulable) bind fewer.
+    const size_t expect = static_cast<size_t>(wave["expect_bound"].as_int(static_cast<int64_t>(n)));
     auto t0 = std::chrono::steady_clock::now();
     store->create_many("podgroups", std::move(pgs));
     // PodGroup-aligned chunks, as the Python bulk-create path commits them.
     store->create_chunked("pods", [&](const std::function<void(Json&&)>& emit) {
       for (auto& p : pods) emit(std::move(p));
     });
-    if (!wait_bound(bound + n, "wave", w)) {
+    if (!wait_bound(bound + expect, "wave", w)) {
       sched.stop();
       return 1;
     }
-    bound += n;
+    bound += expect;
     std::string ns = wave["namespace"].str_or("bench");
     store->delete_all("pods", ns);
     store->delete_all("podgroups", ns);

@@ -43,8 +43,10 @@ def write_workload(out: str | Path, name: str, nodes: int, pods: int, options: d
         (d / "init.json").unlink()
     ns = w["pods"][0]["metadata"].get("namespace", "default")
     for i in range(4):
-        (d / f"wave_{i}.json").write_text(json.dumps({"namespace": ns, "podgroups": w["extra_objects"].get("podgroups", []),
-                                                      "pods": w["pods"]}))
+        wave = {"namespace": ns, "podgroups": w["extra_objects"].get("podgroups", []), "pods": w["pods"]}
+        if w.get("expect_bound") is not None:
+            wave["expect_bound"] = w["expect_bound"]
+        (d / f"wave_{i}.json").write_text(json.dumps(wave))
     return d
 
 

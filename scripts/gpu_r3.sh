@@ -25,7 +25,7 @@ for step in "$@"; do
                 --cpus l3 > "$OUT/sched_perf_500.jsonl" 2>&1 ;;
     sched5000) timeout -k 10 700 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 5000 --pods 5000 \
                 --cpus l3 > "$OUT/sched_perf_5000.jsonl" 2>&1 ;;
-    remote) timeout -k 10 600 python -u -m flex_gpu_scheduler_amd.tools.remote_bench > "$OUT/remote_bench.jsonl" \
+    remote) timeout -k 10 600 python -u -m flex_gpu_scheduler_amd.tools.remote_bench --matrix > "$OUT/remote_bench.jsonl" \
               2>&1 ;;
     sample_pre|sample_sched)
       # Wall-clock thread sampler of the native stress driver

@@ -24,7 +24,7 @@ run() {  # name dir waves
 }
 run bench64 /tmp/san_bench 3
 for spec in "PreemptionBasic 200 400" "SchedulingBasic 500 1000" "TopologySpreading 300 600" \
-            "SchedulingPodAntiAffinity 300 300" "Unschedulable 300 600" "SchedulingGangs 200 800"; do
+            "SchedulingPodAntiAffinity 300 300" "Unschedulable 300 600" "MI355X-Gang8 200 800" "MI355X-FlexGPUMix 200 800"; do
   set -- $spec
   python -m flex_gpu_scheduler_amd.tools.stress "/tmp/san_$1" --workload "$1" --nodes "$2" --pods "$3" > /dev/null \
     || { echo "skip $1 (no such workload)" | tee -a "$out"; continue; }
