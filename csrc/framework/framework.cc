@@ -239,6 +239,27 @@ Status Framework::run_filter_with_nominated_pods_inplace(CycleState& s, const Po
   return filter_with_nominated(s, p, ni, &ni);
 }
 
+uint64_t Framework::nominated_signature(const CycleState& s, const Pod& p, const NodeInfo& ni, bool* cacheable) const {
+  *cacheable = true;
+  if (!s.nominated || !ni.node) {
+    *cacheable = false;  // no cycle view: nominations not pinned for this cycle
+    return 1;
+  }
+  auto it = s.nominated->find(ni.name());
+  if (it == s.nominated->end()) return 0;
+  uint64_t h = 1469598103934665603ULL;
+  bool any = false;
+  for (const auto& np : it->second) {
+    if (np->priority < p.priority || np->uid() == p.uid()) continue;
+    any = true;
+    uint64_t x = std::hash<std::string>{}(np->uid()) ^ (np->template_hash * 0x9E3779B97F4A7C15ULL) ^
+                 (static_cast<uint64_t>(static_cast<uint32_t>(np->priority)) << 17);
+    h = (h ^ x) * 1099511628211ULL;
+    if (pre_filter_extensions_affected(s, p, *np)) *cacheable = false;
+  }
+  return any ? (h ? h : 1) : 0;
+}
+
 Status Framework::filter_with_nominated(CycleState& s, const Pod& p, const NodeInfo& ni, NodeInfo* inplace) {
   Status st;
   bool pods_added = false;

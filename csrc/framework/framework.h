@@ -34,6 +34,11 @@ struct ProfileConfig {
 struct EqSlot {
   int64_t filter_gen = -1;
   Status filter;
+  // The verdict with the node's nominated pods added, for the set of them
+  // whose signature is nom_sig (Framework::nominated_signature).
+  int64_t nom_gen = -1;
+  uint64_t nom_sig = 0;
+  Status nom_filter;
   int64_t score_gen = -1;
   std::vector<int64_t> raw;  // per scorer, in Framework scorer order
 };
@@ -64,6 +69,10 @@ class Framework {
   bool pre_filter_extensions_affected(const CycleState& s, const Pod& to_schedule, const Pod& other) const;
   Status run_filter(CycleState& s, const Pod& p, const NodeInfo& ni);
   Status run_filter_with_nominated_pods(CycleState& s, const Pod& p, const NodeInfo& ni);
+  // Hash of the nominated pods on `ni` that run_filter_with_nominated_pods
+  // would add for `p` (priority >= p's, not p itself), 0 if none. `cacheable`
+  // turns false when one of them reacts with a PreFilter extension.
+  uint64_t nominated_signature(const CycleState& s, const Pod& p, const NodeInfo& ni, bool* cacheable) const;
   // The same on a NodeInfo the caller owns (a preemption dry run's scratch):
   // nominated pods are added to it and removed again, no copy is made.
   Status run_filter_with_nominated_pods_inplace(CycleState& s, const Pod& p, NodeInfo& ni);

@@ -135,8 +135,28 @@ const std::vector<NodeInfoPtr>& nodes_where_preemption_might_help(const Snapshot
   return out;
 }
 
+struct Evaluator::DryRun {
+  struct Slot {
+    const MemoEntry* memo = nullptr;
+    const NodeInfo* node = nullptr;
+    Candidate c;
+  };
+  std::vector<Slot> slots;
+  std::vector<CandidateRef> refs;  // into slots / memo entries, non-violating first
+};
+
 std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
                                           const std::vector<PDBPtr>& pdbs, int offset, int num_candidates) {
+  DryRun dr;
+  dry_run_refs(s, pod, potential, pdbs, offset, num_candidates, dr);
+  std::vector<Candidate> out;
+  out.reserve(dr.refs.size());
+  for (const auto& r : dr.refs) out.push_back(Candidate{*r.node, *r.victims, r.num_pdb_violations});
+  return out;
+}
+
+void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
+                             const std::vector<PDBPtr>& pdbs, int offset, int num_candidates, DryRun& dr) {
   std::atomic<bool> stop{false};
   int n = static_cast<int>(potential.size());
   // Reuse is sound when the policy's victims depend on the node alone, no
@@ -158,13 +178,10 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
   // pointer here (its victims are copied on this thread afterwards, so the
   // workers allocate nothing for it). Workers overshoot the stop by at most
   // one node each.
-  struct Slot {
-    const MemoEntry* memo = nullptr;
-    const NodeInfo* node = nullptr;
-    Candidate c;
-  };
+  using Slot = DryRun::Slot;
   const int cap = num_candidates + 64;
-  std::vector<Slot> slots(static_cast<size_t>(cap));
+  std::vector<Slot>& slots = dr.slots;
+  slots.assign(static_cast<size_t>(cap), Slot{});
   std::atomic<int> used{0}, non_violating{0};
   auto claim = [&](int num_pdb_violations) -> Slot* {
     int k = used.fetch_add(1, std::memory_order_relaxed);
@@ -244,69 +261,74 @@ std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const s
   }, &stop);
   // Non-violating candidates first, then the violating ones (upstream order).
   const int k = std::min(used.load(), cap);
-  std::vector<Candidate> out;
-  out.reserve(static_cast<size_t>(k));
+  dr.refs.clear();
+  dr.refs.reserve(static_cast<size_t>(k));
   for (int pass = 0; pass < 2; ++pass) {
     for (int j = 0; j < k; ++j) {
-      Slot& sl = slots[static_cast<size_t>(j)];
-      const int npv = sl.memo ? sl.memo->num_pdb_violations : sl.c.num_pdb_violations;
-      if ((npv == 0) != (pass == 0)) continue;
+      const Slot& sl = slots[static_cast<size_t>(j)];
       if (sl.memo) {
-        Candidate c;
-        c.node = sl.node->name();
-        c.victims = sl.memo->victims;
-        c.num_pdb_violations = npv;
-        out.push_back(std::move(c));
+        if ((sl.memo->num_pdb_violations == 0) != (pass == 0)) continue;
+        dr.refs.push_back(CandidateRef{&sl.node->name(), &sl.memo->victims, sl.memo->num_pdb_violations});
       } else if (!sl.c.node.empty()) {
-        out.push_back(std::move(sl.c));
+        if ((sl.c.num_pdb_violations == 0) != (pass == 0)) continue;
+        dr.refs.push_back(CandidateRef{&sl.c.node, &sl.c.victims, sl.c.num_pdb_violations});
       }
     }
   }
-  XS_LOGV(5, "preemption dry run").kv("pod", pod.key()).kv("potentialNodes", n).kv("candidates", out.size())
+  XS_LOGV(5, "preemption dry run").kv("pod", pod.key()).kv("potentialNodes", n).kv("candidates", dr.refs.size())
       .kv("memo", memo_ok).kv("memoHits", memo_->hits.load()).kv("memoMisses", memo_->misses.load());
-  return out;
 }
 
 std::string Evaluator::pick_one_node(const std::vector<Candidate>& cands) {
-  if (cands.empty()) return {};
-  std::vector<const Candidate*> cur;
-  for (const auto& c : cands) {
-    if (c.victims.empty()) return c.node;  // no preemption needed at all
-    cur.push_back(&c);
+  std::vector<CandidateRef> refs;
+  refs.reserve(cands.size());
+  for (const auto& c : cands) refs.push_back(CandidateRef{&c.node, &c.victims, c.num_pdb_violations});
+  size_t i = pick_one(refs);
+  return i < cands.size() ? cands[i].node : std::string();
+}
+
+size_t Evaluator::pick_one(const std::vector<CandidateRef>& cands) {
+  if (cands.empty()) return SIZE_MAX;
+  // Candidate indices still tied; filtered in place by each criterion.
+  thread_local std::vector<uint32_t> cur;
+  cur.clear();
+  for (size_t i = 0; i < cands.size(); ++i) {
+    if (cands[i].victims->empty()) return i;  // no preemption needed at all
+    cur.push_back(static_cast<uint32_t>(i));
   }
   auto keep_min = [&](auto key) {
     int64_t best = LLONG_MAX;
-    for (auto* c : cur) best = std::min<int64_t>(best, key(*c));
-    std::vector<const Candidate*> next;
-    for (auto* c : cur)
-      if (key(*c) == best) next.push_back(c);
-    cur.swap(next);
+    for (uint32_t i : cur) best = std::min<int64_t>(best, key(cands[i]));
+    size_t w = 0;
+    for (uint32_t i : cur)
+      if (key(cands[i]) == best) cur[w++] = i;
+    cur.resize(w);
   };
   // victims are sorted most-important first, so victims[0] is the highest priority.
-  keep_min([](const Candidate& c) { return static_cast<int64_t>(c.num_pdb_violations); });
-  if (cur.size() > 1) keep_min([](const Candidate& c) { return static_cast<int64_t>(c.victims[0]->priority); });
+  keep_min([](const CandidateRef& c) { return static_cast<int64_t>(c.num_pdb_violations); });
+  if (cur.size() > 1) keep_min([](const CandidateRef& c) { return static_cast<int64_t>((*c.victims)[0]->priority); });
   if (cur.size() > 1)
-    keep_min([](const Candidate& c) {
+    keep_min([](const CandidateRef& c) {
       int64_t sum = 0;
-      for (const auto& v : c.victims) sum += static_cast<int64_t>(v->priority) + INT32_MAX + 1;
+      for (const auto& v : *c.victims) sum += static_cast<int64_t>(v->priority) + INT32_MAX + 1;
       return sum;
     });
-  if (cur.size() > 1) keep_min([](const Candidate& c) { return static_cast<int64_t>(c.victims.size()); });
+  if (cur.size() > 1) keep_min([](const CandidateRef& c) { return static_cast<int64_t>(c.victims->size()); });
   if (cur.size() > 1) {
     // The node whose earliest-started victim started latest.
-    const Candidate* best = nullptr;
+    size_t best = cur.front();
     int64_t latest = LLONG_MIN;
-    for (auto* c : cur) {
+    for (uint32_t i : cur) {
       int64_t earliest = LLONG_MAX;
-      for (const auto& v : c->victims) earliest = std::min(earliest, pod_start_time(*v));
+      for (const auto& v : *cands[i].victims) earliest = std::min(earliest, pod_start_time(*v));
       if (earliest > latest) {
         latest = earliest;
-        best = c;
+        best = i;
       }
     }
-    return best->node;
+    return best;
   }
-  return cur.front()->node;
+  return cur.front();
 }
 
 Status Evaluator::prepare_candidate(const Candidate& c, const Pod& pod) {
@@ -418,25 +440,33 @@ std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod&
                                                       " nodes are available: preemption is not helpful for scheduling.")};
   std::vector<PDBPtr> pdbs = h_.informers ? h_.informers->pdbs() : std::vector<PDBPtr>{};
   auto [offset, num] = policy_->offset_and_num_candidates(static_cast<int>(potential.size()));
-  auto cands = dry_run(s, pod, potential, pdbs, offset, num);
-  if (cands.empty())
+  DryRun dr;
+  dry_run_refs(s, pod, potential, pdbs, offset, num, dr);
+  if (dr.refs.empty())
     return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +
                                                       " nodes are available: no preemption victims found.")};
-  // 3) extenders with a preempt verb narrow the candidates
+  Candidate best;
   if (h_.extenders && !h_.extenders->empty()) {
+    // 3) extenders with a preempt verb narrow the candidates (they need the
+    // whole node -> victims map, so the candidates are materialized)
+    std::vector<Candidate> cands;
+    cands.reserve(dr.refs.size());
+    for (const auto& r : dr.refs) cands.push_back(Candidate{*r.node, *r.victims, r.num_pdb_violations});
     Status est = call_extenders(pod, cands);
     if (!est.is_success()) return {PostFilterResult{}, est};
     if (cands.empty()) return {PostFilterResult{}, Status::unschedulable("no candidate node for preemption")};
+    std::string node = pick_one_node(cands);
+    for (auto& c : cands)
+      if (c.node == node) best = std::move(c);
+  } else {
+    // 4) best candidate, chosen over references; only it is copied
+    const CandidateRef& r = dr.refs[pick_one(dr.refs)];
+    best = Candidate{*r.node, *r.victims, r.num_pdb_violations};
   }
-  // 4) best candidate
-  std::string node = pick_one_node(cands);
-  const Candidate* best = nullptr;
-  for (const auto& c : cands)
-    if (c.node == node) best = &c;
   // 5) prepare
-  Status st = prepare_candidate(*best, pod);
+  Status st = prepare_candidate(best, pod);
   if (!st.is_success()) return {PostFilterResult{}, st};
-  return {PostFilterResult{node}, Status()};
+  return {PostFilterResult{best.node}, Status()};
 }
 
 }  // namespace xsched

@@ -48,6 +48,12 @@ struct Candidate {
   std::vector<PodPtr> victims;
   int num_pdb_violations = 0;
 };
+// A candidate by reference (into a dry run's results or a Candidate).
+struct CandidateRef {
+  const std::string* node = nullptr;
+  const std::vector<PodPtr>* victims = nullptr;
+  int num_pdb_violations = 0;
+};
 
 class Evaluator {
  public:
@@ -59,6 +65,8 @@ class Evaluator {
   std::vector<Candidate> dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
                                  const std::vector<PDBPtr>& pdbs, int offset, int num_candidates);
   static std::string pick_one_node(const std::vector<Candidate>& cands);
+  // pickOneNodeForPreemption over references: the index of the chosen one.
+  static size_t pick_one(const std::vector<CandidateRef>& cands);
   // prepareCandidate: reject waiting victims, delete the others, clear
   // lower-priority nominations on the node (also used by CrossNodePreemption).
   Status prepare_candidate(const Candidate& c, const Pod& pod);
@@ -69,6 +77,11 @@ class Evaluator {
   uint64_t memo_misses() const { return memo_->misses.load(std::memory_order_relaxed); }
 
  private:
+  struct DryRun;
+  // The dry run proper: candidates in `out` (non-violating first), each a
+  // reference into `out`'s storage or the memo, nothing copied.
+  void dry_run_refs(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
+                    const std::vector<PDBPtr>& pdbs, int offset, int num_candidates, DryRun& out);
   // Dry-run results per node, valid while (node generation, preemptor
   // template) match and the node has no nominated pods. PreemptionBasic-like
   // waves evaluate the same unchanged nodes for every preemptor of one

@@ -859,10 +859,10 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status));
   }
   // Filter verdicts are reused only when every Filter plugin is node-local for
-  // this pod; a node with nominated pods is always evaluated with them added
-  // (uncached), every other node reads and fills the cache. (While any pod
-  // is nominated somewhere, e.g. during a preemption wave, the nodes without
-  // nominations keep their cached verdicts.)
+  // this pod. A node with nominated pods is evaluated with them added; that
+  // verdict is cached too, keyed by the set of nominated pods that count for
+  // this pod (Framework::nominated_signature), unless one of them reacts
+  // with a PreFilter extension (the state would then not be node-local).
   bool eq_filter = eq && fw.filters_node_local(p, snapshot_);
   const char* nom_mark = nullptr;
   if (eq_filter && s.nominated && !s.nominated->empty()) {
@@ -888,6 +888,41 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   uint64_t hits = 0;
   if (static_cast<int>(found_buf_.size()) < to_find) found_buf_.resize(to_find);
   if (static_cast<int>(found_pos_buf_.size()) < to_find) found_pos_buf_.resize(to_find);
+  // One node's verdict: from the equivalence cache when it is valid for the
+  // node's version (and, on a node with nominated pods, for the same set of
+  // nominated pods), else computed into `own` or the cache slot.
+  auto eval_node = [&](int pos, const NodeInfo& ni, Status& own, bool* hit) -> const Status* {
+    if (!eq_filter) {
+      own = fw.run_filter_with_nominated_pods(s, p, ni);
+      return &own;
+    }
+    EqSlot& slot = eq->slots[pos];
+    uint64_t sig = 0;
+    bool cacheable = true;
+    if (nom_mark && nom_mark[pos]) sig = fw.nominated_signature(s, p, ni, &cacheable);
+    if (sig == 0) {  // no nominated pod counts for this pod: the plain verdict
+      if (slot.filter_gen == ni.generation) {
+        *hit = true;
+      } else {
+        slot.filter = fw.run_filter(s, p, ni);
+        slot.filter_gen = ni.generation;
+      }
+      return &slot.filter;
+    }
+    if (cacheable && slot.nom_gen == ni.generation && slot.nom_sig == sig) {
+      *hit = true;
+      return &slot.nom_filter;
+    }
+    Status st = fw.run_filter_with_nominated_pods(s, p, ni);
+    if (!cacheable) {
+      own = std::move(st);
+      return &own;
+    }
+    slot.nom_filter = std::move(st);
+    slot.nom_gen = ni.generation;
+    slot.nom_sig = sig;
+    return &slot.nom_filter;
+  };
   if (parallelizer_->plan_inline(n, &filter_site_)) {
     // Serial path (every cluster below the parallel threshold, and larger
     // ones whose verdicts mostly come from the equivalence cache): plain
@@ -897,20 +932,9 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       int pos = start + i;
       if (pos >= n) pos -= n;
       const NodeInfo& ni = *all[pos];
-      const Status* fp;
-      if (eq_filter && !(nom_mark && nom_mark[pos])) {
-        EqSlot& slot = eq->slots[pos];
-        if (slot.filter_gen == ni.generation) {
-          ++hits;
-        } else {
-          slot.filter = fw.run_filter(s, p, ni);
-          slot.filter_gen = ni.generation;
-        }
-        fp = &slot.filter;
-      } else {
-        fail_buf_[pos] = fw.run_filter_with_nominated_pods(s, p, ni);
-        fp = &fail_buf_[pos];
-      }
+      bool hit = false;
+      const Status* fp = eval_node(pos, ni, fail_buf_[pos], &hit);
+      hits += hit;
       ++processed;
       if (fp->is_success()) {
         found_buf_[c] = &ni;
@@ -936,19 +960,9 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       const int pos = (start + i) % n;
       const NodeInfo& ni = *all[pos];
       Status own;
-      const Status* fp = &own;
-      if (eq_filter && !(nom_mark && nom_mark[pos])) {
-        EqSlot& slot = eq->slots[pos];
-        if (slot.filter_gen == ni.generation) {
-          ahits.fetch_add(1, std::memory_order_relaxed);
-        } else {
-          slot.filter = fw.run_filter(s, p, ni);
-          slot.filter_gen = ni.generation;
-        }
-        fp = &slot.filter;
-      } else {
-        own = fw.run_filter_with_nominated_pods(s, p, ni);
-      }
+      bool hit = false;
+      const Status* fp = eval_node(pos, ni, own, &hit);
+      if (hit) ahits.fetch_add(1, std::memory_order_relaxed);
       const Status& fst = *fp;
       if (fst.is_success()) {
         int len = count.fetch_add(1) + 1;
