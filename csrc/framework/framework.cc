@@ -247,9 +247,16 @@ uint64_t Framework::nominated_signature(const CycleState& s, const Pod& p, const
   }
   auto it = s.nominated->find(ni.name());
   if (it == s.nominated->end()) return 0;
+  return nominated_signature(s, p, &it->second, cacheable);
+}
+
+uint64_t Framework::nominated_signature(const CycleState& s, const Pod& p, const std::vector<PodPtr>* list,
+                                        bool* cacheable) const {
+  *cacheable = true;
+  if (!list) return 0;
   uint64_t h = 1469598103934665603ULL;
   bool any = false;
-  for (const auto& np : it->second) {
+  for (const auto& np : *list) {
     if (np->priority < p.priority || np->uid() == p.uid()) continue;
     any = true;
     uint64_t x = std::hash<std::string>{}(np->uid()) ^ (np->template_hash * 0x9E3779B97F4A7C15ULL) ^

@@ -73,6 +73,9 @@ class Framework {
   // would add for `p` (priority >= p's, not p itself), 0 if none. `cacheable`
   // turns false when one of them reacts with a PreFilter extension.
   uint64_t nominated_signature(const CycleState& s, const Pod& p, const NodeInfo& ni, bool* cacheable) const;
+  // The same over the node's nominated list when the caller already has it.
+  uint64_t nominated_signature(const CycleState& s, const Pod& p, const std::vector<PodPtr>* list,
+                               bool* cacheable) const;
   // The same on a NodeInfo the caller owns (a preemption dry run's scratch):
   // nominated pods are added to it and removed again, no copy is made.
   Status run_filter_with_nominated_pods_inplace(CycleState& s, const Pod& p, NodeInfo& ni);

@@ -749,10 +749,13 @@ void Scheduler::refresh_nom_mark(const NominatedMap* view) {
     auto it = snapshot_.index.find(node);
     if (it == snapshot_.index.end()) return;
     auto vit = view->find(node);
-    nom_mark_[it->second] = vit != view->end() && !vit->second.empty();
+    const bool on = vit != view->end() && !vit->second.empty();
+    nom_mark_[it->second] = on;
+    nom_list_[it->second] = on ? &vit->second : nullptr;  // map nodes do not move
   };
   if (!nom_mark_valid_ || view != nom_src_ || snapshot_.node_epoch != nom_epoch_ || nom_mark_.size() != n) {
     nom_mark_.assign(n, 0);
+    nom_list_.assign(n, nullptr);
     for (const auto& [node, pods] : *view)
       if (!pods.empty()) mark(node);
   } else {
@@ -899,7 +902,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     EqSlot& slot = eq->slots[pos];
     uint64_t sig = 0;
     bool cacheable = true;
-    if (nom_mark && nom_mark[pos]) sig = fw.nominated_signature(s, p, ni, &cacheable);
+    if (nom_mark && nom_mark[pos]) sig = fw.nominated_signature(s, p, nom_list_[pos], &cacheable);
     if (sig == 0) {  // no nominated pod counts for this pod: the plain verdict
       if (slot.filter_gen == ni.generation) {
         *hit = true;
@@ -1672,7 +1675,15 @@ void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const
   // the next cycle must already see this one, before the status patch comes
   // back through the informer (scheduler.go handleSchedulingFailure).
   if (!nominated.empty()) nominator_->add(latest && latest->uid() == pod->uid() ? latest : pod, nominated);
-  fw.handle().client->record_event("Pod", pod->ns(), pod->name(), "Warning", "FailedScheduling", st.message());
+  // The event goes out on the binder pool: the recorder is asynchronous in
+  // kube-scheduler too (an EventBroadcaster), only the status update below
+  // is written from the scheduling loop.
+  binder_->submit([client = fw.handle().client, pod, msg = st.message()] {
+    try {
+      client->record_event("Pod", pod->ns(), pod->name(), "Warning", "FailedScheduling", msg);
+    } catch (const std::exception&) {
+    }
+  });
   if (!opts_.status_updates) return;
   // updatePod: PodScheduled=False condition + nominatedNodeName, only when changed.
   std::string msg = st.message();

@@ -180,6 +180,7 @@ class Scheduler {
   void release_retired();
   std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
   std::vector<char> nom_mark_;    // nodes with nominated pods, per snapshot position (refresh_nom_mark)
+  std::vector<const std::vector<PodPtr>*> nom_list_;  // ... and their lists in the view (valid for the cycle)
   std::vector<std::string> nom_changed_;
   const NominatedMap* nom_src_ = nullptr;  // the view nom_mark_ describes
   uint64_t nom_epoch_ = UINT64_MAX;

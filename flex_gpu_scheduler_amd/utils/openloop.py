@@ -85,17 +85,26 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
             "mean_arrival_lag_us": round(late_us / max(1, n), 1)}
 
 
-def open_loop_capacity(shard, offered_pods_per_s: float, duration_s: float = 0.5, seed: int = 0) -> float:
-    """Sustained open-loop throughput (pods/s): gangs offered faster than
-    they can be served and deleted as soon as they are bound (no GPU
-    pressure), so the run is limited by the scheduler, the store and the
-    per-gang API writes, not by the cluster filling up. The burst headline
-    creates and deletes whole waves in one store transaction each; arriving
-    one gang at a time costs more per pod, so this is the capacity the
-    50%/90% loads are fractions of."""
-    r = run_open_loop(shard, offered_pods_per_s, duration_s, seed=seed, occupancy=0.0)
-    pods = sum(v["n"] * (4 if k == "cpx4" else int(k)) for k, v in r["by_gang"].items())
-    return pods / max(r["wall_s"], 1e-6)
+def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 0.3, seed: int = 0,
+                       start_pods_per_s: float = 2000.0) -> float:
+    """Sustained open-loop throughput (pods/s): the highest rate the shard
+    keeps up with when gangs arrive one at a time and are deleted as soon as
+    they are bound (no GPU pressure, so the scheduler, the store and the
+    per-gang API writes are the limit, not the cluster filling up). Probes
+    at rates x1.5 apart from `start_pods_per_s` up to `max_pods_per_s` (the
+    burst capacity) and stops at the first rate it cannot keep up with (the
+    last gang done more than 1.5x the arrival window after the first
+    arrival): past that point a backlog builds and the throughput of an
+    overloaded run would understate the capacity."""
+    best, rate = 0.0, start_pods_per_s
+    while rate <= max_pods_per_s:
+        r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=0.0)
+        pods = sum(v["n"] * (4 if k == "cpx4" else int(k)) for k, v in r["by_gang"].items())
+        if r["wall_s"] > 1.5 * duration_s + 0.05 or any(v["unbound"] for v in r["by_gang"].values()):
+            break
+        best = max(best, pods / max(r["wall_s"], 1e-6))
+        rate *= 1.5
+    return best
 
 
 def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: int = 0,
