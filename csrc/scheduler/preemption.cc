@@ -7,6 +7,7 @@
 #include <climits>
 #include <map>
 #include <mutex>
+#include <tuple>
 
 #include "framework/framework.h"
 #include "framework/waiting_pods.h"
@@ -288,47 +289,37 @@ std::string Evaluator::pick_one_node(const std::vector<Candidate>& cands) {
 }
 
 size_t Evaluator::pick_one(const std::vector<CandidateRef>& cands) {
+  // pickOneNodeForPreemption's criteria in order, as one lexicographic key
+  // per candidate and a single pass: fewest PDB violations, lowest
+  // highest-priority victim, lowest priority sum, fewest victims, then the
+  // latest "earliest victim start"; the first candidate wins a full tie.
   if (cands.empty()) return SIZE_MAX;
-  // Candidate indices still tied; filtered in place by each criterion.
-  thread_local std::vector<uint32_t> cur;
-  cur.clear();
-  for (size_t i = 0; i < cands.size(); ++i) {
-    if (cands[i].victims->empty()) return i;  // no preemption needed at all
-    cur.push_back(static_cast<uint32_t>(i));
-  }
-  auto keep_min = [&](auto key) {
-    int64_t best = LLONG_MAX;
-    for (uint32_t i : cur) best = std::min<int64_t>(best, key(cands[i]));
-    size_t w = 0;
-    for (uint32_t i : cur)
-      if (key(cands[i]) == best) cur[w++] = i;
-    cur.resize(w);
-  };
-  // victims are sorted most-important first, so victims[0] is the highest priority.
-  keep_min([](const CandidateRef& c) { return static_cast<int64_t>(c.num_pdb_violations); });
-  if (cur.size() > 1) keep_min([](const CandidateRef& c) { return static_cast<int64_t>((*c.victims)[0]->priority); });
-  if (cur.size() > 1)
-    keep_min([](const CandidateRef& c) {
-      int64_t sum = 0;
-      for (const auto& v : *c.victims) sum += static_cast<int64_t>(v->priority) + INT32_MAX + 1;
-      return sum;
-    });
-  if (cur.size() > 1) keep_min([](const CandidateRef& c) { return static_cast<int64_t>(c.victims->size()); });
-  if (cur.size() > 1) {
-    // The node whose earliest-started victim started latest.
-    size_t best = cur.front();
-    int64_t latest = LLONG_MIN;
-    for (uint32_t i : cur) {
-      int64_t earliest = LLONG_MAX;
-      for (const auto& v : *cands[i].victims) earliest = std::min(earliest, pod_start_time(*v));
-      if (earliest > latest) {
-        latest = earliest;
-        best = i;
-      }
+  struct Key {
+    int64_t npv, top, sum, size, neg_earliest;
+    bool operator<(const Key& o) const {
+      return std::tie(npv, top, sum, size, neg_earliest) < std::tie(o.npv, o.top, o.sum, o.size, o.neg_earliest);
     }
-    return best;
+  };
+  size_t best = SIZE_MAX;
+  Key best_key{};
+  for (size_t i = 0; i < cands.size(); ++i) {
+    const auto& v = *cands[i].victims;
+    if (v.empty()) return i;  // no preemption needed at all
+    // victims are sorted most-important first, so v[0] is the highest priority.
+    Key k{cands[i].num_pdb_violations, v[0]->priority, 0, static_cast<int64_t>(v.size()), 0};
+    if (best != SIZE_MAX && (k.npv > best_key.npv || (k.npv == best_key.npv && k.top > best_key.top))) continue;
+    int64_t earliest = LLONG_MAX;
+    for (const auto& p : v) {
+      k.sum += static_cast<int64_t>(p->priority) + INT32_MAX + 1;
+      earliest = std::min(earliest, pod_start_time(*p));
+    }
+    k.neg_earliest = earliest == LLONG_MIN ? LLONG_MAX : -earliest;
+    if (best == SIZE_MAX || k < best_key) {
+      best = i;
+      best_key = k;
+    }
   }
-  return cur.front();
+  return best;
 }
 
 Status Evaluator::prepare_candidate(const Candidate& c, const Pod& pod) {

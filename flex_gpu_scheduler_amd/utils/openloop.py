@@ -85,25 +85,29 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
             "mean_arrival_lag_us": round(late_us / max(1, n), 1)}
 
 
-def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 0.3, seed: int = 0,
-                       start_pods_per_s: float = 2000.0) -> float:
-    """Sustained open-loop throughput (pods/s): the highest rate the shard
-    keeps up with when gangs arrive one at a time and are deleted as soon as
-    they are bound (no GPU pressure, so the scheduler, the store and the
-    per-gang API writes are the limit, not the cluster filling up). Probes
-    at rates x1.5 apart from `start_pods_per_s` up to `max_pods_per_s` (the
-    burst capacity) and stops at the first rate it cannot keep up with (the
-    last gang done more than 1.5x the arrival window after the first
-    arrival): past that point a backlog builds and the throughput of an
-    overloaded run would understate the capacity."""
+def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 0.5, seed: int = 0,
+                       start_pods_per_s: float = 2000.0, occupancy: float = 0.5,
+                       p99_budget_ms: float = 50.0) -> float:
+    """Sustained open-loop capacity (pods/s): the highest arrival rate, in
+    steps x1.4 apart from `start_pods_per_s` up to `max_pods_per_s` (the
+    burst capacity), that the shard serves under the same conditions as the
+    measured loads (gangs one at a time, held at `occupancy` of the SPX GPUs)
+    with every gang bound, the last one done within 1.2x the arrival window
+    plus the hold, and every gang type's p99 PG-create -> last-Bind under
+    `p99_budget_ms`. Past that rate a backlog builds (gang members fail on a
+    cluster whose deletions the scheduler has not seen yet, and Coscheduling
+    denies the group), so the throughput of an overloaded run would say
+    nothing about admission latency."""
     best, rate = 0.0, start_pods_per_s
     while rate <= max_pods_per_s:
-        r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=0.0)
-        pods = sum(v["n"] * (4 if k == "cpx4" else int(k)) for k, v in r["by_gang"].items())
-        if r["wall_s"] > 1.5 * duration_s + 0.05 or any(v["unbound"] for v in r["by_gang"].values()):
+        r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=occupancy)
+        ok = all(v["unbound"] == 0 and (v["create_to_bound_ms"]["p99"] or 0) <= p99_budget_ms
+                 for v in r["by_gang"].values())
+        ok = ok and r["wall_s"] <= 1.2 * duration_s + r["hold_ms"] / 1e3 + 0.05
+        if not ok:
             break
-        best = max(best, pods / max(r["wall_s"], 1e-6))
-        rate *= 1.5
+        best = rate
+        rate *= 1.4
     return best
 
 
