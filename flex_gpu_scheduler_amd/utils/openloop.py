@@ -85,11 +85,11 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
             "mean_arrival_lag_us": round(late_us / max(1, n), 1)}
 
 
-def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 0.5, seed: int = 0,
+def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, seed: int = 0,
                        start_pods_per_s: float = 2000.0, occupancy: float = 0.5,
-                       p99_budget_ms: float = 50.0) -> float:
+                       p99_budget_ms: float = 25.0) -> float:
     """Sustained open-loop capacity (pods/s): the highest arrival rate, in
-    steps x1.4 apart from `start_pods_per_s` up to `max_pods_per_s` (the
+    steps x1.3 apart from `start_pods_per_s` up to `max_pods_per_s` (the
     burst capacity), that the shard serves under the same conditions as the
     measured loads (gangs one at a time, held at `occupancy` of the SPX GPUs)
     with every gang bound, the last one done within 1.2x the arrival window
@@ -107,7 +107,7 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 0.5, se
         if not ok:
             break
         best = rate
-        rate *= 1.4
+        rate *= 1.3
     return best
 
 

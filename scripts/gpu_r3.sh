@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Round-3 box session. Usage: bash scripts/gpu_r3.sh TAG step [step ...]
-# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote sample_pre sample_sched
+# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote sample_pre sample_sched sample_bench
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure (no retries).
 set -u
@@ -37,6 +37,12 @@ for step in "$@"; do
       cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
       XSCHED_SAMPLE_HZ=2000 XSCHED_SAMPLE="$OUT/$wl.samples" timeout -k 5 300 taskset -c "$cpus" \
         abbin/xsched_stress_prof "/tmp/s_$wl" 1 > "$OUT/$wl.sample_run.txt" 2>&1 ;;
+    sample_bench)
+      # The headline bench waves (64 nodes, 40 waves) under the sampler.
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_bench --nodes 64 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      XSCHED_SAMPLE_HZ=2000 XSCHED_SAMPLE="$OUT/bench.samples" timeout -k 5 300 taskset -c "$cpus" \
+        abbin/xsched_stress_prof /tmp/s_bench 40 > "$OUT/bench.sample_run.txt" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
