@@ -315,6 +315,9 @@ struct Snapshot {
   // Nodes carrying at least one PreferNoSchedule taint, kept by the cache as
   // Nodes change. Zero lets TaintToleration skip its Score pass.
   int64_t nodes_with_prefer_no_schedule = 0;
+  // Lowest priority of any pod on a node (INT32_MAX when none): a preemptor
+  // at or below it has no possible lower-priority victim anywhere.
+  int32_t min_pod_priority = INT32_MAX;
   // No node carries a kubernetes.io/hostname label other than its own name,
   // so a hostname topology domain is exactly one node: InterPodAffinity then
   // evaluates hostname-keyed anti-affinity on the node's own pods instead of

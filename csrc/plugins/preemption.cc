@@ -50,6 +50,9 @@ class DefaultPreemption : public Plugin, public PreemptionPolicy {
   // a function of the node and the preemptor alone. Subclasses with their
   // own victim rules (PreemptionToleration: clock-dependent) opt out.
   bool victims_depend_only_on_node() const override { return !overrides_victims_; }
+  // Default and PreemptionToleration victims are lower-priority pods (the
+  // latter only narrows that set).
+  bool victims_have_lower_priority() const override { return true; }
 
  protected:
   bool overrides_victims_ = false;  // set by subclasses that replace select_victims_on_node

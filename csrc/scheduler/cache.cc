@@ -129,6 +129,7 @@ void SchedulerCache::record_delta(const PodPtr& p, const NodeInfo& ni, int d) {
 void SchedulerCache::add_pod_locked(const PodPtr& p) {
   auto& ni = info_for(p->node_name);
   writable(ni).add_pod(p);
+  ++prio_count_[p->priority];
   group_delta(*p, +1);
   record_delta(p, *ni, +1);
   mark_dirty(p->node_name);
@@ -140,6 +141,8 @@ void SchedulerCache::remove_pod_locked(const PodPtr& p) {
   if (writable(it->second).remove_pod(p->uid())) {
     group_delta(*p, -1);
     record_delta(p, *it->second, -1);
+    auto pit = prio_count_.find(p->priority);
+    if (pit != prio_count_.end() && --pit->second <= 0) prio_count_.erase(pit);
   }
   mark_dirty(p->node_name);
   if (it->second->node == nullptr && it->second->pods.empty()) nodes_.erase(it);
@@ -405,6 +408,7 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
   s.topology_epoch = topology_epoch_;
   s.generation = generation_;
   s.nodes_with_prefer_no_schedule = prefer_nodes_;
+  s.min_pod_priority = prio_count_.empty() ? INT32_MAX : prio_count_.begin()->first;
   s.hostname_domains_are_nodes = foreign_hostnames_ == 0;
   if (s.image_spread != image_spread_) s.image_spread = image_spread_;
   s.node_epoch = node_epoch_;

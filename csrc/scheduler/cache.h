@@ -15,6 +15,7 @@
 #pragma once
 
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -135,6 +136,7 @@ class SchedulerCache {
   int64_t generation_ = 0;
   uint64_t node_epoch_ = 1;
   int64_t prefer_nodes_ = 0;
+  std::map<int32_t, int64_t> prio_count_;  // pods on nodes per priority (Snapshot::min_pod_priority)
   int64_t foreign_hostnames_ = 0;  // nodes whose hostname label is not their name
   uint64_t topology_epoch_ = 1;     // Snapshot::topology_epoch
   std::vector<PodDelta> pending_deltas_;  // since the last snapshot refresh

@@ -429,6 +429,9 @@ std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod&
   if (potential.empty())
     return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +
                                                       " nodes are available: preemption is not helpful for scheduling.")};
+  if (policy_->victims_have_lower_priority() && h_.snapshot->min_pod_priority >= pod.priority)
+    return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +
+                                                      " nodes are available: no preemption victims found.")};
   std::vector<PDBPtr> pdbs = h_.informers ? h_.informers->pdbs() : std::vector<PDBPtr>{};
   auto [offset, num] = policy_->offset_and_num_candidates(static_cast<int>(potential.size()));
   DryRun dr;

@@ -41,6 +41,11 @@ class PreemptionPolicy {
   // (no clock, no quota or other cluster-wide state): the evaluator may then
   // reuse a node's dry-run result across preemptors (Evaluator::dry_run).
   virtual bool victims_depend_only_on_node() const { return false; }
+  // True when every victim must have a lower priority than the preemptor:
+  // with no such pod on any node the dry run is skipped (it could only find
+  // no candidate), which keeps a scheduler overloaded with equal-priority
+  // pods from dry-running every node for each failure.
+  virtual bool victims_have_lower_priority() const { return false; }
 };
 
 struct Candidate {

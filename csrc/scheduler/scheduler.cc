@@ -251,6 +251,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
   }
   queue_->set_cluster_event_map(std::move(emap));
   binder_ = std::make_unique<Executor>(opts_.bind_workers);
+  status_writer_ = std::make_unique<Executor>(1);
 
   std::set<std::string> kinds(kBaseKinds.begin(), kBaseKinds.end());
   for (const auto& k : plugin_kinds_) kinds.insert(k);
@@ -311,6 +312,7 @@ void Scheduler::stop() {
   timer_ids_.clear();
   for (auto& w : waiting_) w->reject_all("scheduler stopped");
   if (binder_) binder_->stop();
+  if (status_writer_) status_writer_->stop();
   if (was_running)
     for (auto& fw : frameworks_) fw->stop();
   timers_->stop();
@@ -1675,10 +1677,12 @@ void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const
   // the next cycle must already see this one, before the status patch comes
   // back through the informer (scheduler.go handleSchedulingFailure).
   if (!nominated.empty()) nominator_->add(latest && latest->uid() == pod->uid() ? latest : pod, nominated);
-  // The event goes out on the binder pool: the recorder is asynchronous in
-  // kube-scheduler too (an EventBroadcaster), only the status update below
-  // is written from the scheduling loop.
-  binder_->submit([client = fw.handle().client, pod, msg = st.message()] {
+  // The event goes out on the status writer (kube-scheduler's recorder is
+  // asynchronous too); the status update stays on the scheduling loop, as
+  // upstream's updatePod: written asynchronously it could land after a later
+  // cycle bound the pod and overwrite its PodScheduled=True condition.
+  ApiClient* client = fw.handle().client;
+  status_writer_->submit([client, pod, msg = st.message()] {
     try {
       client->record_event("Pod", pod->ns(), pod->name(), "Warning", "FailedScheduling", msg);
     } catch (const std::exception&) {
@@ -1707,7 +1711,7 @@ void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const
   if (!nominated.empty()) status.set("nominatedNodeName", Json(nominated));
   patch.set("status", std::move(status));
   try {
-    fw.handle().client->patch("pods", pod->ns(), pod->name(), patch);
+    client->patch("pods", pod->ns(), pod->name(), patch);
   } catch (const std::exception&) {
   }
 }

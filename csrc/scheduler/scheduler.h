@@ -285,6 +285,8 @@ class Scheduler {
   std::vector<std::unique_ptr<Framework>> frameworks_;
   std::unordered_map<std::string, Framework*> by_name_;
   std::unique_ptr<Executor> binder_;
+  // FailedScheduling events: one FIFO worker, off the scheduling loop.
+  std::unique_ptr<Executor> status_writer_;
   Snapshot snapshot_;
   Tracer tracer_;
   WatcherPtr watcher_;

@@ -17,6 +17,7 @@
 #include <string>
 #include <thread>
 
+#include "scheduler/openloop.h"
 #include "scheduler/scheduler.h"
 #include "tools/sampler.h"
 
@@ -55,6 +56,31 @@ int main(int argc, char** argv) {
   // (tools/sample_report.py symbolizes the dump).
   const char* sample_path = std::getenv("XSCHED_SAMPLE");
   if (sample_path) sampler::start(std::getenv("XSCHED_SAMPLE_HZ") ? std::atoi(std::getenv("XSCHED_SAMPLE_HZ")) : 4000);
+  // Open-loop mode: <dir>/openloop.json {"gangs":[{"podgroup":..,"pods":[..]}],
+  // "offsets_us":[..], "hold_us":N} written by tools/stress.py --openloop RATE
+  // (utils/openloop.py plan()); arrivals paced by run_open_loop.
+  if (std::filesystem::exists(dir + "/openloop.json")) {
+    Json ol = Json::parse(slurp(dir + "/openloop.json"));
+    std::vector<OpenLoopGang> gangs;
+    for (const auto& g : ol["gangs"].items()) {
+      OpenLoopGang og;
+      og.pod_group = g["podgroup"];
+      og.pods.assign(g["pods"].items().begin(), g["pods"].items().end());
+      gangs.push_back(std::move(og));
+    }
+    std::vector<int64_t> offsets;
+    for (const auto& o : ol["offsets_us"].items()) offsets.push_back(o.as_int());
+    size_t pods = 0;
+    for (const auto& g : gangs) pods += g.pods.size();
+    OpenLoopResult r = run_open_loop(*store, sched, std::move(gangs), offsets, ol["hold_us"].as_int(1000), 10'000'000);
+    if (sample_path) sampler::dump(sample_path);
+    size_t unbound = 0;
+    for (const auto& g : r.gangs) unbound += g.bound_us == 0;
+    sched.stop();
+    std::printf("openloop: %zu pods, %zu gangs unbound, wall %.4fs (%.0f pods/s), mean arrival lag %.1f us\n", pods,
+                unbound, r.wall_us / 1e6, pods / (r.wall_us / 1e6), r.gangs.empty() ? 0.0 : double(r.late_us) / r.gangs.size());
+    return unbound ? 1 : 0;
+  }
   uint64_t bound = 0;
   double total_s = 0;
   size_t total_pods = 0;

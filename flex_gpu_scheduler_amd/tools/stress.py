@@ -50,6 +50,18 @@ def write_workload(out: str | Path, name: str, nodes: int, pods: int, options: d
     return d
 
 
+def write_openloop(out: str | Path, nodes: int, rate: float, seconds: float, occupancy: float = 0.5,
+                   seed: int = 0, options: dict | None = None) -> Path:
+    """Inputs of the stress driver's open-loop mode: the bench cluster and one
+    planned run of utils/openloop.py (Poisson gang arrivals at `rate` pods/s)."""
+    from ..utils.openloop import plan
+
+    d = write_inputs(out, nodes, seed=seed, options=options)
+    gangs, _, offsets, hold_us = plan(ClusterSpec(nodes=nodes), rate, seconds, seed, occupancy=occupancy)
+    (d / "openloop.json").write_text(json.dumps({"gangs": gangs, "offsets_us": offsets, "hold_us": hold_us}))
+    return d
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
@@ -57,7 +69,16 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=1000, help="pods per wave (--workload only)")
     ap.add_argument("--workload", default="", help="a tools/sched_perf.py workload instead of the bench waves")
     ap.add_argument("--parallelism", type=int, default=16)
+    ap.add_argument("--openloop", type=float, default=0.0,
+                    help="open-loop mode: Poisson gang arrivals at this many pods/s (utils/openloop.py)")
+    ap.add_argument("--seconds", type=float, default=1.0, help="open-loop arrival window")
+    ap.add_argument("--occupancy", type=float, default=0.5, help="open-loop hold, as SPX GPU occupancy")
     a = ap.parse_args()
+    if a.openloop > 0:
+        write_openloop(a.out, a.nodes, a.openloop, a.seconds, a.occupancy, options={"parallelism": a.parallelism})
+        return
+    if (Path(a.out) / "openloop.json").exists():
+        (Path(a.out) / "openloop.json").unlink()
     if a.workload:
         write_workload(a.out, a.workload, a.nodes, a.pods, options={"parallelism": a.parallelism})
     else:
