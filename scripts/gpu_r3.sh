@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Round-3 box session. Usage: bash scripts/gpu_r3.sh TAG step [step ...]
-# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote sample_pre sample_sched sample_bench
+# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote sample_pre sample_sched sample_bench rocprof
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure (no retries).
 set -u
@@ -43,6 +43,11 @@ for step in "$@"; do
       cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
       XSCHED_SAMPLE_HZ=2000 XSCHED_SAMPLE="$OUT/bench.samples" timeout -k 5 300 taskset -c "$cpus" \
         abbin/xsched_stress_prof /tmp/s_bench 40 > "$OUT/bench.sample_run.txt" 2>&1 ;;
+    rocprof)
+      # Kernel trace + per-kernel stats of one short bench run (the probe,
+      # health, MFMA and placement kernels on the GPU path).
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_bench" -o bench -- \
+        python3 bench.py --steps 5 --warmup 1 --no-open-loop --no-scenarios > "$OUT/rocprof_bench.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
