@@ -124,6 +124,33 @@ def check_native() -> list[str]:
     return errs
 
 
+_LOG_CALL = re.compile(r"\bXS_(LOGV|INFO|WARN|ERROR)\(")
+
+
+def check_logging() -> list[str]:
+    """Structured logging (the reference's hack/verify-structured-logging.sh):
+    native log calls take a constant message and put every variable in
+    key/values (`XS_LOGV(6, "fit indexes").kv("pod", ...)`), never a message
+    built at run time."""
+    errs = []
+    for f in _files(NATIVE_DIRS, NATIVE_EXT):
+        if f.name not in ("log.h", "log.cc"):
+            errs += log_call_errors(f, f.read_text())
+    return errs
+
+
+def log_call_errors(f, text: str) -> list[str]:
+    errs = []
+    for m in _LOG_CALL.finditer(text):
+        rest = text[m.end():]
+        if m.group(1) == "LOGV":
+            rest = rest.split(",", 1)[1] if "," in rest else ""
+        if not re.match(r'\s*"(?:[^"\\]|\\.)*"\s*\)', rest):
+            line = text.count("\n", 0, m.start()) + 1
+            errs.append(f"{f}:{line}: log message is not a constant string (use .kv() for values)")
+    return errs
+
+
 def check_crds() -> list[str]:
     from ..deploy.crds import write_all
 
@@ -226,8 +253,8 @@ def check_docker() -> list[str]:
     return errs
 
 
-CHECKS = {"python": check_python, "native": check_native, "crds": check_crds, "charts": check_charts,
-          "configs": check_configs, "docker": check_docker}
+CHECKS = {"python": check_python, "native": check_native, "logging": check_logging, "crds": check_crds,
+          "charts": check_charts, "configs": check_configs, "docker": check_docker}
 
 
 def main(argv: list[str] | None = None) -> int:

@@ -34,7 +34,7 @@ def test_make_verify_is_clean():
     r = subprocess.run([sys.executable, "-m", "flex_gpu_scheduler_amd.tools.verify"], cwd=ROOT,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
-    assert r.stdout.count(": ok") == 6
+    assert r.stdout.count(": ok") == 7
 
 
 def test_verify_catches_problems(tmp_path, monkeypatch):
@@ -47,3 +47,13 @@ def test_verify_catches_problems(tmp_path, monkeypatch):
     text = bad.read_text()
     errs = verify._text_checks(bad, text) + verify.unused_imports(bad, ast.parse(text), text)
     assert any("trailing whitespace" in e for e in errs) and any("unused import os" in e for e in errs)
+
+
+def test_logging_lint_wants_constant_messages():
+    from flex_gpu_scheduler_amd.tools.verify import log_call_errors
+
+    good = 'XS_LOGV(6, "fit indexes").kv("pod", p.key());\nXS_WARN("dropped").kv("err", e.what());'
+    bad = 'XS_WARN("dropped " + name);\nXS_LOGV(6, msg).kv("x", 1);'
+    assert log_call_errors("a.cc", good) == []
+    errs = log_call_errors("b.cc", bad)
+    assert len(errs) == 2 and errs[0].startswith("b.cc:1:") and errs[1].startswith("b.cc:2:")
