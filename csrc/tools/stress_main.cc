@@ -8,6 +8,7 @@
 // flex_gpu_scheduler_amd/tools/stress.py, and optionally init.json (pods
 // created and bound before every wave, untimed: e.g. PreemptionBasic's
 // low-priority victims).
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -17,6 +18,8 @@
 #include <string>
 #include <thread>
 
+#include "apiserver/apiserver.h"
+#include "rest/kube.h"
 #include "scheduler/openloop.h"
 #include "scheduler/scheduler.h"
 #include "tools/sampler.h"
@@ -34,11 +37,97 @@ static std::string slurp(const std::string& p) {
   return ss.str();
 }
 
+// `xsched_stress apiserver [clients] [objects]`: the native HTTP API server
+// under concurrent REST clients (create / get / patch / list with selectors /
+// bind / delete), two raw watch streams and a LIST/WATCH mirror, then a stop
+// with streams still open: the sanitizer builds run this for the server's
+// connection threads, watcher registry and shutdown.
+static int apiserver_stress(int clients, int objects) {
+  auto store = std::make_shared<ObjectStore>();
+  store->create("nodes", Json::parse(R"({"metadata":{"name":"n0"},"status":{"allocatable":{"cpu":"64","pods":"1000"}}})"));
+  apiserver::Options o;
+  apiserver::Server srv(store, o);
+  srv.start();
+  rest::Endpoint ep;
+  ep.port = srv.port();
+  auto local = std::make_shared<ObjectStore>();
+  rest::RemoteMirror mirror(ep, local, {"pods", "nodes"});
+  mirror.start();
+  if (!mirror.wait_synced(10'000)) {
+    std::fprintf(stderr, "mirror did not sync\n");
+    return 1;
+  }
+  std::atomic<int> failures{0};
+  std::atomic<uint64_t> requests{0};
+  std::atomic<bool> stop_watch{false};
+  std::vector<std::thread> watchers;
+  std::atomic<uint64_t> watch_lines{0};
+  for (int w = 0; w < 2; ++w) {
+    watchers.emplace_back([&] {
+      try {
+        rest::HttpConn c(ep, nullptr, true);
+        if (c.open_stream("/api/v1/pods?watch=1&allowWatchBookmarks=true") != 200) {
+          ++failures;
+          return;
+        }
+        std::string line;
+        while (!stop_watch.load() && c.next_line(line)) ++watch_lines;
+      } catch (const std::exception&) {
+      }
+    });
+  }
+  std::vector<std::thread> ts;
+  for (int t = 0; t < clients; ++t) {
+    ts.emplace_back([&, t] {
+      rest::ConnPool pool(ep);
+      auto call = [&](const char* m, const std::string& path, const std::string& body, int want,
+                      const char* ct = "application/json") {
+        auto r = pool.call(m, path, body, ct);
+        ++requests;
+        if (r.status != want) {
+          ++failures;
+          std::fprintf(stderr, "%s %s -> %d %s\n", m, path.c_str(), r.status, r.body.substr(0, 200).c_str());
+        }
+      };
+      for (int i = 0; i < objects; ++i) {
+        std::string name = "p" + std::to_string(t) + "-" + std::to_string(i);
+        std::string path = "/api/v1/namespaces/s/pods/" + name;
+        call("POST", "/api/v1/namespaces/s/pods",
+             R"({"metadata":{"name":")" + name + R"(","labels":{"t":")" + std::to_string(t) +
+                 R"("}},"spec":{"containers":[{"name":"c"}]}})",
+             201);
+        call("GET", path, "", 200);
+        call("PATCH", path, R"({"metadata":{"annotations":{"k":"v"}}})", 200, "application/merge-patch+json");
+        call("PATCH", path, R"([{"op":"add","path":"/metadata/labels/j","value":"x"}])", 200,
+             "application/json-patch+json");
+        call("GET", "/api/v1/namespaces/s/pods?labelSelector=t%3D" + std::to_string(t) + "%2Cj", "", 200);
+        call("POST", path + "/binding", R"({"target":{"name":"n0"}})", 201);
+        call("DELETE", path, "", 200);
+        call("GET", path, "", 404);
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  for (int i = 0; i < 500 && local->count("pods") > 0; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  size_t left = local->count("pods");
+  // Stop with both watch streams still open: the server must end them.
+  srv.stop();
+  stop_watch = true;
+  for (auto& w : watchers) w.join();
+  mirror.stop();
+  std::printf("apiserver stress: %llu requests, %d failures, %llu watch lines, %zu pods left in the mirror\n",
+              static_cast<unsigned long long>(requests.load()), failures.load(),
+              static_cast<unsigned long long>(watch_lines.load()), left);
+  return failures.load() == 0 && left == 0 ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
-    std::fprintf(stderr, "usage: %s <dir> [waves]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s <dir> [waves] | apiserver [clients] [objects]\n", argv[0]);
     return 2;
   }
+  if (std::string(argv[1]) == "apiserver")
+    return apiserver_stress(argc > 2 ? std::atoi(argv[2]) : 8, argc > 3 ? std::atoi(argv[3]) : 200);
   std::string dir = argv[1];
   int waves = argc > 2 ? std::atoi(argv[2]) : 4;
   auto store = std::make_shared<ObjectStore>();

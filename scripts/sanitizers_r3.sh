@@ -23,6 +23,7 @@ run() {  # name dir waves
   done
 }
 run bench64 /tmp/san_bench 3
+run apiserver apiserver 4   # native HTTP API server: 4 REST clients, 2 watch streams, mirror, stop
 for spec in "PreemptionBasic 200 400" "SchedulingBasic 500 1000" "TopologySpreading 300 600" \
             "SchedulingPodAntiAffinity 300 300" "Unschedulable 300 600" "MI355X-Gang8 200 800" "MI355X-FlexGPUMix 200 800"; do
   set -- $spec
