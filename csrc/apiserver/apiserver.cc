@@ -6,6 +6,8 @@
 #include <netinet/tcp.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -370,6 +372,7 @@ struct Server::Request {
 
 struct Server::Conn {
   int fd = -1;
+  SSL* ssl = nullptr;  // HTTPS: every read and write goes through it
   std::string buf;
   size_t pos = 0;
 
@@ -383,21 +386,27 @@ struct Server::Conn {
     }
     char tmp[65536];
     for (;;) {
-      ssize_t n = ::recv(fd, tmp, sizeof tmp, 0);
+      ssize_t n = ssl ? SSL_read(ssl, tmp, sizeof tmp) : ::recv(fd, tmp, sizeof tmp, 0);
       if (n > 0) {
         buf.append(tmp, static_cast<size_t>(n));
         return true;
       }
-      if (n < 0 && errno == EINTR) continue;
+      if (!ssl && n < 0 && errno == EINTR) continue;
       return false;
     }
   }
   bool send_all(std::string_view d) {
     while (!d.empty()) {
-      ssize_t n = ::send(fd, d.data(), d.size(), MSG_NOSIGNAL);
-      if (n < 0) {
-        if (errno == EINTR) continue;
-        return false;
+      ssize_t n;
+      if (ssl) {
+        n = SSL_write(ssl, d.data(), static_cast<int>(std::min<size_t>(d.size(), 1u << 30)));
+        if (n <= 0) return false;
+      } else {
+        n = ::send(fd, d.data(), d.size(), MSG_NOSIGNAL);
+        if (n < 0) {
+          if (errno == EINTR) continue;
+          return false;
+        }
       }
       d.remove_prefix(static_cast<size_t>(n));
     }
@@ -563,7 +572,37 @@ bool peer_closed(int fd) {
 
 }  // namespace
 
+namespace {
+std::string ssl_error() {
+  unsigned long e = ERR_get_error();
+  char buf[256];
+  ERR_error_string_n(e, buf, sizeof buf);
+  return buf;
+}
+}  // namespace
+
 Server::Server(std::shared_ptr<ObjectStore> store, Options o) : store_(std::move(store)), opts_(std::move(o)) {
+  if (!opts_.tls_cert_file.empty()) {
+    SSL_CTX* ctx = SSL_CTX_new(TLS_server_method());
+    if (!ctx) throw std::runtime_error("apiserver: SSL_CTX_new: " + ssl_error());
+    SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+    const std::string& key = opts_.tls_key_file.empty() ? opts_.tls_cert_file : opts_.tls_key_file;
+    if (SSL_CTX_use_certificate_chain_file(ctx, opts_.tls_cert_file.c_str()) != 1 ||
+        SSL_CTX_use_PrivateKey_file(ctx, key.c_str(), SSL_FILETYPE_PEM) != 1 || SSL_CTX_check_private_key(ctx) != 1) {
+      std::string err = ssl_error();
+      SSL_CTX_free(ctx);
+      throw std::runtime_error("apiserver: TLS certificate/key: " + err);
+    }
+    if (!opts_.client_ca_file.empty()) {
+      if (SSL_CTX_load_verify_locations(ctx, opts_.client_ca_file.c_str(), nullptr) != 1) {
+        std::string err = ssl_error();
+        SSL_CTX_free(ctx);
+        throw std::runtime_error("apiserver: client CA: " + err);
+      }
+      SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER | SSL_VERIFY_FAIL_IF_NO_PEER_CERT, nullptr);
+    }
+    tls_ctx_ = ctx;
+  }
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -591,10 +630,17 @@ Server::Server(std::shared_ptr<ObjectStore> store, Options o) : store_(std::move
     ::close(fd);
   }
   ::freeaddrinfo(res);
-  if (listen_fd_ < 0) throw std::runtime_error("apiserver: cannot listen on " + opts_.host + ":" + port + ": " + err);
+  if (listen_fd_ < 0) {
+    if (tls_ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(tls_ctx_));
+    tls_ctx_ = nullptr;
+    throw std::runtime_error("apiserver: cannot listen on " + opts_.host + ":" + port + ": " + err);
+  }
 }
 
-Server::~Server() { stop(); }
+Server::~Server() {
+  stop();
+  if (tls_ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(tls_ctx_));
+}
 
 void Server::start() {
   if (acceptor_.joinable() || stopping_) return;
@@ -648,6 +694,18 @@ void Server::serve(int fd) {
   Conn c;
   c.fd = fd;
   Request r;
+  if (tls_ctx_) {
+    c.ssl = SSL_new(static_cast<SSL_CTX*>(tls_ctx_));
+    if (!c.ssl || SSL_set_fd(c.ssl, fd) != 1 || SSL_accept(c.ssl) != 1) {
+      if (c.ssl) SSL_free(c.ssl);
+      ERR_clear_error();
+      ::close(fd);
+      std::lock_guard<std::mutex> g(mu_);
+      conns_.erase(fd);
+      if (--live_threads_ == 0) idle_cv_.notify_all();
+      return;
+    }
+  }
   for (;;) {
     int rc = read_request(c, r);
     if (rc < 0) break;
@@ -656,6 +714,11 @@ void Server::serve(int fd) {
       break;
     }
     if (!handle(c, r) || stopping_) break;
+  }
+  if (c.ssl) {
+    SSL_shutdown(c.ssl);
+    SSL_free(c.ssl);
+    ERR_clear_error();
   }
   ::close(fd);
   std::lock_guard<std::mutex> g(mu_);

@@ -22,8 +22,8 @@
 // connections plus one watch per kind; connections are few and long-lived),
 // TCP_NODELAY, responses written in one send. Watches stream chunked JSON
 // lines exactly like kube-apiserver (ERROR + 410 Status when the version is
-// compacted, BOOKMARKs on request). Bearer-token auth; TLS stays with the
-// Python server (control/apiserver.py picks it when certificates are given).
+// compacted, BOOKMARKs on request). Bearer-token auth; HTTPS and mutual TLS
+// through OpenSSL (the handshake runs on the connection's own thread).
 #pragma once
 
 #include <atomic>
@@ -48,6 +48,9 @@ struct Options {
   std::string token;          // bearer token ("" = no auth)
   int bookmark_interval_ms = 10'000;
   int max_connections = 4096;
+  // HTTPS (kube-apiserver --tls-cert-file / --tls-private-key-file) and,
+  // with a client CA, mutual TLS (--client-ca-file). PEM files.
+  std::string tls_cert_file, tls_key_file, client_ca_file;
 };
 
 // Label / field selector requirement (k8s.io/apimachinery labels + fields
@@ -90,6 +93,7 @@ class Server {
 
   std::shared_ptr<ObjectStore> store_;
   Options opts_;
+  void* tls_ctx_ = nullptr;  // SSL_CTX* when serving HTTPS
   int listen_fd_ = -1;
   int port_ = 0;
   std::thread acceptor_;

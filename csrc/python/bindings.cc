@@ -304,16 +304,21 @@ PYBIND11_MODULE(_xsched, m) {
   // ---- native API server (apiserver/apiserver.h) ----
   py::class_<apiserver::Server, std::shared_ptr<apiserver::Server>>(m, "NativeApiServer")
       .def(py::init([](std::shared_ptr<ObjectStore> store, const std::string& host, int port, const std::string& token,
-                       int bookmark_interval_ms) {
+                       int bookmark_interval_ms, const std::string& tls_cert, const std::string& tls_key,
+                       const std::string& client_ca) {
              apiserver::Options o;
              o.host = host;
              o.port = port;
              o.token = token;
              o.bookmark_interval_ms = bookmark_interval_ms;
+             o.tls_cert_file = tls_cert;
+             o.tls_key_file = tls_key;
+             o.client_ca_file = client_ca;
              return std::make_shared<apiserver::Server>(std::move(store), o);
            }),
            py::arg("store"), py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("token") = "",
-           py::arg("bookmark_interval_ms") = 10000)
+           py::arg("bookmark_interval_ms") = 10000, py::arg("tls_cert") = "", py::arg("tls_key") = "",
+           py::arg("client_ca") = "")
       .def("start", &apiserver::Server::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &apiserver::Server::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &apiserver::Server::port)

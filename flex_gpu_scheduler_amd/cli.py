@@ -440,7 +440,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--save", help="write a JSON snapshot on exit (and every --save-period s)")
     p.add_argument("--save-period", type=float, default=0.0)
     p.add_argument("--python-http", action="store_true",
-                   help="serve with the Python http.server front end instead of the native one (TLS always uses it)")
+                   help="serve with the Python http.server front end instead of the native one")
     p.set_defaults(fn=cmd_apiserver)
 
     p = sub.add_parser("scheduler", help="the scheduler service")

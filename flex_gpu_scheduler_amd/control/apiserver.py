@@ -125,9 +125,10 @@ def apply_json_patch(doc: Any, ops: list) -> Any:
 class ApiServer:
     """Owns a native Store and serves it over HTTP on background threads.
 
-    By default the HTTP layer is native (csrc/apiserver/apiserver.cc: same
-    REST surface, no interpreter on the request path); with TLS certificates
-    (or `native_http=False`) it is this module's http.server handler."""
+    By default the HTTP(S) layer is native (csrc/apiserver/apiserver.cc: same
+    REST surface, TLS and mutual TLS through OpenSSL, no interpreter on the
+    request path); `native_http=False` selects this module's http.server
+    handler."""
 
     def __init__(self, store=None, host: str = "127.0.0.1", port: int = 0, *, token: str | None = None,
                  bookmark_interval: float = 10.0, tls_cert: str | None = None, tls_key: str | None = None,
@@ -141,15 +142,14 @@ class ApiServer:
         self._py_requests = 0
         self.tls = bool(tls_cert)
         if native_http is None:
-            native_http = not self.tls
-        if native_http and self.tls:
-            raise ValueError("the native HTTP server does not terminate TLS; use native_http=False")
+            native_http = True
         self._native = None
         self.httpd = None
         self._thread: threading.Thread | None = None
         if native_http:
             self._native = native().NativeApiServer(self.store, host, port, token or "",
-                                                    int(bookmark_interval * 1000))
+                                                    int(bookmark_interval * 1000), tls_cert or "",
+                                                    tls_key or "", client_ca or "")
             self._host = host
         else:
             handler = type("Handler", (_Handler,), {"api": self})

@@ -298,3 +298,22 @@ def test_retried_binding_conflict_on_same_node_is_success():
             c.bind_json(_pod("c"), "n2")
     finally:
         srv.close()
+
+
+@pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
+@pytest.mark.parametrize("native_http", [True, False], ids=["native-http", "python-http"])
+def test_mtls_server_requires_a_client_certificate(store, pki, native_http):
+    """--client-ca-file: a client with the right CA but no certificate is
+    refused at the handshake; one with a CA-signed certificate gets in."""
+    srv = ApiServer(store, tls_cert=str(pki / "server.crt"), tls_key=str(pki / "server.key"),
+                    client_ca=str(pki / "ca.crt"), native_http=native_http).start()
+    try:
+        assert srv.native_http is native_http and srv.url.startswith("https://")
+        anon = RestClient(srv.url, tls=TLSConfig(ca_file=str(pki / "ca.crt")))
+        with pytest.raises(Exception):
+            anon.list("nodes")
+        ok = RestClient(srv.url, tls=TLSConfig(ca_file=str(pki / "ca.crt"), cert_file=str(pki / "client.crt"),
+                                                key_file=str(pki / "client.key")))
+        assert ok.list("nodes")[0] == []
+    finally:
+        srv.stop()
