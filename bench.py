@@ -198,7 +198,7 @@ def main() -> int:
             "burst_capacity_pods_per_s": round(burst, 1),
             "capacity_pods_per_s": round(cap, 1),
             **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed + 1)
-               for f in (0.5, 0.9)}} if cap > 0 else {}
+               for f in (0.5, 0.9) if cap > 0}}
     shard.close()
 
     if not args.no_placement and (ctx.distributed or ctx.cuda):

@@ -98,14 +98,23 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     cluster whose deletions the scheduler has not seen yet, and Coscheduling
     denies the group), so the throughput of an overloaded run would say
     nothing about admission latency."""
-    best, rate = 0.0, start_pods_per_s
-    while rate <= max_pods_per_s:
+    def served(rate: float) -> bool:
         r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=occupancy)
         ok = all(v["unbound"] == 0 and (v["create_to_bound_ms"]["p99"] or 0) <= p99_budget_ms
                  for v in r["by_gang"].values())
-        ok = ok and r["wall_s"] <= 1.2 * duration_s + r["hold_ms"] / 1e3 + 0.05
-        if not ok:
-            break
+        return ok and r["wall_s"] <= 1.2 * duration_s + r["hold_ms"] / 1e3 + 0.05
+
+    rate = min(start_pods_per_s, max(max_pods_per_s, 1.0))
+    # A small cluster or a loaded host may not serve even the start rate:
+    # halve down to it first (a few probes at most), then climb.
+    floor = rate / 64
+    while rate > floor and not served(rate):
+        rate /= 2
+    if rate <= floor:
+        return 0.0
+    best = rate
+    rate *= 1.3
+    while rate <= max_pods_per_s and served(rate):
         best = rate
         rate *= 1.3
     return best

@@ -26,7 +26,7 @@ def test_bench_multi_rank_gloo(n):
     env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(n),
-           "--steps", "2", "--warmup", "1", "--nodes", "8", "--no-gpu-probe", "--no-scenarios"]
+           "--steps", "2", "--warmup", "1", "--nodes", "8", "--no-gpu-probe", "--no-scenarios", "--no-open-loop"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
