@@ -13,6 +13,7 @@
 #include <set>
 
 #include "api/types.h"
+#include "common/alloc.h"
 #include "common/json.h"
 #include "common/quantity.h"
 #include "rest/kube.h"
@@ -194,6 +195,9 @@ void release_scheduler(Scheduler* s) {
 
 PYBIND11_MODULE(_xsched, m) {
   m.doc() = "MI355X-native scheduler core (C++): object store, scheduling framework, plugins";
+  tune_allocator();
+  m.def("allocator_settings", [] { return tune_allocator(); },
+        "The process allocator settings in effect (common/alloc.h).");
 
   py::register_exception<JsonError>(m, "JsonError");
   static py::exception<StoreError> store_exc(m, "StoreError");

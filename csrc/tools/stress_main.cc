@@ -19,6 +19,7 @@
 #include <thread>
 
 #include "apiserver/apiserver.h"
+#include "common/alloc.h"
 #include "rest/kube.h"
 #include "scheduler/openloop.h"
 #include "scheduler/scheduler.h"
@@ -126,6 +127,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s <dir> [waves] | apiserver [clients] [objects]\n", argv[0]);
     return 2;
   }
+  tune_allocator();  // XSCHED_MALLOC_TUNE=0 keeps glibc's defaults (A/B runs)
   if (std::string(argv[1]) == "apiserver")
     return apiserver_stress(argc > 2 ? std::atoi(argv[2]) : 8, argc > 3 ? std::atoi(argv[3]) : 200);
   std::string dir = argv[1];
@@ -212,19 +214,24 @@ int main(int argc, char** argv) {
     store->create_chunked("pods", [&](const std::function<void(Json&&)>& emit) {
       for (auto& p : pods) emit(std::move(p));
     });
+    auto t_created = std::chrono::steady_clock::now();
     if (!wait_bound(bound + expect, "wave", w)) {
       sched.stop();
       return 1;
     }
+    auto t_bound = std::chrono::steady_clock::now();
     bound += expect;
     std::string ns = wave["namespace"].str_or("bench");
     store->delete_all("pods", ns);
     store->delete_all("podgroups", ns);
     while (sched.cache().pod_count() > 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
-    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    auto t_end = std::chrono::steady_clock::now();
+    double s = std::chrono::duration<double>(t_end - t0).count();
+    auto ms = [](auto d) { return std::chrono::duration<double, std::milli>(d).count(); };
     total_s += s;
     total_pods += n;
-    std::printf("wave %d: %zu pods in %.4fs (%.0f pods/s)\n", w, n, s, n / s);
+    std::printf("wave %d: %zu pods in %.4fs (%.0f pods/s) create %.2fms to_bound %.2fms delete_drain %.2fms\n", w, n,
+                s, n / s, ms(t_created - t0), ms(t_bound - t_created), ms(t_end - t_bound));
   }
   if (sample_path) sampler::dump(sample_path);
   sched.stop();

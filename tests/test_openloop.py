@@ -27,7 +27,7 @@ def test_plan_interleaves_types_and_sizes_hold():
 def test_open_loop_admits_every_gang_with_ordered_timeline():
     sh = Shard(ClusterSpec(nodes=16), namespace="b")
     try:
-        gangs, kinds, offsets, hold_us = plan(sh.spec, 2000.0, 0.3, seed=1)
+        gangs, kinds, offsets, hold_us = plan(sh.spec, 1000.0, 0.3, seed=1)
         from flex_gpu_scheduler_amd._native import native
 
         res = native().run_open_loop(sh.store, sh.sched, json.dumps(gangs), offsets, hold_us, 5_000_000)
@@ -40,7 +40,7 @@ def test_open_loop_admits_every_gang_with_ordered_timeline():
         sh.sched.wait_idle(10_000)
         assert sh.sched.wait_cache_empty(10.0)
         assert sh.store.count("pods") == 0 and sh.store.count("podgroups") == 0
-        out = run_open_loop(sh, 1500.0, duration_s=0.2, seed=2)
+        out = run_open_loop(sh, 800.0, duration_s=0.2, seed=2)
         assert out["gangs"] > 0 and all(v["unbound"] == 0 for v in out["by_gang"].values())
         for v in out["by_gang"].values():
             assert v["create_to_bound_ms"]["p99"] >= v["create_to_bound_ms"]["p50"] > 0
