@@ -258,6 +258,17 @@ void SchedulerCache::remove_pod(const Pod& p) {
   pod_states_.erase(it);
 }
 
+void SchedulerCache::remove_pods(const std::vector<PodPtr>& ps) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& p : ps) {
+    auto it = pod_states_.find(p->uid());
+    if (it == pod_states_.end()) continue;
+    remove_pod_locked(it->second.pod);
+    assumed_.erase(p->uid());
+    pod_states_.erase(it);
+  }
+}
+
 bool SchedulerCache::is_assumed(const std::string& uid) const {
   std::lock_guard<std::mutex> g(mu_);
   return assumed_.count(uid) > 0;

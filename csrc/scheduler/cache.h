@@ -44,6 +44,7 @@ class SchedulerCache {
   void add_pod(const PodPtr& p);  // assigned pod observed by the informer
   void update_pod(const PodPtr& old_pod, const PodPtr& new_pod);
   void remove_pod(const Pod& p);
+  void remove_pods(const std::vector<PodPtr>& ps);  // one lock for a run of deletions
 
   // p->node_name must be set. Called by the scheduling thread between cycles
   // (Scheduler holds sched_mu_): the node's NodeInfo is updated in place even

@@ -35,6 +35,16 @@ void Informers::delete_pod(const Pod& p) {
   pods_.erase(it);
 }
 
+void Informers::delete_pods(const std::vector<PodPtr>& ps) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  for (const auto& p : ps) {
+    auto it = pods_.find(p->key());
+    if (it == pods_.end()) continue;
+    if (it->second->pg_key) group_remove(it->second);
+    pods_.erase(it);
+  }
+}
+
 void Informers::upsert_pod_group(const PodGroupPtr& pg) {
   std::unique_lock<std::shared_mutex> g(mu_);
   std::string key = pg->meta.key();

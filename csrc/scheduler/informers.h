@@ -28,6 +28,7 @@ class Informers {
   // ---- mutation (informer thread) ----
   void upsert_pod(const PodPtr& p);
   void delete_pod(const Pod& p);
+  void delete_pods(const std::vector<PodPtr>& ps);  // one lock for a run of deletions
   void upsert_pod_group(const PodGroupPtr& pg);
   void delete_pod_group(const std::string& key);
   void upsert_elastic_quota(const ElasticQuotaPtr& eq);

@@ -377,13 +377,23 @@ void Scheduler::informer_loop() {
         prev[hi - 1] = informers_->pod(parsed[hi - 1]->ns(), parsed[hi - 1]->name());
         informers_->upsert_pod(parsed[hi - 1]);
       }
-      for (size_t i = lo; i < hi; ++i) {
+      for (size_t i = lo; i < hi;) {
+        if (!parsed[i] && evs[i].type == EventType::Deleted && evs[i].kind == "pods") {
+          size_t j = i + 1;
+          while (j < hi && evs[j].type == EventType::Deleted && evs[j].kind == "pods") ++j;
+          if (j - i > 1) {
+            handle_pod_deletes(&evs[i], j - i);
+            i = j;
+            continue;
+          }
+        }
         if (parsed[i])
           handle_parsed_pod_event(evs[i], parsed[i], prev[i]);
         else
           handle_event(evs[i]);
         parsed[i].reset();
         prev[i].reset();
+        ++i;
       }
       lo = hi;
     }
@@ -473,30 +483,63 @@ void Scheduler::report_informer_error(const WatchEvent& ev, const char* what) {
   }
 }
 
+// The pod a Deleted event removes. The lister copy stands in for the final
+// state when it is the same pod on the same node (all deletion needs), saving
+// a parse per delete.
+PodPtr Scheduler::deleted_pod(const WatchEvent& ev) {
+  const Json& md = (*ev.obj)["metadata"];
+  PodPtr p = informers_->pod(md["namespace"].as_string(), md["name"].as_string());
+  if (!p || p->uid() != md["uid"].as_string() || p->node_name != (*ev.obj)["spec"]["nodeName"].as_string())
+    p = Pod::from_json(*ev.obj, *gpu_names_);
+  return p;
+}
+
+void Scheduler::forget_unassigned_pod(const Pod& p) {
+  queue_->remove(p);
+  for (auto& w : waiting_)
+    if (auto wp = w->get(p.uid())) wp->reject("", "pod " + p.key() + " was deleted");
+  // An assumed-but-unbound pod may still sit in the cache.
+  if (cache_->is_assumed(p.uid())) {
+    if (auto cached = cache_->get_pod(p.uid())) {
+      cache_->forget_pod(*cached);
+      queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+    }
+  }
+}
+
+void Scheduler::handle_pod_deletes(const WatchEvent* evs, size_t n) {
+  std::vector<PodPtr> gone, assigned;
+  gone.reserve(n);
+  assigned.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    try {
+      for (auto& fw : frameworks_) fw->dispatch_object_event("pods", static_cast<int>(evs[i].type), evs[i].obj, evs[i].old);
+      PodPtr p = deleted_pod(evs[i]);
+      if (!p->node_name.empty()) assigned.push_back(p);
+      gone.push_back(std::move(p));
+    } catch (const std::exception& e) {
+      report_informer_error(evs[i], e.what());
+    }
+  }
+  informers_->delete_pods(gone);
+  if (!assigned.empty()) {
+    cache_->remove_pods(assigned);
+    queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+  }
+  for (const auto& p : gone)
+    if (p->node_name.empty()) forget_unassigned_pod(*p);
+}
+
 void Scheduler::handle_pod_event(const WatchEvent& ev) {
   for (auto& fw : frameworks_) fw->dispatch_object_event("pods", static_cast<int>(ev.type), ev.obj, ev.old);
   if (ev.type == EventType::Deleted) {
-    // The lister copy stands in for the final state when it is the same pod
-    // on the same node (all deletion needs), saving a parse per delete.
-    const Json& md = (*ev.obj)["metadata"];
-    PodPtr p = informers_->pod(md["namespace"].as_string(), md["name"].as_string());
-    if (!p || p->uid() != md["uid"].as_string() || p->node_name != (*ev.obj)["spec"]["nodeName"].as_string())
-      p = Pod::from_json(*ev.obj, *gpu_names_);
+    PodPtr p = deleted_pod(ev);
     informers_->delete_pod(*p);
     if (!p->node_name.empty()) {
       cache_->remove_pod(*p);
       queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
     } else {
-      queue_->remove(*p);
-      for (auto& w : waiting_)
-        if (auto wp = w->get(p->uid())) wp->reject("", "pod " + p->key() + " was deleted");
-      // An assumed-but-unbound pod may still sit in the cache.
-      if (cache_->is_assumed(p->uid())) {
-        if (auto cached = cache_->get_pod(p->uid())) {
-          cache_->forget_pod(*cached);
-          queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
-        }
-      }
+      forget_unassigned_pod(*p);
     }
     return;
   }

@@ -217,6 +217,11 @@ class Scheduler {
   void informer_loop();
   void handle_event(const WatchEvent& ev);
   void handle_pod_event(const WatchEvent& ev);
+  // A run of pod Deleted events (a DeleteCollection, a wave torn down):
+  // lister and cache updated under one lock each, one cluster event.
+  void handle_pod_deletes(const WatchEvent* evs, size_t n);
+  PodPtr deleted_pod(const WatchEvent& ev);
+  void forget_unassigned_pod(const Pod& p);
   void report_informer_error(const WatchEvent& ev, const char* what);
   void handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, PodPtr old);
   PodPtr bound_copy_of_assumed(const WatchEvent& ev);

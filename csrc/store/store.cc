@@ -397,6 +397,13 @@ size_t ObjectStore::delete_all(const std::string& kind, const std::string& ns) {
     int64_t rv = rv_.fetch_add(1) + 1;
     emit_locked(EventType::Deleted, kind, old, old, rv);
     ++n;
+    // Handed to the watchers in chunks (as kube-apiserver's DeleteCollection
+    // deletes item by item): informers start on the first deletions while
+    // the rest are still being removed.
+    if (batch.size() >= kCreateChunk) {
+      flush_batch_locked(batch);
+      batch.clear();
+    }
   }
   return n;
 }
