@@ -564,6 +564,9 @@ PYBIND11_MODULE(_xsched, m) {
         res["gangs"] = out;
         res["wall_us"] = r.wall_us;
         res["late_us"] = r.late_us;
+        res["delete_late_us"] = r.delete_late_us;
+        res["max_in_flight_pods"] = r.max_in_flight_pods;
+        res["max_held_pods"] = r.max_held_pods;
         return res;
       },
       py::arg("store"), py::arg("sched"), py::arg("gangs_json"), py::arg("offsets_us"), py::arg("hold_us"),

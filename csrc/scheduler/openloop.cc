@@ -48,6 +48,7 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
   const int64_t t0 = clock->now_us();
   size_t next = 0, done = 0;
   int64_t last_arrival = t0;
+  int64_t in_flight = 0, held = 0;
   for (;;) {
     int64_t now = clock->now_us();
     bool busy = false;
@@ -59,6 +60,8 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
       store.create("podgroups", g.pod_group);
       store.create_many("pods", g.pods);  // copies: the objects are needed again for deletion names
       last_arrival = now;
+      in_flight += out.gangs[next].size;
+      out.max_in_flight_pods = std::max(out.max_in_flight_pods, in_flight);
       ++next;
       busy = true;
       now = clock->now_us();
@@ -73,11 +76,16 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
       g.admit_us = r.admit_us;
       g.bound_us = r.bound_us;
       deletions.push({r.bound_us + hold_us, it->second});
+      in_flight -= g.size;
+      held += g.size;
+      out.max_held_pods = std::max(out.max_held_pods, held);
       ++done;
       busy = true;
     }
     // Departures due now.
     while (!deletions.empty() && deletions.top().first <= now) {
+      out.delete_late_us += now - deletions.top().first;
+      held -= out.gangs[deletions.top().second].size;
       remove_gang(deletions.top().second);
       deletions.pop();
       busy = true;

@@ -42,6 +42,10 @@ struct OpenLoopResult {
   std::vector<Gang> gangs;  // in arrival order; bound_us == 0: not admitted in time
   int64_t wall_us = 0;      // first arrival -> last gang done
   int64_t late_us = 0;      // total lag of arrivals behind their schedule (driver overload)
+  int64_t delete_late_us = 0;  // total lag of deletions behind bound + hold
+  // Peaks over the run, in pods: created but not yet bound (the scheduler's
+  // backlog), and bound but not yet deleted (the held occupancy).
+  int64_t max_in_flight_pods = 0, max_held_pods = 0;
 };
 
 // Runs to completion on the calling thread. `offsets_us[i]` is gang i's

@@ -129,5 +129,8 @@ def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: 
     res = native().run_open_loop(shard.store, shard.sched, json.dumps(gangs), offsets, hold_us, 10_000_000)
     shard.sched.wait_idle(10_000)
     out = summarize(kinds, res["gangs"], res["wall_us"], res["late_us"])
+    n = max(1, len(res["gangs"]))
+    out.update({"mean_delete_lag_us": round(res.get("delete_late_us", 0) / n, 1),
+                "max_in_flight_pods": res.get("max_in_flight_pods"), "max_held_pods": res.get("max_held_pods")})
     out.update({"offered_pods_per_s": round(rate_pods_per_s, 1), "hold_ms": round(hold_us / 1e3, 3)})
     return out
