@@ -132,6 +132,7 @@ SchedulerOptions SchedulerOptions::from_json(const Json& j) {
   o.equivalence_cache = j["equivalenceCache"].as_bool(o.equivalence_cache);
   o.trace = j["trace"].as_bool(false);
   o.seed = static_cast<uint64_t>(j["seed"].as_int(0));
+  o.dump_on_fit_error = j["dumpOnFitError"].str_or("");
   return o;
 }
 
@@ -1355,6 +1356,23 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         std::lock_guard<std::mutex> g(stats_mu_);
         ++stats_.preemption_attempts;
       }
+    }
+    if (fit_error && !opts_.dump_on_fit_error.empty() && !fit_error_dumped_.exchange(true)) {
+      Json d = dump_cache();
+      d.set("pod", Json(pod->key()));
+      d.set("message", Json(st.message()));
+      d.set("at_us", Json(clock_->now_us()));
+      if (FILE* f = std::fopen(opts_.dump_on_fit_error.c_str(), "w")) {
+        const std::string text = d.dump();
+        std::fwrite(text.data(), 1, text.size(), f);
+        std::fclose(f);
+      }
+      if (tracer_.enabled())  // the trace ring up to this failure
+        if (FILE* f = std::fopen((opts_.dump_on_fit_error + ".trace.json").c_str(), "w")) {
+          const std::string text = tracer_.chrome_json();
+          std::fwrite(text.data(), 1, text.size(), f);
+          std::fclose(f);
+        }
     }
     const int result = fit_error ? 1 : 2;
     cm.attempts[result]->inc();

@@ -93,6 +93,9 @@ struct SchedulerOptions {
   bool equivalence_cache = true;     // reuse node-local Filter/Score results across a pod template
   bool trace = false;
   uint64_t seed = 0;
+  // Debugging: on the first fit error, write the cache and queue (the cache
+  // debugger's dump) and the failing pod's diagnosis to this file.
+  std::string dump_on_fit_error;
   static SchedulerOptions from_json(const Json& j);
 };
 
@@ -310,6 +313,7 @@ class Scheduler {
   mutable std::mutex stats_mu_;
   Stats stats_;
   std::atomic<uint64_t> bound_total_{0};  // stats_.bound, readable without stats_mu_
+  std::atomic<bool> fit_error_dumped_{false};  // dump_on_fit_error written
   std::unordered_map<std::string, GangRecord> gangs_;  // open groups
   std::vector<GangRecord> gang_done_;
   std::unordered_map<std::string, std::string> last_condition_;  // uid -> last failure message

@@ -126,3 +126,31 @@ def test_bind_failures_recover_and_leave_cache_consistent(store):
         assert report["clean"], report
     finally:
         s.stop()
+
+
+def test_dump_on_first_fit_error(store, tmp_path):
+    """dumpOnFitError: the first Unschedulable cycle writes the cache dump,
+    the failing pod and its diagnosis (and, with tracing on, the trace ring up
+    to that cycle) — the post-mortem of an open-loop overload."""
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    path = tmp_path / "fit.json"
+    s = new_scheduler(store, load_config(flagship_config()), dumpOnFitError=str(path), trace=True,
+                      podInitialBackoffSeconds=0.01, podMaxBackoffSeconds=0.05)
+    s.start()
+    try:
+        store.create("pods", make_pod("ok", "default", limits={GPU: "8"}))
+        store.create("pods", make_pod("big", "default", limits={GPU: "8"}))
+        end = time.time() + 10
+        while not path.exists() and time.time() < end:
+            time.sleep(0.02)
+        import json
+
+        d = json.loads(path.read_text())
+        assert d["pod"] == "default/big" and "insufficient resource amd.com/gpu" in d["message"]
+        (node,) = d["nodes"]
+        assert node["name"] == "mi-0" and node["gpu"]["free_whole"] == 0 and len(node["pods"]) == 1
+        trace = json.loads((tmp_path / "fit.json.trace.json").read_text())
+        events = trace["traceEvents"] if isinstance(trace, dict) else trace
+        assert any(e["name"] == "schedule" for e in events)
+    finally:
+        s.stop()
