@@ -567,6 +567,7 @@ PYBIND11_MODULE(_xsched, m) {
         res["delete_late_us"] = r.delete_late_us;
         res["max_in_flight_pods"] = r.max_in_flight_pods;
         res["max_held_pods"] = r.max_held_pods;
+        res["timeline"] = r.timeline;
         return res;
       },
       py::arg("store"), py::arg("sched"), py::arg("gangs_json"), py::arg("offsets_us"), py::arg("hold_us"),

@@ -18,12 +18,14 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
   out.gangs.resize(n);
   std::unordered_map<std::string, size_t> by_key;  // "ns/pg" -> gang
   std::vector<std::string> ns(n), pg(n);
+  std::vector<std::vector<std::string>> members(n);  // pod names, for the deletion
   for (size_t i = 0; i < n; ++i) {
     const Json& md = gangs[i].pod_group["metadata"];
     ns[i] = md["namespace"].str_or("default");
     pg[i] = md["name"].as_string();
     by_key[ns[i] + "/" + pg[i]] = i;
     out.gangs[i].size = static_cast<int>(gangs[i].pods.size());
+    for (const auto& p : gangs[i].pods) members[i].push_back(p["metadata"]["name"].as_string());
   }
   (void)sched.gang_records(true);  // start from a clean slate
   using Due = std::pair<int64_t, size_t>;
@@ -32,11 +34,10 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
   auto remove_gang = [&](size_t i) {
     if (deleted[i]) return;
     deleted[i] = 1;
-    for (const auto& p : gangs[i].pods) {
-      try {
-        store.remove("pods", ns[i], p["metadata"]["name"].as_string());
-      } catch (const std::exception&) {
-      }
+    // The gang's members in one call, as `kubectl delete pods -l <group>`.
+    try {
+      store.remove_many("pods", ns[i], members[i]);
+    } catch (const std::exception&) {
     }
     try {
       store.remove("podgroups", ns[i], pg[i]);
@@ -49,16 +50,21 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
   size_t next = 0, done = 0;
   int64_t last_arrival = t0;
   int64_t in_flight = 0, held = 0;
+  int64_t next_slice = t0 + 5000;
   for (;;) {
     int64_t now = clock->now_us();
+    while (now >= next_slice) {
+      out.timeline.emplace_back(static_cast<int32_t>(in_flight), static_cast<int32_t>(held));
+      next_slice += 5000;
+    }
     bool busy = false;
     // Arrivals due now.
     while (next < n && now >= t0 + offsets_us[next]) {
       out.late_us += now - (t0 + offsets_us[next]);
       OpenLoopGang& g = gangs[next];
       out.gangs[next].create_us = clock->now_us();
-      store.create("podgroups", g.pod_group);
-      store.create_many("pods", g.pods);  // copies: the objects are needed again for deletion names
+      store.create("podgroups", std::move(g.pod_group));
+      store.create_many("pods", std::move(g.pods));
       last_arrival = now;
       in_flight += out.gangs[next].size;
       out.max_in_flight_pods = std::max(out.max_in_flight_pods, in_flight);

@@ -46,6 +46,8 @@ struct OpenLoopResult {
   // Peaks over the run, in pods: created but not yet bound (the scheduler's
   // backlog), and bound but not yet deleted (the held occupancy).
   int64_t max_in_flight_pods = 0, max_held_pods = 0;
+  // Every 5 ms of the run: pods in flight and held at the end of the slice.
+  std::vector<std::pair<int32_t, int32_t>> timeline;
 };
 
 // Runs to completion on the calling thread. `offsets_us[i]` is gang i's

@@ -55,19 +55,21 @@ bool Executor::try_pop(std::function<void()>& fn) {
 }
 
 Executor::Executor(int threads) {
+  if (const char* e = std::getenv("XSCHED_BIND_SPIN_NS")) spin_ns_ = std::max<int64_t>(0, std::atoll(e));
   for (int i = 0; i < std::max(1, threads); ++i) {
     threads_.emplace_back([this] {
       name_this_thread("xs-bind");
       bool spin = false;  // just finished a task: poll before sleeping
       for (;;) {
         std::function<void()> fn;
-        if (spin && spinners_.fetch_add(1) < kMaxSpinners) {
-          const int64_t until = Parallelizer::now_ns() + kSpinNs;
-          while (queued_.load(std::memory_order_relaxed) == 0 && Parallelizer::now_ns() < until) __builtin_ia32_pause();
+        if (spin && spin_ns_ > 0) {
+          if (spinners_.fetch_add(1) < kMaxSpinners) {
+            const int64_t until = Parallelizer::now_ns() + spin_ns_;
+            while (queued_.load(std::memory_order_relaxed) == 0 && Parallelizer::now_ns() < until)
+              __builtin_ia32_pause();
+          }
           // Leave the spinner set before the locked check below: a submit
           // that still saw this spinner finds its task taken here.
-          spinners_.fetch_sub(1);
-        } else if (spin) {
           spinners_.fetch_sub(1);
         }
         {
@@ -426,7 +428,15 @@ void Scheduler::handle_event(const WatchEvent& ev) {
       bool del = ev.type == EventType::Deleted;
       if (ev.kind == "podgroups") {
         auto pg = PodGroup::from_json(o);
-        if (del) informers_->delete_pod_group(pg->meta.key()); else informers_->upsert_pod_group(pg);
+        if (del) {
+          informers_->delete_pod_group(pg->meta.key());
+          // A gang deleted before it was admitted leaves no open record: a
+          // later PodGroup of the same name starts its own timeline.
+          std::lock_guard<std::mutex> g(stats_mu_);
+          gangs_.erase(pg->meta.key());
+        } else {
+          informers_->upsert_pod_group(pg);
+        }
       } else if (ev.kind == "elasticquotas") {
         auto eq = ElasticQuota::from_json(o);
         if (del) informers_->delete_elastic_quota(eq->meta.key()); else informers_->upsert_elastic_quota(eq);

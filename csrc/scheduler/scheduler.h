@@ -66,8 +66,9 @@ class Executor {
   // sleeps, and submit() skips the futex wake while a spinning worker can
   // take the task: under load the scheduling thread hands bindings over
   // without a syscall.
-  static constexpr int64_t kSpinNs = 30'000;
+  static constexpr int64_t kSpinNs = 30'000;  // XSCHED_BIND_SPIN_NS overrides (A/B runs)
   static constexpr int kMaxSpinners = 2;
+  int64_t spin_ns_ = kSpinNs;
   bool try_pop(std::function<void()>& fn);  // under mu_
   mutable std::mutex mu_;
   std::condition_variable cv_;

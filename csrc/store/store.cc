@@ -372,6 +372,28 @@ JsonPtr ObjectStore::remove(const std::string& kind, const std::string& ns, cons
   return old;
 }
 
+size_t ObjectStore::remove_many(const std::string& kind, const std::string& ns,
+                                const std::vector<std::string>& names) {
+  check_faults("delete", kind);
+  std::lock_guard<std::mutex> g(mu_);
+  auto& km = kinds_[kind];
+  std::vector<WatchEvent> batch;
+  batch_ = &batch;
+  size_t n = 0;
+  for (const auto& name : names) {
+    auto it = km.find(key_of(namespaced(kind) ? ns : "", name));
+    if (it == km.end()) continue;
+    JsonPtr old = it->second.obj;
+    km.erase(it);
+    int64_t rv = rv_.fetch_add(1) + 1;
+    emit_locked(EventType::Deleted, kind, old, old, rv);
+    ++n;
+  }
+  batch_ = nullptr;
+  flush_batch_locked(batch);
+  return n;
+}
+
 size_t ObjectStore::delete_all(const std::string& kind, const std::string& ns) {
   std::lock_guard<std::mutex> g(mu_);
   auto kit = kinds_.find(kind);

@@ -126,6 +126,10 @@ class ObjectStore {
   size_t create_chunked(const std::string& kind,
                         const std::function<void(const std::function<void(Json&&)>&)>& produce);
   size_t delete_all(const std::string& kind, const std::string& ns = "");
+  // Deletes the named objects of one namespace under one lock with one watch
+  // hand-off (a DeleteCollection by label, e.g. every member of a gang);
+  // names not found are skipped. Returns the number deleted.
+  size_t remove_many(const std::string& kind, const std::string& ns, const std::vector<std::string>& names);
 
   static std::string key_of(const std::string& ns, const std::string& name) { return ns.empty() ? name : ns + "/" + name; }
   static bool namespaced(const std::string& kind);

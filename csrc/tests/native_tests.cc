@@ -341,6 +341,21 @@ TEST(store_watch_replay_and_expiry) {
   CHECK(dup);
 }
 
+TEST(store_remove_many_is_one_batch) {
+  // A gang's members deleted in one call: one watch hand-off with every
+  // Deleted event, names that do not exist skipped, other pods untouched.
+  ObjectStore st;
+  for (int i = 0; i < 5; ++i)
+    st.create("pods", Json::parse(R"({"metadata":{"namespace":"d","name":"p)" + std::to_string(i) + R"("}})"));
+  auto w = st.watch({"pods"}, "d", 0);
+  size_t n = st.remove_many("pods", "d", {"p0", "p2", "nope", "p4"});
+  CHECK_EQ(n, 3u);
+  auto evs = w->next(100, 100000);
+  CHECK_EQ(evs.size(), 3u);
+  for (const auto& ev : evs) CHECK(ev.type == EventType::Deleted);
+  CHECK_EQ(st.count("pods"), 2u);
+}
+
 TEST(store_create_chunked_keeps_gangs_whole) {
   // 200 pods in gangs of 3 (plus ungrouped pods every 10th), streamed from
   // JSON text: watchers see commits of >= kCreateChunk pods, each ending on a

@@ -43,9 +43,12 @@ def gang_objects(kind: str, name: str, ns: str, rng: random.Random) -> dict:
 
 
 def plan(spec: ClusterSpec, rate_pods_per_s: float, duration_s: float, seed: int = 0, ns: str = "openloop",
-         occupancy: float = 0.5) -> tuple[list[dict], list[str], list[int], int]:
+         occupancy: float = 0.5, tag: str = "") -> tuple[list[dict], list[str], list[int], int]:
     """Gangs, their types, Poisson arrival offsets (us) and the hold time (us)
-    that keeps ~`occupancy` of the SPX GPUs busy at this arrival rate."""
+    that keeps ~`occupancy` of the SPX GPUs busy at this arrival rate. `tag`
+    goes into every gang name, so consecutive runs on one shard do not reuse
+    PodGroup names (Coscheduling remembers a denied group by name for
+    deniedPGExpirationTimeSeconds)."""
     rng = random.Random(seed)
     mean_pods = sum(4 if t == "cpx4" else int(t) for t in GANG_TYPES) / len(GANG_TYPES)
     gang_rate = rate_pods_per_s / mean_pods
@@ -55,7 +58,7 @@ def plan(spec: ClusterSpec, rate_pods_per_s: float, duration_s: float, seed: int
     for _ in range(n):
         t += rng.expovariate(gang_rate)
         offsets.append(int(t * 1e6))
-    gangs = [gang_objects(k, f"ol{i}-{k}", ns, rng) for i, k in enumerate(kinds)]
+    gangs = [gang_objects(k, f"ol{tag}{i}-{k}", ns, rng) for i, k in enumerate(kinds)]
     # Whole-GPU GPU-seconds arriving per second on the SPX side.
     whole = [int(k) for k in GANG_TYPES if k != "cpx4"]
     spx_gpu_rate = gang_rate * (len(whole) / len(GANG_TYPES)) * (sum(whole) / len(whole))
@@ -120,17 +123,26 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     return best
 
 
+_runs = 0  # run_open_loop calls in this process: the gang-name tag
+
+
 def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: int = 0,
-                  occupancy: float = 0.5) -> dict:
-    """One load level on `shard` (utils/benchrun.py Shard, idle)."""
+                  occupancy: float = 0.5, timeline: bool = False) -> dict:
+    """One load level on `shard` (utils/benchrun.py Shard, idle). With
+    `timeline`, also [pods in flight, pods held] at the end of every 5 ms."""
     from .._native import native
 
-    gangs, kinds, offsets, hold_us = plan(shard.spec, rate_pods_per_s, duration_s, seed, occupancy=occupancy)
+    global _runs
+    _runs += 1
+    gangs, kinds, offsets, hold_us = plan(shard.spec, rate_pods_per_s, duration_s, seed, occupancy=occupancy,
+                                          tag=f"{_runs}r")
     res = native().run_open_loop(shard.store, shard.sched, json.dumps(gangs), offsets, hold_us, 10_000_000)
     shard.sched.wait_idle(10_000)
     out = summarize(kinds, res["gangs"], res["wall_us"], res["late_us"])
     n = max(1, len(res["gangs"]))
     out.update({"mean_delete_lag_us": round(res.get("delete_late_us", 0) / n, 1),
                 "max_in_flight_pods": res.get("max_in_flight_pods"), "max_held_pods": res.get("max_held_pods")})
+    if timeline:
+        out["timeline"] = [list(x) for x in res.get("timeline", [])]
     out.update({"offered_pods_per_s": round(rate_pods_per_s, 1), "hold_ms": round(hold_us / 1e3, 3)})
     return out

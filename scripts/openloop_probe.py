@@ -60,7 +60,7 @@ try:
     for rate in (float(x) for x in a.rates.split(",")):
         s0 = sh.sched.stats()
         ts0 = thread_sched()
-        r = run_open_loop(sh, rate, a.seconds, seed=0, occupancy=a.occupancy)
+        r = run_open_loop(sh, rate, a.seconds, seed=0, occupancy=a.occupancy, timeline=True)
         s1 = sh.sched.stats()
         threads = sched_delta(ts0, thread_sched())
         # Why attempts failed: FailedScheduling events of this rate, by message.
@@ -88,6 +88,7 @@ try:
             "attempts": s1["attempts"] - s0["attempts"],
             "first_failures": [m for _, m in fails[:3]],
             "threads": threads,
+            "timeline_5ms": r.get("timeline"),
             "cache_drained": drained, "cache_clean": chk.get("clean"),
             "accounting_mismatches": len(chk.get("accounting", [])),
             "failed_scheduling": dict(sorted(why.items(), key=lambda kv: -kv[1])[:8])}), flush=True)

@@ -57,3 +57,38 @@ def test_burst_summary_splits_cpx_gangs():
     typed = gang_latency_summary(recs, by_type=True)
     assert list(typed) == ["1", "4", "cpx4"]
     assert typed["4"]["p99_ms"] == 1.0 and typed["cpx4"]["p99_ms"] == 9.0
+
+
+def test_recreated_podgroup_starts_a_fresh_gang_record():
+    """A gang deleted before admission leaves no open record behind: a later
+    PodGroup of the same name is timed from its own first enqueue (the open
+    loop reuses names across runs; a stale record would both inflate the
+    latency and count the old binds toward the new gang)."""
+    import time
+
+    from flex_gpu_scheduler_amd.models import GPU, make_pod, make_pod_group
+
+    sh = Shard(ClusterSpec(nodes=2), namespace="b")
+    try:
+        st, s = sh.store, sh.sched
+        st.create("podgroups", make_pod_group("g", "b", 2))
+        st.create("pods", make_pod("g-0", "b", limits={GPU: "1"}, pod_group="g"))
+        end = time.time() + 5
+        while s.stats()["attempts"] == 0 and time.time() < end:
+            time.sleep(0.01)
+        st.delete("pods", "b", "g-0")
+        st.delete("podgroups", "b", "g")
+        time.sleep(0.5)
+        st.create("podgroups", make_pod_group("g", "b", 2))
+        st.create_many("pods", json.dumps([make_pod(f"g-{i}", "b", limits={GPU: "1"}, pod_group="g")
+                                           for i in range(2)]))
+        assert s.wait_bound(2, 10.0)
+        end = time.time() + 5
+        recs = []
+        while not recs and time.time() < end:
+            recs = [r for r in s.gang_records(True) if r["pod_group"] == "b/g"]
+            time.sleep(0.01)
+        (r,) = recs
+        assert r["size"] == 2 and (r["bound_us"] - r["first_enqueue_us"]) < 400_000
+    finally:
+        sh.close()
