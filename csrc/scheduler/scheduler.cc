@@ -751,8 +751,10 @@ bool Scheduler::wait_idle(int timeout_ms) {
     auto c = queue_->counts();
     size_t waiting = 0;
     for (auto& w : waiting_) waiting += w->size();
+    // Idle includes the FailedScheduling event writer: after an overload its
+    // backlog would otherwise keep writing into the next measurement.
     if (c.active == 0 && c.backoff == 0 && waiting == 0 && inflight_.load() == 0 && in_cycle_.load() == 0 &&
-        watcher_->pending() == 0)
+        watcher_->pending() == 0 && (!status_writer_ || status_writer_->pending() == 0))
       return true;
     if (rc.now_us() > real_deadline && clock_->now_us() > deadline) return false;
     std::this_thread::sleep_for(std::chrono::microseconds(200));
