@@ -427,15 +427,18 @@ void Scheduler::handle_event(const WatchEvent& ev) {
       const Json& o = *ev.obj;
       bool del = ev.type == EventType::Deleted;
       if (ev.kind == "podgroups") {
-        auto pg = PodGroup::from_json(o);
         if (del) {
-          informers_->delete_pod_group(pg->meta.key());
+          // A deletion needs the key only (no parse: a wave tears down
+          // hundreds of groups at once).
+          const Json& md = o["metadata"];
+          const std::string key = md["namespace"].as_string() + "/" + md["name"].as_string();
+          informers_->delete_pod_group(key);
           // A gang deleted before it was admitted leaves no open record: a
           // later PodGroup of the same name starts its own timeline.
           std::lock_guard<std::mutex> g(stats_mu_);
-          gangs_.erase(pg->meta.key());
+          gangs_.erase(key);
         } else {
-          informers_->upsert_pod_group(pg);
+          informers_->upsert_pod_group(PodGroup::from_json(o));
         }
       } else if (ev.kind == "elasticquotas") {
         auto eq = ElasticQuota::from_json(o);
