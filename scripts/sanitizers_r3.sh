@@ -24,6 +24,10 @@ run() {  # name dir waves
 }
 run bench64 /tmp/san_bench 3
 run apiserver apiserver 4   # native HTTP API server: 4 REST clients, 2 watch streams, mirror, stop
+# Open-loop arrivals: gangs created and deleted one by one while they are
+# scheduled (run_open_loop, batched gang deletion, gang-record cleanup).
+python -m flex_gpu_scheduler_amd.tools.stress /tmp/san_ol --nodes 16 --openloop 2000 --seconds 0.5 > /dev/null || exit 1
+run openloop /tmp/san_ol 1
 for spec in "PreemptionBasic 200 400" "SchedulingBasic 500 1000" "TopologySpreading 300 600" \
             "SchedulingPodAntiAffinity 300 300" "Unschedulable 300 600" "MI355X-Gang8 200 800" "MI355X-FlexGPUMix 200 800"; do
   set -- $spec
