@@ -356,9 +356,13 @@ class Coscheduling : public Plugin {
     auto& e = patched_[key];
     if (e.uid == uid && e.phase == phase && now - e.at_us < kPatchMemoUs) return false;
     e = {uid, phase, now};
-    if (patched_.size() > 8192) {
+    // Amortized expiry: sweep when the memo has doubled since the last sweep
+    // (a sweep on every call past a fixed size made each PostBind O(groups)
+    // once thousands of distinct groups had bound within the memo window).
+    if (patched_.size() > patched_sweep_at_) {
       for (auto it = patched_.begin(); it != patched_.end();)
         it = now - it->second.at_us >= kPatchMemoUs ? patched_.erase(it) : std::next(it);
+      patched_sweep_at_ = std::max<size_t>(8192, 2 * patched_.size());
     }
     return true;
   }
@@ -368,6 +372,7 @@ class Coscheduling : public Plugin {
   };
   std::mutex patched_mu_;
   std::unordered_map<uint64_t, Patched> patched_;
+  size_t patched_sweep_at_ = 8192;
 
   Handle& h_;
   TTLSet denied_, permitted_;
