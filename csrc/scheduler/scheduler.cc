@@ -24,6 +24,35 @@ void StoreClient::patch(const std::string& kind, const std::string& ns, const st
 void StoreClient::record_event(const std::string& kind, const std::string& ns, const std::string& name,
                                const std::string& type, const std::string& reason, const std::string& msg) {
   if (!events_enabled) return;
+  const int64_t now = wall_now_us();
+  std::string corr;
+  corr.reserve(kind.size() + ns.size() + name.size() + reason.size() + msg.size() + 4);
+  corr.append(kind).push_back('\0');
+  corr.append(ns).push_back('\0');
+  corr.append(name).push_back('\0');
+  corr.append(reason).push_back('\0');
+  corr.append(msg);
+  Recent seen;
+  {
+    std::lock_guard<std::mutex> g(events_mu_);
+    auto it = recent_.find(corr);
+    if (it != recent_.end() && now - it->second.last_us < kAggregateUs) {
+      it->second.count += 1;
+      it->second.last_us = now;
+      seen = it->second;
+    }
+  }
+  if (seen.count > 0) {
+    Json p = Json::object();
+    p.set("count", Json(seen.count));
+    p.set("lastTimestamp", Json(format_rfc3339(now)));
+    try {
+      store_->patch("events", seen.ns, seen.name, p);
+      return;
+    } catch (const StoreError&) {
+      // expired or deleted: record a fresh Event below
+    }
+  }
   Json ev = Json::object();
   Json md = Json::object();
   md.set("generateName", Json(name + "."));
@@ -38,9 +67,22 @@ void StoreClient::record_event(const std::string& kind, const std::string& ns, c
   ev.set("reason", Json(reason));
   ev.set("message", Json(msg));
   ev.set("reportingController", Json("xsched"));
+  ev.set("count", Json(int64_t{1}));
+  ev.set("firstTimestamp", Json(format_rfc3339(now)));
+  ev.set("lastTimestamp", Json(format_rfc3339(now)));
+  JsonPtr created;
   try {
-    store_->create("events", std::move(ev));
+    created = store_->create("events", std::move(ev));
   } catch (const StoreError&) {
+    return;
+  }
+  const Json& md2 = (*created)["metadata"];
+  std::lock_guard<std::mutex> g(events_mu_);
+  recent_[std::move(corr)] = Recent{md2["namespace"].as_string(), md2["name"].as_string(), 1, now};
+  if (recent_.size() > recent_sweep_at_) {  // amortized: sweep when doubled
+    for (auto it = recent_.begin(); it != recent_.end();)
+      it = now - it->second.last_us >= kAggregateUs ? recent_.erase(it) : std::next(it);
+    recent_sweep_at_ = std::max<size_t>(4096, 2 * recent_.size());
   }
 }
 

@@ -50,6 +50,18 @@ class StoreClient : public ApiClient {
 
  private:
   std::shared_ptr<ObjectStore> store_;
+  // client-go's EventCorrelator aggregation: the same (object, reason,
+  // message) within kAggregateUs bumps count/lastTimestamp of the existing
+  // Event instead of creating another (a pod failing for the same reason on
+  // every retry is one Event with a count, as upstream).
+  static constexpr int64_t kAggregateUs = 600LL * 1000000;
+  struct Recent {
+    std::string ns, name;  // the Event object
+    int64_t count = 0, last_us = 0;
+  };
+  std::mutex events_mu_;
+  std::unordered_map<std::string, Recent> recent_;
+  size_t recent_sweep_at_ = 4096;
 };
 
 // Bounded worker pool for binding cycles.

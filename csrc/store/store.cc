@@ -166,7 +166,27 @@ JsonPtr ObjectStore::create_locked(const std::string& kind, Json obj) {
   auto ptr = std::make_shared<const Json>(std::move(obj));
   km[key] = Entry{ptr};
   emit_locked(EventType::Added, kind, ptr, nullptr, rv);
+  if (kind == "events") expire_events_locked(key);
   return ptr;
+}
+
+void ObjectStore::set_event_ttl_us(int64_t ttl_us) {
+  std::lock_guard<std::mutex> g(mu_);
+  event_ttl_us_ = ttl_us;
+}
+
+void ObjectStore::expire_events_locked(const std::string& created_key) {
+  const int64_t now = wall_now_us();
+  event_expiry_.emplace_back(now, created_key);
+  auto& km = kinds_["events"];
+  while (!event_expiry_.empty() && now - event_expiry_.front().first >= event_ttl_us_) {
+    auto it = km.find(event_expiry_.front().second);
+    event_expiry_.pop_front();
+    if (it == km.end()) continue;  // deleted already
+    JsonPtr old = it->second.obj;
+    km.erase(it);
+    emit_locked(EventType::Deleted, "events", old, old, rv_.fetch_add(1) + 1);
+  }
 }
 
 JsonPtr ObjectStore::create(const std::string& kind, Json obj) {

@@ -116,6 +116,12 @@ class ObjectStore {
   void add_fault(const FaultRule& r);
   void clear_faults();
 
+  // Events expire `ttl_us` after creation (kube-apiserver --event-ttl,
+  // default 1 h), so a long-running scheduler's FailedScheduling events do not
+  // grow the store without bound. Expiry is lazy, on later event writes, and
+  // emits DELETED to watchers as etcd's lease expiry does.
+  void set_event_ttl_us(int64_t ttl_us);
+
   // Bulk helpers for benchmarks (one lock hold, one event per object).
   std::vector<JsonPtr> create_many(const std::string& kind, std::vector<Json> objs);
   // Streaming bulk create: `produce` calls emit(obj) per object. Objects are
@@ -141,6 +147,7 @@ class ObjectStore {
   using KindMap = std::unordered_map<std::string, Entry>;
 
   void check_faults(const std::string& verb, const std::string& kind);
+  void expire_events_locked(const std::string& created_key);
   void emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv);
   JsonPtr create_locked(const std::string& kind, Json obj);
   void flush_batch_locked(std::vector<WatchEvent>& batch);
@@ -161,6 +168,8 @@ class ObjectStore {
   std::vector<WatcherPtr> watchers_;
   std::deque<WatchEvent> history_;
   size_t history_cap_ = 50000;
+  int64_t event_ttl_us_ = 3600LL * 1000000;
+  std::deque<std::pair<int64_t, std::string>> event_expiry_;  // (created wall us, key), creation order
   int64_t compacted_rv_ = 0;
   uint64_t uid_counter_ = 0;
   uint64_t uid_salt_;

@@ -356,6 +356,25 @@ TEST(store_remove_many_is_one_batch) {
   CHECK_EQ(st.count("pods"), 2u);
 }
 
+TEST(store_events_expire_after_ttl) {
+  // Events live event_ttl_us (kube-apiserver --event-ttl); expiry is lazy, on
+  // a later event write, and watchers see DELETED. Other kinds never expire.
+  ObjectStore st;
+  st.set_event_ttl_us(20'000);
+  st.create("events", Json::parse(R"({"metadata":{"namespace":"d","name":"e0"}})"));
+  st.create("pods", Json::parse(R"({"metadata":{"namespace":"d","name":"p0"}})"));
+  auto w = st.watch({"events"}, "d", 0);
+  std::this_thread::sleep_for(std::chrono::milliseconds(40));
+  st.create("events", Json::parse(R"({"metadata":{"namespace":"d","name":"e1"}})"));
+  CHECK_EQ(st.count("events"), 1u);
+  CHECK(st.get("events", "d", "e0") == nullptr && st.get("events", "d", "e1") != nullptr);
+  CHECK_EQ(st.count("pods"), 1u);
+  auto evs = w->next(100, 100);
+  bool deleted = false;
+  for (const auto& ev : evs) deleted |= ev.type == EventType::Deleted;
+  CHECK(deleted);
+}
+
 TEST(store_create_chunked_keeps_gangs_whole) {
   // 200 pods in gangs of 3 (plus ungrouped pods every 10th), streamed from
   // JSON text: watchers see commits of >= kCreateChunk pods, each ending on a

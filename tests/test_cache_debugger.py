@@ -154,3 +154,29 @@ def test_dump_on_first_fit_error(store, tmp_path):
         assert any(e["name"] == "schedule" for e in events)
     finally:
         s.stop()
+
+
+def test_repeated_failures_aggregate_into_one_event(store):
+    """client-go's EventCorrelator: a pod failing for the same reason on every
+    retry is one FailedScheduling Event whose count grows, not one object per
+    attempt (the store would otherwise grow with every retry)."""
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = new_scheduler(store, load_config(flagship_config()), podInitialBackoffSeconds=0.01,
+                      podMaxBackoffSeconds=0.02)
+    s.start()
+    try:
+        store.create("pods", make_pod("big", "default", limits={GPU: "16"}))
+        end = time.time() + 10
+        evs = []
+        while time.time() < end:
+            evs = [e for e in store.list("events", "default")[0]
+                   if e.get("reason") == "FailedScheduling" and e["involvedObject"]["name"] == "big"]
+            if evs and evs[0].get("count", 1) >= 3:
+                break
+            # A node label change requeues the unschedulable pod (NodeUpdate).
+            store.patch("nodes", "", "mi-0", {"metadata": {"labels": {"tick": str(time.time_ns())}}})
+            time.sleep(0.05)
+        assert len(evs) == 1 and evs[0]["count"] >= 2 and s.stats()["unschedulable"] >= evs[0]["count"]
+        assert evs[0]["firstTimestamp"] <= evs[0]["lastTimestamp"]
+    finally:
+        s.stop()
