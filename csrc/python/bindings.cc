@@ -452,6 +452,7 @@ PYBIND11_MODULE(_xsched, m) {
           [](ObjectStore& s, const std::string& kind, const std::string& ns, const std::string& name, int64_t grace,
              const std::string& uid) { return ptr_to_py(s.remove(kind, ns, name, grace, uid)); },
           py::arg("kind"), py::arg("ns"), py::arg("name"), py::arg("grace_seconds") = 0, py::arg("uid") = "")
+      .def("set_event_ttl_us", &ObjectStore::set_event_ttl_us, py::arg("ttl_us"))
       .def("delete_all", &ObjectStore::delete_all, py::arg("kind"), py::arg("ns") = "",
            py::call_guard<py::gil_scoped_release>())
       .def(

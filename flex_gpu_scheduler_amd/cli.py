@@ -133,6 +133,7 @@ def cmd_apiserver(args) -> int:
     from .control.snapshot import restore, snapshot_to_file
 
     store = Store()
+    store.set_event_ttl_us(int(args.event_ttl * 1e6))
     if args.load and os.path.exists(args.load):
         n = restore(store, json.loads(Path(args.load).read_text()))
         log.info("restored %d objects from %s", n, args.load)
@@ -441,6 +442,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--save-period", type=float, default=0.0)
     p.add_argument("--python-http", action="store_true",
                    help="serve with the Python http.server front end instead of the native one")
+    p.add_argument("--event-ttl", type=float, default=3600.0,
+                   help="seconds an Event is kept (kube-apiserver --event-ttl)")
     p.set_defaults(fn=cmd_apiserver)
 
     p = sub.add_parser("scheduler", help="the scheduler service")
