@@ -152,7 +152,11 @@ def main() -> int:
                   options=json.loads(args.sched_options))
     # Pre-render every wave's JSON (data preparation, outside the timed region).
     waves = [shard.wave(i) for i in range(args.warmup + args.steps + 1)]  # +1: the untimed check wave
-    prepared = [(w.groups_json(), w.pods_json()) for w in waves]
+    # Each chunk's PodGroups are written just before its pods (as job
+    # submitters do), unless XSCHED_BENCH_INTERLEAVE=0 (all PodGroups first;
+    # A/B runs).
+    interleave = os.environ.get("XSCHED_BENCH_INTERLEAVE", "1") != "0"
+    prepared = [w.chunks_json() if interleave else (w.groups_json(), w.pods_json()) for w in waves]
 
     for i in range(args.warmup):
         shard.run(waves[i], prepared=prepared[i])

@@ -17,6 +17,7 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <unordered_map>
 
 #include "apiserver/apiserver.h"
 #include "common/alloc.h"
@@ -209,11 +210,36 @@ int main(int argc, char** argv) {
     // Workloads with pods that fit nowhere (Unschedulable) bind fewer.
     const size_t expect = static_cast<size_t>(wave["expect_bound"].as_int(static_cast<int64_t>(n)));
     auto t0 = std::chrono::steady_clock::now();
-    store->create_many("podgroups", std::move(pgs));
-    // PodGroup-aligned chunks, as the Python bulk-create path commits them.
-    store->create_chunked("pods", [&](const std::function<void(Json&&)>& emit) {
-      for (auto& p : pods) emit(std::move(p));
-    });
+    // As bench.py (Wave.chunks_json): chunks of >= 64 pods ending on a gang
+    // boundary, each chunk's PodGroups written just before its pods.
+    {
+      auto group_of = [](const Json& o) -> const std::string& {
+        return o["metadata"]["labels"]["pod-group.scheduling.sigs.k8s.io"].as_string();
+      };
+      std::unordered_map<std::string, size_t> pg_at;
+      for (size_t i = 0; i < pgs.size(); ++i) pg_at[pgs[i]["metadata"]["name"].as_string()] = i;
+      std::vector<char> pg_done(pgs.size(), 0);
+      std::vector<Json> chunk_pgs, chunk_pods;
+      for (size_t i = 0; i < n; ++i) {
+        const std::string g = group_of(pods[i]);
+        if (auto it = pg_at.find(g); !g.empty() && it != pg_at.end() && !pg_done[it->second]) {
+          pg_done[it->second] = 1;
+          chunk_pgs.push_back(std::move(pgs[it->second]));
+        }
+        chunk_pods.push_back(std::move(pods[i]));
+        const bool last = i + 1 == n;
+        if (last || (chunk_pods.size() >= ObjectStore::kCreateChunk && (g.empty() || group_of(pods[i + 1]) != g))) {
+          if (!chunk_pgs.empty()) store->create_many("podgroups", std::move(chunk_pgs));
+          store->create_many("pods", std::move(chunk_pods));
+          chunk_pgs.clear();
+          chunk_pods.clear();
+        }
+      }
+      std::vector<Json> rest;  // groups with no pod in this wave
+      for (size_t i = 0; i < pgs.size(); ++i)
+        if (!pg_done[i]) rest.push_back(std::move(pgs[i]));
+      if (!rest.empty()) store->create_many("podgroups", std::move(rest));
+    }
     auto t_created = std::chrono::steady_clock::now();
     if (!wait_bound(bound + expect, "wave", w)) {
       sched.stop();

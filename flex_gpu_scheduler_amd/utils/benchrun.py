@@ -48,18 +48,24 @@ class Shard:
     def wave(self, step: int) -> Wave:
         return make_wave(self.spec, step, namespace=self.ns, seed=self.seed)
 
-    def run(self, wave: Wave, timeout_s: float = 120.0, *, prepared: tuple[str, str] | None = None,
+    def run(self, wave: Wave, timeout_s: float = 120.0, *,
+            prepared: tuple[str, str] | list[tuple[str, str]] | None = None,
             check_cache: dict | None = None) -> StepResult:
         """One wave: create, wait until bound, delete, wait until the cache
-        drained. With `check_cache` (a dict, filled in), the cache debugger
+        drained. `prepared` is the wave's JSON, either (PodGroups, pods) or
+        Wave.chunks_json() (PodGroups written chunk by chunk just before their
+        pods). With `check_cache` (a dict, filled in), the cache debugger
         runs once the wave is bound and no binding is in flight, before the
         deletion (untimed callers only)."""
-        groups_js, pods_js = prepared if prepared else (wave.groups_json(), wave.pods_json())
+        chunks = prepared if isinstance(prepared, list) else [prepared or (wave.groups_json(), wave.pods_json())]
         n = len(wave.pods)
         target = self._bound + n
         t0 = time.perf_counter()
-        self.store.create_many("podgroups", groups_js)
-        self.store.create_many("pods", pods_js)
+        for groups_js, pods_js in chunks:
+            if groups_js != "[]":
+                self.store.create_many("podgroups", groups_js)
+            if pods_js != "[]":
+                self.store.create_many("pods", pods_js)
         t_created = time.perf_counter()
         deadline = t0 + timeout_s
         sched = self.sched

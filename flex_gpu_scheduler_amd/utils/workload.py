@@ -17,7 +17,7 @@ import random
 from dataclasses import dataclass, field
 
 from ..models.mi355x import GPU, GPU_MEMORY, GPU_XCD, default_gpus, mi355x_node, mi355x_nrt
-from ..models.objects import make_container, make_pod, make_pod_group
+from ..models.objects import POD_GROUP_LABEL, make_container, make_pod, make_pod_group
 
 GROUP_SIZES = (1, 2, 4, 8)
 
@@ -64,6 +64,34 @@ class Wave:
 
     def groups_json(self) -> str:
         return json.dumps(self.pod_groups)
+
+    def chunks_json(self, chunk: int = 64) -> list[tuple[str, str]]:
+        """The wave as the API server would receive it from many job
+        submitters: (PodGroups, pods) per chunk of >= `chunk` pods ending on a
+        gang boundary, each chunk's PodGroups written just before its pods.
+        The scheduler starts on the first gangs instead of after every
+        PodGroup of the wave."""
+        by_name = {pg["metadata"]["name"]: pg for pg in self.pod_groups}
+        out: list[tuple[str, str]] = []
+        groups: list[dict] = []
+        pods: list[dict] = []
+        seen: set[str] = set()
+        for i, p in enumerate(self.pods):
+            g = (p["metadata"].get("labels") or {}).get(POD_GROUP_LABEL, "")
+            if g and g not in seen:
+                seen.add(g)
+                if g in by_name:
+                    groups.append(by_name[g])
+            pods.append(p)
+            nxt = self.pods[i + 1] if i + 1 < len(self.pods) else None
+            ng = (nxt["metadata"].get("labels") or {}).get(POD_GROUP_LABEL, "") if nxt else None
+            if nxt is None or (len(pods) >= chunk and (not g or ng != g)):
+                out.append((json.dumps(groups), json.dumps(pods)))
+                groups, pods = [], []
+        leftover = [pg for name, pg in by_name.items() if name not in seen]
+        if leftover:  # groups without pods in this wave
+            out.insert(0, (json.dumps(leftover), "[]"))
+        return out
 
 
 def _rand_cpu_mem(rng: random.Random) -> dict:

@@ -92,3 +92,36 @@ def test_recreated_podgroup_starts_a_fresh_gang_record():
         assert r["size"] == 2 and (r["bound_us"] - r["first_enqueue_us"]) < 400_000
     finally:
         sh.close()
+
+
+def test_wave_chunks_write_each_podgroup_before_its_pods():
+    """Wave.chunks_json (bench.py's default creation order): every PodGroup
+    and pod exactly once, chunks of >= 64 pods ending on a gang boundary, and
+    each pod's PodGroup in its own chunk or an earlier one. The shard binds
+    the whole wave created that way."""
+    from flex_gpu_scheduler_amd.models.objects import POD_GROUP_LABEL
+    from flex_gpu_scheduler_amd.utils.workload import make_wave
+
+    spec = ClusterSpec(nodes=16)
+    w = make_wave(spec, 2)
+    chunks = [(json.loads(g), json.loads(p)) for g, p in w.chunks_json()]
+    assert sorted(pg["metadata"]["name"] for g, _ in chunks for pg in g) == \
+        sorted(pg["metadata"]["name"] for pg in w.pod_groups)
+    assert [p["metadata"]["name"] for _, ps in chunks for p in ps] == [p["metadata"]["name"] for p in w.pods]
+    created: set[str] = set()
+    for i, (groups, pods) in enumerate(chunks):
+        created |= {pg["metadata"]["name"] for pg in groups}
+        for p in pods:
+            g = p["metadata"].get("labels", {}).get(POD_GROUP_LABEL)
+            assert not g or g in created
+        if i + 1 < len(chunks):
+            assert len(pods) >= 64
+            last = pods[-1]["metadata"].get("labels", {}).get(POD_GROUP_LABEL)
+            first_next = chunks[i + 1][1][0]["metadata"].get("labels", {}).get(POD_GROUP_LABEL)
+            assert not last or last != first_next
+    sh = Shard(spec, namespace="bench")
+    try:
+        r = sh.run(w, prepared=w.chunks_json())
+        assert r.pods == len(w.pods)
+    finally:
+        sh.close()
