@@ -145,6 +145,12 @@ class PersistentVolumeController(_Controller):
                 return
         cls_name = claim_class(pvc)
         sc = self.sc_informer.get("", cls_name) if cls_name else None
+        if cls_name and sc is None:
+            # The class may be newer than this informer's view (upstream syncs
+            # its caches before the first claim; our informers start together):
+            # treating a WaitForFirstConsumer claim as Immediate would bind it
+            # behind the scheduler's back.
+            sc = self.client.get("storageclasses", "", cls_name)
         wffc = bool(sc and sc.get("volumeBindingMode") == "WaitForFirstConsumer")
         selected = ann.get(ANN_SELECTED_NODE)
         if wffc and not selected:
@@ -163,19 +169,29 @@ class PersistentVolumeController(_Controller):
         want = _quantity_bytes(((pvc.get("spec") or {}).get("resources") or {}).get("requests", {}).get("storage"))
         modes = set((pvc.get("spec") or {}).get("accessModes") or [])
         vmode = (pvc.get("spec") or {}).get("volumeMode") or "Filesystem"
-        best, best_size = None, None
+        def free(pv: dict) -> bool:
+            return not (pv.get("spec") or {}).get("claimRef") and \
+                (pv.get("status") or {}).get("phase") in (None, "", "Available")
+
+        fits = []
         for pv in self.pv_informer.list(None):
             spec = pv.get("spec") or {}
-            if spec.get("claimRef") or (pv.get("status") or {}).get("phase") not in (None, "", "Available"):
+            if not free(pv):
                 continue
             if volume_class(pv) != cls_name or (spec.get("volumeMode") or "Filesystem") != vmode:
                 continue
             size = _quantity_bytes((spec.get("capacity") or {}).get("storage"))
             if size < want or not modes <= set(spec.get("accessModes") or []):
                 continue
-            if best is None or size < best_size:
-                best, best_size = pv, size
-        return best
+            fits.append((size, pv["metadata"]["name"]))
+        # The informer can lag this controller's own claimRef patches (the
+        # upstream controller keeps an assumed-volume store for the same
+        # reason): confirm the volume is still free on the API object.
+        for _, name in sorted(fits):
+            pv = self.client.get("persistentvolumes", "", name)
+            if pv is not None and free(pv):
+                return pv
+        return None
 
     def _provisions(self, provisioner: str) -> bool:
         if not provisioner or provisioner == NO_PROVISIONER:

@@ -179,6 +179,27 @@ def test_gang_with_per_rank_claims_gets_distinct_volumes(store, pvctl):
         s.stop()
 
 
+def test_pv_controller_with_stale_informers(store):
+    """The controller's informers can lag the API: a StorageClass it has not
+    seen yet must not turn a WaitForFirstConsumer claim into an Immediate one,
+    and a PV it still sees as free must not be bound to a second claim."""
+    store.create("storageclasses", sc("local"))
+    store.create("storageclasses", sc("imm", mode="Immediate"))
+    store.create("persistentvolumes", pv("only", cls="imm"))
+    for name, cls in (("wffc", "local"), ("a", "imm"), ("b", "imm")):
+        store.create("persistentvolumeclaims", pvc(name, cls=cls))
+    c = PersistentVolumeController(LocalClient(store))  # informers never started: always stale
+    stale_pv = store.get("persistentvolumes", "", "only")
+    c.pv_informer.list = lambda _sel=None: [stale_pv]
+    for name in ("wffc", "a", "b"):
+        c.sync(f"claim/default/{name}")
+    get = lambda n: store.get("persistentvolumeclaims", "default", n)  # noqa: E731
+    assert not get("wffc")["spec"].get("volumeName")  # left for the scheduler
+    assert get("a")["spec"].get("volumeName") == "only"
+    assert not get("b")["spec"].get("volumeName")  # "only" is taken on the API object
+    assert store.get("persistentvolumes", "", "only")["spec"]["claimRef"]["name"] == "a"
+
+
 def test_claim_errors_are_unresolvable(store):
     store.create("nodes", node("n0"))
     store.create("storageclasses", sc("imm", mode="Immediate"))
