@@ -100,12 +100,22 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     `p99_budget_ms`. Past that rate a backlog builds (gang members fail on a
     cluster whose deletions the scheduler has not seen yet, and Coscheduling
     denies the group), so the throughput of an overloaded run would say
-    nothing about admission latency."""
-    def served(rate: float) -> bool:
-        r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=occupancy)
+    nothing about admission latency.
+
+    A rate whose first trial fails gets two more trials (other arrival
+    seeds) and counts as served when both pass: near capacity a single
+    8-rank gang can find the SPX pool momentarily full and be denied for the
+    reference's denied-PodGroup TTL, and one such draw stopped the climb
+    anywhere between 21k and 47k pods/s on the same tree
+    (profiles/r3al_bench64_{1,2}.json)."""
+    def trial(rate: float, k: int) -> bool:
+        r = run_open_loop(shard, rate, duration_s, seed=seed + 7717 * k, occupancy=occupancy)
         ok = all(v["unbound"] == 0 and (v["create_to_bound_ms"]["p99"] or 0) <= p99_budget_ms
                  for v in r["by_gang"].values())
         return ok and r["wall_s"] <= 1.2 * duration_s + r["hold_ms"] / 1e3 + 0.05
+
+    def served(rate: float) -> bool:
+        return trial(rate, 0) or (trial(rate, 1) and trial(rate, 2))
 
     rate = min(start_pods_per_s, max(max_pods_per_s, 1.0))
     # A small cluster or a loaded host may not serve even the start rate:
