@@ -30,7 +30,9 @@ def test_open_loop_admits_every_gang_with_ordered_timeline():
         gangs, kinds, offsets, hold_us = plan(sh.spec, 1000.0, 0.3, seed=1)
         from flex_gpu_scheduler_amd._native import native
 
-        res = native().run_open_loop(sh.store, sh.sched, json.dumps(gangs), offsets, hold_us, 5_000_000)
+        # 20 s: on an overloaded host a gang can be denied for the 3 s TTL and back
+        # off before it binds; a healthy run returns as soon as every gang is bound.
+        res = native().run_open_loop(sh.store, sh.sched, json.dumps(gangs), offsets, hold_us, 20_000_000)
         assert len(res["gangs"]) == len(gangs)
         for g, k in zip(res["gangs"], kinds):
             assert g["bound_us"] > 0, g
