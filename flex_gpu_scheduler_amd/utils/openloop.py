@@ -97,7 +97,8 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     measured loads (gangs one at a time, held at `occupancy` of the SPX GPUs)
     with every gang bound, the last one done within 1.2x the arrival window
     plus the hold, and every gang type's p99 PG-create -> last-Bind under
-    `p99_budget_ms`. Past that rate a backlog builds (gang members fail on a
+    `p99_budget_ms`, then refined by two bisection steps inside the last
+    interval. Past that rate a backlog builds (gang members fail on a
     cluster whose deletions the scheduler has not seen yet, and Coscheduling
     denies the group), so the throughput of an overloaded run would say
     nothing about admission latency.
@@ -130,6 +131,16 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     while rate <= max_pods_per_s and served(rate):
         best = rate
         rate *= 1.3
+    # Two bisection steps inside the last x1.3 interval when a rate failed
+    # (rather than ran past the burst capacity): the capacity to ~7%.
+    hi = rate
+    if hi <= max_pods_per_s:
+        for _ in range(2):
+            mid = (best + hi) / 2
+            if served(mid):
+                best = mid
+            else:
+                hi = mid
     return best
 
 
