@@ -633,6 +633,8 @@ PYBIND11_MODULE(_xsched, m) {
              d["active"] = c.active;
              d["backoff"] = c.backoff;
              d["unschedulable"] = c.unschedulable;
+             d["in_flight"] = s.queue().in_flight();
+             d["activation_marks"] = s.queue().pending_activations();
              return d;
            })
       .def("flush_backoff", [](Scheduler& s) { s.queue().flush_backoff_completed(); })

@@ -213,6 +213,7 @@ void SchedulingQueue::add(const PodPtr& p) {
     q->enqueue_seq = ++seq_;
     unschedulable_.erase(p->uid());
     backoff_.erase(p->uid());
+    in_flight_.erase(p->uid());
     active_.push(q);
   }
   nominator_->add(p, "");
@@ -234,7 +235,11 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
       } else if ((q = backoff_.get(uid))) {
         backoff_.erase(uid);
       }
-      if (!q) continue;  // not queued (in flight or assigned)
+      if (!q) {  // in flight: remember the request for when its cycle fails
+        auto f = in_flight_.find(uid);
+        if (f != in_flight_.end()) f->second = true;
+        continue;
+      }
       active_.push(q);
       moved = true;
     }
@@ -243,19 +248,41 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
 }
 
 bool SchedulingQueue::add_unschedulable_if_not_present(const QueuedPodInfoPtr& p, int64_t pod_cycle) {
+  bool activated = false;
   {
     std::lock_guard<std::mutex> g(mu_);
     const std::string& uid = p->pod->uid();
     if (unschedulable_.count(uid) || active_.contains(uid) || backoff_.contains(uid)) return false;
     p->timestamp_us = clock_->now_us();
-    if (move_request_cycle_ >= pod_cycle) {
+    bool marked = false;
+    if (auto f = in_flight_.find(uid); f != in_flight_.end()) {
+      marked = f->second;
+      in_flight_.erase(f);
+    }
+    if (marked) {
+      active_.push(p);  // activated while in flight; Activate skips backoff
+      activated = true;
+    } else if (move_request_cycle_ >= pod_cycle) {
       backoff_.push(p);
     } else {
       unschedulable_[uid] = p;
     }
   }
   nominator_->add(p->pod, "");
+  if (activated) cv_.notify_all();
   return true;
+}
+
+size_t SchedulingQueue::pending_activations() const {
+  std::lock_guard<std::mutex> g(mu_);
+  size_t n = 0;
+  for (const auto& kv : in_flight_) n += kv.second;
+  return n;
+}
+
+size_t SchedulingQueue::in_flight() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return in_flight_.size();
 }
 
 int64_t SchedulingQueue::scheduling_cycle() const {
@@ -272,6 +299,7 @@ QueuedPodInfoPtr SchedulingQueue::pop(int timeout_ms) {
     return nullptr;
   if (closed_ && active_.empty()) return nullptr;
   QueuedPodInfoPtr q = active_.pop();
+  in_flight_.insert_or_assign(q->pod->uid(), false);
   q->attempts++;
   scheduling_cycle_++;
   return q;
@@ -322,6 +350,7 @@ void SchedulingQueue::update(const PodPtr& old_p, const PodPtr& new_p) {
       }
     } else {
       // Not queued anywhere: add to activeQ (it may have been in flight).
+      in_flight_.erase(uid);
       auto q = new_info(new_p);
       q->enqueue_seq = ++seq_;
       active_.push(q);
@@ -340,6 +369,7 @@ void SchedulingQueue::remove(const Pod& p) {
   active_.erase(p.uid());
   backoff_.erase(p.uid());
   unschedulable_.erase(p.uid());
+  in_flight_.erase(p.uid());
 }
 
 bool SchedulingQueue::affinity_term_matches(const Pod& waiting, const Pod& assigned) {
@@ -353,6 +383,7 @@ bool SchedulingQueue::affinity_term_matches(const Pod& waiting, const Pod& assig
 
 void SchedulingQueue::assigned_pod_added(const Pod& p) {
   std::lock_guard<std::mutex> g(mu_);
+  in_flight_.erase(p.uid());  // bound: its cycles are over
   std::vector<QueuedPodInfoPtr> match;
   for (const auto& kv : unschedulable_)
     if (affinity_term_matches(*kv.second->pod, p)) match.push_back(kv.second);

@@ -100,9 +100,17 @@ class SchedulingQueue {
   void set_cluster_event_map(std::vector<std::pair<ClusterEvent, std::set<std::string>>> m);
 
   void add(const PodPtr& p);
+  // Moves the pods to activeQ. A pod that is in flight (popped, in its
+  // scheduling or binding cycle) is marked instead, and
+  // add_unschedulable_if_not_present sends a marked pod to activeQ when that
+  // cycle fails: the request is not lost. (The reference drops it,
+  // scheduling_queue.go:307-337; its moveRequestCycle covers only cluster
+  // events, :376-400,629.)
   void activate(const std::vector<PodPtr>& pods);
   // Returns false if the pod is already queued (active/backoff).
   bool add_unschedulable_if_not_present(const QueuedPodInfoPtr& p, int64_t pod_scheduling_cycle);
+  size_t pending_activations() const;  // in-flight pods carrying an activation mark
+  size_t in_flight() const;
   int64_t scheduling_cycle() const;
   // Blocks until a pod is available or the queue is closed (nullptr).
   QueuedPodInfoPtr pop(int timeout_ms = -1);
@@ -138,6 +146,10 @@ class SchedulingQueue {
   PodHeap active_;
   PodHeap backoff_;
   std::unordered_map<std::string, QueuedPodInfoPtr> unschedulable_;
+  // Popped pods -> "activated while in flight". An entry lives until the pod
+  // re-enters a queue, is removed, or shows up assigned (every pod ends in one
+  // of those), so the map is bounded by the pods that exist.
+  std::unordered_map<std::string, bool> in_flight_;
   std::vector<std::pair<ClusterEvent, std::set<std::string>>> event_map_;
   int64_t scheduling_cycle_ = 0;
   int64_t move_request_cycle_ = -1;

@@ -657,8 +657,12 @@ void Scheduler::apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr 
       cache_->add_pod(np);
       queue_->assigned_pod_added(*np);
     } else if (responsible_for(*np) && !np->terminating()) {
-      queue_->add(np);
+      // The gang record first: once queued, the pod can be scheduled, admitted
+      // and bound by other threads before this one runs again, and a record
+      // opened after its own completion would never close (the gang would
+      // read as never bound).
       note_gang_enqueue(*np, clock_->now_us());
+      queue_->add(np);
       // A new member may complete its PodGroup: re-activate siblings parked
       // in unschedulableQ/backoffQ (targeted form of the Pod/Add cluster
       // event Coscheduling registers; O(group size), not O(queue)).

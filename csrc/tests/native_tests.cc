@@ -265,6 +265,47 @@ TEST(queue_backoff_and_unschedulable_flush) {
   q.close();
 }
 
+// An activation that arrives while the pod is in flight (popped, cycle not yet
+// failed) must survive until the failure is recorded: the pod goes straight to
+// activeQ instead of parking in unschedulableQ until the 60 s flush.
+TEST(queue_activation_while_in_flight_is_not_lost) {
+  auto clock = std::make_shared<FakeClock>();
+  Nominator nom;
+  QueueOptions o;
+  SchedulingQueue q([](const QueuedPodInfo& a, const QueuedPodInfo& b) { return a.pod->name() < b.pod->name(); },
+                    clock, o, &nom);
+  auto a = mk_pod("a", 0), b = mk_pod("b", 0);
+  q.add(a);
+  q.add(b);
+  auto qa = q.pop(0);
+  CHECK(qa && qa->pod->name() == "a");
+  int64_t cycle = q.scheduling_cycle();
+  CHECK_EQ(q.in_flight(), 1u);
+  q.activate({a, b});  // b is already active; a is mid-cycle
+  CHECK_EQ(q.pending_activations(), 1u);
+  qa->unschedulable_plugins = {"Coscheduling"};
+  CHECK(q.add_unschedulable_if_not_present(qa, cycle));
+  CHECK_EQ(q.counts().unschedulable, 0u);
+  CHECK_EQ(q.counts().active, 2u);
+  CHECK_EQ(q.in_flight(), 0u);
+  // Without an activation mark the failure parks the pod as before.
+  auto q1 = q.pop(0);
+  int64_t c1 = q.scheduling_cycle();
+  q1->unschedulable_plugins = {"Coscheduling"};
+  CHECK(q.add_unschedulable_if_not_present(q1, c1));
+  CHECK_EQ(q.counts().unschedulable, 1u);
+  // A pod that binds drops its in-flight entry (no mark leaks).
+  auto q2 = q.pop(0);
+  CHECK(q2);
+  q.activate({q2->pod});
+  Pod bound = *q2->pod;
+  bound.node_name = "n0";
+  q.assigned_pod_added(bound);
+  CHECK_EQ(q.in_flight(), 0u);
+  CHECK_EQ(q.pending_activations(), 0u);
+  q.close();
+}
+
 // -------------------------------------------------------------- TimerService
 TEST(timers_fire_in_deadline_order_with_fake_clock) {
   auto clock = std::make_shared<FakeClock>();

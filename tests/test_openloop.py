@@ -26,9 +26,6 @@ def test_plan_interleaves_types_and_sizes_hold():
     assert abs(hold_us - 0.5 * 96 / (gang_rate * 0.8 * 3.75) * 1e6) < 1000
 
 
-@pytest.mark.xfail(strict=False, reason="open issue (docs/STATUS.md): in 2 of 4 full-suite runs one gang "
-                                        "stays unbound for 20 s after the last arrival; it passes when the file "
-                                        "runs alone; cause not yet found")
 def test_open_loop_admits_every_gang_with_ordered_timeline():
     sh = Shard(ClusterSpec(nodes=16), namespace="b")
     try:
