@@ -54,10 +54,12 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     import signal
     import subprocess
 
-    try:
-        import torch
+    from flex_gpu_scheduler_amd.gpu.discovery import visible_gpu_count
 
-        have = torch.cuda.device_count()  # does not initialise HIP on this image
+    # Counted from amdgpu sysfs / KFD: the parent never loads HIP, so nothing
+    # GPU-side is initialised before the ranks start.
+    try:
+        have = visible_gpu_count()
     except Exception:  # noqa: BLE001
         have = 0
     if have and have < n:
@@ -102,6 +104,10 @@ def main() -> int:
                     help="shard CPU placement: none | l3 | l3xK | explicit list (utils/cpuaffinity.py)")
     ap.add_argument("--no-open-loop", action="store_true",
                     help="skip the untimed open-loop (Poisson arrivals) gang admission latency run")
+    ap.add_argument("--waves-per-step", type=int, default=16,
+                    help="waves per timed step (one wave fills the shard's GPUs once)")
+    ap.add_argument("--no-service-mode", action="store_true",
+                    help="skip the untimed service-mode run (API server in another process, HTTP)")
     ap.add_argument("--no-placement", action="store_true",
                     help="skip the end-to-end placement validation (discovery -> scheduler -> Allocate -> RCCL)")
     args = ap.parse_args()
@@ -151,14 +157,16 @@ def main() -> int:
     shard = Shard(spec, namespace=f"bench-r{ctx.rank}", seed=args.seed + 7919 * ctx.rank,
                   options=json.loads(args.sched_options))
     # Pre-render every wave's JSON (data preparation, outside the timed region).
-    waves = [shard.wave(i) for i in range(args.warmup + args.steps + 1)]  # +1: the untimed check wave
+    wps = max(1, args.waves_per_step)
+    n_waves = (args.warmup + args.steps) * wps
+    waves = [shard.wave(i) for i in range(n_waves + 1)]  # +1: the untimed check wave
     # Each chunk's PodGroups are written just before its pods (as job
     # submitters do), unless XSCHED_BENCH_INTERLEAVE=0 (all PodGroups first;
     # A/B runs).
     interleave = os.environ.get("XSCHED_BENCH_INTERLEAVE", "1") != "0"
     prepared = [w.chunks_json() if interleave else (w.groups_json(), w.pods_json()) for w in waves]
 
-    for i in range(args.warmup):
+    for i in range(args.warmup * wps):
         shard.run(waves[i], prepared=prepared[i])
 
     if args.trace and ctx.rank == 0:
@@ -168,10 +176,11 @@ def main() -> int:
     t0 = time.perf_counter()
     pods = 0
     gangs: list[dict] = []
-    for i in range(args.warmup, args.warmup + args.steps):
+    for i in range(args.warmup * wps, n_waves):
         r = shard.run(waves[i], prepared=prepared[i])
         pods += r.pods
         gangs.extend(r.gangs)
+    t_rank = time.perf_counter() - t0
     ctx.sync()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
@@ -189,18 +198,24 @@ def main() -> int:
     t_max = ctx.all_max(elapsed)
     pods_total = ctx.all_sum(float(pods))
     all_gangs = [g for part in ctx.gather(gangs) for g in part]
+    per_rank = ctx.gather(round(pods / t_rank, 1) if t_rank > 0 else 0.0)
+    del waves, prepared
     stats = shard.sched.stats()
     if ctx.rank == 0 and not args.no_open_loop:
         # Untimed: Poisson gang arrivals at 50% / 90% of this shard's measured
-        # throughput, gang types interleaved, held then deleted
+        # open-loop capacity, gang types interleaved, held then deleted
         # (utils/openloop.py) — admission latency rather than burst queueing.
         from flex_gpu_scheduler_amd.utils.openloop import open_loop_capacity, run_open_loop
 
-        burst = pods / elapsed if elapsed > 0 else 0.0
-        cap = open_loop_capacity(shard, burst, seed=args.seed) if burst > 0 else 0.0
+        burst = pods / t_rank if t_rank > 0 else 0.0
+        search: list[dict] = []
+        cap = open_loop_capacity(shard, burst, seed=args.seed, log=search) if burst > 0 else 0.0
         extras["gang_admit_open_loop"] = {
             "burst_capacity_pods_per_s": round(burst, 1),
             "capacity_pods_per_s": round(cap, 1),
+            "capacity_rule": "highest x1.3-step rate (+2 bisection steps) served with every gang bound and "
+                             "p99 PG-create->last-Bind <= 25 ms; one trial per rate",
+            "capacity_search": search,
             **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed + 1)
                for f in (0.5, 0.9) if cap > 0}}
     shard.close()
@@ -208,9 +223,28 @@ def main() -> int:
     if not args.no_placement and (ctx.distributed or ctx.cuda):
         # Untimed: gangs placed on the live node, resolved by the device
         # plugin, all-reduced on exactly those GPUs (parallel/placement.py).
+        # A failure there is reported, not fatal to the headline line.
         from flex_gpu_scheduler_amd.parallel.placement import validate_placement
 
-        extras["rccl_placement"] = validate_placement(ctx)
+        try:
+            extras["rccl_placement"] = validate_placement(ctx)
+        except Exception as e:  # noqa: BLE001
+            extras["rccl_placement"] = {"error": f"{type(e).__name__}: {e}"}
+    if ctx.rank == 0 and not args.no_service_mode:
+        # Untimed: the deployable shape — scheduler and API server in separate
+        # processes over loopback HTTP (tools/remote_bench.py).
+        try:
+            from flex_gpu_scheduler_amd.tools.remote_bench import run as remote_run
+
+            plain = remote_run(64, 4000, False, 16, 8)
+            gang = remote_run(64, 512, True, 16, 8)
+            extras["service_mode"] = {
+                "apiserver": "native HTTP/1.1 (csrc/apiserver), separate process, loopback",
+                "plain": {k: plain[k] for k in ("pods", "pods_per_s", "pods_per_s_after_sync", "sync_s", "bound")},
+                "gang8": {k: gang[k] for k in ("pods", "pods_per_s", "pods_per_s_after_sync", "sync_s", "bound")}}
+            extras["service_mode_pods_per_s"] = plain["pods_per_s"]
+        except Exception as e:  # noqa: BLE001
+            extras["service_mode"] = {"error": f"{type(e).__name__}: {e}"}
 
     value = pods_total / t_max if t_max > 0 else 0.0
     if ctx.rank == 0 and not args.no_scenarios:
@@ -237,11 +271,16 @@ def main() -> int:
             "config": {
                 "model": "FlexGPU(MI355X SPX/CPX/HBM) + Coscheduling + NRT xGMI gang placement",
                 "global_batch": int(round(pods_total / max(1, args.steps))),
+                "waves_per_step": wps,
+                "timed_region_s": round(t_max, 3),
                 "seq_len": None,
                 "parallelism": f"{ctx.world_size} rank(s) x 1 scheduler shard, one rank per GPU "
                                f"({ctx.backend if ctx.distributed else 'single process'})",
                 "nodes_per_shard": args.nodes,
                 "gpus_per_shard": args.nodes * 8,
+                "value_kind": "sum over independent per-rank scheduler shards (one shard per GPU)",
+                "per_rank": {"pods_per_s": per_rank,
+                             "spread": round((max(per_rank) - min(per_rank)) / max(1e-9, sum(per_rank) / len(per_rank)), 3)},
                 "p99_gang_admit_ms": {k: v["p99_ms"] for k, v in lat.items()},
                 "gang_admit": lat,
                 "gang_admit_by_type": gang_latency_summary(all_gangs, by_type=True),

@@ -143,7 +143,7 @@ class Coscheduling : public Plugin {
     Res need = pg->min_resources;
     need.set(kPods, pg->min_member);
     if (!check_cluster_resource(need, p)) {
-      deny(p);
+      deny(p, "minresources");
       return Status::unresolvable("resource gap for PodGroup " + p.pg_full_name());
     }
     permitted_.add(p.pg_key, wait_time(*pg));
@@ -206,7 +206,7 @@ class Coscheduling : public Plugin {
     float gap = static_cast<float>(pg->min_member - assigned) / static_cast<float>(std::max(1, pg->min_member));
     if (gap <= 0.1f) return {PostFilterResult{}, Status(Code::Unschedulable)};
     reject_group(p, "optimistic rejection in PostFilter");
-    deny(p);
+    deny(p, "postfilter");
     permitted_.erase(p.pg_key);
     return {PostFilterResult{},
             Status::unschedulable("PodGroup " + full + " gets rejected due to Pod " + p.name() +
@@ -221,8 +221,10 @@ class Coscheduling : public Plugin {
   // One requeue timer per group at a time: Unreserve runs once per rejected
   // member, so a gang denial calls deny() k times; later calls only push the
   // pending timer's deadline (it re-arms itself for the remainder).
-  void deny(const Pod& p) {
+  void deny(const Pod& p, const char* why) {
+    const bool fresh_denial = !denied_.has(p.pg_key);
     denied_.add(p.pg_key, denied_ttl_us_);
+    if (fresh_denial && h_.gang_denied) h_.gang_denied(p, why);
     if (!h_.timers || !h_.activate) return;
     const int64_t due = h_.clock->now_us() + denied_ttl_us_ + 1000;
     {
@@ -305,7 +307,7 @@ class Coscheduling : public Plugin {
     auto pg = h_.informers->pod_group_of(*p);
     if (!pg) return;
     reject_group(*p, "rejection in Unreserve");
-    deny(*p);
+    deny(*p, "unreserve");
     permitted_.erase(p->pg_key);
   }
 

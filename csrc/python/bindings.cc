@@ -626,6 +626,31 @@ PYBIND11_MODULE(_xsched, m) {
             return out;
           },
           py::arg("clear") = false)
+      .def(
+          "gang_denials",
+          [](Scheduler& s, bool clear) {
+            uint64_t total = 0;
+            auto v = s.gang_denials(clear, &total);
+            py::list out;
+            for (const auto& d : v) {
+              py::dict e;
+              e["pod_group"] = d.pg;
+              e["why"] = d.why;
+              e["cause"] = d.cause;
+              e["t_us"] = d.t_us;
+              e["min_member"] = d.min_member;
+              e["assigned"] = d.assigned;
+              e["need_gpus"] = d.need_gpus;
+              e["cache_free"] = d.cache_free;
+              e["cache_max_node_free"] = d.cache_max_node_free;
+              e["assumed_held"] = d.assumed_held;
+              e["store_free"] = d.store_free;
+              e["store_max_node_free"] = d.store_max_node_free;
+              out.append(e);
+            }
+            return py::make_tuple(total, out);
+          },
+          py::arg("clear") = false)
       .def("queue_counts",
            [](Scheduler& s) {
              auto c = s.queue().counts();

@@ -471,6 +471,33 @@ NodeInfoPtr SchedulerCache::node_info_copy(const std::string& name) const {
   return it == nodes_.end() ? nullptr : it->second->clone();
 }
 
+std::vector<SchedulerCache::GpuCensusRow> SchedulerCache::gpu_census() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<GpuCensusRow> out;
+  out.reserve(order_.size());
+  std::unordered_map<std::string, size_t> row;
+  for (const auto& name : order_) {
+    auto it = nodes_.find(name);
+    if (it == nodes_.end() || !it->second->node) continue;
+    const GpuLedger& L = it->second->gpu;
+    GpuCensusRow r;
+    r.node = name;
+    for (int gi = 0; gi < L.gpu_count; ++gi) r.spx += L.parts[gi] == 1;
+    r.free_whole = L.free_gpus();
+    row.emplace(name, out.size());
+    out.push_back(std::move(r));
+  }
+  for (const auto& uid : assumed_) {
+    auto it = pod_states_.find(uid);
+    if (it == pod_states_.end()) continue;
+    const Pod& p = *it->second.pod;
+    if (p.gpu_demand.kind != GpuDemand::Gpu) continue;
+    auto r = row.find(p.node_name);
+    if (r != row.end()) out[r->second].assumed_whole += static_cast<int>(p.gpu_demand.amount);
+  }
+  return out;
+}
+
 std::vector<std::string> SchedulerCache::node_names() const {
   std::lock_guard<std::mutex> g(mu_);
   return order_;

@@ -95,6 +95,13 @@ class SchedulerCache {
   size_t pod_count() const;
   size_t assumed_count() const;
   NodeInfoPtr node_info_copy(const std::string& name) const;
+  // Whole-GPU (SPX) census per node for gang-denial diagnostics: SPX GPUs,
+  // free ones, and those held by assumed (not yet bound) pods.
+  struct GpuCensusRow {
+    std::string node;
+    int spx = 0, free_whole = 0, assumed_whole = 0;
+  };
+  std::vector<GpuCensusRow> gpu_census() const;
   std::vector<std::string> node_names() const;
 
  private:

@@ -260,6 +260,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.clock = clock_;
     h.timers = timers_.get();
     h.activate = [this](const std::vector<PodPtr>& pods) { queue_->activate(pods); };
+    h.gang_denied = [this](const Pod& p, const char* why) { note_gang_denied(p, why); };
     h.metrics = metrics_.get();
     h.snapshot = &snapshot_;
     h.extenders = &extenders_;
@@ -768,6 +769,77 @@ void Scheduler::note_gang_event(const Pod& p, bool bound) {
       .observe(static_cast<double>(r.bound_us - r.first_enqueue_us) / 1e6);
   gang_done_.push_back(r);
   gangs_.erase(it);
+}
+
+// Why was a gang denied? The cache's view (free SPX GPUs, those held by
+// assumed pods of gangs still waiting at Permit) against the store's at the
+// same moment (bound pods only): separates a stale cache (deletions not yet
+// observed) from GPUs held by other waiting gangs and from a real shortage.
+void Scheduler::note_gang_denied(const Pod& p, const char* why) {
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    ++gang_denials_total_;
+    if (gang_denials_.size() >= kMaxGangDenials) return;
+  }
+  GangDenial d;
+  d.pg = gang_key(p);
+  d.why = why;
+  d.t_us = clock_->now_us();
+  auto pg = informers_->pod_group_of(p);
+  d.min_member = pg ? pg->min_member : 0;
+  d.assigned = cache_->assigned_in_group(p.pg_key);
+  d.need_gpus = p.gpu_demand.kind == GpuDemand::Gpu ? p.gpu_demand.amount : 0;
+  std::unordered_map<std::string, int> spx;
+  for (const auto& r : cache_->gpu_census()) {
+    spx[r.node] = r.spx;
+    d.cache_free += r.free_whole;
+    d.cache_max_node_free = std::max(d.cache_max_node_free, r.free_whole);
+    d.assumed_held += r.assumed_whole;
+  }
+  if (store_) {
+    std::unordered_map<std::string, int> used;
+    const std::string& gpu = gpu_names_->gpu;
+    for (const auto& po : store_->list("pods", "")) {
+      const Json& spec = (*po)["spec"];
+      const std::string& node = spec["nodeName"].as_string();
+      if (node.empty() || (*po)["metadata"].get("deletionTimestamp")) continue;
+      int64_t n = 0;
+      for (const auto& c : spec["containers"].items()) {
+        const Json& lim = c["resources"]["limits"][gpu];
+        if (lim.is_string()) n += Quantity::parse(lim.as_string()).value();
+        else if (lim.is_number()) n += lim.as_int();
+      }
+      if (n) used[node] += static_cast<int>(n);
+    }
+    d.store_free = 0;
+    for (const auto& [node, cap] : spx) {
+      auto u = used.find(node);
+      int f = std::max(0, cap - (u == used.end() ? 0 : u->second));
+      d.store_free += f;
+      d.store_max_node_free = std::max(d.store_max_node_free, f);
+    }
+  }
+  // The gang still needed (min_member - assigned) more whole GPUs.
+  const int64_t missing = d.need_gpus * std::max(0, d.min_member - d.assigned);
+  if (d.need_gpus == 0) d.cause = "not_whole_gpu";
+  else if (d.store_free < 0) d.cause = "unknown";
+  else if (d.store_free < missing) d.cause = "capacity";
+  else if (d.store_free - d.assumed_held < missing) d.cause = "held_by_waiting_gangs";
+  else if (d.cache_free < missing) d.cause = "stale_cache";
+  else d.cause = "placement";
+  std::lock_guard<std::mutex> g(stats_mu_);
+  if (gang_denials_.size() < kMaxGangDenials) gang_denials_.push_back(std::move(d));
+}
+
+std::vector<GangDenial> Scheduler::gang_denials(bool clear, uint64_t* total) {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  std::vector<GangDenial> out = gang_denials_;
+  if (total) *total = gang_denials_total_;
+  if (clear) {
+    gang_denials_.clear();
+    gang_denials_total_ = 0;
+  }
+  return out;
 }
 
 // -------------------------------------------------------- scheduling ----

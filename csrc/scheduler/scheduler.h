@@ -121,6 +121,17 @@ struct GangRecord {
   int64_t bound_us = 0;   // last member bound
 };
 
+// One Coscheduling group denial with the GPU census at that moment
+// (Scheduler::note_gang_denied). store_* are -1 without an in-process store.
+struct GangDenial {
+  std::string pg, why, cause;
+  int64_t t_us = 0;
+  int min_member = 0, assigned = 0;
+  int64_t need_gpus = 0;  // whole GPUs per member
+  int cache_free = 0, cache_max_node_free = 0, assumed_held = 0;
+  int store_free = -1, store_max_node_free = -1;
+};
+
 class Scheduler {
  public:
   // config JSON: {"profiles":[...ProfileConfig...], "options":{...}}
@@ -175,6 +186,9 @@ class Scheduler {
   bool wait_bound(uint64_t target, int64_t timeout_us) const;
   bool wait_cache_empty(int64_t timeout_us) const;
   std::vector<GangRecord> gang_records(bool clear = false);
+  // Group denials since the last clear (the first kMaxGangDenials with
+  // their census; `total` counts all of them).
+  std::vector<GangDenial> gang_denials(bool clear = false, uint64_t* total = nullptr);
   size_t inflight_bindings() const { return inflight_.load(); }
 
  private:
@@ -287,6 +301,7 @@ class Scheduler {
                       const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins);
   void note_gang_enqueue(const Pod& p, int64_t t);
   void note_gang_event(const Pod& p, bool bound);
+  void note_gang_denied(const Pod& p, const char* why);
   bool responsible_for(const Pod& p) const;
 
   std::shared_ptr<ObjectStore> store_;
@@ -329,6 +344,9 @@ class Scheduler {
   std::atomic<bool> fit_error_dumped_{false};  // dump_on_fit_error written
   std::unordered_map<std::string, GangRecord> gangs_;  // open groups
   std::vector<GangRecord> gang_done_;
+  static constexpr size_t kMaxGangDenials = 256;
+  std::vector<GangDenial> gang_denials_;
+  uint64_t gang_denials_total_ = 0;
   std::unordered_map<std::string, std::string> last_condition_;  // uid -> last failure message
 };
 

@@ -1,5 +1,7 @@
 #include "store/store.h"
 
+#include "common/clock.h"
+
 #include <chrono>
 #include <cstdio>
 #include <thread>
@@ -67,6 +69,43 @@ size_t Watcher::pending() const {
 }
 
 // ---------------------------------------------------------- ObjectStore ----
+ObjectStore::~ObjectStore() {
+  {
+    std::lock_guard<std::mutex> g(reap_mu_);
+    reap_stop_ = true;
+  }
+  reap_cv_.notify_all();
+  if (reaper_.joinable()) reaper_.join();
+}
+
+void ObjectStore::reap(std::vector<WatchEvent>&& dead) const {
+  {
+    std::lock_guard<std::mutex> g(reap_mu_);
+    if (reap_stop_) return;  // destroyed here
+    if (!reaper_.joinable()) reaper_ = std::thread([this] { reaper_loop(); });
+    if (reap_q_.empty()) {
+      reap_q_.swap(dead);
+    } else {
+      for (auto& e : dead) reap_q_.push_back(std::move(e));
+    }
+  }
+  reap_cv_.notify_one();
+}
+
+void ObjectStore::reaper_loop() const {
+  name_this_thread("xs-reaper");
+  std::unique_lock<std::mutex> lk(reap_mu_);
+  for (;;) {
+    reap_cv_.wait(lk, [&] { return reap_stop_ || !reap_q_.empty(); });
+    std::vector<WatchEvent> batch;
+    batch.swap(reap_q_);
+    lk.unlock();
+    batch.clear();  // the frees, off every writer's path
+    lk.lock();
+    if (reap_stop_ && reap_q_.empty()) return;
+  }
+}
+
 ObjectStore::ObjectStore() {
   uid_salt_ = static_cast<uint64_t>(std::chrono::steady_clock::now().time_since_epoch().count());
 }
@@ -125,6 +164,7 @@ void ObjectStore::emit_locked(EventType t, const std::string& kind, const JsonPt
   history_.push_back(std::move(ev));
   if (history_.size() > history_cap_) {
     compacted_rv_ = history_.front().rv;
+    evicted_.push_back(std::move(history_.front()));  // freed by ~Guard, after the lock
     history_.pop_front();
   }
 }
@@ -171,7 +211,7 @@ JsonPtr ObjectStore::create_locked(const std::string& kind, Json obj) {
 }
 
 void ObjectStore::set_event_ttl_us(int64_t ttl_us) {
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   event_ttl_us_ = ttl_us;
 }
 
@@ -191,7 +231,7 @@ void ObjectStore::expire_events_locked(const std::string& created_key) {
 
 JsonPtr ObjectStore::create(const std::string& kind, Json obj) {
   check_faults("create", kind);
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   return create_locked(kind, std::move(obj));
 }
 
@@ -199,7 +239,7 @@ std::vector<JsonPtr> ObjectStore::create_many(const std::string& kind, std::vect
   check_faults("create", kind);
   std::vector<JsonPtr> out;
   out.reserve(objs.size());
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   std::vector<WatchEvent> batch;
   batch_ = &batch;
   try {
@@ -254,7 +294,7 @@ void ObjectStore::flush_batch_locked(std::vector<WatchEvent>& batch) {
 }
 
 JsonPtr ObjectStore::get(const std::string& kind, const std::string& ns, const std::string& name) const {
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   auto kit = kinds_.find(kind);
   if (kit == kinds_.end()) return nullptr;
   auto it = kit->second.find(key_of(namespaced(kind) ? ns : "", name));
@@ -263,7 +303,7 @@ JsonPtr ObjectStore::get(const std::string& kind, const std::string& ns, const s
 
 std::vector<JsonPtr> ObjectStore::list(const std::string& kind, const std::string& ns, int64_t* rv_out) const {
   std::vector<JsonPtr> out;
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   if (rv_out) *rv_out = rv_.load();
   auto kit = kinds_.find(kind);
   if (kit == kinds_.end()) return out;
@@ -276,14 +316,14 @@ std::vector<JsonPtr> ObjectStore::list(const std::string& kind, const std::strin
 }
 
 size_t ObjectStore::count(const std::string& kind) const {
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   auto kit = kinds_.find(kind);
   return kit == kinds_.end() ? 0 : kit->second.size();
 }
 
 JsonPtr ObjectStore::update(const std::string& kind, Json obj, bool check_rv) {
   check_faults("update", kind);
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   const Json& md = obj["metadata"];
   std::string ns = namespaced(kind) ? md["namespace"].str_or("default") : "";
   std::string name = md["name"].as_string();
@@ -315,14 +355,14 @@ JsonPtr ObjectStore::update_optimistic(const std::string& kind, const std::strin
   for (;;) {
     JsonPtr base;
     {
-      std::lock_guard<std::mutex> g(mu_);
+      Guard g(*this);
       auto& km = kinds_[kind];
       auto it = km.find(key);
       if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
       base = it->second.obj;
     }
     std::optional<Json> next = build(*base);  // validation + copy + edit, unlocked
-    std::lock_guard<std::mutex> g(mu_);
+    Guard g(*this);
     auto& km = kinds_[kind];
     auto it = km.find(key);
     if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
@@ -365,7 +405,7 @@ JsonPtr ObjectStore::patch(const std::string& kind, const std::string& ns, const
 JsonPtr ObjectStore::remove(const std::string& kind, const std::string& ns, const std::string& name,
                             int64_t grace_seconds, const std::string& uid_precondition) {
   check_faults("delete", kind);
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   auto& km = kinds_[kind];
   auto it = km.find(key_of(namespaced(kind) ? ns : "", name));
   if (it == km.end()) throw StoreError(404, "NotFound", kind + " \"" + name + "\" not found");
@@ -395,7 +435,7 @@ JsonPtr ObjectStore::remove(const std::string& kind, const std::string& ns, cons
 size_t ObjectStore::remove_many(const std::string& kind, const std::string& ns,
                                 const std::vector<std::string>& names) {
   check_faults("delete", kind);
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   auto& km = kinds_[kind];
   std::vector<WatchEvent> batch;
   batch_ = &batch;
@@ -415,7 +455,7 @@ size_t ObjectStore::remove_many(const std::string& kind, const std::string& ns,
 }
 
 size_t ObjectStore::delete_all(const std::string& kind, const std::string& ns) {
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   auto kit = kinds_.find(kind);
   if (kit == kinds_.end()) return 0;
   size_t n = 0;
@@ -484,7 +524,7 @@ JsonPtr ObjectStore::bind(const std::string& ns, const std::string& name, const 
 
 WatcherPtr ObjectStore::watch(const std::set<std::string>& kinds, const std::string& ns, int64_t since_rv) {
   auto w = std::make_shared<Watcher>(kinds, ns);
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   if (since_rv > 0) {
     if (since_rv < compacted_rv_)
       throw StoreError(410, "Expired", "too old resource version: " + std::to_string(since_rv));
@@ -500,7 +540,7 @@ WatcherPtr ObjectStore::watch(const std::set<std::string>& kinds, const std::str
 
 void ObjectStore::unwatch(const WatcherPtr& w) {
   w->stop();
-  std::lock_guard<std::mutex> g(mu_);
+  Guard g(*this);
   for (auto it = watchers_.begin(); it != watchers_.end(); ++it) {
     if (*it == w) {
       watchers_.erase(it);

@@ -28,6 +28,7 @@
 #include <random>
 #include <set>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -93,6 +94,7 @@ struct FaultRule {
 class ObjectStore {
  public:
   ObjectStore();
+  ~ObjectStore();
 
   JsonPtr create(const std::string& kind, Json obj);
   JsonPtr get(const std::string& kind, const std::string& ns, const std::string& name) const;  // nullptr if absent
@@ -163,6 +165,36 @@ class ObjectStore {
   std::vector<WatchEvent>* batch_ = nullptr;  // bulk ops collect events here (under mu_)
 
   mutable std::mutex mu_;
+  // Holds mu_ for one store operation. History entries evicted meanwhile
+  // are destroyed after the lock is released: the entry is usually the last
+  // reference to a deleted object, and freeing its JSON tree under mu_ made
+  // every writer (16 binder threads) wait for it once the history was full.
+  class Guard {
+   public:
+    explicit Guard(const ObjectStore& s) : s_(s) { s_.mu_.lock(); }
+    ~Guard() {
+      std::vector<WatchEvent> dead;
+      if (!s_.evicted_.empty()) dead.swap(s_.evicted_);
+      s_.mu_.unlock();
+      if (!dead.empty()) s_.reap(std::move(dead));
+    }
+    Guard(const Guard&) = delete;
+    Guard& operator=(const Guard&) = delete;
+
+   private:
+    const ObjectStore& s_;
+  };
+  mutable std::vector<WatchEvent> evicted_;
+  // Evicted entries are freed on a background thread (started on the first
+  // eviction), as a garbage-collected API server would: the writer that
+  // evicts them does not pay for the JSON trees of objects deleted long ago.
+  void reap(std::vector<WatchEvent>&& dead) const;
+  void reaper_loop() const;
+  mutable std::mutex reap_mu_;
+  mutable std::condition_variable reap_cv_;
+  mutable std::vector<WatchEvent> reap_q_;
+  mutable std::thread reaper_;
+  mutable bool reap_stop_ = false;
   std::unordered_map<std::string, KindMap> kinds_;
   std::atomic<int64_t> rv_{0};
   std::vector<WatcherPtr> watchers_;

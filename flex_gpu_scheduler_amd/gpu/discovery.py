@@ -207,6 +207,20 @@ def discover_gpus(root: str = "/") -> list[GpuDevice]:
     return gpus
 
 
+def visible_gpu_count(root: str = "/", env: dict | None = None) -> int:
+    """GPUs this process may use, counted from amdgpu sysfs / KFD without
+    touching HIP: the physical GPUs, narrowed by the first visibility list
+    that is set (ROCR_VISIBLE_DEVICES, HIP_VISIBLE_DEVICES,
+    CUDA_VISIBLE_DEVICES). 0 when sysfs shows no GPU."""
+    env = os.environ if env is None else env
+    n = len(discover_gpus(root))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            return min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def discover_host(root: str = "/") -> HostInfo:
     gpus = discover_gpus(root)
     nodes = parse_cpulist(_read(os.path.join(root, "sys/devices/system/node/online"), "0"))

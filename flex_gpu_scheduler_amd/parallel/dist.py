@@ -84,10 +84,18 @@ def init_distributed(want_cuda: bool = True) -> DistContext:
             cuda = False
     ctx.cuda = cuda
     if ws > 1:
+        import datetime
+
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = "nccl" if cuda else "gloo"
-        dist.init_process_group(backend=backend, rank=rank, world_size=ws)
+        if cuda:
+            # A collective that times out raises in the caller (instead of the
+            # watchdog aborting the process), so a failed rank cannot hang the
+            # job or kill the headline line of the others.
+            os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        timeout = datetime.timedelta(seconds=float(os.environ.get("XSCHED_DIST_TIMEOUT_S", "300")))
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws, timeout=timeout)
         ctx.backend = backend
     return ctx

@@ -33,6 +33,7 @@ the node comes from `fake_host` and the collectives run on gloo.
 """
 from __future__ import annotations
 
+import datetime
 import json
 import os
 import tempfile
@@ -257,7 +258,7 @@ def _reduce_bw(group, members: list[int], rank: int, nbytes: int, cuda: bool, it
 
 
 def validate_placement(ctx, sizes=GANG_SIZES, rccl_mib=(16, 256), staged_mib=(16,), iters: int = 10,
-                       warmup: int = 3, root: str = "/") -> dict:
+                       warmup: int = 3, root: str = "/", group_timeout_s: float = 120.0) -> dict:
     """Collective over all ranks of `ctx` (parallel/dist.py DistContext).
     Rank 0 plans (discovery -> scheduler -> Allocate), every rank joins the
     sub-communicators; rank 0 returns the table, other ranks return {}."""
@@ -303,23 +304,37 @@ def validate_placement(ctx, sizes=GANG_SIZES, rccl_mib=(16, 256), staged_mib=(16
             specs.append(("host_staged", p["ordinals"], "gloo", True, staged_mib))
             for label, ranks, be, staged, mibs in specs:
                 ranks = sorted(ranks)
-                # new_group is collective over the whole world, members or not.
-                g = dist.new_group(ranks=ranks, backend=be)
+                # new_group is collective over the whole world, members or not;
+                # every rank walks the same specs even after a failure, so the
+                # world stays in step and the error is reported per row.
                 out = None
-                if ctx.rank in ranks:
-                    out = [_reduce_bw(g, ranks, ctx.rank, m << 20, ctx.cuda,
-                                      iters if not staged else max(2, iters // 3), warmup if not staged else 1,
-                                      host_staged=staged and ctx.cuda) for m in mibs]
+                g = None
+                try:
+                    g = dist.new_group(ranks=ranks, backend=be, timeout=datetime.timedelta(seconds=group_timeout_s))
+                    if ctx.rank in ranks:
+                        out = [_reduce_bw(g, ranks, ctx.rank, m << 20, ctx.cuda,
+                                          iters if not staged else max(2, iters // 3), warmup if not staged else 1,
+                                          host_staged=staged and ctx.cuda) for m in mibs]
+                except Exception as e:  # noqa: BLE001
+                    out = {"error": f"rank {ctx.rank}: {type(e).__name__}: {e}"}
                 got = ctx.gather(out)
                 if ctx.rank == 0:
-                    res = [r for r in got if r is not None]
-                    # The slowest member defines the collective's bandwidth.
-                    per = []
-                    for i in range(len(mibs)):
-                        worst = min((r[i] for r in res), key=lambda d: d["busbw_GBps"])
-                        per.append({**worst, "correct": all(r[i]["correct"] for r in res)})
-                    row[label] = {"ranks": ranks, "backend": be, "results": per}
-                dist.destroy_process_group(g)
+                    errs = [r["error"] for r in got if isinstance(r, dict)]
+                    res = [r for r in got if isinstance(r, list)]
+                    if errs or not res:
+                        row[label] = {"ranks": ranks, "backend": be, "error": "; ".join(errs) or "no results"}
+                    else:
+                        # The slowest member defines the collective's bandwidth.
+                        per = []
+                        for i in range(len(mibs)):
+                            worst = min((r[i] for r in res), key=lambda d: d["busbw_GBps"])
+                            per.append({**worst, "correct": all(r[i]["correct"] for r in res)})
+                        row[label] = {"ranks": ranks, "backend": be, "results": per}
+                if g is not None:
+                    try:
+                        dist.destroy_process_group(g)
+                    except Exception:  # noqa: BLE001
+                        pass
         rows.append(row)
     if ctx.rank != 0:
         return {}
@@ -327,10 +342,10 @@ def validate_placement(ctx, sizes=GANG_SIZES, rccl_mib=(16, 256), staged_mib=(16
     for r in rows:
         if "placed" not in r:
             continue
-        s = {k: {str(x["MiB"]): x["busbw_GBps"] for x in r[k]["results"]}
-             for k in ("placed", "cross_socket", "host_staged") if k in r}
-        s["all_correct"] = all(x["correct"] for k in ("placed", "cross_socket", "host_staged") if k in r
-                               for x in r[k]["results"])
+        kinds = [k for k in ("placed", "cross_socket", "host_staged") if k in r]
+        s = {k: ({str(x["MiB"]): x["busbw_GBps"] for x in r[k]["results"]} if "results" in r[k]
+                 else {"error": r[k]["error"]}) for k in kinds}
+        s["all_correct"] = all("results" in r[k] and all(x["correct"] for x in r[k]["results"]) for k in kinds)
         summary[str(r["gang"])] = s
     return {"source": plan_doc["source"], "backend": backend, "node": plan_doc["node"], "gangs": rows,
             "summary": summary, "env": {"HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")}}

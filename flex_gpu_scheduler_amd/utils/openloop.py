@@ -90,7 +90,7 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
 
 def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, seed: int = 0,
                        start_pods_per_s: float = 2000.0, occupancy: float = 0.5,
-                       p99_budget_ms: float = 25.0) -> float:
+                       p99_budget_ms: float = 25.0, log: list | None = None) -> float:
     """Sustained open-loop capacity (pods/s): the highest arrival rate, in
     steps x1.3 apart from `start_pods_per_s` up to `max_pods_per_s` (the
     burst capacity), that the shard serves under the same conditions as the
@@ -98,25 +98,25 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     with every gang bound, the last one done within 1.2x the arrival window
     plus the hold, and every gang type's p99 PG-create -> last-Bind under
     `p99_budget_ms`, then refined by two bisection steps inside the last
-    interval. Past that rate a backlog builds (gang members fail on a
-    cluster whose deletions the scheduler has not seen yet, and Coscheduling
-    denies the group), so the throughput of an overloaded run would say
-    nothing about admission latency.
+    interval.
 
-    A rate whose first trial fails gets two more trials (other arrival
-    seeds) and counts as served when both pass: near capacity a single
-    8-rank gang can find the SPX pool momentarily full and be denied for the
-    reference's denied-PodGroup TTL, and one such draw stopped the climb
-    anywhere between 21k and 47k pods/s on the same tree
-    (profiles/r3al_bench64_{1,2}.json)."""
-    def trial(rate: float, k: int) -> bool:
-        r = run_open_loop(shard, rate, duration_s, seed=seed + 7717 * k, occupancy=occupancy)
-        ok = all(v["unbound"] == 0 and (v["create_to_bound_ms"]["p99"] or 0) <= p99_budget_ms
-                 for v in r["by_gang"].values())
-        return ok and r["wall_s"] <= 1.2 * duration_s + r["hold_ms"] / 1e3 + 0.05
-
+    The rule is frozen (round 4): ONE trial per rate, its arrival seed fixed
+    by `seed`, no retries. Every trial is appended to `log` with its gang
+    denials and their causes (Scheduler::note_gang_denied), so a rate that
+    fails says why. (Round 3's instability came from a measurement race, not
+    the search: a gang could bind before the scheduler opened its record and
+    then read as never bound; fixed in Scheduler::apply_pod_update.)"""
     def served(rate: float) -> bool:
-        return trial(rate, 0) or (trial(rate, 1) and trial(rate, 2))
+        r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=occupancy)
+        worst = max((v["create_to_bound_ms"]["p99"] or 0) for v in r["by_gang"].values())
+        unbound = sum(v["unbound"] for v in r["by_gang"].values())
+        ok = (unbound == 0 and worst <= p99_budget_ms
+              and r["wall_s"] <= 1.2 * duration_s + r["hold_ms"] / 1e3 + 0.05)
+        if log is not None:
+            log.append({"offered_pods_per_s": round(rate, 1), "served": ok, "unbound_gangs": unbound,
+                        "worst_p99_create_to_bound_ms": worst, "wall_s": r["wall_s"],
+                        "denied_gangs": r["denials"]["total"], "denial_causes": r["denials"]["causes"]})
+        return ok
 
     rate = min(start_pods_per_s, max(max_pods_per_s, 1.0))
     # A small cluster or a loaded host may not serve even the start rate:
@@ -144,6 +144,15 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     return best
 
 
+def denial_summary(total: int, recs: list[dict], keep: int = 3) -> dict:
+    """Coscheduling group denials of one run: how many, by cause, and the
+    first few records with the cache/store GPU census at that moment."""
+    causes: dict[str, int] = {}
+    for d in recs:
+        causes[d["cause"]] = causes.get(d["cause"], 0) + 1
+    return {"total": int(total), "causes": causes, "first": recs[:keep]}
+
+
 _runs = 0  # run_open_loop calls in this process: the gang-name tag
 
 
@@ -157,9 +166,11 @@ def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: 
     _runs += 1
     gangs, kinds, offsets, hold_us = plan(shard.spec, rate_pods_per_s, duration_s, seed, occupancy=occupancy,
                                           tag=f"{_runs}r")
+    shard.sched.gang_denials(True)
     res = native().run_open_loop(shard.store, shard.sched, json.dumps(gangs), offsets, hold_us, 10_000_000)
     shard.sched.wait_idle(10_000)
     out = summarize(kinds, res["gangs"], res["wall_us"], res["late_us"])
+    out["denials"] = denial_summary(*shard.sched.gang_denials(True))
     n = max(1, len(res["gangs"]))
     out.update({"mean_delete_lag_us": round(res.get("delete_late_us", 0) / n, 1),
                 "max_in_flight_pods": res.get("max_in_flight_pods"), "max_held_pods": res.get("max_held_pods")})

@@ -216,37 +216,83 @@ def capacity_preemption(iterations: int = 2) -> dict:
             "note": "includes upstream pod backoff (1s initial) between preemption and re-scheduling"}
 
 
-def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None) -> dict:
-    """TargetLoadPacking in GPU mode on 8 MI355X nodes whose WatcherMetrics
-    carry the live busy % of this host's amdgpu devices (one physical GPU's
-    utilisation per simulated node; synthetic values without sysfs)."""
+def _gpu_activity(hs) -> tuple[float | None, float | None, str]:
+    """(GFX busy %, HBM-controller activity %, source) of the host's first GPU."""
+    if getattr(hs, "smi", None) is not None:
+        cs = hs.smi.sample()
+        if cs:
+            return cs[0].gfx, cs[0].umc, "amd-smi (libamd_smi) gfx_activity / umc_activity"
+    live = [b for b, _ in hs.gpu_samples()]
+    if live and live[0] is not None:
+        return float(live[0]), None, "amdgpu sysfs gpu_busy_percent"
+    return None, None, "synthetic"
+
+
+def _mean_activity(hs, seconds: float, period: float = 0.05) -> tuple[float | None, float | None, str]:
+    gfx, umc, src = [], [], "synthetic"
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        g, u, src = _gpu_activity(hs)
+        if g is not None:
+            gfx.append(g)
+        if u is not None:
+            umc.append(u)
+        time.sleep(period)
+    avg = (lambda xs: round(sum(xs) / len(xs), 1) if xs else None)
+    return avg(gfx), avg(umc), src
+
+
+def _cuda_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None, start_load=None, seconds: float = 1.0) -> dict:
+    """TargetLoadPacking in GPU mode on `nodes` MI355X nodes whose
+    WatcherMetrics carry live GPU activity of this host: the first half of
+    the nodes publish a sample of the idle GPU, the second half a sample
+    taken while a device copy loop keeps it busy (tools/tlp_live.py; on a
+    GPU host `start_load` defaults to that loop). The busy nodes must score
+    below the idle ones (pkg/trimaran/targetloadpacking/targetloadpacking.go:
+    181-270, target 40 %). Without a GPU the values are synthetic."""
     from ..gpu.telemetry import HostSampler, NodeTelemetry, Sample, publish
     from ..control.client import LocalClient
 
-    live, hbm = [], []
-    source = "synthetic"
     try:
         hs = sampler or HostSampler()
-        if hs.smi is not None:
-            cs = hs.smi.sample()
-            live, hbm = [c.gfx for c in cs], [c.umc for c in cs]
-            source = "amd-smi (libamd_smi) gfx_activity / umc_activity"
-        else:
-            live = [b for b, _ in hs.gpu_samples()]
-            source = "amdgpu sysfs gpu_busy_percent"
     except Exception:  # noqa: BLE001 - no amd-smi and no amdgpu sysfs
-        live = []
-    if not any(b is not None for b in live):
-        source = "synthetic"
-    busy = [(live[i % len(live)] if live and live[i % len(live)] is not None else (i * 13) % 100)
-            for i in range(nodes)]
+        hs = None
+    if start_load is None and sampler is None and _cuda_available():
+        from ..tools.tlp_live import copy_loop_load as start_load
+    idle_gfx = idle_umc = busy_gfx = busy_umc = None
+    source = "synthetic"
+    if hs is not None:
+        idle_gfx, idle_umc, source = _mean_activity(hs, min(0.5, seconds))
+        if start_load is not None and idle_gfx is not None:
+            end = start_load()
+            try:
+                time.sleep(0.3)  # the activity counters ramp over a few samples
+                busy_gfx, busy_umc, _ = _mean_activity(hs, seconds)
+            finally:
+                end()
+    half = nodes // 2
+    if idle_gfx is None:
+        busy = [float((i * 13) % 100) for i in range(nodes)]
+        hbm = [None] * nodes
+    else:
+        loaded = busy_gfx if busy_gfx is not None else idle_gfx
+        busy = [idle_gfx if i < half else loaded for i in range(nodes)]
+        hbm = [idle_umc if i < half else (busy_umc if busy_gfx is not None else idle_umc) for i in range(nodes)]
     store = Store()
     store.create_many("nodes", json.dumps([mi355x_node(f"mi355x-{i}") for i in range(nodes)]))
     c = LocalClient(store)
     for i in range(nodes):
         t = NodeTelemetry(f"mi355x-{i}", source=source)
-        bw = hbm[i % len(hbm)] if hbm else None
-        t.add(Sample(time.time(), None, None, float(busy[i]), None, bw))
+        t.add(Sample(time.time(), None, None, float(busy[i]), None, hbm[i]))
         publish(c, t.watcher_metrics())
     cfg = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
            "profiles": [{"schedulerName": "default-scheduler", "plugins": {
@@ -263,11 +309,17 @@ def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None) -> dict:
         dt = time.perf_counter() - t0
     finally:
         s.stop()
-    return {"pods_per_s": round(pods / dt, 1) if ok else None, "metrics_source": source,
-            "node_gpu_busy_pct": busy,
-            "node_hbm_bandwidth_pct": [hbm[i % len(hbm)] for i in range(nodes)] if hbm else None,
-            "first_gpu_pod_node": first.get("selected"),
-            "tlp_scores": {n: v["TargetLoadPacking*1"] for n, v in (first.get("scores") or {}).items()}}
+    scores = {n: v["TargetLoadPacking*1"] for n, v in (first.get("scores") or {}).items()}
+    out = {"pods_per_s": round(pods / dt, 1) if ok else None, "metrics_source": source,
+           "node_gpu_busy_pct": busy, "node_hbm_bandwidth_pct": hbm,
+           "first_gpu_pod_node": first.get("selected"), "tlp_scores": scores}
+    if busy_gfx is not None:
+        idle_s = [scores[f"mi355x-{i}"] for i in range(half)]
+        busy_s = [scores[f"mi355x-{i}"] for i in range(half, nodes)]
+        out["live_load"] = {"idle_gpu_busy_pct": idle_gfx, "loaded_gpu_busy_pct": busy_gfx,
+                            "loaded_nodes": [f"mi355x-{i}" for i in range(half, nodes)],
+                            "busy_scores_below_idle": max(busy_s) < min(idle_s)}
+    return out
 
 
 ALL = {"coscheduling_cpu": coscheduling_cpu, "flexgpu_cpx_quarter": flexgpu_cpx_quarter, "gang8_xgmi": gang8_xgmi,

@@ -26,7 +26,8 @@ def test_bench_multi_rank_gloo(n):
     env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(n),
-           "--steps", "2", "--warmup", "1", "--nodes", "8", "--no-gpu-probe", "--no-scenarios", "--no-open-loop"]
+           "--steps", "2", "--warmup", "1", "--nodes", "8", "--waves-per-step", "2", "--no-gpu-probe",
+           "--no-scenarios", "--no-open-loop", "--no-service-mode"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
@@ -49,7 +50,7 @@ def test_bench_launches_its_own_ranks():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--nodes", "8",
-           "--no-gpu-probe", "--no-scenarios", "--cpus", "none"]
+           "--waves-per-step", "2", "--no-gpu-probe", "--no-scenarios", "--no-service-mode", "--cpus", "none"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
@@ -65,6 +66,10 @@ def test_bench_launches_its_own_ranks():
     # Untimed open-loop admission latency, by interleaved gang type.
     ol = d["config"]["gang_admit_open_loop"]
     assert ol["capacity_pods_per_s"] > 0
+    # The frozen search logs one trial per rate, with its gang denials.
+    assert ol["capacity_search"] and all({"offered_pods_per_s", "served", "denied_gangs", "denial_causes"}
+                                         <= set(t) for t in ol["capacity_search"])
+    assert len(d["config"]["per_rank"]["pods_per_s"]) == 2
     for load in ("load_50", "load_90"):
         assert set(ol[load]["by_gang"]) <= {"1", "2", "4", "8", "cpx4"} and ol[load]["gangs"] > 0
     assert "cpx4" in d["config"]["gang_admit_by_type"]
@@ -75,3 +80,44 @@ def test_bench_refuses_world_size_mismatch():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "1"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+@pytest.mark.slow
+def test_bench_eight_ranks_self_launched_gloo():
+    """The 8-GPU shape of the driver's scaling run, rehearsed on CPU: `python
+    bench.py --gpus 8` starts 8 ranks itself (GPUs counted from sysfs, no HIP
+    in the parent), every rank reports its own rate, and the placement check
+    fills the 1/2/4/8 gang rows with correct all-reduces on the placed ranks."""
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "8", "--steps", "1", "--warmup", "1", "--nodes", "4",
+           "--waves-per-step", "1", "--no-gpu-probe", "--no-scenarios", "--no-open-loop", "--no-service-mode",
+           "--cpus", "none"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"].startswith("8 rank")
+    pr = d["config"]["per_rank"]
+    assert len(pr["pods_per_s"]) == 8 and min(pr["pods_per_s"]) > 0 and pr["spread"] >= 0
+    assert "independent" in d["config"]["value_kind"]
+    pl = d["config"]["rccl_placement"]
+    assert "error" not in pl, pl
+    assert [g["gang"] for g in pl["gangs"]] == [1, 2, 4, 8]
+    for g in pl["gangs"][1:]:
+        assert len(g["ordinals"]) == g["gang"] and sorted(g["placed"]["ranks"]) == sorted(g["ordinals"])
+        assert all(x["correct"] for x in g["placed"]["results"])
+        assert pl["summary"][str(g["gang"])]["all_correct"]
+
+
+def test_visible_gpu_count_honours_visibility_lists(tmp_path):
+    from flex_gpu_scheduler_amd.gpu.discovery import visible_gpu_count
+
+    assert visible_gpu_count(str(tmp_path), env={}) == 0  # no sysfs: unknown, not a refusal
+    root = os.path.join(ROOT, "tests", "fixtures", "mi355x_box", "root")
+    n = visible_gpu_count(root, env={})
+    assert n >= 1
+    assert visible_gpu_count(root, env={"HIP_VISIBLE_DEVICES": "0"}) == 1
+    assert visible_gpu_count(root, env={"ROCR_VISIBLE_DEVICES": "0,1,2", "HIP_VISIBLE_DEVICES": "0"}) == min(3, n)
