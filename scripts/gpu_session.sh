@@ -1,25 +1,32 @@
 #!/usr/bin/env bash
-# Round-3 box session. Usage: bash scripts/gpu_r3.sh TAG step [step ...]
-# steps: pytest smoke bench bench3 pmc sched500 sched5000 remote sample_pre sample_sched sample_bench rocprof
+# One MI355X box session. Usage: bash scripts/gpu_session.sh TAG step [step ...]
+# steps: pytest smoke bench bench3 nodes1024 pmc sched500 sched5000 remote sample_pre sample_sched
+#        sample_bench rocprof
 # Every GPU step runs under its own time limit; the script stops at the first
-# failure (no retries).
+# failure (no retries). A heartbeat line every 60 s keeps long steps visible.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=$1; shift
 OUT=gpurun_out/$tag
 mkdir -p "$OUT"
+( while sleep 60; do echo "[$tag] heartbeat $(date +%T)"; done ) &
+hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
 for step in "$@"; do
   echo "[$tag] $step $(date +%T)"
   case $step in
     pytest) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
               > "$OUT/pytest_gpu.txt" 2>&1 ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 ;;
-    bench) timeout -k 10 300 python bench.py > "$OUT/bench1.json" 2> "$OUT/bench1.err" ;;
+    bench) timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench1.json" \
+             2> "$OUT/bench1.err" ;;
     bench3) for i in 1 2 3; do
-              timeout -k 10 200 python bench.py --no-scenarios --no-placement > "$OUT/bench64_$i.json" \
-                2> "$OUT/bench64_$i.err" || exit $?
+              timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-scenarios --no-placement \
+                --no-service-mode > "$OUT/bench64_$i.json" 2> "$OUT/bench64_$i.err" || exit $?
             done ;;
+    nodes1024) timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
+                 --no-service-mode > "$OUT/bench_nodes_1024.json" 2> "$OUT/bench_nodes_1024.err" ;;
     pmc) OUTDIR="$OUT" bash scripts/pmc_round.sh ;;
     sched500) timeout -k 10 400 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 500 --pods 1000 \
                 --cpus l3 > "$OUT/sched_perf_500.jsonl" 2>&1 ;;
@@ -47,7 +54,8 @@ for step in "$@"; do
       # Kernel trace + per-kernel stats of one short bench run (the probe,
       # health, MFMA and placement kernels on the GPU path).
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_bench" -o bench -- \
-        python3 bench.py --steps 5 --warmup 1 --no-open-loop --no-scenarios > "$OUT/rocprof_bench.log" 2>&1 ;;
+        python3 bench.py --steps 5 --warmup 1 --no-open-loop --no-scenarios --no-service-mode \
+        > "$OUT/rocprof_bench.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
