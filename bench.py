@@ -213,8 +213,8 @@ def main() -> int:
         extras["gang_admit_open_loop"] = {
             "burst_capacity_pods_per_s": round(burst, 1),
             "capacity_pods_per_s": round(cap, 1),
-            "capacity_rule": "highest x1.3-step rate (+2 bisection steps) served with every gang bound and "
-                             "p99 PG-create->last-Bind <= 25 ms; one trial per rate",
+            "capacity_rule": "highest x1.3-step rate (+2 bisection steps) whose p99 PG-create->last-Bind over "
+                             "all gangs (unbound = infinite) is <= 25 ms; one trial per rate",
             "capacity_search": search,
             **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed + 1)
                for f in (0.5, 0.9) if cap > 0}}
