@@ -438,8 +438,29 @@ namespace {
 
 constexpr size_t kMaxBody = 256u << 20;
 
-// 0: ok, -1: connection closed, >0: HTTP error to send before closing.
-int read_request(Server::Conn& c, Server::Request& r) {
+// Chunk-size line of a chunked body: 1-15 hex digits, optionally followed by
+// ";extensions". False for anything else (an overlong or non-hex size is a
+// malformed request, not a huge allocation).
+bool parse_chunk_size(const std::string& line, size_t* out) {
+  size_t v = 0, i = 0;
+  for (; i < line.size() && i < 16; ++i) {
+    char ch = line[i];
+    int d = ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
+    if (d < 0) break;
+    v = v * 16 + static_cast<size_t>(d);
+  }
+  if (i == 0 || i > 15) return false;
+  if (i < line.size() && line[i] != ';' && line[i] != ' ' && line[i] != '\t') return false;
+  *out = v;
+  return true;
+}
+
+bool open_path(const std::string& path) { return path == "/healthz" || path == "/readyz" || path == "/livez" || path == "/version"; }
+
+// 0: ok, -1: connection closed, >0: HTTP error to send before closing. With
+// a bearer `token`, a request without it is refused (401) before its body is
+// read: an unauthenticated client cannot make the server buffer 256 MiB.
+int read_request(Server::Conn& c, Server::Request& r, const std::string& token) {
   r.query.clear();
   r.content_type.clear();
   r.authorization.clear();
@@ -489,17 +510,19 @@ int read_request(Server::Conn& c, Server::Request& r) {
     }
   }
   r.body.clear();
+  if (!token.empty() && !open_path(r.path) && r.authorization != "Bearer " + token) return 401;
   if (chunked) {
     for (;;) {
       if (!c.line(line)) return -1;
-      size_t sz = std::strtoull(line.c_str(), nullptr, 16);
+      size_t sz = 0;
+      if (!parse_chunk_size(line, &sz)) return 400;
       if (sz == 0) {
         do {
           if (!c.line(line)) return -1;
         } while (!line.empty());
         break;
       }
-      if (r.body.size() + sz > kMaxBody) return 413;
+      if (sz > kMaxBody - r.body.size()) return 413;
       if (!c.exact(sz, r.body) || !c.line(line)) return -1;
     }
   } else if (content_length > 0) {
@@ -707,10 +730,12 @@ void Server::serve(int fd) {
     }
   }
   for (;;) {
-    int rc = read_request(c, r);
+    int rc = read_request(c, r, opts_.token);
     if (rc < 0) break;
     if (rc > 0) {
-      respond_json(c, rc, status_obj(rc, "BadRequest", "malformed request"), false);
+      const char* reason = rc == 401 ? "Unauthorized" : rc == 413 ? "RequestEntityTooLarge" : "BadRequest";
+      const char* msg = rc == 401 ? "Unauthorized" : rc == 413 ? "request body too large" : "malformed request";
+      respond_json(c, rc, status_obj(rc, reason, msg), false);
       break;
     }
     if (!handle(c, r) || stopping_) break;

@@ -646,6 +646,8 @@ PYBIND11_MODULE(_xsched, m) {
               e["assumed_held"] = d.assumed_held;
               e["store_free"] = d.store_free;
               e["store_max_node_free"] = d.store_max_node_free;
+              e["waiting_at_permit"] = d.waiting_at_permit;
+              e["in_binding"] = d.in_binding;
               out.append(e);
             }
             return py::make_tuple(total, out);

@@ -788,6 +788,8 @@ void Scheduler::note_gang_denied(const Pod& p, const char* why) {
   auto pg = informers_->pod_group_of(p);
   d.min_member = pg ? pg->min_member : 0;
   d.assigned = cache_->assigned_in_group(p.pg_key);
+  for (const auto& w : waiting_) d.waiting_at_permit += static_cast<int>(w->size());
+  d.in_binding = std::max(0, inflight_.load() - d.waiting_at_permit);
   d.need_gpus = p.gpu_demand.kind == GpuDemand::Gpu ? p.gpu_demand.amount : 0;
   std::unordered_map<std::string, int> spx;
   for (const auto& r : cache_->gpu_census()) {
@@ -819,12 +821,16 @@ void Scheduler::note_gang_denied(const Pod& p, const char* why) {
       d.store_max_node_free = std::max(d.store_max_node_free, f);
     }
   }
-  // The gang still needed (min_member - assigned) more whole GPUs.
+  // The gang still needed (min_member - assigned) more whole GPUs. GPUs free
+  // in the store are either truly taken by pods in flight (waiting at Permit
+  // or being bound: not yet bound in the store) or seen as used only by a
+  // cache that has not observed the deletions yet.
   const int64_t missing = d.need_gpus * std::max(0, d.min_member - d.assigned);
+  const int64_t in_flight = d.waiting_at_permit + d.in_binding;
   if (d.need_gpus == 0) d.cause = "not_whole_gpu";
   else if (d.store_free < 0) d.cause = "unknown";
   else if (d.store_free < missing) d.cause = "capacity";
-  else if (d.store_free - d.assumed_held < missing) d.cause = "held_by_waiting_gangs";
+  else if (d.store_free - in_flight < missing) d.cause = "held_by_gangs_in_flight";
   else if (d.cache_free < missing) d.cause = "stale_cache";
   else d.cause = "placement";
   std::lock_guard<std::mutex> g(stats_mu_);

@@ -130,6 +130,7 @@ struct GangDenial {
   int64_t need_gpus = 0;  // whole GPUs per member
   int cache_free = 0, cache_max_node_free = 0, assumed_held = 0;
   int store_free = -1, store_max_node_free = -1;
+  int waiting_at_permit = 0, in_binding = 0;  // assumed pods by stage
 };
 
 class Scheduler {

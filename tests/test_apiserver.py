@@ -233,3 +233,53 @@ def test_workqueue_dedup_and_rate_limit():
     th.start()
     assert q.get() is None
     th.join()
+
+
+def _raw(url: str, payload: bytes) -> bytes:
+    import socket
+    from urllib.parse import urlparse
+
+    u = urlparse(url)
+    with socket.create_connection((u.hostname, u.port), timeout=5) as s:
+        s.sendall(payload)
+        out = b""
+        while True:
+            chunk = s.recv(65536)
+            if not chunk:
+                break
+            out += chunk
+        return out
+
+
+def test_native_http_rejects_oversized_and_malformed_chunks(store):
+    """A chunk size near 2**64 used to wrap the size check and make the
+    server read forever; it is 413 now, and a non-hex size line is 400."""
+    srv = ApiServer(store, native_http=True).start()
+    try:
+        head = b"POST /api/v1/namespaces/default/pods HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+        out = _raw(srv.url, head + b"ffffffffffffffff\r\n")
+        assert out.startswith(b"HTTP/1.1 400"), out[:80]  # 16 hex digits: more than any body
+        out = _raw(srv.url, head + b"fffffffffffffff\r\n")
+        assert out.startswith(b"HTTP/1.1 413"), out[:80]
+        out = _raw(srv.url, head + b"zz\r\n")
+        assert out.startswith(b"HTTP/1.1 400"), out[:80]
+        # A well-formed chunked create still works.
+        body = json.dumps(make_pod("chunked")).encode()
+        head_close = head.replace(b"Host: x\r\n", b"Host: x\r\nConnection: close\r\n")
+        out = _raw(srv.url, head_close + b"%x\r\n" % len(body) + body + b"\r\n0\r\n\r\n")
+        assert out.startswith(b"HTTP/1.1 201"), out[:120]
+    finally:
+        srv.stop()
+
+
+def test_native_http_refuses_unauthenticated_body_before_reading_it(store):
+    srv = ApiServer(store, native_http=True, token="s3cret").start()
+    try:
+        # Claims a 200 MiB body and sends none: answered 401 at once.
+        out = _raw(srv.url, b"POST /api/v1/namespaces/default/pods HTTP/1.1\r\nHost: x\r\n"
+                            b"Content-Length: 209715200\r\n\r\n")
+        assert out.startswith(b"HTTP/1.1 401"), out[:80]
+        out = _raw(srv.url, b"GET /healthz HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+        assert out.startswith(b"HTTP/1.1 200")
+    finally:
+        srv.stop()
