@@ -86,6 +86,10 @@ struct Handle {
   // Coscheduling denied `member`'s group (`why`: postfilter | unreserve |
   // minresources); the scheduler keeps a diagnostic record. Optional.
   std::function<void(const Pod& member, const char* why)> gang_denied;
+  // Bracket a long wait inside a binding-cycle extension point (PreBind):
+  // the binder pool adds a worker for the duration, so waiting pods cannot
+  // starve the bindings of unrelated pods. Optional.
+  std::function<void()> blocking_begin, blocking_end;
   // HTTP extenders of the configuration (preemption's callExtenders) and the
   // informer store's objects they are sent.
   const std::vector<std::shared_ptr<Extender>>* extenders = nullptr;

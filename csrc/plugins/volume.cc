@@ -672,7 +672,21 @@ class VolumeBinding : public Plugin {
       revert(rest);
       return Status::error(e.what());
     }
-    // checkBindings until the PV controller has finished (wait.Poll).
+    // checkBindings until the PV controller has finished (wait.Poll). The
+    // wait can last bindTimeoutSeconds: it holds a binder thread, so the
+    // pool is told (upstream blocks one goroutine per pod instead).
+    std::string err0;
+    if (check_bindings(*p, node, pv, &err0) && err0.empty()) return {};
+    if (!err0.empty()) return Status::error("binding volumes: " + err0);
+    struct Blocking {
+      const Handle& h;
+      explicit Blocking(const Handle& hh) : h(hh) {
+        if (h.blocking_begin) h.blocking_begin();
+      }
+      ~Blocking() {
+        if (h.blocking_end) h.blocking_end();
+      }
+    } blocking(h_);
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(bind_timeout_us_);
     for (;;) {
       std::string err;

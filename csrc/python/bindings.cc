@@ -608,6 +608,7 @@ PYBIND11_MODULE(_xsched, m) {
              d["eq_filter_hits"] = st.eq_filter_hits;
              d["eq_filter_misses"] = st.eq_filter_misses;
              d["inflight_bindings"] = s.inflight_bindings();
+             d["bind_threads"] = s.bind_threads();
              return d;
            })
       .def(

@@ -98,35 +98,58 @@ bool Executor::try_pop(std::function<void()>& fn) {
 
 Executor::Executor(int threads) {
   if (const char* e = std::getenv("XSCHED_BIND_SPIN_NS")) spin_ns_ = std::max<int64_t>(0, std::atoll(e));
-  for (int i = 0; i < std::max(1, threads); ++i) {
-    threads_.emplace_back([this] {
-      name_this_thread("xs-bind");
-      bool spin = false;  // just finished a task: poll before sleeping
-      for (;;) {
-        std::function<void()> fn;
-        if (spin && spin_ns_ > 0) {
-          if (spinners_.fetch_add(1) < kMaxSpinners) {
-            const int64_t until = Parallelizer::now_ns() + spin_ns_;
-            while (queued_.load(std::memory_order_relaxed) == 0 && Parallelizer::now_ns() < until)
-              __builtin_ia32_pause();
-          }
-          // Leave the spinner set before the locked check below: a submit
-          // that still saw this spinner finds its task taken here.
-          spinners_.fetch_sub(1);
+  base_ = std::max(1, threads);
+  std::lock_guard<std::mutex> g(mu_);
+  for (int i = 0; i < base_; ++i) spawn_locked();
+}
+
+void Executor::spawn_locked() {
+  threads_.emplace_back([this] {
+    name_this_thread("xs-bind");
+    bool spin = false;  // just finished a task: poll before sleeping
+    for (;;) {
+      std::function<void()> fn;
+      if (spin && spin_ns_ > 0) {
+        if (spinners_.fetch_add(1) < kMaxSpinners) {
+          const int64_t until = Parallelizer::now_ns() + spin_ns_;
+          while (queued_.load(std::memory_order_relaxed) == 0 && Parallelizer::now_ns() < until)
+            __builtin_ia32_pause();
         }
-        {
-          std::unique_lock<std::mutex> lk(mu_);
-          if (!try_pop(fn)) {
-            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-            if (!try_pop(fn)) return;  // stop_ and drained
-          }
-        }
-        fn();
-        busy_.fetch_sub(1);
-        spin = true;
+        // Leave the spinner set before the locked check below: a submit
+        // that still saw this spinner finds its task taken here.
+        spinners_.fetch_sub(1);
       }
-    });
-  }
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        if (!try_pop(fn)) {
+          cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+          if (!try_pop(fn)) return;  // stop_ and drained
+        }
+      }
+      fn();
+      busy_.fetch_sub(1);
+      spin = true;
+    }
+  });
+}
+
+void Executor::enter_blocking() {
+  std::lock_guard<std::mutex> g(mu_);
+  ++blocked_;
+  // Keep `base_` workers able to run tasks (Go's runtime hands a P to a new
+  // M when a goroutine blocks in a syscall): the pool grows to the
+  // high-water mark of concurrently blocked tasks, capped.
+  if (!stop_ && static_cast<int>(threads_.size()) - blocked_ < base_ && threads_.size() < kMaxThreads) spawn_locked();
+}
+
+void Executor::exit_blocking() {
+  std::lock_guard<std::mutex> g(mu_);
+  --blocked_;
+}
+
+size_t Executor::threads() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return threads_.size();
 }
 
 Executor::~Executor() { stop(); }
@@ -149,7 +172,12 @@ void Executor::stop() {
     stop_ = true;
   }
   cv_.notify_all();
-  for (auto& t : threads_) t.join();
+  std::vector<std::thread> ts;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ts.swap(threads_);  // no spawn after stop_
+  }
+  for (auto& t : ts) t.join();
 }
 
 size_t Executor::pending() const {
@@ -261,6 +289,12 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.timers = timers_.get();
     h.activate = [this](const std::vector<PodPtr>& pods) { queue_->activate(pods); };
     h.gang_denied = [this](const Pod& p, const char* why) { note_gang_denied(p, why); };
+    h.blocking_begin = [this] {
+      if (binder_) binder_->enter_blocking();
+    };
+    h.blocking_end = [this] {
+      if (binder_) binder_->exit_blocking();
+    };
     h.metrics = metrics_.get();
     h.snapshot = &snapshot_;
     h.extenders = &extenders_;

@@ -72,6 +72,12 @@ class Executor {
   void submit(std::function<void()> fn);
   void stop();
   size_t pending() const;
+  // A task about to block for a long time (VolumeBinding's PreBind waiting
+  // for the PV controller) brackets the wait with these, so blocked tasks
+  // never take the pool's last runnable workers (BlockingScope below).
+  void enter_blocking();
+  void exit_blocking();
+  size_t threads() const;
 
  private:
   // A worker that finishes a task spins briefly on `queued_` before it
@@ -82,6 +88,10 @@ class Executor {
   static constexpr int kMaxSpinners = 2;
   int64_t spin_ns_ = kSpinNs;
   bool try_pop(std::function<void()>& fn);  // under mu_
+  void spawn_locked();
+  static constexpr size_t kMaxThreads = 1024;
+  int base_ = 1;
+  int blocked_ = 0;  // under mu_
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
@@ -191,6 +201,7 @@ class Scheduler {
   // their census; `total` counts all of them).
   std::vector<GangDenial> gang_denials(bool clear = false, uint64_t* total = nullptr);
   size_t inflight_bindings() const { return inflight_.load(); }
+  size_t bind_threads() const { return binder_ ? binder_->threads() : 0; }
 
  private:
   struct ScheduleResult {

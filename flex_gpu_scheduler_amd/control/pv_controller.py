@@ -205,9 +205,17 @@ class PersistentVolumeController(_Controller):
         pv_name = pv["metadata"]["name"]
         ref = (pv.get("spec") or {}).get("claimRef") or {}
         if not ref.get("uid"):
-            self.client.patch("persistentvolumes", "", pv_name, {"spec": {"claimRef": {
-                "kind": "PersistentVolumeClaim", "apiVersion": "v1", "namespace": ns, "name": name,
-                "uid": md.get("uid", "")}}})
+            # Conditional on the version _find_matching saw (a merge patch
+            # carrying metadata.resourceVersion is a precondition): with
+            # several workers two claims can pick the same free volume; the
+            # loser gets a 409, its sync fails and the claim is requeued to
+            # look again (upstream's assume cache plays this role).
+            patch = {"spec": {"claimRef": {"kind": "PersistentVolumeClaim", "apiVersion": "v1", "namespace": ns,
+                                           "name": name, "uid": md.get("uid", "")}}}
+            rv = (pv.get("metadata") or {}).get("resourceVersion")
+            if rv:
+                patch["metadata"] = {"resourceVersion": rv}
+            pv = self.client.patch("persistentvolumes", "", pv_name, patch)
         if (pv.get("status") or {}).get("phase") != "Bound":
             self.client.patch("persistentvolumes", "", pv_name, {"status": {"phase": "Bound"}})
         ann = md.get("annotations") or {}

@@ -295,3 +295,49 @@ def test_pods_without_volumes_skip_the_volume_filters(store):
     out = s.explain(make_pod("p", requests={"cpu": "100"}))  # fails NodeResourcesFit only
     assert out["filtered"]["n0"]["plugin"] == "NodeResourcesFit"
     s.stop()
+
+
+def test_prebind_waits_do_not_starve_other_bindings(store):
+    """More pods whose claims never bind than there are binder workers: each
+    VolumeBinding PreBind waits (no PV controller runs), the pool adds a worker
+    per blocked wait, and an unrelated pod still binds at once (upstream
+    blocks one goroutine per pod, vendor/k8s.io/kubernetes/pkg/scheduler/
+    framework/plugins/volumebinding/binder.go BindPodVolumes)."""
+    store.create("nodes", node("n0"))
+    store.create("storageclasses", sc("fast", provisioner="nvme.csi.amd.com"))
+    cfg = {**V1B2, "profiles": [{"schedulerName": "default-scheduler", "pluginConfig": [
+        {"name": "VolumeBinding", "args": {"bindTimeoutSeconds": 3}}]}]}
+    s = new_scheduler(store, load_config(cfg), start=True, bindWorkers=4)
+    try:
+        for i in range(10):
+            store.create("persistentvolumeclaims", pvc(f"scratch-{i}", size="1Gi", cls="fast"))
+            store.create("pods", with_claims(make_pod(f"vol-{i}", requests={"cpu": "100m"}), f"scratch-{i}"))
+        wait_for(lambda: s.stats()["inflight_bindings"] >= 10, timeout=5)
+        assert s.stats()["bind_threads"] >= 4 + 10 - 1
+        t0 = time.time()
+        store.create("pods", make_pod("plain", requests={"cpu": "100m"}))
+        wait_for(lambda: placements(store).get("plain") == "n0", timeout=2)
+        assert time.time() - t0 < 1.0
+    finally:
+        s.stop()
+
+
+def test_pv_controller_claimref_patch_is_conditional(store):
+    """Two claims that both saw one free volume: the second claimRef patch
+    carries the version it matched against, fails with 409 (its sync is
+    retried), and the volume stays bound to the first claim."""
+    from flex_gpu_scheduler_amd.control.client import ApiException
+
+    client = LocalClient(store)
+    ctl = PersistentVolumeController(client)
+    store.create("storageclasses", sc("imm", mode="Immediate"))
+    store.create("persistentvolumes", pv("only", cls="imm"))
+    a = store.create("persistentvolumeclaims", pvc("a", cls="imm"))
+    b = store.create("persistentvolumeclaims", pvc("b", cls="imm"))
+    stale = client.get("persistentvolumes", "", "only")
+    ctl._bind(stale, a)
+    with pytest.raises(ApiException) as ei:
+        ctl._bind(stale, b)
+    assert ei.value.code == 409
+    vol = client.get("persistentvolumes", "", "only")
+    assert vol["spec"]["claimRef"]["name"] == "a"
