@@ -762,6 +762,7 @@ PYBIND11_MODULE(_xsched, m) {
            },
            py::arg("pod"), py::arg("iterations") = 100)
       .def("metrics_text", [](Scheduler& s) { return s.metrics().expose(); })
+      .def("loop_age_seconds", &Scheduler::loop_age_seconds)
       .def("set_trace", [](Scheduler& s, bool on) { s.tracer().enable(on); })
       .def("trace_json", [](Scheduler& s) { return s.tracer().chrome_json(); })
       .def("clear_trace", [](Scheduler& s) { s.tracer().clear(); })

@@ -78,6 +78,10 @@ const Def kDefs[] = {
     {"scheduler_preemption_victims", "histogram", "Number of selected preemption victims", 1, 2, 7},
     {"scheduler_preemption_attempts_total", "counter", "Total preemption attempts in the cluster till now", 0, 0, 0},
     {"scheduler_pending_pods", "gauge", "Number of pending pods, by the queue type.", 0, 0, 0},
+    {"scheduler_scheduler_goroutines", "gauge",
+     "Number of running goroutines split by the work they do such as binding.", 0, 0, 0},
+    {"scheduler_scheduler_cache_size", "gauge", "Number of nodes, pods, and assumed (bound) pods in the scheduler cache.",
+     0, 0, 0},
     {"scheduler_queue_incoming_pods_total", "counter",
      "Number of pods added to scheduling queues by event and queue type.", 0, 0, 0},
     {"xsched_gang_admit_seconds", "histogram",

@@ -369,6 +369,15 @@ void Scheduler::start() {
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"active\"", static_cast<double>(c.active));
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"backoff\"", static_cast<double>(c.backoff));
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"unschedulable\"", static_cast<double>(c.unschedulable));
+    // Upstream metrics.go:102 (Goroutines, by work) and :171 (CacheSize).
+    int waiting = 0;
+    for (const auto& w : waiting_) waiting += static_cast<int>(w->size());
+    const int inflight = inflight_.load();
+    metrics_->set_gauge("scheduler_scheduler_goroutines", "work=\"binding\"", static_cast<double>(std::max(0, inflight - waiting)));
+    metrics_->set_gauge("scheduler_scheduler_goroutines", "work=\"permit\"", static_cast<double>(waiting));
+    metrics_->set_gauge("scheduler_scheduler_cache_size", "type=\"assumed_pods\"", static_cast<double>(cache_->assumed_count()));
+    metrics_->set_gauge("scheduler_scheduler_cache_size", "type=\"pods\"", static_cast<double>(cache_->pod_count()));
+    metrics_->set_gauge("scheduler_scheduler_cache_size", "type=\"nodes\"", static_cast<double>(cache_->node_count()));
   }));
   informer_thread_ = std::thread([this] {
     name_this_thread("xs-informer");
@@ -883,8 +892,16 @@ std::vector<GangDenial> Scheduler::gang_denials(bool clear, uint64_t* total) {
 }
 
 // -------------------------------------------------------- scheduling ----
+double Scheduler::loop_age_seconds() const {
+  int64_t t = loop_tick_us_.load(std::memory_order_relaxed);
+  if (!t || !running_.load()) return 0.0;
+  return static_cast<double>(RealClock().now_us() - t) / 1e6;
+}
+
 void Scheduler::scheduling_loop() {
+  RealClock rc;
   while (running_.load()) {
+    loop_tick_us_.store(rc.now_us(), std::memory_order_relaxed);
     auto qpi = queue_->pop(100);
     if (!qpi) continue;
     std::lock_guard<std::mutex> g(sched_mu_);

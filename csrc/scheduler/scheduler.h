@@ -202,6 +202,9 @@ class Scheduler {
   std::vector<GangDenial> gang_denials(bool clear = false, uint64_t* total = nullptr);
   size_t inflight_bindings() const { return inflight_.load(); }
   size_t bind_threads() const { return binder_ ? binder_->threads() : 0; }
+  // Seconds since the scheduling loop last ticked (it ticks at least every
+  // 100 ms while running; /healthz uses this). 0 before start().
+  double loop_age_seconds() const;
 
  private:
   struct ScheduleResult {
@@ -345,6 +348,7 @@ class Scheduler {
   std::mutex sched_mu_;  // serializes scheduling cycles (loop vs schedule_one)
   std::atomic<int> inflight_{0};
   std::atomic<int> in_cycle_{0};
+  std::atomic<int64_t> loop_tick_us_{0};  // RealClock time of the last loop iteration
   int next_start_node_ = 0;
   std::mt19937_64 rng_;
   std::vector<uint64_t> timer_ids_;

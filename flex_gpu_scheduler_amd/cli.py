@@ -236,6 +236,19 @@ def cmd_scheduler(args) -> int:
     http.add_route("GET", "/debug/cache/compare", lambda q, b: (200, "application/json", rs.scheduler.check_cache()))
     http.add_route("GET", "/debug/cache/dump", lambda q, b: (200, "application/json", rs.scheduler.dump_cache()))
     _on_sigusr2(rs.scheduler)
+    started = threading.Event()
+    stall_s = float(getattr(args, "healthz_stall_seconds", 30.0))
+
+    def loop_check() -> tuple[bool, str]:
+        # The scheduling loop ticks at least every 100 ms, idle or not: a
+        # cycle stuck in a plugin (or a dead loop thread) stops the ticks.
+        if not started.is_set():
+            return True, "not started"
+        age = rs.scheduler.loop_age_seconds()
+        return (age < stall_s, f"scheduling loop made no progress for {age:.1f}s")
+
+    http.add_health_check("scheduling-loop", loop_check)
+    http.add_health_check("informer-sync", lambda: (started.is_set(), "informers not synced yet"), ready_only=True)
     http.start()
     print(json.dumps({"scheduler": [p.scheduler_name for p in cfg.profiles], "metrics": http.url}), flush=True)
     stop = threading.Event()
@@ -244,11 +257,13 @@ def cmd_scheduler(args) -> int:
         for f in fetchers:
             f.start()
         rs.start()
+        started.set()
 
     if args.leader_elect or cfg.leader_elect:
         identity = f"{socket.gethostname()}_{os.getpid()}"
         le = LeaderElector(remote, args.lock_name or cfg.profiles[0].scheduler_name, args.lock_namespace, identity,
                            on_started_leading=lead, on_stopped_leading=stop.set)
+        http.add_health_check("leaderElection", le.healthz)
         threading.Thread(target=le.run, daemon=True).start()
         _wait_forever(stop)
         le.stop()
@@ -453,6 +468,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--leader-elect", action="store_true")
     p.add_argument("--lock-name")
     p.add_argument("--lock-namespace", default="kube-system")
+    p.add_argument("--healthz-stall-seconds", type=float, default=30.0,
+                   help="/healthz fails when the scheduling loop has not ticked for this long")
     p.add_argument("--trace", action="store_true", help="record per-cycle phase traces (/debug/trace)")
     p.add_argument("--cpu-affinity", default="none",
                    help="pin the scheduler's threads: none | l3 | l3xK | CPU list (utils/cpuaffinity.py)")

@@ -30,12 +30,15 @@ from __future__ import annotations
 import base64
 import copy
 import json
+import logging
 import re
 from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Any
 
 import yaml
+
+_log = logging.getLogger(__name__)
 
 API_VERSIONS = ("kubescheduler.config.k8s.io/v1beta2", "kubescheduler.config.k8s.io/v1beta3")
 EXT_POINTS = ("queueSort", "preFilter", "filter", "postFilter", "preScore", "score", "reserve", "permit",
@@ -571,6 +574,10 @@ def _resolve_profile(p: dict, api_version: str, available: set[str] | None, inde
         names = []
         for n, w in cur:
             if n in NOT_APPLICABLE:
+                # Upstream registers it (spreading the pods of one Service /
+                # ReplicaSet / StatefulSet, default_plugins.go:119-127 behind a
+                # feature gate); this scheduler has no such controllers' objects.
+                _log.warning('plugin "%s" (%s) is not implemented by this scheduler and is ignored', n, pt)
                 continue
             if n not in PLUGIN_POINTS:
                 raise ConfigError(f'plugin "{n}" does not exist')

@@ -22,13 +22,39 @@ class ServiceHTTP:
     def __init__(self, host: str = "127.0.0.1", port: int = 0):
         self.routes: dict[tuple[str, str], Route] = {}
         self.metrics_providers: list[Callable[[], str]] = []
-        self.add_route("GET", "/healthz", lambda q, b: (200, "text/plain", "ok"))
-        self.add_route("GET", "/readyz", lambda q, b: (200, "text/plain", "ok"))
+        # name -> () -> (ok, detail); /healthz (and /livez) fail when any
+        # check fails, /readyz also when a readiness check fails.
+        self.health_checks: dict[str, Callable[[], tuple[bool, str]]] = {}
+        self.ready_checks: dict[str, Callable[[], tuple[bool, str]]] = {}
+        self.add_route("GET", "/healthz", lambda q, b: self._health(q, self.health_checks))
+        self.add_route("GET", "/livez", lambda q, b: self._health(q, self.health_checks))
+        self.add_route("GET", "/readyz", lambda q, b: self._health(q, {**self.health_checks, **self.ready_checks}))
         self.add_route("GET", "/metrics", self._metrics)
         handler = type("Handler", (_Handler,), {"svc": self})
         self.httpd = ThreadingHTTPServer((host, port), handler)
         self.httpd.daemon_threads = True
         self._thread: threading.Thread | None = None
+
+    def add_health_check(self, name: str, fn: Callable[[], tuple[bool, str]], ready_only: bool = False) -> None:
+        (self.ready_checks if ready_only else self.health_checks)[name] = fn
+
+    @staticmethod
+    def _health(q: dict, checks: dict) -> tuple[int, str, str]:
+        """The apiserver healthz format: "ok", or one "[+]name ok" /
+        "[-]name failed: reason" line per check and a 500 when one fails
+        (with ?verbose the lines are shown on success too)."""
+        lines, ok = [], True
+        for name, fn in checks.items():
+            try:
+                good, detail = fn()
+            except Exception as e:  # noqa: BLE001
+                good, detail = False, f"check raised {type(e).__name__}: {e}"
+            ok &= good
+            lines.append(f"[+]{name} ok" if good else f"[-]{name} failed: {detail}")
+        if ok and "verbose" not in q:
+            return 200, "text/plain", "ok"
+        lines.append("healthz check passed" if ok else "healthz check failed")
+        return (200 if ok else 500), "text/plain", "\n".join(lines) + "\n"
 
     def add_route(self, method: str, path: str, fn: Route) -> None:
         self.routes[(method, path)] = fn

@@ -43,6 +43,7 @@ class LeaderElector:
         self._stop = threading.Event()
         self.is_leader = threading.Event()
         self.transitions_seen = 0
+        self.renewed_at = 0.0  # monotonic time of the last successful acquire/renew
 
     @property
     def leader(self) -> str:
@@ -90,7 +91,21 @@ class LeaderElector:
                 return False
             raise
         self._observe(spec)
+        self.renewed_at = time.monotonic()
         return True
+
+    def healthz(self, timeout: float = 20.0) -> tuple[bool, str]:
+        """HealthzAdaptor (client-go leaderelection/healthzadaptor.go): a
+        leader that has not renewed its lease within lease_duration +
+        `timeout` is unhealthy (kube-scheduler installs this check,
+        vendor/k8s.io/kubernetes/cmd/kube-scheduler/app/server.go:151-154).
+        Followers are healthy."""
+        if not self.is_leader.is_set():
+            return True, "not leading"
+        age = time.monotonic() - self.renewed_at
+        if age > self.lease_duration + timeout:
+            return False, f"failed election to renew leadership on lease {self.ns}/{self.name} ({age:.1f}s)"
+        return True, "leading"
 
     def release(self) -> None:
         """Give the lease up on clean shutdown (ReleaseOnCancel)."""

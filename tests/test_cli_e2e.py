@@ -150,3 +150,59 @@ def test_processes_schedule_a_gang(tmp_path):
     s2 = Store()
     assert restore(s2, data) >= 7
     assert all(p["spec"]["nodeName"] for p in s2.list("pods", "default")[0])
+
+
+def test_healthz_checks_fail_and_report():
+    from flex_gpu_scheduler_amd.control.httpserve import ServiceHTTP
+    import urllib.error
+    import urllib.request
+
+    http = ServiceHTTP().start()
+    state = {"ok": True}
+    http.add_health_check("loop", lambda: (state["ok"], "no progress for 31.0s"))
+    http.add_health_check("sync", lambda: (False, "not synced"), ready_only=True)
+    try:
+        assert urllib.request.urlopen(http.url + "/healthz").read() == b"ok"
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(http.url + "/readyz")
+        assert ei.value.code == 500 and b"[-]sync failed: not synced" in ei.value.read()
+        state["ok"] = False
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            urllib.request.urlopen(http.url + "/healthz")
+        body = ei.value.read()
+        assert ei.value.code == 500 and b"[-]loop failed: no progress" in body
+    finally:
+        http.stop()
+
+
+def test_leader_healthz_adaptor():
+    from flex_gpu_scheduler_amd.control.leaderelection import LeaderElector
+
+    le = LeaderElector(None, "l", "kube-system", "me", lease_duration=15.0, renew_deadline=10.0, retry_period=2.0)
+    assert le.healthz()[0]  # not leading
+    le.is_leader.set()
+    import time as _t
+
+    le.renewed_at = _t.monotonic()
+    assert le.healthz()[0]
+    le.renewed_at = _t.monotonic() - 40
+    ok, why = le.healthz()
+    assert not ok and "renew" in why
+
+
+def test_scheduler_loop_age_and_new_gauges(store):
+    import time as _t
+
+    from flex_gpu_scheduler_amd import load_config, new_scheduler
+
+    s = new_scheduler(store, load_config(None), start=True)
+    try:
+        _t.sleep(1.3)
+        assert 0 <= s.loop_age_seconds() < 1.0
+        text = s.metrics_text()
+        for line in ('scheduler_scheduler_goroutines{work="binding"}', 'scheduler_scheduler_cache_size{type="nodes"}',
+                     'scheduler_scheduler_cache_size{type="assumed_pods"}'):
+            assert line in text, line
+    finally:
+        s.stop()
+    assert s.loop_age_seconds() == 0.0

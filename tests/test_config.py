@@ -324,3 +324,17 @@ def test_flagship_config_uses_v1beta3_weights():
 
     w = load_config(flagship_config()).profiles[0].score_weights
     assert w["TaintToleration"] == 3 and w["NodeAffinity"] == 2 and w["NodeResourceTopologyMatch"] == 2
+
+
+def test_selector_spread_is_ignored_with_a_warning(caplog):
+    import logging
+
+    from flex_gpu_scheduler_amd import load_config
+
+    with caplog.at_level(logging.WARNING, logger="flex_gpu_scheduler_amd.config"):
+        c = load_config({"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
+                         "profiles": [{"schedulerName": "s", "plugins": {
+                             "preScore": {"enabled": [{"name": "SelectorSpread"}]},
+                             "score": {"enabled": [{"name": "SelectorSpread", "weight": 1}]}}}]})
+    assert "SelectorSpread" not in c.profiles[0].plugins["score"]
+    assert any("SelectorSpread" in r.getMessage() and "ignored" in r.getMessage() for r in caplog.records)
