@@ -181,6 +181,14 @@ class Plugin {
   // Periodic work registered at start (metrics refresh, cache cleanup).
   virtual void start() {}
   virtual void stop() {}
+  // Unit-test hook for plugin internals that are not an extension point
+  // (Scheduler::plugin_call; e.g. Coscheduling "checkClusterResource",
+  // CapacityScheduling "dryRunPreemption"). Returns {"error": ...} when unknown.
+  virtual Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) {
+    Json out = Json::object();
+    out.set("error", Json(name() + " has no debug call " + what));
+    return out;
+  }
 
  protected:
   std::string name_;

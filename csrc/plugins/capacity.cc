@@ -367,6 +367,29 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     return {{"Pod", kDelete, ""}, {"ElasticQuota", kAll, ""}};
   }
 
+  // Unit-test hook (capacity_scheduling_test.go:166 TestDryRunPreemption):
+  // the evaluator's dry run over every snapshot node, after PreFilter.
+  Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) override {
+    if (what != "dryRunPreemption") return Plugin::debug_call(what, s, p, args);
+    cur_state_ = &s;
+    std::vector<NodeInfoPtr> nodes = h_.snapshot->nodes;
+    auto cands = ev_.dry_run(s, *p, nodes, h_.informers->pdbs(), 0, static_cast<int>(nodes.size()));
+    cur_state_ = nullptr;
+    Json out = Json::object();
+    Json arr = Json::array();
+    for (const auto& c : cands) {
+      Json e = Json::object();
+      e.set("node", Json(c.node));
+      Json v = Json::array();
+      for (const auto& x : c.victims) v.push_back(Json(x->name()));
+      e.set("victims", std::move(v));
+      e.set("numPDBViolations", Json(static_cast<int64_t>(c.num_pdb_violations)));
+      arr.push_back(std::move(e));
+    }
+    out.set("candidates", std::move(arr));
+    return out;
+  }
+
  private:
   Handle& h_;
   Evaluator ev_;

@@ -349,6 +349,24 @@ class Coscheduling : public Plugin {
     return {{"Pod", kAdd, ""}, {"PodGroup", kAdd | kUpdate, ""}};
   }
 
+  // Unit-test hook (core/core_test.go:303 TestCheckClusterResource):
+  // args["need"] is a resource list; `p` names the group whose own pods count
+  // as free. "deny" puts p's group in the denied cache (core_test.go:42's
+  // pre-filled lastDeniedPG).
+  Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) override {
+    Json out = Json::object();
+    if (what == "checkClusterResource") {
+      out.set("enough", Json(check_cluster_resource(Res::from_json(args["need"]), *p)));
+      return out;
+    }
+    if (what == "deny") {
+      denied_.add(p->pg_key, denied_ttl_us_);
+      out.set("denied", Json(true));
+      return out;
+    }
+    return Plugin::debug_call(what, s, p, args);
+  }
+
  private:
   // True the first time (group uid, phase) is seen within kPatchMemoUs.
   static constexpr int64_t kPatchMemoUs = 60'000'000;

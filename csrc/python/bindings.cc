@@ -763,6 +763,18 @@ PYBIND11_MODULE(_xsched, m) {
            py::arg("pod"), py::arg("iterations") = 100)
       .def("metrics_text", [](Scheduler& s) { return s.metrics().expose(); })
       .def("loop_age_seconds", &Scheduler::loop_age_seconds)
+      .def(
+          "plugin_call",
+          [](Scheduler& s, const std::string& plugin, const std::string& point, py::handle args) {
+            Json a = json_arg(args);
+            Json out;
+            {
+              py::gil_scoped_release r;
+              out = s.plugin_call(plugin, point, a);
+            }
+            return to_py(out);
+          },
+          py::arg("plugin"), py::arg("point"), py::arg("args"))
       .def("set_trace", [](Scheduler& s, bool on) { s.tracer().enable(on); })
       .def("trace_json", [](Scheduler& s) { return s.tracer().chrome_json(); })
       .def("clear_trace", [](Scheduler& s) { s.tracer().clear(); })

@@ -1709,6 +1709,97 @@ Json Scheduler::dump_cache() const {
   return out;
 }
 
+namespace {
+Code code_from_name(const std::string& n) {
+  for (Code c : {Code::Success, Code::Error, Code::Unschedulable, Code::UnschedulableAndUnresolvable, Code::Wait,
+                 Code::Skip})
+    if (n == code_name(c)) return c;
+  throw std::runtime_error("unknown status code " + n);
+}
+Json status_json(const Status& st) {
+  Json out = Json::object();
+  out.set("code", Json(code_name(st.code())));
+  out.set("message", Json(st.message()));
+  return out;
+}
+}  // namespace
+
+Json Scheduler::plugin_call(const std::string& plugin, const std::string& point, const Json& args) {
+  std::lock_guard<std::mutex> g(sched_mu_);
+  Framework* fw = frameworks_.front().get();
+  if (args["schedulerName"].is_string()) fw = framework_for(args["schedulerName"].as_string());
+  if (!fw) throw std::runtime_error("no such profile");
+  Plugin* pl = nullptr;
+  for (const auto& x : fw->all_plugins())
+    if (x->name() == plugin) pl = x.get();
+  if (!pl) throw std::runtime_error("plugin " + plugin + " is not enabled in the profile");
+  cache_->update_snapshot(snapshot_);
+  auto state = std::make_shared<CycleState>();
+  state->write(kPodsToActivateKey, std::make_shared<PodsToActivate>());
+  auto parse = [&](const Json& j) {
+    auto p = Pod::from_json(j, *gpu_names_);
+    if (p->uid().empty()) p->meta.uid = "harness-" + p->key();
+    return p;
+  };
+  PodPtr pod = args.get("pod") ? parse(args["pod"]) : nullptr;
+  const std::string node = args["node"].str_or("");
+  if (point == "less") {
+    QueuedPodInfo a, b;
+    a.pod = parse(args["a"]);
+    b.pod = parse(args["b"]);
+    a.initial_attempt_wall = args["a_initial_attempt_us"].as_int(0);
+    b.initial_attempt_wall = args["b_initial_attempt_us"].as_int(0);
+    Json out = Json::object();
+    out.set("less", Json(pl->less(a, b)));
+    return out;
+  }
+  if (!pod) throw std::runtime_error("args.pod is required");
+  if (point == "preFilter") return status_json(pl->pre_filter(*state, *pod));
+  if (point == "postFilter") {
+    NodeStatusMap m;
+    for (const auto& [n, c] : args["statuses"].members()) {
+      Status st(code_from_name(c.as_string()), c.as_string() == "Success" ? "" : "harness");
+      m.emplace(n, st);
+    }
+    auto [res, st] = pl->post_filter(*state, *pod, m);
+    Json out = status_json(st);
+    out.set("nominatedNodeName", Json(res.nominated_node_name));
+    return out;
+  }
+  if (point == "permit" || point == "reserve" || point == "unreserve" || point == "postBind") {
+    // As in the real cycle these run on the assumed pod: the cache holds it
+    // (Coscheduling's assigned count includes it) while the point runs.
+    auto assumed = std::make_shared<Pod>(*pod);
+    assumed->node_name = node;
+    const bool assume = !node.empty() && args["assume"].as_bool(true) && point != "postBind";
+    if (assume) {
+      Status ast = cache_->assume_pod(assumed);
+      if (!ast.is_success()) return status_json(ast);
+    }
+    Json out;
+    if (point == "permit") {
+      auto [st, timeout] = pl->permit(*state, assumed, node);
+      out = status_json(st);
+      out.set("timeout_us", Json(timeout));
+    } else if (point == "reserve") {
+      out = status_json(pl->reserve(*state, assumed, node));
+    } else if (point == "unreserve") {
+      pl->unreserve(*state, assumed, node);
+      out = status_json(Status());
+    } else {
+      pl->post_bind(*state, assumed, node);
+      out = status_json(Status());
+    }
+    if (assume) cache_->forget_pod(*assumed);
+    return out;
+  }
+  if (args["runPreFilter"].as_bool(false)) {
+    Status st = fw->run_pre_filter(*state, *pod);
+    if (!st.is_success()) return status_json(st);
+  }
+  return pl->debug_call(point, *state, pod, args);
+}
+
 Json Scheduler::explain(const Json& pod_obj) {
   std::lock_guard<std::mutex> g(sched_mu_);
   Json out = Json::object();

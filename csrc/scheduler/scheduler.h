@@ -174,6 +174,13 @@ class Scheduler {
   // of the snapshot, `iterations` times. Returns the mean microseconds per
   // pass (and the node count / a checksum of the totals in `out`).
   double score_benchmark(const Json& pod, int iterations, Json* out = nullptr);
+  // Plugin unit-test harness (the reference's per-plugin *_test.go tables):
+  // runs one extension point of one plugin of the first profile for
+  // args["pod"] against the current cache snapshot, on the calling thread,
+  // with a fresh CycleState. `point`: less | preFilter | postFilter | permit |
+  // reserve | unreserve | postBind, or a plugin debug call (args["runPreFilter"]
+  // runs the profile's PreFilter plugins first). Returns {"code", "message", ...}.
+  Json plugin_call(const std::string& plugin, const std::string& point, const Json& args);
 
   SchedulingQueue& queue() { return *queue_; }
   SchedulerCache& cache() { return *cache_; }
