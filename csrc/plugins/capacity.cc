@@ -20,6 +20,7 @@
 #include <map>
 #include <mutex>
 #include <set>
+#include <unordered_map>
 
 #include "framework/framework.h"
 #include "framework/plugin.h"
@@ -44,37 +45,87 @@ bool cmp2(const Res& x1, const Res& x2, const Res& y) {
 }
 bool cmp(const Res& x, const Res& y) { return cmp2(x, Res{}, y); }
 
-struct EQInfo {
-  std::string ns;
-  std::set<std::string> pods;
+// One namespace's quota as the scheduling cycle sees it.
+struct Quota {
   Res min, max, used;
   bool used_over_min_with(const Res& req) const { return cmp2(req, used, min); }
   bool used_over_max_with(const Res& req) const { return cmp2(req, used, max); }
   bool used_over_min() const { return cmp(used, min); }
-  void add_pod(const Pod& p) {
-    if (!pods.insert(p.key()).second) return;
+};
+
+// Live quota of one namespace: the pods counted in `used` (a pod event can
+// repeat, so add/delete are idempotent by key) and the immutable Quota last
+// published for it (reset on change, rebuilt on the next publish).
+struct EQInfo {
+  std::string ns;
+  std::set<std::string> pods;
+  Res min, max, used;
+  std::shared_ptr<const Quota> published;
+  bool add_pod(const Pod& p) {
+    if (!pods.insert(p.key()).second) return false;
     used += p.request;
+    published.reset();
+    return true;
   }
-  void delete_pod(const Pod& p) {
-    if (!pods.erase(p.key())) return;
+  bool delete_pod(const Pod& p) {
+    if (!pods.erase(p.key())) return false;
     used -= p.request;
+    published.reset();
+    return true;
   }
 };
 using EQInfos = std::map<std::string, EQInfo>;
 
-bool aggregated_used_over_min_with(const EQInfos& infos, const Res& req) {
-  Res used, min;
-  for (const auto& [ns, e] : infos) {
-    used += e.used;
-    min += e.min;
-  }
-  used += req;
-  return cmp(used, min);
-}
+// Every quota at one version of the live state; shared by the cycles that
+// run at that version (published when a PreFilter finds the live state
+// changed, reusing the Quota of every namespace that did not).
+struct QuotaView {
+  std::unordered_map<std::string, std::shared_ptr<const Quota>> q;
+  Res sum_used, sum_min;
+};
 
+// The CycleState's quota snapshot: the shared view plus this cycle's own
+// changes (preemption dry runs add and remove pods through the PreFilter
+// extensions). The reference deep-copies every ElasticQuotaInfo, including
+// each namespace's set of pod keys, into every cycle
+// (capacity_scheduling.go:201-211, elasticquota.go Clone).
 struct EQSnapshot : StateData {
-  EQInfos infos;
+  std::shared_ptr<const QuotaView> base;
+  std::unordered_map<std::string, Res> delta;  // namespace -> change of `used`
+  Res delta_sum;
   std::shared_ptr<StateData> clone() const override { return std::make_shared<EQSnapshot>(*this); }
+
+  const Quota* find(const std::string& ns) const {
+    auto it = base->q.find(ns);
+    return it == base->q.end() ? nullptr : it->second.get();
+  }
+  bool has(const std::string& ns) const { return find(ns) != nullptr; }
+  // The namespace's quota with this cycle's changes applied (requires has(ns)).
+  Quota quota(const std::string& ns) const {
+    Quota out = *find(ns);
+    auto d = delta.find(ns);
+    if (d != delta.end()) out.used += d->second;
+    return out;
+  }
+  bool aggregated_used_over_min_with(const Res& req) const {
+    Res used = base->sum_used;
+    used += delta_sum;
+    used += req;
+    return cmp(used, base->sum_min);
+  }
+  // PreFilterExtensions AddPod / RemovePod. Terminal pods are not counted in
+  // `used` (the live accounting skips them), so they are not moved here.
+  void add(const Pod& p, int sign) {
+    if (!has(p.ns()) || p.phase == "Succeeded" || p.phase == "Failed") return;
+    Res& d = delta[p.ns()];
+    if (sign > 0) {
+      d += p.request;
+      delta_sum += p.request;
+    } else {
+      d -= p.request;
+      delta_sum -= p.request;
+    }
+  }
 };
 struct CSPreFilterState : StateData {
   Res pod_req, nominated_in_eq_with_req, nominated_with_req;
@@ -96,13 +147,14 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     if (kind == "elasticquotas") {
       auto eq = ElasticQuota::from_json(*obj);
       std::lock_guard<std::mutex> g(mu_);
+      ++version_;
       if (t == EventType::Deleted) {
         infos_.erase(eq->meta.ns);
         return;
       }
       auto it = infos_.find(eq->meta.ns);
       if (t == EventType::Added && it != infos_.end()) return;  // first listed wins
-      EQInfo info{eq->meta.ns, {}, eq->min, eq->max, {}};
+      EQInfo info{eq->meta.ns, {}, eq->min, eq->max, {}, nullptr};
       if (it != infos_.end()) {
         info.pods = it->second.pods;
         info.used = it->second.used;
@@ -117,7 +169,17 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       infos_[eq->meta.ns] = std::move(info);
       return;
     }
-    // pods: FilteringResourceEventHandler over assigned pods.
+    // pods: FilteringResourceEventHandler over assigned pods. Only pods of a
+    // namespace with a quota matter: decided before the pod is parsed.
+    {
+      const std::string& ns = (*obj)["metadata"]["namespace"].as_string();
+      bool known;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        known = infos_.count(ns) > 0;
+      }
+      if (!known && !h_.informers->elastic_quota_for_namespace(ns)) return;
+    }
     auto np = Pod::from_json(*obj, *h_.gpu_names);
     bool now_assigned = !np->node_name.empty();
     PodPtr op = old ? Pod::from_json(*old, *h_.gpu_names) : nullptr;
@@ -133,7 +195,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       if (op->phase == "Succeeded" || op->phase == "Failed") return;
       if (np->phase != "Running" && np->phase != "Pending") {
         auto it = infos_.find(np->ns());
-        if (it != infos_.end()) it->second.delete_pod(*np);
+        if (it != infos_.end() && it->second.delete_pod(*np)) ++version_;
       }
     } else if (!now_assigned && was_assigned) {
       delete_pod_locked(*op);
@@ -145,13 +207,32 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     if (it == infos_.end()) {
       auto eq = h_.informers->elastic_quota_for_namespace(p.ns());
       if (!eq) return;
-      it = infos_.emplace(p.ns(), EQInfo{p.ns(), {}, eq->min, eq->max, {}}).first;
+      it = infos_.emplace(p.ns(), EQInfo{p.ns(), {}, eq->min, eq->max, {}, nullptr}).first;
+      ++version_;
     }
-    it->second.add_pod(p);
+    if (it->second.add_pod(p)) ++version_;
   }
   void delete_pod_locked(const Pod& p) {
     auto it = infos_.find(p.ns());
-    if (it != infos_.end()) it->second.delete_pod(p);
+    if (it != infos_.end() && it->second.delete_pod(p)) ++version_;
+  }
+
+  // The view of the current live state (under mu_): republished only when
+  // the live state changed since the last one, and then only the changed
+  // namespaces get a new Quota.
+  std::shared_ptr<const QuotaView> view_locked() {
+    if (view_ && view_version_ == version_) return view_;
+    auto v = std::make_shared<QuotaView>();
+    v->q.reserve(infos_.size());
+    for (auto& [ns, e] : infos_) {
+      if (!e.published) e.published = std::make_shared<const Quota>(Quota{e.min, e.max, e.used});
+      v->q.emplace(ns, e.published);
+      v->sum_used += e.used;
+      v->sum_min += e.min;
+    }
+    view_ = std::move(v);
+    view_version_ = version_;
+    return view_;
   }
 
   // ---- PreFilter (capacity_scheduling.go:201-275) ----
@@ -159,41 +240,41 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     auto snap = std::make_shared<EQSnapshot>();
     {
       std::lock_guard<std::mutex> g(mu_);
-      snap->infos = infos_;
+      snap->base = view_locked();
     }
     s.write(kSnapKey, snap);
     auto pfs = std::make_shared<CSPreFilterState>();
     pfs->pod_req = pod.request;
-    auto eit = snap->infos.find(pod.ns());
-    if (eit == snap->infos.end()) {
+    const Quota* own = snap->find(pod.ns());
+    if (!own) {
       s.write(kStateKey, pfs);
       return {};
     }
     Res in_eq, global;
     if (h_.snapshot && h_.nominator && !h_.nominator->empty()) {
-      for (const auto& ni : h_.snapshot->nodes) {
-        for (const auto& np : h_.nominator->nominated_pods_for_node(ni->name())) {
-          if (np->uid() == pod.uid()) continue;
-          auto it = snap->infos.find(np->ns());
-          if (it == snap->infos.end()) continue;
-          if (np->ns() == pod.ns() && np->priority >= pod.priority) {
-            in_eq += np->request;
-            global += np->request;
-          } else if (np->ns() != pod.ns() && !it->second.used_over_min()) {
-            global += np->request;
-          }
+      // Pods nominated onto nodes of the snapshot (the reference walks every
+      // node and asks for its nominations).
+      h_.nominator->for_each([&](const std::string& node, const PodPtr& np) {
+        if (np->uid() == pod.uid() || !h_.snapshot->get(node)) return;
+        const Quota* q = snap->find(np->ns());
+        if (!q) return;
+        if (np->ns() == pod.ns() && np->priority >= pod.priority) {
+          in_eq += np->request;
+          global += np->request;
+        } else if (np->ns() != pod.ns() && !q->used_over_min()) {
+          global += np->request;
         }
-      }
+      });
     }
     in_eq += pod.request;
     global += pod.request;
     pfs->nominated_in_eq_with_req = in_eq;
     pfs->nominated_with_req = global;
     s.write(kStateKey, pfs);
-    if (eit->second.used_over_max_with(in_eq))
+    if (own->used_over_max_with(in_eq))
       return Status::unschedulable("Pod " + pod.key() + " is rejected in PreFilter because ElasticQuota " + pod.ns() +
                                    " is more than Max");
-    if (aggregated_used_over_min_with(snap->infos, global))
+    if (snap->aggregated_used_over_min_with(global))
       return Status::unschedulable("Pod " + pod.key() +
                                    " is rejected in PreFilter because total ElasticQuota used is more than min");
     return {};
@@ -203,20 +284,14 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
   // AddPod/RemovePod touch only the quota of the other pod's namespace.
   bool pre_filter_extension_affects(const CycleState& s, const Pod&, const Pod& other) const override {
     auto* snap = s.read_as<EQSnapshot>(kSnapKey);
-    return snap && snap->infos.count(other.ns());
+    return snap && snap->has(other.ns());
   }
   Status add_pod(CycleState& s, const Pod&, const PodPtr& to_add, const NodeInfo&) override {
-    if (auto* snap = s.read_as<EQSnapshot>(kSnapKey)) {
-      auto it = snap->infos.find(to_add->ns());
-      if (it != snap->infos.end()) it->second.add_pod(*to_add);
-    }
+    if (auto* snap = s.read_as<EQSnapshot>(kSnapKey)) snap->add(*to_add, +1);
     return {};
   }
   Status remove_pod(CycleState& s, const Pod&, const PodPtr& to_remove, const NodeInfo&) override {
-    if (auto* snap = s.read_as<EQSnapshot>(kSnapKey)) {
-      auto it = snap->infos.find(to_remove->ns());
-      if (it != snap->infos.end()) it->second.delete_pod(*to_remove);
-    }
+    if (auto* snap = s.read_as<EQSnapshot>(kSnapKey)) snap->add(*to_remove, -1);
     return {};
   }
 
@@ -240,19 +315,17 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     if (!snap) return true;
     auto ni = h_.snapshot ? h_.snapshot->get(pod.nominated_node_name) : nullptr;
     if (!ni) return true;
-    auto pit = snap->infos.find(pod.ns());
-    if (pit != snap->infos.end()) {
-      bool more_than_min = pit->second.used_over_min_with(pfs->nominated_in_eq_with_req);
+    if (snap->has(pod.ns())) {
+      bool more_than_min = snap->quota(pod.ns()).used_over_min_with(pfs->nominated_in_eq_with_req);
       for (const auto& p : ni->pods) {
         if (!p->terminating()) continue;
-        auto it = snap->infos.find(p->ns());
-        if (it == snap->infos.end()) continue;
+        if (!snap->has(p->ns())) continue;
         if (p->ns() == pod.ns() && p->priority < pod.priority) return false;
-        if (p->ns() != pod.ns() && !more_than_min && it->second.used_over_min()) return false;
+        if (p->ns() != pod.ns() && !more_than_min && snap->quota(p->ns()).used_over_min()) return false;
       }
     } else {
       for (const auto& p : ni->pods) {
-        if (snap->infos.count(p->ns())) continue;
+        if (snap->has(p->ns())) continue;
         if (p->terminating() && p->priority < pod.priority) return false;
       }
     }
@@ -267,9 +340,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     if (!snap) return Status::unschedulable("Failed to read elasticQuotaSnapshot from cycleState");
     if (!pfs) return Status::unschedulable("Failed to read preFilterState from cycleState");
     Framework& fw = *h_.framework;
-    EQInfos& infos = snap->infos;
-    auto pit = infos.find(pod.ns());
-    bool with_eq = pit != infos.end();
+    const bool with_eq = snap->has(pod.ns());
     auto remove = [&](const PodPtr& p) {
       ni.remove_pod(p->uid());
       return fw.run_pre_filter_remove_pod(s, pod, p, ni);
@@ -285,12 +356,11 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
                      [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*b, *a); });
     std::vector<PodPtr> potential;
     if (with_eq) {
-      bool more_than_min = pit->second.used_over_min_with(pfs->nominated_in_eq_with_req);
+      bool more_than_min = snap->quota(pod.ns()).used_over_min_with(pfs->nominated_in_eq_with_req);
       for (const auto& p : pods) {
-        auto it = infos.find(p->ns());
-        if (it == infos.end()) continue;
+        if (!snap->has(p->ns())) continue;
         bool victim = more_than_min ? (p->ns() == pod.ns() && p->priority < pod.priority)
-                                    : (p->ns() != pod.ns() && it->second.used_over_min());
+                                    : (p->ns() != pod.ns() && snap->quota(p->ns()).used_over_min());
         if (victim) {
           potential.push_back(p);
           Status st = remove(p);
@@ -299,7 +369,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       }
     } else {
       for (const auto& p : pods) {
-        if (infos.count(p->ns())) continue;
+        if (snap->has(p->ns())) continue;
         if (p->priority < pod.priority) {
           potential.push_back(p);
           Status st = remove(p);
@@ -311,8 +381,8 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       return Status::unresolvable("No victims found on node " + ni.name() + " for preemptor pod " + pod.name());
     Status fst = fw.run_filter_with_nominated_pods(s, pod, ni);
     if (!fst.is_success()) return fst;
-    pit = infos.find(pod.ns());
-    if (with_eq && (pit->second.used_over_max_with(pfs->pod_req) || aggregated_used_over_min_with(infos, pfs->pod_req)))
+    if (with_eq && (snap->quota(pod.ns()).used_over_max_with(pfs->pod_req) ||
+                    snap->aggregated_used_over_min_with(pfs->pod_req)))
       return Status::unschedulable("global quota max exceeded");
     std::stable_sort(potential.begin(), potential.end(),
               [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*a, *b); });
@@ -329,9 +399,8 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       }
       // The reference re-removes (and double-lists) a pod that already
       // failed the fit check; only a reprieved pod is re-checked here.
-      auto pit2 = infos.find(pod.ns());
-      if (fits && pit2 != infos.end() && (pit2->second.used_over_max_with(pfs->nominated_in_eq_with_req) ||
-                                  aggregated_used_over_min_with(infos, pfs->nominated_with_req))) {
+      if (fits && with_eq && (snap->quota(pod.ns()).used_over_max_with(pfs->nominated_in_eq_with_req) ||
+                              snap->aggregated_used_over_min_with(pfs->nominated_with_req))) {
         Status rst = remove(p);
         if (!rst.is_success()) return {false, rst};
         victims.push_back(p);
@@ -354,13 +423,13 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
   Status reserve(CycleState&, const PodPtr& p, const std::string&) override {
     std::lock_guard<std::mutex> g(mu_);
     auto it = infos_.find(p->ns());
-    if (it != infos_.end()) it->second.add_pod(*p);
+    if (it != infos_.end() && it->second.add_pod(*p)) ++version_;
     return {};
   }
   void unreserve(CycleState&, const PodPtr& p, const std::string&) override {
     std::lock_guard<std::mutex> g(mu_);
     auto it = infos_.find(p->ns());
-    if (it != infos_.end()) it->second.delete_pod(*p);
+    if (it != infos_.end() && it->second.delete_pod(*p)) ++version_;
   }
 
   std::vector<ClusterEvent> events_to_register() const override {
@@ -395,6 +464,9 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
   Evaluator ev_;
   std::mutex mu_;
   EQInfos infos_;
+  uint64_t version_ = 0;  // bumped on every change of infos_ (under mu_)
+  std::shared_ptr<const QuotaView> view_;
+  uint64_t view_version_ = ~0ULL;
   CycleState* cur_state_ = nullptr;  // PostFilter runs on the scheduling thread only
 };
 

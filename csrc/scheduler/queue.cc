@@ -137,6 +137,12 @@ std::vector<PodPtr> Nominator::nominated_pods_for_node(const std::string& node) 
   return it == by_node_.end() ? std::vector<PodPtr>{} : it->second;
 }
 
+void Nominator::for_each(const std::function<void(const std::string&, const PodPtr&)>& fn) const {
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& [node, pods] : by_node_)
+    for (const auto& p : pods) fn(node, p);
+}
+
 std::shared_ptr<const NominatedMap> Nominator::view(std::vector<std::string>* changed) const {
   std::lock_guard<std::mutex> g(mu_);
   NominatedMap& m = *mirror_;

@@ -55,6 +55,9 @@ class Nominator {
   void remove(const Pod& p);
   void update(const PodPtr& old_p, const PodPtr& new_p);
   std::vector<PodPtr> nominated_pods_for_node(const std::string& node) const;
+  // Every nominated pod with its node, under the lock (callers needing all of
+  // them: one pass over the nominations instead of a lookup per node).
+  void for_each(const std::function<void(const std::string& node, const PodPtr& p)>& fn) const;
   // Every node's nominated pods for the cycle about to start. Single
   // consumer: the scheduling thread, between cycles. The view is a mirror
   // that the changes since the last call are applied to (O(changes), not a

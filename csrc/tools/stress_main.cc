@@ -141,6 +141,15 @@ int main(int argc, char** argv) {
   };
   load_many("nodes", "nodes.json");
   load_many("noderesourcetopologies", "nrts.json");
+  // extra.json: {"<kind>": [objects]} created before the scheduler starts
+  // (e.g. a scheduler_perf workload's ElasticQuotas).
+  if (std::filesystem::exists(dir + "/extra.json")) {
+    Json extra = Json::parse(slurp(dir + "/extra.json"));
+    for (const auto& [kind, objs] : extra.members()) {
+      std::vector<Json> v(objs.items().begin(), objs.items().end());
+      store->create_many(kind, std::move(v));
+    }
+  }
   Json cfg = Json::parse(slurp(dir + "/config.json"));
   Scheduler sched(store, cfg);
   sched.start();
@@ -248,7 +257,7 @@ int main(int argc, char** argv) {
     auto t_bound = std::chrono::steady_clock::now();
     bound += expect;
     std::string ns = wave["namespace"].str_or("bench");
-    store->delete_all("pods", ns);
+    store->delete_all("pods", has_init ? std::string() : ns);  // init pods may live in other namespaces
     store->delete_all("podgroups", ns);
     while (sched.cache().pod_count() > 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
     auto t_end = std::chrono::steady_clock::now();

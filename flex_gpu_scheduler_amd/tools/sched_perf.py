@@ -191,6 +191,53 @@ def mi355x_gangs(n_nodes: int, n_pods: int) -> dict:
     return _spec("MI355X-Gang8", nodes, [], pods, config=flagship_config(), extra_objects={"podgroups": pgs})
 
 
+def _capacity_config() -> dict:
+    """Default plugins plus CapacityScheduling (its PostFilter replaces
+    DefaultPreemption), as manifests/capacityscheduling/scheduler-config.yaml."""
+    return {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
+            "profiles": [{"schedulerName": "default-scheduler", "plugins": {
+                "preFilter": {"enabled": [{"name": "CapacityScheduling"}]},
+                "postFilter": {"enabled": [{"name": "CapacityScheduling"}], "disabled": [{"name": "*"}]},
+                "reserve": {"enabled": [{"name": "CapacityScheduling"}]}}}]}
+
+
+def _quotas(n_nodes: int, share: float = 0.5) -> list[dict]:
+    """Two namespaces, each guaranteed `share` of the cluster's CPU and
+    memory and allowed to borrow up to all of it."""
+    from ..models import make_elastic_quota
+
+    cpu, mem = 32 * n_nodes, 128 * n_nodes
+    mn = {"cpu": str(int(cpu * share)), "memory": f"{int(mem * share)}Gi"}
+    mx = {"cpu": str(cpu), "memory": f"{mem}Gi"}
+    return [make_elastic_quota(f"quota-{ns}", ns, min=mn, max=mx) for ns in ("team-a", "team-b")]
+
+
+def capacity_admission(n_nodes: int, n_pods: int) -> dict:
+    """SchedulingBasic with every pod under an ElasticQuota (2 namespaces
+    sharing the cluster): the per-cycle quota snapshot, nominated-pod sums
+    and Reserve accounting on the admission path."""
+    init = [make_pod(f"init-{i}", ("team-a", "team-b")[i % 2], requests={"cpu": "100m", "memory": "100Mi"})
+            for i in range(n_nodes)]
+    pods = [make_pod(f"p-{i}", ("team-a", "team-b")[i % 2], requests={"cpu": "100m", "memory": "100Mi"})
+            for i in range(n_pods)]
+    return _spec("CapacityScheduling-Admission", _nodes_plain(n_nodes), init, pods, config=_capacity_config(),
+                 extra_objects={"elasticquotas": _quotas(n_nodes)})
+
+
+def capacity_reclaim(n_nodes: int, n_pods: int) -> dict:
+    """PreemptionBasic across quotas: team-a borrowed the whole cluster (4
+    pods of 8 CPUs per node, beyond its 50% min); team-b's pods, within its
+    min, each reclaim one borrowed pod (capacity_scheduling.go:465-644)."""
+    n = min(n_pods, n_nodes)
+    init = [make_pod(f"borrow-{i}", "team-a", requests={"cpu": "8", "memory": "1Gi"}, priority=1)
+            for i in range(4 * n_nodes)]
+    pods = [make_pod(f"reclaim-{i}", "team-b", requests={"cpu": "8", "memory": "1Gi"}, priority=1)
+            for i in range(n)]
+    return _spec("CapacityScheduling-Reclaim", _nodes_plain(n_nodes), init, pods, config=_capacity_config(),
+                 extra_objects={"elasticquotas": _quotas(n_nodes)},
+                 options={"podInitialBackoffSeconds": 0.01, "podMaxBackoffSeconds": 0.1})
+
+
 WORKLOADS = {
     "SchedulingBasic": scheduling_basic,
     "SchedulingPodAntiAffinity": pod_anti_affinity,
@@ -204,6 +251,8 @@ WORKLOADS = {
     "PreemptionBasic": preemption_basic,
     "MI355X-FlexGPUMix": mi355x_flexgpu_mix,
     "MI355X-Gang8": mi355x_gangs,
+    "CapacityScheduling-Admission": capacity_admission,
+    "CapacityScheduling-Reclaim": capacity_reclaim,
 }
 
 

@@ -37,6 +37,11 @@ def write_workload(out: str | Path, name: str, nodes: int, pods: int, options: d
     (d / "nrts.json").write_text("[]")
     cfg = load_config(w["config"]).to_native(**{**w["options"], **(options or {})})
     (d / "config.json").write_text(json.dumps(cfg))
+    extra = {k: v for k, v in (w.get("extra_objects") or {}).items() if k != "podgroups"}
+    if extra:
+        (d / "extra.json").write_text(json.dumps(extra))
+    elif (d / "extra.json").exists():
+        (d / "extra.json").unlink()
     if w["init_pods"]:
         (d / "init.json").write_text(json.dumps(w["init_pods"]))
     elif (d / "init.json").exists():
