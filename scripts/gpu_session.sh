@@ -32,6 +32,11 @@ for step in "$@"; do
                 --cpus l3 > "$OUT/sched_perf_500.jsonl" 2>&1 ;;
     sched5000) timeout -k 10 700 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 5000 --pods 5000 \
                 --cpus l3 > "$OUT/sched_perf_5000.jsonl" 2>&1 ;;
+    schedperf_capacity)
+      timeout -k 10 600 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 5000 --pods 5000 --cpus l3 \
+        --only SchedulingBasic CapacityScheduling-Admission > "$OUT/sched_perf_capacity_5000.jsonl" 2>&1 &&
+      timeout -k 10 600 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 5000 --pods 1000 --cpus l3 \
+        --only PreemptionBasic CapacityScheduling-Reclaim >> "$OUT/sched_perf_capacity_5000.jsonl" 2>&1 ;;
     remote) timeout -k 10 600 python -u -m flex_gpu_scheduler_amd.tools.remote_bench --matrix > "$OUT/remote_bench.jsonl" \
               2>&1 ;;
     sample_pre|sample_sched)
