@@ -98,13 +98,11 @@ def gang_latency_summary(gangs: list[dict], sizes: dict[str, int] | None = None,
     """p50/p99 first-member-enqueue -> last-member-bound (ms) per group size.
 
     With `by_type`, CPX quarter-GPU gangs (workload.make_wave names them
-    "<step>-q<i>") are keyed "cpx4" apart from whole-GPU gangs of 4: the wave
-    appends them after every whole-GPU gang, so in a burst they queue longest
-    and dominate the mixed size-4 p99."""
+    "s<step>-<k>-q") are keyed "cpx4" apart from whole-GPU gangs of 4."""
     by: dict[str, list[float]] = {}
     for g in gangs:
         key = str(g["size"])
-        if by_type and "-q" in g.get("pod_group", "").rsplit("/", 1)[-1]:
+        if by_type and g.get("pod_group", "").endswith("-q"):
             key = "cpx4"
         by.setdefault(key, []).append((g["bound_us"] - g["first_enqueue_us"]) / 1000.0)
     out = {}

@@ -100,40 +100,52 @@ def _rand_cpu_mem(rng: random.Random) -> dict:
 
 def make_wave(spec: ClusterSpec, step: int, *, namespace: str = "bench", fill: float = 0.85, seed: int = 0,
               scheduler_name: str | None = None) -> Wave:
-    """One wave of gangs filling ~`fill` of the SPX GPUs and CPX XCDs."""
+    """One wave of gangs filling ~`fill` of the SPX GPUs and CPX XCDs.
+
+    Whole-GPU gangs (1/2/4/8 ranks) and CPX quarter gangs (4 x 0.25 GPU) are
+    interleaved evenly in creation order, and named with one running index
+    so the queue (PodGroup creation time, then ns/name) keeps that order: a
+    burst no longer queues every CPX gang behind all whole-GPU gangs."""
     rng = random.Random(seed * 1_000_003 + step)
     w = Wave()
     gpu_budget = int(spec.spx_gpus * fill)
-    # Whole-GPU gangs: cycle through sizes so each wave has all four.
+    # Whole-GPU gang sizes: cycle through sizes so each wave has all four.
+    whole: list[int] = []
     gi = 0
     while gpu_budget > 0:
         size = GROUP_SIZES[gi % len(GROUP_SIZES)] if gi < 4 else rng.choice(GROUP_SIZES)
         gi += 1
         if size > gpu_budget:
             size = 1
-        name = f"s{step}-g{gi}-x{size}"
-        w.pod_groups.append(make_pod_group(name, namespace, size))
-        w.group_sizes[f"{namespace}/{name}"] = size
-        req = _rand_cpu_mem(rng)
-        for r in range(size):
-            c = make_container("trainer", requests=req, limits={GPU: "1"})
-            w.pods.append(make_pod(f"{name}-r{r}", namespace, containers=[c], pod_group=name,
-                                   scheduler_name=scheduler_name))
+        whole.append(size)
         gpu_budget -= size
     # CPX fractional gangs: 4 pods x 0.25 GPU (2 XCDs each) = one CPX GPU.
-    xcd_budget = int(spec.cpx_xcds * fill * 0.75)
-    fi = 0
-    while xcd_budget >= 8:
-        fi += 1
-        name = f"s{step}-q{fi}"
-        w.pod_groups.append(make_pod_group(name, namespace, 4))
-        w.group_sizes[f"{namespace}/{name}"] = 4
+    n_cpx = max(0, int(spec.cpx_xcds * fill * 0.75) // 8)
+    kinds: list[int] = []  # gang size, 0 = CPX quarter gang
+    total = len(whole) + n_cpx
+    wi = ci = 0
+    for k in range(total):
+        # Bresenham-style merge: CPX gangs at their share of the positions.
+        if ci < n_cpx and (wi >= len(whole) or (ci + 1) * total <= (k + 1) * n_cpx):
+            kinds.append(0)
+            ci += 1
+        else:
+            kinds.append(whole[wi])
+            wi += 1
+    for k, size in enumerate(kinds):
+        if size:
+            name = f"s{step}-{k:04d}-x{size}"
+            limits, cname, n = {GPU: "1"}, "trainer", size
+        else:
+            name = f"s{step}-{k:04d}-q"
+            limits, cname, n = {GPU_XCD: "2"}, "shard", 4
+        w.pod_groups.append(make_pod_group(name, namespace, n))
+        w.group_sizes[f"{namespace}/{name}"] = n
         req = _rand_cpu_mem(rng)
-        for r in range(4):
-            c = make_container("shard", requests=req, limits={GPU_XCD: "2"})
+        for r in range(n):
+            c = make_container(cname, requests=req, limits=limits)
             w.pods.append(make_pod(f"{name}-r{r}", namespace, containers=[c], pod_group=name,
                                    scheduler_name=scheduler_name))
-        xcd_budget -= 8
     # Shared-HBM inference pods packed into the remaining CPX partitions.
     for m in range(int(spec.cpx_xcds * fill * 0.25 / 2)):
         c = make_container("infer", requests=_rand_cpu_mem(rng), limits={GPU_MEMORY: str(rng.choice([8, 12, 16]))})

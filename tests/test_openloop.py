@@ -53,9 +53,9 @@ def test_open_loop_admits_every_gang_with_ordered_timeline():
 
 
 def test_burst_summary_splits_cpx_gangs():
-    recs = [{"pod_group": "ns/s1-g3-x4", "size": 4, "first_enqueue_us": 0, "bound_us": 1000},
-            {"pod_group": "ns/s1-q1", "size": 4, "first_enqueue_us": 0, "bound_us": 9000},
-            {"pod_group": "ns/s1-g1-x1", "size": 1, "first_enqueue_us": 0, "bound_us": 500}]
+    recs = [{"pod_group": "ns/s1-0003-x4", "size": 4, "first_enqueue_us": 0, "bound_us": 1000},
+            {"pod_group": "ns/s1-0001-q", "size": 4, "first_enqueue_us": 0, "bound_us": 9000},
+            {"pod_group": "ns/s1-0000-x1", "size": 1, "first_enqueue_us": 0, "bound_us": 500}]
     mixed = gang_latency_summary(recs)
     assert mixed["4"]["n"] == 2
     typed = gang_latency_summary(recs, by_type=True)
@@ -129,3 +129,20 @@ def test_wave_chunks_write_each_podgroup_before_its_pods():
         assert r.pods == len(w.pods)
     finally:
         sh.close()
+
+
+def test_burst_wave_interleaves_cpx_gangs_in_queue_order():
+    """CPX quarter gangs are spread through the wave and their names sort in
+    creation order (the queue's tie-break after PodGroup creation time), so
+    they no longer all queue behind the whole-GPU gangs."""
+    from flex_gpu_scheduler_amd.utils.workload import make_wave
+
+    w = make_wave(ClusterSpec(nodes=64), 3)
+    names = [pg["metadata"]["name"] for pg in w.pod_groups]
+    assert names == sorted(names)
+    cpx = [i for i, n in enumerate(names) if n.endswith("-q")]
+    assert len(cpx) > 10 and len(names) - len(cpx) > 10
+    # Evenly spread: the first CPX gang comes early, the last one late.
+    assert cpx[0] < len(names) // 5 and cpx[-1] > len(names) * 4 // 5
+    sizes = {pg["spec"]["minMember"] for pg in w.pod_groups if not pg["metadata"]["name"].endswith("-q")}
+    assert sizes == {1, 2, 4, 8}
