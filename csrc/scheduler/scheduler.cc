@@ -1113,6 +1113,23 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     eq_filter = false;
   }
   int start = next_start_node_;
+  // The members of one gang that share a pod template are evaluated over the
+  // node window of the first of them (upstream rotates the window every
+  // cycle, numFeasibleNodesToFind > 100 nodes): a rank then reuses its
+  // sibling's Filter verdicts and node-local scores for every node but the
+  // one the sibling took, and the gang's candidates are the same nodes
+  // XGMIGangAffinity ranks.
+  static const bool gang_window = !std::getenv("XSCHED_GANG_WINDOW") || std::string(std::getenv("XSCHED_GANG_WINDOW")) != "0";
+  if (gang_window && !full_diagnosis && p.pg_key) {
+    if (p.pg_key == window_gang_ && p.template_hash == window_tmpl_ && window_n_ == n) {
+      start = window_start_;
+    } else {
+      window_gang_ = p.pg_key;
+      window_tmpl_ = p.template_hash;
+      window_start_ = start;
+      window_n_ = n;
+    }
+  }
   // Per-node failures go to a position-indexed buffer (no lock, no map
   // insert per node); the NodeToStatusMap is only materialized when the
   // diagnosis is consumed: no feasible node (PostFilter / FitError) or explain.

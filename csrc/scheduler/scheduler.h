@@ -357,6 +357,10 @@ class Scheduler {
   std::atomic<int> in_cycle_{0};
   std::atomic<int64_t> loop_tick_us_{0};  // RealClock time of the last loop iteration
   int next_start_node_ = 0;
+  // Node window shared by consecutive members of one gang and template
+  // (find_nodes_that_fit; scheduling thread only).
+  uint64_t window_gang_ = 0, window_tmpl_ = 0;
+  int window_start_ = 0, window_n_ = -1;
   std::mt19937_64 rng_;
   std::vector<uint64_t> timer_ids_;
   std::unordered_map<Framework*, std::unordered_map<uint64_t, std::unique_ptr<EqEntry>>> eq_;  // scheduling thread only

@@ -55,6 +55,26 @@ for step in "$@"; do
       cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
       XSCHED_SAMPLE_HZ=2000 XSCHED_SAMPLE="$OUT/bench.samples" timeout -k 5 300 taskset -c "$cpus" \
         abbin/xsched_stress_prof /tmp/s_bench 40 > "$OUT/bench.sample_run.txt" 2>&1 ;;
+    ab1024)
+      # A/B of an env toggle (AB_VAR, default XSCHED_GANG_WINDOW) on the
+      # 1,024-node bench waves in the native stress driver (abbin/xsched_stress),
+      # pinned to one idle L3 domain, alternating 3x.
+      var=${AB_VAR:-XSCHED_GANG_WINDOW}
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_1024 --nodes 1024 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      for i in 1 2 3; do
+        for v in 0 1; do
+          echo "$var=$v $(env "$var=$v" timeout -k 5 200 taskset -c "$cpus" abbin/xsched_stress /tmp/s_1024 6 | tail -1)" \
+            >> "$OUT/ab1024.txt" || exit 1
+        done
+      done ;;
+    sample1024)
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_1024 --nodes 1024 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      XSCHED_SAMPLE_HZ=2000 XSCHED_SAMPLE="$OUT/n1024.samples" timeout -k 5 200 taskset -c "$cpus" \
+        abbin/xsched_stress /tmp/s_1024 6 > "$OUT/n1024.sample_run.txt" 2>&1 &&
+      python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/n1024.samples" --exe abbin/xsched_stress --top 40 \
+        > "$OUT/n1024_samples.txt" 2>&1 && rm -f "$OUT/n1024.samples" ;;
     rocprof)
       # Kernel trace + per-kernel stats of one short bench run (the probe,
       # health, MFMA and placement kernels on the GPU path).
