@@ -10,7 +10,13 @@
 //                       lane), non-temporal vs default cache policy, 4/8/16
 //                       workgroups of 256 threads per CU; probe_bench sweeps
 //                       them and the node agent keeps the fastest. HBM3E peak
-//                       is 8 TB/s; ~6.3 TB/s is the achievable streaming rate.
+//                       is 8 TB/s. Each launch is timed by its own event pair
+//                       and the median is reported (the back-to-back batch
+//                       rate, launch gaps included, is kept as a second
+//                       figure); working sets default to 1 GiB, 4x the 256 MB
+//                       Infinity Cache, so the rate is HBM's and not the
+//                       cache's (profiles/r4*_pmc_probe_summary.md checks the
+//                       median against rocprofv3's dispatch times and bytes).
 //  * xs_hbm_bandwidth_xcd  the same traffic executed only by workgroups that
 //                       land on the XCDs in `xcd_mask` (work handed out by an
 //                       atomic chunk counter, so every launched workgroup
@@ -30,6 +36,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -243,6 +250,36 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint32_t* __restrict_
   }
 }
 
+// Per-launch timing: `launch(i)` enqueues launch i; every launch sits
+// between its own event pair on `s`. out: [median ms, min ms, batch ms per
+// launch (first start to last end / iters)]. Events are created once.
+template <typename F>
+int time_launches(hipStream_t s, int iters, F&& launch, double out[3]) {
+  std::vector<Event> ev(2 * static_cast<size_t>(iters));
+  for (auto& e : ev) XS_CHECK(hipEventCreate(&e.e));
+  for (int i = 0; i < iters; ++i) {
+    XS_CHECK(hipEventRecord(ev[2 * i].e, s));
+    launch(i);
+    XS_CHECK(hipEventRecord(ev[2 * i + 1].e, s));
+  }
+  XS_CHECK(hipEventSynchronize(ev.back().e));
+  XS_CHECK(hipGetLastError());
+  std::vector<double> per(iters);
+  for (int i = 0; i < iters; ++i) {
+    float ms = 0;
+    XS_CHECK(hipEventElapsedTime(&ms, ev[2 * i].e, ev[2 * i + 1].e));
+    per[i] = ms;
+  }
+  float total = 0;
+  XS_CHECK(hipEventElapsedTime(&total, ev.front().e, ev.back().e));
+  std::vector<double> sorted = per;
+  std::sort(sorted.begin(), sorted.end());
+  out[0] = sorted[sorted.size() / 2];
+  out[1] = sorted.front();
+  out[2] = static_cast<double>(total) / iters;
+  return 0;
+}
+
 int cu_count(int dev) {
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
@@ -339,8 +376,9 @@ int xs_device_props(int dev, char* out, int len) {
 
 // mode: 0 read, 1 write, 2 copy, 3 triad. bytes = working set per array.
 // cu_limit > 0 caps the grid at cu_limit * blocks_per_cu workgroups.
-int xs_hbm_bandwidth_v(int dev, size_t bytes, int iters, int cu_limit, int mode, int variant, double* gbps,
-                       double* ms_per_iter) {
+// detail (optional, 3 doubles): min-launch GB/s, batch GB/s, batch ms/launch.
+int xs_hbm_bandwidth_d(int dev, size_t bytes, int iters, int cu_limit, int mode, int variant, double* gbps,
+                       double* ms_per_iter, double* detail) {
   XS_CHECK(hipSetDevice(dev));
   if (iters <= 0) iters = 10;
   size_t n = bytes / sizeof(vec4);
@@ -364,21 +402,23 @@ int xs_hbm_bandwidth_v(int dev, size_t bytes, int iters, int cu_limit, int mode,
   XS_CHECK(hipGetLastError());
   launch(v, mode, grid, s.s, a.p, b.p, c.p, n, sink.as<uint32_t>());
   XS_CHECK(hipStreamSynchronize(s.s));
-  Event e0, e1;
-  XS_CHECK(hipEventCreate(&e0.e));
-  XS_CHECK(hipEventCreate(&e1.e));
-  XS_CHECK(hipEventRecord(e0.e, s.s));
-  for (int i = 0; i < iters; ++i) launch(v, mode, grid, s.s, a.p, b.p, c.p, n, sink.as<uint32_t>());
-  XS_CHECK(hipEventRecord(e1.e, s.s));
-  XS_CHECK(hipEventSynchronize(e1.e));
-  XS_CHECK(hipGetLastError());
-  float ms = 0;
-  XS_CHECK(hipEventElapsedTime(&ms, e0.e, e1.e));
-  double per = ms / iters;
-  double moved = static_cast<double>(bytes) * (mode == 2 ? 2.0 : mode == 3 ? 3.0 : 1.0);
-  if (gbps) *gbps = moved / (per * 1e-3) / 1e9;
-  if (ms_per_iter) *ms_per_iter = per;
+  double t[3];
+  int rc = time_launches(s.s, iters, [&](int) { launch(v, mode, grid, s.s, a.p, b.p, c.p, n, sink.as<uint32_t>()); }, t);
+  if (rc) return rc;
+  const double moved = static_cast<double>(bytes) * (mode == 2 ? 2.0 : mode == 3 ? 3.0 : 1.0);
+  if (gbps) *gbps = moved / (t[0] * 1e-3) / 1e9;
+  if (ms_per_iter) *ms_per_iter = t[0];
+  if (detail) {
+    detail[0] = moved / (t[1] * 1e-3) / 1e9;
+    detail[1] = moved / (t[2] * 1e-3) / 1e9;
+    detail[2] = t[2];
+  }
   return 0;
+}
+
+int xs_hbm_bandwidth_v(int dev, size_t bytes, int iters, int cu_limit, int mode, int variant, double* gbps,
+                       double* ms_per_iter) {
+  return xs_hbm_bandwidth_d(dev, bytes, iters, cu_limit, mode, variant, gbps, ms_per_iter, nullptr);
 }
 
 // One streaming kernel over caller-owned device buffers (e.g. torch tensors),
@@ -428,9 +468,9 @@ int xs_hbm_bandwidth(int dev, size_t bytes, int iters, int cu_limit, int mode, d
 }
 
 // Bandwidth pulled by the workgroups resident on the XCDs in xcd_mask
-// (mode 0 read, 1 write, 2 copy).
-int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, int mode, double* gbps,
-                         double* ms_per_iter) {
+// (mode 0 read, 1 write, 2 copy). detail as in xs_hbm_bandwidth_d.
+int xs_hbm_bandwidth_xcd_d(int dev, size_t bytes, int iters, uint32_t xcd_mask, int mode, double* gbps,
+                           double* ms_per_iter, double* detail) {
   XS_CHECK(hipSetDevice(dev));
   if (iters <= 0) iters = 10;
   if (mode < 0 || mode > 2 || xcd_mask == 0) return -1000;
@@ -453,23 +493,26 @@ int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, in
                                      sink.as<uint32_t>());
   XS_CHECK(hipGetLastError());
   XS_CHECK(hipStreamSynchronize(s.s));
-  Event e0, e1;
-  XS_CHECK(hipEventCreate(&e0.e));
-  XS_CHECK(hipEventCreate(&e1.e));
-  XS_CHECK(hipEventRecord(e0.e, s.s));
-  for (int i = 0; i < iters; ++i)
+  double t[3];
+  int rc = time_launches(s.s, iters, [&](int i) {
     k_pinned<<<grid, kBlock, 0, s.s>>>(a.as<const vec4>(), b.as<vec4>(), n, xcd_mask, &ctr[i * per_launch], mode,
                                        sink.as<uint32_t>());
-  XS_CHECK(hipEventRecord(e1.e, s.s));
-  XS_CHECK(hipEventSynchronize(e1.e));
-  XS_CHECK(hipGetLastError());
-  float ms = 0;
-  XS_CHECK(hipEventElapsedTime(&ms, e0.e, e1.e));
-  double per = ms / iters;
-  double moved = static_cast<double>(bytes) * (mode == 2 ? 2.0 : 1.0);
-  if (gbps) *gbps = moved / (per * 1e-3) / 1e9;
-  if (ms_per_iter) *ms_per_iter = per;
+  }, t);
+  if (rc) return rc;
+  const double moved = static_cast<double>(bytes) * (mode == 2 ? 2.0 : 1.0);
+  if (gbps) *gbps = moved / (t[0] * 1e-3) / 1e9;
+  if (ms_per_iter) *ms_per_iter = t[0];
+  if (detail) {
+    detail[0] = moved / (t[1] * 1e-3) / 1e9;
+    detail[1] = moved / (t[2] * 1e-3) / 1e9;
+    detail[2] = t[2];
+  }
   return 0;
+}
+
+int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, int mode, double* gbps,
+                         double* ms_per_iter) {
+  return xs_hbm_bandwidth_xcd_d(dev, bytes, iters, xcd_mask, mode, gbps, ms_per_iter, nullptr);
 }
 
 // Launches `blocks` single-wave workgroups; returns the number of distinct

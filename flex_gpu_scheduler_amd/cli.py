@@ -330,7 +330,7 @@ def cmd_manager(args) -> int:
 
 
 def cmd_node_agent(args) -> int:
-    from .control.node_agent import NodeAgent, hip_health_fn
+    from .control.node_agent import NodeAgent, hip_bandwidth_fn, hip_health_fn
     from .gpu.discovery import discover_host, fake_host
 
     client = _client(args)
@@ -343,6 +343,7 @@ def cmd_node_agent(args) -> int:
                       publish_metrics=not args.no_telemetry, reserved_cpu=args.reserved_cpu,
                       reserved_memory_gib=args.reserved_memory_gib,
                       health_fn=hip_health_fn() if args.health_probe else None,
+                      bandwidth_fn=hip_bandwidth_fn() if args.bandwidth_probe else None,
                       kubelet_managed=args.kubelet_managed).start()
     if args.device_plugin:
         from .control.device_plugin import start_plugins
@@ -496,6 +497,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--telemetry-period", type=float, default=60.0)
     p.add_argument("--no-telemetry", action="store_true")
     p.add_argument("--health-probe", action="store_true", help="run the HIP health probe on each GPU")
+    p.add_argument("--bandwidth-probe", action="store_true",
+                   help="measure HBM bandwidth per compute-partition size on each GPU and publish it "
+                        "(amd.com/gpu-hbm-bandwidth)")
     p.add_argument("--reserved-cpu", type=int, default=0)
     p.add_argument("--reserved-memory-gib", type=int, default=0)
     p.add_argument("--device-plugin", action="store_true",

@@ -33,6 +33,8 @@ from .client import Client, is_conflict
 
 log = logging.getLogger(__name__)
 
+# Per-GPU HBM bandwidth by compute-partition size (NodeAgent.measure_bandwidth).
+BANDWIDTH_ANNOTATION = "amd.com/gpu-hbm-bandwidth"
 UNHEALTHY_TAINT = {"key": "amd.com/gpu-unhealthy", "value": "true", "effect": "NoSchedule"}
 MEMORY_PARTITION_LABEL = "amd.com/gpu.memory-partition"
 HIVE_LABEL = "amd.com/xgmi.hive"
@@ -46,13 +48,18 @@ class NodeAgent:
     def __init__(self, client: Client, node_name: str, *, host_fn: Callable[[], HostInfo] | None = None,
                  root: str = "/", labels: dict | None = None, reserved_cpu: int = 0, reserved_memory_gib: int = 0,
                  heartbeat: float = 10.0, telemetry_period: float = 60.0, publish_metrics: bool = True,
-                 health_fn: Callable[[int], bool] | None = None, sampler=None, kubelet_managed: bool = False):
+                 health_fn: Callable[[int], bool] | None = None, sampler=None, kubelet_managed: bool = False,
+                 bandwidth_fn: Callable[[int], dict] | None = None):
         self.client, self.name = client, node_name
         self.host_fn = host_fn or (lambda: discover_host(root))
         self.labels = dict(labels or {})
         self.reserved_cpu, self.reserved_memory_gib = reserved_cpu, reserved_memory_gib
         self.heartbeat, self.telemetry_period = heartbeat, telemetry_period
         self.health_fn = health_fn
+        # HBM bandwidth per compute-partition size, per GPU (ops/hip_probe.py
+        # partition_table): measured once per GPU and published with the node.
+        self.bandwidth_fn = bandwidth_fn
+        self.bandwidth: dict[int, dict] = {}
         self.publish_metrics = publish_metrics
         self._sampler = sampler
         self._root = root
@@ -85,6 +92,21 @@ class NodeAgent:
                 bad.add(g.index)
         return bad
 
+    def measure_bandwidth(self, host: HostInfo) -> None:
+        """Partition bandwidth table per healthy GPU (HIP ordinal order, as
+        check_health), measured the first time a GPU is seen."""
+        if self.bandwidth_fn is None:
+            return
+        visible = sorted((g for g in host.gpus if g.kfd_node is not None), key=lambda g: g.kfd_node)
+        targets = [(i, g) for i, g in enumerate(visible)] if visible else [(g.index, g) for g in host.gpus]
+        for ordinal, g in targets:
+            if g.index in self.bandwidth or g.index in self.unhealthy:
+                continue
+            try:
+                self.bandwidth[g.index] = self.bandwidth_fn(ordinal)
+            except Exception as e:  # noqa: BLE001
+                log.warning("bandwidth probe GPU %d failed: %s", g.index, e)
+
     def build_node(self, host: HostInfo, unhealthy: set[int] = frozenset()) -> dict:
         healthy = [g for g in host.gpus if g.index not in unhealthy]
         infos = [g.to_gpu_info() for g in healthy]
@@ -110,6 +132,9 @@ class NodeAgent:
                          xgmiLinkMBps=max((lk.bandwidth_mbps for lk in g.xgmi_links), default=0))
         topo["unhealthy"] = sorted(unhealthy)
         node["metadata"]["annotations"][TOPOLOGY_ANNOTATION] = json.dumps(topo, sort_keys=True)
+        if self.bandwidth:
+            node["metadata"]["annotations"][BANDWIDTH_ANNOTATION] = json.dumps(
+                {str(i): t for i, t in sorted(self.bandwidth.items()) if i not in unhealthy}, sort_keys=True)
         # Capacity reports the hardware; allocatable withholds unhealthy GPUs.
         cap = dict(node["status"]["allocatable"])
         cap[GPU] = str(len(host.gpus))
@@ -184,6 +209,7 @@ class NodeAgent:
     def sync(self) -> HostInfo:
         host = self.host_fn()
         self.unhealthy = self.check_health(host)
+        self.measure_bandwidth(host)
         for dp in self.device_plugins:
             dp.host = host
             dp.set_unhealthy(self.unhealthy)
@@ -250,6 +276,15 @@ def hip_health_fn() -> Callable[[int], bool]:
     # HBM pattern/checksum and an exact-integer MFMA tile: a GPU whose matrix
     # cores mis-compute is withheld even if its memory checks out.
     return lambda dev: bool(p.health(dev)["healthy"]) and bool(p.mfma_check(dev)["healthy"])
+
+
+def hip_bandwidth_fn(nbytes: int = 1 << 30, iters: int = 10) -> Callable[[int], dict]:
+    """Partition bandwidth table backed by the HIP XCD-pinned streaming probe
+    (read and copy over a 1 GiB working set per CPX/QPX/DPX/SPX XCD set)."""
+    from ..ops.hip_probe import probe
+
+    p = probe()
+    return lambda dev: p.partition_table(dev, nbytes, iters)
 
 
 def run_forever(agent: NodeAgent) -> None:  # pragma: no cover - CLI

@@ -25,11 +25,22 @@ class ProbeError(RuntimeError):
 
 @dataclass
 class Bandwidth:
+    """`gbps` / `ms_per_iter`: the median launch, each timed by its own event
+    pair (what rocprofv3 reports as the dispatch time). `best_gbps`: the
+    fastest launch. `batch_gbps`: back-to-back launches including the gaps
+    between them."""
     mode: str
     bytes: int
     gbps: float
     ms_per_iter: float
     cu_limit: int
+    best_gbps: float = 0.0
+    batch_gbps: float = 0.0
+
+
+# Working sets default to 1 GiB per array: 4x the MI355X's 256 MB Infinity
+# Cache, so a streaming rate is HBM's, not the cache's.
+DEFAULT_BYTES = 1 << 30
 
 
 class HipProbe:
@@ -55,6 +66,12 @@ class HipProbe:
                                          ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.xs_hbm_bandwidth_xcd.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.xs_hbm_bandwidth_d.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double)]
+        L.xs_hbm_bandwidth_xcd_d.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32,
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.xs_xcd_census.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                     ctypes.POINTER(ctypes.c_int)]
         L.xs_health_check.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_ulonglong),
@@ -82,13 +99,15 @@ class HipProbe:
             raise self._err(rc, "device_props")
         return json.loads(buf.value.decode())
 
-    def hbm_bandwidth(self, dev: int = 0, nbytes: int = 1 << 30, iters: int = 20, cu_limit: int = 0,
-                      mode: str = "copy") -> Bandwidth:
+    def hbm_bandwidth(self, dev: int = 0, nbytes: int = DEFAULT_BYTES, iters: int = 20, cu_limit: int = 0,
+                      mode: str = "copy", variant: int = 0) -> Bandwidth:
         g, ms = ctypes.c_double(), ctypes.c_double()
-        rc = self.lib.xs_hbm_bandwidth(dev, nbytes, iters, cu_limit, MODES[mode], ctypes.byref(g), ctypes.byref(ms))
+        d = (ctypes.c_double * 3)()
+        rc = self.lib.xs_hbm_bandwidth_d(dev, nbytes, iters, cu_limit, MODES[mode], variant, ctypes.byref(g),
+                                         ctypes.byref(ms), d)
         if rc != 0:
             raise self._err(rc, "hbm_bandwidth")
-        return Bandwidth(mode, nbytes, g.value, ms.value, cu_limit)
+        return Bandwidth(mode, nbytes, g.value, ms.value, cu_limit, d[0], d[1])
 
     @staticmethod
     def variant(unroll: int = 4, nontemporal: bool = True, blocks_per_cu: int = 8) -> int:
@@ -96,14 +115,10 @@ class HipProbe:
 
     def hbm_bandwidth_variant(self, dev: int, nbytes: int, iters: int, mode: str, unroll: int, nontemporal: bool,
                               blocks_per_cu: int, cu_limit: int = 0) -> Bandwidth:
-        g, ms = ctypes.c_double(), ctypes.c_double()
-        v = self.variant(unroll, nontemporal, blocks_per_cu)
-        rc = self.lib.xs_hbm_bandwidth_v(dev, nbytes, iters, cu_limit, MODES[mode], v, ctypes.byref(g), ctypes.byref(ms))
-        if rc != 0:
-            raise self._err(rc, "hbm_bandwidth_v")
-        return Bandwidth(mode, nbytes, g.value, ms.value, cu_limit)
+        return self.hbm_bandwidth(dev, nbytes, iters, cu_limit, mode,
+                                  variant=self.variant(unroll, nontemporal, blocks_per_cu))
 
-    def tune(self, dev: int = 0, mode: str = "copy", nbytes: int = 1 << 30, iters: int = 10) -> dict:
+    def tune(self, dev: int = 0, mode: str = "copy", nbytes: int = DEFAULT_BYTES, iters: int = 10) -> dict:
         """Sweep unroll x cache policy x workgroups/CU; return the fastest."""
         results = []
         for unroll in (1, 4, 8):
@@ -174,15 +189,29 @@ class HipProbe:
         if rc != 0:
             raise self._err(rc, "pinned_op")
 
-    def hbm_bandwidth_xcd(self, dev: int = 0, xcd_mask: int = 0x1, nbytes: int = 1 << 30, iters: int = 10,
+    def hbm_bandwidth_xcd(self, dev: int = 0, xcd_mask: int = 0x1, nbytes: int = DEFAULT_BYTES, iters: int = 10,
                           mode: str = "read") -> Bandwidth:
-        """HBM bandwidth pulled by the workgroups on the XCDs of `xcd_mask`
-        only — what one CPX (1 XCD) / QPX (2) / DPX (4) partition can stream."""
         g, ms = ctypes.c_double(), ctypes.c_double()
-        rc = self.lib.xs_hbm_bandwidth_xcd(dev, nbytes, iters, xcd_mask, MODES[mode], ctypes.byref(g), ctypes.byref(ms))
+        d = (ctypes.c_double * 3)()
+        rc = self.lib.xs_hbm_bandwidth_xcd_d(dev, nbytes, iters, xcd_mask, MODES[mode], ctypes.byref(g),
+                                             ctypes.byref(ms), d)
         if rc != 0:
             raise self._err(rc, "hbm_bandwidth_xcd")
-        return Bandwidth(mode, nbytes, g.value, ms.value, bin(xcd_mask).count("1") * 32)
+        return Bandwidth(mode, nbytes, g.value, ms.value, bin(xcd_mask).count("1") * 32, d[0], d[1])
+
+    def partition_table(self, dev: int = 0, nbytes: int = DEFAULT_BYTES, iters: int = 10) -> dict:
+        """HBM read/copy GB/s that the CUs of one compute partition pull, for
+        each partition size of an MI355X (CPX = 1 XCD, QPX = 2, DPX = 4,
+        SPX = 8), measured on the XCDs a partition of that size would own.
+        The node agent publishes it with the GPU's health (gpu/telemetry)."""
+        rows = {}
+        for mode_name, xcds in (("CPX", 1), ("QPX", 2), ("DPX", 4), ("SPX", 8)):
+            mask = (1 << xcds) - 1
+            r = self.hbm_bandwidth_xcd(dev, mask, nbytes, iters, "read")
+            c = self.hbm_bandwidth_xcd(dev, mask, nbytes, iters, "copy")
+            rows[mode_name] = {"xcds": xcds, "cus": xcds * 32, "read_GBps": round(r.gbps, 1),
+                               "copy_GBps": round(c.gbps, 1), "read_ms": round(r.ms_per_iter, 4)}
+        return {"bytes": nbytes, "timing": "median of per-launch event pairs", "partitions": rows}
 
     def xcd_census(self, dev: int = 0, blocks: int = 4096) -> dict:
         hist = (ctypes.c_int * 8)()

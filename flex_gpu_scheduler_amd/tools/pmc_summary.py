@@ -1,13 +1,20 @@
-"""Summarise `scripts/pmc_round.sh` output into a markdown table.
+"""Summarise `scripts/pmc_round.sh` output into markdown tables.
 
-    python -m flex_gpu_scheduler_amd.tools.pmc_summary gpurun_out/r3a > profiles/r3a_pmc_probe_summary.md
+    python -m flex_gpu_scheduler_amd.tools.pmc_summary gpurun_out/r4d > profiles/r4d_pmc_probe_summary.md
 
-For every counter pass (`pmc_<name>/pmc_counter_collection.csv` plus the
-probe's own JSON line in `pmc_<name>.log`) it lists, per kernel, the number
-of dispatches and the counters per dispatch, and derives the HBM traffic:
-FETCH_SIZE and WRITE_SIZE are in KiB, so bytes per dispatch against the
-bytes the kernel must move tells whether it over-fetches, and the probe's
-timing turns the bytes into GB/s and % of the 8 TB/s HBM3E peak.
+Every streaming probe ran in two counter passes, FETCH_SIZE and WRITE_SIZE
+(`pmc_<probe>_fetch`, `pmc_<probe>_write`; one pass for read-only probes),
+each with --kernel-trace and the probe's own JSON line in `pmc_<name>.log`.
+Per probe the table gives:
+
+* the bytes the counters saw per dispatch against the bytes the kernel must
+  move (the probe's read_bytes / write_bytes): FETCH_SIZE and WRITE_SIZE are
+  in KiB, and gfx950 counts 64 B per 128-B read request in FETCH_SIZE, so the
+  read traffic is 2 x FETCH_SIZE;
+* the median dispatch time of the measured kernel in the trace (both
+  passes), and the GB/s it implies for the counted bytes ("counter GB/s");
+* the probe's own figure: the median of its per-launch event pairs;
+* the difference between the two (the probe must agree within 5 %).
 """
 from __future__ import annotations
 
@@ -16,6 +23,7 @@ import glob
 import json
 import os
 import re
+import statistics
 import sys
 from collections import defaultdict
 
@@ -38,53 +46,92 @@ def _probe_line(log: str) -> dict:
     return {}
 
 
+def _pass(d: str) -> dict[str, dict]:
+    """kernel -> {"ns": [dispatch ns...], "counters": {name: per-dispatch mean}}."""
+    csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not csvs:
+        return {}
+    per: dict[str, dict] = defaultdict(lambda: {"disp": {}, "sum": defaultdict(float)})
+    with open(csvs[0]) as f:
+        for r in csv.DictReader(f):
+            k = _short(r["Kernel_Name"])
+            per[k]["disp"][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            per[k]["sum"][r["Counter_Name"]] += float(r["Counter_Value"])
+    out = {}
+    for k, v in per.items():
+        nd = len(v["disp"])
+        out[k] = {"ns": sorted(v["disp"].values()), "counters": {c: s / nd for c, s in v["sum"].items()}}
+    return out
+
+
+def _measured_kernel(kernels: dict[str, dict], probe: dict) -> str | None:
+    """The probe's kernel in a pass: not the runtime's fills, not the warm-up
+    write of the buffers (k_write<4, true>) unless the probe is a write."""
+    want = "k_pinned" if str(probe.get("kernel", "")).startswith("k_pinned") else None
+    best = None
+    for k, v in kernels.items():
+        if k.startswith("__amd_rocclr"):
+            continue
+        if want and not k.startswith(want):
+            continue
+        if not want and k == "k_write<4, true>" and probe.get("kernel") != "hbm-write":
+            continue
+        if best is None or len(v["ns"]) > len(kernels[best]["ns"]):
+            best = k
+    return best
+
+
 def summarize(root: str) -> str:
-    rows = []
+    passes: dict[str, dict[str, str]] = defaultdict(dict)  # probe -> {"fetch"|"write"|"": dir}
     for d in sorted(glob.glob(os.path.join(root, "pmc_*"))):
         if not os.path.isdir(d):
             continue
         name = os.path.basename(d)[4:]
-        csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-        if not csvs:
+        m = re.match(r"(.+)_(fetch|write)$", name)
+        probe, kind = (m.group(1), m.group(2)) if m else (name, "")
+        passes[probe][kind] = d
+    lines = ["| probe | kernel | bytes to move per dispatch | counted per dispatch | median dispatch (trace) | "
+             "counter GB/s | probe GB/s (median launch) | probe vs counter |",
+             "|---|---|---|---|---|---|---|---|"]
+    other = []
+    for probe, kinds in sorted(passes.items()):
+        ns_all: list[int] = []
+        read_b = write_b = None
+        kernel = None
+        pj: dict = {}
+        for kind, d in sorted(kinds.items()):
+            kern = _pass(d)
+            pj = _probe_line(d + ".log") or pj
+            k = _measured_kernel(kern, pj)
+            if k is None:
+                continue
+            kernel = k
+            ns_all += kern[k]["ns"][1:] if len(kern[k]["ns"]) > 2 else kern[k]["ns"]  # first: cold
+            c = kern[k]["counters"]
+            if "FETCH_SIZE" in c:
+                read_b = 2 * c["FETCH_SIZE"] * 1024
+            if "WRITE_SIZE" in c:
+                write_b = c["WRITE_SIZE"] * 1024
+            if not ("FETCH_SIZE" in c or "WRITE_SIZE" in c):
+                other.append(f"| {probe} | `{k}` | " + ", ".join(f"{n}={v:,.0f}" for n, v in sorted(c.items())) +
+                             f" | {json.dumps(pj)} |")
+        if kernel is None or "read_bytes" not in pj:
             continue
-        per: dict[str, dict] = defaultdict(lambda: {"dispatches": {}, "counters": defaultdict(float)})
-        with open(csvs[0]) as f:
-            for r in csv.DictReader(f):
-                k = _short(r["Kernel_Name"])
-                per[k]["dispatches"][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                per[k]["counters"][r["Counter_Name"]] += float(r["Counter_Value"])
-        probe = _probe_line(os.path.join(root, f"pmc_{name}.log"))
-        for k, v in per.items():
-            nd = len(v["dispatches"])
-            cnt = {c: val / nd for c, val in v["counters"].items()}
-            ns = sum(v["dispatches"].values()) / nd
-            rows.append((name, k, nd, cnt, ns, probe))
-    out = ["| pass | kernel | dispatches | counters per dispatch | HBM bytes per dispatch | counter GB/s "
-           "(bytes / dispatch time) | probe-reported |",
-           "|---|---|---|---|---|---|---|"]
-    for name, k, nd, cnt, ns, probe in rows:
-        if k.startswith("__amd_rocclr"):
-            continue  # runtime fills/copies around the probe
-        cs = ", ".join(f"{c}={v:,.0f}" for c, v in sorted(cnt.items()))
-        moved, nbytes = [], 0.0
-        if "FETCH_SIZE" in cnt:
-            # gfx950 counts 64 B per 128-B read request in FETCH_SIZE: every
-            # streaming read reports exactly half its bytes (r1f and r3
-            # passes), so the read traffic is 2 x FETCH_SIZE.
-            nbytes += 2 * cnt["FETCH_SIZE"] * 1024
-            moved.append(f"read {2 * cnt['FETCH_SIZE'] * 1024 / 2**30:.3f} GiB (2 x FETCH_SIZE)")
-        if "WRITE_SIZE" in cnt:
-            nbytes += cnt["WRITE_SIZE"] * 1024
-            moved.append(f"written {cnt['WRITE_SIZE'] * 1024 / 2**30:.3f} GiB")
-        cgb = f"{nbytes / ns:,.0f}" if nbytes and ns > 0 and nbytes > (1 << 20) else ""
-        pr = ""
-        # The probe's line belongs to the measured kernel, not the buffer fill.
-        if probe and "k_write<4, true>" not in k:
-            gbps = probe.get("GBps") or 0
-            pr = f"{gbps:,.0f} GB/s = {100 * gbps / HBM_PEAK_GBPS:.1f}% of 8 TB/s" if gbps else \
-                json.dumps(probe)
-        out.append(f"| {name} | `{k}` | {nd} | {cs} | {'; '.join(moved)} | {cgb} | {pr} |")
-    return "\n".join(out) + "\n"
+        want_r, want_w = pj["read_bytes"], pj["write_bytes"]
+        counted = (read_b or 0) + (write_b or 0)
+        med = statistics.median(ns_all) if ns_all else 0
+        cgb = counted / med if med else 0.0
+        pgb = float(pj.get("GBps") or 0)
+        diff = f"{100 * (pgb - cgb) / cgb:+.1f}%" if cgb else ""
+        lines.append(
+            f"| {probe} | `{kernel}` | read {want_r / 2**30:.2f} GiB, write {want_w / 2**30:.2f} GiB | "
+            f"read {0 if read_b is None else read_b / 2**30:.3f} GiB, "
+            f"write {0 if write_b is None else write_b / 2**30:.3f} GiB | {med / 1e3:,.1f} us | {cgb:,.0f} | "
+            f"{pgb:,.0f} ({100 * pgb / HBM_PEAK_GBPS:.1f}% of 8 TB/s) | {diff} |")
+    out = "\n".join(lines) + "\n"
+    if other:
+        out += "\n| pass | kernel | counters per dispatch | probe |\n|---|---|---|---|\n" + "\n".join(other) + "\n"
+    return out
 
 
 def main() -> int:

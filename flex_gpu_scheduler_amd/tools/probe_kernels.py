@@ -5,6 +5,7 @@
     PROBE: mfma | hbm-read | hbm-copy | hbm-triad | hbm-write
            | xcd-read-K | xcd-copy-K   (k_pinned on the first K XCDs: K=1 is
              one CPX partition's CUs, 2 QPX, 4 DPX, 8 the whole GPU)
+           | partitions                (the node agent's per-partition table)
 
 Prints the probe's own measurement as one JSON line, so a counter pass can be
 cross-checked against the timing the probe reports.
@@ -26,16 +27,24 @@ def main() -> int:
         r = pr.mfma_peak(dev, 0xFF, iters=8192)
         out = {"kernel": "k_mfma_peak", "TFLOPs": round(r["tflops"], 1), "ms": round(r["ms"], 3)}
     elif what in ("hbm-read", "hbm-copy", "hbm-triad", "hbm-write"):
-        bw = pr.hbm_bandwidth(dev, 2 << 30, iters=iters, mode=what.split("-")[1])
-        arrays = {"read": 1, "write": 1, "copy": 2, "triad": 3}[what.split("-")[1]]
-        out = {"kernel": what, "iters": iters, "bytes_per_array": 2 << 30, "arrays": arrays, "GBps": round(bw.gbps, 1),
-               "ms": round(bw.ms_per_iter, 4), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
+        mode = what.split("-")[1]
+        bw = pr.hbm_bandwidth(dev, 2 << 30, iters=iters, mode=mode)
+        arrays = {"read": 1, "write": 1, "copy": 2, "triad": 3}[mode]
+        reads, writes = {"read": (1, 0), "write": (0, 1), "copy": (1, 1), "triad": (2, 1)}[mode]
+        out = {"kernel": what, "iters": iters, "bytes_per_array": 2 << 30, "arrays": arrays,
+               "read_bytes": reads * (2 << 30), "write_bytes": writes * (2 << 30),
+               "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4), "best_GBps": round(bw.best_gbps, 1),
+               "batch_GBps": round(bw.batch_gbps, 1), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
     elif what.startswith("xcd-"):
         _, mode, k = what.split("-")
         mask = (1 << int(k)) - 1
         bw = pr.hbm_bandwidth_xcd(dev, mask, 1 << 30, iters=iters, mode=mode)
         out = {"kernel": f"k_pinned[{mode}]", "iters": iters, "xcds": int(k), "xcd_mask": mask, "bytes": 1 << 30,
-               "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
+               "read_bytes": 1 << 30, "write_bytes": (1 << 30) if mode == "copy" else 0,
+               "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4), "best_GBps": round(bw.best_gbps, 1),
+               "batch_GBps": round(bw.batch_gbps, 1), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
+    elif what == "partitions":
+        out = pr.partition_table(dev, 1 << 30, iters)
     else:
         raise SystemExit(f"unknown probe {what!r}")
     print(json.dumps(out))

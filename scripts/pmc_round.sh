@@ -1,6 +1,10 @@
 #!/usr/bin/env bash
 # Hardware-counter passes over the HIP probe kernels (one rocprofv3 --pmc run
 # per counter group, each under its own SIGKILL timeout; no tracing domains).
+# Every streaming probe gets a FETCH_SIZE pass and, when it writes, a
+# WRITE_SIZE pass (the two do not fit one pass: 3 + 2 TCC counters), so
+# tools/pmc_summary.py can check the bytes each dispatch moves and compare
+# the probe's own median launch time with the dispatch times of the trace.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -15,15 +19,12 @@ run() {  # name probe counters...
   echo "[pmc] $name rc=$rc" | tee -a "$OUT/pmc_steps.log"
   return $rc
 }
-timeout -s KILL 60 rocprofv3 --list-avail > "$OUT/pmc_list_avail.txt" 2>&1 || true
-run mfma mfma SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE &&
-run hbm_read hbm-read FETCH_SIZE GRBM_GUI_ACTIVE &&
-run hbm_copy hbm-copy WRITE_SIZE GRBM_GUI_ACTIVE &&
-run triad_fetch hbm-triad FETCH_SIZE GRBM_GUI_ACTIVE &&
-run triad_write hbm-triad WRITE_SIZE GRBM_GUI_ACTIVE &&
-run xcd1_read xcd-read-1 FETCH_SIZE GRBM_GUI_ACTIVE &&
-run xcd2_read xcd-read-2 FETCH_SIZE GRBM_GUI_ACTIVE &&
-run xcd4_read xcd-read-4 FETCH_SIZE GRBM_GUI_ACTIVE &&
-run xcd8_read xcd-read-8 FETCH_SIZE GRBM_GUI_ACTIVE &&
-run xcd1_copy xcd-copy-1 WRITE_SIZE GRBM_GUI_ACTIVE
+run mfma mfma SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE || exit $?
+for p in hbm-read xcd-read-1 xcd-read-2 xcd-read-4 xcd-read-8; do
+  run "${p}_fetch" "$p" FETCH_SIZE GRBM_GUI_ACTIVE || exit $?
+done
+for p in hbm-copy hbm-triad xcd-copy-1 xcd-copy-2 xcd-copy-4 xcd-copy-8; do
+  run "${p}_fetch" "$p" FETCH_SIZE GRBM_GUI_ACTIVE || exit $?
+  run "${p}_write" "$p" WRITE_SIZE GRBM_GUI_ACTIVE || exit $?
+done
 echo "[pmc] done" | tee -a "$OUT/pmc_steps.log"

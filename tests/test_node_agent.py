@@ -175,3 +175,28 @@ def test_load_watcher_service_and_fetcher(store):
     finally:
         http.stop()
     assert merge_documents([]) is None
+
+
+def test_partition_bandwidth_table_is_published(store):
+    """measure_bandwidth runs the (injected) partition probe once per healthy
+    GPU and build_node publishes the table as amd.com/gpu-hbm-bandwidth."""
+    import json as _json
+
+    from flex_gpu_scheduler_amd.control import LocalClient
+    from flex_gpu_scheduler_amd.control.node_agent import BANDWIDTH_ANNOTATION, NodeAgent
+    from flex_gpu_scheduler_amd.gpu.discovery import fake_host
+
+    calls = []
+
+    def bw(dev):
+        calls.append(dev)
+        return {"bytes": 1 << 30, "partitions": {"CPX": {"xcds": 1, "read_GBps": 1000.0 + dev},
+                                                  "SPX": {"xcds": 8, "read_GBps": 5000.0 + dev}}}
+
+    agent = NodeAgent(LocalClient(store), "n0", host_fn=lambda: fake_host(4), bandwidth_fn=bw,
+                      health_fn=lambda dev: dev != 2, publish_metrics=False)
+    agent.sync()
+    agent.sync()  # measured once per GPU
+    assert sorted(calls) == [0, 1, 3]
+    ann = _json.loads(store.get("nodes", "", "n0")["metadata"]["annotations"][BANDWIDTH_ANNOTATION])
+    assert sorted(ann) == ["0", "1", "3"] and ann["3"]["partitions"]["SPX"]["read_GBps"] == 5003.0
