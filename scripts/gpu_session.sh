@@ -63,7 +63,7 @@ for step in "$@"; do
       python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_1024 --nodes 1024 &&
       cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
       for i in 1 2 3; do
-        for v in 0 1; do
+        for v in ${AB_VALUES:-0 1}; do
           echo "$var=$v $(env "$var=$v" timeout -k 5 200 taskset -c "$cpus" abbin/xsched_stress /tmp/s_1024 6 | tail -1)" \
             >> "$OUT/ab1024.txt" || exit 1
         done
