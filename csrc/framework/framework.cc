@@ -459,9 +459,44 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
     }
   };
   if (handle_.parallelizer->plan_inline(static_cast<int>(n), &score_site_)) {
-    // Serial path: a plain loop, no std::function dispatch per node.
+    // Serial path, plugin-major: each scorer runs over every node that needs
+    // it in one call (Plugin::score_many), equivalence-cache hits copied in.
     const int64_t s0 = Parallelizer::now_ns();
-    for (size_t i = 0; i < n && !failed.load(std::memory_order_relaxed); ++i) score_node(i);
+    thread_local std::vector<char> hit_buf;
+    std::vector<char>& hit = hit_buf;
+    hit.assign(n, 0);
+    bool any_hit = false;
+    if (eq)
+      for (size_t i = 0; i < n; ++i) {
+        const EqSlot* slot = eq->slots[i];
+        hit[i] = slot && slot->score_gen == nodes[i]->generation && slot->raw.size() == ns;
+        any_hit = any_hit || hit[i];
+      }
+    for (size_t k = 0; k < ns; ++k) {
+      std::vector<NodeScore>& row = per[k];
+      if (skip[k]) {
+        for (size_t i = 0; i < n; ++i) row[i].score = 0;
+        continue;
+      }
+      const bool reuse = any_hit && eq->local[k];
+      if (reuse)
+        for (size_t i = 0; i < n; ++i)
+          if (hit[i]) row[i].score = eq->slots[i]->raw[k];
+      Status st = scorers_[k].first->score_many(s, p, nodes, reuse ? hit.data() : nullptr, row);
+      if (!st.is_success()) {
+        err = "running Score plugin " + scorers_[k].first->name() + ": " + st.message();
+        failed.store(true);
+        break;
+      }
+    }
+    if (eq && !failed.load())
+      for (size_t i = 0; i < n; ++i) {
+        EqSlot* slot = eq->slots[i];
+        if (!slot || hit[i]) continue;
+        slot->raw.resize(ns);
+        for (size_t k = 0; k < ns; ++k) slot->raw[k] = per[k][i].score;
+        slot->score_gen = nodes[i]->generation;
+      }
     Parallelizer::record_inline(&score_site_, Parallelizer::now_ns() - s0, static_cast<int>(n), static_cast<int>(n));
   } else {
     handle_.parallelizer->until_forked(static_cast<int>(n), [&](int i) { score_node(static_cast<size_t>(i)); },

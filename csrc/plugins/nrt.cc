@@ -376,6 +376,16 @@ class TopologyMatch : public Plugin {
     return {0, {}};
   }
 
+  // XGMIGangAffinity over many nodes: the gang context is read once.
+  Status score_many(CycleState& s, const Pod& p, const NodeList& nodes, const char* skip,
+                    std::vector<NodeScore>& out) override {
+    const GangCtx* c = strategy_ == Strategy::XGMI ? s.read_as<GangCtx>(kGangKey) : nullptr;
+    if (!c) return Plugin::score_many(s, p, nodes, skip, out);
+    for (size_t i = 0; i < nodes.size(); ++i)
+      if (!skip || !skip[i]) out[i].score = gang_score(*c, *nodes[i]);
+    return {};
+  }
+
   std::vector<ClusterEvent> events_to_register() const override {
     return {{"Pod", kDelete, ""}, {"Node", kAdd | kUpdateNodeAllocatable, ""}, {"NodeResourceTopology", kAdd | kUpdate, ""}};
   }
