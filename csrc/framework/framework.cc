@@ -469,7 +469,8 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
     if (eq)
       for (size_t i = 0; i < n; ++i) {
         const EqSlot* slot = eq->slots[i];
-        hit[i] = slot && slot->score_gen == nodes[i]->generation && slot->raw.size() == ns;
+        const int64_t gen = eq->gens.size() == n ? eq->gens[i] : nodes[i]->generation;
+        hit[i] = slot && slot->score_gen == gen && slot->raw.size() == ns;
         any_hit = any_hit || hit[i];
       }
     for (size_t k = 0; k < ns; ++k) {
@@ -495,7 +496,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
         if (!slot || hit[i]) continue;
         slot->raw.resize(ns);
         for (size_t k = 0; k < ns; ++k) slot->raw[k] = per[k][i].score;
-        slot->score_gen = nodes[i]->generation;
+        slot->score_gen = eq->gens.size() == n ? eq->gens[i] : nodes[i]->generation;
       }
     Parallelizer::record_inline(&score_site_, Parallelizer::now_ns() - s0, static_cast<int>(n), static_cast<int>(n));
   } else {

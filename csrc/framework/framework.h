@@ -45,6 +45,7 @@ struct EqSlot {
 struct EqScoreCache {
   std::vector<char> local;       // per scorer: raw score is node-local for this pod
   std::vector<EqSlot*> slots;    // per node passed to run_score (nullptr: uncached)
+  std::vector<int64_t> gens;     // the nodes' generations (Snapshot::gen), same order
 };
 
 class Framework {

@@ -302,6 +302,9 @@ struct Snapshot {
   std::vector<std::string> names;
   std::unordered_map<std::string, NodeInfoPtr> by_name;
   std::unordered_map<std::string, size_t> index;  // name -> position in `nodes`
+  // nodes[i]->generation, contiguous: equivalence-cache checks on the Filter
+  // and Score paths compare generations without touching each NodeInfo.
+  std::vector<int64_t> gen;
   // Nodes with affinity / required anti-affinity pods, in no particular
   // order. Kept incrementally by the cache: *_pos[i] is node i's slot in the
   // list (-1 if absent) and *_idx the reverse, so a refresh touches only the

@@ -45,6 +45,10 @@ struct GangCtx : StateData {
   int64_t remaining = 0;    // members still to place (>= 1)
   enum { kWhole, kXcd } kind = kWhole;
   int64_t amount = 0;       // per member: GPUs or XCDs
+  // Snapshot nodes hosting members already (from the cache's group index):
+  // the co-location test then reads only those NodeInfos, not every node's.
+  std::vector<const NodeInfo*> hosts;
+  bool hosts_known = false;
   std::shared_ptr<StateData> clone() const override { return std::make_shared<GangCtx>(*this); }
 };
 constexpr const char* kGangKey = "NodeResourceTopologyMatch/gang";
@@ -310,6 +314,11 @@ class TopologyMatch : public Plugin {
         ctx->remaining = std::max<int64_t>(1, pg->min_member - h_.cache->assigned_in_group(ctx->key));
         ctx->kind = d.kind == GpuDemand::Gpu ? GangCtx::kWhole : GangCtx::kXcd;
         ctx->amount = d.amount;
+        if (h_.snapshot) {
+          for (const auto& node : h_.cache->nodes_of_group(ctx->key))
+            if (auto ni = h_.snapshot->get(node)) ctx->hosts.push_back(ni.get());
+          ctx->hosts_known = true;
+        }
       }
     }
     s.write(kGangKey, ctx);
@@ -337,7 +346,14 @@ class TopologyMatch : public Plugin {
     }
     if (free <= 0) return 0;
     int64_t remaining = c.remaining * per;
-    bool co_located = ni.pg_pods(c.key) > 0;
+    bool co_located;
+    if (c.hosts_known) {
+      co_located = false;
+      for (const NodeInfo* h : c.hosts)
+        if (h == &ni) co_located = ni.pg_pods(c.key) > 0;
+    } else {
+      co_located = ni.pg_pods(c.key) > 0;
+    }
     bool fits_all = remaining <= free;
     if (fits_all && co_located) return 100;
     if (fits_all) return 60 + 30 * remaining / free;  // tightest whole-gang fit first

@@ -36,6 +36,23 @@ void SchedulerCache::group_delta(const Pod& p, int d) {
   auto it = group_assigned_.try_emplace(p.pg_key, 0).first;
   it->second += d;
   if (it->second <= 0) group_assigned_.erase(it);
+  auto& hosts = group_nodes_[p.pg_key];
+  auto h = std::find_if(hosts.begin(), hosts.end(), [&](const auto& e) { return e.first == p.node_name; });
+  if (h == hosts.end()) {
+    if (d > 0) hosts.emplace_back(p.node_name, d);
+  } else if ((h->second += d) <= 0) {
+    hosts.erase(h);
+  }
+  if (hosts.empty()) group_nodes_.erase(p.pg_key);
+}
+
+std::vector<std::string> SchedulerCache::nodes_of_group(uint64_t pg_key) const {
+  std::lock_guard<std::mutex> g(group_mu_);
+  std::vector<std::string> out;
+  auto it = group_nodes_.find(pg_key);
+  if (it != group_nodes_.end())
+    for (const auto& [node, n] : it->second) out.push_back(node);
+  return out;
 }
 
 void SchedulerCache::account_node(const Node* old_node, const Node* new_node) {
@@ -376,6 +393,8 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
       s.by_name[name] = cl;
     }
     structure_changed_ = false;
+    s.gen.resize(s.nodes.size());
+    for (size_t i = 0; i < s.nodes.size(); ++i) s.gen[i] = s.nodes[i]->generation;
     s.have_pods_with_affinity.clear();
     s.have_pods_with_required_anti_affinity.clear();
     s.affinity_idx.clear();
@@ -399,6 +418,7 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
         s.nodes[i] = cl;
         sit->second = cl;
       }
+      s.gen[i] = cl->generation;
       sync_affinity_lists(s, i);
     }
   }

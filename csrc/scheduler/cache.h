@@ -79,6 +79,8 @@ class SchedulerCache {
   // Pods of a PodGroup that are assumed or bound, keyed by Pod::pg_key (a
   // 64-bit hash of "ns/name", as NodeInfo::pg_count).
   int assigned_in_group(uint64_t pg_key) const;
+  // Nodes hosting assumed or bound pods of the group (by Pod::pg_key).
+  std::vector<std::string> nodes_of_group(uint64_t pg_key) const;
   int assigned_in_group(const std::string& pg_full_name) const { return assigned_in_group(pg_key_of(pg_full_name)); }
   // Cache debugger (upstream internal/cache/debugger): compares the cache
   // with the listers' view — `assigned` pods (nodeName set) and Node names —
@@ -139,6 +141,9 @@ class SchedulerCache {
   // PreScore read a gang's count without waiting behind NodeInfo copies.
   mutable std::mutex group_mu_;
   std::unordered_map<uint64_t, int> group_assigned_;
+  // PodGroup key -> (node, members on it): where a gang's assumed or bound
+  // members sit (XGMIGangAffinity's co-location test without a per-node look).
+  std::unordered_map<uint64_t, std::vector<std::pair<std::string, int>>> group_nodes_;
   std::unordered_set<std::string> dirty_;
   bool structure_changed_ = true;
   int64_t generation_ = 0;

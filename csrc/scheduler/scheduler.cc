@@ -1156,16 +1156,17 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     uint64_t sig = 0;
     bool cacheable = true;
     if (nom_mark && nom_mark[pos]) sig = fw.nominated_signature(s, p, nom_list_[pos], &cacheable);
+    const int64_t gen = snapshot_.gen[pos];
     if (sig == 0) {  // no nominated pod counts for this pod: the plain verdict
-      if (slot.filter_gen == ni.generation) {
+      if (slot.filter_gen == gen) {
         *hit = true;
       } else {
         slot.filter = fw.run_filter(s, p, ni);
-        slot.filter_gen = ni.generation;
+        slot.filter_gen = gen;
       }
       return &slot.filter;
     }
-    if (cacheable && slot.nom_gen == ni.generation && slot.nom_sig == sig) {
+    if (cacheable && slot.nom_gen == gen && slot.nom_sig == sig) {
       *hit = true;
       return &slot.nom_filter;
     }
@@ -1175,7 +1176,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       return &own;
     }
     slot.nom_filter = std::move(st);
-    slot.nom_gen = ni.generation;
+    slot.nom_gen = gen;
     slot.nom_sig = sig;
     return &slot.nom_filter;
   };
@@ -1538,7 +1539,11 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         if (eq) fw->local_scorers(*pod, snapshot_, esc.local);
         if (!esc.local.empty()) {
           esc.slots.resize(feasible.size());
-          for (size_t i = 0; i < feasible.size(); ++i) esc.slots[i] = &eq->slots[feasible_pos_buf_[i]];
+          esc.gens.resize(feasible.size());
+          for (size_t i = 0; i < feasible.size(); ++i) {
+            esc.slots[i] = &eq->slots[feasible_pos_buf_[i]];
+            esc.gens[i] = snapshot_.gen[feasible_pos_buf_[i]];
+          }
         }
         if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores, nullptr, esc.local.empty() ? nullptr : &esc);
       }
