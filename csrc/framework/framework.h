@@ -31,6 +31,25 @@ struct ProfileConfig {
 // One (pod template, node) entry of the scheduler's equivalence cache:
 // the Filter verdict and raw (pre-normalization) Score values last computed
 // for that template on that node, valid while the node's generation matches.
+// Raw scores per scorer of one (template, node): inline up to 12 scorers, so
+// a cache hit reads the slot itself and no further heap block.
+class RawScores {
+ public:
+  size_t size() const { return n_; }
+  void resize(size_t n) {
+    if (n > kInline) spill_.resize(n);
+    n_ = n;
+  }
+  int64_t& operator[](size_t i) { return n_ > kInline ? spill_[i] : inl_[i]; }
+  int64_t operator[](size_t i) const { return n_ > kInline ? spill_[i] : inl_[i]; }
+
+ private:
+  static constexpr size_t kInline = 12;  // the default profile plus FlexGPU and NRT score with 10
+  int64_t inl_[kInline] = {};
+  std::vector<int64_t> spill_;
+  size_t n_ = 0;
+};
+
 struct EqSlot {
   int64_t filter_gen = -1;
   Status filter;
@@ -40,7 +59,7 @@ struct EqSlot {
   uint64_t nom_sig = 0;
   Status nom_filter;
   int64_t score_gen = -1;
-  std::vector<int64_t> raw;  // per scorer, in Framework scorer order
+  RawScores raw;  // per scorer, in Framework scorer order
 };
 struct EqScoreCache {
   std::vector<char> local;       // per scorer: raw score is node-local for this pod
