@@ -483,7 +483,8 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
       if (reuse)
         for (size_t i = 0; i < n; ++i)
           if (hit[i]) row[i].score = eq->slots[i]->raw[k];
-      Status st = scorers_[k].first->score_many(s, p, nodes, reuse ? hit.data() : nullptr, row);
+      Status st = scorers_[k].first->score_many(s, p, nodes, reuse ? hit.data() : nullptr, row,
+                                                (eq && eq->pos.size() == n) ? eq->pos.data() : nullptr);
       if (!st.is_success()) {
         err = "running Score plugin " + scorers_[k].first->name() + ": " + st.message();
         failed.store(true);

@@ -65,6 +65,7 @@ struct EqScoreCache {
   std::vector<char> local;       // per scorer: raw score is node-local for this pod
   std::vector<EqSlot*> slots;    // per node passed to run_score (nullptr: uncached)
   std::vector<int64_t> gens;     // the nodes' generations (Snapshot::gen), same order
+  std::vector<int> pos;          // the nodes' snapshot positions, same order
 };
 
 class Framework {

@@ -138,10 +138,11 @@ class Plugin {
   virtual Status pre_score(CycleState& s, const Pod& p, const NodeList& nodes) { return {}; }
   virtual std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) { return {0, {}}; }
   // Raw scores of every node whose `skip` entry is 0 (skip may be null) into
-  // out[i].score, on the calling thread. The default calls score() per node;
-  // plugins with per-cycle state override it to read that state once.
+  // out[i].score, on the calling thread. `pos` (may be null) holds each
+  // node's snapshot position. The default calls score() per node; plugins
+  // with per-cycle state override it to read that state once.
   virtual Status score_many(CycleState& s, const Pod& p, const NodeList& nodes, const char* skip,
-                            std::vector<NodeScore>& out) {
+                            std::vector<NodeScore>& out, const int* pos = nullptr) {
     for (size_t i = 0; i < nodes.size(); ++i) {
       if (skip && skip[i]) continue;
       auto [sc, st] = score(s, p, *nodes[i]);

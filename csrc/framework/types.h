@@ -305,6 +305,8 @@ struct Snapshot {
   // nodes[i]->generation, contiguous: equivalence-cache checks on the Filter
   // and Score paths compare generations without touching each NodeInfo.
   std::vector<int64_t> gen;
+  // nodes[i]->gpu.free_gpus() (whole SPX GPUs free), contiguous likewise.
+  std::vector<int32_t> free_whole;
   // Nodes with affinity / required anti-affinity pods, in no particular
   // order. Kept incrementally by the cache: *_pos[i] is node i's slot in the
   // list (-1 if absent) and *_idx the reverse, so a refresh touches only the

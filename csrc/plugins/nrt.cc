@@ -325,6 +325,25 @@ class TopologyMatch : public Plugin {
     return {};
   }
 
+  static bool co_located(const GangCtx& c, const NodeInfo& ni) {
+    if (!c.hosts_known) return ni.pg_pods(c.key) > 0;
+    for (const NodeInfo* h : c.hosts)
+      if (h == &ni) return ni.pg_pods(c.key) > 0;
+    return false;
+  }
+  static int64_t fit_score(int64_t remaining, int64_t free, bool co) {
+    if (free <= 0) return 0;
+    bool fits_all = remaining <= free;
+    if (fits_all && co) return 100;
+    if (fits_all) return 60 + 30 * remaining / free;  // tightest whole-gang fit first
+    if (co) return 50;
+    return 40 * std::min(free, remaining) / remaining;  // most of the gang on one node
+  }
+  // gang_score for a whole-GPU rank given the node's free GPUs.
+  static int64_t whole_gang_score(const GangCtx& c, int64_t free_gpus, const NodeInfo& ni) {
+    if (free_gpus <= 0) return 0;
+    return fit_score(c.remaining * c.amount, free_gpus, co_located(c, ni));
+  }
   // Gang co-location score in [0, 100] (XGMIGangAffinity).
   static int64_t gang_score(const GangCtx& c, const NodeInfo& ni) {
     if (!c.gang) return 50;
@@ -345,20 +364,7 @@ class TopologyMatch : public Plugin {
       free = L.free_xcds();
     }
     if (free <= 0) return 0;
-    int64_t remaining = c.remaining * per;
-    bool co_located;
-    if (c.hosts_known) {
-      co_located = false;
-      for (const NodeInfo* h : c.hosts)
-        if (h == &ni) co_located = ni.pg_pods(c.key) > 0;
-    } else {
-      co_located = ni.pg_pods(c.key) > 0;
-    }
-    bool fits_all = remaining <= free;
-    if (fits_all && co_located) return 100;
-    if (fits_all) return 60 + 30 * remaining / free;  // tightest whole-gang fit first
-    if (co_located) return 50;
-    return 40 * std::min(free, remaining) / remaining;  // most of the gang on one node
+    return fit_score(c.remaining * per, free, co_located(c, ni));
   }
 
   std::pair<int64_t, Status> score(CycleState& s, const Pod& p, const NodeInfo& ni) override {
@@ -394,9 +400,17 @@ class TopologyMatch : public Plugin {
 
   // XGMIGangAffinity over many nodes: the gang context is read once.
   Status score_many(CycleState& s, const Pod& p, const NodeList& nodes, const char* skip,
-                    std::vector<NodeScore>& out) override {
+                    std::vector<NodeScore>& out, const int* pos) override {
     const GangCtx* c = strategy_ == Strategy::XGMI ? s.read_as<GangCtx>(kGangKey) : nullptr;
-    if (!c) return Plugin::score_many(s, p, nodes, skip, out);
+    if (!c) return Plugin::score_many(s, p, nodes, skip, out, pos);
+    const Snapshot* snap = h_.snapshot;
+    if (pos && snap && c->gang && c->kind == GangCtx::kWhole && snap->free_whole.size() == snap->nodes.size()) {
+      // Whole-GPU ranks: free GPUs from the snapshot's contiguous array; only
+      // the few nodes already hosting the gang are dereferenced.
+      for (size_t i = 0; i < nodes.size(); ++i)
+        if (!skip || !skip[i]) out[i].score = whole_gang_score(*c, snap->free_whole[pos[i]], *nodes[i]);
+      return {};
+    }
     for (size_t i = 0; i < nodes.size(); ++i)
       if (!skip || !skip[i]) out[i].score = gang_score(*c, *nodes[i]);
     return {};

@@ -1540,6 +1540,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         if (!esc.local.empty()) {
           esc.slots.resize(feasible.size());
           esc.gens.resize(feasible.size());
+          esc.pos.assign(feasible_pos_buf_.begin(), feasible_pos_buf_.begin() + feasible.size());
           for (size_t i = 0; i < feasible.size(); ++i) {
             esc.slots[i] = &eq->slots[feasible_pos_buf_[i]];
             esc.gens[i] = snapshot_.gen[feasible_pos_buf_[i]];
