@@ -607,6 +607,8 @@ PYBIND11_MODULE(_xsched, m) {
              d["preemption_attempts"] = st.preemption_attempts;
              d["eq_filter_hits"] = st.eq_filter_hits;
              d["eq_filter_misses"] = st.eq_filter_misses;
+             d["scan_memo_served"] = st.scan_memo_served;
+             d["scan_memo_mismatches"] = st.scan_memo_mismatches;
              d["inflight_bindings"] = s.inflight_bindings();
              d["bind_threads"] = s.bind_threads();
              return d;

@@ -202,6 +202,13 @@ SchedulerOptions SchedulerOptions::from_json(const Json& j) {
   o.status_updates = j["statusUpdates"].as_bool(o.status_updates);
   o.events = j["events"].as_bool(o.events);
   o.equivalence_cache = j["equivalenceCache"].as_bool(o.equivalence_cache);
+  auto env_on = [](const char* var) {
+    const char* v = std::getenv(var);
+    return !v || std::string(v) != "0";
+  };
+  o.gang_window = j["gangWindow"].as_bool(env_on("XSCHED_GANG_WINDOW"));
+  o.scan_memo = j["scanMemo"].as_bool(env_on("XSCHED_SCAN_MEMO"));
+  o.scan_memo_verify = j["scanMemoVerify"].as_bool(false);
   o.trace = j["trace"].as_bool(false);
   o.seed = static_cast<uint64_t>(j["seed"].as_int(0));
   o.dump_on_fit_error = j["dumpOnFitError"].str_or("");
@@ -1017,6 +1024,7 @@ Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
   if (e->epoch != snapshot_.node_epoch || e->slots.size() != snapshot_.nodes.size()) {
     e->epoch = snapshot_.node_epoch;
     e->slots.assign(snapshot_.nodes.size(), EqSlot{});
+    e->scan.valid = false;
   }
   return e.get();
 }
@@ -1119,8 +1127,7 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   // sibling's Filter verdicts and node-local scores for every node but the
   // one the sibling took, and the gang's candidates are the same nodes
   // XGMIGangAffinity ranks.
-  static const bool gang_window = !std::getenv("XSCHED_GANG_WINDOW") || std::string(std::getenv("XSCHED_GANG_WINDOW")) != "0";
-  if (gang_window && !full_diagnosis && p.pg_key) {
+  if (opts_.gang_window && !full_diagnosis && p.pg_key) {
     if (p.pg_key == window_gang_ && p.template_hash == window_tmpl_ && window_n_ == n) {
       start = window_start_;
     } else {
@@ -1180,11 +1187,94 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     slot.nom_sig = sig;
     return &slot.nom_filter;
   };
-  if (parallelizer_->plan_inline(n, &filter_site_)) {
+  // The template's last scan of this window (EqEntry::scan): a gang rank
+  // after its sibling re-evaluates only the scanned nodes whose version
+  // changed since (usually the node the sibling took) and re-cuts the list at
+  // numFeasibleNodesToFind, instead of walking the whole window again.
+  EqEntry::ScanMemo* memo =
+      (opts_.scan_memo && eq && eq_filter && !nom_mark && !full_diagnosis && !ext) ? &eq->scan : nullptr;
+  if (memo && !(memo->valid && memo->start == start && memo->n == n && memo->to_find == to_find &&
+                memo->epoch == snapshot_.node_epoch))
+    memo->valid = false;
+  const bool inline_ok = parallelizer_->plan_inline(n, &filter_site_);
+  bool served = false;
+  if (memo && memo->valid && inline_ok) {
+    bool ok = true;
+    int reevaluated = 0;
+    const int m = memo->processed;
+    auto at = [&](int off) { return start + off >= n ? start + off - n : start + off; };
+    for (int off = 0; off < m && ok; ++off) {
+      const int pos = at(off);
+      if (memo->gens[off] == snapshot_.gen[pos]) continue;
+      bool hit = false;
+      const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
+      ++reevaluated;
+      ok = fp->is_success() || fp->is_unschedulable();
+      memo->ok[off] = fp->is_success();
+      memo->gens[off] = snapshot_.gen[pos];
+    }
+    int off = 0;
+    for (; ok && off < m && c < to_find; ++off)
+      if (memo->ok[off]) {
+        const int pos = at(off);
+        found_buf_[c] = all[pos].get();
+        found_pos_buf_[c] = pos;
+        ++c;
+      }
+    for (; ok && c < to_find && off < n; ++off) {  // the scan has to reach further now
+      const int pos = at(off);
+      bool hit = false;
+      const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
+      ++reevaluated;
+      ok = fp->is_success() || fp->is_unschedulable();
+      if (off < static_cast<int>(memo->gens.size())) {
+        memo->gens[off] = snapshot_.gen[pos];
+        memo->ok[off] = fp->is_success();
+      } else {
+        memo->gens.push_back(snapshot_.gen[pos]);
+        memo->ok.push_back(fp->is_success());
+      }
+      if (fp->is_success()) {
+        found_buf_[c] = all[pos].get();
+        found_pos_buf_[c] = pos;
+        ++c;
+      }
+    }
+    if (ok && c > 0) {
+      processed = off;
+      memo->processed = off;
+      hits = static_cast<uint64_t>(std::max(0, processed - reevaluated));
+      served = true;
+    } else {  // an error, or nothing feasible (the diagnosis needs every verdict): the full walk
+      memo->valid = false;
+      c = 0;
+    }
+  }
+  if (served) {
+    bool mismatch = false;
+    if (opts_.scan_memo_verify) {  // the full walk must find the same nodes and stop at the same one
+      int vc = 0, vp = 0;
+      for (int i = 0; i < n && vc < to_find && !mismatch; ++i) {
+        const int pos = start + i >= n ? start + i - n : start + i;
+        bool hit = false;
+        const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
+        ++vp;
+        if (fp->is_success()) mismatch = vc >= c || found_pos_buf_[vc++] != pos;
+      }
+      mismatch = mismatch || vc != c || vp != processed;
+    }
+    std::lock_guard<std::mutex> g(stats_mu_);
+    ++stats_.scan_memo_served;
+    stats_.scan_memo_mismatches += mismatch;
+  } else if (inline_ok) {
     // Serial path (every cluster below the parallel threshold, and larger
     // ones whose verdicts mostly come from the equivalence cache): plain
     // counters, no std::function call or atomic per node.
     const int64_t t0 = Parallelizer::now_ns();
+    if (memo) {
+      memo->gens.clear();
+      memo->ok.clear();
+    }
     for (int i = 0; i < n; ++i) {
       int pos = start + i;
       if (pos >= n) pos -= n;
@@ -1193,6 +1283,10 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       const Status* fp = eval_node(pos, ni, fail_buf_[pos], &hit);
       hits += hit;
       ++processed;
+      if (memo) {
+        memo->gens.push_back(snapshot_.gen[pos]);
+        memo->ok.push_back(fp->is_success());
+      }
       if (fp->is_success()) {
         found_buf_[c] = &ni;
         found_pos_buf_[c] = pos;
@@ -1207,8 +1301,17 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       has_err = true;
       break;
     }
+    if (memo) {
+      memo->valid = !has_err && c > 0;
+      memo->start = start;
+      memo->n = n;
+      memo->to_find = to_find;
+      memo->epoch = snapshot_.node_epoch;
+      memo->processed = processed;
+    }
     Parallelizer::record_inline(&filter_site_, Parallelizer::now_ns() - t0, processed, n);
   } else {
+    if (memo) memo->valid = false;
     std::atomic<int> count{0};
     std::atomic<bool> stop{false};
     std::atomic<uint64_t> ahits{0};

@@ -114,6 +114,14 @@ struct SchedulerOptions {
   bool status_updates = true;        // PodScheduled=False condition patches on failure
   bool events = true;                // FailedScheduling / Preempted events (in-process StoreClient)
   bool equivalence_cache = true;     // reuse node-local Filter/Score results across a pod template
+  // Gang ranks share the first rank's node window (find_nodes_that_fit) and a
+  // template's last Filter scan is updated instead of repeated (EqEntry::scan).
+  // Defaults: on, unless XSCHED_GANG_WINDOW / XSCHED_SCAN_MEMO is "0" (A/B runs).
+  bool gang_window = true;
+  bool scan_memo = true;
+  // Testing: every scan the memo answers is repeated in full and compared
+  // (Stats::scan_memo_mismatches).
+  bool scan_memo_verify = false;
   bool trace = false;
   uint64_t seed = 0;
   // Debugging: on the first fit error, write the cache and queue (the cache
@@ -197,6 +205,7 @@ class Scheduler {
     uint64_t attempts = 0, scheduled = 0, unschedulable = 0, errors = 0, bound = 0, bind_failures = 0;
     uint64_t preemption_attempts = 0;
     uint64_t eq_filter_hits = 0, eq_filter_misses = 0;  // equivalence-cache Filter lookups
+    uint64_t scan_memo_served = 0, scan_memo_mismatches = 0;  // EqEntry::scan answers (and failed checks)
   };
   Stats stats() const;
   // Blocks (without the Python lock, from the bindings) until `target`
@@ -227,6 +236,15 @@ class Scheduler {
   struct EqEntry {
     uint64_t epoch = 0;
     std::vector<EqSlot> slots;
+    // The last serial Filter scan of this template (find_nodes_that_fit):
+    // per scan offset from `start`, the node version it saw and its verdict.
+    struct ScanMemo {
+      bool valid = false;
+      int start = 0, n = 0, to_find = 0, processed = 0;
+      uint64_t epoch = 0;
+      std::vector<int64_t> gens;
+      std::vector<char> ok;
+    } scan;
   };
   EqEntry* eq_entry(Framework& fw, const Pod& p);
   void release_retired();

@@ -105,3 +105,41 @@ def test_bench_wave_identical_with_and_without_cache():
         results.append({p["metadata"]["name"]: p["spec"].get("nodeName", "") for p in placed})
     assert results[0] == results[1]
     assert all(results[0].values())
+
+
+def _wave_stats(options: dict) -> dict:
+    """One burst wave on 300 MI355X nodes (the adaptive share of nodes to
+    score is < 100% there, so the node window matters), scheduled by
+    schedule_one on the calling thread; returns the scheduler's stats."""
+    import json as _json
+
+    from flex_gpu_scheduler_amd import Store, load_config, new_scheduler
+    from flex_gpu_scheduler_amd.utils.workload import ClusterSpec, flagship_config, make_wave
+
+    spec = ClusterSpec(nodes=300)
+    store = Store()
+    store.create_many("nodes", _json.dumps(spec.node_objects()))
+    store.create_many("noderesourcetopologies", _json.dumps(spec.nrt_objects()))
+    w = make_wave(spec, 1, namespace="w", fill=0.6)
+    store.create_many("podgroups", _json.dumps(w.pod_groups))
+    store.create_many("pods", _json.dumps(w.pods))
+    s = new_scheduler(store, load_config(flagship_config()), seed=7, **options)
+    try:
+        s.sync_informers(50)
+        while s.schedule_one(200):
+            pass
+        assert s.wait_bound(len(w.pods), 20.0), s.stats()
+        return s.stats()
+    finally:
+        s.stop()
+
+
+def test_scan_memo_answers_as_the_full_scan():
+    """EqEntry::scan re-evaluates only the changed nodes of a template's
+    window and re-cuts the feasible list; with scanMemoVerify every answer is
+    checked against the full Filter walk (same nodes, in order, same stop)."""
+    st = _wave_stats({"scanMemo": True, "scanMemoVerify": True})
+    assert st["scan_memo_served"] > 100, st
+    assert st["scan_memo_mismatches"] == 0, st
+    off = _wave_stats({"scanMemo": False})
+    assert off["scan_memo_served"] == 0
