@@ -9,7 +9,8 @@ scheduling cycle, so the interleaving is exact, not timing-dependent:
 1. the gang is denied (extender rejects every node -> Coscheduling PostFilter
    rejects and denies the group, coscheduling.go:140-176) and the denied-group
    timer is armed;
-2. the clock passes the denial TTL; member ``a`` starts a cycle and blocks in
+2. the clock passes the denial TTL (not yet the timer's deadline, TTL + 1 ms);
+   member ``a`` starts a cycle and blocks in
    the extender's filter call;
 3. the timer fires (``run_timers``) and activates the group: ``a`` is in
    flight, so the queue can only mark it;
@@ -70,8 +71,10 @@ def test_member_in_flight_when_denied_group_timer_fires_is_requeued():
         assert s.schedule_one(2000) and s.schedule_one(2000)
         q = s.queue_counts()
         assert q["unschedulable"] == 2 and q["active"] == 0, q
-        # 2. past the TTL (3 s + the timer's 1 ms slack), without running the timer.
-        clock.advance(3.5)
+        # 2. past the TTL (3 s) but short of the requeue timer's deadline
+        # (TTL + 1 ms): the timer thread polls the FakeClock on its own, so it
+        # must not be due before `a` is in flight.
+        clock.advance(3.0005)
         s.move_all()
         assert s.queue_counts()["active"] == 2
         ext.mode = "gate"
@@ -79,6 +82,7 @@ def test_member_in_flight_when_denied_group_timer_fires_is_requeued():
         t.start()
         assert ext.entered.wait(10)
         # 3. the denied-group timer fires while `a` is in its scheduling cycle.
+        clock.advance(0.001)
         s.run_timers()
         q = s.queue_counts()
         assert q["in_flight"] == 1 and q["activation_marks"] == 1, q
