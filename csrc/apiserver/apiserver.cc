@@ -445,7 +445,10 @@ bool parse_chunk_size(const std::string& line, size_t* out) {
   size_t v = 0, i = 0;
   for (; i < line.size() && i < 16; ++i) {
     char ch = line[i];
-    int d = ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
+    int d = ch >= '0' && ch <= '9'   ? ch - '0'
+            : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10
+            : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10
+                                     : -1;
     if (d < 0) break;
     v = v * 16 + static_cast<size_t>(d);
   }
@@ -455,7 +458,9 @@ bool parse_chunk_size(const std::string& line, size_t* out) {
   return true;
 }
 
-bool open_path(const std::string& path) { return path == "/healthz" || path == "/readyz" || path == "/livez" || path == "/version"; }
+bool open_path(const std::string& path) {
+  return path == "/healthz" || path == "/readyz" || path == "/livez" || path == "/version";
+}
 
 // 0: ok, -1: connection closed, >0: HTTP error to send before closing. With
 // a bearer `token`, a request without it is refused (401) before its body is

@@ -380,7 +380,8 @@ void Scheduler::start() {
     int waiting = 0;
     for (const auto& w : waiting_) waiting += static_cast<int>(w->size());
     const int inflight = inflight_.load();
-    metrics_->set_gauge("scheduler_scheduler_goroutines", "work=\"binding\"", static_cast<double>(std::max(0, inflight - waiting)));
+    metrics_->set_gauge("scheduler_scheduler_goroutines", "work=\"binding\"",
+                        static_cast<double>(std::max(0, inflight - waiting)));
     metrics_->set_gauge("scheduler_scheduler_goroutines", "work=\"permit\"", static_cast<double>(waiting));
     metrics_->set_gauge("scheduler_scheduler_cache_size", "type=\"assumed_pods\"", static_cast<double>(cache_->assumed_count()));
     metrics_->set_gauge("scheduler_scheduler_cache_size", "type=\"pods\"", static_cast<double>(cache_->pod_count()));

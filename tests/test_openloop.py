@@ -1,8 +1,6 @@
 """Open-loop gang admission (utils/openloop.py, csrc/scheduler/openloop.cc)."""
 import json
 
-import pytest
-
 from flex_gpu_scheduler_amd.utils.benchrun import Shard, gang_latency_summary
 from flex_gpu_scheduler_amd.utils.openloop import GANG_TYPES, plan, run_open_loop
 from flex_gpu_scheduler_amd.utils.workload import ClusterSpec
