@@ -51,11 +51,25 @@ std::vector<std::string> Registry::names() const {
 }
 
 void default_normalize_score(int64_t max_priority, bool reverse, std::vector<NodeScore>& scores) {
-  int64_t max_count = 0;
-  for (const auto& s : scores) max_count = std::max(max_count, s.score);
+  int64_t max_count = 0, min_count = 0;
+  for (const auto& s : scores) {
+    max_count = std::max(max_count, s.score);
+    min_count = std::min(min_count, s.score);
+  }
   if (max_count == 0) {
     if (reverse)
       for (auto& s : scores) s.score = max_priority;
+    return;
+  }
+  // Raw scores are mostly small counts (free GPUs, matching pods): one
+  // division per distinct value instead of one per node.
+  if (min_count >= 0 && max_count < 256 && static_cast<size_t>(max_count) * 2 < scores.size()) {
+    int64_t table[256];
+    for (int64_t v = 0; v <= max_count; ++v) {
+      const int64_t sc = max_priority * v / max_count;
+      table[v] = reverse ? max_priority - sc : sc;
+    }
+    for (auto& s : scores) s.score = table[s.score];
     return;
   }
   for (auto& s : scores) {
@@ -473,16 +487,19 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
         hit[i] = slot && slot->score_gen == gen && slot->raw.size() == ns;
         any_hit = any_hit || hit[i];
       }
+    // Hits first, node-major (one slot visit per node); skipped plugins'
+    // rows are never read, so they are not filled.
+    if (any_hit)
+      for (size_t i = 0; i < n; ++i) {
+        if (!hit[i]) continue;
+        const RawScores& raw = eq->slots[i]->raw;
+        for (size_t k = 0; k < ns; ++k)
+          if (!skip[k] && eq->local[k]) per[k][i].score = raw[k];
+      }
     for (size_t k = 0; k < ns; ++k) {
       std::vector<NodeScore>& row = per[k];
-      if (skip[k]) {
-        for (size_t i = 0; i < n; ++i) row[i].score = 0;
-        continue;
-      }
+      if (skip[k]) continue;
       const bool reuse = any_hit && eq->local[k];
-      if (reuse)
-        for (size_t i = 0; i < n; ++i)
-          if (hit[i]) row[i].score = eq->slots[i]->raw[k];
       Status st = scorers_[k].first->score_many(s, p, nodes, reuse ? hit.data() : nullptr, row,
                                                 (eq && eq->pos.size() == n) ? eq->pos.data() : nullptr);
       if (!st.is_success()) {
@@ -496,7 +513,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
         EqSlot* slot = eq->slots[i];
         if (!slot || hit[i]) continue;
         slot->raw.resize(ns);
-        for (size_t k = 0; k < ns; ++k) slot->raw[k] = per[k][i].score;
+        for (size_t k = 0; k < ns; ++k) slot->raw[k] = skip[k] ? 0 : per[k][i].score;
         slot->score_gen = eq->gens.size() == n ? eq->gens[i] : nodes[i]->generation;
       }
     Parallelizer::record_inline(&score_site_, Parallelizer::now_ns() - s0, static_cast<int>(n), static_cast<int>(n));
@@ -505,12 +522,13 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
                                        &failed, &score_site_);
   }
   if (failed.load()) return Status(Code::Error, err);
+  int64_t skipped_total = 0;  // the skipped plugins' constant contribution
+  for (size_t k = 0; k < scorers_.size(); ++k)
+    if (skip[k]) skipped_total += scorers_[k].first->score_skip_value() * scorers_[k].second;
+  if (skipped_total)
+    for (size_t i = 0; i < n; ++i) total[i].score += skipped_total;
   for (size_t k = 0; k < scorers_.size(); ++k) {
-    if (skip[k]) {
-      if (int64_t c = scorers_[k].first->score_skip_value() * scorers_[k].second)
-        for (size_t i = 0; i < n; ++i) total[i].score += c;
-      continue;
-    }
+    if (skip[k]) continue;
     auto& pl = scorers_[k].first;
     if (pl->has_normalize_score()) {
       if (pl->normalize_uses_names())

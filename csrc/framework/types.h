@@ -239,6 +239,17 @@ struct GpuLedger : GpuLedgerState {
   int free_gpus() const { return tot_whole; }  // GPUScore (gpu_node.go:179-187): free whole (SPX) GPUs
   int64_t free_memory() const { return tot_mem; }  // MemScore (gpu_node.go:189-199)
   int free_xcds() const { return tot_xcds; }
+  // Bit b set: some GPU without a whole-GPU owner is partitioned into
+  // (1 << b)-XCD partitions (b = 0..3: CPX .. SPX).
+  uint8_t part_mask() const {
+    uint8_t m = 0;
+    for (int g = 0; g < gpu_count; ++g) {
+      const int x = xcds_per_part(g);
+      if (monopoly[g] > 0 || x <= 0) continue;
+      m |= static_cast<uint8_t>(x >= 8 ? 8 : x >= 4 ? 4 : x >= 2 ? 2 : 1);
+    }
+    return m;
+  }
 
  private:
   GpuFree compute(int g) const;
@@ -307,6 +318,16 @@ struct Snapshot {
   std::vector<int64_t> gen;
   // nodes[i]->gpu.free_gpus() (whole SPX GPUs free), contiguous likewise.
   std::vector<int32_t> free_whole;
+  // nodes[i]->gpu.free_xcds() and .part_mask(), contiguous likewise (XCD gangs).
+  std::vector<int32_t> free_xcd;
+  std::vector<uint8_t> part_mask;
+  void set_gpu_summary(size_t i) {
+    const GpuLedger& L = nodes[i]->gpu;
+    gen[i] = nodes[i]->generation;
+    free_whole[i] = L.free_gpus();
+    free_xcd[i] = L.free_xcds();
+    part_mask[i] = L.part_mask();
+  }
   // Nodes with affinity / required anti-affinity pods, in no particular
   // order. Kept incrementally by the cache: *_pos[i] is node i's slot in the
   // list (-1 if absent) and *_idx the reverse, so a refresh touches only the

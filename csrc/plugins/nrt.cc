@@ -411,6 +411,29 @@ class TopologyMatch : public Plugin {
         if (!skip || !skip[i]) out[i].score = whole_gang_score(*c, snap->free_whole[pos[i]], *nodes[i]);
       return {};
     }
+    if (pos && snap && c->gang && c->kind == GangCtx::kXcd && snap->part_mask.size() == snap->nodes.size()) {
+      // XCD ranks: a member's partition footprint depends only on which
+      // partition sizes the node offers (Snapshot::part_mask), so it is
+      // tabulated once per cycle; free XCDs come from the contiguous array.
+      int64_t per_of[16];
+      for (int m = 0; m < 16; ++m) {
+        int64_t per = 0;
+        for (int b = 0; b < 4; ++b) {
+          if (!(m & (1 << b))) continue;
+          const int64_t xpp = 1 << b;
+          const int64_t use = (c->amount + xpp - 1) / xpp * xpp;
+          if (per == 0 || use < per) per = use;
+        }
+        per_of[m] = per;
+      }
+      for (size_t i = 0; i < nodes.size(); ++i) {
+        if (skip && skip[i]) continue;
+        const int64_t per = per_of[snap->part_mask[pos[i]]];
+        const int64_t free = snap->free_xcd[pos[i]];
+        out[i].score = per == 0 || free <= 0 ? 0 : fit_score(c->remaining * per, free, co_located(*c, *nodes[i]));
+      }
+      return {};
+    }
     for (size_t i = 0; i < nodes.size(); ++i)
       if (!skip || !skip[i]) out[i].score = gang_score(*c, *nodes[i]);
     return {};

@@ -395,10 +395,9 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
     structure_changed_ = false;
     s.gen.resize(s.nodes.size());
     s.free_whole.resize(s.nodes.size());
-    for (size_t i = 0; i < s.nodes.size(); ++i) {
-      s.gen[i] = s.nodes[i]->generation;
-      s.free_whole[i] = s.nodes[i]->gpu.free_gpus();
-    }
+    s.free_xcd.resize(s.nodes.size());
+    s.part_mask.resize(s.nodes.size());
+    for (size_t i = 0; i < s.nodes.size(); ++i) s.set_gpu_summary(i);
     s.have_pods_with_affinity.clear();
     s.have_pods_with_required_anti_affinity.clear();
     s.affinity_idx.clear();
@@ -422,8 +421,7 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
         s.nodes[i] = cl;
         sit->second = cl;
       }
-      s.gen[i] = cl->generation;
-      s.free_whole[i] = cl->gpu.free_gpus();
+      s.set_gpu_summary(i);
       sync_affinity_lists(s, i);
     }
   }

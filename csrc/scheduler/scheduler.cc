@@ -1978,9 +1978,19 @@ Json Scheduler::explain(const Json& pod_obj) {
       out.set("scores", std::move(sc));
       out.set("selected", Json(feasible[select_host(scores)]->name()));
       // The scheduling path's totals (all-zero plugins skipped, their
-      // normalized constant still added) for parity checks against "total".
+      // normalized constant still added, the plugins' snapshot-array paths
+      // given the nodes' positions) for parity checks against "total".
       std::vector<NodeScore> hot;
-      if (fw->run_score(*state, *pod, feasible, hot, nullptr).is_success()) {
+      EqScoreCache pos_only;  // no cached slots: positions and versions only
+      pos_only.slots.assign(feasible.size(), nullptr);
+      for (const NodeInfo* ni : feasible) {
+        auto it = snapshot_.index.find(ni->name());
+        if (it == snapshot_.index.end()) break;
+        pos_only.pos.push_back(static_cast<int>(it->second));
+        pos_only.gens.push_back(snapshot_.gen[it->second]);
+      }
+      EqScoreCache* hot_eq = pos_only.pos.size() == feasible.size() ? &pos_only : nullptr;
+      if (fw->run_score(*state, *pod, feasible, hot, nullptr, hot_eq).is_success()) {
         Json h = Json::object();
         for (size_t i = 0; i < feasible.size(); ++i) h.set(feasible[i]->name(), Json(hot[i].score));
         out.set("hot_path_totals", std::move(h));

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # One MI355X box session. Usage: bash scripts/gpu_session.sh TAG step [step ...]
-# steps: pytest smoke bench bench3 nodes1024 pmc sched500 sched5000 remote sample_pre sample_sched
+# steps: pytest smoke bench bench3 nodes1024 ab1024 abbin1024 sample1024 pmc sched500 sched5000 remote sample_pre sample_sched
 #        sample_bench rocprof
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure (no retries). A heartbeat line every 60 s keeps long steps visible.
@@ -66,6 +66,16 @@ for step in "$@"; do
         for v in ${AB_VALUES:-0 1}; do
           echo "$var=$v $(env "$var=$v" timeout -k 5 200 taskset -c "$cpus" abbin/xsched_stress /tmp/s_1024 6 | tail -1)" \
             >> "$OUT/ab1024.txt" || exit 1
+        done
+      done ;;
+    abbin1024)
+      # A/B of two stress binaries (abbin/xsched_stress_base vs abbin/xsched_stress)
+      # on the 1,024-node bench waves, same CPU domain, alternating 3x.
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_1024 --nodes 1024 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      for i in 1 2 3; do
+        for b in xsched_stress_base xsched_stress; do
+          echo "$b $(timeout -k 5 200 taskset -c "$cpus" abbin/$b /tmp/s_1024 6 | tail -1)" >> "$OUT/abbin1024.txt" || exit 1
         done
       done ;;
     sample1024)

@@ -143,3 +143,45 @@ def test_scan_memo_answers_as_the_full_scan():
     assert st["scan_memo_mismatches"] == 0, st
     off = _wave_stats({"scanMemo": False})
     assert off["scan_memo_served"] == 0
+
+
+def test_gang_scores_from_snapshot_arrays_match_per_node_scoring():
+    """XGMIGangAffinity scores whole-GPU and XCD gang ranks from the
+    snapshot's contiguous arrays (free GPUs, free XCDs, partition sizes) on
+    the scheduling path; explain() runs every plugin per node. Mid-wave, with
+    gangs partly placed and CPX partitions partly used, both must agree."""
+    import json as _json
+
+    from flex_gpu_scheduler_amd import Store, load_config, new_scheduler
+    from flex_gpu_scheduler_amd.utils.workload import ClusterSpec, flagship_config, make_wave
+
+    spec = ClusterSpec(nodes=48)
+    store = Store()
+    store.create_many("nodes", _json.dumps(spec.node_objects()))
+    store.create_many("noderesourcetopologies", _json.dumps(spec.nrt_objects()))
+    w = make_wave(spec, 1, namespace="w", fill=0.6)
+    store.create_many("podgroups", _json.dumps(w.pod_groups))
+    store.create_many("pods", _json.dumps(w.pods))
+    s = new_scheduler(store, load_config(flagship_config()), seed=3)
+    try:
+        s.sync_informers(50)
+        for _ in range(len(w.pods) // 2):
+            if not s.schedule_one(200):
+                break
+        s.sync_informers(50)
+        pods, _ = store.list("pods", "w")
+        pending = [p for p in pods if not p["spec"].get("nodeName")]
+        kinds = set()
+        checked = 0
+        for p in pending[:: max(1, len(pending) // 40)]:
+            out = s.explain(p)
+            if "scores" not in out:
+                continue
+            totals = {n: v["total"] for n, v in out["scores"].items()}
+            assert out["hot_path_totals"] == totals, (p["metadata"]["name"], out)
+            parts = p["metadata"]["name"].split("-")
+            kinds.add(parts[2] if len(parts) > 3 else parts[-1])
+            checked += 1
+        assert checked >= 10 and {"q", "x8"} <= kinds, (checked, kinds)
+    finally:
+        s.stop()
