@@ -11,9 +11,12 @@ Per probe the table gives:
   move (the probe's read_bytes / write_bytes): FETCH_SIZE and WRITE_SIZE are
   in KiB, and gfx950 counts 64 B per 128-B read request in FETCH_SIZE, so the
   read traffic is 2 x FETCH_SIZE;
-* the median dispatch time of the measured kernel in the trace (both
-  passes), and the GB/s it implies for the counted bytes ("counter GB/s");
-* the probe's own figure: the median of its per-launch event pairs;
+* the median dispatch time of the measured kernel, from a --kernel-trace
+  only run when scripts/probe_timing.sh left one (`trace_<probe>`), else from
+  the counter passes, and the GB/s it implies for the counted bytes
+  ("counter GB/s");
+* the probe's own figure: the median of its per-launch event pairs, from a
+  plain run when there is one (`plain_<probe>.log`), else from the passes;
 * the difference between the two (the probe must agree within 5 %).
 """
 from __future__ import annotations
@@ -64,6 +67,18 @@ def _pass(d: str) -> dict[str, dict]:
     return out
 
 
+def _trace(d: str) -> dict[str, dict]:
+    """kernel -> {"ns": [dispatch ns...]} from a --kernel-trace-only run."""
+    csvs = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not csvs:
+        return {}
+    out: dict[str, dict] = defaultdict(lambda: {"ns": [], "counters": {}})
+    with open(csvs[0]) as f:
+        for r in csv.DictReader(f):
+            out[_short(r["Kernel_Name"])]["ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return dict(out)
+
+
 def _measured_kernel(kernels: dict[str, dict], probe: dict) -> str | None:
     """The probe's kernel in a pass: not the runtime's fills, not the warm-up
     write of the buffers (k_write<4, true>) unless the probe is a write."""
@@ -90,9 +105,9 @@ def summarize(root: str) -> str:
         m = re.match(r"(.+)_(fetch|write)$", name)
         probe, kind = (m.group(1), m.group(2)) if m else (name, "")
         passes[probe][kind] = d
-    lines = ["| probe | kernel | bytes to move per dispatch | counted per dispatch | median dispatch (trace) | "
-             "counter GB/s | probe GB/s (median launch) | probe vs counter |",
-             "|---|---|---|---|---|---|---|---|"]
+    lines = ["| probe | kernel | bytes to move per dispatch | counted per dispatch | median dispatch | "
+             "counter GB/s | probe GB/s (median launch) | probe vs counter | timing from |",
+             "|---|---|---|---|---|---|---|---|---|"]
     other = []
     for probe, kinds in sorted(passes.items()):
         ns_all: list[int] = []
@@ -119,6 +134,21 @@ def summarize(root: str) -> str:
             continue
         want_r, want_w = pj["read_bytes"], pj["write_bytes"]
         counted = (read_b or 0) + (write_b or 0)
+        # Timing from the counter-free runs when present (scripts/probe_timing.sh):
+        # counter collection serializes dispatches and stretches the probe's
+        # own event timing, so the comparison is made without it.
+        timing = "pmc pass"
+        tdir = os.path.join(root, f"trace_{probe}")
+        plain = _probe_line(os.path.join(root, f"plain_{probe}.log"))
+        if os.path.isdir(tdir):
+            tr = _trace(tdir)
+            k = _measured_kernel(tr, pj)
+            if k is not None and tr[k]["ns"]:
+                ns_all = tr[k]["ns"][1:] if len(tr[k]["ns"]) > 2 else tr[k]["ns"]
+                timing = "kernel trace"
+        if plain.get("GBps"):
+            pj = plain
+            timing += ", plain probe"
         med = statistics.median(ns_all) if ns_all else 0
         cgb = counted / med if med else 0.0
         pgb = float(pj.get("GBps") or 0)
@@ -127,7 +157,7 @@ def summarize(root: str) -> str:
             f"| {probe} | `{kernel}` | read {want_r / 2**30:.2f} GiB, write {want_w / 2**30:.2f} GiB | "
             f"read {0 if read_b is None else read_b / 2**30:.3f} GiB, "
             f"write {0 if write_b is None else write_b / 2**30:.3f} GiB | {med / 1e3:,.1f} us | {cgb:,.0f} | "
-            f"{pgb:,.0f} ({100 * pgb / HBM_PEAK_GBPS:.1f}% of 8 TB/s) | {diff} |")
+            f"{pgb:,.0f} ({100 * pgb / HBM_PEAK_GBPS:.1f}% of 8 TB/s) | {diff} | {timing} |")
     out = "\n".join(lines) + "\n"
     if other:
         out += "\n| pass | kernel | counters per dispatch | probe |\n|---|---|---|---|\n" + "\n".join(other) + "\n"

@@ -28,6 +28,7 @@ for step in "$@"; do
     nodes1024) timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
                  --no-service-mode > "$OUT/bench_nodes_1024.json" 2> "$OUT/bench_nodes_1024.err" ;;
     pmc) OUTDIR="$OUT" bash scripts/pmc_round.sh ;;
+    probe_timing) OUTDIR="$OUT" bash scripts/probe_timing.sh ;;
     sched500) timeout -k 10 400 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 500 --pods 1000 \
                 --cpus l3 > "$OUT/sched_perf_500.jsonl" 2>&1 ;;
     sched5000) timeout -k 10 700 python -u -m flex_gpu_scheduler_amd.tools.sched_perf --nodes 5000 --pods 5000 \

@@ -27,4 +27,5 @@ for p in hbm-copy hbm-triad xcd-copy-1 xcd-copy-2 xcd-copy-4 xcd-copy-8; do
   run "${p}_fetch" "$p" FETCH_SIZE GRBM_GUI_ACTIVE || exit $?
   run "${p}_write" "$p" WRITE_SIZE GRBM_GUI_ACTIVE || exit $?
 done
+OUTDIR="$OUT" bash scripts/probe_timing.sh || exit $?
 echo "[pmc] done" | tee -a "$OUT/pmc_steps.log"
