@@ -1543,20 +1543,25 @@ void Scheduler::add_extender_scores(const Pod& p, const NodeList& feasible, std:
 }
 
 size_t Scheduler::select_host(const std::vector<NodeScore>& scores) {
+  // Uniform among the top-scored nodes, as upstream's reservoir sampling
+  // (generic_scheduler.go selectHost), with one draw per cycle instead of one
+  // per tie: idle nodes of a large cluster tie by the hundred.
   int64_t best = scores[0].score;
-  size_t sel = 0;
-  int cnt = 1;
+  size_t first = 0;
+  uint64_t cnt = 1;
   for (size_t i = 1; i < scores.size(); ++i) {
     if (scores[i].score > best) {
       best = scores[i].score;
-      sel = i;
+      first = i;
       cnt = 1;
     } else if (scores[i].score == best) {
       ++cnt;
-      if (rng_() % static_cast<uint64_t>(cnt) == 0) sel = i;  // reservoir sampling
     }
   }
-  return sel;
+  if (cnt == 1) return first;
+  uint64_t k = rng_() % cnt;
+  for (size_t i = first;; ++i)
+    if (scores[i].score == best && k-- == 0) return i;
 }
 
 Scheduler::CycleMetrics& Scheduler::cycle_metrics(const Framework& fw) {
