@@ -441,20 +441,32 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
   std::string err;
   std::mutex err_mu;
   const size_t ns = scorers_.size();
+  // The template's equivalence table, when every node's snapshot position is
+  // known (ns <= 64: scorer sets are bitmasks). Per node it holds raw columns
+  // valid at score_gen (the set `cols`) and the weighted sum of the plain
+  // scorers (node-local, no normalization) over the set `plain_mask`.
+  EqTable* table =
+      eq && eq->table && eq->pos.size() == n && eq->local.size() == ns && ns <= 64 ? eq->table : nullptr;
+  if (table) table->ensure_scorers(ns);
+  const int* tpos = table ? eq->pos.data() : nullptr;
+  uint64_t local_mask = 0;  // non-skipped node-local scorers
+  if (table)
+    for (size_t k = 0; k < ns; ++k)
+      if (!skip[k] && eq->local[k]) local_mask |= 1ULL << k;
   // One node: every score plugin (raw scores; normalizers read the rows).
   auto score_node = [&](size_t i) {
     // Equivalence cache: node-local raw scores of this pod template on an
     // unchanged node are reused; the others are recomputed.
-    EqSlot* slot = eq ? eq->slots[i] : nullptr;
     const NodeInfo& ni = *nodes[i];
-    const bool hit = slot && slot->score_gen == ni.generation && slot->raw.size() == ns;
+    const size_t pos = tpos ? static_cast<size_t>(tpos[i]) : 0;
+    const bool hit = table && table->score_gen[pos] == ni.generation && (table->cols[pos] & local_mask) == local_mask;
     for (size_t k = 0; k < ns; ++k) {
       if (skip[k]) {
         per[k][i].score = 0;
         continue;
       }
       if (hit && eq->local[k]) {
-        per[k][i].score = slot->raw[k];
+        per[k][i].score = table->raw_at(k, pos);
         continue;
       }
       auto [sc, st] = scorers_[k].first->score(s, p, ni);
@@ -466,36 +478,68 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
       }
       per[k][i].score = sc;
     }
-    if (slot && !hit) {
-      slot->raw.resize(ns);
-      for (size_t k = 0; k < ns; ++k) slot->raw[k] = per[k][i].score;
-      slot->score_gen = ni.generation;
+    if (table && !hit) {
+      for (size_t k = 0; k < ns; ++k)
+        if ((local_mask >> k) & 1) table->raw_at(k, pos) = per[k][i].score;
+      table->score_gen[pos] = ni.generation;
+      table->cols[pos] = local_mask;
+      table->plain_mask[pos] = 0;  // no sum here: a serial lookup with plain scorers misses
     }
   };
-  if (handle_.parallelizer->plan_inline(static_cast<int>(n), &score_site_)) {
+  // The serial path splits the local scorers into plain ones, summed per node
+  // version once (a hit then costs one read for all of them), and row ones
+  // (normalized per cycle), whose raw column is kept.
+  uint64_t plain_mask = 0, row_mask = 0;
+  thread_local std::vector<int64_t> plain_buf;
+  std::vector<int64_t>& plain_tot = plain_buf;
+  const bool inline_score = handle_.parallelizer->plan_inline(static_cast<int>(n), &score_site_);
+  if (inline_score && table) {
+    for (size_t k = 0; k < ns; ++k)
+      if ((local_mask >> k) & 1) {
+        if (!breakdown && !scorers_[k].first->has_normalize_score()) plain_mask |= 1ULL << k;
+        else row_mask |= 1ULL << k;
+      }
+  }
+  auto is_plain = [&](size_t k) { return (plain_mask >> k) & 1; };
+  if (inline_score) {
     // Serial path, plugin-major: each scorer runs over every node that needs
     // it in one call (Plugin::score_many), equivalence-cache hits copied in.
     const int64_t s0 = Parallelizer::now_ns();
     thread_local std::vector<char> hit_buf;
     std::vector<char>& hit = hit_buf;
+    thread_local std::vector<uint32_t> miss_buf;
+    std::vector<uint32_t>& miss = miss_buf;  // indices of the nodes recomputed
     hit.assign(n, 0);
+    miss.clear();
+    if (plain_mask) plain_tot.assign(n, 0);
     bool any_hit = false;
-    if (eq)
+    const bool have_gens = eq && eq->gens.size() == n;
+    if (table) {
+      const int64_t* sgen = table->score_gen.data();
+      const uint64_t* pm = table->plain_mask.data();
+      const uint64_t* cm = table->cols.data();
       for (size_t i = 0; i < n; ++i) {
-        const EqSlot* slot = eq->slots[i];
-        const int64_t gen = eq->gens.size() == n ? eq->gens[i] : nodes[i]->generation;
-        hit[i] = slot && slot->score_gen == gen && slot->raw.size() == ns;
-        any_hit = any_hit || hit[i];
+        const size_t pos = static_cast<size_t>(tpos[i]);
+        const int64_t gen = have_gens ? eq->gens[i] : nodes[i]->generation;
+        const bool h = sgen[pos] == gen && pm[pos] == plain_mask && (cm[pos] & row_mask) == row_mask;
+        hit[i] = h;
+        if (!h) miss.push_back(static_cast<uint32_t>(i));
       }
-    // Hits first, node-major (one slot visit per node); skipped plugins'
-    // rows are never read, so they are not filled.
-    if (any_hit)
-      for (size_t i = 0; i < n; ++i) {
-        if (!hit[i]) continue;
-        const RawScores& raw = eq->slots[i]->raw;
-        for (size_t k = 0; k < ns; ++k)
-          if (!skip[k] && eq->local[k]) per[k][i].score = raw[k];
+      any_hit = miss.size() < n;
+    }
+    // Hits: plain sums and row columns; skipped and plain scorers' rows are
+    // never read, so they are not filled.
+    if (any_hit) {
+      if (plain_mask)
+        for (size_t i = 0; i < n; ++i)
+          if (hit[i]) plain_tot[i] = table->plain_sum[tpos[i]];
+      for (size_t k = 0; k < ns; ++k) {  // column by column
+        if (!((row_mask >> k) & 1)) continue;
+        const int64_t* col = &table->raw[k * table->n];
+        for (size_t i = 0; i < n; ++i)
+          if (hit[i]) per[k][i].score = col[tpos[i]];
       }
+    }
     for (size_t k = 0; k < ns; ++k) {
       std::vector<NodeScore>& row = per[k];
       if (skip[k]) continue;
@@ -508,14 +552,37 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
         break;
       }
     }
-    if (eq && !failed.load())
-      for (size_t i = 0; i < n; ++i) {
-        EqSlot* slot = eq->slots[i];
-        if (!slot || hit[i]) continue;
-        slot->raw.resize(ns);
-        for (size_t k = 0; k < ns; ++k) slot->raw[k] = skip[k] ? 0 : per[k][i].score;
-        slot->score_gen = eq->gens.size() == n ? eq->gens[i] : nodes[i]->generation;
+    if (plain_mask && !failed.load())
+      for (uint32_t i : miss) {
+        int64_t sum = 0;
+        for (size_t k = 0; k < ns; ++k) {
+          if (!is_plain(k)) continue;
+          const int64_t sc = per[k][i].score;
+          if (sc > kMaxNodeScore || sc < kMinNodeScore) {
+            err = "plugin \"" + scorers_[k].first->name() + "\" returns an invalid score " + std::to_string(sc) +
+                  ", it should in the range of [0, 100] after normalizing";
+            failed.store(true);
+            break;
+          }
+          sum += sc * scorers_[k].second;
+        }
+        if (failed.load()) break;
+        plain_tot[i] = sum;
       }
+    if (table && !failed.load() && !miss.empty()) {
+      for (size_t k = 0; k < ns; ++k) {  // row columns of the recomputed nodes
+        if (!((row_mask >> k) & 1)) continue;
+        int64_t* col = &table->raw[k * table->n];
+        for (uint32_t i : miss) col[tpos[i]] = per[k][i].score;
+      }
+      for (uint32_t i : miss) {
+        const size_t pos = static_cast<size_t>(tpos[i]);
+        table->score_gen[pos] = have_gens ? eq->gens[i] : nodes[i]->generation;
+        table->cols[pos] = row_mask;
+        table->plain_mask[pos] = plain_mask;
+        table->plain_sum[pos] = plain_tot.size() == n && plain_mask ? plain_tot[i] : 0;
+      }
+    }
     Parallelizer::record_inline(&score_site_, Parallelizer::now_ns() - s0, static_cast<int>(n), static_cast<int>(n));
   } else {
     handle_.parallelizer->until_forked(static_cast<int>(n), [&](int i) { score_node(static_cast<size_t>(i)); },
@@ -525,10 +592,13 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
   int64_t skipped_total = 0;  // the skipped plugins' constant contribution
   for (size_t k = 0; k < scorers_.size(); ++k)
     if (skip[k]) skipped_total += scorers_[k].first->score_skip_value() * scorers_[k].second;
-  if (skipped_total)
+  if (plain_mask) {
+    for (size_t i = 0; i < n; ++i) total[i].score += skipped_total + plain_tot[i];
+  } else if (skipped_total) {
     for (size_t i = 0; i < n; ++i) total[i].score += skipped_total;
+  }
   for (size_t k = 0; k < scorers_.size(); ++k) {
-    if (skip[k]) continue;
+    if (skip[k] || is_plain(k)) continue;
     auto& pl = scorers_[k].first;
     if (pl->has_normalize_score()) {
       if (pl->normalize_uses_names())

@@ -28,44 +28,59 @@ struct ProfileConfig {
   static ProfileConfig from_json(const Json& j);
 };
 
-// One (pod template, node) entry of the scheduler's equivalence cache:
-// the Filter verdict and raw (pre-normalization) Score values last computed
-// for that template on that node, valid while the node's generation matches.
-// Raw scores per scorer of one (template, node): inline up to 12 scorers, so
-// a cache hit reads the slot itself and no further heap block.
-class RawScores {
- public:
-  size_t size() const { return n_; }
-  void resize(size_t n) {
-    if (n > kInline) spill_.resize(n);
-    n_ = n;
-  }
-  int64_t& operator[](size_t i) { return n_ > kInline ? spill_[i] : inl_[i]; }
-  int64_t operator[](size_t i) const { return n_ > kInline ? spill_[i] : inl_[i]; }
-
- private:
-  static constexpr size_t kInline = 12;  // the default profile plus FlexGPU and NRT score with 10
-  int64_t inl_[kInline] = {};
-  std::vector<int64_t> spill_;
-  size_t n_ = 0;
-};
-
-struct EqSlot {
-  int64_t filter_gen = -1;
-  Status filter;
+// One pod template's equivalence cache over the snapshot's node positions,
+// kept as columns (structure of arrays): a lookup reads a node version and a
+// value from dense arrays instead of a per-node record of a few hundred bytes,
+// so a scan over a window of nodes touches one cache line per 8 nodes and
+// column. Filter verdicts and raw (pre-normalization) Score values are valid
+// while the node's generation matches the one recorded with them.
+struct EqTable {
+  size_t n = 0;   // snapshot positions
+  size_t ns = 0;  // scorers (raw columns)
+  std::vector<int64_t> filter_gen;
+  std::vector<Status> filter;
   // The verdict with the node's nominated pods added, for the set of them
   // whose signature is nom_sig (Framework::nominated_signature).
-  int64_t nom_gen = -1;
-  uint64_t nom_sig = 0;
-  Status nom_filter;
-  int64_t score_gen = -1;
-  RawScores raw;  // per scorer, in Framework scorer order
+  std::vector<int64_t> nom_gen;
+  std::vector<uint64_t> nom_sig;
+  std::vector<Status> nom_filter;
+  // Score, per node version score_gen[pos]: raw[k * n + pos] for the scorers
+  // k in cols[pos] (bit k), and plain_sum, the weighted sum of the "plain"
+  // scorers in plain_mask[pos] (node-local, no normalization).
+  std::vector<int64_t> score_gen;
+  std::vector<uint64_t> cols;
+  std::vector<uint64_t> plain_mask;
+  std::vector<int64_t> plain_sum;
+  std::vector<int64_t> raw;
+
+  void reset(size_t nodes) {
+    n = nodes;
+    ns = 0;
+    filter_gen.assign(n, -1);
+    filter.assign(n, Status());
+    nom_gen.assign(n, -1);
+    nom_sig.assign(n, 0);
+    nom_filter.assign(n, Status());
+    score_gen.assign(n, -1);
+    cols.assign(n, 0);
+    plain_mask.assign(n, 0);
+    plain_sum.assign(n, 0);
+    raw.clear();
+  }
+  // Sizes the raw columns for `scorers` (every score entry invalid on change).
+  void ensure_scorers(size_t scorers) {
+    if (ns == scorers && raw.size() == ns * n) return;
+    ns = scorers;
+    raw.assign(ns * n, 0);
+    score_gen.assign(n, -1);
+  }
+  int64_t& raw_at(size_t k, size_t pos) { return raw[k * n + pos]; }
 };
 struct EqScoreCache {
-  std::vector<char> local;       // per scorer: raw score is node-local for this pod
-  std::vector<EqSlot*> slots;    // per node passed to run_score (nullptr: uncached)
-  std::vector<int64_t> gens;     // the nodes' generations (Snapshot::gen), same order
-  std::vector<int> pos;          // the nodes' snapshot positions, same order
+  std::vector<char> local;    // per scorer: raw score is node-local for this pod
+  EqTable* table = nullptr;   // the template's table (nullptr: uncached)
+  std::vector<int64_t> gens;  // the nodes' generations (Snapshot::gen), in run_score order
+  std::vector<int> pos;       // the nodes' snapshot positions, same order
 };
 
 class Framework {

@@ -1022,9 +1022,9 @@ Scheduler::EqEntry* Scheduler::eq_entry(Framework& fw, const Pod& p) {
     }
     e = std::make_unique<EqEntry>();
   }
-  if (e->epoch != snapshot_.node_epoch || e->slots.size() != snapshot_.nodes.size()) {
+  if (e->epoch != snapshot_.node_epoch || e->table.n != snapshot_.nodes.size()) {
     e->epoch = snapshot_.node_epoch;
-    e->slots.assign(snapshot_.nodes.size(), EqSlot{});
+    e->table.reset(snapshot_.nodes.size());
     e->scan.valid = false;
   }
   return e.get();
@@ -1160,33 +1160,33 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       own = fw.run_filter_with_nominated_pods(s, p, ni);
       return &own;
     }
-    EqSlot& slot = eq->slots[pos];
+    EqTable& t = eq->table;
     uint64_t sig = 0;
     bool cacheable = true;
     if (nom_mark && nom_mark[pos]) sig = fw.nominated_signature(s, p, nom_list_[pos], &cacheable);
     const int64_t gen = snapshot_.gen[pos];
     if (sig == 0) {  // no nominated pod counts for this pod: the plain verdict
-      if (slot.filter_gen == gen) {
+      if (t.filter_gen[pos] == gen) {
         *hit = true;
       } else {
-        slot.filter = fw.run_filter(s, p, ni);
-        slot.filter_gen = gen;
+        t.filter[pos] = fw.run_filter(s, p, ni);
+        t.filter_gen[pos] = gen;
       }
-      return &slot.filter;
+      return &t.filter[pos];
     }
-    if (cacheable && slot.nom_gen == gen && slot.nom_sig == sig) {
+    if (cacheable && t.nom_gen[pos] == gen && t.nom_sig[pos] == sig) {
       *hit = true;
-      return &slot.nom_filter;
+      return &t.nom_filter[pos];
     }
     Status st = fw.run_filter_with_nominated_pods(s, p, ni);
     if (!cacheable) {
       own = std::move(st);
       return &own;
     }
-    slot.nom_filter = std::move(st);
-    slot.nom_gen = gen;
-    slot.nom_sig = sig;
-    return &slot.nom_filter;
+    t.nom_filter[pos] = std::move(st);
+    t.nom_gen[pos] = gen;
+    t.nom_sig[pos] = sig;
+    return &t.nom_filter[pos];
   };
   // The template's last scan of this window (EqEntry::scan): a gang rank
   // after its sibling re-evaluates only the scanned nodes whose version
@@ -1647,13 +1647,10 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         esc.local.clear();
         if (eq) fw->local_scorers(*pod, snapshot_, esc.local);
         if (!esc.local.empty()) {
-          esc.slots.resize(feasible.size());
+          esc.table = &eq->table;
           esc.gens.resize(feasible.size());
           esc.pos.assign(feasible_pos_buf_.begin(), feasible_pos_buf_.begin() + feasible.size());
-          for (size_t i = 0; i < feasible.size(); ++i) {
-            esc.slots[i] = &eq->slots[feasible_pos_buf_[i]];
-            esc.gens[i] = snapshot_.gen[feasible_pos_buf_[i]];
-          }
+          for (size_t i = 0; i < feasible.size(); ++i) esc.gens[i] = snapshot_.gen[feasible_pos_buf_[i]];
         }
         if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores, nullptr, esc.local.empty() ? nullptr : &esc);
       }
@@ -1985,16 +1982,20 @@ Json Scheduler::explain(const Json& pod_obj) {
       // The scheduling path's totals (all-zero plugins skipped, their
       // normalized constant still added, the plugins' snapshot-array paths
       // given the nodes' positions) for parity checks against "total".
+      // The template's equivalence slots are used as the scheduling cycle
+      // uses them (hits included), so the parity check covers cached sums.
       std::vector<NodeScore> hot;
-      EqScoreCache pos_only;  // no cached slots: positions and versions only
-      pos_only.slots.assign(feasible.size(), nullptr);
+      EqScoreCache hot_cache;
+      EqEntry* eq = eq_entry(*fw, *pod);
+      if (eq) fw->local_scorers(*pod, snapshot_, hot_cache.local);
       for (const NodeInfo* ni : feasible) {
         auto it = snapshot_.index.find(ni->name());
         if (it == snapshot_.index.end()) break;
-        pos_only.pos.push_back(static_cast<int>(it->second));
-        pos_only.gens.push_back(snapshot_.gen[it->second]);
+        hot_cache.pos.push_back(static_cast<int>(it->second));
+        hot_cache.gens.push_back(snapshot_.gen[it->second]);
       }
-      EqScoreCache* hot_eq = pos_only.pos.size() == feasible.size() ? &pos_only : nullptr;
+      if (eq && !hot_cache.local.empty()) hot_cache.table = &eq->table;
+      EqScoreCache* hot_eq = hot_cache.pos.size() == feasible.size() ? &hot_cache : nullptr;
       if (fw->run_score(*state, *pod, feasible, hot, nullptr, hot_eq).is_success()) {
         Json h = Json::object();
         for (size_t i = 0; i < feasible.size(); ++i) h.set(feasible[i]->name(), Json(hot[i].score));

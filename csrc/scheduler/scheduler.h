@@ -235,7 +235,7 @@ class Scheduler {
   // node position, valid for one node epoch (node set / Node objects).
   struct EqEntry {
     uint64_t epoch = 0;
-    std::vector<EqSlot> slots;
+    EqTable table;
     // The last serial Filter scan of this template (find_nodes_that_fit):
     // per scan offset from `start`, the node version it saw and its verdict.
     struct ScanMemo {

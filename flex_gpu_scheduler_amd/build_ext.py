@@ -158,15 +158,18 @@ def build_asan(verbose: bool = True) -> Path:
     return out
 
 
-def build_prof(verbose: bool = True, gprof: bool = True) -> Path:
+def build_prof(verbose: bool = True, gprof: bool = True, debuginfo: bool = False) -> Path:
     """Native stress driver (no Python in the loop). With `gprof` it is built
     with -pg for a per-function CPU profile of the scheduling hot path;
-    without, at the core's optimisation level for timing."""
+    without, at the core's optimisation level for timing (`debuginfo` adds
+    -g, same code, for sample_report --lines)."""
     includes = [str(CSRC)]
     extra = ["-pg", "-g", "-O2", "-fno-omit-frame-pointer", "-fno-inline-functions-called-once"] if gprof else []
-    sub = "prof" if gprof else "stress"
+    if debuginfo and not gprof:
+        extra = ["-g"]
+    sub = "prof" if gprof else ("stress_g" if debuginfo else "stress")
     objs = build_objects(core_sources() + [CSRC / "tools" / "stress_main.cc"], BUILD / sub, extra, includes)
-    out = BUILD / ("xsched_stress_prof" if gprof else "xsched_stress")
+    out = BUILD / ("xsched_stress_prof" if gprof else ("xsched_stress_g" if debuginfo else "xsched_stress"))
     cmd = ["g++", *(["-pg"] if gprof else []), "-pthread", *[str(o) for o in objs], *LINK_LIBS, "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -203,13 +206,14 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--asan", action="store_true")
     ap.add_argument("--prof", action="store_true")
     ap.add_argument("--stress", action="store_true")
+    ap.add_argument("--stress-g", action="store_true", help="stress driver with -g (sample_report --lines)")
     ap.add_argument("--tests", action="store_true")
     a = ap.parse_args(argv)
     if a.tests:
         build_tests()
         return 0
-    if a.prof or a.stress:
-        build_prof(gprof=a.prof)
+    if a.prof or a.stress or a.stress_g:
+        build_prof(gprof=a.prof, debuginfo=a.stress_g)
         return 0
     everything = not (a.core or a.hip or a.tsan or a.asan)
     if a.core or everything:

@@ -128,13 +128,50 @@ def summarize(dump: str, exe: str, top: int = 25) -> dict:
     return out
 
 
+def lines(dump: str, exe: str, func: str, top: int = 25) -> list[tuple[float, str]]:
+    """Source lines (addr2line on a -g build) of the busy samples whose leaf
+    frame is in our code and whose function name contains `func`, as
+    fractions of those samples."""
+    samples, resolve = load(dump, exe)
+    base = 0
+    with open(dump) as f:
+        for line in f:
+            if line.startswith("exe_base "):
+                base = int(line.split()[1], 16)
+                break
+    offs: collections.Counter = collections.Counter()
+    for _tname, pcs in samples:
+        if len(pcs) < 3:
+            continue
+        frames = [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
+        if is_idle(frames):
+            continue
+        if func in frames[0] and "[lib" not in frames[0]:
+            offs[pcs[2] - base] += 1
+    if not offs:
+        return []
+    addrs = list(offs)
+    out = subprocess.run(["addr2line", "-C", "-e", exe, *[hex(a) for a in addrs]], capture_output=True,
+                         text=True, check=False).stdout.splitlines()
+    by_line: collections.Counter = collections.Counter()
+    for a, loc in zip(addrs, out):
+        by_line[loc.split(" (")[0]] += offs[a]
+    matched = sum(offs.values())  # fractions of the matched function(s)' own samples
+    return [(c / max(1, matched), loc) for loc, c in by_line.most_common(top)]
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("dump")
     ap.add_argument("--exe", default="build/xsched_stress")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--json", default="")
+    ap.add_argument("--lines", default="", help="per source line of the leaf frames in functions matching this")
     a = ap.parse_args()
+    if a.lines:
+        for frac, loc in lines(a.dump, a.exe, a.lines, a.top):
+            print(f"{100 * frac:5.1f}%  {loc}")
+        return 0
     rep = summarize(a.dump, a.exe, a.top)
     if a.json:
         with open(a.json, "w") as f:
