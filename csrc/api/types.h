@@ -36,12 +36,47 @@ using StrMap = std::vector<std::pair<std::string, std::string>>;  // small, orde
 const std::string* strmap_get(const StrMap& m, std::string_view k);
 StrMap strmap_from_json(const Json& j);
 
+// An object's labels or annotations, shared between copies of the object
+// until one of them changes (copy on write): the scheduler copies a Pod per
+// assume and per bind confirmation, and the maps are rarely touched then.
+class SharedStrMap {
+ public:
+  SharedStrMap() = default;
+  SharedStrMap(StrMap m) { *this = std::move(m); }  // NOLINT(google-explicit-constructor)
+  SharedStrMap(std::initializer_list<std::pair<std::string, std::string>> l) : SharedStrMap(StrMap(l)) {}
+  SharedStrMap& operator=(StrMap m) {
+    p_ = m.empty() ? nullptr : std::make_shared<const StrMap>(std::move(m));
+    return *this;
+  }
+  const StrMap& get() const { return p_ ? *p_ : none(); }
+  operator const StrMap&() const { return get(); }  // NOLINT(google-explicit-constructor)
+  StrMap::const_iterator begin() const { return get().begin(); }
+  StrMap::const_iterator end() const { return get().end(); }
+  size_t size() const { return p_ ? p_->size() : 0; }
+  bool empty() const { return size() == 0; }
+  // The map for writing: copied first when another object shares it.
+  StrMap& mut() {
+    if (!p_) p_ = std::make_shared<const StrMap>();
+    else if (p_.use_count() > 1) p_ = std::make_shared<const StrMap>(*p_);
+    return const_cast<StrMap&>(*p_);
+  }
+  bool operator==(const SharedStrMap& o) const { return p_ == o.p_ || get() == o.get(); }
+  bool operator!=(const SharedStrMap& o) const { return !(*this == o); }
+
+ private:
+  static const StrMap& none() {
+    static const StrMap e;
+    return e;
+  }
+  std::shared_ptr<const StrMap> p_;
+};
+
 inline constexpr const char* kHostnameLabel = "kubernetes.io/hostname";
 
 struct ObjectMeta {
   std::string ns, name, uid;
   int64_t resource_version = 0;
-  StrMap labels, annotations;
+  SharedStrMap labels, annotations;
   MicroTime creation = 0;
   MicroTime deletion = 0;  // deletionTimestamp
   std::string key() const { return ns.empty() ? name : ns + "/" + name; }

@@ -290,14 +290,15 @@ class FlexGPU : public Plugin {
     if (!pl.parts.empty()) st->annotations.set(gn.partition_annotation, Json(join_parts(pl.parts)));
     const Json& ann = st->annotations;
     h_.cache->annotate_assumed_pod(p->uid(), [&](Pod& cp) {
+      StrMap& am = cp.meta.annotations.mut();
       for (const auto& kv : ann.members()) {
         bool set = false;
-        for (auto& a : cp.meta.annotations)
+        for (auto& a : am)
           if (a.first == kv.first) {
             a.second = kv.second.as_string();
             set = true;
           }
-        if (!set) cp.meta.annotations.emplace_back(kv.first, kv.second.as_string());
+        if (!set) am.emplace_back(kv.first, kv.second.as_string());
       }
     });
     s.write(kFlexGPUStateKey, st);
@@ -309,7 +310,7 @@ class FlexGPU : public Plugin {
     s.erase(kFlexGPUStateKey);
     if (!h_.cache->is_assumed(p->uid())) return;
     h_.cache->mutate_pod(p->uid(), [&](Pod& cp) {
-      auto& a = cp.meta.annotations;
+      auto& a = cp.meta.annotations.mut();
       a.erase(std::remove_if(a.begin(), a.end(),
                              [&](const auto& kv) {
                                return kv.first == gn.index_annotation || kv.first == gn.partition_annotation;

@@ -596,7 +596,7 @@ class VolumeBinding : public Plugin {
         copy->claim_name = c->meta.name;
         copy->claim_uid = c->meta.uid;
         if (!prebound && !copy->meta.annotation(kAnnBoundByController))
-          copy->meta.annotations.emplace_back(kAnnBoundByController, "yes");
+          copy->meta.annotations.mut().emplace_back(kAnnBoundByController, "yes");
         nv = copy;
         assume_pv(nv);
       }
@@ -605,12 +605,13 @@ class VolumeBinding : public Plugin {
     for (const auto& c : pv->provisions) {
       auto copy = std::make_shared<PersistentVolumeClaim>(*c);
       bool set = false;
-      for (auto& [k, v] : copy->meta.annotations)
+      StrMap& am = copy->meta.annotations.mut();
+      for (auto& [k, v] : am)
         if (k == kAnnSelectedNode) {
           v = node;
           set = true;
         }
-      if (!set) copy->meta.annotations.emplace_back(kAnnSelectedNode, node);
+      if (!set) am.emplace_back(kAnnSelectedNode, node);
       assume_pvc(copy);
       assumed->provisions.push_back(copy);
     }

@@ -131,8 +131,8 @@ py::dict pod_struct_summary(const Pod& pod) {
   d["node_name"] = p->node_name;
   d["uid"] = p->uid();
   d["resource_version"] = p->meta.resource_version;
-  d["labels"] = p->meta.labels;
-  d["annotations"] = p->meta.annotations;
+  d["labels"] = p->meta.labels.get();
+  d["annotations"] = p->meta.annotations.get();
   d["phase"] = p->phase;
   d["scheduled_at"] = static_cast<int64_t>(p->scheduled_at);
   d["start_time"] = static_cast<int64_t>(p->start_time);
