@@ -446,9 +446,9 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
   // valid at score_gen (the set `cols`) and the weighted sum of the plain
   // scorers (node-local, no normalization) over the set `plain_mask`.
   EqTable* table =
-      eq && eq->table && eq->pos.size() == n && eq->local.size() == ns && ns <= 64 ? eq->table : nullptr;
+      eq && eq->table && eq->npos == n && eq->local.size() == ns && ns <= 64 ? eq->table : nullptr;
   if (table) table->ensure_scorers(ns);
-  const int* tpos = table ? eq->pos.data() : nullptr;
+  const int* tpos = table ? eq->pos : nullptr;
   uint64_t local_mask = 0;  // non-skipped node-local scorers
   if (table)
     for (size_t k = 0; k < ns; ++k)
@@ -513,14 +513,14 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
     miss.clear();
     if (plain_mask) plain_tot.assign(n, 0);
     bool any_hit = false;
-    const bool have_gens = eq && eq->gens.size() == n;
+    const bool have_gens = eq && eq->gen && eq->npos == n;
     if (table) {
       const int64_t* sgen = table->score_gen.data();
       const uint64_t* pm = table->plain_mask.data();
       const uint64_t* cm = table->cols.data();
       for (size_t i = 0; i < n; ++i) {
         const size_t pos = static_cast<size_t>(tpos[i]);
-        const int64_t gen = have_gens ? eq->gens[i] : nodes[i]->generation;
+        const int64_t gen = have_gens ? eq->gen[pos] : nodes[i]->generation;
         const bool h = sgen[pos] == gen && pm[pos] == plain_mask && (cm[pos] & row_mask) == row_mask;
         hit[i] = h;
         if (!h) miss.push_back(static_cast<uint32_t>(i));
@@ -545,7 +545,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
       if (skip[k]) continue;
       const bool reuse = any_hit && eq->local[k];
       Status st = scorers_[k].first->score_many(s, p, nodes, reuse ? hit.data() : nullptr, row,
-                                                (eq && eq->pos.size() == n) ? eq->pos.data() : nullptr);
+                                                (eq && eq->npos == n) ? eq->pos : nullptr);
       if (!st.is_success()) {
         err = "running Score plugin " + scorers_[k].first->name() + ": " + st.message();
         failed.store(true);
@@ -577,7 +577,7 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
       }
       for (uint32_t i : miss) {
         const size_t pos = static_cast<size_t>(tpos[i]);
-        table->score_gen[pos] = have_gens ? eq->gens[i] : nodes[i]->generation;
+        table->score_gen[pos] = have_gens ? eq->gen[pos] : nodes[i]->generation;
         table->cols[pos] = row_mask;
         table->plain_mask[pos] = plain_mask;
         table->plain_sum[pos] = plain_tot.size() == n && plain_mask ? plain_tot[i] : 0;

@@ -78,9 +78,10 @@ struct EqTable {
 };
 struct EqScoreCache {
   std::vector<char> local;    // per scorer: raw score is node-local for this pod
-  EqTable* table = nullptr;   // the template's table (nullptr: uncached)
-  std::vector<int64_t> gens;  // the nodes' generations (Snapshot::gen), in run_score order
-  std::vector<int> pos;       // the nodes' snapshot positions, same order
+  EqTable* table = nullptr;      // the template's table (nullptr: uncached)
+  const int* pos = nullptr;      // the nodes' snapshot positions, in run_score order
+  size_t npos = 0;               // entries in pos
+  const int64_t* gen = nullptr;  // node versions by snapshot position (Snapshot::gen)
 };
 
 class Framework {

@@ -1648,9 +1648,9 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
         if (eq) fw->local_scorers(*pod, snapshot_, esc.local);
         if (!esc.local.empty()) {
           esc.table = &eq->table;
-          esc.gens.resize(feasible.size());
-          esc.pos.assign(feasible_pos_buf_.begin(), feasible_pos_buf_.begin() + feasible.size());
-          for (size_t i = 0; i < feasible.size(); ++i) esc.gens[i] = snapshot_.gen[feasible_pos_buf_[i]];
+          esc.pos = feasible_pos_buf_.data();
+          esc.npos = feasible.size();
+          esc.gen = snapshot_.gen.data();
         }
         if (st.is_success()) st = fw->run_score(*state, *pod, feasible, scores, nullptr, esc.local.empty() ? nullptr : &esc);
       }
@@ -1986,16 +1986,19 @@ Json Scheduler::explain(const Json& pod_obj) {
       // uses them (hits included), so the parity check covers cached sums.
       std::vector<NodeScore> hot;
       EqScoreCache hot_cache;
+      std::vector<int> hot_pos;
       EqEntry* eq = eq_entry(*fw, *pod);
       if (eq) fw->local_scorers(*pod, snapshot_, hot_cache.local);
       for (const NodeInfo* ni : feasible) {
         auto it = snapshot_.index.find(ni->name());
         if (it == snapshot_.index.end()) break;
-        hot_cache.pos.push_back(static_cast<int>(it->second));
-        hot_cache.gens.push_back(snapshot_.gen[it->second]);
+        hot_pos.push_back(static_cast<int>(it->second));
       }
       if (eq && !hot_cache.local.empty()) hot_cache.table = &eq->table;
-      EqScoreCache* hot_eq = hot_cache.pos.size() == feasible.size() ? &hot_cache : nullptr;
+      hot_cache.pos = hot_pos.data();
+      hot_cache.npos = hot_pos.size();
+      hot_cache.gen = snapshot_.gen.data();
+      EqScoreCache* hot_eq = hot_pos.size() == feasible.size() ? &hot_cache : nullptr;
       if (fw->run_score(*state, *pod, feasible, hot, nullptr, hot_eq).is_success()) {
         Json h = Json::object();
         for (size_t i = 0; i < feasible.size(); ++i) h.set(feasible[i]->name(), Json(hot[i].score));
