@@ -280,6 +280,15 @@ struct Pod {
   // that NodeInfos (and Snapshot readers) already hold (cache.cc).
   RelaxedI64 start_time = 0;
   RelaxedI64 scheduled_at = 0;
+  // The informer instance whose lister holds exactly this object (0: none
+  // or superseded). Not copied: a copy is a different object.
+  struct ListedMark {
+    std::atomic<uint64_t> by{0};
+    ListedMark() = default;
+    ListedMark(const ListedMark&) {}
+    ListedMark& operator=(const ListedMark&) { return *this; }
+  };
+  mutable ListedMark listed;
 
   // ---- derived at parse time ----
   Res request;          // computePodResourceRequest: max(sum(containers), each init) + overhead

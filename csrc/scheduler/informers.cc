@@ -22,8 +22,10 @@ void Informers::upsert_pod(const PodPtr& p) {
   auto [it, fresh] = pods_.try_emplace(p->key(), p);
   if (!fresh) {
     if (it->second->pg_key) group_remove(it->second);
+    if (it->second != p) it->second->listed.by.store(0, std::memory_order_relaxed);
     it->second = p;
   }
+  p->listed.by.store(instance_, std::memory_order_relaxed);
   if (p->pg_key) pods_by_group_[p->pg_key].push_back(p);
 }
 
@@ -32,6 +34,7 @@ void Informers::delete_pod(const Pod& p) {
   auto it = pods_.find(p.key());
   if (it == pods_.end()) return;
   if (it->second->pg_key) group_remove(it->second);
+  it->second->listed.by.store(0, std::memory_order_relaxed);
   pods_.erase(it);
 }
 
@@ -41,6 +44,7 @@ void Informers::delete_pods(const std::vector<PodPtr>& ps) {
     auto it = pods_.find(p->key());
     if (it == pods_.end()) continue;
     if (it->second->pg_key) group_remove(it->second);
+    it->second->listed.by.store(0, std::memory_order_relaxed);
     pods_.erase(it);
   }
 }

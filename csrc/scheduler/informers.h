@@ -68,6 +68,8 @@ class Informers {
   std::vector<PDBPtr> pdbs() const;
   PriorityClassPtr priority_class(const std::string& name) const;
   size_t pod_count() const;
+  // True while `p` is the object this lister holds for its key (no lookup).
+  bool lists(const Pod& p) const { return p.listed.by.load(std::memory_order_relaxed) == instance_; }
   PVPtr pv(const std::string& name) const;
   PVCPtr pvc(const std::string& ns, const std::string& name) const;
   StorageClassPtr storage_class(const std::string& name) const;

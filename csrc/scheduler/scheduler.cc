@@ -1585,9 +1585,14 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   PodPtr pod = qpi->pod;
   Framework* fw = framework_for(pod->scheduler_name);
   if (!fw) return;
-  // skipPodSchedule: deleted or already assumed.
-  PodPtr latest = informers_->pod(pod->ns(), pod->name());
-  if (!latest || latest->uid() != pod->uid() || latest->terminating() || !latest->node_name.empty()) return;
+  // skipPodSchedule: deleted or already assumed. The queued object is
+  // usually still the lister's current one (no lookup then).
+  if (informers_->lists(*pod)) {
+    if (pod->terminating() || !pod->node_name.empty()) return;
+  } else {
+    PodPtr latest = informers_->pod(pod->ns(), pod->name());
+    if (!latest || latest->uid() != pod->uid() || latest->terminating() || !latest->node_name.empty()) return;
+  }
 
   int64_t cycle_start = clock_->now_us();
   auto state = std::make_shared<CycleState>();
