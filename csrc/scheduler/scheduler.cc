@@ -964,15 +964,22 @@ int Scheduler::num_feasible_nodes_to_find(Framework& fw, int n) const {
 
 // Replaced snapshot versions may hold the last reference to deleted pods;
 // free them in batches on a binder thread instead of in the scheduling cycle.
+void Scheduler::run_bind_task(BindTask* t) {
+  std::shared_ptr<BindTask> hold = std::move(t->keep);
+  t->self->binding_cycle(*t, t->permit_status);
+}
+
 void Scheduler::release_retired() {
   if (snapshot_.retired.size() >= 32) {
     auto batch = std::make_shared<std::vector<NodeInfoPtr>>(std::move(snapshot_.retired));
     snapshot_.retired.clear();
+    snapshot_.retired.reserve(64);  // not regrown from empty push by push
     binder_->submit([batch] { batch->clear(); });
   }
   if (snapshot_.retired_deltas.size() >= 256) {
     auto batch = std::make_shared<std::vector<PodDelta>>(std::move(snapshot_.retired_deltas));
     snapshot_.retired_deltas.clear();
+    snapshot_.retired_deltas.reserve(512);
     binder_->submit([batch] { batch->clear(); });
   }
 }
@@ -1749,10 +1756,14 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   task->permit_start_us = permit_start;
   task->to_activate = to_activate;
   task->e2e = cycle_metrics(*fw).e2e;
-  Status pst = fw->run_permit(*state, assumed, host, [task](const Status& wst) {
-    task->self->binder_->submit([task, wst] { task->self->binding_cycle(*task, wst); });
+  task->keep = task;
+  BindTask* tp = task.get();
+  Status pst = fw->run_permit(*state, assumed, host, [tp](const Status& wst) {
+    tp->permit_status = wst;
+    tp->self->binder_->submit([tp] { run_bind_task(tp); });
   });
   if (!pst.is_success() && !pst.is_wait()) {
+    task->keep.reset();  // rejected before waiting: the callback never runs
     inflight_.fetch_sub(1);
     fw->run_unreserve(*state, assumed, host);
     cache_->forget_pod(*assumed);
@@ -1781,9 +1792,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     std::lock_guard<std::mutex> g(stats_mu_);
     ++stats_.scheduled;
   }
-  if (pst.is_success()) {
-    binder_->submit([task = std::move(task)] { task->self->binding_cycle(*task, Status()); });
-  }
+  if (pst.is_success()) binder_->submit([tp] { run_bind_task(tp); });
   if (tracer_.enabled()) {
     int64_t t_end = clock_->now_us();
     tracer_.record(TraceEvent{"assume_reserve_permit", assumed->key(), "", algo_end, t_end - algo_end, 0});

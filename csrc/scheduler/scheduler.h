@@ -335,7 +335,13 @@ class Scheduler {
     int64_t permit_start_us = 0;
     std::shared_ptr<PodsToActivate> to_activate;
     Histogram* e2e = nullptr;  // scheduler_e2e_scheduling_duration_seconds{profile}
+    Status permit_status;      // set by the Permit waiter before the task is queued
+    // The task owns itself until its binding cycle starts, so the Permit
+    // callback and the binder queue hold a raw pointer: a one-pointer capture
+    // is stored inside std::function, without a heap block per pod.
+    std::shared_ptr<BindTask> keep;
   };
+  static void run_bind_task(BindTask* t);
   void binding_cycle(const BindTask& t, const Status& permit_status);
   void handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const Status& st, const std::string& reason,
                       const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins);

@@ -160,6 +160,22 @@ def lines(dump: str, exe: str, func: str, top: int = 25) -> list[tuple[float, st
     return [(c / max(1, matched), loc) for loc, c in by_line.most_common(top)]
 
 
+def callers(dump: str, exe: str, func: str, top: int = 25) -> list[tuple[float, str]]:
+    """For busy samples whose first frame in our code matches `func`: the
+    next frame in our code (who called it), as fractions of those samples."""
+    samples, resolve = load(dump, exe)
+    by: collections.Counter = collections.Counter()
+    for _tname, pcs in samples:
+        frames = [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
+        if not frames or is_idle(frames):
+            continue
+        own = [f for f in frames if "[lib" not in f]
+        if len(own) >= 1 and func in own[0]:
+            by[short(own[1]) if len(own) > 1 else "?"] += 1
+    total = sum(by.values())
+    return [(c / max(1, total), f) for f, c in by.most_common(top)]
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("dump")
@@ -167,7 +183,12 @@ def main() -> int:
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--json", default="")
     ap.add_argument("--lines", default="", help="per source line of the leaf frames in functions matching this")
+    ap.add_argument("--callers", default="", help="callers of the functions matching this (first own-code frame)")
     a = ap.parse_args()
+    if a.callers:
+        for frac, f in callers(a.dump, a.exe, a.callers, a.top):
+            print(f"{100 * frac:5.1f}%  {f}")
+        return 0
     if a.lines:
         for frac, loc in lines(a.dump, a.exe, a.lines, a.top):
             print(f"{100 * frac:5.1f}%  {loc}")
