@@ -397,6 +397,16 @@ struct QueuedPodInfo {
   // QueueSort plugins may memoize an immutable sort key here (e.g.
   // Coscheduling's PodGroup creation time); INT64_MIN = not cached.
   mutable int64_t sort_key_cache = INT64_MIN;
+  // pod->priority, memoized for heap comparisons (valid while prio_of == pod.get()).
+  mutable const Pod* prio_of = nullptr;
+  mutable int32_t prio_cache = 0;
+  int32_t priority() const {
+    if (prio_of != pod.get()) {
+      prio_cache = pod->priority;
+      prio_of = pod.get();
+    }
+    return prio_cache;
+  }
   // Position in the PodHeap currently holding this entry (a QueuedPodInfo
   // sits in at most one heap at a time); lets sift-up/down skip uid hashing.
   size_t heap_index = 0;

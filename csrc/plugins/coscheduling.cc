@@ -105,7 +105,8 @@ class Coscheduling : public Plugin {
     return q.initial_attempt_wall;
   }
   bool less(const QueuedPodInfo& a, const QueuedPodInfo& b) const override {
-    if (a.pod->priority != b.pod->priority) return a.pod->priority > b.pod->priority;
+    const int32_t pa = a.priority(), pb = b.priority();
+    if (pa != pb) return pa > pb;
     MicroTime ta = creation(a), tb = creation(b);
     if (ta == tb) return key_less(*a.pod, *b.pod);
     return ta < tb;
