@@ -72,6 +72,20 @@ void default_normalize_score(int64_t max_priority, bool reverse, std::vector<Nod
     for (auto& s : scores) s.score = table[s.score];
     return;
   }
+  if (min_count >= 0 && max_priority > 0 && max_count <= (int64_t{1} << 52) / max_priority) {
+    // Non-negative numerators below 2^52 (exact as doubles): a double
+    // reciprocal is within one of the quotient, and one correction step
+    // each way makes it exact.
+    const double inv = 1.0 / static_cast<double>(max_count);
+    for (auto& s : scores) {
+      const int64_t num = max_priority * s.score;
+      int64_t q = static_cast<int64_t>(static_cast<double>(num) * inv);
+      if (q * max_count > num) --q;
+      else if ((q + 1) * max_count <= num) ++q;
+      s.score = reverse ? max_priority - q : q;
+    }
+    return;
+  }
   for (auto& s : scores) {
     int64_t sc = max_priority * s.score / max_count;
     if (reverse) sc = max_priority - sc;

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "api/types.h"
+#include "framework/plugin.h"
 #include "common/clock.h"
 #include "common/json.h"
 #include "common/parallel.h"
@@ -574,6 +575,32 @@ TEST(cache_debugger_reports_drift) {
   auto fields = ni.verify();
   CHECK_EQ(fields.size(), 1u);
   CHECK_EQ(fields[0], "requested");
+}
+
+TEST(default_normalize_matches_integer_division) {
+  // The table and reciprocal paths of default_normalize_score against the
+  // plain max_priority * score / max over small, mid and 2^40-sized raws.
+  std::mt19937_64 r(7);
+  for (int t = 0; t < 3000; ++t) {
+    const int n = 1 + static_cast<int>(r() % 600);
+    const int64_t cap = t % 3 == 0 ? 200 : t % 3 == 1 ? (int64_t{1} << 40) : 100000;
+    std::vector<NodeScore> a(static_cast<size_t>(n));
+    for (auto& s : a) s.score = static_cast<int64_t>(r() % static_cast<uint64_t>(cap + 1));
+    std::vector<NodeScore> b = a;
+    const bool rev = (r() & 1) != 0;
+    default_normalize_score(kMaxNodeScore, rev, a);
+    int64_t mx = 0;
+    for (const auto& s : b) mx = std::max(mx, s.score);
+    for (auto& s : b) {
+      if (mx == 0) {
+        if (rev) s.score = kMaxNodeScore;
+        continue;
+      }
+      const int64_t sc = kMaxNodeScore * s.score / mx;
+      s.score = rev ? kMaxNodeScore - sc : sc;
+    }
+    for (int i = 0; i < n; ++i) CHECK_EQ(a[static_cast<size_t>(i)].score, b[static_cast<size_t>(i)].score);
+  }
 }
 
 int main() {
