@@ -25,6 +25,13 @@ for step in "$@"; do
               timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-scenarios --no-placement \
                 --no-service-mode > "$OUT/bench64_$i.json" 2> "$OUT/bench64_$i.err" || exit $?
             done ;;
+    bench_r3shape)
+      # The round-3 measurement shape (20 timed single-wave steps) next to the
+      # default 16-wave steps, same tree and box.
+      for i in 1 2; do
+        timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --waves-per-step 1 --no-scenarios --no-placement \
+          --no-service-mode --no-open-loop > "$OUT/bench_r3shape_$i.json" 2> "$OUT/bench_r3shape_$i.err" || exit $?
+      done ;;
     nodes1024) timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
                  --no-service-mode > "$OUT/bench_nodes_1024.json" 2> "$OUT/bench_nodes_1024.err" ;;
     pmc) OUTDIR="$OUT" bash scripts/pmc_round.sh ;;
