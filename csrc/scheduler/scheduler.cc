@@ -119,13 +119,26 @@ void Executor::spawn_locked() {
         // that still saw this spinner finds its task taken here.
         spinners_.fetch_sub(1);
       }
+      bool chain = false;
       {
         std::unique_lock<std::mutex> lk(mu_);
         if (!try_pop(fn)) {
-          cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+          ++waiters_;
+          while (!stop_ && q_.empty()) {
+            cv_.wait(lk);
+            if (wakes_ > 0) --wakes_;  // every wake-up consumes one, taken task or not
+          }
+          --waiters_;
           if (!try_pop(fn)) return;  // stop_ and drained
         }
+        // Chain wake-up: a burst submitted at once (a gang's Allows) costs
+        // the submitter one futex wake; each woken worker wakes the next.
+        if (!q_.empty() && waiters_ > 0 && wakes_ == 0 && queued_.load(std::memory_order_relaxed) > spinners_.load()) {
+          ++wakes_;
+          chain = true;
+        }
       }
+      if (chain) cv_.notify_one();
       fn();
       busy_.fetch_sub(1);
       spin = true;
@@ -155,14 +168,19 @@ size_t Executor::threads() const {
 Executor::~Executor() { stop(); }
 
 void Executor::submit(std::function<void()> fn) {
+  bool wake = false;
   {
     std::lock_guard<std::mutex> g(mu_);
     q_.push_back(std::move(fn));
     queued_.fetch_add(1, std::memory_order_relaxed);
+    // Wake a sleeper unless a spinning worker is free for this task or a
+    // wake-up is already on its way (that worker wakes the next one).
+    if (waiters_ > 0 && wakes_ == 0 && queued_.load(std::memory_order_relaxed) > spinners_.load()) {
+      ++wakes_;
+      wake = true;
+    }
   }
-  // Wake a sleeper unless a spinning worker is free for this task (a burst of
-  // k Allows from one gang still fans out over k workers).
-  if (queued_.load() > spinners_.load()) cv_.notify_one();
+  if (wake) cv_.notify_one();
 }
 
 void Executor::stop() {
@@ -973,7 +991,7 @@ void Scheduler::release_retired() {
   if (snapshot_.retired.size() >= 32) {
     auto batch = std::make_shared<std::vector<NodeInfoPtr>>(std::move(snapshot_.retired));
     snapshot_.retired.clear();
-    snapshot_.retired.reserve(64);  // not regrown from empty push by push
+    snapshot_.retired.reserve(snapshot_.nodes.size());  // a drain retires every node at once: no regrowth
     binder_->submit([batch] { batch->clear(); });
   }
   if (snapshot_.retired_deltas.size() >= 256) {

@@ -100,6 +100,8 @@ class Executor {
   std::atomic<int> busy_{0};
   std::atomic<int> queued_{0};
   std::atomic<int> spinners_{0};
+  int waiters_ = 0;  // workers in cv_.wait (under mu_)
+  int wakes_ = 0;    // notifications sent and not yet consumed by a waking worker (under mu_)
 };
 
 struct SchedulerOptions {

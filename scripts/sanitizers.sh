@@ -2,7 +2,7 @@
 # Host-only sanitizer runs of the native stress driver (no GPU code):
 # ThreadSanitizer and AddressSanitizer+UBSan builds over the bench waves and
 # the scheduler_perf shapes that exercise preemption, topology spreading and
-# inter-pod affinity. Usage: bash scripts/sanitizers_r3.sh OUTFILE
+# inter-pod affinity. Usage: bash scripts/sanitizers.sh OUTFILE
 set -u
 cd "$(dirname "$0")/.."
 out=${1:-profiles/r3_sanitizers.txt}
@@ -23,6 +23,10 @@ run() {  # name dir waves
   done
 }
 run bench64 /tmp/san_bench 3
+# The 1,024-node headline waves: gang window, Filter scan memo, column
+# equivalence table, snapshot arrays (one wave of 12k pods).
+python -m flex_gpu_scheduler_amd.tools.stress /tmp/san_1024 --nodes 1024 > /dev/null || exit 1
+run n1024 /tmp/san_1024 1
 run apiserver apiserver 4   # native HTTP API server: 4 REST clients, 2 watch streams, mirror, stop
 # Open-loop arrivals: gangs created and deleted one by one while they are
 # scheduled (run_open_loop, batched gang deletion, gang-record cleanup).
