@@ -307,13 +307,14 @@ void Pod::recompute_gpu_assignment(const GpuNames& gn) {
   std::vector<int> gpus = parse_int_list(*idx);
   if (gpus.empty()) return;  // unparsable annotation: skipped (gpu_node.go:91-96)
   int gid = gn.gpu_id(), mid = gn.memory_id(), xid = gn.xcd_id();
-  if (limit_sum.has(gid) && limit_sum.get(gid) > 0) {
+  const Res& limits = limit_sum();
+  if (limits.has(gid) && limits.get(gid) > 0) {
     gpu.kind = GpuAssignment::Kind::WholeGpu;
-  } else if (limit_sum.has(xid) && limit_sum.get(xid) > 0) {
+  } else if (limits.has(xid) && limits.get(xid) > 0) {
     gpu.kind = GpuAssignment::Kind::Partition;
-  } else if (limit_sum.has(mid)) {
+  } else if (limits.has(mid)) {
     gpu.kind = GpuAssignment::Kind::Memory;
-    gpu.memory = limit_sum.get(mid);
+    gpu.memory = limits.get(mid);
   } else {
     return;
   }
@@ -379,7 +380,8 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj, const GpuNames& gn) {
     p->init_containers = std::move(ics);
   }
   p->volumes = parse_pod_volumes(spec, p->meta.name);
-  p->overhead = Res::from_json(spec["overhead"]);
+  auto res = std::make_shared<PodRes>();
+  res->overhead = Res::from_json(spec["overhead"]);
   p->node_selector = strmap_from_json(spec["nodeSelector"]);
   if (const Json* na = spec.path({"affinity", "nodeAffinity"})) {
     if (const Json* req = na->get("requiredDuringSchedulingIgnoredDuringExecution")) {
@@ -425,28 +427,29 @@ std::shared_ptr<Pod> Pod::from_json(const Json& obj, const GpuNames& gn) {
   Res sum;
   for (const auto& c : p->containers) {
     sum += c.requests;
-    p->limit_sum += c.limits;
+    res->limit_sum += c.limits;
     Res nz;
     nz.set(kCPU, c.requests.has(kCPU) && c.requests.get(kCPU) != 0 ? c.requests.get(kCPU) : kDefaultMilliCPU);
     nz.set(kMemory, c.requests.has(kMemory) && c.requests.get(kMemory) != 0 ? c.requests.get(kMemory) : kDefaultMemory);
-    p->nonzero_request += nz;
+    res->nonzero_request += nz;
     for (const auto& port : c.ports)
       if (port.host_port > 0) p->host_ports.push_back(port);
   }
   if (p->containers.empty()) {
-    p->nonzero_request.set(kCPU, 0);
-    p->nonzero_request.set(kMemory, 0);
+    res->nonzero_request.set(kCPU, 0);
+    res->nonzero_request.set(kMemory, 0);
   }
   for (const auto& c : p->init_containers) {
     sum.set_max(c.requests);
     Res nz;
     nz.set(kCPU, c.requests.has(kCPU) && c.requests.get(kCPU) != 0 ? c.requests.get(kCPU) : kDefaultMilliCPU);
     nz.set(kMemory, c.requests.has(kMemory) && c.requests.get(kMemory) != 0 ? c.requests.get(kMemory) : kDefaultMemory);
-    p->nonzero_request.set_max(nz);
+    res->nonzero_request.set_max(nz);
   }
-  sum += p->overhead;
-  p->nonzero_request += p->overhead;
-  p->request = sum;
+  sum += res->overhead;
+  res->nonzero_request += res->overhead;
+  res->request = sum;
+  p->res = std::move(res);
   p->qos = compute_qos(*p);
   if (const std::string* pg = p->meta.label(kPodGroupLabel)) {
     p->pod_group = *pg;
@@ -685,13 +688,13 @@ GpuDemand compute_gpu_demand(const Pod& p, const GpuNames& gn) {
   }
   if (has_g) {
     d.kind = GpuDemand::Gpu;
-    d.amount = p.limit_sum.get(gid);
+    d.amount = p.limit_sum().get(gid);
   } else if (has_x) {
     d.kind = GpuDemand::Xcd;
-    d.amount = p.limit_sum.get(xid);
+    d.amount = p.limit_sum().get(xid);
   } else {
     d.kind = GpuDemand::Memory;
-    d.amount = p.limit_sum.get(mid);
+    d.amount = p.limit_sum().get(mid);
   }
   return d;
 }

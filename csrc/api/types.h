@@ -258,6 +258,20 @@ struct RelaxedI64 {
 struct GpuNames;
 const GpuNames& default_gpu_names();
 
+// What a Pod asks for, derived once at parse time. Immutable and shared by
+// the copies of a Pod (the scheduler copies a Pod per assume and per bind
+// confirmation; four Res vectors are 1.5 KB of the object).
+struct PodRes {
+  Res request;          // computePodResourceRequest: max(sum(containers), each init) + overhead
+  Res nonzero_request;  // cpu/memory with scheduler defaults for zero requests
+  Res limit_sum;        // Σ container limits (FlexGPU accounting uses limits)
+  Res overhead;         // spec.overhead
+  static const std::shared_ptr<const PodRes>& empty() {
+    static const std::shared_ptr<const PodRes> e = std::make_shared<const PodRes>();
+    return e;
+  }
+};
+
 struct Pod {
   ObjectMeta meta;
   IStr scheduler_name = kDefaultSchedulerName;
@@ -266,7 +280,6 @@ struct Pod {
   int32_t priority = 0;
   SharedVec<Container> containers, init_containers;
   SharedVec<PodVolume> volumes;  // PVC / ephemeral / in-tree disk volumes (others are not parsed)
-  Res overhead;
   StrMap node_selector;
   std::vector<NodeSelectorTerm> required_node_terms;  // OR of terms
   bool has_required_node_affinity = false;
@@ -291,9 +304,13 @@ struct Pod {
   mutable ListedMark listed;
 
   // ---- derived at parse time ----
-  Res request;          // computePodResourceRequest: max(sum(containers), each init) + overhead
-  Res nonzero_request;  // cpu/memory with scheduler defaults for zero requests
-  Res limit_sum;        // Σ container limits (FlexGPU accounting uses limits)
+  // The resource vectors derived from the spec (PodRes), one immutable block
+  // shared by every copy of the Pod.
+  std::shared_ptr<const PodRes> res = PodRes::empty();
+  const Res& request() const { return res->request; }
+  const Res& nonzero_request() const { return res->nonzero_request; }
+  const Res& limit_sum() const { return res->limit_sum; }
+  const Res& overhead() const { return res->overhead; }
   QoS qos = QoS::BestEffort;
   std::string pod_group;  // value of kPodGroupLabel ("" if none)
   uint64_t pg_key = 0;    // pg_key_of("ns/pod_group"), 0 if no group

@@ -252,8 +252,8 @@ void NodeInfo::add_pod(const PodPtr& p) {
   pods.push_back(p);
   if (has_affinity(*p)) pods_with_affinity.push_back(p);
   if (!p->pod_anti_affinity_required.empty()) pods_with_required_anti_affinity.push_back(p);
-  requested += p->request;
-  nonzero_requested += p->nonzero_request;
+  requested += p->request();
+  nonzero_requested += p->nonzero_request();
   for (const auto& port : p->host_ports) used_ports.emplace(port.host_ip, port.protocol, port.host_port);
   gpu.apply(p->gpu, +1);
   if (p->pg_key) {
@@ -290,8 +290,8 @@ bool NodeInfo::remove_pod(const std::string& uid) {
   erase_from(pods);
   erase_from(pods_with_affinity);
   erase_from(pods_with_required_anti_affinity);
-  requested -= victim->request;
-  nonzero_requested -= victim->nonzero_request;
+  requested -= victim->request();
+  nonzero_requested -= victim->nonzero_request();
   for (const auto& port : victim->host_ports) used_ports.erase({port.host_ip, port.protocol, port.host_port});
   gpu.apply(victim->gpu, -1);
   if (victim->pg_key) {

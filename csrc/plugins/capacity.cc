@@ -63,13 +63,13 @@ struct EQInfo {
   std::shared_ptr<const Quota> published;
   bool add_pod(const Pod& p) {
     if (!pods.insert(p.key()).second) return false;
-    used += p.request;
+    used += p.request();
     published.reset();
     return true;
   }
   bool delete_pod(const Pod& p) {
     if (!pods.erase(p.key())) return false;
-    used -= p.request;
+    used -= p.request();
     published.reset();
     return true;
   }
@@ -119,11 +119,11 @@ struct EQSnapshot : StateData {
     if (!has(p.ns()) || p.phase == "Succeeded" || p.phase == "Failed") return;
     Res& d = delta[p.ns()];
     if (sign > 0) {
-      d += p.request;
-      delta_sum += p.request;
+      d += p.request();
+      delta_sum += p.request();
     } else {
-      d -= p.request;
-      delta_sum -= p.request;
+      d -= p.request();
+      delta_sum -= p.request();
     }
   }
 };
@@ -244,7 +244,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     }
     s.write(kSnapKey, snap);
     auto pfs = std::make_shared<CSPreFilterState>();
-    pfs->pod_req = pod.request;
+    pfs->pod_req = pod.request();
     const Quota* own = snap->find(pod.ns());
     if (!own) {
       s.write(kStateKey, pfs);
@@ -259,15 +259,15 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
         const Quota* q = snap->find(np->ns());
         if (!q) return;
         if (np->ns() == pod.ns() && np->priority >= pod.priority) {
-          in_eq += np->request;
-          global += np->request;
+          in_eq += np->request();
+          global += np->request();
         } else if (np->ns() != pod.ns() && !q->used_over_min()) {
-          global += np->request;
+          global += np->request();
         }
       });
     }
-    in_eq += pod.request;
-    global += pod.request;
+    in_eq += pod.request();
+    global += pod.request();
     pfs->nominated_in_eq_with_req = in_eq;
     pfs->nominated_with_req = global;
     s.write(kStateKey, pfs);

@@ -162,7 +162,7 @@ class Coscheduling : public Plugin {
       int64_t pods = ni->num_pods();
       for (const auto& q : ni->pods)
         if (q->pg_key == member.pg_key && q->pod_group == member.pod_group && q->ns() == member.ns()) {
-          requested -= q->request;
+          requested -= q->request();
           --pods;
         }
       left.set(kPods, ni->allocatable.get(kPods) - pods);

@@ -128,7 +128,7 @@ class NodeResourcesFit : public Plugin {
     // pods") and their Status is built once per distinct mask per thread.
     uint64_t fail = 0;
     if (ni.num_pods() + 1 > ni.allocatable.get(kPods) && ni.allocatable.has(kPods)) fail |= 1ull << kPods;
-    const Res& req = p.request;
+    const Res& req = p.request();
     for (uint64_t m = req.mask; m; m &= m - 1) {
       int i = __builtin_ctzll(m);
       if (i == kPods) continue;
@@ -161,8 +161,8 @@ class NodeResourcesFit : public Plugin {
     int64_t num = 0, den = 0;
     for (const auto& w : weights_) {
       int64_t alloc = ni.allocatable.get(w.id);
-      int64_t req = (w.id == kCPU || w.id == kMemory) ? ni.nonzero_requested.get(w.id) + p.nonzero_request.get(w.id)
-                                                       : ni.requested.get(w.id) + p.request.get(w.id);
+      int64_t req = (w.id == kCPU || w.id == kMemory) ? ni.nonzero_requested.get(w.id) + p.nonzero_request().get(w.id)
+                                                       : ni.requested.get(w.id) + p.request().get(w.id);
       int64_t s = 0;
       if (strategy_ == "MostAllocated") {
         s = (alloc == 0 || req > alloc) ? 0 : req * kMaxNodeScore / alloc;
@@ -217,8 +217,8 @@ class BalancedAllocation : public Plugin {
     for (const auto& w : weights_) {
       int64_t alloc = ni.allocatable.get(w.id);
       if (alloc == 0) continue;
-      int64_t req = (w.id == kCPU || w.id == kMemory) ? ni.nonzero_requested.get(w.id) + p.nonzero_request.get(w.id)
-                                                       : ni.requested.get(w.id) + p.request.get(w.id);
+      int64_t req = (w.id == kCPU || w.id == kMemory) ? ni.nonzero_requested.get(w.id) + p.nonzero_request().get(w.id)
+                                                       : ni.requested.get(w.id) + p.request().get(w.id);
       double f = static_cast<double>(req) / static_cast<double>(alloc);
       if (f >= 1) return {0, {}};  // over-committed
       if (n < static_cast<size_t>(kMaxRes)) fr[n++] = f;

@@ -224,7 +224,7 @@ class TopologyMatch : public Plugin {
         continue;
       }
       if (pol == "SingleNUMANodePodLevel") {
-        if (!fits_fast(*nrt, ni, p.request, p.qos)) {
+        if (!fits_fast(*nrt, ni, p.request(), p.qos)) {
           thread_local std::string memo_uid;
           thread_local Status memo;
           if (memo_uid != p.uid()) {
@@ -382,7 +382,7 @@ class TopologyMatch : public Plugin {
     for (const auto& pol : nrt->topology_policies) {
       if (pol != "SingleNUMANodePodLevel" && pol != "SingleNUMANodeContainerLevel") continue;
       auto nodes = numa_list(*nrt, ni);
-      if (pol == "SingleNUMANodePodLevel") return {min_numa_score(p.request, nodes), {}};
+      if (pol == "SingleNUMANodePodLevel") return {min_numa_score(p.request(), nodes), {}};
       double sum = 0;
       size_t n = 0;
       for (const auto& c : p.init_containers) {

@@ -255,7 +255,7 @@ class TargetLoadPacking : public TrimaranBase {
   int64_t pod_usage(const Pod& p) const {
     int64_t u = 0;
     for (const auto& c : p.containers) u += predict(c);
-    if (!gpu_mode_) u += p.overhead.get(kCPU);
+    if (!gpu_mode_) u += p.overhead().get(kCPU);
     return u;
   }
 
@@ -353,8 +353,8 @@ class LoadVariationRiskBalancing : public TrimaranBase {
       req_cpu = std::max(req_cpu, c.requests.get(kCPU));
       req_mem = std::max(req_mem, c.requests.get(kMemory));
     }
-    req_cpu += p.overhead.get(kCPU);
-    req_mem += p.overhead.get(kMemory);
+    req_cpu += p.overhead().get(kCPU);
+    req_mem += p.overhead().get(kMemory);
     constexpr int kDims = 5;  // cpu, memory, GPU busy, HBM bandwidth, xGMI
     double scores[kDims];
     bool valid[kDims] = {false, false, false, false, false};
@@ -385,13 +385,13 @@ class LoadVariationRiskBalancing : public TrimaranBase {
       if (!resource_data(it->second, type, &avg, &sd)) return;
       ResourceStats rs;
       rs.capacity = static_cast<double>(ni.node->allocatable.get(gid));
-      rs.req = static_cast<double>(p.limit_sum.get(gid));
+      rs.req = static_cast<double>(p.limit_sum().get(gid));
       rs.used_avg = avg * rs.capacity / 100;
       rs.used_std = sd * rs.capacity / 100;
       scores[slot] = rs.score(margin_, sensitivity_);
       valid[slot] = true;
     };
-    if (p.limit_sum.get(gid) > 0) {
+    if (p.limit_sum().get(gid) > 0) {
       gpu_dim(kTGPU, 2);
       gpu_dim(kTGPUMemoryBandwidth, 3);
       if (!p.pod_group.empty()) gpu_dim(kTXGMI, 4);

@@ -117,9 +117,9 @@ py::dict pod_struct_summary(const Pod& pod) {
   const Pod* p = &pod;
   py::dict d;
   d["key"] = p->key();
-  d["request"] = to_py(p->request.to_json());
-  d["nonzero_request"] = to_py(p->nonzero_request.to_json());
-  d["limits"] = to_py(p->limit_sum.to_json());
+  d["request"] = to_py(p->request().to_json());
+  d["nonzero_request"] = to_py(p->nonzero_request().to_json());
+  d["limits"] = to_py(p->limit_sum().to_json());
   const char* q[] = {"BestEffort", "Burstable", "Guaranteed"};
   d["qos"] = q[static_cast<int>(p->qos)];
   d["pod_group"] = p->pod_group;

@@ -314,7 +314,7 @@ QueuedPodInfoPtr SchedulingQueue::pop(int timeout_ms) {
 namespace {
 bool pod_spec_changed(const Pod& a, const Pod& b) {
   // isPodUpdated: ignore status/resourceVersion-only changes.
-  return !(a.request == b.request && a.meta.labels == b.meta.labels && a.meta.annotations == b.meta.annotations &&
+  return !(a.request() == b.request() && a.meta.labels == b.meta.labels && a.meta.annotations == b.meta.annotations &&
            a.node_selector == b.node_selector && a.priority == b.priority && a.tolerations.size() == b.tolerations.size());
 }
 }  // namespace
