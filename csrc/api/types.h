@@ -302,6 +302,15 @@ struct Pod {
     ListedMark& operator=(const ListedMark&) { return *this; }
   };
   mutable ListedMark listed;
+  // Which PodHeap holds exactly this object (PodHeap::tag; 0: none). Read and
+  // written under the SchedulingQueue's lock only; not copied.
+  struct HeapTag {
+    uint8_t v = 0;
+    HeapTag() = default;
+    HeapTag(const HeapTag&) {}
+    HeapTag& operator=(const HeapTag&) { return *this; }
+  };
+  mutable HeapTag heap_tag;
 
   // ---- derived at parse time ----
   // The resource vectors derived from the spec (PodRes), one immutable block

@@ -37,7 +37,9 @@ void PodHeap::push(const QueuedPodInfoPtr& p) {
   auto it = pos_.find(p->pod->uid());
   if (it != pos_.end()) {
     size_t i = it->second->heap_index;
+    if (tag_) v_[i]->pod->heap_tag.v = 0;
     v_[i] = p;
+    if (tag_) p->pod->heap_tag.v = tag_;
     p->heap_index = i;
     it->second = p.get();
     up(i);
@@ -45,6 +47,7 @@ void PodHeap::push(const QueuedPodInfoPtr& p) {
     return;
   }
   v_.push_back(p);
+  if (tag_) p->pod->heap_tag.v = tag_;
   p->heap_index = v_.size() - 1;
   pos_.emplace(p->pod->uid(), p.get());
   up(v_.size() - 1);
@@ -53,6 +56,7 @@ void PodHeap::push(const QueuedPodInfoPtr& p) {
 QueuedPodInfoPtr PodHeap::pop() {
   if (v_.empty()) return nullptr;
   QueuedPodInfoPtr top = v_.front();
+  if (tag_) top->pod->heap_tag.v = 0;
   swap_at(0, v_.size() - 1);
   v_.pop_back();
   pos_.erase(top->pod->uid());
@@ -69,6 +73,7 @@ bool PodHeap::erase(const std::string& uid) {
   auto it = pos_.find(uid);
   if (it == pos_.end()) return false;
   size_t i = it->second->heap_index;
+  if (tag_) v_[i]->pod->heap_tag.v = 0;
   size_t last = v_.size() - 1;
   if (i != last) swap_at(i, last);
   v_.pop_back();
@@ -180,7 +185,7 @@ SchedulingQueue::SchedulingQueue(PodHeap::Less less, std::shared_ptr<Clock> cloc
     : clock_(std::move(clock)),
       opts_(opts),
       nominator_(nominator),
-      active_(std::move(less)),
+      active_(std::move(less), /*tag=*/1),
       backoff_([this](const QueuedPodInfo& a, const QueuedPodInfo& b) { return backoff_expiry(a) < backoff_expiry(b); }) {}
 
 void SchedulingQueue::set_cluster_event_map(std::vector<std::pair<ClusterEvent, std::set<std::string>>> m) {
@@ -231,6 +236,7 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
   {
     std::lock_guard<std::mutex> g(mu_);
     for (const auto& pod : pods) {
+      if (active_.holds(*pod)) continue;  // already active: no uid lookups
       const std::string& uid = pod->uid();
       if (active_.contains(uid)) continue;
       QueuedPodInfoPtr q;

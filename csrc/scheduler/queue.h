@@ -27,7 +27,10 @@ namespace xsched {
 class PodHeap {
  public:
   using Less = std::function<bool(const QueuedPodInfo&, const QueuedPodInfo&)>;
-  explicit PodHeap(Less less) : less_(std::move(less)) {}
+  // `tag` (non-zero) is written into Pod::heap_tag of the objects this heap
+  // holds, so a caller holding the same object can test membership without
+  // a uid lookup (holds()).
+  explicit PodHeap(Less less, uint8_t tag = 0) : less_(std::move(less)), tag_(tag) {}
   void set_less(Less l) { less_ = std::move(l); }
   void push(const QueuedPodInfoPtr& p);  // add or update
   QueuedPodInfoPtr pop();
@@ -35,6 +38,9 @@ class PodHeap {
   QueuedPodInfoPtr get(const std::string& uid) const;
   bool erase(const std::string& uid);
   bool contains(const std::string& uid) const { return pos_.count(uid) > 0; }
+  // True when this very Pod object is in the heap (false does not rule out
+  // another object of the same pod: use contains() for that).
+  bool holds(const Pod& p) const { return tag_ != 0 && p.heap_tag.v == tag_; }
   size_t size() const { return v_.size(); }
   bool empty() const { return v_.empty(); }
   std::vector<QueuedPodInfoPtr> items() const { return v_; }
@@ -44,6 +50,7 @@ class PodHeap {
   void down(size_t i);
   void swap_at(size_t a, size_t b);
   Less less_;
+  uint8_t tag_ = 0;
   std::vector<QueuedPodInfoPtr> v_;
   std::unordered_map<std::string, QueuedPodInfo*> pos_;  // uid -> entry (index lives in the entry)
 };
