@@ -532,34 +532,54 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
       const int64_t* sgen = table->score_gen.data();
       const uint64_t* pm = table->plain_mask.data();
       const uint64_t* cm = table->cols.data();
+      // Branch-free: hits and misses interleave unpredictably.
+      miss.resize(n);
+      size_t nm = 0;
       for (size_t i = 0; i < n; ++i) {
         const size_t pos = static_cast<size_t>(tpos[i]);
         const int64_t gen = have_gens ? eq->gen[pos] : nodes[i]->generation;
-        const bool h = sgen[pos] == gen && pm[pos] == plain_mask && (cm[pos] & row_mask) == row_mask;
+        const bool h = (sgen[pos] == gen) & (pm[pos] == plain_mask) & ((cm[pos] & row_mask) == row_mask);
         hit[i] = h;
-        if (!h) miss.push_back(static_cast<uint32_t>(i));
+        miss[nm] = static_cast<uint32_t>(i);
+        nm += !h;
       }
-      any_hit = miss.size() < n;
+      miss.resize(nm);
+      any_hit = nm < n;
     }
-    // Hits: plain sums and row columns; skipped and plain scorers' rows are
-    // never read, so they are not filled.
+    // Hits: plain sums and row columns, copied for every node (a miss's
+    // cells are overwritten below); skipped and plain scorers' rows are never
+    // read, so they are not filled.
     if (any_hit) {
-      if (plain_mask)
-        for (size_t i = 0; i < n; ++i)
-          if (hit[i]) plain_tot[i] = table->plain_sum[tpos[i]];
+      if (plain_mask) {
+        const int64_t* ps = table->plain_sum.data();
+        for (size_t i = 0; i < n; ++i) plain_tot[i] = ps[tpos[i]];
+      }
       for (size_t k = 0; k < ns; ++k) {  // column by column
         if (!((row_mask >> k) & 1)) continue;
         const int64_t* col = &table->raw[k * table->n];
-        for (size_t i = 0; i < n; ++i)
-          if (hit[i]) per[k][i].score = col[tpos[i]];
+        NodeScore* row = per[k].data();
+        for (size_t i = 0; i < n; ++i) row[i].score = col[tpos[i]];
       }
     }
     for (size_t k = 0; k < ns; ++k) {
       std::vector<NodeScore>& row = per[k];
       if (skip[k]) continue;
       const bool reuse = any_hit && eq->local[k];
-      Status st = scorers_[k].first->score_many(s, p, nodes, reuse ? hit.data() : nullptr, row,
-                                                (eq && eq->npos == n) ? eq->pos : nullptr);
+      Status st;
+      if (reuse && miss.size() * 4 < n) {
+        // Few misses: score just those (no pass over the hits).
+        for (uint32_t i : miss) {
+          auto [sc, one] = scorers_[k].first->score(s, p, *nodes[i]);
+          if (!one.is_success()) {
+            st = one;
+            break;
+          }
+          row[i].score = sc;
+        }
+      } else {
+        st = scorers_[k].first->score_many(s, p, nodes, reuse ? hit.data() : nullptr, row,
+                                           (eq && eq->npos == n) ? eq->pos : nullptr);
+      }
       if (!st.is_success()) {
         err = "running Score plugin " + scorers_[k].first->name() + ": " + st.message();
         failed.store(true);

@@ -3,6 +3,7 @@
 #include "common/log.h"
 
 #include <algorithm>
+#include <cstring>
 #include <chrono>
 #include <thread>
 #include <map>
@@ -989,10 +990,23 @@ void Scheduler::run_bind_task(BindTask* t) {
 
 void Scheduler::release_retired() {
   if (snapshot_.retired.size() >= 32) {
+    // The batch is released on a binder thread; its emptied vector comes back
+    // through retired_spare_ with its capacity (no allocation per batch).
     auto batch = std::make_shared<std::vector<NodeInfoPtr>>(std::move(snapshot_.retired));
     snapshot_.retired.clear();
-    snapshot_.retired.reserve(snapshot_.nodes.size());  // a drain retires every node at once: no regrowth
-    binder_->submit([batch] { batch->clear(); });
+    {
+      std::lock_guard<std::mutex> g(retired_spare_mu_);
+      if (!retired_spare_.empty()) {
+        snapshot_.retired.swap(retired_spare_.back());
+        retired_spare_.pop_back();
+      }
+    }
+    if (snapshot_.retired.capacity() < 64) snapshot_.retired.reserve(64);
+    binder_->submit([this, batch] {
+      batch->clear();
+      std::lock_guard<std::mutex> g(retired_spare_mu_);
+      if (retired_spare_.size() < 8) retired_spare_.push_back(std::move(*batch));
+    });
   }
   if (snapshot_.retired_deltas.size() >= 256) {
     auto batch = std::make_shared<std::vector<PodDelta>>(std::move(snapshot_.retired_deltas));
@@ -1175,8 +1189,8 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
   bool has_err = false;
   int c = 0, processed = 0;
   uint64_t hits = 0;
-  if (static_cast<int>(found_buf_.size()) < to_find) found_buf_.resize(to_find);
-  if (static_cast<int>(found_pos_buf_.size()) < to_find) found_pos_buf_.resize(to_find);
+  if (static_cast<int>(found_buf_.size()) < to_find + 1) found_buf_.resize(to_find + 1);
+  if (static_cast<int>(found_pos_buf_.size()) < to_find + 1) found_pos_buf_.resize(to_find + 1);
   // One node's verdict: from the equivalence cache when it is valid for the
   // node's version (and, on a node with nominated pods, for the same set of
   // nominated pods), else computed into `own` or the cache slot.
@@ -1229,24 +1243,37 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     int reevaluated = 0;
     const int m = memo->processed;
     auto at = [&](int off) { return start + off >= n ? start + off - n : start + off; };
-    for (int off = 0; off < m && ok; ++off) {
-      const int pos = at(off);
-      if (memo->gens[off] == snapshot_.gen[pos]) continue;
-      bool hit = false;
-      const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
-      ++reevaluated;
-      ok = fp->is_success() || fp->is_unschedulable();
-      memo->ok[off] = fp->is_success();
-      memo->gens[off] = snapshot_.gen[pos];
-    }
-    int off = 0;
-    for (; ok && off < m && c < to_find; ++off)
-      if (memo->ok[off]) {
-        const int pos = at(off);
-        found_buf_[c] = all[pos].get();
-        found_pos_buf_[c] = pos;
-        ++c;
+    // The window is at most two contiguous runs of positions; each is checked
+    // in blocks with memcmp, and only a block that differs element-wise.
+    const int64_t* mg = memo->gens.data();
+    const int64_t* sg = snapshot_.gen.data();
+    constexpr int kBlock = 32;
+    for (int off0 = 0; off0 < m && ok;) {
+      const int pos0 = at(off0);
+      const int run = std::min({m - off0, n - pos0, kBlock});
+      if (std::memcmp(mg + off0, sg + pos0, static_cast<size_t>(run) * sizeof(int64_t)) != 0) {
+        for (int j = 0; j < run && ok; ++j) {
+          const int off = off0 + j, pos = pos0 + j;
+          if (mg[off] == sg[pos]) continue;
+          bool hit = false;
+          const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
+          ++reevaluated;
+          ok = fp->is_success() || fp->is_unschedulable();
+          memo->ok[off] = fp->is_success();
+          memo->gens[off] = sg[pos];
+        }
       }
+      off0 += run;
+    }
+    // Re-cut the list: branch-free appends (the buffers hold to_find + 1).
+    int off = 0;
+    const char* okv = memo->ok.data();
+    for (; ok && off < m && c < to_find; ++off) {
+      const int pos = at(off);
+      found_buf_[c] = all[pos].get();
+      found_pos_buf_[c] = pos;
+      c += okv[off] != 0;
+    }
     for (; ok && c < to_find && off < n; ++off) {  // the scan has to reach further now
       const int pos = at(off);
       bool hit = false;

@@ -250,6 +250,8 @@ class Scheduler {
   };
   EqEntry* eq_entry(Framework& fw, const Pod& p);
   void release_retired();
+  std::mutex retired_spare_mu_;
+  std::vector<std::vector<NodeInfoPtr>> retired_spare_;  // emptied retired batches, capacity kept
   std::vector<Status> fail_buf_;  // find_nodes_that_fit scratch (scheduling thread)
   std::vector<char> nom_mark_;    // nodes with nominated pods, per snapshot position (refresh_nom_mark)
   std::vector<const std::vector<PodPtr>*> nom_list_;  // ... and their lists in the view (valid for the cycle)
