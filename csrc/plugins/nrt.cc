@@ -339,6 +339,22 @@ class TopologyMatch : public Plugin {
     if (co) return 50;
     return 40 * std::min(free, remaining) / remaining;  // most of the gang on one node
   }
+  // fit_score for one gang demand over a cycle's nodes: the few distinct
+  // (free, co-located) pairs are computed once each (no division per node).
+  struct FitMemo {
+    int64_t remaining = -1;
+    int64_t v[2][65];
+    int64_t get(int64_t r, int64_t free, bool co) {
+      if (free < 0 || free > 64) return fit_score(r, free, co);
+      if (r != remaining) {
+        remaining = r;
+        std::fill(&v[0][0], &v[0][0] + 2 * 65, int64_t{-1});
+      }
+      int64_t& slot = v[co][free];
+      if (slot < 0) slot = fit_score(r, free, co);
+      return slot;
+    }
+  };
   // gang_score for a whole-GPU rank given the node's free GPUs.
   static int64_t whole_gang_score(const GangCtx& c, int64_t free_gpus, const NodeInfo& ni) {
     if (free_gpus <= 0) return 0;
@@ -407,8 +423,13 @@ class TopologyMatch : public Plugin {
     if (pos && snap && c->gang && c->kind == GangCtx::kWhole && snap->free_whole.size() == snap->nodes.size()) {
       // Whole-GPU ranks: free GPUs from the snapshot's contiguous array; only
       // the few nodes already hosting the gang are dereferenced.
-      for (size_t i = 0; i < nodes.size(); ++i)
-        if (!skip || !skip[i]) out[i].score = whole_gang_score(*c, snap->free_whole[pos[i]], *nodes[i]);
+      FitMemo fm;
+      const int64_t r = c->remaining * c->amount;
+      for (size_t i = 0; i < nodes.size(); ++i) {
+        if (skip && skip[i]) continue;
+        const int64_t free = snap->free_whole[pos[i]];
+        out[i].score = free <= 0 ? 0 : fm.get(r, free, co_located(*c, *nodes[i]));
+      }
       return {};
     }
     if (pos && snap && c->gang && c->kind == GangCtx::kXcd && snap->part_mask.size() == snap->nodes.size()) {
@@ -426,11 +447,12 @@ class TopologyMatch : public Plugin {
         }
         per_of[m] = per;
       }
+      FitMemo fm;
       for (size_t i = 0; i < nodes.size(); ++i) {
         if (skip && skip[i]) continue;
         const int64_t per = per_of[snap->part_mask[pos[i]]];
         const int64_t free = snap->free_xcd[pos[i]];
-        out[i].score = per == 0 || free <= 0 ? 0 : fit_score(c->remaining * per, free, co_located(*c, *nodes[i]));
+        out[i].score = per == 0 || free <= 0 ? 0 : fm.get(c->remaining * per, free, co_located(*c, *nodes[i]));
       }
       return {};
     }
