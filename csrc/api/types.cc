@@ -306,6 +306,27 @@ void Pod::recompute_gpu_assignment(const GpuNames& gn) {
   if (!idx) return;
   std::vector<int> gpus = parse_int_list(*idx);
   if (gpus.empty()) return;  // unparsable annotation: skipped (gpu_node.go:91-96)
+  std::vector<std::pair<int, int>> parts;
+  if (const std::string* ps = meta.annotation(gn.partition_annotation)) {
+    size_t i = 0;
+    const std::string& s = *ps;
+    while (i < s.size()) {
+      size_t j = s.find(',', i);
+      if (j == std::string::npos) j = s.size();
+      std::string tok = s.substr(i, j - i);
+      size_t c = tok.find(':');
+      if (c != std::string::npos) {
+        parts.emplace_back(std::atoi(tok.substr(0, c).c_str()), std::atoi(tok.substr(c + 1).c_str()));
+      }
+      i = j + 1;
+    }
+  }
+  set_gpu_assignment(std::move(gpus), std::move(parts), gn);
+}
+
+void Pod::set_gpu_assignment(std::vector<int> gpus, std::vector<std::pair<int, int>> parts, const GpuNames& gn) {
+  gpu = GpuAssignment{};
+  if (gpus.empty()) return;
   int gid = gn.gpu_id(), mid = gn.memory_id(), xid = gn.xcd_id();
   const Res& limits = limit_sum();
   if (limits.has(gid) && limits.get(gid) > 0) {
@@ -319,20 +340,7 @@ void Pod::recompute_gpu_assignment(const GpuNames& gn) {
     return;
   }
   gpu.gpus = std::move(gpus);
-  if (const std::string* parts = meta.annotation(gn.partition_annotation)) {
-    size_t i = 0;
-    const std::string& s = *parts;
-    while (i < s.size()) {
-      size_t j = s.find(',', i);
-      if (j == std::string::npos) j = s.size();
-      std::string tok = s.substr(i, j - i);
-      size_t c = tok.find(':');
-      if (c != std::string::npos) {
-        gpu.partitions.emplace_back(std::atoi(tok.substr(0, c).c_str()), std::atoi(tok.substr(c + 1).c_str()));
-      }
-      i = j + 1;
-    }
-  }
+  gpu.partitions = std::move(parts);
 }
 
 const std::string& IStr::intern(std::string_view v) {

@@ -347,6 +347,11 @@ struct Pod {
 
   static std::shared_ptr<Pod> from_json(const Json& obj, const GpuNames& gn = default_gpu_names());
   void recompute_gpu_assignment(const GpuNames& gn = default_gpu_names());
+  // The assignment recompute_gpu_assignment derives from the index and
+  // partition annotations, from already-parsed values (FlexGPU Reserve sets
+  // the annotations and this together).
+  void set_gpu_assignment(std::vector<int> gpus, std::vector<std::pair<int, int>> parts,
+                          const GpuNames& gn = default_gpu_names());
 };
 using PodPtr = std::shared_ptr<Pod>;
 

@@ -300,7 +300,8 @@ class FlexGPU : public Plugin {
           }
         if (!set) am.emplace_back(kv.first, kv.second.as_string());
       }
-    });
+      cp.set_gpu_assignment(pl.gpus, pl.parts, gn);  // what the annotations just written parse to
+    }, /*recompute=*/false);
     s.write(kFlexGPUStateKey, st);
     return {};
   }

@@ -310,7 +310,8 @@ PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<vo
   return fresh;
 }
 
-PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn) {
+PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn,
+                                            bool recompute) {
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = pod_states_.find(uid);
@@ -322,7 +323,7 @@ PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::f
       NodeInfo& ni = writable(nit->second);
       ni.gpu.apply(pod->gpu, -1);
       fn(*pod);
-      pod->recompute_gpu_assignment(*gpu_names_);
+      if (recompute) pod->recompute_gpu_assignment(*gpu_names_);
       ni.gpu.apply(pod->gpu, +1);
       mark_dirty(pod->node_name);
       in_place_ = false;

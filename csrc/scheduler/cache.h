@@ -65,7 +65,9 @@ class SchedulerCache {
   // copy, and since `fn` may only change annotations, only the node's GPU
   // ledger is re-accounted (Pod::recompute_gpu_assignment). Falls back to
   // mutate_pod for pods that are not (or no longer) assumed.
-  PodPtr annotate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn);
+  // `fn` edits the assumed pod's annotations in place; with `recompute` the
+  // GPU assignment is then re-derived from them (false: fn set it).
+  PodPtr annotate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn, bool recompute = true);
 
   // Returns the number of NodeInfo versions refreshed (shared, not cloned:
   // the cache copies on write); replaced versions go to `s.retired`; `lock_wait_us` (optional)

@@ -603,6 +603,26 @@ TEST(default_normalize_matches_integer_division) {
   }
 }
 
+TEST(gpu_assignment_direct_matches_annotations) {
+  // FlexGPU Reserve sets the assignment from its placement; the informer's
+  // copy derives it from the annotations Reserve wrote. Both must agree.
+  const GpuNames& gn = default_gpu_names();
+  const char* limits[] = {R"({"amd.com/gpu":"2"})", R"({"amd.com/gpu-xcd":"2"})", R"({"amd.com/gpu-memory":"3"})"};
+  for (const char* lim : limits) {
+    Json j = Json::parse(std::string(R"({"metadata":{"namespace":"d","name":"p","uid":"u",)") +
+                         R"("annotations":{"amd.com/gpu-index":"1,3,12","amd.com/gpu-partitions":"0:2,3:1,12:7"}},)" +
+                         R"("spec":{"containers":[{"name":"c","resources":{"limits":)" + lim + "}}]}}");
+    auto a = Pod::from_json(j, gn);
+    Pod b = *a;
+    b.set_gpu_assignment({1, 3, 12}, {{0, 2}, {3, 1}, {12, 7}}, gn);
+    CHECK(a->gpu.valid());
+    CHECK(a->gpu.kind == b.gpu.kind);
+    CHECK(a->gpu.gpus == b.gpu.gpus);
+    CHECK(a->gpu.partitions == b.gpu.partitions);
+    CHECK_EQ(a->gpu.memory, b.gpu.memory);
+  }
+}
+
 int main() {
   for (const auto& t : tests()) {
     int before = g_failed;
