@@ -32,6 +32,10 @@ for step in "$@"; do
         timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --waves-per-step 1 --no-scenarios --no-placement \
           --no-service-mode --no-open-loop > "$OUT/bench_r3shape_$i.json" 2> "$OUT/bench_r3shape_$i.err" || exit $?
       done ;;
+    nodes1024_3) for i in 1 2 3; do
+                   timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
+                     --no-service-mode > "$OUT/bench_nodes_1024_$i.json" 2> "$OUT/bench_nodes_1024_$i.err" || exit $?
+                 done ;;
     nodes1024) timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
                  --no-service-mode > "$OUT/bench_nodes_1024.json" 2> "$OUT/bench_nodes_1024.err" ;;
     pmc) OUTDIR="$OUT" bash scripts/pmc_round.sh ;;
