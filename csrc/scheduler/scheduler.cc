@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <optional>
 #include <chrono>
 #include <thread>
 #include <map>
@@ -168,7 +169,34 @@ size_t Executor::threads() const {
 
 Executor::~Executor() { stop(); }
 
+namespace {
+thread_local Executor::Batch* tl_batch = nullptr;
+}  // namespace
+
+Executor::Batch::Batch(Executor& e) : e_(e), prev_(tl_batch) { tl_batch = this; }
+
+Executor::Batch::~Batch() {
+  tl_batch = prev_;
+  if (fns_.empty()) return;
+  bool wake = false;
+  {
+    std::lock_guard<std::mutex> g(e_.mu_);
+    for (auto& fn : fns_) e_.q_.push_back(std::move(fn));
+    e_.queued_.fetch_add(static_cast<int>(fns_.size()), std::memory_order_relaxed);
+    if (e_.waiters_ > 0 && e_.wakes_ == 0 && e_.queued_.load(std::memory_order_relaxed) > e_.spinners_.load()) {
+      ++e_.wakes_;
+      wake = true;
+    }
+  }
+  if (wake) e_.cv_.notify_one();
+}
+
 void Executor::submit(std::function<void()> fn) {
+  for (Batch* b = tl_batch; b; b = b->prev_)
+    if (&b->e_ == this) {
+      b->fns_.push_back(std::move(fn));
+      return;
+    }
   bool wake = false;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -442,8 +470,20 @@ Framework* Scheduler::framework_for(const std::string& scheduler_name) {
 bool Scheduler::responsible_for(const Pod& p) const { return by_name_.count(p.scheduler_name) > 0; }
 
 Scheduler::Stats Scheduler::stats() const {
-  std::lock_guard<std::mutex> g(stats_mu_);
-  return stats_;
+  Stats st;
+  auto rd = [](const std::atomic<uint64_t>& a) { return a.load(std::memory_order_relaxed); };
+  st.attempts = rd(cnt_.attempts);
+  st.scheduled = rd(cnt_.scheduled);
+  st.unschedulable = rd(cnt_.unschedulable);
+  st.errors = rd(cnt_.errors);
+  st.bound = rd(cnt_.bound);
+  st.bind_failures = rd(cnt_.bind_failures);
+  st.preemption_attempts = rd(cnt_.preemption_attempts);
+  st.eq_filter_hits = rd(cnt_.eq_filter_hits);
+  st.eq_filter_misses = rd(cnt_.eq_filter_misses);
+  st.scan_memo_served = rd(cnt_.scan_memo_served);
+  st.scan_memo_mismatches = rd(cnt_.scan_memo_mismatches);
+  return st;
 }
 
 std::vector<GangRecord> Scheduler::gang_records(bool clear) {
@@ -1316,9 +1356,8 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       }
       mismatch = mismatch || vc != c || vp != processed;
     }
-    std::lock_guard<std::mutex> g(stats_mu_);
-    ++stats_.scan_memo_served;
-    stats_.scan_memo_mismatches += mismatch;
+    cnt_.scan_memo_served.fetch_add(1, std::memory_order_relaxed);
+    cnt_.scan_memo_mismatches.fetch_add(mismatch, std::memory_order_relaxed);
   } else if (inline_ok) {
     // Serial path (every cluster below the parallel threshold, and larger
     // ones whose verdicts mostly come from the equivalence cache): plain
@@ -1413,9 +1452,8 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     hits = ahits.load();
   }
   if (eq_filter) {
-    std::lock_guard<std::mutex> g(stats_mu_);
-    stats_.eq_filter_hits += hits;
-    stats_.eq_filter_misses += static_cast<uint64_t>(processed) - hits;
+    cnt_.eq_filter_hits.fetch_add(hits, std::memory_order_relaxed);
+    cnt_.eq_filter_misses.fetch_add(static_cast<uint64_t>(processed) - hits, std::memory_order_relaxed);
   }
   if (has_err) return first_err;
   next_start_node_ = (start + processed) % n;
@@ -1666,8 +1704,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   refresh_nom_mark(state->nominated.get());
   const std::string& profile = fw->profile_name();
   {
-    std::lock_guard<std::mutex> g(stats_mu_);
-    ++stats_.attempts;
+    cnt_.attempts.fetch_add(1, std::memory_order_relaxed);
   }
   int64_t snap_end = clock_->now_us();
   if (tracer_.enabled()) {
@@ -1729,8 +1766,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
       auto [res, pst] = fw->run_post_filter(*state, *pod, diag.node_to_status);
       if (pst.is_success()) nominated = res.nominated_node_name;
       {
-        std::lock_guard<std::mutex> g(stats_mu_);
-        ++stats_.preemption_attempts;
+        cnt_.preemption_attempts.fetch_add(1, std::memory_order_relaxed);
       }
     }
     if (fit_error && !opts_.dump_on_fit_error.empty() && !fit_error_dumped_.exchange(true)) {
@@ -1754,8 +1790,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     cm.attempts[result]->inc();
     cm.attempt[result]->observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
     {
-      std::lock_guard<std::mutex> g(stats_mu_);
-      if (fit_error) ++stats_.unschedulable; else ++stats_.errors;
+      (fit_error ? cnt_.unschedulable : cnt_.errors).fetch_add(1, std::memory_order_relaxed);
     }
     handle_failure(*fw, qpi, st, fit_error ? "Unschedulable" : "SchedulerError", nominated, cycle,
                    diag.unschedulable_plugins);
@@ -1781,8 +1816,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   if (!rst.is_success()) {
     fw->run_unreserve(*state, assumed, host);
     cache_->forget_pod(*assumed);
-    std::lock_guard<std::mutex> g(stats_mu_);
-    ++stats_.errors;
+    cnt_.errors.fetch_add(1, std::memory_order_relaxed);
     handle_failure(*fw, qpi, rst, rst.is_unschedulable() ? "Unschedulable" : "SchedulerError", "", cycle,
                    rst.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{rst.failed_plugin()});
     return;
@@ -1803,6 +1837,9 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   task->e2e = cycle_metrics(*fw).e2e;
   task->keep = task;
   BindTask* tp = task.get();
+  // The binding cycles this Permit releases (the gang's waiting members and
+  // this pod) reach the binder pool in one hand-over.
+  std::optional<Executor::Batch> batch(std::in_place, *binder_);
   Status pst = fw->run_permit(*state, assumed, host, [tp](const Status& wst) {
     tp->permit_status = wst;
     tp->self->binder_->submit([tp] { run_bind_task(tp); });
@@ -1813,8 +1850,7 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
     fw->run_unreserve(*state, assumed, host);
     cache_->forget_pod(*assumed);
     {
-      std::lock_guard<std::mutex> g(stats_mu_);
-      ++stats_.unschedulable;
+      cnt_.unschedulable.fetch_add(1, std::memory_order_relaxed);
     }
     handle_failure(*fw, qpi, pst, pst.is_unschedulable() ? "Unschedulable" : "SchedulerError", "", cycle,
                    pst.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{pst.failed_plugin()});
@@ -1834,10 +1870,10 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   cm.attempts[0]->inc();
   cm.attempt[0]->observe(static_cast<double>(clock_->now_us() - cycle_start) / 1e6);
   {
-    std::lock_guard<std::mutex> g(stats_mu_);
-    ++stats_.scheduled;
+    cnt_.scheduled.fetch_add(1, std::memory_order_relaxed);
   }
   if (pst.is_success()) binder_->submit([tp] { run_bind_task(tp); });
+  batch.reset();
   if (tracer_.enabled()) {
     int64_t t_end = clock_->now_us();
     tracer_.record(TraceEvent{"assume_reserve_permit", assumed->key(), "", algo_end, t_end - algo_end, 0});
@@ -2133,8 +2169,7 @@ void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
     // A forgotten pod frees resources: let waiting pods retry (AssignedPodDelete).
     queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
     {
-      std::lock_guard<std::mutex> g(stats_mu_);
-      ++stats_.bind_failures;
+      cnt_.bind_failures.fetch_add(1, std::memory_order_relaxed);
     }
     handle_failure(*fw, qpi, st, reason, "", cycle,
                    st.failed_plugin().empty() ? std::set<std::string>{} : std::set<std::string>{st.failed_plugin()});
@@ -2193,8 +2228,7 @@ void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
   if (tracer_.enabled()) tracer_.record(TraceEvent{"bind", assumed->key(), host, t0, t1 - t0, 1});
   fw->run_post_bind(*s, assumed, host);
   {
-    std::lock_guard<std::mutex> g(stats_mu_);
-    ++stats_.bound;
+    cnt_.bound.fetch_add(1, std::memory_order_relaxed);
   }
   bound_total_.fetch_add(1, std::memory_order_release);
   note_gang_event(*assumed, true);

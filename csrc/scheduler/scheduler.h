@@ -70,6 +70,22 @@ class Executor {
   explicit Executor(int threads);
   ~Executor();
   void submit(std::function<void()> fn);
+  // While a Batch is alive, submit() calls from its thread to this executor
+  // are collected and handed over under one lock with one wake-up when it
+  // ends (a gang's Allows fire k binding cycles from one Permit call).
+  class Batch {
+   public:
+    explicit Batch(Executor& e);
+    ~Batch();
+    Batch(const Batch&) = delete;
+    Batch& operator=(const Batch&) = delete;
+
+   private:
+    friend class Executor;
+    Executor& e_;
+    Batch* prev_;
+    std::vector<std::function<void()>> fns_;
+  };
   void stop();
   size_t pending() const;
   // A task about to block for a long time (VolumeBinding's PreBind waiting
@@ -393,8 +409,14 @@ class Scheduler {
   std::vector<uint64_t> timer_ids_;
   std::unordered_map<Framework*, std::unordered_map<uint64_t, std::unique_ptr<EqEntry>>> eq_;  // scheduling thread only
 
-  mutable std::mutex stats_mu_;
-  Stats stats_;
+  mutable std::mutex stats_mu_;  // gang records and denials, condition memo
+  // Stats counters: relaxed atomics, bumped by the scheduling, binding and
+  // informer threads without a shared lock.
+  struct Counters {
+    std::atomic<uint64_t> attempts{0}, scheduled{0}, unschedulable{0}, errors{0}, bound{0}, bind_failures{0};
+    std::atomic<uint64_t> preemption_attempts{0}, eq_filter_hits{0}, eq_filter_misses{0};
+    std::atomic<uint64_t> scan_memo_served{0}, scan_memo_mismatches{0};
+  } cnt_;
   std::atomic<uint64_t> bound_total_{0};  // stats_.bound, readable without stats_mu_
   std::atomic<bool> fit_error_dumped_{false};  // dump_on_fit_error written
   std::unordered_map<std::string, GangRecord> gangs_;  // open groups

@@ -90,6 +90,15 @@ for step in "$@"; do
           echo "$b $(timeout -k 5 200 taskset -c "$cpus" abbin/$b /tmp/s_1024 6 | tail -1)" >> "$OUT/abbin1024.txt" || exit 1
         done
       done ;;
+    abbin64)
+      # The same binary A/B on the 64-node headline waves (40 waves).
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_bench --nodes 64 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      for i in 1 2 3; do
+        for b in xsched_stress_base xsched_stress; do
+          echo "$b $(timeout -k 5 200 taskset -c "$cpus" abbin/$b /tmp/s_bench 40 | tail -1)" >> "$OUT/abbin64.txt" || exit 1
+        done
+      done ;;
     sample1024)
       python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_1024 --nodes 1024 &&
       cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
