@@ -49,6 +49,22 @@ void Informers::delete_pods(const std::vector<PodPtr>& ps) {
   }
 }
 
+std::vector<PodPtr> Informers::take_pods(const std::vector<std::string>& keys, const std::vector<std::string_view>& uids,
+                                         const std::vector<std::string_view>& nodes) {
+  std::vector<PodPtr> out(keys.size());
+  std::unique_lock<std::shared_mutex> g(mu_);
+  for (size_t k = 0; k < keys.size(); ++k) {
+    auto it = pods_.find(keys[k]);
+    if (it == pods_.end()) continue;
+    PodPtr p = std::move(it->second);
+    if (p->pg_key) group_remove(p);
+    p->listed.by.store(0, std::memory_order_relaxed);
+    pods_.erase(it);
+    if (p->uid() == uids[k] && p->node_name == nodes[k]) out[k] = std::move(p);
+  }
+  return out;
+}
+
 void Informers::upsert_pod_group(const PodGroupPtr& pg) {
   std::unique_lock<std::shared_mutex> g(mu_);
   std::string key = pg->meta.key();

@@ -29,6 +29,11 @@ class Informers {
   void upsert_pod(const PodPtr& p);
   void delete_pod(const Pod& p);
   void delete_pods(const std::vector<PodPtr>& ps);  // one lock for a run of deletions
+  // A run of Deleted events, one lock: removes each "ns/name" key and returns
+  // the lister's object where it is the same pod (uid) on the same node, else
+  // nullptr (the caller parses the event's final state).
+  std::vector<PodPtr> take_pods(const std::vector<std::string>& keys, const std::vector<std::string_view>& uids,
+                                const std::vector<std::string_view>& nodes);
   void upsert_pod_group(const PodGroupPtr& pg);
   void delete_pod_group(const std::string& key);
   void upsert_elastic_quota(const ElasticQuotaPtr& eq);

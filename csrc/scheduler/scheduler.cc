@@ -678,17 +678,44 @@ void Scheduler::handle_pod_deletes(const WatchEvent* evs, size_t n) {
   std::vector<PodPtr> gone, assigned;
   gone.reserve(n);
   assigned.reserve(n);
+  // One lister lock for the run: keys out, lister objects back where they
+  // still describe the deleted pod (no parse for those).
+  std::vector<std::string> keys;
+  std::vector<std::string_view> uids, nodes;
+  std::vector<size_t> idx;
+  keys.reserve(n);
+  uids.reserve(n);
+  nodes.reserve(n);
+  idx.reserve(n);
   for (size_t i = 0; i < n; ++i) {
     try {
       for (auto& fw : frameworks_) fw->dispatch_object_event("pods", static_cast<int>(evs[i].type), evs[i].obj, evs[i].old);
-      PodPtr p = deleted_pod(evs[i]);
-      if (!p->node_name.empty()) assigned.push_back(p);
-      gone.push_back(std::move(p));
+      const Json& o = *evs[i].obj;
+      const Json& md = o["metadata"];
+      const std::string& ns = md["namespace"].as_string();
+      const std::string& name = md["name"].as_string();
+      std::string key;
+      key.reserve(ns.size() + 1 + name.size());
+      key.append(ns).push_back('/');
+      key.append(name);
+      keys.push_back(std::move(key));
+      uids.push_back(md["uid"].as_string());
+      nodes.push_back(o["spec"]["nodeName"].as_string());
+      idx.push_back(i);
     } catch (const std::exception& e) {
       report_informer_error(evs[i], e.what());
     }
   }
-  informers_->delete_pods(gone);
+  std::vector<PodPtr> listed = informers_->take_pods(keys, uids, nodes);
+  for (size_t k = 0; k < idx.size(); ++k) {
+    try {
+      PodPtr p = listed[k] ? std::move(listed[k]) : Pod::from_json(*evs[idx[k]].obj, *gpu_names_);
+      if (!p->node_name.empty()) assigned.push_back(p);
+      gone.push_back(std::move(p));
+    } catch (const std::exception& e) {
+      report_informer_error(evs[idx[k]], e.what());
+    }
+  }
   if (!assigned.empty()) {
     cache_->remove_pods(assigned);
     queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
