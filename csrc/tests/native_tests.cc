@@ -26,6 +26,7 @@
 #include "framework/types.h"
 #include "scheduler/cache.h"
 #include "scheduler/queue.h"
+#include "scheduler/scheduler.h"
 #include "store/store.h"
 
 using namespace xsched;
@@ -621,6 +622,35 @@ TEST(gpu_assignment_direct_matches_annotations) {
     CHECK(a->gpu.partitions == b.gpu.partitions);
     CHECK_EQ(a->gpu.memory, b.gpu.memory);
   }
+}
+
+TEST(executor_runs_every_task_with_chain_wakeups_and_batches) {
+  // Bursts from several submitters, some inside Batches, with idle gaps so
+  // workers go to sleep between bursts: every task must run (a lost wake-up
+  // would leave tasks queued past the deadline).
+  Executor ex(8);
+  std::atomic<int> ran{0};
+  int want = 0;
+  for (int round = 0; round < 40; ++round) {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 3; ++t)
+      ts.emplace_back([&, t] {
+        if (t == 0) {
+          Executor::Batch b(ex);
+          for (int k = 0; k < 9; ++k) ex.submit([&] { ran.fetch_add(1); });
+        } else {
+          for (int k = 0; k < 5; ++k) ex.submit([&] { ran.fetch_add(1); });
+        }
+      });
+    for (auto& th : ts) th.join();
+    want += 9 + 5 + 5;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(5);
+    while (ran.load() < want && std::chrono::steady_clock::now() < deadline)
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    CHECK_EQ(ran.load(), want);
+    if (round % 4 == 0) std::this_thread::sleep_for(std::chrono::milliseconds(2));  // let workers sleep
+  }
+  ex.stop();
 }
 
 int main() {

@@ -99,6 +99,13 @@ for step in "$@"; do
           echo "$b $(timeout -k 5 200 taskset -c "$cpus" abbin/$b /tmp/s_bench 40 | tail -1)" >> "$OUT/abbin64.txt" || exit 1
         done
       done ;;
+    sample64)
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_bench --nodes 64 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      XSCHED_SAMPLE_HZ=4000 XSCHED_SAMPLE="$OUT/n64.samples" timeout -k 5 200 taskset -c "$cpus" \
+        abbin/xsched_stress /tmp/s_bench 160 > "$OUT/n64.sample_run.txt" 2>&1 &&
+      python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/n64.samples" --exe abbin/xsched_stress --top 40 \
+        > "$OUT/n64_samples.txt" 2>&1 && rm -f "$OUT/n64.samples" ;;
     sample1024)
       python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_1024 --nodes 1024 &&
       cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
