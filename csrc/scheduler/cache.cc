@@ -172,6 +172,7 @@ Status SchedulerCache::assume_pod(const PodPtr& p) {
   add_pod_locked(p);
   in_place_ = false;
   pod_states_[p->uid()] = PodState{p, 0, false};
+  pod_count_.store(pod_states_.size(), std::memory_order_relaxed);
   assumed_.insert(p->uid());
   return {};
 }
@@ -193,6 +194,7 @@ void SchedulerCache::forget_pod(const Pod& p) {
   remove_pod_locked(cur);
   assumed_.erase(p.uid());
   pod_states_.erase(it);
+  pod_count_.store(pod_states_.size(), std::memory_order_relaxed);
 }
 
 namespace {
@@ -242,6 +244,7 @@ void SchedulerCache::add_pod(const PodPtr& p) {
   }
   add_pod_locked(p);
   pod_states_[p->uid()] = PodState{p, 0, false};
+  pod_count_.store(pod_states_.size(), std::memory_order_relaxed);
 }
 
 void SchedulerCache::update_pod(const PodPtr& old_pod, const PodPtr& new_pod) {
@@ -250,6 +253,7 @@ void SchedulerCache::update_pod(const PodPtr& old_pod, const PodPtr& new_pod) {
   if (it == pod_states_.end()) {
     add_pod_locked(new_pod);
     pod_states_[new_pod->uid()] = PodState{new_pod, 0, false};
+    pod_count_.store(pod_states_.size(), std::memory_order_relaxed);
     return;
   }
   if (assumed_.count(new_pod->uid())) {
@@ -273,6 +277,7 @@ void SchedulerCache::remove_pod(const Pod& p) {
   remove_pod_locked(it->second.pod);
   assumed_.erase(p.uid());
   pod_states_.erase(it);
+  pod_count_.store(pod_states_.size(), std::memory_order_relaxed);
 }
 
 void SchedulerCache::remove_pods(const std::vector<PodPtr>& ps) {
@@ -283,6 +288,7 @@ void SchedulerCache::remove_pods(const std::vector<PodPtr>& ps) {
     remove_pod_locked(it->second.pod);
     assumed_.erase(p->uid());
     pod_states_.erase(it);
+    pod_count_.store(pod_states_.size(), std::memory_order_relaxed);
   }
 }
 
@@ -465,6 +471,7 @@ void SchedulerCache::cleanup_expired_assumed_pods() {
     remove_pod_locked(it->second.pod);
     assumed_.erase(uid);
     pod_states_.erase(it);
+    pod_count_.store(pod_states_.size(), std::memory_order_relaxed);
   }
 }
 
@@ -479,10 +486,7 @@ size_t SchedulerCache::node_count() const {
   return order_.size();
 }
 
-size_t SchedulerCache::pod_count() const {
-  std::lock_guard<std::mutex> g(mu_);
-  return pod_states_.size();
-}
+size_t SchedulerCache::pod_count() const { return pod_count_.load(std::memory_order_relaxed); }
 
 size_t SchedulerCache::assumed_count() const {
   std::lock_guard<std::mutex> g(mu_);

@@ -138,6 +138,7 @@ class SchedulerCache {
   std::unordered_map<std::string, NodeInfoPtr> nodes_;
   std::vector<std::string> order_;  // node names with a Node object, insertion order
   std::unordered_map<std::string, PodState> pod_states_;
+  std::atomic<size_t> pod_count_{0};  // pod_states_.size(), readable without mu_
   std::unordered_set<std::string> assumed_;
   // Written under mu_ + group_mu_, read under group_mu_ only: Permit and
   // PreScore read a gang's count without waiting behind NodeInfo copies.

@@ -29,6 +29,23 @@ void Informers::upsert_pod(const PodPtr& p) {
   if (p->pg_key) pods_by_group_[p->pg_key].push_back(p);
 }
 
+void Informers::upsert_pods(const PodPtr* ps, PodPtr* prev, size_t n) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  for (size_t i = 0; i < n; ++i) {
+    const PodPtr& p = ps[i];
+    if (!p) continue;
+    auto [it, fresh] = pods_.try_emplace(p->key(), p);
+    if (!fresh) {
+      prev[i] = it->second;
+      if (it->second->pg_key) group_remove(it->second);
+      if (it->second != p) it->second->listed.by.store(0, std::memory_order_relaxed);
+      it->second = p;
+    }
+    p->listed.by.store(instance_, std::memory_order_relaxed);
+    if (p->pg_key) pods_by_group_[p->pg_key].push_back(p);
+  }
+}
+
 void Informers::delete_pod(const Pod& p) {
   std::unique_lock<std::shared_mutex> g(mu_);
   auto it = pods_.find(p.key());

@@ -29,6 +29,9 @@ class Informers {
   void upsert_pod(const PodPtr& p);
   void delete_pod(const Pod& p);
   void delete_pods(const std::vector<PodPtr>& ps);  // one lock for a run of deletions
+  // upsert_pod for the non-null ps[0..n), one lock; prev[i] receives the
+  // object each replaced (nullptr if none).
+  void upsert_pods(const PodPtr* ps, PodPtr* prev, size_t n);
   // A run of Deleted events, one lock: removes each "ns/name" key and returns
   // the lister's object where it is the same pod (uid) on the same node, else
   // nullptr (the caller parses the event's final state).

@@ -530,9 +530,9 @@ void Scheduler::informer_loop() {
         } catch (const std::exception&) {
           continue;
         }
-        prev[hi - 1] = informers_->pod(parsed[hi - 1]->ns(), parsed[hi - 1]->name());
-        informers_->upsert_pod(parsed[hi - 1]);
       }
+      // The window's pods enter the listers under one lock (previous objects back).
+      informers_->upsert_pods(&parsed[lo], &prev[lo], hi - lo);
       for (size_t i = lo; i < hi;) {
         if (!parsed[i] && evs[i].type == EventType::Deleted && evs[i].kind == "pods") {
           size_t j = i + 1;
@@ -1911,26 +1911,37 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
   }
 }
 
-bool Scheduler::wait_bound(uint64_t target, int64_t timeout_us) const {
-  // Polls a counter instead of a condition variable: the binder threads
-  // then pay nothing per bind, and the waiter (a benchmark harness) wakes
-  // within ~50 us of the last binding.
-  // Wall time, not clock_ (a fake clock in tests does not advance).
-  const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
-  while (bound_total_.load(std::memory_order_acquire) < target) {
-    if (std::chrono::steady_clock::now() > end) return false;
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
+namespace {
+// Polls `done` until it holds or `timeout_us` passes (wall time, not clock_:
+// a fake clock in tests does not advance): a short spin first, since a
+// benchmark harness usually waits for the last few bindings of a wave, then
+// sleeps of 20 us (a sleep overshoots by tens of microseconds).
+template <class F>
+bool poll_until(F done, int64_t timeout_us) {
+  const auto start = std::chrono::steady_clock::now();
+  const auto end = start + std::chrono::microseconds(timeout_us);
+  const auto spin_end = start + std::chrono::microseconds(300);
+  while (!done()) {
+    const auto now = std::chrono::steady_clock::now();
+    if (now > end) return false;
+    if (now < spin_end) {
+      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
   }
   return true;
 }
+}  // namespace
+
+bool Scheduler::wait_bound(uint64_t target, int64_t timeout_us) const {
+  // Polls a counter instead of a condition variable: the binder threads
+  // then pay nothing per bind.
+  return poll_until([&] { return bound_total_.load(std::memory_order_acquire) >= target; }, timeout_us);
+}
 
 bool Scheduler::wait_cache_empty(int64_t timeout_us) const {
-  const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
-  while (cache_->pod_count() > 0) {
-    if (std::chrono::steady_clock::now() > end) return false;
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
-  }
-  return true;
+  return poll_until([&] { return cache_->pod_count() == 0; }, timeout_us);
 }
 
 Json Scheduler::check_cache() const {
