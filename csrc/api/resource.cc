@@ -26,6 +26,23 @@ ResourceRegistry::ResourceRegistry() {
 }
 
 int ResourceRegistry::id(std::string_view name) {
+  // Ids never change once assigned: a per-thread cache of the names a thread
+  // saw skips the lock and the key allocation (pod parses run on several
+  // threads and ask for the same handful of names).
+  struct Seen {
+    const ResourceRegistry* reg;
+    std::string name;
+    int id;
+  };
+  thread_local std::vector<Seen> seen;
+  for (const auto& e : seen)
+    if (e.reg == this && e.name == name) return e.id;
+  const int id = id_locked(name);
+  if (seen.size() < 32) seen.push_back(Seen{this, std::string(name), id});
+  return id;
+}
+
+int ResourceRegistry::id_locked(std::string_view name) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = ids_.find(std::string(name));
   if (it != ids_.end()) return it->second;

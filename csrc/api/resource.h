@@ -39,6 +39,7 @@ class ResourceRegistry {
   bool is_hugepages(int id) const { return id >= 0 && id < kMaxRes && (flags_[id] & kHuge); }
 
  private:
+  int id_locked(std::string_view name);
   enum : uint8_t { kNative = 1, kHuge = 2 };
   static uint8_t flags_for(std::string_view name);
   ResourceRegistry();

@@ -9,10 +9,11 @@
 
 namespace xsched {
 
-Parallelizer::Parallelizer(int workers, int inline_below) : workers_(std::max(1, workers)), inline_below_(inline_below) {
+Parallelizer::Parallelizer(int workers, int inline_below, const char* thread_name)
+    : workers_(std::max(1, workers)), inline_below_(inline_below) {
   if (const char* e = std::getenv("XSCHED_MIN_PARALLEL_NS")) min_parallel_work_ns_ = std::max<int64_t>(0, std::atoll(e));
-  for (int i = 0; i < workers_ - 1; ++i) threads_.emplace_back([this] {
-    name_this_thread("xs-filter");
+  for (int i = 0; i < workers_ - 1; ++i) threads_.emplace_back([this, thread_name] {
+    name_this_thread(thread_name);
     worker_loop();
   });
 }

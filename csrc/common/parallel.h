@@ -38,7 +38,7 @@ struct ParallelSite {
 
 class Parallelizer {
  public:
-  explicit Parallelizer(int workers = 16, int inline_below = 128);
+  explicit Parallelizer(int workers = 16, int inline_below = 128, const char* thread_name = "xs-filter");
   ~Parallelizer();
   Parallelizer(const Parallelizer&) = delete;
   Parallelizer& operator=(const Parallelizer&) = delete;

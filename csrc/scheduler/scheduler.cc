@@ -298,6 +298,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
   tracer_.enable(opts_.trace);
   timers_ = std::make_unique<TimerService>(clock_);
   parallelizer_ = std::make_unique<Parallelizer>(opts_.parallelism, opts_.parallel_inline_below);
+  parse_pool_ = std::make_unique<Parallelizer>(4, 8, "xs-parse");
   metrics_ = std::make_unique<Metrics>();
   cache_ = std::make_unique<SchedulerCache>(clock_, opts_.assumed_pod_ttl_us);
   informers_ = std::make_unique<Informers>();
@@ -508,6 +509,7 @@ void Scheduler::informer_loop() {
     // drives cache and queue.
     std::vector<PodPtr> parsed(evs.size());
     std::vector<PodPtr> prev(evs.size());
+    std::vector<size_t> to_parse;
     auto group_of = [](const WatchEvent& ev) -> const std::string& {
       return (*ev.obj)["metadata"]["labels"][kPodGroupLabel].as_string();
     };
@@ -526,10 +528,22 @@ void Scheduler::informer_loop() {
         if (ev.kind != "pods" || ev.type == EventType::Deleted) continue;
         try {
           if (ev.type == EventType::Modified) parsed[hi - 1] = bound_copy_of_assumed(ev);
-          if (!parsed[hi - 1]) parsed[hi - 1] = Pod::from_json(*ev.obj, *gpu_names_);
         } catch (const std::exception&) {
           continue;
         }
+        if (!parsed[hi - 1]) to_parse.push_back(hi - 1);
+      }
+      // Pod::from_json is pure: a window's parses run on the parse helpers.
+      if (!to_parse.empty()) {
+        parse_pool_->until(static_cast<int>(to_parse.size()), [&](int k) {
+          const size_t i = to_parse[static_cast<size_t>(k)];
+          try {
+            parsed[i] = Pod::from_json(*evs[i].obj, *gpu_names_);
+          } catch (const std::exception&) {
+            // left unparsed: handle_event below parses it again and reports
+          }
+        }, nullptr, &parse_site_);
+        to_parse.clear();
       }
       // The window's pods enter the listers under one lock (previous objects back).
       informers_->upsert_pods(&parsed[lo], &prev[lo], hi - lo);

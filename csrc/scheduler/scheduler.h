@@ -375,6 +375,9 @@ class Scheduler {
   SchedulerOptions opts_;
   std::unique_ptr<TimerService> timers_;
   std::unique_ptr<Parallelizer> parallelizer_;
+  // Informer windows parse their pods' JSON on a few helpers ("xs-parse").
+  std::unique_ptr<Parallelizer> parse_pool_;
+  ParallelSite parse_site_;
   std::unique_ptr<Metrics> metrics_;
   std::unique_ptr<SchedulerCache> cache_;
   std::unique_ptr<Informers> informers_;
