@@ -50,13 +50,15 @@ class Shard:
 
     def run(self, wave: Wave, timeout_s: float = 120.0, *,
             prepared: tuple[str, str] | list[tuple[str, str]] | None = None,
-            check_cache: dict | None = None) -> StepResult:
+            check_cache: dict | None = None, collect_gangs: bool = True) -> StepResult:
         """One wave: create, wait until bound, delete, wait until the cache
         drained. `prepared` is the wave's JSON, either (PodGroups, pods) or
         Wave.chunks_json() (PodGroups written chunk by chunk just before their
         pods). With `check_cache` (a dict, filled in), the cache debugger
         runs once the wave is bound and no binding is in flight, before the
-        deletion (untimed callers only)."""
+        deletion (untimed callers only). With `collect_gangs` False the gang
+        records stay in the scheduler (a caller collects many waves' worth
+        at once with sched.gang_records)."""
         chunks = prepared if isinstance(prepared, list) else [prepared or (wave.groups_json(), wave.pods_json())]
         n = len(wave.pods)
         target = self._bound + n
@@ -82,7 +84,7 @@ class Shard:
             while sched.stats()["inflight_bindings"] > 0 and time.perf_counter() < deadline:
                 time.sleep(0.0002)
             check_cache.update(sched.check_cache())
-        gangs = sched.gang_records(True)
+        gangs = sched.gang_records(True) if collect_gangs else []
         self.store.delete_all("pods", self.ns)
         self.store.delete_all("podgroups", self.ns)
         if not sched.wait_cache_empty(max(0.0, deadline - time.perf_counter())):
