@@ -298,7 +298,9 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
   tracer_.enable(opts_.trace);
   timers_ = std::make_unique<TimerService>(clock_);
   parallelizer_ = std::make_unique<Parallelizer>(opts_.parallelism, opts_.parallel_inline_below);
-  parse_pool_ = std::make_unique<Parallelizer>(4, 8, "xs-parse");
+  // XSCHED_PARSE_POOL=0: parse on the informer thread (A/B runs).
+  if (const char* v = std::getenv("XSCHED_PARSE_POOL"); !v || std::string(v) != "0")
+    parse_pool_ = std::make_unique<Parallelizer>(4, 32, "xs-parse");
   metrics_ = std::make_unique<Metrics>();
   cache_ = std::make_unique<SchedulerCache>(clock_, opts_.assumed_pod_ttl_us);
   informers_ = std::make_unique<Informers>();
@@ -535,14 +537,19 @@ void Scheduler::informer_loop() {
       }
       // Pod::from_json is pure: a window's parses run on the parse helpers.
       if (!to_parse.empty()) {
-        parse_pool_->until(static_cast<int>(to_parse.size()), [&](int k) {
+        auto parse_one = [&](int k) {
           const size_t i = to_parse[static_cast<size_t>(k)];
           try {
             parsed[i] = Pod::from_json(*evs[i].obj, *gpu_names_);
           } catch (const std::exception&) {
             // left unparsed: handle_event below parses it again and reports
           }
-        }, nullptr, &parse_site_);
+        };
+        if (parse_pool_) {
+          parse_pool_->until(static_cast<int>(to_parse.size()), parse_one, nullptr, &parse_site_);
+        } else {
+          for (size_t k = 0; k < to_parse.size(); ++k) parse_one(static_cast<int>(k));
+        }
         to_parse.clear();
       }
       // The window's pods enter the listers under one lock (previous objects back).

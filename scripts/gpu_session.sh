@@ -32,6 +32,16 @@ for step in "$@"; do
         timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --waves-per-step 1 --no-scenarios --no-placement \
           --no-service-mode --no-open-loop > "$OUT/bench_r3shape_$i.json" 2> "$OUT/bench_r3shape_$i.err" || exit $?
       done ;;
+    benchab)
+      # A/B of an env toggle (AB_VAR, AB_VALUES) on the default 64-node bench
+      # (open-loop capacity included), alternating 2x.
+      var=${AB_VAR:-XSCHED_PARSE_POOL}
+      for i in 1 2; do
+        for v in ${AB_VALUES:-0 1}; do
+          env "$var=$v" timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-scenarios --no-placement \
+            --no-service-mode > "$OUT/benchab_${var}_${v}_$i.json" 2> "$OUT/benchab_${var}_${v}_$i.err" || exit $?
+        done
+      done ;;
     nodes1024_3) for i in 1 2 3; do
                    timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
                      --no-service-mode > "$OUT/bench_nodes_1024_$i.json" 2> "$OUT/bench_nodes_1024_$i.err" || exit $?
