@@ -298,8 +298,10 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
   tracer_.enable(opts_.trace);
   timers_ = std::make_unique<TimerService>(clock_);
   parallelizer_ = std::make_unique<Parallelizer>(opts_.parallelism, opts_.parallel_inline_below);
-  // XSCHED_PARSE_POOL=0: parse on the informer thread (A/B runs).
-  if (const char* v = std::getenv("XSCHED_PARSE_POOL"); !v || std::string(v) != "0")
+  // XSCHED_PARSE_POOL=1: parse informer windows on 4 helper threads. Off by
+  // default: on the 16-CPU L3 domain a shard runs in, the helpers' spinning
+  // made some box runs markedly slower (profiles/r4q_treeab_*).
+  if (const char* v = std::getenv("XSCHED_PARSE_POOL"); v && std::string(v) == "1")
     parse_pool_ = std::make_unique<Parallelizer>(4, 32, "xs-parse");
   metrics_ = std::make_unique<Metrics>();
   cache_ = std::make_unique<SchedulerCache>(clock_, opts_.assumed_pod_ttl_us);
@@ -1933,23 +1935,15 @@ void Scheduler::schedule_cycle(const QueuedPodInfoPtr& qpi) {
 }
 
 namespace {
-// Polls `done` until it holds or `timeout_us` passes (wall time, not clock_:
-// a fake clock in tests does not advance): a short spin first, since a
-// benchmark harness usually waits for the last few bindings of a wave, then
-// sleeps of 20 us (a sleep overshoots by tens of microseconds).
+// Polls `done` every 20 us until it holds or `timeout_us` passes (wall time,
+// not clock_: a fake clock in tests does not advance). No spinning: the
+// waiter shares its CPU domain with the scheduler's threads.
 template <class F>
 bool poll_until(F done, int64_t timeout_us) {
-  const auto start = std::chrono::steady_clock::now();
-  const auto end = start + std::chrono::microseconds(timeout_us);
-  const auto spin_end = start + std::chrono::microseconds(300);
+  const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
   while (!done()) {
-    const auto now = std::chrono::steady_clock::now();
-    if (now > end) return false;
-    if (now < spin_end) {
-      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
-    } else {
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
+    if (std::chrono::steady_clock::now() > end) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
   return true;
 }

@@ -72,8 +72,7 @@ class Shard:
         deadline = t0 + timeout_s
         sched = self.sched
         # Waits natively (no Python per poll, no stats lock): wait_bound polls
-        # the scheduler's bound counter with the GIL released (a short spin,
-        # then 20 us sleeps).
+        # the scheduler's bound counter every 20 us with the GIL released.
         if not sched.wait_bound(target, max(0.0, deadline - time.perf_counter())):
             b = sched.stats()["bound"]
             raise WaveTimeout(f"wave not bound after {timeout_s}s: {b - self._bound}/{n} "

@@ -45,13 +45,13 @@ for step in "$@"; do
     treeab)
       # A/B of two trees on one box: ./abtree (an older commit, built in
       # place) against this tree, default 64-node bench and 1,024 nodes.
-      for i in 1 2; do
+      for i in 1 2 3; do
         for t in abtree .; do
-          tag=$( [ "$t" = . ] && echo cur || echo old )
+          which=$( [ "$t" = . ] && echo cur || echo old )
           (cd "$t" && timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-scenarios --no-placement \
-            --no-service-mode) > "$OUT/treeab_${tag}_64_$i.json" 2> "$OUT/treeab_${tag}_64_$i.err" || exit $?
+            --no-service-mode) > "$OUT/treeab_${which}_64_$i.json" 2> "$OUT/treeab_${which}_64_$i.err" || exit $?
           (cd "$t" && timeout -k 10 300 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
-            --no-service-mode --no-open-loop) > "$OUT/treeab_${tag}_1024_$i.json" 2> "$OUT/treeab_${tag}_1024_$i.err" || exit $?
+            --no-service-mode --no-open-loop) > "$OUT/treeab_${which}_1024_$i.json" 2> "$OUT/treeab_${which}_1024_$i.err" || exit $?
         done
       done ;;
     nodes1024_3) for i in 1 2 3; do
