@@ -493,7 +493,7 @@ Scheduler::Stats Scheduler::stats() const {
 
 std::vector<GangRecord> Scheduler::gang_records(bool clear) {
   std::lock_guard<std::mutex> g(stats_mu_);
-  std::vector<GangRecord> out = gang_done_;
+  std::vector<GangRecord> out(gang_done_.begin(), gang_done_.end());
   if (clear) gang_done_.clear();
   return out;
 }
@@ -925,8 +925,15 @@ void Scheduler::note_gang_event(const Pod& p, bool bound) {
   if (++r.bound < need) return;
   r.bound_us = now;
   if (r.admit_us == 0) r.admit_us = now;
-  metrics_->histogram("xsched_gang_admit_seconds", "size=\"" + std::to_string(need) + "\"")
-      .observe(static_cast<double>(r.bound_us - r.first_enqueue_us) / 1e6);
+  // The per-size histogram, looked up once per size and metrics epoch.
+  const uint64_t epoch = metrics_->epoch();
+  if (gang_hist_epoch_ != epoch) {
+    gang_hist_.clear();
+    gang_hist_epoch_ = epoch;
+  }
+  Histogram*& hist = gang_hist_[need];
+  if (!hist) hist = &metrics_->histogram("xsched_gang_admit_seconds", "size=\"" + std::to_string(need) + "\"");
+  hist->observe(static_cast<double>(r.bound_us - r.first_enqueue_us) / 1e6);
   gang_done_.push_back(r);
   gangs_.erase(it);
 }

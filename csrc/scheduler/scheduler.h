@@ -423,7 +423,12 @@ class Scheduler {
   std::atomic<uint64_t> bound_total_{0};  // stats_.bound, readable without stats_mu_
   std::atomic<bool> fit_error_dumped_{false};  // dump_on_fit_error written
   std::unordered_map<std::string, GangRecord> gangs_;  // open groups
-  std::vector<GangRecord> gang_done_;
+  // Completed gangs until a caller collects them: a deque, so the push on a
+  // binding thread (under stats_mu_) never moves the records already there
+  // (a benchmark collects ~10^5 of them at once).
+  std::deque<GangRecord> gang_done_;
+  std::unordered_map<int, Histogram*> gang_hist_;  // xsched_gang_admit_seconds{size} (under stats_mu_)
+  uint64_t gang_hist_epoch_ = ~0ULL;
   static constexpr size_t kMaxGangDenials = 256;
   std::vector<GangDenial> gang_denials_;
   uint64_t gang_denials_total_ = 0;
