@@ -298,6 +298,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
   tracer_.enable(opts_.trace);
   timers_ = std::make_unique<TimerService>(clock_);
   parallelizer_ = std::make_unique<Parallelizer>(opts_.parallelism, opts_.parallel_inline_below);
+  if (const char* v = std::getenv("XSCHED_INFORMER_WINDOW")) informer_window_ = std::max<size_t>(1, std::atoll(v));
   // XSCHED_PARSE_POOL=1: parse informer windows on 4 helper threads. Off by
   // default: on the 16-CPU L3 domain a shard runs in, the helpers' spinning
   // made some box runs markedly slower (profiles/r4q_treeab_*).
@@ -522,7 +523,7 @@ void Scheduler::informer_loop() {
       size_t hi = lo;
       while (hi < evs.size()) {
         const auto& ev = evs[hi];
-        if (hi - lo >= kInformerWindow) {
+        if (hi - lo >= informer_window_) {
           const auto& pe = evs[hi - 1];
           bool same_group = ev.kind == "pods" && pe.kind == "pods" && ev.type == EventType::Added &&
                             pe.type == EventType::Added && !group_of(ev).empty() && group_of(ev) == group_of(pe);

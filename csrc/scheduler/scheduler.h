@@ -278,6 +278,7 @@ class Scheduler {
   void refresh_nom_mark(const NominatedMap* view);
   std::vector<const Status*> fail_ptr_;
   static constexpr size_t kInformerWindow = 64;
+  size_t informer_window_ = kInformerWindow;  // XSCHED_INFORMER_WINDOW overrides (A/B runs)
   ParallelSite filter_site_;  // inline-vs-parallel cost model of Filter
   // Per-profile metric cells of the scheduling cycle, cached per metrics
   // epoch (scheduling thread / sched_mu_ only).
