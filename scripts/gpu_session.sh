@@ -54,6 +54,11 @@ for step in "$@"; do
             --no-service-mode --no-open-loop) > "$OUT/treeab_${which}_1024_$i.json" 2> "$OUT/treeab_${which}_1024_$i.err" || exit $?
         done
       done ;;
+    tune)
+      # Probe variant sweep (unroll x cache policy x workgroups/CU) per mode at
+      # the default 2 GiB working set.
+      timeout -k 10 400 python3 -c "import json; from flex_gpu_scheduler_amd.ops.hip_probe import probe; p = probe(); print(json.dumps([p.tune(mode=m, iters=10) for m in ('read', 'write', 'copy', 'triad')]))" \
+        > "$OUT/tune.json" 2> "$OUT/tune.err" ;;
     nodes1024_3) for i in 1 2 3; do
                    timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
                      --no-service-mode > "$OUT/bench_nodes_1024_$i.json" 2> "$OUT/bench_nodes_1024_$i.err" || exit $?
