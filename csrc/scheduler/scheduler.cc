@@ -505,7 +505,7 @@ void Scheduler::informer_loop() {
     auto evs = watcher_->next(50, 8192);
     if (evs.empty()) continue;
     int64_t batch_start = tracer_.enabled() ? clock_->now_us() : 0;
-    // The batch is handled in windows of >= kInformerWindow events that end
+    // The batch is handled in windows of >= informer_window_ events that end
     // on a PodGroup boundary, so the scheduling thread starts on the first
     // gangs of a bulk create instead of waiting for the whole batch.
     // Per window, pass 1 parses every pod once and publishes it to the

@@ -421,7 +421,7 @@ class Scheduler {
     std::atomic<uint64_t> preemption_attempts{0}, eq_filter_hits{0}, eq_filter_misses{0};
     std::atomic<uint64_t> scan_memo_served{0}, scan_memo_mismatches{0};
   } cnt_;
-  std::atomic<uint64_t> bound_total_{0};  // stats_.bound, readable without stats_mu_
+  std::atomic<uint64_t> bound_total_{0};  // bound pods, released for wait_bound (cnt_.bound counts the same)
   std::atomic<bool> fit_error_dumped_{false};  // dump_on_fit_error written
   std::unordered_map<std::string, GangRecord> gangs_;  // open groups
   // Completed gangs until a caller collects them: a deque, so the push on a
