@@ -334,13 +334,14 @@ void launch(const Variant& v, int mode, int grid, hipStream_t s, void* a, void* 
 }
 
 Variant default_variant(int mode) {
-  // Measured optimum per mode on MI355X (profiles/r1b_probe_sweep.json):
-  // one 16-B access per lane per iteration wins; non-temporal loads help,
-  // plain stores beat nt stores for pure writes; 4-8 workgroups per CU.
+  // Measured optimum per mode on MI355X at the 2 GiB working set
+  // (profiles/r4v_probe_variant_sweep_2GiB.json): one 16-B access per lane
+  // per iteration wins; non-temporal accesses help except for pure writes;
+  // 8 workgroups per CU for read and write, 4 for copy and triad.
   Variant v;
   v.unroll = 1;
   v.nt = mode != 1;
-  v.bpc = mode == 0 ? 8 : 4;
+  v.bpc = (mode == 0 || mode == 1) ? 8 : 4;
   return v;
 }
 
