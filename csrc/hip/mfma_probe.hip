@@ -17,6 +17,7 @@
 // register q holds C[(q&3) + 8(q>>2) + 4h][r].
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <vector>
@@ -138,14 +139,18 @@ int xs_mfma_check(int dev, int K) {
 }
 
 // Dense bf16 MFMA throughput on the XCDs of `xcd_mask` (0xff = whole GPU).
-// `blocks` = launch size (0: 2 per CU). Returns 0 and TFLOP/s, ms and the
+// `blocks` = launch size (0: 8 per CU = 8 waves per SIMD). With the clock
+// ramped by the warm-up, 2-8 waves per SIMD all issue at 98-99% of the
+// 2.5 PF rate (profiles/r4z_mfma_sweep.jsonl); the earlier 79% reading was a
+// clock still ramping under a short warm-up (r4x/r4y sweeps: rate rising with
+// launch size and length only because each point ran hotter). Returns 0 and TFLOP/s, ms and the
 // number of workgroups that ran on the selected XCDs.
 int xs_mfma_peak(int dev, int iters, uint32_t xcd_mask, int blocks, double* tflops, double* ms_out,
                  int* active_blocks) {
   XS_MCHECK(hipSetDevice(dev));
   hipDeviceProp_t p;
   XS_MCHECK(hipGetDeviceProperties(&p, dev));
-  if (blocks <= 0) blocks = 2 * p.multiProcessorCount;
+  if (blocks <= 0) blocks = 8 * p.multiProcessorCount;
   if (iters <= 0) iters = 4096;
   xsprobe::DevMem active_mem, sink_mem;
   XS_MCHECK(hipMalloc(&active_mem.p, sizeof(unsigned)));
@@ -155,15 +160,25 @@ int xs_mfma_peak(int dev, int iters, uint32_t xcd_mask, int blocks, double* tflo
   xsprobe::Stream stream;
   XS_MCHECK(hipStreamCreate(&stream.s));
   hipStream_t s = stream.s;
-  // Warm-up (clocks up, code resident).
-  XS_MCHECK(hipMemsetAsync(d_active, 0, sizeof(unsigned), s));
-  hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters / 4 + 1, xcd_mask, d_active, d_sink);
-  XS_MCHECK(hipGetLastError());
-  XS_MCHECK(hipMemsetAsync(d_active, 0, sizeof(unsigned), s));
   xsprobe::Event ev0, ev1;
   XS_MCHECK(hipEventCreate(&ev0.e));
   XS_MCHECK(hipEventCreate(&ev1.e));
   hipEvent_t e0 = ev0.e, e1 = ev1.e;
+  // Warm-up: code resident, then about 20 ms of the same load so the clock has
+  // ramped before the timed launch (a fresh process timed after a short
+  // warm-up read ~17% low, profiles/r4y_probe_kernels_a.log).
+  float warm_ms = 0.f;
+  XS_MCHECK(hipEventRecord(e0, s));
+  hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters, xcd_mask, d_active, d_sink);
+  XS_MCHECK(hipGetLastError());
+  XS_MCHECK(hipEventRecord(e1, s));
+  XS_MCHECK(hipEventSynchronize(e1));
+  XS_MCHECK(hipEventElapsedTime(&warm_ms, e0, e1));
+  const int warm = warm_ms > 0.f ? std::min(64, static_cast<int>(20.f / warm_ms) + 1) : 4;
+  for (int w = 0; w < warm; ++w)
+    hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters, xcd_mask, d_active, d_sink);
+  XS_MCHECK(hipGetLastError());
+  XS_MCHECK(hipMemsetAsync(d_active, 0, sizeof(unsigned), s));
   XS_MCHECK(hipEventRecord(e0, s));
   hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters, xcd_mask, d_active, d_sink);
   XS_MCHECK(hipGetLastError());

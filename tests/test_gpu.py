@@ -155,9 +155,10 @@ def test_mfma_peak_scales_with_xcds():
     p = probe()
     full = p.mfma_peak(0, 0xFF, iters=8192)
     one = p.mfma_peak(0, 0x01, iters=8192)
-    assert full["active_blocks"] == 2 * p.props(0)["computeUnits"]
-    # Dense bf16: well above the f32 vector rate, below the 2.5 PF spec peak.
-    assert 300.0 < full["tflops"] < 2600.0, full
+    assert full["active_blocks"] == 8 * p.props(0)["computeUnits"]
+    # Dense bf16 after a clock-ramping warm-up: near the 2.5 PF issue rate
+    # (2.40-2.49 PF measured, profiles/r4z_mfma_sweep.jsonl), never above it.
+    assert 1800.0 < full["tflops"] < 2600.0, full
     # One XCD is an eighth of the chip (CPX partition budget).
     ratio = one["tflops"] / full["tflops"]
     assert 0.08 < ratio < 0.2, (one, full)
