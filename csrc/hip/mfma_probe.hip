@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "hip/device_raii.h"
@@ -165,8 +166,9 @@ int xs_mfma_peak(int dev, int iters, uint32_t xcd_mask, int blocks, double* tflo
   XS_MCHECK(hipEventCreate(&ev1.e));
   hipEvent_t e0 = ev0.e, e1 = ev1.e;
   // Warm-up: code resident, then about 20 ms of the same load so the clock has
-  // ramped before the timed launch (a fresh process timed after a short
-  // warm-up read ~17% low, profiles/r4y_probe_kernels_a.log).
+  // ramped before the timed launch: 2.11 -> 2.40-2.41 PF/s in a fresh process
+  // (profiles/r4za_probe_warm_ab.jsonl). The HBM probes are memory-bound and
+  // read the same with or without it (same file), so they keep their short one.
   float warm_ms = 0.f;
   XS_MCHECK(hipEventRecord(e0, s));
   hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters, xcd_mask, d_active, d_sink);
@@ -174,7 +176,9 @@ int xs_mfma_peak(int dev, int iters, uint32_t xcd_mask, int blocks, double* tflo
   XS_MCHECK(hipEventRecord(e1, s));
   XS_MCHECK(hipEventSynchronize(e1));
   XS_MCHECK(hipEventElapsedTime(&warm_ms, e0, e1));
-  const int warm = warm_ms > 0.f ? std::min(64, static_cast<int>(20.f / warm_ms) + 1) : 4;
+  const char* env = std::getenv("XS_PROBE_WARM_MS");  // as the HBM probes; 0 = one launch
+  const float target = env ? static_cast<float>(std::atof(env)) : 20.f;
+  const int warm = target <= 0.f ? 0 : warm_ms > 0.f ? std::min(64, static_cast<int>(target / warm_ms) + 1) : 4;
   for (int w = 0; w < warm; ++w)
     hipLaunchKernelGGL(k_mfma_peak, dim3(blocks), dim3(kPeakBlock), 0, s, iters, xcd_mask, d_active, d_sink);
   XS_MCHECK(hipGetLastError());
