@@ -5,9 +5,11 @@ clock/power-bound one (flat across launch sizes, falling with run length).
 Prints one JSON line per point. Usage: python scripts/mfma_sweep.py [out.jsonl]
 """
 import json
+import os
 import sys
 
-from flex_gpu_scheduler_amd.ops.hip_probe import probe
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flex_gpu_scheduler_amd.ops.hip_probe import probe  # noqa: E402
 
 
 def main() -> int:
