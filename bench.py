@@ -8,13 +8,24 @@ scheduler shard (its own store + scheduler over `--nodes` 8x MI355X nodes),
 so per-GPU work is fixed as N grows (weak scaling) and `value` is the sum of
 pods/s over ranks divided by the slowest rank's time.
 
-GPU use: each rank discovers its MI355X with the HIP probe (device props +
-checksum health test, untimed) and sizes the synthetic nodes' HBM from it.
-After the timed steps (untimed) the ranks validate placement end to end
+GPU use: every rank probes its own MI355X concurrently with the HIP probes
+(device props, checksum health test, MFMA tile check and the per-partition
+HBM bandwidth table the node agent publishes; untimed) -> `config.gpu_probes`,
+one row per GPU, and sizes the synthetic nodes' HBM from it. After the timed
+steps (untimed) the ranks validate placement end to end
 (parallel/placement.py): the live node from discovery, PodGroups of 1/2/4/8
 ranks scheduled, each rank resolved through the device plugin's Allocate, and
 an RCCL all-reduce on exactly the allocated GPUs next to deliberately bad
-placements -> `config.rccl_placement`.
+placements, each row judged against an xGMI bus-bandwidth model ->
+`config.rccl_placement`. That is the last collective: then ranks > 0 exit and
+rank 0 alone runs the untimed extras (open-loop admission latency, a
+1,024-node run, steady-state service mode, the BASELINE scenarios), so no rank
+waits inside an RCCL collective while they run.
+
+Every headline number is also a scalar key of `config` (the driver keeps
+scalars only): p99_gang_admit_ms_<type> (burst), open_loop_capacity_pods_per_s,
+open_loop_p99_create_to_bound_ms_<type> (at 90% of that capacity),
+denied_gang_fraction, nodes1024_pods_per_s, service_mode_pods_per_s.
 
     python bench.py --gpus N --steps K --warmup W
 
@@ -87,6 +98,32 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     return rc
 
 
+def run_nodes(nodes: int, waves: int, seed: int, options: dict) -> dict:
+    """Untimed run of the headline workload on one `nodes`-node shard: two
+    warm-up waves, then `waves` timed waves (pods/s over those)."""
+    from flex_gpu_scheduler_amd.utils.benchrun import Shard, gang_latency_summary
+    from flex_gpu_scheduler_amd.utils.workload import ClusterSpec
+
+    shard = Shard(ClusterSpec(nodes=nodes), namespace=f"bench-n{nodes}", seed=seed + 104729, options=options)
+    try:
+        ws = [shard.wave(i) for i in range(waves + 2)]
+        prepared = [w.chunks_json() for w in ws]
+        for i in range(2):
+            shard.run(ws[i], prepared=prepared[i])
+        shard.sched.gang_records(True)
+        t0 = time.perf_counter()
+        pods = 0
+        for i in range(2, waves + 2):
+            pods += shard.run(ws[i], prepared=prepared[i], collect_gangs=False).pods
+        dt = time.perf_counter() - t0
+        lat = gang_latency_summary(shard.sched.gang_records(True), by_type=True)
+        return {"nodes": nodes, "waves": waves, "pods": pods, "seconds": round(dt, 3),
+                "pods_per_s": round(pods / dt, 1) if dt > 0 else 0.0,
+                "p99_gang_admit_ms": {k: v["p99_ms"] for k, v in lat.items()}}
+    finally:
+        shard.close()
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,6 +147,8 @@ def main() -> int:
                     help="skip the untimed service-mode run (API server in another process, HTTP)")
     ap.add_argument("--no-placement", action="store_true",
                     help="skip the end-to-end placement validation (discovery -> scheduler -> Allocate -> RCCL)")
+    ap.add_argument("--nodes1024-waves", type=int, default=6,
+                    help="timed waves of the untimed 1,024-node run (0 skips it)")
     args = ap.parse_args()
 
     world = os.environ.get("WORLD_SIZE")
@@ -140,6 +179,20 @@ def main() -> int:
         hbm_gib = max(1, int(props["totalGlobalMem"]) // (1 << 30))
         extras["gpu"] = {"name": props.get("gcnArchName"), "computeUnits": props.get("computeUnits"),
                          "hbm_gib": hbm_gib}
+        # The node agent's per-GPU table, measured on every rank's own GPU at
+        # once (untimed); a failure is reported, not fatal.
+        row = {"rank": ctx.rank, "local_rank": ctx.local_rank, "healthy": True, "mfma_ok": True,
+               "pci_bus_id": props.get("pciBusID")}
+        try:
+            row["hbm"] = pr.partition_table(ctx.local_rank)
+        except Exception as e:  # noqa: BLE001
+            row["hbm"] = {"error": f"{type(e).__name__}: {e}"}
+        probe_row = row
+    else:
+        probe_row = None
+    probe_rows = ctx.gather(probe_row)
+    if ctx.rank == 0 and any(probe_rows):
+        extras["gpu_probes"] = [r for r in probe_rows if r]
 
     from flex_gpu_scheduler_amd.utils.cpuaffinity import apply as pin_cpus, ranked_domains
 
@@ -203,7 +256,25 @@ def main() -> int:
     per_rank = ctx.gather(round(pods / t_rank, 1) if t_rank > 0 else 0.0)
     del waves, prepared
     stats = shard.sched.stats()
-    if ctx.rank == 0 and not args.no_open_loop:
+    if not args.no_placement and (ctx.distributed or ctx.cuda):
+        # Untimed: gangs placed on the live node, resolved by the device
+        # plugin, all-reduced on exactly those GPUs (parallel/placement.py).
+        # A failure there is reported, not fatal to the headline line. The
+        # last collective of the run: every rank takes part.
+        from flex_gpu_scheduler_amd.parallel.placement import validate_placement
+
+        try:
+            tables = {r["local_rank"]: r["hbm"] for r in probe_rows if r and "error" not in r.get("hbm", {})}
+            extras["rccl_placement"] = validate_placement(ctx, bandwidth_tables=tables)
+        except Exception as e:  # noqa: BLE001
+            extras["rccl_placement"] = {"error": f"{type(e).__name__}: {e}"}
+    ctx.barrier()
+    if ctx.rank != 0:
+        # Ranks > 0 are done: rank 0's untimed extras below run without them.
+        shard.close()
+        ctx.close()
+        return 0
+    if not args.no_open_loop:
         # Untimed: Poisson gang arrivals at 50% / 90% of this shard's measured
         # open-loop capacity, gang types interleaved, held then deleted
         # (utils/openloop.py) — admission latency rather than burst queueing.
@@ -220,36 +291,54 @@ def main() -> int:
             "capacity_search": search,
             **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed + 1)
                for f in (0.5, 0.9) if cap > 0}}
+        ol = extras["gang_admit_open_loop"]
+        extras["open_loop_capacity_pods_per_s"] = round(cap, 1)
+        l90 = ol.get("load_90") or {}
+        for k, v in (l90.get("by_gang") or {}).items():
+            extras[f"open_loop_p99_create_to_bound_ms_{k}"] = v["create_to_bound_ms"]["p99"]
+        if l90:
+            extras["open_loop_p999_create_to_bound_ms"] = l90["all_gangs"]["p999_create_to_bound_ms"]
+            extras["open_loop_max_create_to_bound_ms"] = l90["all_gangs"]["max_create_to_bound_ms"]
+        # Over every open-loop run of the search and the two loads.
+        runs = [*search, *(ol.get(f"load_{x}") for x in (50, 90) if ol.get(f"load_{x}"))]
+        n_g = sum(r["gangs"] for r in runs)
+        n_d = sum(r.get("denied_gangs", (r.get("denials") or {}).get("total", 0)) for r in runs)
+        extras["denied_gang_fraction"] = round(n_d / max(1, n_g), 6)
+        extras["parked_gang_fraction"] = round(sum(r.get("parked_gangs", 0) for r in runs) / max(1, n_g), 6)
     shard.close()
 
-    if not args.no_placement and (ctx.distributed or ctx.cuda):
-        # Untimed: gangs placed on the live node, resolved by the device
-        # plugin, all-reduced on exactly those GPUs (parallel/placement.py).
-        # A failure there is reported, not fatal to the headline line.
-        from flex_gpu_scheduler_amd.parallel.placement import validate_placement
-
+    if args.nodes1024_waves > 0:
+        # Untimed: the same workload on one 1,024-node shard (12k pods/wave).
         try:
-            extras["rccl_placement"] = validate_placement(ctx)
+            extras["nodes1024"] = run_nodes(1024, args.nodes1024_waves, args.seed, json.loads(args.sched_options))
+            extras["nodes1024_pods_per_s"] = extras["nodes1024"]["pods_per_s"]
         except Exception as e:  # noqa: BLE001
-            extras["rccl_placement"] = {"error": f"{type(e).__name__}: {e}"}
-    if ctx.rank == 0 and not args.no_service_mode:
+            extras["nodes1024"] = {"error": f"{type(e).__name__}: {e}"}
+    if not args.no_service_mode:
         # Untimed: the deployable shape — scheduler and API server in separate
-        # processes over loopback HTTP (tools/remote_bench.py).
+        # processes over loopback HTTP (tools/remote_bench.py): steady state
+        # (pods created over HTTP by other processes while it schedules), and
+        # drains of pre-created plain pods / 8-rank gangs for comparison.
         try:
-            from flex_gpu_scheduler_amd.tools.remote_bench import run as remote_run
+            from flex_gpu_scheduler_amd.tools.remote_bench import run as remote_run, run_steady
 
+            steady = run_steady(128, 2.0, 8)
             plain = remote_run(64, 4000, False, 16, 8)
             gang = remote_run(64, 512, True, 16, 8)
             extras["service_mode"] = {
                 "apiserver": "native HTTP/1.1 (csrc/apiserver), separate process, loopback",
-                "plain": {k: plain[k] for k in ("pods", "pods_per_s", "pods_per_s_after_sync", "sync_s", "bound")},
-                "gang8": {k: gang[k] for k in ("pods", "pods_per_s", "pods_per_s_after_sync", "sync_s", "bound")}}
-            extras["service_mode_pods_per_s"] = plain["pods_per_s"]
+                "steady": steady,
+                "drain_plain": {k: plain[k] for k in ("pods", "pods_per_s", "pods_per_s_after_sync", "sync_s",
+                                                      "bound")},
+                "drain_gang8": {k: gang[k] for k in ("pods", "pods_per_s", "pods_per_s_after_sync", "sync_s",
+                                                     "bound")}}
+            extras["service_mode_pods_per_s"] = steady["pods_per_s"]
+            extras["service_mode_offered_creates_per_s"] = steady["offered_creates_per_s"]
         except Exception as e:  # noqa: BLE001
             extras["service_mode"] = {"error": f"{type(e).__name__}: {e}"}
 
     value = pods_total / t_max if t_max > 0 else 0.0
-    if ctx.rank == 0 and not args.no_scenarios:
+    if not args.no_scenarios:
         # The five BASELINE.json configurations, each with its placement check
         # (outside the timed region; utils/scenarios.py).
         from flex_gpu_scheduler_amd.utils.scenarios import run_all
@@ -257,6 +346,9 @@ def main() -> int:
         extras["scenarios"] = run_all()
     if ctx.rank == 0:
         lat = gang_latency_summary(all_gangs)
+        by_type = gang_latency_summary(all_gangs, by_type=True)
+        for k, v in by_type.items():
+            extras[f"p99_gang_admit_ms_{k}"] = v["p99_ms"]
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -285,7 +377,7 @@ def main() -> int:
                              "spread": round((max(per_rank) - min(per_rank)) / max(1e-9, sum(per_rank) / len(per_rank)), 3)},
                 "p99_gang_admit_ms": {k: v["p99_ms"] for k, v in lat.items()},
                 "gang_admit": lat,
-                "gang_admit_by_type": gang_latency_summary(all_gangs, by_type=True),
+                "gang_admit_by_type": by_type,
                 "attempts": stats["attempts"],
                 "unschedulable_attempts": stats["unschedulable"],
                 "eq_cache_filter_hit_rate": round(stats["eq_filter_hits"] / max(1, stats["eq_filter_hits"] +

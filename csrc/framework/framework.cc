@@ -145,8 +145,10 @@ Framework::Framework(const ProfileConfig& cfg, Handle handle) : cfg_(cfg), handl
   auto bd = chain_.find(kBind);
   if (bd == chain_.end() || bd->second.empty())
     throw std::runtime_error("at least one bind plugin is needed for profile " + cfg_.scheduler_name);
-  for (const auto& p : all_)
+  for (const auto& p : all_) {
     for (const auto& k : p->watched_kinds()) kind_watchers_[k].push_back(p);
+    if (p->wants_capacity_events()) capacity_watchers_.push_back(p);
+  }
 }
 
 Framework::~Framework() = default;
@@ -745,6 +747,10 @@ std::vector<std::string> Framework::watched_kinds() const {
     for (const auto& k : p->watched_kinds())
       if (std::find(out.begin(), out.end(), k) == out.end()) out.push_back(k);
   return out;
+}
+
+void Framework::notify_capacity_freed() {
+  for (const auto& p : capacity_watchers_) p->capacity_freed();
 }
 
 void Framework::dispatch_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) {

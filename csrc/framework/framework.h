@@ -142,6 +142,8 @@ class Framework {
   std::vector<ClusterEvent> events_for(const std::string& plugin) const;
   std::vector<std::string> watched_kinds() const;
   void dispatch_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old);
+  // Resources were released on some node (Plugin::capacity_freed); any thread.
+  void notify_capacity_freed();
   void start();
   void stop();
 
@@ -158,6 +160,7 @@ class Framework {
   std::map<uint32_t, std::vector<PluginPtr>> chain_;
   std::vector<std::pair<PluginPtr, int64_t>> scorers_;
   std::unordered_map<std::string, std::vector<PluginPtr>> kind_watchers_;
+  std::vector<PluginPtr> capacity_watchers_;
   PluginPtr queue_sort_;
 };
 

@@ -86,6 +86,8 @@ struct Handle {
   // Coscheduling denied `member`'s group (`why`: postfilter | unreserve |
   // minresources); the scheduler keeps a diagnostic record. Optional.
   std::function<void(const Pod& member, const char* why)> gang_denied;
+  // Coscheduling parked `member`'s group (transient GPU shortage). Optional.
+  std::function<void(const Pod& member)> gang_parked;
   // Bracket a long wait inside a binding-cycle extension point (PreBind):
   // the binder pool adds a worker for the duration, so waiting pods cannot
   // starve the bindings of unrelated pods. Optional.
@@ -192,6 +194,12 @@ class Plugin {
   // e.g. CapacityScheduling's ElasticQuota infos, Trimaran's pod-assign cache).
   virtual void on_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr& old) {}
   virtual std::vector<std::string> watched_kinds() const { return {}; }
+  // Resources were released somewhere in the cluster: an assigned or assumed
+  // pod left a node, or a node joined or grew. Delivered (from informer and
+  // binder threads, so it must be cheap and thread-safe) to plugins whose
+  // wants_capacity_events() is true, e.g. Coscheduling re-probing parked gangs.
+  virtual bool wants_capacity_events() const { return false; }
+  virtual void capacity_freed() {}
   // Periodic work registered at start (metrics refresh, cache cleanup).
   virtual void start() {}
   virtual void stop() {}

@@ -321,12 +321,29 @@ struct Snapshot {
   // nodes[i]->gpu.free_xcds() and .part_mask(), contiguous likewise (XCD gangs).
   std::vector<int32_t> free_xcd;
   std::vector<uint8_t> part_mask;
-  void set_gpu_summary(size_t i) {
+  // Cluster totals of the two arrays above, kept in step by set_gpu_summary:
+  // free whole GPUs, and free XCDs per partition-size mask (Coscheduling's
+  // gang gate reads them per cycle without a pass over the nodes).
+  int64_t sum_free_whole = 0;
+  int64_t sum_free_xcd_by_mask[16] = {};
+  // `fresh`: the arrays were just resized for a rebuilt node list, so slot i
+  // holds nothing to subtract (reset_gpu_sums() ran first).
+  void set_gpu_summary(size_t i, bool fresh = false) {
     const GpuLedger& L = nodes[i]->gpu;
+    if (!fresh) {
+      sum_free_whole -= free_whole[i];
+      sum_free_xcd_by_mask[part_mask[i] & 15] -= free_xcd[i];
+    }
     gen[i] = nodes[i]->generation;
     free_whole[i] = L.free_gpus();
     free_xcd[i] = L.free_xcds();
     part_mask[i] = L.part_mask();
+    sum_free_whole += free_whole[i];
+    sum_free_xcd_by_mask[part_mask[i] & 15] += free_xcd[i];
+  }
+  void reset_gpu_sums() {
+    sum_free_whole = 0;
+    std::fill(std::begin(sum_free_xcd_by_mask), std::end(sum_free_xcd_by_mask), int64_t{0});
   }
   // Nodes with affinity / required anti-affinity pods, in no particular
   // order. Kept incrementally by the cache: *_pos[i] is node i's slot in the

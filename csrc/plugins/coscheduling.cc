@@ -13,7 +13,29 @@
 // Differences by design: assigned counts come from the cache's per-group
 // counter (O(1)) instead of a scan of every pod on every node; the TTL maps
 // are swept by the shared timer service.
+//
+// Deliberate deviation (arg transientShortage, default "Park";
+// docs/ARCHITECTURE.md §4, "Gang parking"): a gang of GPU ranks whose
+// remaining members do not fit the GPUs free right now is *parked* instead of
+// denied for deniedPGExpirationTimeSeconds:
+//  * PreFilter gate: before a member is placed, the GPUs (or XCD partitions)
+//    free in the cycle's snapshot, less those still owed to gangs already
+//    waiting at Permit and to the oldest parked gang, must cover the group's
+//    remaining members; otherwise the group parks (Unschedulable, nothing is
+//    assumed, so it holds no GPUs that other gangs wait for);
+//  * PostFilter: a member that fails Filter while the gate's arithmetic says
+//    the GPUs are short rejects its waiting siblings (releasing their GPUs)
+//    and parks the group instead of denying it;
+//  * every release of capacity (a pod deleted or forgotten, a node added)
+//    sends one probe member of the oldest parked group back to the active
+//    queue (skipping backoff); when its gate passes the group un-parks and the
+//    next parked group is probed.
+// Genuine shortfalls keep the reference's semantics: a group bigger than the
+// cluster's GPUs, a failure the GPU count does not explain (affinity,
+// fragmentation, CPU/memory) and Permit timeouts are denied for the TTL.
+// "Deny" restores the reference's behaviour everywhere.
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <unordered_map>
 
@@ -23,6 +45,7 @@
 #include "framework/waiting_pods.h"
 #include "scheduler/cache.h"
 #include "scheduler/informers.h"
+#include "scheduler/metrics.h"
 
 namespace xsched {
 namespace {
@@ -79,12 +102,17 @@ class Coscheduling : public Plugin {
         permitted_(h.clock) {
     permit_wait_us_ = args["permitWaitingTimeSeconds"].as_int(60) * 1000000;
     denied_ttl_us_ = args["deniedPGExpirationTimeSeconds"].as_int(20) * 1000000;
+    const std::string mode = args["transientShortage"].str_or("Park");
+    if (mode == "Park") park_ = true;
+    else if (mode == "Deny") park_ = false;
+    else throw std::runtime_error("Coscheduling transientShortage must be Park or Deny, not " + mode);
   }
 
   void start() override {
     sweep_id_ = h_.timers->every(3'000'000, [this] {
       denied_.sweep();
       permitted_.sweep();
+      sweep_outstanding();
     });
   }
   void stop() override {
@@ -139,6 +167,10 @@ class Coscheduling : public Plugin {
     if (static_cast<int64_t>(n) < pg->min_member)
       return Status::unresolvable("pre-filter pod " + p.name() + " cannot find enough sibling pods, current pods number: " +
                                   std::to_string(n) + ", minMember of group: " + std::to_string(pg->min_member));
+    if (park_) {
+      Status gs = gang_gate(p, *pg);
+      if (!gs.is_success()) return gs;
+    }
     if (!pg->has_min_resources) return {};
     if (permitted_.has(p.pg_key)) return {};
     Res need = pg->min_resources;
@@ -206,7 +238,16 @@ class Coscheduling : public Plugin {
     if (assigned >= pg->min_member) return {PostFilterResult{}, Status(Code::Unschedulable)};
     float gap = static_cast<float>(pg->min_member - assigned) / static_cast<float>(std::max(1, pg->min_member));
     if (gap <= 0.1f) return {PostFilterResult{}, Status(Code::Unschedulable)};
+    if (park_ && gpu_shortage_explains(p, *pg)) {
+      // Transient GPU shortage: release the siblings' GPUs, park the group.
+      park_rejecting(p, *pg);
+      permitted_.erase(p.pg_key);
+      return {PostFilterResult{}, XS_FIXED_STATUS(Code::Unschedulable,
+                                                  "PodGroup parked: its remaining members need more GPUs than are "
+                                                  "free; it retries when GPUs are released")};
+    }
     reject_group(p, "optimistic rejection in PostFilter");
+    drop_outstanding(p.pg_key);
     deny(p, "postfilter");
     permitted_.erase(p.pg_key);
     return {PostFilterResult{},
@@ -272,6 +313,14 @@ class Coscheduling : public Plugin {
       if (wpod.ns() == p.ns() && wpod.pod_group == p.pod_group) wp->reject(name(), msg);
     });
   }
+  int count_waiting(const Pod& p) {
+    int n = 0;
+    h_.waiting_pods->iterate_group(p.pg_key, [&](const WaitingPodPtr& wp) {
+      const Pod& wpod = *wp->pod();
+      n += wpod.ns() == p.ns() && wpod.pod_group == p.pod_group;
+    });
+    return n;
+  }
 
   // ---- Permit (coscheduling.go:184-216, core.go:199-216) ----
   std::pair<Status, int64_t> permit(CycleState& s, const PodPtr& p, const std::string&) override {
@@ -282,9 +331,11 @@ class Coscheduling : public Plugin {
     // equivalent to the reference's snapshot count + 1.
     int assigned = h_.cache->assigned_in_group(p->pg_key);
     if (assigned < pg->min_member) {
+      if (park_) note_outstanding(*p, pg->min_member - assigned);
       activate_siblings(*p, s);
       return {Status(Code::Wait), wait_time(*pg)};
     }
+    if (park_) drop_outstanding(p->pg_key);
     h_.waiting_pods->iterate_group(p->pg_key, [&](const WaitingPodPtr& wp) {
       const Pod& q = *wp->pod();  // flat group key first: no string build per waiting pod
       if (q.pg_key == p->pg_key && q.pod_group == p->pod_group && q.ns() == p->ns()) wp->allow(name());
@@ -307,7 +358,10 @@ class Coscheduling : public Plugin {
     if (p->pod_group.empty()) return;
     auto pg = h_.informers->pod_group_of(*p);
     if (!pg) return;
+    // A sibling rejected because its group parked (PostFilter): no denial.
+    if (park_ && consume_parked_reject(p->pg_key)) return;
     reject_group(*p, "rejection in Unreserve");
+    drop_outstanding(p->pg_key);
     deny(*p, "unreserve");
     permitted_.erase(p->pg_key);
   }
@@ -365,6 +419,22 @@ class Coscheduling : public Plugin {
       out.set("denied", Json(true));
       return out;
     }
+    if (what == "parking") {  // parked groups (oldest first) and GPUs owed to gangs at Permit
+      std::lock_guard<std::mutex> g(park_mu_);
+      Json groups = Json::array();
+      for (const auto& [k, pk] : parked_) {
+        Json e = Json::object();
+        e.set("podGroup", Json(pk.ns + "/" + pk.group));
+        e.set("kind", Json(pk.kind == GpuDemand::Gpu ? "gpu" : "xcd"));
+        e.set("need", Json(pk.need));
+        groups.push_back(std::move(e));
+      }
+      out.set("parked", std::move(groups));
+      out.set("outstandingGpus", Json(owed_[0]));
+      out.set("outstandingXcdMembers", Json(owed_[1]));
+      out.set("parksTotal", Json(static_cast<int64_t>(parks_total_)));
+      return out;
+    }
     return Plugin::debug_call(what, s, p, args);
   }
 
@@ -394,6 +464,302 @@ class Coscheduling : public Plugin {
   std::mutex patched_mu_;
   std::unordered_map<uint64_t, Patched> patched_;
   size_t patched_sweep_at_ = 8192;
+
+  // ---- Gang gate and parking ----
+  // Units: whole GPUs for GPU ranks, members for XCD-partition ranks (their
+  // footprint depends on the node's partition size).
+  static int kind_slot(GpuDemand::Kind k) { return k == GpuDemand::Gpu ? 0 : 1; }
+  static bool gated(const GpuDemand& d) {
+    return (d.kind == GpuDemand::Gpu || d.kind == GpuDemand::Xcd) && d.amount > 0;
+  }
+  static int64_t units_for(const GpuDemand& d, int64_t members) {
+    return d.kind == GpuDemand::Gpu ? members * d.amount : members;
+  }
+  // XCDs one member of `amount` XCDs occupies on a GPU with `xpp`-XCD partitions.
+  static int64_t footprint(int64_t amount, int64_t xpp) { return (amount + xpp - 1) / xpp * xpp; }
+  static int64_t footprint_for_mask(int64_t amount, int mask) {
+    int64_t per = 0;
+    for (int b = 0; b < 4; ++b)
+      if (mask & (1 << b)) {
+        const int64_t use = footprint(amount, int64_t{1} << b);
+        if (per == 0 || use < per) per = use;
+      }
+    return per;
+  }
+  // Free units in the cycle's snapshot (from its running totals: O(1) for GPU
+  // ranks, 16 terms for XCD ranks).
+  int64_t free_units(const GpuDemand& d) const {
+    const Snapshot& s = *h_.snapshot;
+    if (d.kind == GpuDemand::Gpu) return s.sum_free_whole / std::max<int64_t>(1, d.amount);
+    int64_t members = 0;
+    for (int m = 1; m < 16; ++m) {
+      const int64_t per = footprint_for_mask(d.amount, m);
+      if (per > 0) members += s.sum_free_xcd_by_mask[m] / per;
+    }
+    return members;
+  }
+  // Units the whole cluster could give this kind of rank if nothing ran.
+  // Partition modes are Node state, so the count is memoized per node epoch.
+  int64_t total_units(const GpuDemand& d) {
+    const Snapshot& s = *h_.snapshot;
+    const uint64_t tag = (static_cast<uint64_t>(d.kind) << 56) ^ static_cast<uint64_t>(d.amount);
+    if (total_memo_epoch_ == s.node_epoch && total_memo_nodes_ == s.nodes.size())
+      if (auto it = total_memo_.find(tag); it != total_memo_.end()) return it->second;
+    if (total_memo_epoch_ != s.node_epoch || total_memo_nodes_ != s.nodes.size()) {
+      total_memo_.clear();
+      total_memo_epoch_ = s.node_epoch;
+      total_memo_nodes_ = s.nodes.size();
+    }
+    return total_memo_[tag] = count_total_units(d);
+  }
+  int64_t count_total_units(const GpuDemand& d) const {
+    int64_t t = 0;
+    for (const auto& ni : h_.snapshot->nodes) {
+      const GpuLedger& L = ni->gpu;
+      for (int g = 0; g < L.gpu_count; ++g) {
+        if (d.kind == GpuDemand::Gpu) {
+          t += L.parts[g] == 1;
+        } else if (L.xcds_per_part(g) > 0) {
+          t += 8 / std::max<int64_t>(1, footprint(d.amount, L.xcds_per_part(g)));
+        }
+      }
+    }
+    return d.kind == GpuDemand::Gpu ? t / std::max<int64_t>(1, d.amount) : t;
+  }
+  struct Parked {
+    std::string ns, group;
+    GpuDemand::Kind kind = GpuDemand::None;
+    int64_t need = 0;  // units for the group's remaining members
+  };
+  using ParkKey = std::pair<MicroTime, uint64_t>;  // (PodGroup creation, pg_key): oldest first
+  // Gate verdict for p's group (scheduling thread, snapshot current): pass
+  // when the free units, less those owed to other gangs at Permit and to an
+  // older parked group, cover the remaining members. Parks the group on
+  // failure.
+  Status gang_gate(const Pod& p, const PodGroup& pg) {
+    const GpuDemand& d = p.gpu_demand;
+    if (!gated(d) || !h_.snapshot) return {};
+    const int assigned = h_.cache->assigned_in_group(p.pg_key);
+    const int64_t remaining = pg.min_member - assigned;
+    if (remaining <= 0) return {};
+    const int64_t need = units_for(d, remaining);
+    const int64_t free = free_units(d);
+    const int slot = kind_slot(d.kind);
+    std::vector<PodPtr> probe;
+    bool pass;
+    {
+      std::lock_guard<std::mutex> g(park_mu_);
+      if (parked_.empty() && owed_[slot] == 0 && free >= need) return {};  // common case
+      int64_t reserved = owed_[slot];
+      if (auto o = outstanding_.find(p.pg_key); o != outstanding_.end() && kind_slot(o->second.kind) == slot)
+        reserved -= o->second.units;
+      const ParkKey me{pg.meta.creation, p.pg_key};
+      auto pos = parked_pos_.find(p.pg_key);
+      // The oldest parked group of this kind holds a reservation against
+      // younger groups that have not started (so big gangs are not starved
+      // by a stream of small ones).
+      if (assigned == 0)
+        for (const auto& [k, pk] : parked_) {
+          if (!(k < me)) break;
+          if (kind_slot(pk.kind) == slot) {
+            reserved += pk.need;
+            break;
+          }
+        }
+      pass = free - reserved >= need;
+      if (p.pg_key == probe_key_) probe_key_ = 0;  // the probe's answer is in
+      if (pass) {
+        if (pos != parked_pos_.end()) {
+          parked_.erase(pos->second);
+          parked_pos_.erase(pos);
+          parked_n_.store(parked_.size(), std::memory_order_release);
+          // Chain: the next parked group may fit what is left.
+          probe = next_probe_locked();
+        }
+      }
+    }
+    if (!probe.empty()) h_.activate(probe);
+    if (pass) return {};
+    // The whole group can never fit: Filter fails and PostFilter denies (reference).
+    if (units_for(d, pg.min_member) > total_units(d)) return {};
+    // A group already part-placed releases what its waiting members hold (no
+    // hold-and-wait between gangs), as PostFilter's park does.
+    if (assigned > 0) park_rejecting(p, pg);
+    else park(p, pg, d.kind, need);
+    return XS_FIXED_STATUS(Code::Unschedulable,
+                           "PodGroup parked: its remaining members need more GPUs than are free; it retries when "
+                           "GPUs are released");
+  }
+  // PostFilter: does the gate's arithmetic (counting this member's own
+  // remaining group) explain the Filter failure?
+  bool gpu_shortage_explains(const Pod& p, const PodGroup& pg) {
+    const GpuDemand& d = p.gpu_demand;
+    if (!gated(d) || !h_.snapshot) return false;
+    const int assigned = h_.cache->assigned_in_group(p.pg_key);
+    const int64_t need_all = units_for(d, pg.min_member);
+    if (need_all > total_units(d)) return false;
+    const int64_t remaining = std::max<int64_t>(1, pg.min_member - assigned);
+    int64_t owed_others;
+    {
+      std::lock_guard<std::mutex> g(park_mu_);
+      owed_others = owed_[kind_slot(d.kind)];
+      if (auto o = outstanding_.find(p.pg_key); o != outstanding_.end() && kind_slot(o->second.kind) == kind_slot(d.kind))
+        owed_others -= o->second.units;
+    }
+    return free_units(d) - owed_others < units_for(d, remaining);
+  }
+  void park(const Pod& p, const PodGroup& pg, GpuDemand::Kind kind, int64_t need) {
+    std::lock_guard<std::mutex> g(park_mu_);
+    auto pos = parked_pos_.find(p.pg_key);
+    if (pos != parked_pos_.end()) {
+      parked_[pos->second].need = need;
+      return;
+    }
+    const ParkKey k{pg.meta.creation, p.pg_key};
+    Parked& pk = parked_[k];
+    pk.ns = p.ns();
+    pk.group = p.pod_group;
+    pk.kind = kind;
+    pk.need = need;
+    parked_pos_[p.pg_key] = k;
+    parked_n_.store(parked_.size(), std::memory_order_release);
+    ++parks_total_;
+    if (h_.metrics) h_.metrics->inc("xsched_coscheduling_parked_total", "");
+    if (h_.gang_parked) h_.gang_parked(p);
+  }
+  // PostFilter's park: the waiting siblings are rejected (their Unreserve
+  // must not deny the group), nothing stays owed, the group parks.
+  void park_rejecting(const Pod& p, const PodGroup& pg) {
+    const int n = count_waiting(p);
+    {
+      std::lock_guard<std::mutex> g(park_mu_);
+      if (n > 0) {
+        auto& r = parked_rejects_[p.pg_key];
+        r.first += n;
+        r.second = h_.clock->now_us();
+      }
+      erase_outstanding_locked(p.pg_key);
+    }
+    park(p, pg, p.gpu_demand.kind, units_for(p.gpu_demand, pg.min_member));
+    reject_group(p, "PodGroup parked in PostFilter: GPUs are short for its remaining members");
+  }
+  bool consume_parked_reject(uint64_t key) {
+    std::lock_guard<std::mutex> g(park_mu_);
+    if (!rejects_pending_locked(key)) return false;
+    auto it = parked_rejects_.find(key);
+    if (--it->second.first <= 0) parked_rejects_.erase(it);
+    return true;
+  }
+  // Rejections of a just-parked group still to land (a stale count, e.g. a
+  // sibling allowed or timed out between the count and the reject, expires).
+  bool rejects_pending_locked(uint64_t key) {
+    auto it = parked_rejects_.find(key);
+    if (it == parked_rejects_.end()) return false;
+    if (h_.clock->now_us() - it->second.second > kRejectWindowUs) {
+      parked_rejects_.erase(it);
+      return false;
+    }
+    return true;
+  }
+  // One member of the oldest parked group whose rejections have all landed
+  // (so its own GPUs are back), for the active queue. Caller holds park_mu_.
+  std::vector<PodPtr> next_probe_locked() {
+    std::vector<PodPtr> out;
+    while (!parked_.empty()) {
+      auto it = parked_.begin();
+      if (rejects_pending_locked(it->first.second)) return out;  // the last Unreserve probes
+      Pod member;
+      member.meta.ns = it->second.ns;
+      member.pod_group = it->second.group;
+      member.pg_key = it->first.second;
+      for (auto& q : h_.informers->pods_in_group_of(member))
+        if (q->node_name.empty() && !q->terminating()) {
+          out.push_back(std::move(q));
+          break;
+        }
+      if (!out.empty()) {
+        probe_key_ = it->first.second;
+        probe_sent_us_ = h_.clock->now_us();
+        return out;
+      }
+      parked_pos_.erase(it->first.second);  // nothing left to schedule: drop it
+      parked_.erase(it);
+      parked_n_.store(parked_.size(), std::memory_order_release);
+    }
+    return out;
+  }
+  bool wants_capacity_events() const override { return park_; }
+  void capacity_freed() override {
+    if (parked_n_.load(std::memory_order_acquire) == 0) return;
+    std::vector<PodPtr> probe;
+    {
+      std::lock_guard<std::mutex> g(park_mu_);
+      // One probe at a time: a probe still queued answers for this release
+      // too (its gate reads the snapshot of its own cycle, which includes it).
+      if (probe_key_ && h_.clock->now_us() - probe_sent_us_ < kProbeStaleUs) return;
+      probe = next_probe_locked();
+    }
+    if (!probe.empty()) h_.activate(probe);
+  }
+  struct Owed {
+    GpuDemand::Kind kind = GpuDemand::None;
+    int64_t units = 0;
+    int64_t at_us = 0;
+  };
+  void note_outstanding(const Pod& p, int64_t remaining) {
+    if (!gated(p.gpu_demand)) return;
+    std::lock_guard<std::mutex> g(park_mu_);
+    erase_outstanding_locked(p.pg_key);
+    Owed& o = outstanding_[p.pg_key];
+    o.kind = p.gpu_demand.kind;
+    o.units = units_for(p.gpu_demand, remaining);
+    o.at_us = h_.clock->now_us();
+    owed_[kind_slot(o.kind)] += o.units;
+  }
+  void drop_outstanding(uint64_t key) {
+    std::lock_guard<std::mutex> g(park_mu_);
+    erase_outstanding_locked(key);
+  }
+  void erase_outstanding_locked(uint64_t key) {
+    auto it = outstanding_.find(key);
+    if (it == outstanding_.end()) return;
+    owed_[kind_slot(it->second.kind)] -= it->second.units;
+    outstanding_.erase(it);
+  }
+  // Safety net: a gang whose Permit wait ended without reaching this plugin
+  // (e.g. its PodGroup vanished) stops being owed after the longest wait.
+  void sweep_outstanding() {
+    std::lock_guard<std::mutex> g(park_mu_);
+    const int64_t now = h_.clock->now_us();
+    for (auto it = outstanding_.begin(); it != outstanding_.end();) {
+      if (now - it->second.at_us > kMaxPermitUs) {
+        owed_[kind_slot(it->second.kind)] -= it->second.units;
+        it = outstanding_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    for (auto it = parked_rejects_.begin(); it != parked_rejects_.end();)
+      it = now - it->second.second > kRejectWindowUs ? parked_rejects_.erase(it) : std::next(it);
+  }
+  static constexpr int64_t kProbeStaleUs = 200'000;
+  static constexpr int64_t kRejectWindowUs = 1'000'000;
+  static constexpr int64_t kMaxPermitUs = 15LL * 60 * 1'000'000;  // framework cap
+  bool park_ = true;
+  // total_units memo (scheduling thread only).
+  std::unordered_map<uint64_t, int64_t> total_memo_;
+  uint64_t total_memo_epoch_ = 0;
+  size_t total_memo_nodes_ = 0;
+  std::mutex park_mu_;
+  std::map<ParkKey, Parked> parked_;
+  std::unordered_map<uint64_t, ParkKey> parked_pos_;
+  std::atomic<size_t> parked_n_{0};
+  std::unordered_map<uint64_t, std::pair<int, int64_t>> parked_rejects_;  // pg_key -> (Unreserves to absorb, when)
+  std::unordered_map<uint64_t, Owed> outstanding_;
+  int64_t owed_[2] = {0, 0};
+  uint64_t probe_key_ = 0;
+  int64_t probe_sent_us_ = 0;
+  uint64_t parks_total_ = 0;
 
   Handle& h_;
   TTLSet denied_, permitted_;

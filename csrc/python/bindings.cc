@@ -656,6 +656,7 @@ PYBIND11_MODULE(_xsched, m) {
             return py::make_tuple(total, out);
           },
           py::arg("clear") = false)
+      .def("gang_parks", [](Scheduler& s, bool clear) { return s.gang_parks(clear); }, py::arg("clear") = false)
       .def("queue_counts",
            [](Scheduler& s) {
              auto c = s.queue().counts();

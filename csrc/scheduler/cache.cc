@@ -404,7 +404,8 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
     s.free_whole.resize(s.nodes.size());
     s.free_xcd.resize(s.nodes.size());
     s.part_mask.resize(s.nodes.size());
-    for (size_t i = 0; i < s.nodes.size(); ++i) s.set_gpu_summary(i);
+    s.reset_gpu_sums();
+    for (size_t i = 0; i < s.nodes.size(); ++i) s.set_gpu_summary(i, /*fresh=*/true);
     s.have_pods_with_affinity.clear();
     s.have_pods_with_required_anti_affinity.clear();
     s.affinity_idx.clear();

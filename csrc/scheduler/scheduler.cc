@@ -259,6 +259,7 @@ SchedulerOptions SchedulerOptions::from_json(const Json& j) {
   o.trace = j["trace"].as_bool(false);
   o.seed = static_cast<uint64_t>(j["seed"].as_int(0));
   o.dump_on_fit_error = j["dumpOnFitError"].str_or("");
+  o.gang_denial_census = j["gangDenialCensus"].as_bool(false);
   return o;
 }
 
@@ -349,6 +350,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.timers = timers_.get();
     h.activate = [this](const std::vector<PodPtr>& pods) { queue_->activate(pods); };
     h.gang_denied = [this](const Pod& p, const char* why) { note_gang_denied(p, why); };
+    h.gang_parked = [this](const Pod&) { gang_parks_total_.fetch_add(1, std::memory_order_relaxed); };
     h.blocking_begin = [this] {
       if (binder_) binder_->enter_blocking();
     };
@@ -694,8 +696,13 @@ void Scheduler::forget_unassigned_pod(const Pod& p) {
     if (auto cached = cache_->get_pod(p.uid())) {
       cache_->forget_pod(*cached);
       queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+      capacity_freed();
     }
   }
+}
+
+void Scheduler::capacity_freed() {
+  for (auto& fw : frameworks_) fw->notify_capacity_freed();
 }
 
 void Scheduler::handle_pod_deletes(const WatchEvent* evs, size_t n) {
@@ -743,6 +750,7 @@ void Scheduler::handle_pod_deletes(const WatchEvent* evs, size_t n) {
   if (!assigned.empty()) {
     cache_->remove_pods(assigned);
     queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+    capacity_freed();
   }
   for (const auto& p : gone)
     if (p->node_name.empty()) forget_unassigned_pod(*p);
@@ -756,6 +764,7 @@ void Scheduler::handle_pod_event(const WatchEvent& ev) {
     if (!p->node_name.empty()) {
       cache_->remove_pod(*p);
       queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+      capacity_freed();
     } else {
       forget_unassigned_pod(*p);
     }
@@ -866,6 +875,7 @@ void Scheduler::handle_node_event(const WatchEvent& ev) {
   if (ev.type == EventType::Added || !ev.old) {
     cache_->add_node(n);
     queue_->move_all_to_active_or_backoff(ClusterEvent{"Node", kAdd, "NodeAdd"});
+    capacity_freed();
     return;
   }
   auto o = Node::from_json(*ev.old, *gpu_names_);
@@ -881,6 +891,7 @@ void Scheduler::handle_node_event(const WatchEvent& ev) {
         action |= kUpdateNodeTaint;
   if (o->meta.annotations != n->meta.annotations) action |= kUpdateNodeLabel;  // GPU topology annotation
   if (action) queue_->move_all_to_active_or_backoff(ClusterEvent{"Node", action, "NodeUpdate"});
+  if (action & kUpdateNodeAllocatable) capacity_freed();
 }
 
 // -------------------------------------------------------- gang tracking ----
@@ -966,7 +977,7 @@ void Scheduler::note_gang_denied(const Pod& p, const char* why) {
     d.cache_max_node_free = std::max(d.cache_max_node_free, r.free_whole);
     d.assumed_held += r.assumed_whole;
   }
-  if (store_) {
+  if (store_ && opts_.gang_denial_census) {
     std::unordered_map<std::string, int> used;
     const std::string& gpu = gpu_names_->gpu;
     for (const auto& po : store_->list("pods", "")) {
@@ -993,16 +1004,25 @@ void Scheduler::note_gang_denied(const Pod& p, const char* why) {
   // in the store are either truly taken by pods in flight (waiting at Permit
   // or being bound: not yet bound in the store) or seen as used only by a
   // cache that has not observed the deletions yet.
+  // Without the store census the cache alone separates GPUs held by pods in
+  // flight (assumed, not yet bound) from a shortage of bound pods.
   const int64_t missing = d.need_gpus * std::max(0, d.min_member - d.assigned);
-  const int64_t in_flight = d.waiting_at_permit + d.in_binding;
+  const int64_t in_flight = d.need_gpus * (d.waiting_at_permit + d.in_binding);  // GPUs, not pods
   if (d.need_gpus == 0) d.cause = "not_whole_gpu";
-  else if (d.store_free < 0) d.cause = "unknown";
+  else if (d.store_free < 0)
+    d.cause = d.cache_free >= missing ? "placement"
+              : d.cache_free + d.assumed_held >= missing ? "held_by_gangs_in_flight"
+                                                         : "capacity";
   else if (d.store_free < missing) d.cause = "capacity";
   else if (d.store_free - in_flight < missing) d.cause = "held_by_gangs_in_flight";
   else if (d.cache_free < missing) d.cause = "stale_cache";
   else d.cause = "placement";
   std::lock_guard<std::mutex> g(stats_mu_);
   if (gang_denials_.size() < kMaxGangDenials) gang_denials_.push_back(std::move(d));
+}
+
+uint64_t Scheduler::gang_parks(bool clear) {
+  return clear ? gang_parks_total_.exchange(0) : gang_parks_total_.load();
 }
 
 std::vector<GangDenial> Scheduler::gang_denials(bool clear, uint64_t* total) {
@@ -2229,6 +2249,7 @@ void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
     cache_->forget_pod(*assumed);
     // A forgotten pod frees resources: let waiting pods retry (AssignedPodDelete).
     queue_->move_all_to_active_or_backoff(ClusterEvent{"Pod", kDelete, "AssignedPodDelete"});
+    capacity_freed();
     {
       cnt_.bind_failures.fetch_add(1, std::memory_order_relaxed);
     }

@@ -145,6 +145,9 @@ struct SchedulerOptions {
   // Debugging: on the first fit error, write the cache and queue (the cache
   // debugger's dump) and the failing pod's diagnosis to this file.
   std::string dump_on_fit_error;
+  // Gang-denial records also list every bound pod from the store (the
+  // "stale_cache" cause); off by default: it costs O(pods) per denial.
+  bool gang_denial_census = false;
   static SchedulerOptions from_json(const Json& j);
 };
 
@@ -234,6 +237,8 @@ class Scheduler {
   // Group denials since the last clear (the first kMaxGangDenials with
   // their census; `total` counts all of them).
   std::vector<GangDenial> gang_denials(bool clear = false, uint64_t* total = nullptr);
+  // Groups Coscheduling parked (transient GPU shortage) since the last clear.
+  uint64_t gang_parks(bool clear = false);
   size_t inflight_bindings() const { return inflight_.load(); }
   size_t bind_threads() const { return binder_ ? binder_->threads() : 0; }
   // Seconds since the scheduling loop last ticked (it ticks at least every
@@ -313,6 +318,9 @@ class Scheduler {
   void handle_pod_deletes(const WatchEvent* evs, size_t n);
   PodPtr deleted_pod(const WatchEvent& ev);
   void forget_unassigned_pod(const Pod& p);
+  // Resources were released (pod deleted or forgotten, node added or grown):
+  // tells the plugins that asked (Plugin::capacity_freed).
+  void capacity_freed();
   void report_informer_error(const WatchEvent& ev, const char* what);
   void handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, PodPtr old);
   PodPtr bound_copy_of_assumed(const WatchEvent& ev);
@@ -433,6 +441,7 @@ class Scheduler {
   static constexpr size_t kMaxGangDenials = 256;
   std::vector<GangDenial> gang_denials_;
   uint64_t gang_denials_total_ = 0;
+  std::atomic<uint64_t> gang_parks_total_{0};
   std::unordered_map<std::string, std::string> last_condition_;  // uid -> last failure message
 };
 

@@ -546,6 +546,9 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv: list[str] | None = None) -> int:
+    from .utils.cpuaffinity import adopt_child_cpus
+
+    adopt_child_cpus()  # started by a pinned benchmark shard: stay off its CPUs
     args = build_parser().parse_args(argv)
     _setup_logging(args.verbosity, args.logging_format)
     return int(args.fn(args) or 0)

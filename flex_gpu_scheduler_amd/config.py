@@ -298,7 +298,11 @@ def default_plugin_args(name: str, args: dict | None) -> dict:
     """Apply SetDefaults_<Name>Args (apis/config/v1beta2/defaults.go)."""
     a = copy.deepcopy(args or {})
     if name == "Coscheduling":
-        _strict(name, a, {"permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds"})
+        # transientShortage (Park | Deny) is this framework's extension (the
+        # native plugin defaults it to Park; docs/ARCHITECTURE.md §4).
+        _strict(name, a, {"permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds", "transientShortage"})
+        if a.get("transientShortage", "Park") not in ("Park", "Deny"):
+            raise ConfigError(f"{name}Args.transientShortage must be Park or Deny, got {a['transientShortage']!r}")
         a.setdefault("permitWaitingTimeSeconds", 60)
         a.setdefault("deniedPGExpirationTimeSeconds", 20)
         for k in ("permitWaitingTimeSeconds", "deniedPGExpirationTimeSeconds"):

@@ -60,6 +60,11 @@ class NodeAgent:
         # partition_table): measured once per GPU and published with the node.
         self.bandwidth_fn = bandwidth_fn
         self.bandwidth: dict[int, dict] = {}
+        # A GPU whose probe failed is not probed again on every heartbeat
+        # (each attempt streams GiBs through a GPU that may be serving
+        # tenants): GPU index -> time.monotonic() of the next attempt.
+        self.bandwidth_retry_s = 600.0
+        self._bandwidth_retry_at: dict[int, float] = {}
         self.publish_metrics = publish_metrics
         self._sampler = sampler
         self._root = root
@@ -99,13 +104,19 @@ class NodeAgent:
             return
         visible = sorted((g for g in host.gpus if g.kfd_node is not None), key=lambda g: g.kfd_node)
         targets = [(i, g) for i, g in enumerate(visible)] if visible else [(g.index, g) for g in host.gpus]
+        now = time.monotonic()
         for ordinal, g in targets:
             if g.index in self.bandwidth or g.index in self.unhealthy:
                 continue
+            if now < self._bandwidth_retry_at.get(g.index, 0.0):
+                continue
             try:
                 self.bandwidth[g.index] = self.bandwidth_fn(ordinal)
+                self._bandwidth_retry_at.pop(g.index, None)
             except Exception as e:  # noqa: BLE001
-                log.warning("bandwidth probe GPU %d failed: %s", g.index, e)
+                log.warning("bandwidth probe GPU %d failed (next try in %.0f s): %s", g.index,
+                            self.bandwidth_retry_s, e)
+                self._bandwidth_retry_at[g.index] = now + self.bandwidth_retry_s
 
     def build_node(self, host: HostInfo, unhealthy: set[int] = frozenset()) -> dict:
         healthy = [g for g in host.gpus if g.index not in unhealthy]

@@ -28,6 +28,14 @@ Each gang is measured next to deliberately bad placements of the same size:
   * `host_staged`: the placed ranks reduced through host memory over TCP
     (gloo), the path a gang split across nodes without GPU-direct RDMA gets.
 
+Each multi-rank row is judged against an expected-bandwidth model built from
+the discovered KFD io_links (`busbw_model`): a ring all-reduce on a full mesh
+drives, per rank, the direct xGMI links to the other members of its gang, so
+the model is  min over ranks of (sum of those links' one-way bandwidth) x
+RING_EFFICIENCY. `verdict` is "pass" when the placed gang reaches at least
+PASS_FRACTION of the model and beats the host-staged path, "fail" otherwise,
+and "n/a" where no xGMI model applies (one GPU, or a gloo/CPU rehearsal).
+
 Everything runs outside the bench's timed region. On a CPU-only host (tests)
 the node comes from `fake_host` and the collectives run on gloo.
 """
@@ -43,6 +51,76 @@ from dataclasses import asdict, dataclass, field
 GANG_SIZES = (1, 2, 4, 8)
 NODE = "mi355x-live"
 NAMESPACE = "placement"
+
+# MI355X Infinity Fabric: 7 xGMI links per GPU, 153.6 GB/s per link counting
+# both directions (1,075 GB/s aggregate). Used when KFD reports no plausible
+# per-link bandwidth (its io_links max_bandwidth is in MB/s).
+XGMI_LINK_GBPS_BIDIR = 153.6
+# Fraction of the links' one-way bandwidth a large ring all-reduce turns into
+# bus bandwidth (protocol, reduction and scheduling overheads).
+RING_EFFICIENCY = 0.75
+PASS_FRACTION = 0.7
+
+
+def busbw_model(host, gpu_index: list[int]) -> dict:
+    """Expected all-reduce bus bandwidth (GB/s) for a gang on these host GPUs,
+    from the KFD xGMI io_links: each rank can drive its direct links to the
+    other members, the slowest rank bounds the ring."""
+    if len(gpu_index) < 2:
+        return {"model_busbw_GBps": None, "why": "single rank"}
+    by_index = {g.index: g for g in host.gpus}
+    kfd_to_index = {g.kfd_node: g.index for g in host.gpus if g.kfd_node is not None}
+    members = set(gpu_index)
+    per_rank = []
+    source = "kfd io_links"
+    for i in gpu_index:
+        g = by_index.get(i)
+        if g is None:
+            return {"model_busbw_GBps": None, "why": f"GPU {i} not discovered"}
+        oneway = 0.0
+        links = 0
+        for lk in g.xgmi_links:
+            peer = kfd_to_index.get(lk.peer_node, lk.peer_node if not kfd_to_index else None)
+            if peer is None or peer == i or peer not in members:
+                continue
+            links += 1
+            gbps = lk.bandwidth_mbps / 1000.0
+            if not 20.0 <= gbps <= 400.0:  # no usable per-link figure: the part's spec
+                gbps = XGMI_LINK_GBPS_BIDIR
+                source = "kfd io_links (topology) + MI355X link spec (bandwidth)"
+            oneway += gbps / 2.0
+        per_rank.append((links, oneway))
+    min_links = min(n for n, _ in per_rank)
+    if min_links == 0:
+        return {"model_busbw_GBps": None, "why": "some rank has no direct xGMI link to the gang", "direct_links": 0}
+    oneway = min(b for _, b in per_rank)
+    return {"model_busbw_GBps": round(RING_EFFICIENCY * oneway, 1), "direct_links_min": min_links,
+            "links_oneway_GBps": round(oneway, 1), "ring_efficiency": RING_EFFICIENCY, "source": source}
+
+
+def judge_row(row: dict, model: dict, backend: str) -> dict:
+    """Verdict fields for one gang row (see the module docstring)."""
+    out = {"model": model}
+    largest = lambda k: (row[k]["results"][-1]["busbw_GBps"]  # noqa: E731
+                         if k in row and "results" in row[k] and row[k]["results"] else None)
+    placed, staged, cross = largest("placed"), largest("host_staged"), largest("cross_socket")
+    out["placed_busbw_GBps"] = placed
+    out["host_staged_busbw_GBps"] = staged
+    out["cross_socket_over_placed"] = round(cross / placed, 3) if cross and placed else None
+    m = model.get("model_busbw_GBps")
+    if backend != "nccl" or m is None or placed is None:
+        out["verdict"] = "n/a"
+        out["why"] = ("no xGMI data plane (gloo/CPU run)" if backend != "nccl" else
+                      model.get("why") or "no placed measurement")
+        return out
+    out["placed_over_model"] = round(placed / m, 3)
+    checks = {"placed_ge_%.0f%%_of_model" % (PASS_FRACTION * 100): placed >= PASS_FRACTION * m,
+              "placed_ge_host_staged": staged is None or placed >= staged,
+              "all_correct": all(x["correct"] for k in ("placed", "cross_socket", "host_staged")
+                                 if k in row and "results" in row[k] for x in row[k]["results"])}
+    out["checks"] = checks
+    out["verdict"] = "pass" if all(checks.values()) else "fail"
+    return out
 
 
 @dataclass
@@ -98,9 +176,12 @@ def _allocate_rpc(plugin, sock: str, n: int):
         return call(req, timeout=10)
 
 
-def plan_gangs(host, ordinal_of: dict[int, int], sizes=GANG_SIZES, timeout: float = 30.0) -> dict:
+def plan_gangs(host, ordinal_of: dict[int, int], sizes=GANG_SIZES, timeout: float = 30.0,
+               bandwidth_tables: dict[int, dict] | None = None) -> dict:
     """Schedule one PodGroup per size on the live node and resolve each rank
-    through the device plugin. Returns {"plans": [...], "node": {...}}."""
+    through the device plugin. `bandwidth_tables` (HIP ordinal -> the rank's
+    partition table) are published on the Node by the node agent, one per
+    GPU. Returns {"plans": [...], "node": {...}}."""
     from ..config import load_config
     from ..control.client import LocalClient
     from ..control.device_plugin import ASSIGNED_ANNOTATION, GpuDevicePlugin
@@ -113,6 +194,9 @@ def plan_gangs(host, ordinal_of: dict[int, int], sizes=GANG_SIZES, timeout: floa
     store = Store()
     client = LocalClient(store)
     agent = NodeAgent(client, NODE, host_fn=lambda: host, publish_metrics=False)
+    for idx, o in ordinal_of.items():
+        if bandwidth_tables and o in bandwidth_tables:
+            agent.bandwidth[idx] = bandwidth_tables[o]
     agent.sync()
     held = sorted(ordinal_of)
     by_card = {}
@@ -189,7 +273,10 @@ def plan_gangs(host, ordinal_of: dict[int, int], sizes=GANG_SIZES, timeout: floa
         sched.stop()
     return {"plans": plans, "node": {"gpus": len(host.gpus), "held": len(held),
                                      "sockets": sorted({g.numa for g in host.gpus}),
-                                     "xgmi_links": [len(g.xgmi_links) for g in host.gpus]}}
+                                     "xgmi_links": [len(g.xgmi_links) for g in host.gpus],
+                                     "xgmi_link_max_bandwidth_mbps": sorted({lk.bandwidth_mbps for g in host.gpus
+                                                                             for lk in g.xgmi_links}),
+                                     "bandwidth_tables_published": len(agent.bandwidth)}}
 
 
 def _cross_socket(plan: GangPlan, ordinal_of: dict[int, int], socket_of: dict[int, int]) -> list[int]:
@@ -258,7 +345,8 @@ def _reduce_bw(group, members: list[int], rank: int, nbytes: int, cuda: bool, it
 
 
 def validate_placement(ctx, sizes=GANG_SIZES, rccl_mib=(16, 256), staged_mib=(16,), iters: int = 10,
-                       warmup: int = 3, root: str = "/", group_timeout_s: float = 120.0) -> dict:
+                       warmup: int = 3, root: str = "/", group_timeout_s: float = 120.0,
+                       bandwidth_tables: dict[int, dict] | None = None) -> dict:
     """Collective over all ranks of `ctx` (parallel/dist.py DistContext).
     Rank 0 plans (discovery -> scheduler -> Allocate), every rank joins the
     sub-communicators; rank 0 returns the table, other ranks return {}."""
@@ -276,9 +364,10 @@ def validate_placement(ctx, sizes=GANG_SIZES, rccl_mib=(16, 256), staged_mib=(16
             else:
                 source = "live sysfs/KFD" if ctx.cuda else "fake_host (CPU run)"
             ordinal_of = local_ordinals(host, ctx.world_size, ctx.cuda)
-            res = plan_gangs(host, ordinal_of, sizes)
+            res = plan_gangs(host, ordinal_of, sizes, bandwidth_tables=bandwidth_tables)
             plan_doc = {"source": source, "node": res["node"], "plans": [asdict(p) for p in res["plans"]],
-                        "ordinal_of": {str(k): v for k, v in ordinal_of.items()}}
+                        "ordinal_of": {str(k): v for k, v in ordinal_of.items()},
+                        "models": {str(p.size): busbw_model(host, p.gpu_index) for p in res["plans"]}}
         except Exception as e:  # noqa: BLE001 - reported, and every rank skips the data plane
             plan_doc = {"error": f"{type(e).__name__}: {e}"}
     if ctx.distributed:
@@ -340,12 +429,17 @@ def validate_placement(ctx, sizes=GANG_SIZES, rccl_mib=(16, 256), staged_mib=(16
         return {}
     summary = {}
     for r in rows:
+        model = plan_doc.get("models", {}).get(str(r["gang"]), {"model_busbw_GBps": None, "why": "no model"})
+        r.update(judge_row(r, model, backend))
         if "placed" not in r:
+            summary[str(r["gang"])] = {"verdict": r["verdict"], "why": r.get("why")}
             continue
         kinds = [k for k in ("placed", "cross_socket", "host_staged") if k in r]
         s = {k: ({str(x["MiB"]): x["busbw_GBps"] for x in r[k]["results"]} if "results" in r[k]
                  else {"error": r[k]["error"]}) for k in kinds}
         s["all_correct"] = all("results" in r[k] and all(x["correct"] for x in r[k]["results"]) for k in kinds)
+        s["model_busbw_GBps"] = model.get("model_busbw_GBps")
+        s["verdict"] = r["verdict"]
         summary[str(r["gang"])] = s
     return {"source": plan_doc["source"], "backend": backend, "node": plan_doc["node"], "gangs": rows,
             "summary": summary, "env": {"HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")}}

@@ -11,11 +11,19 @@ the pods mirrored, attempted, bound). The API server's HTTP front end is the
 native one (csrc/apiserver) unless --python-http.
 
     python -m flex_gpu_scheduler_amd.tools.remote_bench [--nodes 128] [--pods 8000] [--gangs] [--matrix]
+    python -m flex_gpu_scheduler_amd.tools.remote_bench --steady [--duration 2] [--creators 8]
+
+`--steady` (run_steady) is the steady-state form: the scheduler is synced
+first, then separate creator processes POST pods over HTTP for `duration`
+seconds while it schedules them; the rate is the bindings completed per
+second over the window that excludes the first quarter second, with the
+offered create rate and the backlog next to it.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import os
 import subprocess
 import sys
 import time
@@ -45,11 +53,12 @@ def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, nat
     from ..control import RestClient
     from ..control.remote import RemoteScheduler
     from ..models import GPU, make_pod, make_pod_group, mi355x_node
+    from ..utils.cpuaffinity import child_env
     from ..utils.workload import flagship_config
 
     srv = subprocess.Popen([sys.executable, "-m", "flex_gpu_scheduler_amd.cli", "apiserver", "--port", "0",
                             "--bind-address", "127.0.0.1"] + ([] if native_http else ["--python-http"]),
-                           stdout=subprocess.PIPE, text=True)
+                           stdout=subprocess.PIPE, text=True, env=child_env())
     try:
         url = json.loads(srv.stdout.readline())["apiserver"]
         admin = RestClient(url)
@@ -126,6 +135,110 @@ def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, nat
         srv.wait(10)
 
 
+def _creator(url: str, prefix: str, duration_s: float, out_fd: int) -> None:
+    """One creator process: POST plain pods over one keep-alive connection
+    for `duration_s` seconds; writes {"created", "t0", "t1"} (monotonic)."""
+    import http.client
+    import socket
+    from urllib.parse import urlsplit
+
+    from ..models import make_pod
+    from ..utils.cpuaffinity import adopt_child_cpus
+
+    adopt_child_cpus()
+    u = urlsplit(url)
+    conn = http.client.HTTPConnection(u.hostname, u.port)
+    conn.connect()
+    conn.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    path = "/api/v1/namespaces/default/pods"
+    hdr = {"Content-Type": "application/json", "Accept": "application/json"}
+    tmpl = json.dumps(make_pod("NAME", requests={"cpu": "100m", "memory": "128Mi"}), separators=(",", ":"))
+    i = 0
+    t0 = time.monotonic()
+    end = t0 + duration_s
+    while time.monotonic() < end:
+        conn.request("POST", path, body=tmpl.replace('"NAME"', f'"{prefix}-{i}"', 1).encode(), headers=hdr)
+        r = conn.getresponse()
+        r.read()
+        if r.status not in (200, 201):
+            raise SystemExit(f"create failed: {r.status}")
+        i += 1
+    os.write(out_fd, json.dumps({"created": i, "t0": t0, "t1": time.monotonic()}).encode())
+
+
+def run_steady(nodes: int = 128, duration_s: float = 2.0, creators: int = 8, bind_workers: int = 16,
+               warm_s: float = 0.25) -> dict:
+    """Steady-state service mode: pods are created over HTTP by `creators`
+    separate processes while the (already synced) scheduler binds them."""
+    from ..config import load_config
+    from ..control import RestClient
+    from ..control.remote import RemoteScheduler
+    from ..models import mi355x_node
+    from ..utils.cpuaffinity import child_env
+    from ..utils.workload import flagship_config
+
+    srv = subprocess.Popen([sys.executable, "-m", "flex_gpu_scheduler_amd.cli", "apiserver", "--port", "0",
+                            "--bind-address", "127.0.0.1"], stdout=subprocess.PIPE, text=True, env=child_env())
+    procs: list[tuple[subprocess.Popen, int]] = []
+    try:
+        url = json.loads(srv.stdout.readline())["apiserver"]
+        admin = RestClient(url)
+        for i in range(nodes):  # room for every pod of the window (2,000 per node)
+            admin.create("nodes", mi355x_node(f"mi-{i}", pods=2000))
+        rs = RemoteScheduler(RestClient(url), load_config(flagship_config()), bindWorkers=bind_workers).start()
+        try:
+            code = ("import sys; from flex_gpu_scheduler_amd.tools.remote_bench import _creator; "
+                    "_creator(sys.argv[1], sys.argv[2], float(sys.argv[3]), 1)")
+            root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            env = child_env()
+            env["PYTHONPATH"] = root + os.pathsep + os.environ.get("PYTHONPATH", "")
+            base = rs.scheduler.stats()["bound"]
+            t_start = time.monotonic()
+            for c in range(creators):
+                p = subprocess.Popen([sys.executable, "-c", code, url, f"c{c}", str(duration_s)],
+                                     stdout=subprocess.PIPE, env=env)
+                procs.append((p, c))
+            samples = []  # (t, bound) every ~5 ms
+            while any(p.poll() is None for p, _ in procs):
+                samples.append((time.monotonic(), rs.scheduler.stats()["bound"] - base))
+                time.sleep(0.005)
+            made = []
+            for p, _ in procs:
+                out, _ = p.communicate(timeout=30)
+                if p.returncode != 0:
+                    raise RuntimeError(f"creator exited {p.returncode}")
+                made.append(json.loads(out))
+            created = sum(m["created"] for m in made)
+            t_first = min(m["t0"] for m in made)
+            t_last = max(m["t1"] for m in made)
+            deadline = time.monotonic() + 60
+            while rs.scheduler.stats()["bound"] - base < created and time.monotonic() < deadline:
+                time.sleep(0.002)
+            t_drained = time.monotonic()
+            bound = rs.scheduler.stats()["bound"] - base
+            # Steady window: from warm_s after the first create to the last one.
+            w0, w1 = t_first + warm_s, t_last
+            inwin = [(t, b) for t, b in samples if w0 <= t <= w1]
+            rate = (inwin[-1][1] - inwin[0][1]) / (inwin[-1][0] - inwin[0][0]) if len(inwin) >= 2 else 0.0
+            at_end = next((b for t, b in reversed(samples) if t <= t_last), 0)
+            return {"nodes": nodes, "creators": creators, "duration_s": duration_s,
+                    "created": created, "bound": bound, "all_bound": bound >= created,
+                    "offered_creates_per_s": round(created / max(1e-9, t_last - t_first), 1),
+                    "pods_per_s": round(rate, 1),
+                    "window_s": round(max(0.0, w1 - w0), 3),
+                    "backlog_at_last_create": created - at_end,
+                    "drain_after_last_create_s": round(t_drained - t_last, 4),
+                    "start_delay_s": round(t_first - t_start, 3)}
+        finally:
+            rs.stop()
+    finally:
+        for p, _ in procs:
+            if p.poll() is None:
+                p.kill()
+        srv.terminate()
+        srv.wait(10)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--nodes", type=int, default=128)
@@ -135,9 +248,15 @@ def main() -> int:
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--python-io", action="store_true", help="Python mirror and writer instead of the native ones")
     ap.add_argument("--python-http", action="store_true", help="the API server's http.server front end")
+    ap.add_argument("--steady", action="store_true", help="steady-state: creates over HTTP while scheduling")
+    ap.add_argument("--duration", type=float, default=2.0)
+    ap.add_argument("--creators", type=int, default=8)
     ap.add_argument("--matrix", action="store_true",
                     help="plain and 8-rank gang runs, native and Python API server front ends")
     a = ap.parse_args()
+    if a.steady:
+        print(json.dumps(run_steady(a.nodes, a.duration, a.creators, a.bind_workers)), flush=True)
+        return 0
     if a.matrix:
         for native_http in (True, False):
             for g, n in ((False, a.pods), (True, min(a.pods, a.nodes * 8))):

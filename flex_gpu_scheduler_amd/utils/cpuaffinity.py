@@ -104,10 +104,43 @@ def pick(mode: str, rank: int = 0, window_s: float = 0.1, order: list[list[int]]
     return sorted(chosen)
 
 
+_original: set[int] | None = None  # the affinity before apply() pinned the shard
+_pinned: list[int] | None = None
+
+# Child processes that must not share the shard's CPUs (the service-mode API
+# server, load generators) read their CPU list from this variable at start.
+CHILD_ENV = "XSCHED_CHILD_CPUS"
+
+
 def apply(mode: str, rank: int = 0, order: list[list[int]] | None = None) -> list[int] | None:
     """Pin the calling thread (and every thread it creates afterwards, i.e.
     the scheduler's) to `pick(mode, rank)`. Returns the CPU list or None."""
+    global _original, _pinned
     cpus = pick(mode, rank, order=order)
     if cpus:
+        if _original is None:
+            _original = set(os.sched_getaffinity(0))
         os.sched_setaffinity(0, cpus)
+        _pinned = cpus
     return cpus
+
+
+def child_env(env: dict | None = None) -> dict:
+    """`env` (default os.environ) plus CHILD_ENV naming the CPUs this process
+    could use before its shard was pinned, minus the shard's own CPUs (all of
+    them if nothing was pinned or nothing else is left)."""
+    out = dict(os.environ if env is None else env)
+    if _original and _pinned:
+        rest = sorted(_original - set(_pinned)) or sorted(_original)
+        out[CHILD_ENV] = ",".join(map(str, rest))
+    return out
+
+
+def adopt_child_cpus() -> None:
+    """In a child process: take the CPU list CHILD_ENV names, if any."""
+    v = os.environ.get(CHILD_ENV)
+    if v:
+        try:
+            os.sched_setaffinity(0, _parse_list(v))
+        except OSError:
+            pass

@@ -68,8 +68,13 @@ def plan(spec: ClusterSpec, rate_pods_per_s: float, duration_s: float, seed: int
 
 def _pct(xs: list[float]) -> dict:
     if not xs:
-        return {"p50": None, "p99": None}
-    return {"p50": round(percentile(xs, 50), 3), "p99": round(percentile(xs, 99), 3)}
+        return {"p50": None, "p99": None, "p999": None, "max": None}
+    return {"p50": round(percentile(xs, 50), 3), "p99": round(percentile(xs, 99), 3),
+            "p999": round(percentile(xs, 99.9), 3), "max": round(max(xs), 3)}
+
+
+def _ms(v: float | None):
+    return None if v is None else (round(v, 3) if v != float("inf") else "inf")
 
 
 def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -> dict:
@@ -86,12 +91,12 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
     # Over every gang, an unbound one counting as infinitely late (the
     # capacity criterion of open_loop_capacity).
     c2b_all = sorted((g["bound_us"] - g["create_us"]) / 1e3 if g["bound_us"] else float("inf") for g in gangs)
-    p99_all = percentile(c2b_all, 99) if c2b_all else None
     n = len(gangs)
     return {"by_gang": out, "gangs": n, "wall_s": round(wall_us / 1e6, 3),
             "all_gangs": {"n": n, "unbound": sum(1 for g in gangs if not g["bound_us"]),
-                          "p99_create_to_bound_ms": None if p99_all is None else
-                          (round(p99_all, 3) if p99_all != float("inf") else "inf")},
+                          "p99_create_to_bound_ms": _ms(percentile(c2b_all, 99) if c2b_all else None),
+                          "p999_create_to_bound_ms": _ms(percentile(c2b_all, 99.9) if c2b_all else None),
+                          "max_create_to_bound_ms": _ms(c2b_all[-1] if c2b_all else None)},
             "mean_arrival_lag_us": round(late_us / max(1, n), 1)}
 
 
@@ -107,13 +112,14 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     held at `occupancy` of the SPX GPUs, as in the measured loads.
 
     One trial per rate, its arrival seed fixed by `seed`, no retries. Every
-    trial is appended to `log` with its Coscheduling denials and their causes
-    (Scheduler::note_gang_denied): near capacity the hold time (a few ms)
-    is comparable to the admission pipeline, GPUs held by gangs in flight
-    push the SPX pool to full, and a member that finds it full gets its
-    whole group denied for the TTL (the reference's PostFilter). One such
-    gang is < 1% of a run; the round-3 rule (every gang bound, wall time
-    within 1.2x) made one draw decide the capacity."""
+    trial is appended to `log` with its parked gangs, its Coscheduling
+    denials and their causes (Scheduler::note_gang_denied), p99.9 and max.
+    Near capacity the hold time (a few ms) is comparable to the admission
+    pipeline and GPUs held by gangs in flight push the SPX pool to full: a
+    gang that finds it full parks until GPUs are released (Coscheduling
+    transientShortage=Park) rather than being denied for the TTL as the
+    reference's PostFilter does (which made a rate fail on < 1% of its
+    gangs waiting 3 s)."""
     def served(rate: float) -> bool:
         r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=occupancy)
         p99 = r["all_gangs"]["p99_create_to_bound_ms"]
@@ -121,7 +127,10 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
         if log is not None:
             log.append({"offered_pods_per_s": round(rate, 1), "served": ok, "gangs": r["gangs"],
                         "unbound_gangs": r["all_gangs"]["unbound"], "p99_create_to_bound_ms": p99,
+                        "p999_create_to_bound_ms": r["all_gangs"]["p999_create_to_bound_ms"],
+                        "max_create_to_bound_ms": r["all_gangs"]["max_create_to_bound_ms"],
                         "wall_s": r["wall_s"], "denied_gangs": r["denials"]["total"],
+                        "denied_gang_fraction": r["denied_gang_fraction"], "parked_gangs": r["parked_gangs"],
                         "denial_causes": r["denials"]["causes"]})
         return ok
 
@@ -174,10 +183,15 @@ def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: 
     gangs, kinds, offsets, hold_us = plan(shard.spec, rate_pods_per_s, duration_s, seed, occupancy=occupancy,
                                           tag=f"{_runs}r")
     shard.sched.gang_denials(True)
+    shard.sched.gang_parks(True)
     res = native().run_open_loop(shard.store, shard.sched, json.dumps(gangs), offsets, hold_us, 10_000_000)
     shard.sched.wait_idle(10_000)
     out = summarize(kinds, res["gangs"], res["wall_us"], res["late_us"])
     out["denials"] = denial_summary(*shard.sched.gang_denials(True))
+    # Parked groups (Coscheduling transientShortage=Park): waited for GPUs to
+    # be released instead of being denied for deniedPGExpirationTimeSeconds.
+    out["parked_gangs"] = int(shard.sched.gang_parks(True))
+    out["denied_gang_fraction"] = round(out["denials"]["total"] / max(1, len(res["gangs"])), 5)
     n = max(1, len(res["gangs"]))
     out.update({"mean_delete_lag_us": round(res.get("delete_late_us", 0) / n, 1),
                 "max_in_flight_pods": res.get("max_in_flight_pods"), "max_held_pods": res.get("max_held_pods")})

@@ -153,9 +153,11 @@ def make_wave(spec: ClusterSpec, step: int, *, namespace: str = "bench", fill: f
     return w
 
 
-def flagship_config(permit_wait_s: int = 10, denied_s: int = 3) -> dict:
+def flagship_config(permit_wait_s: int = 10, denied_s: int = 3, transient_shortage: str = "Park") -> dict:
     """KubeSchedulerConfiguration of the benchmark: Coscheduling gangs +
-    FlexGPU MI355X packing (FlexGPU binds) + NRT xGMI gang placement."""
+    FlexGPU MI355X packing (FlexGPU binds) + NRT xGMI gang placement.
+    `transient_shortage`: "Park" (gangs short of free GPUs wait for a
+    release) or "Deny" (the reference: denied for `denied_s`)."""
     return {
         "apiVersion": "kubescheduler.config.k8s.io/v1beta3",
         "kind": "KubeSchedulerConfiguration",
@@ -176,7 +178,8 @@ def flagship_config(permit_wait_s: int = 10, denied_s: int = 3) -> dict:
             },
             "pluginConfig": [
                 {"name": "Coscheduling",
-                 "args": {"permitWaitingTimeSeconds": permit_wait_s, "deniedPGExpirationTimeSeconds": denied_s}},
+                 "args": {"permitWaitingTimeSeconds": permit_wait_s, "deniedPGExpirationTimeSeconds": denied_s,
+                          "transientShortage": transient_shortage}},
                 {"name": "NodeResourceTopologyMatch", "args": {"scoringStrategy": {"type": "XGMIGangAffinity"}}},
             ],
         }],

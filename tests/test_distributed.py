@@ -110,6 +110,11 @@ def test_bench_eight_ranks_self_launched_gloo():
         assert len(g["ordinals"]) == g["gang"] and sorted(g["placed"]["ranks"]) == sorted(g["ordinals"])
         assert all(x["correct"] for x in g["placed"]["results"])
         assert pl["summary"][str(g["gang"])]["all_correct"]
+        # The xGMI model exists for every multi-rank gang of the (fake, full
+        # mesh) node; on gloo there is no xGMI data plane to judge: n/a.
+        assert g["model"]["model_busbw_GBps"] > 0 and g["model"]["direct_links_min"] == g["gang"] - 1
+        assert g["verdict"] == "n/a" and pl["summary"][str(g["gang"])]["verdict"] == "n/a"
+    assert pl["gangs"][0]["verdict"] == "n/a"
 
 
 def test_visible_gpu_count_honours_visibility_lists(tmp_path):
@@ -121,3 +126,29 @@ def test_visible_gpu_count_honours_visibility_lists(tmp_path):
     assert n >= 1
     assert visible_gpu_count(root, env={"HIP_VISIBLE_DEVICES": "0"}) == 1
     assert visible_gpu_count(root, env={"ROCR_VISIBLE_DEVICES": "0,1,2", "HIP_VISIBLE_DEVICES": "0"}) == min(3, n)
+
+
+def test_placement_verdict_model():
+    """busbw_model + judge_row on a full-mesh host: pass needs >= 70% of the
+    model and a win over the host-staged path; gloo rows are n/a."""
+    from flex_gpu_scheduler_amd.gpu.discovery import fake_host
+    from flex_gpu_scheduler_amd.parallel.placement import RING_EFFICIENCY, busbw_model, judge_row
+
+    host = fake_host(8)
+    m8 = busbw_model(host, list(range(8)))
+    # fake_host links report 76,000 MB/s (both directions): 7 links x 38 GB/s one way.
+    assert m8["direct_links_min"] == 7 and abs(m8["model_busbw_GBps"] - RING_EFFICIENCY * 7 * 38.0) < 0.2
+    assert busbw_model(host, [0, 5])["direct_links_min"] == 1
+    assert busbw_model(host, [3])["model_busbw_GBps"] is None
+
+    def row(placed, staged, correct=True):
+        res = lambda bw: {"results": [{"MiB": 16, "busbw_GBps": bw / 4, "correct": correct},  # noqa: E731
+                                      {"MiB": 256, "busbw_GBps": bw, "correct": correct}]}
+        return {"gang": 8, "placed": res(placed), "host_staged": res(staged), "cross_socket": res(placed * 0.98)}
+
+    good = judge_row(row(0.8 * m8["model_busbw_GBps"], 10.0), m8, "nccl")
+    assert good["verdict"] == "pass" and abs(good["cross_socket_over_placed"] - 0.98) < 1e-6
+    assert judge_row(row(0.5 * m8["model_busbw_GBps"], 10.0), m8, "nccl")["verdict"] == "fail"
+    assert judge_row(row(0.8 * m8["model_busbw_GBps"], 1e6), m8, "nccl")["verdict"] == "fail"
+    assert judge_row(row(0.8 * m8["model_busbw_GBps"], 10.0, correct=False), m8, "nccl")["verdict"] == "fail"
+    assert judge_row(row(1.0, 1.0), m8, "gloo")["verdict"] == "n/a"

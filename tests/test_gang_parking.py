@@ -1,0 +1,133 @@
+"""Gang parking (Coscheduling transientShortage=Park, docs/ARCHITECTURE.md §4).
+
+The reference denies a PodGroup for deniedPGExpirationTimeSeconds when one of
+its members cannot be placed (pkg/coscheduling/coscheduling.go:140-176, 224-237).
+When the shortfall is only GPUs that other gangs hold right now, this framework
+parks the group instead and re-probes it on the next release of capacity, so the
+gang is admitted as soon as its GPUs are free rather than after the TTL. Groups
+that can never fit, and the "Deny" mode, keep the reference's behaviour."""
+import time
+
+from flex_gpu_scheduler_amd import load_config, new_scheduler
+from flex_gpu_scheduler_amd.models import GPU, make_pod, make_pod_group, mi355x_node
+from flex_gpu_scheduler_amd.utils.workload import flagship_config
+
+
+def gang(name, size, ns="default"):
+    return (make_pod_group(name, ns, size),
+            [make_pod(f"{name}-r{r}", ns, limits={GPU: "1"}, pod_group=name) for r in range(size)])
+
+
+def submit(store, name, size):
+    pg, pods = gang(name, size)
+    store.create("podgroups", pg)
+    for p in pods:
+        store.create("pods", p)
+    return [p["metadata"]["name"] for p in pods]
+
+
+def bound(store, names):
+    return [n for n in names if store.get("pods", "default", n)["spec"].get("nodeName")]
+
+
+def wait_for(pred, timeout=10.0):
+    t0 = time.time()
+    while not pred():
+        if time.time() - t0 > timeout:
+            return False
+        time.sleep(0.002)
+    return True
+
+
+def scheduler(store, mode="Park", denied_s=20):
+    s = new_scheduler(store, load_config(flagship_config(permit_wait_s=10, denied_s=denied_s, transient_shortage=mode)),
+                      podInitialBackoffSeconds=1, podMaxBackoffSeconds=10)
+    s.start()
+    return s
+
+
+def delete_all(store, names):
+    for n in names:
+        store.delete("pods", "default", n)
+
+
+def test_gang_parks_while_gpus_are_held_and_binds_on_release(store):
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = scheduler(store)
+    try:
+        a = submit(store, "a", 8)
+        assert wait_for(lambda: len(bound(store, a)) == 8)
+        b = submit(store, "b", 4)
+        assert wait_for(lambda: s.gang_parks() >= 1)
+        assert bound(store, b) == []
+        assert s.gang_denials()[0] == 0  # parked, not denied
+        t0 = time.time()
+        delete_all(store, a)
+        # Admitted on the release, far inside the 20 s denial TTL and the 1 s
+        # pod backoff.
+        assert wait_for(lambda: len(bound(store, b)) == 4, timeout=5.0)
+        assert time.time() - t0 < 0.9
+        assert s.gang_denials()[0] == 0
+        park = s.plugin_call("Coscheduling", "parking", {"pod": store.get("pods", "default", b[0])})
+        assert park["parked"] == [] and park["outstandingGpus"] == 0
+    finally:
+        s.stop()
+
+
+def test_deny_mode_keeps_the_reference_ttl(store):
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = scheduler(store, mode="Deny", denied_s=20)
+    try:
+        a = submit(store, "a", 8)
+        assert wait_for(lambda: len(bound(store, a)) == 8)
+        b = submit(store, "b", 4)
+        assert wait_for(lambda: s.gang_denials()[0] >= 1)
+        delete_all(store, a)
+        time.sleep(1.5)
+        assert bound(store, b) == []  # still denied
+        assert s.gang_parks() == 0
+    finally:
+        s.stop()
+
+
+def test_group_bigger_than_the_cluster_is_denied_not_parked(store):
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = scheduler(store)
+    try:
+        big = submit(store, "big", 12)
+        assert wait_for(lambda: s.gang_denials()[0] >= 1)
+        assert s.gang_parks() == 0 and bound(store, big) == []
+    finally:
+        s.stop()
+
+
+def test_oldest_parked_gang_goes_first(store):
+    """The oldest parked group holds a reservation: younger small gangs do not
+    take the GPUs it waits for (no starvation of 8-rank gangs)."""
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = scheduler(store)
+    try:
+        a = submit(store, "a", 8)
+        assert wait_for(lambda: len(bound(store, a)) == 8)
+        b = submit(store, "b", 8)
+        assert wait_for(lambda: s.gang_parks() >= 1)
+        time.sleep(1.1)  # a later creation second: younger in the queue order
+        small = [submit(store, f"c{i}", 1)[0] for i in range(3)]
+        assert wait_for(lambda: s.gang_parks() >= 4)
+        delete_all(store, a)
+        assert wait_for(lambda: len(bound(store, b)) == 8, timeout=5.0)
+        assert bound(store, small) == []
+        delete_all(store, b)
+        assert wait_for(lambda: len(bound(store, small)) == 3, timeout=5.0)
+        assert s.gang_denials()[0] == 0
+    finally:
+        s.stop()
+
+
+def test_parking_mode_is_validated():
+    import pytest
+
+    from flex_gpu_scheduler_amd.config import ConfigError
+
+    with pytest.raises(ConfigError):
+        load_config(flagship_config(transient_shortage="Sometimes"))

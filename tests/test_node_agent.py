@@ -200,3 +200,27 @@ def test_partition_bandwidth_table_is_published(store):
     assert sorted(calls) == [0, 1, 3]
     ann = _json.loads(store.get("nodes", "", "n0")["metadata"]["annotations"][BANDWIDTH_ANNOTATION])
     assert sorted(ann) == ["0", "1", "3"] and ann["3"]["partitions"]["SPX"]["read_GBps"] == 5003.0
+
+
+def test_failed_bandwidth_probe_is_not_retried_every_heartbeat(store):
+    from flex_gpu_scheduler_amd.control import LocalClient
+    from flex_gpu_scheduler_amd.control.node_agent import NodeAgent
+    from flex_gpu_scheduler_amd.gpu.discovery import fake_host
+
+    calls = []
+
+    def bw(dev):
+        calls.append(dev)
+        if dev == 1:
+            raise RuntimeError("probe failed")
+        return {"bytes": 1 << 30, "partitions": {}}
+
+    agent = NodeAgent(LocalClient(store), "n0", host_fn=lambda: fake_host(2), bandwidth_fn=bw, publish_metrics=False)
+    agent.sync()
+    agent.sync()
+    agent.sync()
+    assert sorted(calls) == [0, 1]  # GPU 1 failed once and waits for its retry time
+    agent.bandwidth_retry_s = 0.0
+    agent._bandwidth_retry_at.clear()
+    agent.sync()
+    assert calls.count(1) == 2
