@@ -83,6 +83,9 @@ struct Handle {
   // Moves these pods (when queued as unschedulable or backing off) to the
   // active queue; callable from any thread (e.g. a plugin's timer).
   std::function<void(const std::vector<PodPtr>&)> activate;
+  // Parks these pods out of the scheduling queues until activate()
+  // (SchedulingQueue::deactivate); callable from any thread.
+  std::function<void(const std::vector<PodPtr>&)> deactivate;
   // Coscheduling denied `member`'s group (`why`: postfilter | unreserve |
   // minresources); the scheduler keeps a diagnostic record. Optional.
   std::function<void(const Pod& member, const char* why)> gang_denied;

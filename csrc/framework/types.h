@@ -410,6 +410,9 @@ struct QueuedPodInfo {
   MicroTime initial_attempt_wall = 0;
   int attempts = 0;
   std::set<std::string> unschedulable_plugins;
+  // "message|nominated node" of the last failure whose PodScheduled=False
+  // status was written (Scheduler::handle_failure skips identical rewrites).
+  std::string last_condition;
   int64_t enqueue_seq = 0;
   // QueueSort plugins may memoize an immutable sort key here (e.g.
   // Coscheduling's PodGroup creation time); INT64_MIN = not cached.

@@ -35,6 +35,8 @@
 // fragmentation, CPU/memory) and Permit timeouts are denied for the TTL.
 // "Deny" restores the reference's behaviour everywhere.
 #include <algorithm>
+#include <array>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -46,6 +48,7 @@
 #include "scheduler/cache.h"
 #include "scheduler/informers.h"
 #include "scheduler/metrics.h"
+#include "store/store.h"
 
 namespace xsched {
 namespace {
@@ -404,6 +407,22 @@ class Coscheduling : public Plugin {
     return {{"Pod", kAdd, ""}, {"PodGroup", kAdd | kUpdate, ""}};
   }
 
+  // A deleted PodGroup leaves the PATCH memo (its entries would otherwise
+  // live out the memo window: 10^5 of them after a few seconds at full
+  // rate).
+  std::vector<std::string> watched_kinds() const override { return {"podgroups"}; }
+  void on_object_event(const std::string& kind, int type, const JsonPtr& obj, const JsonPtr&) override {
+    if (kind != "podgroups" || static_cast<EventType>(type) != EventType::Deleted || !obj) return;
+    const Json& md = (*obj)["metadata"];
+    std::string full = md["namespace"].str_or("default");
+    full.push_back('/');
+    full += md["name"].as_string();
+    const uint64_t key = pg_key_of(full);
+    PatchShard& sh = patch_shard(key);
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.map.erase(key);
+  }
+
   // Unit-test hook (core/core_test.go:303 TestCheckClusterResource):
   // args["need"] is a resource list; `p` names the group whose own pods count
   // as free. "deny" puts p's group in the denied cache (core_test.go:42's
@@ -439,31 +458,40 @@ class Coscheduling : public Plugin {
   }
 
  private:
-  // True the first time (group uid, phase) is seen within kPatchMemoUs.
-  static constexpr int64_t kPatchMemoUs = 60'000'000;
-  bool note_patched(uint64_t key, const std::string& uid, const std::string& phase) {
-    const int64_t now = h_.clock->now_us();
-    std::lock_guard<std::mutex> g(patched_mu_);
-    auto& e = patched_[key];
-    if (e.uid == uid && e.phase == phase && now - e.at_us < kPatchMemoUs) return false;
-    e = {uid, phase, now};
-    // Amortized expiry: sweep when the memo has doubled since the last sweep
-    // (a sweep on every call past a fixed size made each PostBind O(groups)
-    // once thousands of distinct groups had bound within the memo window).
-    if (patched_.size() > patched_sweep_at_) {
-      for (auto it = patched_.begin(); it != patched_.end();)
-        it = now - it->second.at_us >= kPatchMemoUs ? patched_.erase(it) : std::next(it);
-      patched_sweep_at_ = std::max<size_t>(8192, 2 * patched_.size());
-    }
-    return true;
-  }
+  // True the first time (group uid, phase) is seen within kPatchMemoUs. The
+  // memo only has to outlive the informer's lag behind our own PATCH (a
+  // repeated PATCH is harmless), so entries expire in insertion order from a
+  // per-shard queue, O(1) per call: no sweep over the map (an amortized full
+  // sweep of 10^5 entries held every binder waiting on one lock for tens of
+  // ms in the open-loop runs, profiles/r5k_*). Shards split the lock.
+  static constexpr int64_t kPatchMemoUs = 10'000'000;
+  static constexpr size_t kPatchShards = 16;
   struct Patched {
     std::string uid, phase;
     int64_t at_us = 0;
   };
-  std::mutex patched_mu_;
-  std::unordered_map<uint64_t, Patched> patched_;
-  size_t patched_sweep_at_ = 8192;
+  struct PatchShard {
+    std::mutex mu;
+    std::unordered_map<uint64_t, Patched> map;
+    std::deque<std::pair<int64_t, uint64_t>> order;  // (inserted at, key), oldest first
+  };
+  PatchShard& patch_shard(uint64_t key) { return patch_shards_[(key ^ (key >> 29)) % kPatchShards]; }
+  bool note_patched(uint64_t key, const std::string& uid, const std::string& phase) {
+    const int64_t now = h_.clock->now_us();
+    PatchShard& sh = patch_shard(key);
+    std::lock_guard<std::mutex> g(sh.mu);
+    while (!sh.order.empty() && now - sh.order.front().first >= kPatchMemoUs) {
+      auto it = sh.map.find(sh.order.front().second);
+      if (it != sh.map.end() && now - it->second.at_us >= kPatchMemoUs) sh.map.erase(it);
+      sh.order.pop_front();
+    }
+    auto& e = sh.map[key];
+    if (e.uid == uid && e.phase == phase && now - e.at_us < kPatchMemoUs) return false;
+    e = {uid, phase, now};
+    sh.order.emplace_back(now, key);
+    return true;
+  }
+  std::array<PatchShard, kPatchShards> patch_shards_;
 
   // ---- Gang gate and parking ----
   // Units: whole GPUs for GPU ranks, members for XCD-partition ranks (their
@@ -586,6 +614,7 @@ class Coscheduling : public Plugin {
     // hold-and-wait between gangs), as PostFilter's park does.
     if (assigned > 0) park_rejecting(p, pg);
     else park(p, pg, d.kind, need);
+    park_members(p);
     return XS_FIXED_STATUS(Code::Unschedulable,
                            "PodGroup parked: its remaining members need more GPUs than are free; it retries when "
                            "GPUs are released");
@@ -641,7 +670,18 @@ class Coscheduling : public Plugin {
       erase_outstanding_locked(p.pg_key);
     }
     park(p, pg, p.gpu_demand.kind, units_for(p.gpu_demand, pg.min_member));
+    park_members(p);  // before the rejections, so the rejected siblings park as their cycles fail
     reject_group(p, "PodGroup parked in PostFilter: GPUs are short for its remaining members");
+  }
+  // The group's unplaced members leave the scheduling queues until a probe
+  // un-parks it: one failed cycle per parked gang, not one per member, and no
+  // churn from the cluster events the members' plugin registered.
+  void park_members(const Pod& p) {
+    if (!h_.deactivate) return;
+    std::vector<PodPtr> members;
+    for (auto& q : h_.informers->pods_in_group_of(p))
+      if (q->node_name.empty()) members.push_back(std::move(q));
+    if (!members.empty()) h_.deactivate(members);
   }
   bool consume_parked_reject(uint64_t key) {
     std::lock_guard<std::mutex> g(park_mu_);
@@ -672,8 +712,11 @@ class Coscheduling : public Plugin {
       member.meta.ns = it->second.ns;
       member.pod_group = it->second.group;
       member.pg_key = it->first.second;
+      // A member the cache does not hold (an assumed pod may not show its
+      // node in the lister yet): activating one that is binding would lose
+      // the probe until kProbeStaleUs.
       for (auto& q : h_.informers->pods_in_group_of(member))
-        if (q->node_name.empty() && !q->terminating()) {
+        if (q->node_name.empty() && !q->terminating() && !h_.cache->get_pod(q->uid())) {
           out.push_back(std::move(q));
           break;
         }
@@ -697,6 +740,7 @@ class Coscheduling : public Plugin {
       // One probe at a time: a probe still queued answers for this release
       // too (its gate reads the snapshot of its own cycle, which includes it).
       if (probe_key_ && h_.clock->now_us() - probe_sent_us_ < kProbeStaleUs) return;
+      if (probe_key_ && h_.metrics) h_.metrics->inc("xsched_coscheduling_probes_total", "result=\"stale\"");
       probe = next_probe_locked();
     }
     if (!probe.empty()) h_.activate(probe);
@@ -742,7 +786,9 @@ class Coscheduling : public Plugin {
     for (auto it = parked_rejects_.begin(); it != parked_rejects_.end();)
       it = now - it->second.second > kRejectWindowUs ? parked_rejects_.erase(it) : std::next(it);
   }
-  static constexpr int64_t kProbeStaleUs = 200'000;
+  // A probe not answered within this long (its pod went elsewhere: bound,
+  // deleted, failed before the gate) no longer holds back the next one.
+  static constexpr int64_t kProbeStaleUs = 20'000;
   static constexpr int64_t kRejectWindowUs = 1'000'000;
   static constexpr int64_t kMaxPermitUs = 15LL * 60 * 1'000'000;  // framework cap
   bool park_ = true;

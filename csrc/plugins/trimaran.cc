@@ -155,6 +155,56 @@ class TrimaranBase : public Plugin {
   void start() override {
     timer_ = h_.timers->every(kCacheCleanupUs, [this] { cleanup(); });
   }
+
+  // Unit-test hook for handler_test.go:12 TestHandlerCacheCleanup:
+  // "podAssignCache" seeds args.node's entries (args.entries: [{name,
+  // ageSeconds (null = the zero time)}]), applies an OnUpdate that assigns
+  // the pod args.update to that node, runs cleanupCache and returns the
+  // node's remaining pod names in order.
+  Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) override {
+    if (what != "podAssignCache") return Plugin::debug_call(what, s, p, args);
+    const std::string node = args["node"].as_string();
+    const int64_t now = wall_now_us() / 1000000;
+    auto make = [&](const std::string& name, const std::string& on) {
+      auto q = std::make_shared<Pod>();
+      q->meta.ns = "default";
+      q->meta.name = name;
+      q->meta.uid = name;
+      q->node_name = on;
+      return q;
+    };
+    {
+      Shard& sh = shard(node);
+      std::unique_lock<std::shared_mutex> g(sh.mu);
+      auto& v = sh.assigned[node];
+      v.clear();
+      for (const auto& e : args["entries"].items())
+        v.emplace_back(e["ageSeconds"].is_null() ? 0 : now - e["ageSeconds"].as_int(), make(e["name"].as_string(), node));
+    }
+    if (args["update"].is_string()) {
+      Json oldp = Json::object(), newp = Json::object();
+      for (Json* o : {&oldp, &newp}) {
+        Json md = Json::object();
+        md.set("name", Json(args["update"].as_string()));
+        md.set("namespace", Json("default"));
+        md.set("uid", Json(args["update"].as_string()));
+        o->set("metadata", std::move(md));
+      }
+      Json spec = Json::object();
+      spec.set("nodeName", Json(node));
+      newp.set("spec", std::move(spec));
+      on_object_event("pods", static_cast<int>(EventType::Modified), std::make_shared<Json>(std::move(newp)),
+                      std::make_shared<Json>(std::move(oldp)));
+    }
+    cleanup();
+    Json out = Json::object(), names = Json::array();
+    const Shard& sh = shard(node);
+    std::shared_lock<std::shared_mutex> g(sh.mu);
+    if (auto it = sh.assigned.find(node); it != sh.assigned.end())
+      for (const auto& e : it->second) names.push_back(Json(e.second->name()));
+    out.set("pods", std::move(names));
+    return out;
+  }
   void stop() override {
     if (timer_) h_.timers->cancel(timer_);
   }
@@ -343,38 +393,18 @@ class LoadVariationRiskBalancing : public TrimaranBase {
     if (!m->present) return {kMinNodeScore, {}};
     auto it = m->nodes.find(ni.name());
     if (it == m->nodes.end()) return {kMinNodeScore, {}};
-    // getResourceRequested: Σ containers, max with init containers (cpu/mem), + overhead.
     int64_t req_cpu = 0, req_mem = 0;
-    for (const auto& c : p.containers) {
-      req_cpu += c.requests.get(kCPU);
-      req_mem += c.requests.get(kMemory);
-    }
-    for (const auto& c : p.init_containers) {
-      req_cpu = std::max(req_cpu, c.requests.get(kCPU));
-      req_mem = std::max(req_mem, c.requests.get(kMemory));
-    }
-    req_cpu += p.overhead().get(kCPU);
-    req_mem += p.overhead().get(kMemory);
+    requested(p, &req_cpu, &req_mem);
     constexpr int kDims = 5;  // cpu, memory, GPU busy, HBM bandwidth, xGMI
     double scores[kDims];
     bool valid[kDims] = {false, false, false, false, false};
     double avg, sd;
-    if (resource_data(it->second, kTCPU, &avg, &sd)) {
-      ResourceStats rs;
-      rs.capacity = static_cast<double>(ni.node->allocatable.get(kCPU));
-      rs.req = static_cast<double>(req_cpu);
-      rs.used_avg = avg * rs.capacity / 100;
-      rs.used_std = sd * rs.capacity / 100;
+    ResourceStats rs;
+    if (create_stats(it->second, *ni.node, req_cpu, req_mem, kTCPU, &rs)) {
       scores[0] = rs.score(margin_, sensitivity_);
       valid[0] = true;
     }
-    if (resource_data(it->second, kTMemory, &avg, &sd)) {
-      ResourceStats rs;
-      const double mega = 1.0 / 1024.0 / 1024.0;
-      rs.capacity = static_cast<double>(ni.node->allocatable.get(kMemory)) * mega;
-      rs.req = static_cast<double>(req_mem) * mega;
-      rs.used_avg = avg * rs.capacity / 100;
-      rs.used_std = sd * rs.capacity / 100;
+    if (create_stats(it->second, *ni.node, req_cpu, req_mem, kTMemory, &rs)) {
       scores[1] = rs.score(margin_, sensitivity_);
       valid[1] = true;
     }
@@ -408,6 +438,84 @@ class LoadVariationRiskBalancing : public TrimaranBase {
         if (valid[i]) total = std::max(total, scores[i]);
     }
     return {static_cast<int64_t>(std::llround(total)), {}};
+  }
+
+  // getResourceRequested (analysis.go:134-161): Σ containers, max with each
+  // init container (cpu/memory), plus the pod overhead.
+  static void requested(const Pod& p, int64_t* cpu, int64_t* mem) {
+    *cpu = *mem = 0;
+    for (const auto& c : p.containers) {
+      *cpu += c.requests.get(kCPU);
+      *mem += c.requests.get(kMemory);
+    }
+    for (const auto& c : p.init_containers) {
+      *cpu = std::max(*cpu, c.requests.get(kCPU));
+      *mem = std::max(*mem, c.requests.get(kMemory));
+    }
+    *cpu += p.overhead().get(kCPU);
+    *mem += p.overhead().get(kMemory);
+  }
+  // createResourceStats (analysis.go:81-110): usage statistics of one
+  // resource in the resource's units (milli-CPU, MiB).
+  static bool create_stats(const std::vector<Metric>& ms, const Node& node, int64_t req_cpu, int64_t req_mem,
+                           MType type, ResourceStats* rs) {
+    double avg, sd;
+    if (!resource_data(ms, type, &avg, &sd)) return false;
+    *rs = ResourceStats{};
+    if (type == kTCPU) {
+      rs->capacity = static_cast<double>(node.allocatable.get(kCPU));
+      rs->req = static_cast<double>(req_cpu);
+    } else {
+      const double mega = 1.0 / 1024.0 / 1024.0;
+      rs->capacity = static_cast<double>(node.allocatable.get(kMemory)) * mega;
+      rs->req = static_cast<double>(req_mem) * mega;
+    }
+    rs->used_avg = avg * rs->capacity / 100;
+    rs->used_std = sd * rs->capacity / 100;
+    return true;
+  }
+
+  // Unit-test hooks for the reference's analysis_test.go tables:
+  // "computeScore" (TestComputeScore :74), "createResourceStats"
+  // (Test_createResourceStats :212; args.metrics, args.resource, the node
+  // named by args.node), "getResourceRequested" (TestGetResourceRequested).
+  Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) override {
+    Json out = Json::object();
+    if (what == "computeScore") {
+      ResourceStats rs;
+      rs.capacity = args["capacity"].as_double(0);
+      rs.req = args["req"].as_double(0);
+      rs.used_avg = args["usedAvg"].as_double(0);
+      rs.used_std = args["usedStdev"].as_double(0);
+      out.set("score", Json(rs.score(args["margin"].as_double(1), args["sensitivity"].as_double(1))));
+      return out;
+    }
+    if (what == "getResourceRequested" || what == "createResourceStats") {
+      int64_t cpu = 0, mem = 0;
+      requested(*p, &cpu, &mem);
+      if (what == "getResourceRequested") {
+        out.set("milliCPU", Json(cpu));
+        out.set("memory", Json(mem));
+        return out;
+      }
+      std::vector<Metric> ms;
+      for (const auto& x : args["metrics"].items())
+        ms.push_back(Metric{mtype(x["type"].as_string()), mop(x["operator"].as_string()), x["value"].as_double()});
+      NodeInfoPtr ni = h_.snapshot ? h_.snapshot->get(args["node"].as_string()) : nullptr;
+      if (!ni || !ni->node) throw std::runtime_error("createResourceStats: no node " + args["node"].str_or(""));
+      ResourceStats rs;
+      const bool ok = create_stats(ms, *ni->node, cpu, mem, args["resource"].as_string() == "cpu" ? kTCPU : kTMemory,
+                                   &rs);
+      out.set("valid", Json(ok));
+      if (ok) {
+        out.set("capacity", Json(rs.capacity));
+        out.set("req", Json(rs.req));
+        out.set("usedAvg", Json(rs.used_avg));
+        out.set("usedStdev", Json(rs.used_std));
+      }
+      return out;
+    }
+    return TrimaranBase::debug_call(what, s, p, args);
   }
 
  private:

@@ -23,6 +23,7 @@
 #include "scheduler/scheduler.h"
 #include "store/store.h"
 #include "telemetry/amdsmi_sampler.h"
+#include "tools/sampler.h"
 
 namespace py = pybind11;
 using namespace xsched;
@@ -213,6 +214,14 @@ PYBIND11_MODULE(_xsched, m) {
   });
 
   // ---- quantities / parsing helpers ----
+  // Wall-clock sampling profiler of every thread (csrc/tools/sampler.h), for
+  // stall diagnosis in Python-hosted runs (scripts/openloop_probe.py).
+  m.def("sampler_start", [](int hz, size_t max_samples) { sampler::start(hz, max_samples); }, py::arg("hz") = 2000,
+        py::arg("max_samples") = size_t{1} << 21);
+  m.def("sampler_dump", [](const std::string& path) {
+    py::gil_scoped_release nogil;
+    sampler::dump(path);
+  });
   m.def("parse_quantity", [](const std::string& s) {
     Quantity q = Quantity::parse(s);
     return py::make_tuple(q.milli_value(), q.value(), q.str());
@@ -664,6 +673,7 @@ PYBIND11_MODULE(_xsched, m) {
              d["active"] = c.active;
              d["backoff"] = c.backoff;
              d["unschedulable"] = c.unschedulable;
+             d["parked"] = c.parked;
              d["in_flight"] = s.queue().in_flight();
              d["activation_marks"] = s.queue().pending_activations();
              return d;
@@ -778,7 +788,12 @@ PYBIND11_MODULE(_xsched, m) {
             return to_py(out);
           },
           py::arg("plugin"), py::arg("point"), py::arg("args"))
-      .def("set_trace", [](Scheduler& s, bool on) { s.tracer().enable(on); })
+      .def("set_trace",
+           [](Scheduler& s, bool on, size_t capacity) {
+             if (capacity) s.tracer().set_capacity(capacity);
+             s.tracer().enable(on);
+           },
+           py::arg("on"), py::arg("capacity") = 0)
       .def("trace_json", [](Scheduler& s) { return s.tracer().chrome_json(); })
       .def("clear_trace", [](Scheduler& s) { s.tracer().clear(); })
       .def("profiles", [](Scheduler& s) {

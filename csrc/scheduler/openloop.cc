@@ -51,11 +51,22 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
   int64_t last_arrival = t0;
   int64_t in_flight = 0, held = 0;
   int64_t next_slice = t0 + 5000;
+  Scheduler::Stats st0 = sched.stats();
+  uint64_t parks0 = sched.gang_parks();
   for (;;) {
     int64_t now = clock->now_us();
-    while (now >= next_slice) {
-      out.timeline.emplace_back(static_cast<int32_t>(in_flight), static_cast<int32_t>(held));
-      next_slice += 5000;
+    if (now >= next_slice) {
+      const Scheduler::Stats st = sched.stats();
+      const uint64_t parks = sched.gang_parks();
+      while (now >= next_slice) {
+        out.timeline.push_back({static_cast<int32_t>(in_flight), static_cast<int32_t>(held),
+                                static_cast<int32_t>(st.attempts - st0.attempts),
+                                static_cast<int32_t>(st.unschedulable - st0.unschedulable),
+                                static_cast<int32_t>(parks - parks0)});
+        st0 = st;
+        parks0 = parks;
+        next_slice += 5000;
+      }
     }
     bool busy = false;
     // Arrivals due now.

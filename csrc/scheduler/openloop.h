@@ -18,6 +18,8 @@
 // ~10^4 gangs/s.
 #pragma once
 
+#include <array>
+
 #include <cstdint>
 #include <memory>
 #include <vector>
@@ -47,7 +49,9 @@ struct OpenLoopResult {
   // backlog), and bound but not yet deleted (the held occupancy).
   int64_t max_in_flight_pods = 0, max_held_pods = 0;
   // Every 5 ms of the run: pods in flight and held at the end of the slice.
-  std::vector<std::pair<int32_t, int32_t>> timeline;
+  // Per 5 ms slice: pods in flight, pods held, and the scheduler's attempts,
+  // unschedulable attempts and parked groups during the slice.
+  std::vector<std::array<int32_t, 5>> timeline;
 };
 
 // Runs to completion on the calling thread. `offsets_us[i]` is gang i's

@@ -223,6 +223,7 @@ void SchedulingQueue::add(const PodPtr& p) {
     auto q = new_info(p);
     q->enqueue_seq = ++seq_;
     unschedulable_.erase(p->uid());
+    parked_.erase(p->uid());
     backoff_.erase(p->uid());
     in_flight_.erase(p->uid());
     active_.push(q);
@@ -244,12 +245,15 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
       if (it != unschedulable_.end()) {
         q = it->second;
         unschedulable_.erase(it);
+      } else if (auto pk = parked_.find(uid); pk != parked_.end()) {
+        q = pk->second;
+        parked_.erase(pk);
       } else if ((q = backoff_.get(uid))) {
         backoff_.erase(uid);
       }
       if (!q) {  // in flight: remember the request for when its cycle fails
         auto f = in_flight_.find(uid);
-        if (f != in_flight_.end()) f->second = true;
+        if (f != in_flight_.end()) f->second = kActivate;
         continue;
       }
       active_.push(q);
@@ -259,21 +263,46 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
   if (moved) cv_.notify_all();
 }
 
+void SchedulingQueue::deactivate(const std::vector<PodPtr>& pods) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& pod : pods) {
+    const std::string& uid = pod->uid();
+    QueuedPodInfoPtr q;
+    if ((q = active_.get(uid))) {
+      active_.erase(uid);
+    } else if ((q = backoff_.get(uid))) {
+      backoff_.erase(uid);
+    } else if (auto it = unschedulable_.find(uid); it != unschedulable_.end()) {
+      q = it->second;
+      unschedulable_.erase(it);
+    }
+    if (q) {
+      q->timestamp_us = clock_->now_us();
+      parked_[uid] = std::move(q);
+      continue;
+    }
+    if (auto f = in_flight_.find(uid); f != in_flight_.end()) f->second = kPark;
+  }
+}
+
 bool SchedulingQueue::add_unschedulable_if_not_present(const QueuedPodInfoPtr& p, int64_t pod_cycle) {
   bool activated = false;
   {
     std::lock_guard<std::mutex> g(mu_);
     const std::string& uid = p->pod->uid();
-    if (unschedulable_.count(uid) || active_.contains(uid) || backoff_.contains(uid)) return false;
+    if (unschedulable_.count(uid) || parked_.count(uid) || active_.contains(uid) || backoff_.contains(uid))
+      return false;
     p->timestamp_us = clock_->now_us();
-    bool marked = false;
+    uint8_t mark = kNoMark;
     if (auto f = in_flight_.find(uid); f != in_flight_.end()) {
-      marked = f->second;
+      mark = f->second;
       in_flight_.erase(f);
     }
-    if (marked) {
+    if (mark == kActivate) {
       active_.push(p);  // activated while in flight; Activate skips backoff
       activated = true;
+    } else if (mark == kPark) {
+      parked_[uid] = p;
     } else if (move_request_cycle_ >= pod_cycle) {
       backoff_.push(p);
     } else {
@@ -288,7 +317,7 @@ bool SchedulingQueue::add_unschedulable_if_not_present(const QueuedPodInfoPtr& p
 size_t SchedulingQueue::pending_activations() const {
   std::lock_guard<std::mutex> g(mu_);
   size_t n = 0;
-  for (const auto& kv : in_flight_) n += kv.second;
+  for (const auto& kv : in_flight_) n += kv.second == kActivate;
   return n;
 }
 
@@ -311,7 +340,7 @@ QueuedPodInfoPtr SchedulingQueue::pop(int timeout_ms) {
     return nullptr;
   if (closed_ && active_.empty()) return nullptr;
   QueuedPodInfoPtr q = active_.pop();
-  in_flight_.insert_or_assign(q->pod->uid(), false);
+  in_flight_.insert_or_assign(q->pod->uid(), kNoMark);
   q->attempts++;
   scheduling_cycle_++;
   return q;
@@ -341,6 +370,13 @@ void SchedulingQueue::update(const PodPtr& old_p, const PodPtr& new_p) {
       auto nq = std::make_shared<QueuedPodInfo>(*q);
       nq->pod = new_p;
       backoff_.push(nq);
+      nominator_->update(old_p, new_p);
+      return;
+    }
+    if (auto pk = parked_.find(uid); pk != parked_.end()) {
+      auto nq = std::make_shared<QueuedPodInfo>(*pk->second);
+      nq->pod = new_p;
+      pk->second = nq;
       nominator_->update(old_p, new_p);
       return;
     }
@@ -381,6 +417,7 @@ void SchedulingQueue::remove(const Pod& p) {
   active_.erase(p.uid());
   backoff_.erase(p.uid());
   unschedulable_.erase(p.uid());
+  parked_.erase(p.uid());
   in_flight_.erase(p.uid());
 }
 
@@ -466,6 +503,16 @@ void SchedulingQueue::flush_unschedulable_leftover() {
   std::vector<QueuedPodInfoPtr> stale;
   for (const auto& kv : unschedulable_)
     if (now - kv.second->timestamp_us > opts_.unschedulable_timeout_us) stale.push_back(kv.second);
+  // Parked pods too (safety net: their release signal never came).
+  for (auto it = parked_.begin(); it != parked_.end();) {
+    if (now - it->second->timestamp_us > opts_.unschedulable_timeout_us) {
+      unschedulable_[it->first] = it->second;
+      stale.push_back(it->second);
+      it = parked_.erase(it);
+    } else {
+      ++it;
+    }
+  }
   if (!stale.empty()) move_locked(stale, ClusterEvent{"*", kAll, "UnschedulableTimeout"});
 }
 
@@ -479,7 +526,7 @@ void SchedulingQueue::close() {
 
 SchedulingQueue::Counts SchedulingQueue::counts() const {
   std::lock_guard<std::mutex> g(mu_);
-  return Counts{active_.size(), backoff_.size(), unschedulable_.size()};
+  return Counts{active_.size(), backoff_.size(), unschedulable_.size(), parked_.size()};
 }
 
 std::vector<QueuedPodInfoPtr> SchedulingQueue::pending_pods() const {
@@ -488,12 +535,13 @@ std::vector<QueuedPodInfoPtr> SchedulingQueue::pending_pods() const {
   auto b = backoff_.items();
   out.insert(out.end(), b.begin(), b.end());
   for (const auto& kv : unschedulable_) out.push_back(kv.second);
+  for (const auto& kv : parked_) out.push_back(kv.second);
   return out;
 }
 
 bool SchedulingQueue::has_pod(const std::string& uid) const {
   std::lock_guard<std::mutex> g(mu_);
-  return active_.contains(uid) || backoff_.contains(uid) || unschedulable_.count(uid);
+  return active_.contains(uid) || backoff_.contains(uid) || unschedulable_.count(uid) || parked_.count(uid);
 }
 
 }  // namespace xsched

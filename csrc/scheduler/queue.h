@@ -117,6 +117,14 @@ class SchedulingQueue {
   // scheduling_queue.go:307-337; its moveRequestCycle covers only cluster
   // events, :376-400,629.)
   void activate(const std::vector<PodPtr>& pods);
+  // Parks the pods: moved out of activeQ / backoffQ / unschedulableQ into a
+  // holding area that no cluster event and no backoff flush touches; only
+  // activate() (or the unschedulable leftover flush) brings them back. A pod
+  // in flight is marked and parks when its cycle fails. Coscheduling parks a
+  // gang's unplaced members this way while the gang waits for GPUs, so
+  // neither each member's own failed cycle nor every PodGroup creation in the
+  // cluster (its registered event) churns them.
+  void deactivate(const std::vector<PodPtr>& pods);
   // Returns false if the pod is already queued (active/backoff).
   bool add_unschedulable_if_not_present(const QueuedPodInfoPtr& p, int64_t pod_scheduling_cycle);
   size_t pending_activations() const;  // in-flight pods carrying an activation mark
@@ -134,7 +142,7 @@ class SchedulingQueue {
   void close();
 
   struct Counts {
-    size_t active = 0, backoff = 0, unschedulable = 0;
+    size_t active = 0, backoff = 0, unschedulable = 0, parked = 0;
   };
   Counts counts() const;
   std::vector<QueuedPodInfoPtr> pending_pods() const;
@@ -156,10 +164,14 @@ class SchedulingQueue {
   PodHeap active_;
   PodHeap backoff_;
   std::unordered_map<std::string, QueuedPodInfoPtr> unschedulable_;
-  // Popped pods -> "activated while in flight". An entry lives until the pod
-  // re-enters a queue, is removed, or shows up assigned (every pod ends in one
-  // of those), so the map is bounded by the pods that exist.
-  std::unordered_map<std::string, bool> in_flight_;
+  std::unordered_map<std::string, QueuedPodInfoPtr> parked_;  // deactivate()
+  // Popped pods -> what to do when their cycle fails: kNoMark, kActivate
+  // (activated while in flight) or kPark (deactivated while in flight). An
+  // entry lives until the pod re-enters a queue, is removed, or shows up
+  // assigned (every pod ends in one of those), so the map is bounded by the
+  // pods that exist.
+  enum : uint8_t { kNoMark = 0, kActivate = 1, kPark = 2 };
+  std::unordered_map<std::string, uint8_t> in_flight_;
   std::vector<std::pair<ClusterEvent, std::set<std::string>>> event_map_;
   int64_t scheduling_cycle_ = 0;
   int64_t move_request_cycle_ = -1;

@@ -349,6 +349,7 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.clock = clock_;
     h.timers = timers_.get();
     h.activate = [this](const std::vector<PodPtr>& pods) { queue_->activate(pods); };
+    h.deactivate = [this](const std::vector<PodPtr>& pods) { queue_->deactivate(pods); };
     h.gang_denied = [this](const Pod& p, const char* why) { note_gang_denied(p, why); };
     h.gang_parked = [this](const Pod&) { gang_parks_total_.fetch_add(1, std::memory_order_relaxed); };
     h.blocking_begin = [this] {
@@ -431,6 +432,7 @@ void Scheduler::start() {
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"active\"", static_cast<double>(c.active));
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"backoff\"", static_cast<double>(c.backoff));
     metrics_->set_gauge("scheduler_pending_pods", "queue=\"unschedulable\"", static_cast<double>(c.unschedulable));
+    metrics_->set_gauge("scheduler_pending_pods", "queue=\"parked\"", static_cast<double>(c.parked));
     // Upstream metrics.go:102 (Goroutines, by work) and :171 (CacheSize).
     int waiting = 0;
     for (const auto& w : waiting_) waiting += static_cast<int>(w->size());
@@ -2309,6 +2311,10 @@ void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
   bm.attempts.load(std::memory_order_relaxed)->observe(qpi->attempts);
   if (tracer_.enabled()) tracer_.record(TraceEvent{"bind", assumed->key(), host, t0, t1 - t0, 1});
   fw->run_post_bind(*s, assumed, host);
+  if (tracer_.enabled()) {
+    const int64_t t2 = clock_->now_us();
+    tracer_.record(TraceEvent{"post_bind", assumed->key(), "", t1, t2 - t1, 1});
+  }
   {
     cnt_.bound.fetch_add(1, std::memory_order_relaxed);
   }
@@ -2328,12 +2334,18 @@ void Scheduler::binding_cycle(const BindTask& t, const Status& permit_status) {
 void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const Status& st, const std::string& reason,
                                const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins) {
   PodPtr pod = qpi->pod;
+  // updatePod is skipped when the condition and nomination are unchanged
+  // since this pod's last failure (remembered on its queue entry, so the
+  // memo lives and dies with the pod: no scheduler-wide map to sweep).
+  std::string condition = st.message() + "|" + nominated;
+  const bool same_condition = qpi->last_condition == condition && nominated == pod->nominated_node_name;
   // Requeue the latest version unless it was deleted or got assigned.
   PodPtr latest = informers_->pod(pod->ns(), pod->name());
   if (latest && latest->uid() == pod->uid() && latest->node_name.empty() && !latest->terminating()) {
     auto nq = std::make_shared<QueuedPodInfo>(*qpi);
     nq->pod = latest;
     nq->unschedulable_plugins = plugins;
+    nq->last_condition = condition;
     queue_->add_unschedulable_if_not_present(nq, cycle);
   }
   // After the requeue (which re-registers the pod's *observed* nomination):
@@ -2351,16 +2363,9 @@ void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const
     } catch (const std::exception&) {
     }
   });
-  if (!opts_.status_updates) return;
+  if (!opts_.status_updates || same_condition) return;
   // updatePod: PodScheduled=False condition + nominatedNodeName, only when changed.
   std::string msg = st.message();
-  {
-    std::lock_guard<std::mutex> g(stats_mu_);
-    auto& last = last_condition_[pod->uid()];
-    if (last == msg + "|" + nominated && nominated == pod->nominated_node_name) return;
-    last = msg + "|" + nominated;
-    if (last_condition_.size() > 200000) last_condition_.clear();
-  }
   Json patch = Json::object();
   Json status = Json::object();
   Json cond = Json::object();

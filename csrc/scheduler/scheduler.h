@@ -442,7 +442,6 @@ class Scheduler {
   std::vector<GangDenial> gang_denials_;
   uint64_t gang_denials_total_ = 0;
   std::atomic<uint64_t> gang_parks_total_{0};
-  std::unordered_map<std::string, std::string> last_condition_;  // uid -> last failure message
 };
 
 }  // namespace xsched

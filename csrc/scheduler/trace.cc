@@ -1,11 +1,33 @@
 #include "scheduler/trace.h"
 
+#include <algorithm>
+
 #include "common/json.h"
 
 namespace xsched {
 
+void Tracer::set_capacity(size_t cap) {
+  std::lock_guard<std::mutex> g(mu_);
+  ring_.clear();
+  head_ = 0;
+  wrapped_ = false;
+  slots_.reset(cap ? new TraceEvent[cap] : nullptr);
+  nslots_ = cap;
+  next_.store(0);
+}
+
+size_t Tracer::dropped() const {
+  const size_t n = next_.load();
+  return nslots_ && n > nslots_ ? n - nslots_ : 0;
+}
+
 void Tracer::record(TraceEvent ev) {
   if (!enabled()) return;
+  if (nslots_) {
+    const size_t i = next_.fetch_add(1, std::memory_order_relaxed);
+    if (i < nslots_) slots_[i] = std::move(ev);
+    return;
+  }
   std::lock_guard<std::mutex> g(mu_);
   if (ring_.size() < cap_) {
     ring_.push_back(std::move(ev));
@@ -18,6 +40,10 @@ void Tracer::record(TraceEvent ev) {
 
 std::vector<TraceEvent> Tracer::events() const {
   std::lock_guard<std::mutex> g(mu_);
+  if (nslots_) {  // read after recording stopped (enable(false))
+    const size_t n = std::min(next_.load(), nslots_);
+    return std::vector<TraceEvent>(slots_.get(), slots_.get() + n);
+  }
   if (!wrapped_) return ring_;
   std::vector<TraceEvent> out;
   out.reserve(ring_.size());
@@ -50,6 +76,7 @@ std::string Tracer::chrome_json() const {
 
 void Tracer::clear() {
   std::lock_guard<std::mutex> g(mu_);
+  next_.store(0);
   ring_.clear();
   head_ = 0;
   wrapped_ = false;

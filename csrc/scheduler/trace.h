@@ -10,6 +10,7 @@
 #include <atomic>
 #include <cstdint>
 #include <mutex>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -33,6 +34,12 @@ class Tracer {
   std::vector<TraceEvent> events() const;
   std::string chrome_json() const;
   void clear();
+  // Linear recording of up to `cap` events (0: back to the default ring):
+  // the slots are allocated up front and claimed with one atomic increment,
+  // no lock, so a diagnosis run at full load is not serialized on the
+  // tracer; events past the end are dropped (dropped()).
+  void set_capacity(size_t cap);
+  size_t dropped() const;
 
  private:
   size_t cap_;
@@ -41,6 +48,10 @@ class Tracer {
   std::vector<TraceEvent> ring_;
   size_t head_ = 0;
   bool wrapped_ = false;
+  // Linear mode (set_capacity): fixed slots, claimed by next_.
+  std::unique_ptr<TraceEvent[]> slots_;
+  size_t nslots_ = 0;
+  std::atomic<size_t> next_{0};
 };
 
 }  // namespace xsched

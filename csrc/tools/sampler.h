@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstdio>
+#include <ctime>
 #include <fstream>
 #include <map>
 #include <string>
@@ -37,6 +38,7 @@ constexpr int kDepth = 32;
 struct Sample {
   int32_t tid;
   int32_t depth;
+  int64_t t_ns;  // CLOCK_MONOTONIC at the signal (stall windows: sample_report --timeline)
   void* pcs[kDepth];
 };
 
@@ -55,6 +57,9 @@ inline void on_sigprof(int, siginfo_t*, void*) {
   size_t i = next().fetch_add(1, std::memory_order_relaxed);
   if (i < b.size()) {
     Sample& s = b[i];
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);  // async-signal-safe
+    s.t_ns = static_cast<int64_t>(ts.tv_sec) * 1000000000 + ts.tv_nsec;
     s.tid = static_cast<int32_t>(syscall(SYS_gettid));
     s.depth = backtrace(s.pcs, kDepth);
   }
@@ -93,7 +98,9 @@ inline std::vector<int> list_tids(int self) {
 }
 
 inline void start(int hz, size_t max_samples = 1 << 21) {
+  if (running().load()) return;
   buffer().resize(max_samples);
+  next().store(0);
   void* warm[4];
   backtrace(warm, 4);  // load libgcc's unwinder outside the handler
   struct sigaction sa {};
@@ -165,7 +172,7 @@ inline void dump(const std::string& path) {
         if (ch == ' ') ch = '_';
       it = names.emplace(s.tid, nm).first;
     }
-    f << s.tid << ' ' << it->second;
+    f << s.tid << ' ' << it->second << " @" << s.t_ns;
     for (int d = 0; d < s.depth; ++d) f << ' ' << std::hex << reinterpret_cast<uintptr_t>(s.pcs[d]) << std::dec;
     f << "\n";
   }

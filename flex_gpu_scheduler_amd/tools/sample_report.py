@@ -9,6 +9,15 @@ the top functions by self time (leaf frame), by self time with library frames
 charged to their caller in our code, and by inclusive time.
 
     python -m flex_gpu_scheduler_amd.tools.sample_report <dump> [--exe build/xsched_stress] [--top 25] [--json out]
+    python -m flex_gpu_scheduler_amd.tools.sample_report <dump> --exe flex_gpu_scheduler_amd/_xsched*.so \
+        --timeline 1 [--roles xs-sched,xs-bind,xs-informer]
+
+Dumps from the Python extension (`native().sampler_start/_dump`, used by
+scripts/openloop_probe.py --sample-run) carry a timestamp per sample:
+`--timeline BIN_MS` prints, per time bin and thread role, the busy share and
+the most common first own-code frame of the busy samples (a stall shows as
+bins where every role sits in the same lock), and `--window A B` restricts the
+summary to [A, B) ms from the first sample.
 """
 from __future__ import annotations
 
@@ -51,7 +60,7 @@ def short(name: str, width: int = 110) -> str:
 def load(dump: str, exe: str):
     base = 0
     maps: list[tuple[int, int, int, str]] = []
-    samples: list[tuple[str, list[int]]] = []
+    samples: list[tuple[str, list[int], int]] = []
     with open(dump) as f:
         for line in f:
             if line.startswith("exe_base "):
@@ -64,7 +73,11 @@ def load(dump: str, exe: str):
                 parts = line.split()
                 if len(parts) < 3:
                     continue
-                samples.append((parts[1], [int(x, 16) for x in parts[2:]]))
+                t = 0
+                if parts[2].startswith("@"):
+                    t = int(parts[2][1:])
+                    parts = parts[:2] + parts[3:]
+                samples.append((parts[1], [int(x, 16) for x in parts[2:]], t))
     exe_syms = SymbolTable(exe)
     lib_syms: dict[str, SymbolTable] = {}
     cache: dict[int, str] = {}
@@ -76,7 +89,9 @@ def load(dump: str, exe: str):
         for lo, hi, off, path in maps:
             if lo <= pc < hi:
                 if path.endswith(exe.split("/")[-1]):
-                    name = exe_syms.lookup(pc - base)
+                    # the executable at its load base, or a shared object
+                    # (the Python extension) at its mapping
+                    name = exe_syms.lookup(pc - lo + off if ".so" in path else pc - base)
                 else:
                     tab = lib_syms.get(path)
                     if tab is None:
@@ -98,10 +113,43 @@ def is_idle(frames: list[str]) -> bool:
     return any(f.startswith(IDLE_MARKERS) for f in frames[:6])
 
 
-def summarize(dump: str, exe: str, top: int = 25) -> dict:
+def frames_of(pcs: list[int], resolve) -> list[str]:
+    # frames[0] is the handler, [1] the signal trampoline; [2] is the interrupted pc.
+    return [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
+
+
+def timeline(dump: str, exe: str, bin_ms: float, roles: list[str]) -> list[str]:
     samples, resolve = load(dump, exe)
+    if not samples:
+        return []
+    t0 = min(t for _, _, t in samples)
+    bins: dict = collections.defaultdict(lambda: collections.defaultdict(list))
+    for tname, pcs, t in samples:
+        role = re.sub(r"\d+$", "", tname)
+        if role in roles:
+            bins[int((t - t0) / 1e6 // bin_ms)][role].append(frames_of(pcs, resolve))
+    out = []
+    for b in sorted(bins):
+        cells = []
+        for role in roles:
+            stacks = bins[b].get(role, [])
+            busy = [s for s in stacks if not is_idle(s)]
+            own = collections.Counter(next((f for f in s if "[lib" not in f), "?") for s in busy if s)
+            leaf = collections.Counter(s[0] for s in busy if s)
+            top = own.most_common(1)[0][0] if own else "-"
+            lf = leaf.most_common(1)[0][0] if leaf else "-"
+            cells.append(f"{role} {len(busy)}/{len(stacks)} {short(top, 60)} <{short(lf, 40)}>")
+        out.append(f"{b * bin_ms:8.1f} | " + " | ".join(cells))
+    return out
+
+
+def summarize(dump: str, exe: str, top: int = 25, window: tuple[float, float] | None = None) -> dict:
+    samples, resolve = load(dump, exe)
+    if window and samples:
+        t0 = min(t for _, _, t in samples)
+        samples = [s for s in samples if window[0] <= (s[2] - t0) / 1e6 < window[1]]
     by_thread: dict[str, list[list[str]]] = collections.defaultdict(list)
-    for tname, pcs in samples:
+    for tname, pcs, _t in samples:
         # frames[0] is the handler, [1] the signal trampoline; [2] is the interrupted pc.
         frames = [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
         role = re.sub(r"\d+$", "", tname)
@@ -140,7 +188,7 @@ def lines(dump: str, exe: str, func: str, top: int = 25) -> list[tuple[float, st
                 base = int(line.split()[1], 16)
                 break
     offs: collections.Counter = collections.Counter()
-    for _tname, pcs in samples:
+    for _tname, pcs, _t in samples:
         if len(pcs) < 3:
             continue
         frames = [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
@@ -165,7 +213,7 @@ def callers(dump: str, exe: str, func: str, top: int = 25) -> list[tuple[float, 
     next frame in our code (who called it), as fractions of those samples."""
     samples, resolve = load(dump, exe)
     by: collections.Counter = collections.Counter()
-    for _tname, pcs in samples:
+    for _tname, pcs, _t in samples:
         frames = [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
         if not frames or is_idle(frames):
             continue
@@ -184,7 +232,14 @@ def main() -> int:
     ap.add_argument("--json", default="")
     ap.add_argument("--lines", default="", help="per source line of the leaf frames in functions matching this")
     ap.add_argument("--callers", default="", help="callers of the functions matching this (first own-code frame)")
+    ap.add_argument("--timeline", type=float, default=0.0, help="per-bin view (bin width in ms)")
+    ap.add_argument("--roles", default="xs-sched,xs-bind,xs-informer,python")
+    ap.add_argument("--window", type=float, nargs=2, default=None, help="summary over [A, B) ms only")
     a = ap.parse_args()
+    if a.timeline:
+        for line in timeline(a.dump, a.exe, a.timeline, a.roles.split(",")):
+            print(line)
+        return 0
     if a.callers:
         for frac, f in callers(a.dump, a.exe, a.callers, a.top):
             print(f"{100 * frac:5.1f}%  {f}")
@@ -193,7 +248,7 @@ def main() -> int:
         for frac, loc in lines(a.dump, a.exe, a.lines, a.top):
             print(f"{100 * frac:5.1f}%  {loc}")
         return 0
-    rep = summarize(a.dump, a.exe, a.top)
+    rep = summarize(a.dump, a.exe, a.top, tuple(a.window) if a.window else None)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rep, f, indent=1)
