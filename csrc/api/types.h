@@ -45,7 +45,7 @@ class SharedStrMap {
   SharedStrMap(StrMap m) { *this = std::move(m); }  // NOLINT(google-explicit-constructor)
   SharedStrMap(std::initializer_list<std::pair<std::string, std::string>> l) : SharedStrMap(StrMap(l)) {}
   SharedStrMap& operator=(StrMap m) {
-    p_ = m.empty() ? nullptr : std::make_shared<const StrMap>(std::move(m));
+    p_ = m.empty() ? nullptr : std::make_shared<StrMap>(std::move(m));
     return *this;
   }
   const StrMap& get() const { return p_ ? *p_ : none(); }
@@ -54,11 +54,13 @@ class SharedStrMap {
   StrMap::const_iterator end() const { return get().end(); }
   size_t size() const { return p_ ? p_->size() : 0; }
   bool empty() const { return size() == 0; }
-  // The map for writing: copied first when another object shares it.
+  // The map for writing: copied first when another object shares it. The
+  // map is a non-const object (readers only ever see it through get()), so
+  // writing through the sole owner is well-defined.
   StrMap& mut() {
-    if (!p_) p_ = std::make_shared<const StrMap>();
-    else if (p_.use_count() > 1) p_ = std::make_shared<const StrMap>(*p_);
-    return const_cast<StrMap&>(*p_);
+    if (!p_) p_ = std::make_shared<StrMap>();
+    else if (p_.use_count() > 1) p_ = std::make_shared<StrMap>(*p_);
+    return *p_;
   }
   bool operator==(const SharedStrMap& o) const { return p_ == o.p_ || get() == o.get(); }
   bool operator!=(const SharedStrMap& o) const { return !(*this == o); }
@@ -68,7 +70,7 @@ class SharedStrMap {
     static const StrMap e;
     return e;
   }
-  std::shared_ptr<const StrMap> p_;
+  std::shared_ptr<StrMap> p_;
 };
 
 inline constexpr const char* kHostnameLabel = "kubernetes.io/hostname";

@@ -113,10 +113,13 @@ struct EQSnapshot : StateData {
     used += req;
     return cmp(used, base->sum_min);
   }
-  // PreFilterExtensions AddPod / RemovePod. Terminal pods are not counted in
-  // `used` (the live accounting skips them), so they are not moved here.
+  // PreFilterExtensions AddPod / RemovePod. The reference only moves pods
+  // its quota counts (addPodIfNotPresent / deletePodIfPresent); the live
+  // accounting counts assigned pods while they are Running or Pending (it
+  // drops one on any other phase), so the same filter applies here: removing
+  // an Unknown/Succeeded/Failed victim must not subtract its request again.
   void add(const Pod& p, int sign) {
-    if (!has(p.ns()) || p.phase == "Succeeded" || p.phase == "Failed") return;
+    if (!has(p.ns()) || !(p.phase.empty() || p.phase == "Running" || p.phase == "Pending")) return;
     Res& d = delta[p.ns()];
     if (sign > 0) {
       d += p.request();

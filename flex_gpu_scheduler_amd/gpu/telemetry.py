@@ -56,6 +56,24 @@ def _mean(xs) -> float | None:
     return sum(xs) / len(xs) if xs else None
 
 
+@dataclass
+class GpuReading:
+    """One GPU's utilisation percentages at one sample."""
+    index: int
+    gfx: float | None = None          # GFX engine busy
+    vram_used_pct: float | None = None
+    umc: float | None = None          # HBM controller activity
+    xgmi_pct: float | None = None
+
+
+def aggregate(readings: list[GpuReading], t: float, cpu: float | None = None,
+              memory: float | None = None) -> Sample:
+    """A node's Sample from its GPUs' readings: the mean of each counter over
+    the GPUs that report it (what the node agent publishes for the node)."""
+    return Sample(t, cpu, memory, _mean(r.gfx for r in readings), _mean(r.vram_used_pct for r in readings),
+                  _mean(r.umc for r in readings), _mean(r.xgmi_pct for r in readings))
+
+
 class HostSampler:
     """Reads utilisation percentages of the local host (or a sysfs root).
 
@@ -113,13 +131,14 @@ class HostSampler:
             out.append((busy, 100.0 * used / tot if tot else None))
         return out
 
-    def sample(self) -> Sample:
+    def per_gpu(self) -> list[GpuReading]:
+        """Every visible GPU's reading, in amd-smi / sysfs card order."""
         if self.smi is not None:
-            cs = self.smi.sample()
-            return Sample(time.time(), self._cpu(), self._memory(), _mean(c.gfx for c in cs),
-                          _mean(c.vram_used_pct for c in cs), _mean(c.umc for c in cs), _mean(c.xgmi_pct for c in cs))
-        gs = self.gpu_samples()
-        return Sample(time.time(), self._cpu(), self._memory(), _mean(b for b, _ in gs), _mean(m for _, m in gs))
+            return [GpuReading(i, c.gfx, c.vram_used_pct, c.umc, c.xgmi_pct) for i, c in enumerate(self.smi.sample())]
+        return [GpuReading(i, None if b is None else float(b), m) for i, (b, m) in enumerate(self.gpu_samples())]
+
+    def sample(self) -> Sample:
+        return aggregate(self.per_gpu(), time.time(), self._cpu(), self._memory())
 
 
 class RollingWindow:

@@ -41,11 +41,12 @@ def sample_for(tel, seconds: float, period: float) -> int:
     return n
 
 
-def copy_loop_load():
-    """Keeps cuda:0 busy with 1 GiB device copies until the returned stop()."""
+def copy_loop_load(device: int = 0):
+    """Keeps cuda:`device` busy with 1 GiB device copies until the returned
+    stop()."""
     import torch
 
-    x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")
+    x = torch.empty(1 << 30, dtype=torch.uint8, device=f"cuda:{device}")
     y = torch.empty_like(x)
     stop = threading.Event()
 
@@ -53,7 +54,7 @@ def copy_loop_load():
         while not stop.is_set():
             for _ in range(8):
                 y.copy_(x)
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(device)
 
     th = threading.Thread(target=loop, daemon=True)
     th.start()

@@ -216,30 +216,42 @@ def capacity_preemption(iterations: int = 2) -> dict:
             "note": "includes upstream pod backoff (1s initial) between preemption and re-scheduling"}
 
 
-def _gpu_activity(hs) -> tuple[float | None, float | None, str]:
-    """(GFX busy %, HBM-controller activity %, source) of the host's first GPU."""
-    if getattr(hs, "smi", None) is not None:
-        cs = hs.smi.sample()
-        if cs:
-            return cs[0].gfx, cs[0].umc, "amd-smi (libamd_smi) gfx_activity / umc_activity"
-    live = [b for b, _ in hs.gpu_samples()]
-    if live and live[0] is not None:
-        return float(live[0]), None, "amdgpu sysfs gpu_busy_percent"
-    return None, None, "synthetic"
+def _readings(hs) -> tuple[list, str]:
+    """Per-GPU readings of the host (telemetry.GpuReading list) and their
+    source; [] when the sampler sees no GPU."""
+    from ..gpu.telemetry import GpuReading
+
+    if hasattr(hs, "per_gpu"):
+        rs = hs.per_gpu()
+        src = ("amd-smi (libamd_smi) gfx_activity / umc_activity" if getattr(hs, "smi", None) is not None
+               else "amdgpu sysfs gpu_busy_percent")
+    else:  # a bare sampler (tests): sysfs-style (busy, vram%) pairs
+        rs = [GpuReading(i, None if b is None else float(b), m) for i, (b, m) in enumerate(hs.gpu_samples())]
+        src = "amdgpu sysfs gpu_busy_percent"
+    rs = [r for r in rs if r.gfx is not None]
+    return rs, (src if rs else "synthetic")
 
 
-def _mean_activity(hs, seconds: float, period: float = 0.05) -> tuple[float | None, float | None, str]:
-    gfx, umc, src = [], [], "synthetic"
+def _mean_readings(hs, seconds: float, period: float = 0.05) -> tuple[dict, str]:
+    """Per-GPU mean readings over `seconds`: {gpu index: GpuReading}."""
+    from ..gpu.telemetry import GpuReading
+
+    acc: dict[int, list] = {}
+    src = "synthetic"
     t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end:
-        g, u, src = _gpu_activity(hs)
-        if g is not None:
-            gfx.append(g)
-        if u is not None:
-            umc.append(u)
+    while True:
+        rs, src = _readings(hs)
+        for r in rs:
+            acc.setdefault(r.index, []).append(r)
+        if time.perf_counter() >= t_end:
+            break
         time.sleep(period)
     avg = (lambda xs: round(sum(xs) / len(xs), 1) if xs else None)
-    return avg(gfx), avg(umc), src
+    out = {i: GpuReading(i, avg([r.gfx for r in v if r.gfx is not None]),
+                         avg([r.vram_used_pct for r in v if r.vram_used_pct is not None]),
+                         avg([r.umc for r in v if r.umc is not None]),
+                         avg([r.xgmi_pct for r in v if r.xgmi_pct is not None])) for i, v in acc.items()}
+    return out, src
 
 
 def _cuda_available() -> bool:
@@ -252,47 +264,89 @@ def _cuda_available() -> bool:
 
 
 def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None, start_load=None, seconds: float = 1.0) -> dict:
-    """TargetLoadPacking in GPU mode on `nodes` MI355X nodes whose
-    WatcherMetrics carry live GPU activity of this host: the first half of
-    the nodes publish a sample of the idle GPU, the second half a sample
-    taken while a device copy loop keeps it busy (tools/tlp_live.py; on a
-    GPU host `start_load` defaults to that loop). The busy nodes must score
-    below the idle ones (pkg/trimaran/targetloadpacking/targetloadpacking.go:
-    181-270, target 40 %). Without a GPU the values are synthetic."""
-    from ..gpu.telemetry import HostSampler, NodeTelemetry, Sample, publish
+    """TargetLoadPacking in GPU mode on `nodes` synthetic 8x MI355X nodes
+    whose WatcherMetrics carry live per-GPU activity of this host
+    (pkg/trimaran/targetloadpacking/targetloadpacking.go:181-270, target 40%):
+
+    * with G >= 2 visible GPUs, synthetic node i is backed by physical GPU
+      i mod G (all 8 of its GPU slots), and the GPUs of the upper half
+      (index >= G/2) each run their own device copy loop; every node's
+      document is the node agent's aggregate of its 8 GPUs' readings
+      (telemetry.aggregate), so the loaded GPUs' nodes must score below the
+      idle ones;
+    * with one GPU, the first half of the nodes publish its idle sample and
+      the second half the sample taken under load (`replicated_from_gpu0`);
+    * without a GPU the values are synthetic.
+    `start_load(device)` starts a load on one device and returns its stop();
+    on a GPU host it defaults to tools/tlp_live.copy_loop_load."""
+    from ..gpu.telemetry import GpuReading, NodeTelemetry, aggregate, publish
     from ..control.client import LocalClient
 
     try:
-        hs = sampler or HostSampler()
+        if sampler is not None:
+            hs = sampler
+        else:
+            from ..gpu.telemetry import HostSampler
+
+            hs = HostSampler()
     except Exception:  # noqa: BLE001 - no amd-smi and no amdgpu sysfs
         hs = None
     if start_load is None and sampler is None and _cuda_available():
         from ..tools.tlp_live import copy_loop_load as start_load
-    idle_gfx = idle_umc = busy_gfx = busy_umc = None
+    idle: dict = {}
+    busy_r: dict = {}
     source = "synthetic"
     if hs is not None:
-        idle_gfx, idle_umc, source = _mean_activity(hs, min(0.5, seconds))
-        if start_load is not None and idle_gfx is not None:
-            end = start_load()
-            try:
-                time.sleep(0.3)  # the activity counters ramp over a few samples
-                busy_gfx, busy_umc, _ = _mean_activity(hs, seconds)
-            finally:
-                end()
-    half = nodes // 2
-    if idle_gfx is None:
-        busy = [float((i * 13) % 100) for i in range(nodes)]
-        hbm = [None] * nodes
+        idle, source = _mean_readings(hs, min(0.5, seconds))
+    gpus = sorted(idle)
+    n_gpu = len(gpus)
+    if n_gpu >= 2 and start_load is not None:
+        try:
+            import torch
+
+            n_dev = torch.cuda.device_count() if _cuda_available() else n_gpu
+        except Exception:  # noqa: BLE001
+            n_dev = n_gpu
+        loaded = [g for g in gpus if g >= n_gpu // 2 and g < n_dev]
     else:
-        loaded = busy_gfx if busy_gfx is not None else idle_gfx
-        busy = [idle_gfx if i < half else loaded for i in range(nodes)]
-        hbm = [idle_umc if i < half else (busy_umc if busy_gfx is not None else idle_umc) for i in range(nodes)]
+        loaded = [gpus[0]] if n_gpu == 1 and start_load is not None else []
+    if loaded:
+        stops = [start_load(g) for g in loaded]
+        try:
+            time.sleep(0.3)  # the activity counters ramp over a few samples
+            busy_r, _ = _mean_readings(hs, seconds)
+        finally:
+            for stop in stops:
+                stop()
+    half = nodes // 2
+    node_src: dict[str, object] = {}
+    node_readings: list[list] = []
+    if n_gpu >= 2:
+        view = busy_r or idle
+        for i in range(nodes):
+            g = gpus[i % n_gpu]
+            node_src[f"mi355x-{i}"] = g
+            node_readings.append([view.get(g, idle[g])] * 8)  # the node's 8 GPUs, as the agent sees them
+    elif n_gpu == 1:
+        g = gpus[0]
+        for i in range(nodes):
+            r = busy_r.get(g) if (i >= half and busy_r) else idle[g]
+            node_src[f"mi355x-{i}"] = g
+            node_readings.append([r] * 8)
+    else:
+        for i in range(nodes):
+            node_src[f"mi355x-{i}"] = None
+            node_readings.append([GpuReading(j, float((i * 13) % 100)) for j in range(8)])
+    now = time.time()
+    samples = [aggregate(rs, now) for rs in node_readings]
+    busy = [round(s.gpu, 1) if s.gpu is not None else None for s in samples]
+    hbm = [round(s.hbm_bandwidth, 1) if s.hbm_bandwidth is not None else None for s in samples]
     store = Store()
     store.create_many("nodes", json.dumps([mi355x_node(f"mi355x-{i}") for i in range(nodes)]))
     c = LocalClient(store)
     for i in range(nodes):
         t = NodeTelemetry(f"mi355x-{i}", source=source)
-        t.add(Sample(time.time(), None, None, float(busy[i]), None, hbm[i]))
+        t.add(samples[i])
         publish(c, t.watcher_metrics())
     cfg = {"apiVersion": "kubescheduler.config.k8s.io/v1beta2", "kind": "KubeSchedulerConfiguration",
            "profiles": [{"schedulerName": "default-scheduler", "plugins": {
@@ -311,14 +365,19 @@ def trimaran_tlp(pods: int = 256, nodes: int = 8, sampler=None, start_load=None,
         s.stop()
     scores = {n: v["TargetLoadPacking*1"] for n, v in (first.get("scores") or {}).items()}
     out = {"pods_per_s": round(pods / dt, 1) if ok else None, "metrics_source": source,
+           "gpus_sampled": n_gpu, "replicated_from_gpu0": n_gpu == 1,
+           "node_source_gpu": node_src, "loaded_gpus": loaded,
            "node_gpu_busy_pct": busy, "node_hbm_bandwidth_pct": hbm,
            "first_gpu_pod_node": first.get("selected"), "tlp_scores": scores}
-    if busy_gfx is not None:
-        idle_s = [scores[f"mi355x-{i}"] for i in range(half)]
-        busy_s = [scores[f"mi355x-{i}"] for i in range(half, nodes)]
-        out["live_load"] = {"idle_gpu_busy_pct": idle_gfx, "loaded_gpu_busy_pct": busy_gfx,
-                            "loaded_nodes": [f"mi355x-{i}" for i in range(half, nodes)],
-                            "busy_scores_below_idle": max(busy_s) < min(idle_s)}
+    if busy_r and loaded:
+        loaded_nodes = [n for n, g in node_src.items() if (g in loaded if n_gpu >= 2 else int(n.split("-")[1]) >= half)]
+        idle_nodes = [n for n in node_src if n not in loaded_nodes]
+        out["live_load"] = {
+            "idle_gpu_busy_pct": {g: idle[g].gfx for g in gpus},
+            "loaded_gpu_busy_pct": {g: busy_r[g].gfx for g in loaded if g in busy_r},
+            "loaded_nodes": loaded_nodes,
+            "busy_scores_below_idle": bool(idle_nodes) and max(scores[n] for n in loaded_nodes) < min(
+                scores[n] for n in idle_nodes)}
     return out
 
 
