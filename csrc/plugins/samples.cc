@@ -29,7 +29,14 @@ class NodeResourcesAllocatable : public Plugin {
   bool score_node_local(const Pod&, const Snapshot&) const override { return true; }
   explicit NodeResourcesAllocatable(const Json& args) : Plugin("NodeResourcesAllocatable", kScore) {
     most_ = args["mode"].str_or("Least") == "Most";
-    for (const auto& r : args["resources"].items()) weights_.emplace_back(res_id(r["name"].as_string()), r["weight"].as_int(1));
+    for (const auto& r : args["resources"].items()) {
+      const int64_t w = r["weight"].as_int(1);
+      // NewAllocatable (allocatable.go:80-118)
+      if (w <= 0)
+        throw std::runtime_error("resource Weight of " + r["name"].as_string() + " should be a positive value, got " +
+                                 std::to_string(w));
+      weights_.emplace_back(res_id(r["name"].as_string()), w);
+    }
     if (weights_.empty()) weights_ = {{kCPU, 1 << 20}, {kMemory, 1}};
   }
   std::pair<int64_t, Status> score(CycleState&, const Pod&, const NodeInfo& ni) override {

@@ -2100,6 +2100,60 @@ Json Scheduler::plugin_call(const std::string& plugin, const std::string& point,
     if (assume) cache_->forget_pod(*assumed);
     return out;
   }
+  if (point == "filter" || point == "score") {
+    // One plugin's Filter verdicts / Score+NormalizeScore over the snapshot's
+    // nodes (or args.nodes, in that order), as the reference's plugin unit
+    // tests call them (after the plugin's own PreFilter / PreScore).
+    NodeList nodes;
+    if (args["nodes"].is_array()) {
+      for (const auto& n : args["nodes"].items()) {
+        auto it = snapshot_.index.find(n.as_string());
+        if (it == snapshot_.index.end()) throw std::runtime_error("no node " + n.as_string());
+        nodes.push_back(snapshot_.nodes[it->second].get());
+      }
+    } else {
+      for (const auto& ni : snapshot_.nodes) nodes.push_back(ni.get());
+    }
+    Json out = Json::object();
+    if (point == "filter") {
+      if (pl->points() & kPreFilter) {
+        Status pst = pl->pre_filter(*state, *pod);
+        if (!pst.is_success()) {
+          out.set("preFilter", status_json(pst));
+          return out;
+        }
+      }
+      Json per = Json::object();
+      for (const NodeInfo* ni : nodes) per.set(ni->name(), status_json(pl->filter(*state, *pod, *ni)));
+      out.set("nodes", std::move(per));
+      return out;
+    }
+    if (pl->points() & kPreScore) {
+      Status pst = pl->pre_score(*state, *pod, nodes);
+      if (!pst.is_success()) {
+        out.set("preScore", status_json(pst));
+        return out;
+      }
+    }
+    std::vector<NodeScore> scores(nodes.size());
+    Json raw = Json::object();
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      auto [sc, st] = pl->score(*state, *pod, *nodes[i]);
+      if (!st.is_success()) throw std::runtime_error("score " + nodes[i]->name() + ": " + st.message());
+      scores[i].name = &nodes[i]->name();
+      scores[i].score = sc;
+      raw.set(nodes[i]->name(), Json(sc));
+    }
+    if (pl->has_normalize_score()) {
+      Status nst = pl->normalize_score(*state, *pod, scores);
+      if (!nst.is_success()) throw std::runtime_error("normalize: " + nst.message());
+    }
+    Json norm = Json::object();
+    for (size_t i = 0; i < nodes.size(); ++i) norm.set(nodes[i]->name(), Json(scores[i].score));
+    out.set("raw", std::move(raw));
+    out.set("scores", std::move(norm));
+    return out;
+  }
   if (args["runPreFilter"].as_bool(false)) {
     Status st = fw->run_pre_filter(*state, *pod);
     if (!st.is_success()) return status_json(st);
