@@ -439,9 +439,22 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     return {{"Pod", kDelete, ""}, {"ElasticQuota", kAll, ""}};
   }
 
-  // Unit-test hook (capacity_scheduling_test.go:166 TestDryRunPreemption):
-  // the evaluator's dry run over every snapshot node, after PreFilter.
+  // Unit-test hooks: capacity_scheduling_test.go:166 TestDryRunPreemption
+  // (the evaluator's dry run over every snapshot node, after PreFilter) and
+  // elasticquota_test.go:27/79 (reserveResource / unreserveResource: args.used
+  // plus each of args.pods' effective request, computePodResourceRequest).
   Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) override {
+    if (what == "reserveResource" || what == "unreserveResource") {
+      Res used = Res::from_json(args["used"]);
+      for (const auto& j : args["pods"].items()) {
+        auto q = Pod::from_json(j, *h_.gpu_names);
+        if (what == "reserveResource") used += q->request();
+        else used -= q->request();
+      }
+      Json out = Json::object();
+      out.set("used", used.to_json());
+      return out;
+    }
     if (what != "dryRunPreemption") return Plugin::debug_call(what, s, p, args);
     cur_state_ = &s;
     std::vector<NodeInfoPtr> nodes = h_.snapshot->nodes;

@@ -8,6 +8,7 @@
 // priority < minimum-preemptable-priority (default PC.value+1) and
 // (toleration-seconds < 0, or the victim is not scheduled yet, or it was
 // scheduled less than toleration-seconds ago).
+#include <cerrno>
 #include <cstdlib>
 #include <random>
 
@@ -68,19 +69,27 @@ struct TolerationPolicy {
   int64_t toleration_seconds = 0;
 };
 
-bool parse_policy(const PriorityClass& pc, TolerationPolicy* out) {
+// parsePreemptionTolerationPolicy (preemption_toleration_policy.go:54-82);
+// `err` (optional) receives Go's strconv.ParseInt message on failure.
+bool parse_policy(const PriorityClass& pc, TolerationPolicy* out, std::string* err = nullptr) {
   out->min_preemptable = pc.value + 1;
   out->toleration_seconds = 0;
-  if (const std::string* v = pc.meta.annotation(kAnnMinPreemptable)) {
+  auto parse = [&](const std::string& v, int bits, long long* x) {
     char* e = nullptr;
-    long long x = std::strtoll(v->c_str(), &e, 10);
-    if (v->empty() || *e || x < INT32_MIN || x > INT32_MAX) return false;
+    errno = 0;
+    *x = std::strtoll(v.c_str(), &e, 10);
+    const bool range = errno == ERANGE || (bits == 32 && (*x < INT32_MIN || *x > INT32_MAX));
+    if (!v.empty() && !*e && !range) return true;
+    if (err) *err = "strconv.ParseInt: parsing \"" + v + "\": " + (range && !*e ? "value out of range" : "invalid syntax");
+    return false;
+  };
+  long long x = 0;
+  if (const std::string* v = pc.meta.annotation(kAnnMinPreemptable)) {
+    if (!parse(*v, 32, &x)) return false;
     out->min_preemptable = static_cast<int32_t>(x);
   }
   if (const std::string* v = pc.meta.annotation(kAnnTolerationSeconds)) {
-    char* e = nullptr;
-    long long x = std::strtoll(v->c_str(), &e, 10);
-    if (v->empty() || *e) return false;
+    if (!parse(*v, 64, &x)) return false;
     out->toleration_seconds = x;
   }
   return true;
@@ -92,11 +101,15 @@ class PreemptionToleration : public DefaultPreemption {
     overrides_victims_ = true;
   }
 
-  // ExemptedFromPreemption (preemption_toleration.go:125-175).
-  bool exempted(const Pod& victim, const Pod& preemptor, MicroTime now) const {
+  // ExemptedFromPreemption (preemption_toleration.go:125-175). `err`
+  // (optional) receives the lister's not-found error the reference returns.
+  bool exempted(const Pod& victim, const Pod& preemptor, MicroTime now, std::string* err = nullptr) const {
     if (victim.priority_class_name.empty()) return false;
     auto pc = h_.informers->priority_class(victim.priority_class_name);
-    if (!pc) return false;  // lister miss: no toleration (the reference surfaces the error)
+    if (!pc) {  // lister miss: no toleration (the reference surfaces the error)
+      if (err) *err = "priorityclass.scheduling.k8s.io \"" + victim.priority_class_name + "\" not found";
+      return false;
+    }
     if (preemptor.preemption_policy == "Never") return true;
     TolerationPolicy pol;
     if (!parse_policy(*pc, &pol)) return false;
@@ -104,6 +117,35 @@ class PreemptionToleration : public DefaultPreemption {
     if (pol.toleration_seconds < 0) return true;
     if (victim.scheduled_at == 0) return true;
     return victim.scheduled_at + pol.toleration_seconds * 1000000 > now;
+  }
+
+  // Unit-test hooks for preemption_toleration_test.go (exemptedFromPreemption:
+  // args.victim, args.preemptor, args.nowUs) and
+  // preemption_toleration_policy_test.go (parsePolicy: args.priorityClass).
+  Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) override {
+    Json out = Json::object();
+    if (what == "exemptedFromPreemption") {
+      auto victim = Pod::from_json(args["victim"], *h_.gpu_names);
+      auto preemptor = Pod::from_json(args["preemptor"], *h_.gpu_names);
+      std::string err;
+      const bool ex = exempted(*victim, *preemptor, args["nowUs"].as_int(wall_now_us()), &err);
+      if (!err.empty()) out.set("error", Json(err));
+      else out.set("exempted", Json(ex));
+      return out;
+    }
+    if (what == "parsePolicy") {
+      auto pc = PriorityClass::from_json(args["priorityClass"]);
+      TolerationPolicy pol;
+      std::string err;
+      if (!parse_policy(*pc, &pol, &err)) {
+        out.set("error", Json(err));
+      } else {
+        out.set("minimumPreemptablePriority", Json(static_cast<int64_t>(pol.min_preemptable)));
+        out.set("tolerationSeconds", Json(static_cast<int64_t>(pol.toleration_seconds)));
+      }
+      return out;
+    }
+    return Plugin::debug_call(what, s, p, args);
   }
 
   Status select_victims_on_node(CycleState& s, const Pod& preemptor, NodeInfo& ni, const std::vector<PDBPtr>& pdbs,

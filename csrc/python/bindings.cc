@@ -311,6 +311,9 @@ PYBIND11_MODULE(_xsched, m) {
     x.merge_patch(json_arg(b));
     return to_py(x);
   });
+  // Two-way JSON merge patch from `a` to `b` (util.CreateMergePatch).
+  m.def("diff_merge_patch",
+        [](py::handle a, py::handle b) { return to_py(Json::diff_merge_patch(json_arg(a), json_arg(b))); });
   m.def("rfc3339", [](int64_t us) { return format_rfc3339(us); });
   m.def("native_waiters", [] { return g_native_waiters.load(); });
   m.def("parse_rfc3339", [](const std::string& s) { return parse_rfc3339(s); });
