@@ -227,11 +227,14 @@ Status Framework::run_pre_filter_remove_pod(CycleState& s, const Pod& to_schedul
   return {};
 }
 
-bool Framework::pre_filter_extensions_affected(const CycleState& s, const Pod& to_schedule, const Pod& other) const {
+bool Framework::pre_filter_extensions_affected(const CycleState& s, const Pod& to_schedule, const Pod& other,
+                                               const std::string* except) const {
   auto it = chain_.find(kPreFilter);
   if (it == chain_.end()) return false;
   for (const auto& pl : it->second)
-    if (pl->has_pre_filter_extensions() && pl->pre_filter_extension_affects(s, to_schedule, other)) return true;
+    if (pl->has_pre_filter_extensions() && !(except && pl->name() == *except) &&
+        pl->pre_filter_extension_affects(s, to_schedule, other))
+      return true;
   return false;
 }
 

@@ -103,7 +103,9 @@ class Framework {
   Status run_pre_filter_remove_pod(CycleState& s, const Pod& to_schedule, const PodPtr& to_remove, const NodeInfo& ni);
   // Whether adding or removing `other` changes any PreFilter extension's
   // state for `to_schedule` (Plugin::pre_filter_extension_affects).
-  bool pre_filter_extensions_affected(const CycleState& s, const Pod& to_schedule, const Pod& other) const;
+  // `except` (optional): a plugin name whose extensions are not asked.
+  bool pre_filter_extensions_affected(const CycleState& s, const Pod& to_schedule, const Pod& other,
+                                      const std::string* except = nullptr) const;
   Status run_filter(CycleState& s, const Pod& p, const NodeInfo& ni);
   Status run_filter_with_nominated_pods(CycleState& s, const Pod& p, const NodeInfo& ni);
   // Hash of the nominated pods on `ni` that run_filter_with_nominated_pods

@@ -400,6 +400,7 @@ struct Snapshot {
     auto it = by_name.find(name);
     return it == by_name.end() ? nullptr : it->second;
   }
+  bool has(const std::string& name) const { return by_name.count(name) != 0; }
 };
 
 // -------------------------------------------------------- QueuedPodInfo ----

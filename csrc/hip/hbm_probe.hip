@@ -8,8 +8,10 @@
 //                       16-byte lanes (global_load/store_dwordx4). Variants:
 //                       unroll 1/4/8 (independent 16 B accesses in flight per
 //                       lane), non-temporal vs default cache policy, 4/8/16
-//                       workgroups of 256 threads per CU; probe_bench sweeps
-//                       them and the node agent keeps the fastest. HBM3E peak
+//                       persistent workgroups of 256 threads per CU or a
+//                       one-shot grid (one workgroup per 4 KiB, no loop);
+//                       probe_bench sweeps them and the node agent keeps the
+//                       fastest (profiles/r5*_stream_sweep.md). HBM3E peak
 //                       is 8 TB/s. Each launch is timed by its own event pair
 //                       and the median is reported (the back-to-back batch
 //                       rate, launch gaps included, is kept as a second
@@ -250,6 +252,34 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint32_t* __restrict_
   }
 }
 
+// Counter calibration (xs_segment_access): every wave touches segments of
+// `seg_lanes` x 16 B, each at the start of its own `stride_vec`-vec4 slot, so
+// a dispatch moves a known number of bytes in a known number of 128-B lines
+// (touches x ceil(seg/128)); rocprofv3's L2 memory-side request counters are
+// read against that count (scripts/pmc_calibrate.sh). Lanes >= seg_lanes
+// idle; mode 0 reads, 1 writes.
+template <int MODE, bool NT>
+__global__ __launch_bounds__(kBlock) void k_segments(vec4* __restrict__ buf, size_t touches, size_t stride_vec,
+                                                     int seg_lanes, uint32_t* __restrict__ sink) {
+  const size_t wave = (static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const size_t nwaves = (static_cast<size_t>(gridDim.x) * kBlock) >> 6;
+  const int lane = threadIdx.x & 63;
+  uint32_t acc = 0;
+  const vec4 fill = {5u, 6u, 7u, 8u};
+  if (lane < seg_lanes) {
+    for (size_t t = wave; t < touches; t += nwaves) {
+      vec4* p = buf + t * stride_vec + lane;
+      if constexpr (MODE == 0) {
+        vec4 v = ld<NT>(p);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      } else {
+        st<NT>(fill, p);
+      }
+    }
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
 // Per-launch timing: `launch(i)` enqueues launch i; every launch sits
 // between its own event pair on `s`. out: [median ms, min ms, batch ms per
 // launch (first start to last end / iters)]. Events are created once.
@@ -286,11 +316,13 @@ int cu_count(int dev) {
   return p.multiProcessorCount;
 }
 
-// variant = unroll(1|4|8) | (nt ? 0x100 : 0) | (blocks_per_cu << 16); 0 = default.
+// variant = unroll(1|4|8) | (nt ? 0x100 : 0) | (one_shot ? 0x200 : 0) |
+// (blocks_per_cu << 16); 0 = default.
 struct Variant {
   int unroll = 4;
   bool nt = true;
   int bpc = 8;
+  bool one_shot = false;  // grid = one workgroup per 256 x 16 B x unroll (bpc unused)
 };
 Variant decode(int v) {
   Variant o;
@@ -298,9 +330,20 @@ Variant decode(int v) {
   int u = v & 0xff;
   o.unroll = (u == 1 || u == 4 || u == 8) ? u : 4;
   o.nt = (v & 0x100) != 0;
+  o.one_shot = (v & 0x200) != 0;
   int b = (v >> 16) & 0xff;
   o.bpc = (b == 4 || b == 8 || b == 16) ? b : 8;
   return o;
+}
+
+// Workgroups of a launch over n vec4s: the persistent grid (CUs x bpc), or
+// for a one-shot variant enough workgroups that each lane does `unroll`
+// accesses and exits (capped at 2^22 workgroups, where the kernels' grid
+// stride takes over: past 16 GiB per array).
+int grid_for(const Variant& v, size_t n, int cus) {
+  if (!v.one_shot) return cus * v.bpc;
+  const size_t per = static_cast<size_t>(kBlock) * v.unroll;
+  return static_cast<int>(std::min<size_t>((n + per - 1) / per, size_t{1} << 22));
 }
 
 constexpr uint32_t kWriteSeed = 7;
@@ -335,13 +378,18 @@ void launch(const Variant& v, int mode, int grid, hipStream_t s, void* a, void* 
 
 Variant default_variant(int mode) {
   // Measured optimum per mode on MI355X at the 2 GiB working set
-  // (profiles/r4v_probe_variant_sweep_2GiB.json): one 16-B access per lane
-  // per iteration wins; non-temporal accesses help except for pure writes;
-  // 8 workgroups per CU for read and write, 4 for copy and triad.
+  // (profiles/r5_stream_sweep.md, 648 layouts x unroll x policy x grid):
+  // read: a persistent grid of 8 workgroups per CU, one non-temporal 16-B
+  // load per lane per iteration (~7.0 TB/s, 88%). Write and copy: a one-shot
+  // grid, one workgroup per 4 KiB and no loop (write 6.83 TB/s plain, copy
+  // 6.48 TB/s non-temporal, vs 5.7 / 5.95 for the best persistent grid):
+  // freshly dispatched workgroups keep more stores in flight than a
+  // persistent loop whose waves stall on their own store queue.
   Variant v;
   v.unroll = 1;
   v.nt = mode != 1;
-  v.bpc = (mode == 0 || mode == 1) ? 8 : 4;
+  v.bpc = 8;
+  v.one_shot = mode != 0;
   return v;
 }
 
@@ -392,8 +440,11 @@ int xs_hbm_bandwidth_d(int dev, size_t bytes, int iters, int cu_limit, int mode,
   if (mode == 3) XS_CHECK(hipMalloc(&c.p, bytes));
   XS_CHECK(hipMalloc(&sink.p, sizeof(uint32_t)));
   int cus = cu_count(dev);
-  if (cu_limit > 0 && cu_limit < cus) cus = cu_limit;
-  int grid = cus * v.bpc;
+  if (cu_limit > 0 && cu_limit < cus) {
+    cus = cu_limit;
+    v.one_shot = false;  // a CU budget needs the persistent grid
+  }
+  int grid = grid_for(v, n, cus);
   Stream s;
   XS_CHECK(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
   // Page everything in and warm the launch path.
@@ -435,7 +486,7 @@ int xs_stream_op(int dev, int mode, void* a, void* b, void* c, size_t bytes, uin
                           reinterpret_cast<uintptr_t>(c);
   if (!a || (mode >= 2 && !b) || (mode == 3 && !c) || (align & (sizeof(vec4) - 1))) return -1001;
   Variant v = variant == 0 ? default_variant(mode) : decode(variant);
-  int grid = cu_count(dev) * v.bpc;
+  int grid = grid_for(v, bytes / sizeof(vec4), cu_count(dev));
   launch(v, mode, grid, nullptr, a, b, c, bytes / sizeof(vec4), nullptr, seed, scale);
   XS_CHECK(hipGetLastError());
   XS_CHECK(hipDeviceSynchronize());
@@ -514,6 +565,47 @@ int xs_hbm_bandwidth_xcd_d(int dev, size_t bytes, int iters, uint32_t xcd_mask, 
 int xs_hbm_bandwidth_xcd(int dev, size_t bytes, int iters, uint32_t xcd_mask, int mode, double* gbps,
                          double* ms_per_iter) {
   return xs_hbm_bandwidth_xcd_d(dev, bytes, iters, xcd_mask, mode, gbps, ms_per_iter, nullptr);
+}
+
+// Counter calibration: `touches` segments of `seg_bytes` (16..1024, a
+// multiple of 16), one per `stride_bytes` slot (a multiple of 128, >=
+// seg_bytes), read (mode 0) or written (mode 1), default or non-temporal
+// policy; `iters` timed launches after one warm-up. out: [median ms, bytes
+// per dispatch, 128-B lines per dispatch].
+int xs_segment_access(int dev, int mode, int nt, int seg_bytes, size_t stride_bytes, size_t touches, int iters,
+                      double* out) {
+  XS_CHECK(hipSetDevice(dev));
+  if (mode < 0 || mode > 1 || seg_bytes < 16 || seg_bytes > 1024 || seg_bytes % 16 || stride_bytes % 128 ||
+      stride_bytes < static_cast<size_t>(seg_bytes) || touches == 0)
+    return -1000;
+  if (iters <= 0) iters = 10;
+  const size_t bytes = stride_bytes * touches;
+  const size_t n = bytes / sizeof(vec4);
+  DevMem buf, sink;
+  XS_CHECK(hipMalloc(&buf.p, bytes));
+  XS_CHECK(hipMalloc(&sink.p, sizeof(uint32_t)));
+  const int grid = cu_count(dev) * 8;
+  Stream s;
+  XS_CHECK(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
+  k_write<4, true><<<grid, kBlock, 0, s.s>>>(buf.as<vec4>(), n, 1);  // page in
+  const size_t sv = stride_bytes / sizeof(vec4);
+  const int lanes = seg_bytes / 16;
+  auto go = [&] {
+    if (mode == 0 && nt) k_segments<0, true><<<grid, kBlock, 0, s.s>>>(buf.as<vec4>(), touches, sv, lanes, sink.as<uint32_t>());
+    else if (mode == 0) k_segments<0, false><<<grid, kBlock, 0, s.s>>>(buf.as<vec4>(), touches, sv, lanes, sink.as<uint32_t>());
+    else if (nt) k_segments<1, true><<<grid, kBlock, 0, s.s>>>(buf.as<vec4>(), touches, sv, lanes, sink.as<uint32_t>());
+    else k_segments<1, false><<<grid, kBlock, 0, s.s>>>(buf.as<vec4>(), touches, sv, lanes, sink.as<uint32_t>());
+  };
+  go();
+  XS_CHECK(hipGetLastError());
+  XS_CHECK(hipStreamSynchronize(s.s));
+  double t[3];
+  int rc = time_launches(s.s, iters, [&](int) { go(); }, t);
+  if (rc) return rc;
+  out[0] = t[0];
+  out[1] = static_cast<double>(touches) * seg_bytes;
+  out[2] = static_cast<double>(touches) * ((seg_bytes + 127) / 128);
+  return 0;
 }
 
 // Launches `blocks` single-wave workgroups; returns the number of distinct

@@ -17,6 +17,8 @@
 // Fixed (Appendix C5): the live quota map is only touched under the plugin
 // lock (the reference reads it unlocked in PreFilter / addElasticQuota).
 #include <algorithm>
+#include <array>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <set>
@@ -113,27 +115,143 @@ struct EQSnapshot : StateData {
     used += req;
     return cmp(used, base->sum_min);
   }
+  const Res* delta_of(const std::string& ns) const {
+    auto d = delta.find(ns);
+    return d == delta.end() ? nullptr : &d->second;
+  }
   // PreFilterExtensions AddPod / RemovePod. The reference only moves pods
   // its quota counts (addPodIfNotPresent / deletePodIfPresent); the live
   // accounting counts assigned pods while they are Running or Pending (it
   // drops one on any other phase), so the same filter applies here: removing
   // an Unknown/Succeeded/Failed victim must not subtract its request again.
-  void add(const Pod& p, int sign) {
-    if (!has(p.ns()) || !(p.phase.empty() || p.phase == "Running" || p.phase == "Pending")) return;
-    Res& d = delta[p.ns()];
-    if (sign > 0) {
-      d += p.request();
-      delta_sum += p.request();
-    } else {
-      d -= p.request();
-      delta_sum -= p.request();
-    }
-  }
+  void add(const Pod& p, int sign);
 };
 struct CSPreFilterState : StateData {
   Res pod_req, nominated_in_eq_with_req, nominated_with_req;
   std::shared_ptr<StateData> clone() const override { return std::make_shared<CSPreFilterState>(*this); }
 };
+
+// ---- Guards for the dry-run memo (PreemptionPolicy::guarded_victims) ----
+// SelectVictimsOnNode reads cluster-wide state only through the predicates
+// below, each on the cycle's quota snapshot plus the changes its own dry run
+// made so far on this node (`delta`, a function of the node's pods). While a
+// node is dry-run with recording on, every predicate evaluated is logged
+// with its arguments and outcome; a remembered result is reused for a later
+// preemptor only if each logged predicate, re-evaluated on that cycle's
+// snapshot and PreFilter sums, comes out the same.
+enum GuardKind : uint8_t { kGHas, kGOverMin, kGOverMinWith, kGOverMaxWith, kGAggOverMinWith };
+enum GuardArg : uint8_t { kArgNone, kArgPodReq, kArgInEq, kArgGlobal };
+struct EQGuard {
+  GuardKind kind;
+  GuardArg arg;
+  bool out;
+  std::string ns;
+  Res delta;  // this dry run's change of `used` (per namespace, or summed) when evaluated
+};
+bool same_guard(const EQGuard& a, const EQGuard& b) {
+  return a.kind == b.kind && a.arg == b.arg && a.out == b.out && a.ns == b.ns && a.delta.mask == b.delta.mask &&
+         a.delta == b.delta;
+}
+struct EQGuards : VictimGuards {
+  std::vector<EQGuard> v;
+  uint64_t hash = 0;
+  // Verdict of the last dry run that checked this set (interned sets are
+  // shared by every node whose dry run read the same predicates, so a run
+  // evaluates each distinct set once). Written only with the same value
+  // within a run: the verdict is stored before the run number is published.
+  mutable std::atomic<uint64_t> checked_run{0};
+  mutable std::atomic<bool> verdict{false};
+};
+
+// Interned guard sets: identical nodes (same pods, same quotas) share one.
+class GuardIntern {
+ public:
+  std::shared_ptr<EQGuards> intern(std::shared_ptr<EQGuards> g) {
+    Shard& sh = shards_[g->hash % kShards];
+    std::lock_guard<std::mutex> lk(sh.mu);
+    auto& bucket = sh.m[g->hash];
+    for (const auto& c : bucket)
+      if (c->v.size() == g->v.size() &&
+          std::equal(c->v.begin(), c->v.end(), g->v.begin(), same_guard))
+        return c;
+    if (sh.m.size() > 4096) {  // bounded: memo entries keep their own reference
+      sh.m.clear();
+      sh.m[g->hash].push_back(g);
+      return g;
+    }
+    bucket.push_back(g);
+    return g;
+  }
+
+ private:
+  static constexpr size_t kShards = 64;
+  struct Shard {
+    std::mutex mu;
+    std::unordered_map<uint64_t, std::vector<std::shared_ptr<EQGuards>>> m;
+  };
+  std::array<Shard, kShards> shards_;
+};
+thread_local std::shared_ptr<EQGuards> t_guards;  // recording on this worker (null: off)
+
+const Res& guard_arg(const CSPreFilterState& pfs, GuardArg a) {
+  static const Res kNone;
+  switch (a) {
+    case kArgPodReq: return pfs.pod_req;
+    case kArgInEq: return pfs.nominated_in_eq_with_req;
+    case kArgGlobal: return pfs.nominated_with_req;
+    default: return kNone;
+  }
+}
+
+// The predicate on the snapshot's base quotas with `delta` applied. A
+// namespace without a quota makes every quota predicate false (callers only
+// ask after has(), which is itself a guard).
+bool guard_eval(const EQSnapshot& snap, const CSPreFilterState& pfs, GuardKind k, GuardArg a, const std::string& ns,
+                const Res& delta) {
+  if (k == kGHas) return snap.has(ns);
+  if (k == kGAggOverMinWith) {
+    Res used = snap.base->sum_used;
+    used += delta;
+    used += guard_arg(pfs, a);
+    return cmp(used, snap.base->sum_min);
+  }
+  const Quota* q = snap.find(ns);
+  if (!q) return false;
+  Res used = q->used;
+  used += delta;
+  switch (k) {
+    case kGOverMin: return cmp(used, q->min);
+    case kGOverMinWith: return cmp2(guard_arg(pfs, a), used, q->min);
+    default: return cmp2(guard_arg(pfs, a), used, q->max);
+  }
+}
+
+// Evaluates a predicate on the live dry-run state and logs it when recording.
+bool guarded(const EQSnapshot& snap, const CSPreFilterState* pfs, GuardKind k, GuardArg a, const std::string& ns) {
+  static const CSPreFilterState kNoSums;
+  Res delta;
+  if (k == kGAggOverMinWith) delta = snap.delta_sum;
+  else if (k != kGHas)
+    if (const Res* d = snap.delta_of(ns)) delta = *d;
+  const bool out = guard_eval(snap, pfs ? *pfs : kNoSums, k, a, ns, delta);
+  if (t_guards) t_guards->v.push_back(EQGuard{k, a, out, k == kGAggOverMinWith ? std::string() : ns, std::move(delta)});
+  return out;
+}
+
+void EQSnapshot::add(const Pod& p, int sign) {
+  if (!guarded(*this, nullptr, kGHas, kArgNone, p.ns()) ||
+      !(p.phase.empty() || p.phase == "Running" || p.phase == "Pending"))
+    return;
+  Res& d = delta[p.ns()];
+  if (sign > 0) {
+    d += p.request();
+    delta_sum += p.request();
+  } else {
+    d -= p.request();
+    delta_sum -= p.request();
+  }
+}
+
 constexpr const char* kSnapKey = "CapacityScheduling/ElasticQuotaSnapshot";
 constexpr const char* kStateKey = "PreFilterCapacityScheduling";
 
@@ -254,19 +372,34 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       return {};
     }
     Res in_eq, global;
-    if (h_.snapshot && h_.nominator && !h_.nominator->empty()) {
-      // Pods nominated onto nodes of the snapshot (the reference walks every
-      // node and asks for its nominations).
+    // Pods nominated onto nodes of the snapshot (the reference walks every
+    // node and asks for its nominations): the cycle's nominated map when it
+    // has one (one snapshot lookup per node, not per pod), else the Nominator.
+    // Quotas are looked up once per run of pods of one namespace.
+    const std::string* last_ns = nullptr;
+    const Quota* last_q = nullptr;
+    auto count = [&](const PodPtr& np) {
+      if (np->uid() == pod.uid()) return;
+      if (!last_ns || *last_ns != np->ns()) {
+        last_ns = &np->ns();
+        last_q = snap->find(np->ns());
+      }
+      const Quota* q = last_q;
+      if (!q) return;
+      if (np->ns() == pod.ns() && np->priority >= pod.priority) {
+        in_eq += np->request();
+        global += np->request();
+      } else if (np->ns() != pod.ns() && !q->used_over_min()) {
+        global += np->request();
+      }
+    };
+    if (h_.snapshot && s.nominated) {
+      for (const auto& [node, pods] : *s.nominated)
+        if (!pods.empty() && h_.snapshot->has(node))
+          for (const auto& np : pods) count(np);
+    } else if (h_.snapshot && h_.nominator && !h_.nominator->empty()) {
       h_.nominator->for_each([&](const std::string& node, const PodPtr& np) {
-        if (np->uid() == pod.uid() || !h_.snapshot->get(node)) return;
-        const Quota* q = snap->find(np->ns());
-        if (!q) return;
-        if (np->ns() == pod.ns() && np->priority >= pod.priority) {
-          in_eq += np->request();
-          global += np->request();
-        } else if (np->ns() != pod.ns() && !q->used_over_min()) {
-          global += np->request();
-        }
+        if (h_.snapshot->has(node)) count(np);
       });
     }
     in_eq += pod.request();
@@ -307,6 +440,51 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
   }
   std::pair<int, int> offset_and_num_candidates(int n) override { return {0, n}; }
 
+  // Dry-run memo guards (EQGuard above). Recording starts only when the
+  // cycle's own snapshot carries no changes yet (a PostFilter's does not):
+  // the logged deltas are then this node's alone.
+  bool guarded_victims() const override { return true; }
+  const std::string* guarded_plugin() const override { return &name_; }
+  void start_guards(const CycleState& s) override {
+    auto* snap = s.read_as<EQSnapshot>(kSnapKey);
+    t_guards = snap && snap->delta.empty() && snap->delta_sum.mask == 0 ? std::make_shared<EQGuards>() : nullptr;
+  }
+  std::shared_ptr<const VictimGuards> take_guards() override {
+    std::shared_ptr<EQGuards> g = std::exchange(t_guards, nullptr);
+    if (!g) return nullptr;
+    // Duplicates (the same namespace asked again at the same delta) add
+    // nothing to the check; then intern by content.
+    std::vector<EQGuard> u;
+    u.reserve(g->v.size());
+    for (auto& x : g->v)
+      if (std::none_of(u.begin(), u.end(), [&](const EQGuard& y) { return same_guard(x, y); })) u.push_back(std::move(x));
+    g->v = std::move(u);
+    uint64_t h = 1469598103934665603ULL;
+    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ULL; };
+    for (const auto& x : g->v) {
+      mix(x.kind | (x.arg << 8) | (uint64_t{x.out} << 16));
+      mix(std::hash<std::string>{}(x.ns));
+      mix(x.delta.mask);
+      for (uint64_t m = x.delta.mask; m; m &= m - 1) mix(static_cast<uint64_t>(x.delta.v[__builtin_ctzll(m)]));
+    }
+    g->hash = h;
+    return intern_.intern(std::move(g));
+  }
+  bool guards_hold(const CycleState& s, const VictimGuards& vg, uint64_t run) const override {
+    const auto& g = static_cast<const EQGuards&>(vg);
+    if (g.checked_run.load(std::memory_order_acquire) == run) return g.verdict.load(std::memory_order_relaxed);
+    auto* snap = s.read_as<EQSnapshot>(kSnapKey);
+    auto* pfs = s.read_as<CSPreFilterState>(kStateKey);
+    bool ok = snap && pfs && snap->delta.empty() && snap->delta_sum.mask == 0;
+    for (size_t i = 0; ok && i < g.v.size(); ++i) {
+      const EQGuard& x = g.v[i];
+      ok = guard_eval(*snap, *pfs, x.kind, x.arg, x.ns, x.delta) == x.out;
+    }
+    g.verdict.store(ok, std::memory_order_relaxed);
+    g.checked_run.store(run, std::memory_order_release);
+    return ok;
+  }
+
   bool eligible(const Pod& pod, const Status* nom) override {
     if (pod.preemption_policy == "Never") return false;
     CycleState* s = cur_state_;
@@ -343,7 +521,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
     if (!snap) return Status::unschedulable("Failed to read elasticQuotaSnapshot from cycleState");
     if (!pfs) return Status::unschedulable("Failed to read preFilterState from cycleState");
     Framework& fw = *h_.framework;
-    const bool with_eq = snap->has(pod.ns());
+    const bool with_eq = guarded(*snap, pfs, kGHas, kArgNone, pod.ns());
     auto remove = [&](const PodPtr& p) {
       ni.remove_pod(p->uid());
       return fw.run_pre_filter_remove_pod(s, pod, p, ni);
@@ -359,11 +537,11 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
                      [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*b, *a); });
     std::vector<PodPtr> potential;
     if (with_eq) {
-      bool more_than_min = snap->quota(pod.ns()).used_over_min_with(pfs->nominated_in_eq_with_req);
+      bool more_than_min = guarded(*snap, pfs, kGOverMinWith, kArgInEq, pod.ns());
       for (const auto& p : pods) {
-        if (!snap->has(p->ns())) continue;
+        if (!guarded(*snap, pfs, kGHas, kArgNone, p->ns())) continue;
         bool victim = more_than_min ? (p->ns() == pod.ns() && p->priority < pod.priority)
-                                    : (p->ns() != pod.ns() && snap->quota(p->ns()).used_over_min());
+                                    : (p->ns() != pod.ns() && guarded(*snap, pfs, kGOverMin, kArgNone, p->ns()));
         if (victim) {
           potential.push_back(p);
           Status st = remove(p);
@@ -372,7 +550,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       }
     } else {
       for (const auto& p : pods) {
-        if (snap->has(p->ns())) continue;
+        if (guarded(*snap, pfs, kGHas, kArgNone, p->ns())) continue;
         if (p->priority < pod.priority) {
           potential.push_back(p);
           Status st = remove(p);
@@ -384,8 +562,8 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       return Status::unresolvable("No victims found on node " + ni.name() + " for preemptor pod " + pod.name());
     Status fst = fw.run_filter_with_nominated_pods(s, pod, ni);
     if (!fst.is_success()) return fst;
-    if (with_eq && (snap->quota(pod.ns()).used_over_max_with(pfs->pod_req) ||
-                    snap->aggregated_used_over_min_with(pfs->pod_req)))
+    if (with_eq && (guarded(*snap, pfs, kGOverMaxWith, kArgPodReq, pod.ns()) ||
+                    guarded(*snap, pfs, kGAggOverMinWith, kArgPodReq, pod.ns())))
       return Status::unschedulable("global quota max exceeded");
     std::stable_sort(potential.begin(), potential.end(),
               [](const PodPtr& a, const PodPtr& b) { return more_important_pod(*a, *b); });
@@ -402,8 +580,8 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
       }
       // The reference re-removes (and double-lists) a pod that already
       // failed the fit check; only a reprieved pod is re-checked here.
-      if (fits && with_eq && (snap->quota(pod.ns()).used_over_max_with(pfs->nominated_in_eq_with_req) ||
-                              snap->aggregated_used_over_min_with(pfs->nominated_with_req))) {
+      if (fits && with_eq && (guarded(*snap, pfs, kGOverMaxWith, kArgInEq, pod.ns()) ||
+                              guarded(*snap, pfs, kGAggOverMinWith, kArgGlobal, pod.ns()))) {
         Status rst = remove(p);
         if (!rst.is_success()) return {false, rst};
         victims.push_back(p);
@@ -484,6 +662,7 @@ class CapacityScheduling : public Plugin, public PreemptionPolicy {
   std::shared_ptr<const QuotaView> view_;
   uint64_t view_version_ = ~0ULL;
   CycleState* cur_state_ = nullptr;  // PostFilter runs on the scheduling thread only
+  GuardIntern intern_;
 };
 
 PluginRegistrar reg("CapacityScheduling", [](const Json&, Handle& h) { return std::make_shared<CapacityScheduling>(h); });

@@ -137,18 +137,52 @@ const std::vector<NodeInfoPtr>& nodes_where_preemption_might_help(const Snapshot
 }
 
 struct Evaluator::DryRun {
+  // A slot holds a candidate of the run numbered `run` (older contents are
+  // dead: slots are never reset, each write sets every field).
   struct Slot {
+    uint64_t run = 0;
     const MemoEntry* memo = nullptr;
-    const NodeInfo* node = nullptr;
+    const std::string* name = nullptr;  // memo hits: the node's name
     Candidate c;
+    PickKey key;
   };
   std::vector<Slot> slots;
   std::vector<CandidateRef> refs;  // into slots / memo entries, non-violating first
 };
 
+namespace {
+
+// The victims' share of a PickKey (victims sorted most important first).
+void victim_key_parts(const std::vector<PodPtr>& v, int64_t& top, int64_t& sum, int64_t& earliest) {
+  top = v.empty() ? 0 : v[0]->priority;
+  sum = 0;
+  earliest = LLONG_MAX;
+  for (const auto& p : v) {
+    sum += static_cast<int64_t>(p->priority) + INT32_MAX + 1;
+    earliest = std::min(earliest, pod_start_time(*p));
+  }
+}
+
+PickKey make_key(int npv, int64_t top, int64_t sum, size_t size, int64_t earliest) {
+  return PickKey{npv, top, sum, static_cast<int64_t>(size), earliest == LLONG_MIN ? LLONG_MAX : -earliest};
+}
+
+PickKey key_of(const std::vector<PodPtr>& v, int npv) {
+  int64_t top, sum, earliest;
+  victim_key_parts(v, top, sum, earliest);
+  return make_key(npv, top, sum, v.size(), earliest);
+}
+
+}  // namespace
+
+Evaluator::Evaluator(std::string plugin_name, Handle& h, PreemptionPolicy* policy)
+    : plugin_(std::move(plugin_name)), h_(h), policy_(policy), memo_(std::make_unique<Memo>()) {}
+Evaluator::~Evaluator() = default;
+
 std::vector<Candidate> Evaluator::dry_run(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
                                           const std::vector<PDBPtr>& pdbs, int offset, int num_candidates) {
-  DryRun dr;
+  if (!scratch_) scratch_ = std::make_unique<DryRun>();
+  DryRun& dr = *scratch_;
   dry_run_refs(s, pod, potential, pdbs, offset, num_candidates, dr);
   std::vector<Candidate> out;
   out.reserve(dr.refs.size());
@@ -164,7 +198,9 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
   // PDB can change the violation count, and every Filter is node-local for
   // this pod (the equivalence cache's condition); nodes with nominated pods
   // and nodes where a PreFilter extension reacts to a victim are recomputed.
-  const bool memo_ok = policy_->victims_depend_only_on_node() && pdbs.empty() && pod.template_hash != 0 &&
+  const bool guarded = policy_->guarded_victims();
+  const uint64_t run = ++runs_;
+  const bool memo_ok = (policy_->victims_depend_only_on_node() || guarded) && pdbs.empty() && pod.template_hash != 0 &&
                        h_.snapshot && h_.framework && h_.framework->filters_node_local(pod, *h_.snapshot) &&
                        (s.nominated || !h_.nominator || h_.nominator->empty());
   if (memo_ok) {
@@ -180,11 +216,16 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
   // workers allocate nothing for it). Workers overshoot the stop by at most
   // one node each.
   using Slot = DryRun::Slot;
-  const int cap = num_candidates + 64;
+  // When every node is wanted (CapacityScheduling's offset 0, all nodes)
+  // nothing stops early: node i writes slot i, with no shared counter for 16
+  // workers to bounce (and the candidates keep the nodes' order).
+  const bool by_index = num_candidates >= n;
+  const int cap = by_index ? n : num_candidates + 64;
   std::vector<Slot>& slots = dr.slots;
-  slots.assign(static_cast<size_t>(cap), Slot{});
+  if (slots.size() < static_cast<size_t>(cap)) slots.resize(static_cast<size_t>(cap));
   std::atomic<int> used{0}, non_violating{0};
-  auto claim = [&](int num_pdb_violations) -> Slot* {
+  auto claim = [&](int i, int num_pdb_violations) -> Slot* {
+    if (by_index) return &slots[static_cast<size_t>(i)];
     int k = used.fetch_add(1, std::memory_order_relaxed);
     if (k >= cap) {
       stop.store(true);
@@ -197,27 +238,47 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
   h_.parallelizer->until(n, [&](int i) {
     const NodeInfoPtr& src = potential[(offset + i) % n];
     Memo::Shard* shard = nullptr;
+    const std::vector<PodPtr>* noms = nullptr;
+    uint64_t nom_fp = 0;
     if (memo_ok) {
-      bool nominated_here = false;
       if (s.nominated) {
         auto it = s.nominated->find(src->name());
-        nominated_here = it != s.nominated->end() && !it->second.empty();
+        if (it != s.nominated->end() && !it->second.empty()) noms = &it->second;
       }
-      if (!nominated_here) {
+      // Nominated pods join the node in the Filters the dry run calls: a
+      // guarded policy keys its entry on them (their pods' uid and priority),
+      // the others recompute such nodes.
+      if (noms && guarded) {
+        nom_fp = 0x9e3779b97f4a7c15ULL;
+        for (const auto& np : *noms)
+          nom_fp += std::hash<std::string>{}(np->uid()) * 0xff51afd7ed558ccdULL ^ static_cast<uint64_t>(np->priority);
+      }
+      if (!noms || guarded) {
         shard = &memo_->shards[std::hash<std::string>{}(src->name()) % Memo::kShards];
-        const MemoEntry* hit = nullptr;
+        // Entries are stable for the run: only this worker writes this node's
+        // entries during it, so they are checked outside the lock.
+        std::array<const MemoEntry*, Memo::kVariants> match{};
+        size_t nmatch = 0;
         {
           std::lock_guard<std::mutex> g(shard->mu);
           auto it = shard->m.find(src->name());
-          if (it != shard->m.end() && it->second.gen == src->generation && it->second.tmpl == pod.template_hash)
-            hit = &it->second;  // stable: only this worker writes this node's entry during the run
+          if (it != shard->m.end())
+            for (const MemoEntry& e : it->second.v)
+              if (e.gen == src->generation && e.tmpl == pod.template_hash && e.nominated_fp == nom_fp &&
+                  nmatch < match.size())
+                match[nmatch++] = &e;
         }
+        const MemoEntry* hit = nullptr;
+        for (size_t j = 0; j < nmatch && !hit; ++j)
+          if (!match[j]->guards || policy_->guards_hold(s, *match[j]->guards, run)) hit = match[j];
         if (hit) {
           memo_->hits.fetch_add(1, std::memory_order_relaxed);
           if (!hit->candidate) return;
-          if (Slot* sl = claim(hit->num_pdb_violations)) {
+          if (Slot* sl = claim(i, hit->num_pdb_violations)) {
+            sl->run = run;
             sl->memo = hit;
-            sl->node = src.get();
+            sl->name = &src->name();
+            sl->key = make_key(hit->num_pdb_violations, hit->top, hit->sum, hit->victims.size(), hit->earliest);
           }
           return;
         }
@@ -237,42 +298,80 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
     // instead of deep-cloning it per node.
     std::shared_ptr<CycleState> cloned;
     CycleState* st = &s;
-    for (const auto& q : ni->pods)
-      if (h_.framework->pre_filter_extensions_affected(s, pod, *q)) {
+    // A guarded policy's own extensions are covered by its guards; any other
+    // plugin's extension reacting to a pod here makes the result unmemoizable.
+    bool others_react = false;
+    for (const auto& q : ni->pods) {
+      if (!cloned && h_.framework->pre_filter_extensions_affected(s, pod, *q)) {
         cloned = s.clone();
         st = cloned.get();
+        if (!guarded) break;
+      }
+      if (cloned && guarded && h_.framework->pre_filter_extensions_affected(s, pod, *q, policy_->guarded_plugin())) {
+        others_react = true;
         break;
       }
+    }
+    if (shard && guarded && noms && !others_react)
+      for (const auto& np : *noms)
+        if (h_.framework->pre_filter_extensions_affected(s, pod, *np, policy_->guarded_plugin())) {
+          others_react = true;
+          break;
+        }
+    if (shard && guarded) policy_->start_guards(s);
     Candidate c;
     c.node = ni->name();
     Status vs = policy_->select_victims_on_node(*st, pod, *ni, pdbs, c.victims, c.num_pdb_violations);
+    std::shared_ptr<const VictimGuards> guards = shard && guarded ? policy_->take_guards() : nullptr;
     // An Error is not a property of the node: never remembered.
     const bool candidate = vs.is_success() && !c.victims.empty();
-    if (shard && !cloned && (candidate || vs.is_unschedulable())) {
+    const bool storable = guarded ? guards != nullptr && !others_react : !cloned;
+    if (shard && storable && (candidate || vs.is_unschedulable())) {
       std::lock_guard<std::mutex> g(shard->mu);
-      MemoEntry& e = shard->m[c.node];
+      Memo::NodeMemo& nm = shard->m[c.node];
+      // Results of an older node version are dead; then reuse the slot of
+      // the same key (guarded: the same interned guard set) or rotate.
+      nm.v.erase(std::remove_if(nm.v.begin(), nm.v.end(), [&](const MemoEntry& x) { return x.gen != src->generation; }),
+                 nm.v.end());
+      MemoEntry* slot = nullptr;
+      for (MemoEntry& x : nm.v)
+        if (x.tmpl == pod.template_hash && x.nominated_fp == nom_fp && (!guarded || x.guards == guards)) slot = &x;
+      if (!slot && nm.v.size() < Memo::kVariants) slot = &nm.v.emplace_back();
+      if (!slot) slot = &nm.v[nm.next++ % nm.v.size()];
+      MemoEntry& e = *slot;
       e.gen = src->generation;
       e.tmpl = pod.template_hash;
       e.candidate = candidate;
       e.victims = c.victims;
       e.num_pdb_violations = c.num_pdb_violations;
+      e.guards = std::move(guards);
+      e.nominated_fp = nom_fp;
+      victim_key_parts(e.victims, e.top, e.sum, e.earliest);
     }
     if (!candidate) return;
-    if (Slot* sl = claim(c.num_pdb_violations)) sl->c = std::move(c);
+    if (Slot* sl = claim(i, c.num_pdb_violations)) {
+      sl->run = run;
+      sl->memo = nullptr;
+      sl->key = key_of(c.victims, c.num_pdb_violations);
+      sl->c.node = std::move(c.node);
+      sl->c.victims.swap(c.victims);
+      sl->c.num_pdb_violations = c.num_pdb_violations;
+    }
   }, &stop);
   // Non-violating candidates first, then the violating ones (upstream order).
-  const int k = std::min(used.load(), cap);
+  const int k = by_index ? n : std::min(used.load(), cap);
   dr.refs.clear();
   dr.refs.reserve(static_cast<size_t>(k));
   for (int pass = 0; pass < 2; ++pass) {
     for (int j = 0; j < k; ++j) {
       const Slot& sl = slots[static_cast<size_t>(j)];
+      if (sl.run != run) continue;
       if (sl.memo) {
         if ((sl.memo->num_pdb_violations == 0) != (pass == 0)) continue;
-        dr.refs.push_back(CandidateRef{&sl.node->name(), &sl.memo->victims, sl.memo->num_pdb_violations});
-      } else if (!sl.c.node.empty()) {
+        dr.refs.push_back(CandidateRef{sl.name, &sl.memo->victims, sl.memo->num_pdb_violations, &sl.key});
+      } else {
         if ((sl.c.num_pdb_violations == 0) != (pass == 0)) continue;
-        dr.refs.push_back(CandidateRef{&sl.c.node, &sl.c.victims, sl.c.num_pdb_violations});
+        dr.refs.push_back(CandidateRef{&sl.c.node, &sl.c.victims, sl.c.num_pdb_violations, &sl.key});
       }
     }
   }
@@ -294,17 +393,19 @@ size_t Evaluator::pick_one(const std::vector<CandidateRef>& cands) {
   // highest-priority victim, lowest priority sum, fewest victims, then the
   // latest "earliest victim start"; the first candidate wins a full tie.
   if (cands.empty()) return SIZE_MAX;
-  struct Key {
-    int64_t npv, top, sum, size, neg_earliest;
-    bool operator<(const Key& o) const {
-      return std::tie(npv, top, sum, size, neg_earliest) < std::tie(o.npv, o.top, o.sum, o.size, o.neg_earliest);
-    }
-  };
+  using Key = PickKey;
   size_t best = SIZE_MAX;
   Key best_key{};
   for (size_t i = 0; i < cands.size(); ++i) {
     const auto& v = *cands[i].victims;
     if (v.empty()) return i;  // no preemption needed at all
+    if (cands[i].key) {  // computed by the dry run's worker
+      if (best == SIZE_MAX || *cands[i].key < best_key) {
+        best = i;
+        best_key = *cands[i].key;
+      }
+      continue;
+    }
     // victims are sorted most-important first, so v[0] is the highest priority.
     Key k{cands[i].num_pdb_violations, v[0]->priority, 0, static_cast<int64_t>(v.size()), 0};
     if (best != SIZE_MAX && (k.npv > best_key.npv || (k.npv == best_key.npv && k.top > best_key.top))) continue;
@@ -434,7 +535,8 @@ std::pair<PostFilterResult, Status> Evaluator::preempt(CycleState& s, const Pod&
                                                       " nodes are available: no preemption victims found.")};
   std::vector<PDBPtr> pdbs = h_.informers ? h_.informers->pdbs() : std::vector<PDBPtr>{};
   auto [offset, num] = policy_->offset_and_num_candidates(static_cast<int>(potential.size()));
-  DryRun dr;
+  if (!scratch_) scratch_ = std::make_unique<DryRun>();
+  DryRun& dr = *scratch_;
   dry_run_refs(s, pod, potential, pdbs, offset, num, dr);
   if (dr.refs.empty())
     return {PostFilterResult{}, Status::unschedulable("0/" + std::to_string(h_.snapshot->nodes.size()) +

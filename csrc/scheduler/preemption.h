@@ -19,12 +19,20 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
 #include "framework/plugin.h"
 
 namespace xsched {
+
+// What a guarded policy's victim selection read of cluster-wide state on one
+// node, recorded so a later cycle can re-check it (PreemptionPolicy::
+// guarded_victims). Policy-defined.
+struct VictimGuards {
+  virtual ~VictimGuards() = default;
+};
 
 // The per-plugin policy (preemption.Interface).
 class PreemptionPolicy {
@@ -41,6 +49,23 @@ class PreemptionPolicy {
   // (no clock, no quota or other cluster-wide state): the evaluator may then
   // reuse a node's dry-run result across preemptors (Evaluator::dry_run).
   virtual bool victims_depend_only_on_node() const { return false; }
+  // True when select_victims_on_node's outcome is a function of the node's
+  // version, the preemptor's template and the outcomes of cluster-wide
+  // predicates (quota comparisons) that the policy records on the worker's
+  // thread while it runs (start_guards .. take_guards) and can re-evaluate
+  // against a later cycle's state (guards_hold). The evaluator then reuses a
+  // node's result while every recorded predicate still comes out the same:
+  // identical predicate outcomes drive select_victims_on_node down the same
+  // path to the same victims. `run` numbers the dry run (one at a time per
+  // evaluator), so a policy may cache a verdict per guard set within a run.
+  // Victims leaving and re-entering the node
+  // through the PreFilter extensions of `guarded_plugin()` are covered by the
+  // guards; any other plugin's extension reacting disqualifies the node.
+  virtual bool guarded_victims() const { return false; }
+  virtual void start_guards(const CycleState&) {}
+  virtual std::shared_ptr<const VictimGuards> take_guards() { return nullptr; }
+  virtual bool guards_hold(const CycleState&, const VictimGuards&, uint64_t /*run*/) const { return false; }
+  virtual const std::string* guarded_plugin() const { return nullptr; }
   // True when every victim must have a lower priority than the preemptor:
   // with no such pod on any node the dry run is skipped (it could only find
   // no candidate), which keeps a scheduler overloaded with equal-priority
@@ -53,17 +78,29 @@ struct Candidate {
   std::vector<PodPtr> victims;
   int num_pdb_violations = 0;
 };
-// A candidate by reference (into a dry run's results or a Candidate).
+// pickOneNodeForPreemption's criteria as one lexicographic key: fewest PDB
+// violations, lowest highest-priority victim, lowest priority sum, fewest
+// victims, then the latest "earliest victim start".
+struct PickKey {
+  int64_t npv = 0, top = 0, sum = 0, size = 0, neg_earliest = 0;
+  bool operator<(const PickKey& o) const {
+    return std::tie(npv, top, sum, size, neg_earliest) < std::tie(o.npv, o.top, o.sum, o.size, o.neg_earliest);
+  }
+};
+// A candidate by reference (into a dry run's results or a Candidate); `key`
+// when the dry run already computed it (on its worker, not serially in
+// pick_one).
 struct CandidateRef {
   const std::string* node = nullptr;
   const std::vector<PodPtr>* victims = nullptr;
   int num_pdb_violations = 0;
+  const PickKey* key = nullptr;
 };
 
 class Evaluator {
  public:
-  Evaluator(std::string plugin_name, Handle& h, PreemptionPolicy* policy)
-      : plugin_(std::move(plugin_name)), h_(h), policy_(policy), memo_(std::make_unique<Memo>()) {}
+  Evaluator(std::string plugin_name, Handle& h, PreemptionPolicy* policy);
+  ~Evaluator();
   std::pair<PostFilterResult, Status> preempt(CycleState& s, const Pod& pod, const NodeStatusMap& m);
 
   // Exposed for tests / other plugins.
@@ -88,7 +125,8 @@ class Evaluator {
   void dry_run_refs(CycleState& s, const Pod& pod, const std::vector<NodeInfoPtr>& potential,
                     const std::vector<PDBPtr>& pdbs, int offset, int num_candidates, DryRun& out);
   // Dry-run results per node, valid while (node generation, preemptor
-  // template) match and the node has no nominated pods. PreemptionBasic-like
+  // template) match and the node has no nominated pods (guarded policies:
+  // the same nominated pods, and guards that still hold). PreemptionBasic-like
   // waves evaluate the same unchanged nodes for every preemptor of one
   // template: the reference recomputes each (cloning the NodeInfo and
   // re-running every Filter per reprieved victim), here the result is reused.
@@ -98,12 +136,25 @@ class Evaluator {
     bool candidate = false;
     std::vector<PodPtr> victims;
     int num_pdb_violations = 0;
+    std::shared_ptr<const VictimGuards> guards;  // guarded policies: re-checked on every hit
+    uint64_t nominated_fp = 0;                   // guarded policies: the node's nominated pods (0: none)
+    // The victims' part of the PickKey (highest priority, priority sum,
+    // earliest start), computed once when the entry is stored.
+    int64_t top = 0, sum = 0, earliest = 0;
   };
   struct Memo {
     static constexpr size_t kShards = 256;  // 16 dry-run workers rarely meet on one
+    // A node keeps a few results (for different templates, nominations or
+    // guard outcomes: quota sums near a threshold flip a guard back and forth
+    // as nominations come and go, and each side stays remembered).
+    static constexpr size_t kVariants = 4;
+    struct NodeMemo {
+      std::vector<MemoEntry> v;
+      size_t next = 0;  // round-robin victim once kVariants are held
+    };
     struct Shard {
       std::mutex mu;
-      std::unordered_map<std::string, MemoEntry> m;
+      std::unordered_map<std::string, NodeMemo> m;
     };
     std::array<Shard, kShards> shards;
     std::atomic<uint64_t> hits{0}, misses{0};
@@ -112,6 +163,8 @@ class Evaluator {
   Handle& h_;
   PreemptionPolicy* policy_;
   std::unique_ptr<Memo> memo_;
+  std::unique_ptr<DryRun> scratch_;  // reused across dry runs (slots keep their storage)
+  uint64_t runs_ = 0;  // dry runs so far (PostFilter runs on the scheduling thread only)
 };
 
 // ---- helpers shared by policies ----

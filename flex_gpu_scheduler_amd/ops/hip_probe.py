@@ -80,6 +80,8 @@ class HipProbe:
                                    ctypes.c_size_t, ctypes.c_uint32, ctypes.c_float, ctypes.c_int]
         L.xs_pinned_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                    ctypes.c_uint32]
+        L.xs_segment_access.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                        ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.xs_mfma_last_error.restype = ctypes.c_char_p
         L.xs_mfma_check.argtypes = [ctypes.c_int, ctypes.c_int]
         L.xs_mfma_peak.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
@@ -111,6 +113,10 @@ class HipProbe:
 
     @staticmethod
     def variant(unroll: int = 4, nontemporal: bool = True, blocks_per_cu: int = 8) -> int:
+        """blocks_per_cu 0: the one-shot grid (one workgroup per 4 KiB x
+        unroll, no loop) instead of a persistent one."""
+        if blocks_per_cu == 0:
+            return unroll | (0x100 if nontemporal else 0) | 0x200
         return unroll | (0x100 if nontemporal else 0) | (blocks_per_cu << 16)
 
     def hbm_bandwidth_variant(self, dev: int, nbytes: int, iters: int, mode: str, unroll: int, nontemporal: bool,
@@ -123,7 +129,7 @@ class HipProbe:
         results = []
         for unroll in (1, 4, 8):
             for nt in (True, False):
-                for bpc in (4, 8, 16):
+                for bpc in (0, 4, 8, 16):
                     bw = self.hbm_bandwidth_variant(dev, nbytes, iters, mode, unroll, nt, bpc)
                     results.append({"unroll": unroll, "nontemporal": nt, "blocks_per_cu": bpc,
                                     "GBps": round(bw.gbps, 1)})
@@ -221,6 +227,20 @@ class HipProbe:
             rows[mode_name] = {"xcds": xcds, "cus": xcds * 32, "read_GBps": round(r.gbps, 1),
                                "copy_GBps": round(c.gbps, 1), "read_ms": round(r.ms_per_iter, 4), "kernel": kernel}
         return {"bytes": nbytes, "timing": "median of per-launch event pairs", "partitions": rows}
+
+    def segment_access(self, dev: int = 0, mode: str = "read", seg_bytes: int = 128, stride_bytes: int = 4096,
+                       touches: int = 1 << 18, iters: int = 5, nontemporal: bool = False) -> dict:
+        """k_segments: `touches` segments of `seg_bytes`, one per
+        `stride_bytes` slot -- a dispatch of known bytes and 128-B lines, for
+        calibrating rocprofv3's L2 request counters (scripts/pmc_calibrate.sh)."""
+        out = (ctypes.c_double * 3)()
+        rc = self.lib.xs_segment_access(dev, MODES[mode], int(nontemporal), seg_bytes, stride_bytes, touches, iters,
+                                        out)
+        if rc != 0:
+            raise self._err(rc, "segment_access")
+        return {"kernel": "k_segments", "mode": mode, "nontemporal": nontemporal, "seg_bytes": seg_bytes,
+                "stride_bytes": stride_bytes, "touches": touches, "ms": round(out[0], 4),
+                "bytes_per_dispatch": int(out[1]), "lines128_per_dispatch": int(out[2])}
 
     def xcd_census(self, dev: int = 0, blocks: int = 4096) -> dict:
         hist = (ctypes.c_int * 8)()

@@ -164,9 +164,82 @@ def summarize(root: str) -> str:
     return out
 
 
+def _calib_pass(root: str, name: str, prefix: str | None = None) -> tuple[dict, dict]:
+    """(per-dispatch counters of the measured kernel, probe JSON line) of one
+    calibration pass `pmc_<name>`; `prefix` selects the kernel by name."""
+    d = os.path.join(root, f"pmc_{name}")
+    kern = _pass(d)
+    pj = _probe_line(d + ".log")
+    if prefix:
+        ks = [k for k in kern if k.startswith(prefix)]
+        k = max(ks, key=lambda x: len(kern[x]["ns"])) if ks else None
+    else:
+        k = _measured_kernel(kern, pj)
+    return (kern[k]["counters"] if k else {}), pj
+
+
+def calibration(root: str) -> str:
+    """scripts/pmc_calibrate.sh output (`<root>/pmc_*`) as markdown: the L2
+    memory-side request counters per dispatch of k_segments (known bytes and
+    128-B lines), the raw request counters of the streaming probes, and the
+    MFMA instruction counters of k_mfma_peak against the probe's own count."""
+    out = ["### Reads: k_segments, 2^18 segments per dispatch, one per 4 KiB",
+           "", "| segment | policy | bytes | 128-B lines | TCC_EA0_RDREQ | of which 32B | TCC_BUBBLE (128B) | "
+           "RDREQ_DRAM | RDREQ per line | FETCH_SIZE x1024 / bytes |", "|---|---|---|---|---|---|---|---|---|---|"]
+    for seg in (16, 32, 64, 128, 256, 1024):
+        for pol, tag in (("default", ""), ("nt", "nt-")):
+            c, pj = _calib_pass(root, f"seg-read-{tag}{seg}_req", "k_segments")
+            if not c:
+                continue
+            f, _ = _calib_pass(root, f"seg-read-{tag}{seg}_fetch", "k_segments")
+            lines_, bytes_ = pj.get("lines128_per_dispatch", 0), pj.get("bytes_per_dispatch", 0)
+            rd = c.get("TCC_EA0_RDREQ_sum", 0)
+            fs = f"{f['FETCH_SIZE'] * 1024 / bytes_:.3f}" if f.get("FETCH_SIZE") and bytes_ else "-"
+            out.append(f"| {seg} B | {pol} | {bytes_:,} | {lines_:,} | {rd:,.0f} | {c.get('TCC_EA0_RDREQ_32B_sum', 0):,.0f} | "
+                       f"{c.get('TCC_BUBBLE_sum', 0):,.0f} | {c.get('TCC_EA0_RDREQ_DRAM_sum', 0):,.0f} | "
+                       f"{rd / lines_ if lines_ else 0:.3f} | {fs} |")
+    out += ["", "### Writes: k_segments", "", "| segment | policy | bytes | 128-B lines | TCC_EA0_WRREQ | of which 64B | "
+            "WRREQ_DRAM | WRREQ per line | WRITE_SIZE x1024 / bytes |", "|---|---|---|---|---|---|---|---|---|"]
+    for seg in (16, 32, 64, 128, 256, 1024):
+        for pol, tag in (("default", ""), ("nt", "nt-")):
+            c, pj = _calib_pass(root, f"seg-write-{tag}{seg}_req", "k_segments")
+            if not c:
+                continue
+            w, _ = _calib_pass(root, f"seg-write-{tag}{seg}_wsize", "k_segments")
+            lines_, bytes_ = pj.get("lines128_per_dispatch", 0), pj.get("bytes_per_dispatch", 0)
+            wr = c.get("TCC_EA0_WRREQ_sum", 0)
+            ws = f"{w['WRITE_SIZE'] * 1024 / bytes_:.3f}" if w.get("WRITE_SIZE") and bytes_ else "-"
+            out.append(f"| {seg} B | {pol} | {bytes_:,} | {lines_:,} | {wr:,.0f} | {c.get('TCC_EA0_WRREQ_64B_sum', 0):,.0f} | "
+                       f"{c.get('TCC_EA0_WRREQ_DRAM_sum', 0):,.0f} | {wr / lines_ if lines_ else 0:.3f} | {ws} |")
+    out += ["", "### Streaming probes: raw request counters per dispatch", "",
+            "| probe | kernel bytes read / written | TCC_EA0_RDREQ | 32B | BUBBLE | read requests x 128 B / bytes read | "
+            "TCC_EA0_WRREQ | 64B | write requests x 64 B / bytes written |", "|---|---|---|---|---|---|---|---|---|"]
+    for probe in ("hbm-read", "hbm-copy", "hbm-write"):
+        r, pj = _calib_pass(root, f"{probe}_req")
+        w, _ = _calib_pass(root, f"{probe}_wreq")
+        if not (r or w):
+            continue
+        rb, wb = pj.get("read_bytes", 0), pj.get("write_bytes", 0)
+        rd, wr = r.get("TCC_EA0_RDREQ_sum", 0), w.get("TCC_EA0_WRREQ_sum", 0)
+        out.append(f"| {probe} | {rb / 2**30:.2f} GiB / {wb / 2**30:.2f} GiB | {rd:,.0f} | {r.get('TCC_EA0_RDREQ_32B_sum', 0):,.0f} | "
+                   f"{r.get('TCC_BUBBLE_sum', 0):,.0f} | {rd * 128 / rb if rb else 0:.3f} | {wr:,.0f} | "
+                   f"{w.get('TCC_EA0_WRREQ_64B_sum', 0):,.0f} | {wr * 64 / wb if wb else 0:.3f} |")
+    c, pj = _calib_pass(root, "mfma_insts", "k_mfma_peak")
+    if c:
+        insts, mops = c.get("SQ_INSTS_VALU_MFMA_BF16", 0), c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0)
+        want_i, want_f = pj.get("mfma_insts_per_dispatch", 0), pj.get("flops_per_dispatch", 0)
+        out += ["", "### MFMA: k_mfma_peak counters per dispatch vs the probe's own count", "",
+                "| SQ_INSTS_VALU_MFMA_BF16 | probe MFMA instructions | ratio | SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 | "
+                "probe FLOPs | ratio | SQ_WAVES | probe TFLOP/s |", "|---|---|---|---|---|---|---|---|",
+                f"| {insts:,.0f} | {want_i:,} | {insts / want_i if want_i else 0:.4f} | {mops * 512:,.0f} | {want_f:,} | "
+                f"{mops * 512 / want_f if want_f else 0:.4f} | {c.get('SQ_WAVES', 0):,.0f} | {pj.get('TFLOPs')} |"]
+    return "\n".join(out) + "\n"
+
+
 def main() -> int:
-    root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    sys.stdout.write(summarize(root))
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    root = args[0] if args else "gpurun_out"
+    sys.stdout.write(calibration(root) if "--calibration" in sys.argv else summarize(root))
     return 0
 
 

@@ -6,6 +6,8 @@
            | xcd-read-K | xcd-copy-K   (k_pinned on the first K XCDs: K=1 is
              one CPX partition's CUs, 2 QPX, 4 DPX, 8 the whole GPU)
            | partitions                (the node agent's per-partition table)
+           | seg-{read,write}[-nt]-SEG  (k_segments: 2^18 segments of SEG bytes,
+             one per 4 KiB, for counter calibration)
 
 Prints the probe's own measurement as one JSON line, so a counter pass can be
 cross-checked against the timing the probe reports.
@@ -25,7 +27,9 @@ def main() -> int:
     pr = probe()
     if what == "mfma":
         r = pr.mfma_peak(dev, 0xFF, iters=8192)
-        out = {"kernel": "k_mfma_peak", "TFLOPs": round(r["tflops"], 1), "ms": round(r["ms"], 3)}
+        flops = r["tflops"] * 1e12 * r["ms"] * 1e-3  # per dispatch: every dispatch runs the same tile loop
+        out = {"kernel": "k_mfma_peak", "TFLOPs": round(r["tflops"], 1), "ms": round(r["ms"], 3),
+               "flops_per_dispatch": round(flops), "mfma_insts_per_dispatch": round(flops / (2 * 32 * 32 * 16))}
     elif what in ("hbm-read", "hbm-copy", "hbm-triad", "hbm-write"):
         mode = what.split("-")[1]
         bw = pr.hbm_bandwidth(dev, 2 << 30, iters=iters, mode=mode)
@@ -43,6 +47,9 @@ def main() -> int:
                "read_bytes": 1 << 30, "write_bytes": (1 << 30) if mode == "copy" else 0,
                "GBps": round(bw.gbps, 1), "ms": round(bw.ms_per_iter, 4), "best_GBps": round(bw.best_gbps, 1),
                "batch_GBps": round(bw.batch_gbps, 1), "pct_of_8TBps": round(bw.gbps / 80.0, 1)}
+    elif what.startswith("seg-"):
+        parts = what.split("-")
+        out = pr.segment_access(dev, parts[1], int(parts[-1]), 4096, 1 << 18, iters, nontemporal="nt" in parts)
     elif what == "partitions":
         out = pr.partition_table(dev, 1 << 30, iters)
     else:

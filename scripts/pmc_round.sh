@@ -23,7 +23,7 @@ run mfma mfma SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GR
 for p in hbm-read xcd-read-1 xcd-read-2 xcd-read-4 xcd-read-8; do
   run "${p}_fetch" "$p" FETCH_SIZE GRBM_GUI_ACTIVE || exit $?
 done
-for p in hbm-copy hbm-triad xcd-copy-1 xcd-copy-2 xcd-copy-4 xcd-copy-8; do
+for p in hbm-copy hbm-triad hbm-write xcd-copy-1 xcd-copy-2 xcd-copy-4 xcd-copy-8; do
   run "${p}_fetch" "$p" FETCH_SIZE GRBM_GUI_ACTIVE || exit $?
   run "${p}_write" "$p" WRITE_SIZE GRBM_GUI_ACTIVE || exit $?
 done

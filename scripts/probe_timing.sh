@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUTDIR:-gpurun_out}
 mkdir -p "$OUT"
-for p in hbm-read hbm-copy hbm-triad xcd-read-1 xcd-read-2 xcd-read-4 xcd-read-8 \
+for p in hbm-read hbm-copy hbm-triad hbm-write xcd-read-1 xcd-read-2 xcd-read-4 xcd-read-8 \
          xcd-copy-1 xcd-copy-2 xcd-copy-4 xcd-copy-8; do
   echo "[pmc] plain+trace $p" | tee -a "$OUT/pmc_steps.log"
   timeout -s KILL 60 python3 -m flex_gpu_scheduler_amd.tools.probe_kernels "$p" > "$OUT/plain_$p.log" 2>&1 || exit $?

@@ -87,7 +87,17 @@ def test_partition_bandwidth_table(pr):
 
 def test_tuned_variants_run(pr):
     r = pr.tune(0, "write", 256 << 20, 3)
-    assert len(r["all"]) == 18 and r["best"]["GBps"] > 1000
+    assert len(r["all"]) == 24 and r["best"]["GBps"] > 1000
+    assert any(row["blocks_per_cu"] == 0 for row in r["all"])  # the one-shot grid
+
+
+def test_segment_access_counts(pr):
+    # The counter-calibration kernel: known bytes and 128-B lines per dispatch.
+    for mode, seg in (("read", 64), ("write", 1024)):
+        r = pr.segment_access(0, mode, seg, 4096, 1 << 12, 2)
+        assert r["bytes_per_dispatch"] == (1 << 12) * seg
+        assert r["lines128_per_dispatch"] == (1 << 12) * ((seg + 127) // 128)
+        assert r["ms"] > 0
 
 
 def test_smoke_entry():

@@ -381,3 +381,37 @@ def test_capacity_dry_run_preemption(store, name, quotas, victims_prio, want):
         assert all(c["numPDBViolations"] == 0 for c in got["candidates"])
     finally:
         s.stop()
+
+
+def test_capacity_dry_run_memo_follows_quota_changes(store):
+    """The dry-run memo (Evaluator, guarded by the quota predicates the
+    victim selection read) must not serve a result across a quota change
+    that flips those predicates: the same node, preemptor template and node
+    version give the in-namespace victim under one quota set and the
+    cross-namespace one under the other, then the first again."""
+    store.create("nodes", make_node("node-a", {"memory": "150", "cpu": "100", "pods": "110"}))
+    configs = {"in-namespace": ({"ns1": (50, 200), "ns2": (200, 200)}, ["t1-p1"]),
+               "cross-namespace": ({"ns1": (150, 200), "ns2": (50, 200)}, ["t1-p3"])}
+    for ns, (mn, mx) in configs["in-namespace"][0].items():
+        store.create("elasticquotas", make_elastic_quota(f"eq-{ns}", ns, min={"memory": str(mn)},
+                                                         max={"memory": str(mx)}))
+    prios = {"t1-p1": MID, "t1-p2": HIGH, "t1-p3": MID}
+    for nm, ns in (("t1-p1", "ns1"), ("t1-p2", "ns2"), ("t1-p3", "ns2")):
+        store.create("pods", _mem_pod(nm, ns, 50, prios[nm], node="node-a"))
+    cfg = capacity_config()
+    cfg["profiles"][0]["plugins"]["filter"] = {"enabled": [{"name": "NodeResourcesFit"}]}
+    s = harness(store, cfg)
+    preemptor = _mem_pod("t1-p", "ns1", 50, HIGH)
+    try:
+        for step in ("in-namespace", "in-namespace", "cross-namespace", "cross-namespace", "in-namespace"):
+            quotas, want = configs[step]
+            for ns, (mn, mx) in quotas.items():
+                eq = store.get("elasticquotas", ns, f"eq-{ns}")
+                if eq["spec"]["min"]["memory"] != str(mn):
+                    eq["spec"]["min"]["memory"] = str(mn)
+                    store.update("elasticquotas", eq)
+            s.sync_informers(50)
+            got = s.plugin_call("CapacityScheduling", "dryRunPreemption", {"pod": preemptor, "runPreFilter": True})
+            assert [(c["node"], sorted(c["victims"])) for c in got["candidates"]] == [("node-a", want)], (step, got)
+    finally:
+        s.stop()
