@@ -113,12 +113,19 @@ def run_nodes(nodes: int, waves: int, seed: int, options: dict) -> dict:
         shard.sched.gang_records(True)
         t0 = time.perf_counter()
         pods = 0
+        split: dict[str, float] = {}
         for i in range(2, waves + 2):
-            pods += shard.run(ws[i], prepared=prepared[i], collect_gangs=False).pods
+            r = shard.run(ws[i], prepared=prepared[i], collect_gangs=False)
+            pods += r.pods
+            for k, v in r.split_ms.items():
+                split[k] = split.get(k, 0.0) + v
         dt = time.perf_counter() - t0
         lat = gang_latency_summary(shard.sched.gang_records(True), by_type=True)
+        # Where a wave's time goes: API writes (scheduling overlaps them),
+        # until the last pod is bound, deletion + cache drain.
         return {"nodes": nodes, "waves": waves, "pods": pods, "seconds": round(dt, 3),
                 "pods_per_s": round(pods / dt, 1) if dt > 0 else 0.0,
+                "split_ms_per_wave": {k: round(v / max(1, waves), 2) for k, v in split.items()},
                 "p99_gang_admit_ms": {k: v["p99_ms"] for k, v in lat.items()}}
     finally:
         shard.close()

@@ -279,17 +279,19 @@ bool NodeInfo::remove_pod(const std::string& uid) {
       }
     return false;
   };
+  // One pass over `pods` finds the victim and swap-removes it (order is not
+  // semantic); the affinity lists are searched only when it can be in them.
   PodPtr victim;
-  for (const auto& p : pods)
-    if (p->uid() == uid) {
-      victim = p;
+  for (size_t i = 0; i < pods.size(); ++i)
+    if (pods[i]->uid() == uid) {
+      victim = std::move(pods[i]);
+      pods[i] = std::move(pods.back());
+      pods.pop_back();
       break;
     }
   if (!victim) return false;
-  // Keep `pods` order stable-ish: swap-remove is fine (order is not semantic).
-  erase_from(pods);
-  erase_from(pods_with_affinity);
-  erase_from(pods_with_required_anti_affinity);
+  if (has_affinity(*victim)) erase_from(pods_with_affinity);
+  if (!victim->pod_anti_affinity_required.empty()) erase_from(pods_with_required_anti_affinity);
   requested -= victim->request();
   nonzero_requested -= victim->nonzero_request();
   for (const auto& port : victim->host_ports) used_ports.erase({port.host_ip, port.protocol, port.host_port});

@@ -155,14 +155,17 @@ void SchedulerCache::add_pod_locked(const PodPtr& p) {
 void SchedulerCache::remove_pod_locked(const PodPtr& p) {
   auto it = nodes_.find(p->node_name);
   if (it == nodes_.end()) return;
-  if (writable(it->second).remove_pod(p->uid())) {
+  NodeInfo& ni = writable(it->second);
+  if (ni.remove_pod(p->uid())) {
     group_delta(*p, -1);
-    record_delta(p, *it->second, -1);
+    record_delta(p, ni, -1);
     auto pit = prio_count_.find(p->priority);
     if (pit != prio_count_.end() && --pit->second <= 0) prio_count_.erase(pit);
   }
-  mark_dirty(p->node_name);
-  if (it->second->node == nullptr && it->second->pods.empty()) nodes_.erase(it);
+  // mark_dirty, with the node already found and writable.
+  dirty_.insert(p->node_name);
+  ni.generation = ++generation_;
+  if (ni.node == nullptr && ni.pods.empty()) nodes_.erase(it);
 }
 
 Status SchedulerCache::assume_pod(const PodPtr& p) {

@@ -1,7 +1,7 @@
 // Streaming-kernel design sweep for the HBM probe (csrc/hip/hbm_probe.hip).
 //
-// A standalone executable (built by build_ext.build_stream_sweep, run on the
-// GPU box by scripts/stream_sweep.sh): read / write / copy over 2 GiB arrays
+// A standalone executable (built by build_ext.build_stream_sweep into ops/stream_sweep, run on the
+// GPU box as ops/stream_sweep [modes] [GiB]): read / write / copy over 2 GiB arrays
 // for every combination of
 //   layout  0 grid-stride (a persistent grid walks the array in rows of
 //             grid x 4 KiB; the probe's current shape)

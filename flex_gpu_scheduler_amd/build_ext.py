@@ -127,6 +127,23 @@ def build_hip(verbose: bool = True) -> Path | None:
     return out
 
 
+def build_stream_sweep(verbose: bool = True) -> Path:
+    """The HBM streaming design sweep (csrc/tools/stream_sweep.hip), a
+    standalone gfx950 executable next to the probes: ops/stream_sweep."""
+    hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
+    src = CSRC / "tools" / "stream_sweep.hip"
+    out = PKG / "ops" / "stream_sweep"
+    if out.exists() and out.stat().st_mtime >= src.stat().st_mtime:
+        return out
+    cmd = [hipcc, f"--offload-arch={HIP_ARCH}", "-O3", "-std=c++17", str(src), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stderr[-8000:]}")
+    if verbose:
+        print(f"[build_ext] built {out.relative_to(ROOT)} for {HIP_ARCH}")
+    return out
+
+
 def build_tsan(verbose: bool = True) -> Path:
     """Native concurrency stress driver built with -fsanitize=thread (host only)."""
     includes = [str(CSRC)]

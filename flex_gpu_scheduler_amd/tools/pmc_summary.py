@@ -164,9 +164,10 @@ def summarize(root: str) -> str:
     return out
 
 
-def _calib_pass(root: str, name: str, prefix: str | None = None) -> tuple[dict, dict]:
+def _calib_pass(root: str, name: str, prefix: str | None = None, with_ns: bool = False):
     """(per-dispatch counters of the measured kernel, probe JSON line) of one
-    calibration pass `pmc_<name>`; `prefix` selects the kernel by name."""
+    calibration pass `pmc_<name>`; `prefix` selects the kernel by name. With
+    `with_ns`, also the kernel's dispatch durations (ns)."""
     d = os.path.join(root, f"pmc_{name}")
     kern = _pass(d)
     pj = _probe_line(d + ".log")
@@ -175,6 +176,8 @@ def _calib_pass(root: str, name: str, prefix: str | None = None) -> tuple[dict, 
         k = max(ks, key=lambda x: len(kern[x]["ns"])) if ks else None
     else:
         k = _measured_kernel(kern, pj)
+    if with_ns:
+        return (kern[k]["counters"] if k else {}), pj, (kern[k]["ns"] if k else [])
     return (kern[k]["counters"] if k else {}), pj
 
 
@@ -224,15 +227,20 @@ def calibration(root: str) -> str:
         out.append(f"| {probe} | {rb / 2**30:.2f} GiB / {wb / 2**30:.2f} GiB | {rd:,.0f} | {r.get('TCC_EA0_RDREQ_32B_sum', 0):,.0f} | "
                    f"{r.get('TCC_BUBBLE_sum', 0):,.0f} | {rd * 128 / rb if rb else 0:.3f} | {wr:,.0f} | "
                    f"{w.get('TCC_EA0_WRREQ_64B_sum', 0):,.0f} | {wr * 64 / wb if wb else 0:.3f} |")
-    c, pj = _calib_pass(root, "mfma_insts", "k_mfma_peak")
+    c, pj, ns = _calib_pass(root, "mfma_insts", "k_mfma_peak", with_ns=True)
     if c:
         insts, mops = c.get("SQ_INSTS_VALU_MFMA_BF16", 0), c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0)
         want_i, want_f = pj.get("mfma_insts_per_dispatch", 0), pj.get("flops_per_dispatch", 0)
+        # Counted FLOPs over the profiler's own dispatch times (the fastest
+        # dispatch: the first ones run while the clock ramps).
+        t = min(ns) if ns else 0
         out += ["", "### MFMA: k_mfma_peak counters per dispatch vs the probe's own count", "",
                 "| SQ_INSTS_VALU_MFMA_BF16 | probe MFMA instructions | ratio | SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 | "
-                "probe FLOPs | ratio | SQ_WAVES | probe TFLOP/s |", "|---|---|---|---|---|---|---|---|",
+                "probe FLOPs | ratio | SQ_WAVES | fastest dispatch (trace) | counted FLOPs / dispatch time | "
+                "probe TFLOP/s (event timing) |", "|---|---|---|---|---|---|---|---|---|---|",
                 f"| {insts:,.0f} | {want_i:,} | {insts / want_i if want_i else 0:.4f} | {mops * 512:,.0f} | {want_f:,} | "
-                f"{mops * 512 / want_f if want_f else 0:.4f} | {c.get('SQ_WAVES', 0):,.0f} | {pj.get('TFLOPs')} |"]
+                f"{mops * 512 / want_f if want_f else 0:.4f} | {c.get('SQ_WAVES', 0):,.0f} | {t / 1e6:.3f} ms | "
+                f"{mops * 512 / t / 1e3 if t else 0:,.1f} TFLOP/s | {pj.get('TFLOPs')} |"]
     return "\n".join(out) + "\n"
 
 
