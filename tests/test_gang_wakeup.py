@@ -123,3 +123,51 @@ def test_activation_marks_do_not_outlive_bound_pods(store):
         assert q["in_flight"] == 0 and q["activation_marks"] == 0, q
     finally:
         s.stop()
+
+
+def test_marked_member_retries_once_then_parks():
+    """Retry cadence of the in-flight activation mark (a deliberate deviation,
+    docs/STATUS.md): a member activated while in its cycle goes straight back
+    to activeQ when that cycle fails -- once. Its next failure, with no new
+    activation, parks it in unschedulableQ like any other; the mark does not
+    turn into a retry loop while the group keeps failing."""
+    from flex_gpu_scheduler_amd import Store
+    store = Store()
+    ext = GatedExtender()
+    clock = FakeClock()
+    store.create("nodes", make_node("n0", {"pods": "32", "memory": "300", "cpu": "8"}))
+    store.create("podgroups", make_pod_group("pg", "default", 2))
+    for n in ("a", "b"):
+        store.create("pods", make_pod(n, requests={"memory": "10"}, pod_group="pg"))
+    cfg = coscheduling_config(denied=3)
+    cfg["apiVersion"] = "kubescheduler.config.k8s.io/v1beta3"
+    cfg["extenders"] = [{"urlPrefix": ext.url, "filterVerb": "filter"}]
+    s = new_scheduler(store, load_config(cfg), clock=clock)
+    try:
+        s.sync_informers(20)
+        ext.mode = "reject"
+        assert s.schedule_one(2000) and s.schedule_one(2000)
+        clock.advance(3.0005)
+        s.move_all()
+        ext.mode = "gate"
+        t = threading.Thread(target=s.schedule_one, args=(10000,))
+        t.start()
+        assert ext.entered.wait(10)
+        clock.advance(0.001)
+        s.run_timers()
+        assert s.queue_counts()["activation_marks"] == 1
+        # The marked cycle fails: one retry, straight to activeQ.
+        ext.mode = "reject"
+        ext.release.set()
+        t.join(10)
+        q = s.queue_counts()
+        assert q["active"] == 2 and q["activation_marks"] == 0, q
+        # Both fail again with no activation in between: they park.
+        assert s.schedule_one(2000) and s.schedule_one(2000)
+        q = s.queue_counts()
+        assert q["active"] == 0 and q["backoff"] == 0 and q["unschedulable"] == 2, q
+        assert q["activation_marks"] == 0 and q["in_flight"] == 0, q
+        assert not s.schedule_one(200)  # nothing left to retry before the group's TTL
+    finally:
+        s.stop()
+        ext.close()
