@@ -224,8 +224,9 @@ def calibration(root: str) -> str:
             continue
         rb, wb = pj.get("read_bytes", 0), pj.get("write_bytes", 0)
         rd, wr = r.get("TCC_EA0_RDREQ_sum", 0), w.get("TCC_EA0_WRREQ_sum", 0)
-        out.append(f"| {probe} | {rb / 2**30:.2f} GiB / {wb / 2**30:.2f} GiB | {rd:,.0f} | {r.get('TCC_EA0_RDREQ_32B_sum', 0):,.0f} | "
-                   f"{r.get('TCC_BUBBLE_sum', 0):,.0f} | {rd * 128 / rb if rb else 0:.3f} | {wr:,.0f} | "
+        out.append(f"| {probe} | {rb / 2**30:.2f} GiB / {wb / 2**30:.2f} GiB | {rd:,.0f} | "
+                   f"{r.get('TCC_EA0_RDREQ_32B_sum', 0):,.0f} | {r.get('TCC_BUBBLE_sum', 0):,.0f} | "
+                   f"{rd * 128 / rb if rb else 0:.3f} | {wr:,.0f} | "
                    f"{w.get('TCC_EA0_WRREQ_64B_sum', 0):,.0f} | {wr * 64 / wb if wb else 0:.3f} |")
     c, pj, ns = _calib_pass(root, "mfma_insts", "k_mfma_peak", with_ns=True)
     if c:
