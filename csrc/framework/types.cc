@@ -250,6 +250,7 @@ void NodeInfo::set_node(const NodePtr& n) {
 
 void NodeInfo::add_pod(const PodPtr& p) {
   pods.push_back(p);
+  pod_uid_hashes.push_back(std::hash<std::string>{}(p->uid()));
   if (has_affinity(*p)) pods_with_affinity.push_back(p);
   if (!p->pod_anti_affinity_required.empty()) pods_with_required_anti_affinity.push_back(p);
   requested += p->request();
@@ -279,14 +280,18 @@ bool NodeInfo::remove_pod(const std::string& uid) {
       }
     return false;
   };
-  // One pass over `pods` finds the victim and swap-removes it (order is not
-  // semantic); the affinity lists are searched only when it can be in them.
+  // One pass over the uid hashes finds the victim, which is swap-removed
+  // (order is not semantic); the affinity lists are searched only when it
+  // can be in them.
   PodPtr victim;
+  const uint64_t h = std::hash<std::string>{}(uid);
   for (size_t i = 0; i < pods.size(); ++i)
-    if (pods[i]->uid() == uid) {
+    if (pod_uid_hashes[i] == h && pods[i]->uid() == uid) {
       victim = std::move(pods[i]);
       pods[i] = std::move(pods.back());
       pods.pop_back();
+      pod_uid_hashes[i] = pod_uid_hashes.back();
+      pod_uid_hashes.pop_back();
       break;
     }
   if (!victim) return false;
@@ -311,8 +316,9 @@ bool NodeInfo::remove_pod(const std::string& uid) {
 }
 
 const PodPtr* NodeInfo::find_pod(const std::string& uid) const {
-  for (const auto& p : pods)
-    if (p->uid() == uid) return &p;
+  const uint64_t h = std::hash<std::string>{}(uid);
+  for (size_t i = 0; i < pods.size(); ++i)
+    if (pod_uid_hashes[i] == h && pods[i]->uid() == uid) return &pods[i];
   return nullptr;
 }
 

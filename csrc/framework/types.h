@@ -260,6 +260,10 @@ struct GpuLedger : GpuLedgerState {
 struct NodeInfo {
   NodePtr node;
   std::vector<PodPtr> pods;
+  // std::hash of each pod's uid, parallel to `pods`: remove_pod/find_pod scan
+  // this contiguous array instead of dereferencing every pod (and its uid's
+  // heap buffer) on the node.
+  std::vector<uint64_t> pod_uid_hashes;
   std::vector<PodPtr> pods_with_affinity;
   std::vector<PodPtr> pods_with_required_anti_affinity;
   std::set<std::tuple<std::string, std::string, int32_t>> used_ports;  // (ip, proto, port)

@@ -1,6 +1,7 @@
 #include "scheduler/scheduler.h"
 
 #include "common/log.h"
+#include "common/reaper.h"
 
 #include <algorithm>
 #include <cstring>
@@ -756,6 +757,10 @@ void Scheduler::handle_pod_deletes(const WatchEvent* evs, size_t n) {
   }
   for (const auto& p : gone)
     if (p->node_name.empty()) forget_unassigned_pod(*p);
+  // The lister's and the cache's references are gone: the last ones to the
+  // wave's Pod objects are here, freed off the informer thread.
+  assigned.clear();
+  defer_destroy(std::make_shared<std::vector<PodPtr>>(std::move(gone)));
 }
 
 void Scheduler::handle_pod_event(const WatchEvent& ev) {

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # One MI355X box session. Usage: bash scripts/gpu_session.sh TAG step [step ...]
-# steps: pytest smoke bench bench3 nodes1024 ab1024 abbin1024 sample1024 pmc sched500 sched5000 remote sample_pre sample_sched
+# steps: pytest smoke bench bench3 nodes1024 ab1024 abbin1024 sample1024 timeline1024 pmc sched500 sched5000 remote sample_pre sample_sched
 #        sample_bench rocprof
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure (no retries). A heartbeat line every 60 s keeps long steps visible.
@@ -140,6 +140,18 @@ for step in "$@"; do
         abbin/xsched_stress /tmp/s_1024 6 > "$OUT/n1024.sample_run.txt" 2>&1 &&
       python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/n1024.samples" --exe abbin/xsched_stress --top 40 \
         > "$OUT/n1024_samples.txt" 2>&1 && rm -f "$OUT/n1024.samples" ;;
+    timeline1024)
+      # The 1,024-node waves under the timestamped sampler: per 5-ms bin and
+      # thread role, the busy share and the top own-code frame (wave start-up,
+      # scheduling, deletion drain).
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_1024 --nodes 1024 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      XSCHED_SAMPLE_HZ=4000 XSCHED_SAMPLE="$OUT/t1024.samples" timeout -k 5 200 taskset -c "$cpus" \
+        abbin/xsched_stress /tmp/s_1024 4 > "$OUT/t1024.sample_run.txt" 2>&1 &&
+      python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/t1024.samples" --exe abbin/xsched_stress --timeline 5 \
+        --roles xs-sched,xs-informer,xsched_stress,xs-bind > "$OUT/t1024_timeline.txt" 2>&1 &&
+      python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/t1024.samples" --exe abbin/xsched_stress --top 40 \
+        > "$OUT/t1024_samples.txt" 2>&1 ;;
     rocprof)
       # Kernel trace + per-kernel stats of one short bench run (the probe,
       # health, MFMA and placement kernels on the GPU path).
