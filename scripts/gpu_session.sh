@@ -59,6 +59,17 @@ for step in "$@"; do
       # the default 2 GiB working set.
       timeout -k 10 400 python3 -c "import json; from flex_gpu_scheduler_amd.ops.hip_probe import probe; p = probe(); print(json.dumps([p.tune(mode=m, iters=10) for m in ('read', 'write', 'copy', 'triad')]))" \
         > "$OUT/tune.json" 2> "$OUT/tune.err" ;;
+    treeab1024ol)
+      # A/B of two trees on one box (./abtree, an older commit built in place,
+      # against this tree): the 1,024-node bench with its open-loop search.
+      for i in 1 2; do
+        for t in abtree .; do
+          which=$( [ "$t" = . ] && echo cur || echo old )
+          (cd "$t" && timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios \
+            --no-placement --no-service-mode --nodes1024-waves 0) > "$OUT/treeab1024ol_${which}_$i.json" \
+            2> "$OUT/treeab1024ol_${which}_$i.err" || exit $?
+        done
+      done ;;
     nodes1024_3) for i in 1 2 3; do
                    timeout -k 10 400 python3 bench.py --nodes 1024 --steps 4 --warmup 1 --no-scenarios --no-placement \
                      --no-service-mode > "$OUT/bench_nodes_1024_$i.json" 2> "$OUT/bench_nodes_1024_$i.err" || exit $?
