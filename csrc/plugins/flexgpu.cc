@@ -164,8 +164,17 @@ std::string join_parts(const std::vector<std::pair<int, int>>& v) {
   return s;
 }
 
+// The placement Reserve chose, as the annotation values Bind writes; the
+// Json object is built by Bind, on a binder thread, not in the scheduling
+// cycle.
 struct AssignmentState : StateData {
-  Json annotations = Json::object();
+  std::string index, partitions;  // partitions: empty for whole-GPU / HBM pods
+  Json annotations(const GpuNames& gn) const {
+    Json a = Json::object();
+    a.set(gn.index_annotation, Json(index));
+    if (!partitions.empty()) a.set(gn.partition_annotation, Json(partitions));
+    return a;
+  }
   std::shared_ptr<StateData> clone() const override { return std::make_shared<AssignmentState>(*this); }
 };
 
@@ -286,20 +295,20 @@ class FlexGPU : public Plugin {
         .kv("partitions", join_parts(pl.parts));
     const GpuNames& gn = gn_;
     auto st = std::make_shared<AssignmentState>();
-    st->annotations.set(gn.index_annotation, Json(join_ints(pl.gpus)));
-    if (!pl.parts.empty()) st->annotations.set(gn.partition_annotation, Json(join_parts(pl.parts)));
-    const Json& ann = st->annotations;
+    st->index = join_ints(pl.gpus);
+    if (!pl.parts.empty()) st->partitions = join_parts(pl.parts);
     h_.cache->annotate_assumed_pod(p->uid(), [&](Pod& cp) {
       StrMap& am = cp.meta.annotations.mut();
-      for (const auto& kv : ann.members()) {
-        bool set = false;
+      auto put = [&](const std::string& k, const std::string& v) {
         for (auto& a : am)
-          if (a.first == kv.first) {
-            a.second = kv.second.as_string();
-            set = true;
+          if (a.first == k) {
+            a.second = v;
+            return;
           }
-        if (!set) am.emplace_back(kv.first, kv.second.as_string());
-      }
+        am.emplace_back(k, v);
+      };
+      put(gn.index_annotation, st->index);
+      if (!st->partitions.empty()) put(gn.partition_annotation, st->partitions);
       cp.set_gpu_assignment(pl.gpus, pl.parts, gn);  // what the annotations just written parse to
     }, /*recompute=*/false);
     s.write(kFlexGPUStateKey, st);
@@ -322,7 +331,7 @@ class FlexGPU : public Plugin {
 
   Status bind(CycleState& s, const PodPtr& p, const std::string& node) override {
     Json ann = Json::object();
-    if (auto* st = s.read_as<AssignmentState>(kFlexGPUStateKey)) ann = st->annotations;
+    if (auto* st = s.read_as<AssignmentState>(kFlexGPUStateKey)) ann = st->annotations(gn_);
     try {
       h_.client->bind(*p, node, ann);
     } catch (const std::exception& e) {

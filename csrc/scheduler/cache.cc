@@ -32,7 +32,7 @@ void SchedulerCache::mark_dirty(const std::string& node) {
 
 void SchedulerCache::group_delta(const Pod& p, int d) {
   if (!p.pg_key) return;
-  std::lock_guard<std::mutex> g(group_mu_);
+  std::lock_guard<AdaptiveMutex> g(group_mu_);
   auto it = group_assigned_.try_emplace(p.pg_key, 0).first;
   it->second += d;
   if (it->second <= 0) group_assigned_.erase(it);
@@ -47,7 +47,7 @@ void SchedulerCache::group_delta(const Pod& p, int d) {
 }
 
 std::vector<std::string> SchedulerCache::nodes_of_group(uint64_t pg_key) const {
-  std::lock_guard<std::mutex> g(group_mu_);
+  std::lock_guard<AdaptiveMutex> g(group_mu_);
   std::vector<std::string> out;
   auto it = group_nodes_.find(pg_key);
   if (it != group_nodes_.end())
@@ -96,17 +96,17 @@ void SchedulerCache::set_node_locked(const NodePtr& n) {
 }
 
 void SchedulerCache::add_node(const NodePtr& n) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   set_node_locked(n);
 }
 
 void SchedulerCache::update_node(const NodePtr& n) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   set_node_locked(n);
 }
 
 void SchedulerCache::remove_node(const std::string& name) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = nodes_.find(name);
   if (it == nodes_.end()) return;
   ++node_epoch_;
@@ -123,7 +123,7 @@ void SchedulerCache::remove_node(const std::string& name) {
 }
 
 void SchedulerCache::set_nrt(const std::string& node, const NRTPtr& nrt) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = nodes_.find(node);
   if (it == nodes_.end()) {
     if (!nrt) return;
@@ -169,7 +169,7 @@ void SchedulerCache::remove_pod_locked(const PodPtr& p) {
 }
 
 Status SchedulerCache::assume_pod(const PodPtr& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   if (pod_states_.count(p->uid())) return Status::error("pod " + p->key() + " is in the cache, so can't be assumed");
   in_place_ = true;
   add_pod_locked(p);
@@ -181,7 +181,7 @@ Status SchedulerCache::assume_pod(const PodPtr& p) {
 }
 
 void SchedulerCache::finish_binding(const Pod& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pod_states_.find(p.uid());
   if (it == pod_states_.end() || !assumed_.count(p.uid())) return;
   it->second.binding_finished = true;
@@ -189,7 +189,7 @@ void SchedulerCache::finish_binding(const Pod& p) {
 }
 
 void SchedulerCache::forget_pod(const Pod& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pod_states_.find(p.uid());
   if (it == pod_states_.end()) return;
   if (!assumed_.count(p.uid())) return;  // only assumed pods can be forgotten
@@ -227,7 +227,7 @@ bool SchedulerCache::confirm_assumed_locked(std::unordered_map<std::string, PodS
 }
 
 void SchedulerCache::add_pod(const PodPtr& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pod_states_.find(p->uid());
   if (it != pod_states_.end()) {
     if (assumed_.count(p->uid())) {
@@ -251,7 +251,7 @@ void SchedulerCache::add_pod(const PodPtr& p) {
 }
 
 void SchedulerCache::update_pod(const PodPtr& old_pod, const PodPtr& new_pod) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pod_states_.find(new_pod->uid());
   if (it == pod_states_.end()) {
     add_pod_locked(new_pod);
@@ -274,7 +274,7 @@ void SchedulerCache::update_pod(const PodPtr& old_pod, const PodPtr& new_pod) {
 }
 
 void SchedulerCache::remove_pod(const Pod& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pod_states_.find(p.uid());
   if (it == pod_states_.end()) return;
   remove_pod_locked(it->second.pod);
@@ -284,7 +284,7 @@ void SchedulerCache::remove_pod(const Pod& p) {
 }
 
 void SchedulerCache::remove_pods(const std::vector<PodPtr>& ps) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   for (const auto& p : ps) {
     auto it = pod_states_.find(p->uid());
     if (it == pod_states_.end()) continue;
@@ -296,18 +296,18 @@ void SchedulerCache::remove_pods(const std::vector<PodPtr>& ps) {
 }
 
 bool SchedulerCache::is_assumed(const std::string& uid) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return assumed_.count(uid) > 0;
 }
 
 PodPtr SchedulerCache::get_pod(const std::string& uid) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pod_states_.find(uid);
   return it == pod_states_.end() ? nullptr : it->second.pod;
 }
 
 PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<void(Pod&)>& fn) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pod_states_.find(uid);
   if (it == pod_states_.end()) return nullptr;
   auto fresh = std::make_shared<Pod>(*it->second.pod);
@@ -322,7 +322,7 @@ PodPtr SchedulerCache::mutate_pod(const std::string& uid, const std::function<vo
 PodPtr SchedulerCache::annotate_assumed_pod(const std::string& uid, const std::function<void(Pod&)>& fn,
                                             bool recompute) {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     auto it = pod_states_.find(uid);
     if (it == pod_states_.end()) return nullptr;
     auto nit = nodes_.find(it->second.pod->node_name);
@@ -380,7 +380,7 @@ void sync_affinity_lists(Snapshot& s, size_t i) {
 int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const std::string* check_assumed,
                                     bool* is_assumed) {
   int64_t t0 = lock_wait_us ? clock_->now_us() : 0;
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   if (lock_wait_us) *lock_wait_us = clock_->now_us() - t0;
   if (check_assumed && is_assumed) *is_assumed = assumed_.count(*check_assumed) > 0;
   int clones = 0;
@@ -461,7 +461,7 @@ int SchedulerCache::update_snapshot(Snapshot& s, int64_t* lock_wait_us, const st
 }
 
 void SchedulerCache::cleanup_expired_assumed_pods() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   int64_t now = clock_->now_us();
   std::vector<std::string> expired;
   for (const auto& uid : assumed_) {
@@ -480,31 +480,31 @@ void SchedulerCache::cleanup_expired_assumed_pods() {
 }
 
 int SchedulerCache::assigned_in_group(uint64_t pg_key) const {
-  std::lock_guard<std::mutex> g(group_mu_);
+  std::lock_guard<AdaptiveMutex> g(group_mu_);
   auto it = group_assigned_.find(pg_key);
   return it == group_assigned_.end() ? 0 : it->second;
 }
 
 size_t SchedulerCache::node_count() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return order_.size();
 }
 
 size_t SchedulerCache::pod_count() const { return pod_count_.load(std::memory_order_relaxed); }
 
 size_t SchedulerCache::assumed_count() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return assumed_.size();
 }
 
 NodeInfoPtr SchedulerCache::node_info_copy(const std::string& name) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = nodes_.find(name);
   return it == nodes_.end() ? nullptr : it->second->clone();
 }
 
 std::vector<SchedulerCache::GpuCensusRow> SchedulerCache::gpu_census() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   std::vector<GpuCensusRow> out;
   out.reserve(order_.size());
   std::unordered_map<std::string, size_t> row;
@@ -531,7 +531,7 @@ std::vector<SchedulerCache::GpuCensusRow> SchedulerCache::gpu_census() const {
 }
 
 std::vector<std::string> SchedulerCache::node_names() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return order_;
 }
 
@@ -540,7 +540,7 @@ std::vector<std::string> SchedulerCache::node_names() const {
 namespace xsched {
 
 Json SchedulerCache::check(const std::vector<PodPtr>& assigned, const std::vector<std::string>& nodes) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   Json out = Json::object();
   auto list = [](const std::vector<std::string>& v) {
     Json a = Json::array();
@@ -594,7 +594,7 @@ Json SchedulerCache::check(const std::vector<PodPtr>& assigned, const std::vecto
     if (st.pod->pg_key) ++recount[st.pod->pg_key];
   std::vector<std::string> groups;
   {
-    std::lock_guard<std::mutex> gg(group_mu_);
+    std::lock_guard<AdaptiveMutex> gg(group_mu_);
     for (const auto& [k, c] : recount) {
       auto it = group_assigned_.find(k);
       int have_c = it == group_assigned_.end() ? 0 : it->second;
@@ -619,7 +619,7 @@ Json SchedulerCache::check(const std::vector<PodPtr>& assigned, const std::vecto
 }
 
 Json SchedulerCache::dump() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   Json out = Json::object();
   Json ns = Json::array();
   for (const auto& name : order_) {

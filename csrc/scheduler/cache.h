@@ -14,6 +14,8 @@
 //    workers reading an older snapshot never race with Reserve/Unreserve.
 #pragma once
 
+#include "common/adaptive_mutex.h"
+
 #include <functional>
 #include <map>
 #include <memory>
@@ -134,7 +136,7 @@ class SchedulerCache {
   std::shared_ptr<Clock> clock_;
   int64_t ttl_us_;
   const GpuNames* gpu_names_ = &default_gpu_names();
-  mutable std::mutex mu_;
+  mutable AdaptiveMutex mu_;
   std::unordered_map<std::string, NodeInfoPtr> nodes_;
   std::vector<std::string> order_;  // node names with a Node object, insertion order
   std::unordered_map<std::string, PodState> pod_states_;
@@ -142,7 +144,7 @@ class SchedulerCache {
   std::unordered_set<std::string> assumed_;
   // Written under mu_ + group_mu_, read under group_mu_ only: Permit and
   // PreScore read a gang's count without waiting behind NodeInfo copies.
-  mutable std::mutex group_mu_;
+  mutable AdaptiveMutex group_mu_;
   std::unordered_map<uint64_t, int> group_assigned_;
   // PodGroup key -> (node, members on it): where a gang's assumed or bound
   // members sit (XGMIGangAffinity's co-location test without a per-node look).

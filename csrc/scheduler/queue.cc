@@ -189,7 +189,7 @@ SchedulingQueue::SchedulingQueue(PodHeap::Less less, std::shared_ptr<Clock> cloc
       backoff_([this](const QueuedPodInfo& a, const QueuedPodInfo& b) { return backoff_expiry(a) < backoff_expiry(b); }) {}
 
 void SchedulingQueue::set_cluster_event_map(std::vector<std::pair<ClusterEvent, std::set<std::string>>> m) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   event_map_ = std::move(m);
 }
 
@@ -219,7 +219,7 @@ bool SchedulingQueue::backing_off(const QueuedPodInfo& p) const { return backoff
 
 void SchedulingQueue::add(const PodPtr& p) {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     auto q = new_info(p);
     q->enqueue_seq = ++seq_;
     unschedulable_.erase(p->uid());
@@ -235,7 +235,7 @@ void SchedulingQueue::add(const PodPtr& p) {
 void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
   bool moved = false;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     for (const auto& pod : pods) {
       if (active_.holds(*pod)) continue;  // already active: no uid lookups
       const std::string& uid = pod->uid();
@@ -264,7 +264,7 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
 }
 
 void SchedulingQueue::deactivate(const std::vector<PodPtr>& pods) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   for (const auto& pod : pods) {
     const std::string& uid = pod->uid();
     QueuedPodInfoPtr q;
@@ -288,7 +288,7 @@ void SchedulingQueue::deactivate(const std::vector<PodPtr>& pods) {
 bool SchedulingQueue::add_unschedulable_if_not_present(const QueuedPodInfoPtr& p, int64_t pod_cycle) {
   bool activated = false;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     const std::string& uid = p->pod->uid();
     if (unschedulable_.count(uid) || parked_.count(uid) || active_.contains(uid) || backoff_.contains(uid))
       return false;
@@ -315,24 +315,24 @@ bool SchedulingQueue::add_unschedulable_if_not_present(const QueuedPodInfoPtr& p
 }
 
 size_t SchedulingQueue::pending_activations() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   size_t n = 0;
   for (const auto& kv : in_flight_) n += kv.second == kActivate;
   return n;
 }
 
 size_t SchedulingQueue::in_flight() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return in_flight_.size();
 }
 
 int64_t SchedulingQueue::scheduling_cycle() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return scheduling_cycle_;
 }
 
 QueuedPodInfoPtr SchedulingQueue::pop(int timeout_ms) {
-  std::unique_lock<std::mutex> lk(mu_);
+  std::unique_lock<AdaptiveMutex> lk(mu_);
   auto ready = [&] { return closed_ || !active_.empty(); };
   if (timeout_ms < 0)
     cv_.wait(lk, ready);
@@ -357,7 +357,7 @@ bool pod_spec_changed(const Pod& a, const Pod& b) {
 void SchedulingQueue::update(const PodPtr& old_p, const PodPtr& new_p) {
   bool notify = false;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     const std::string& uid = new_p->uid();
     if (auto q = active_.get(uid)) {
       auto nq = std::make_shared<QueuedPodInfo>(*q);
@@ -412,7 +412,7 @@ void SchedulingQueue::update(const PodPtr& old_p, const PodPtr& new_p) {
 }
 
 void SchedulingQueue::remove(const Pod& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   nominator_->remove(p);
   active_.erase(p.uid());
   backoff_.erase(p.uid());
@@ -431,7 +431,7 @@ bool SchedulingQueue::affinity_term_matches(const Pod& waiting, const Pod& assig
 }
 
 void SchedulingQueue::assigned_pod_added(const Pod& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   in_flight_.erase(p.uid());  // bound: its cycles are over
   std::vector<QueuedPodInfoPtr> match;
   for (const auto& kv : unschedulable_)
@@ -440,7 +440,7 @@ void SchedulingQueue::assigned_pod_added(const Pod& p) {
 }
 
 void SchedulingQueue::assigned_pod_updated(const Pod& p) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   std::vector<QueuedPodInfoPtr> match;
   for (const auto& kv : unschedulable_)
     if (affinity_term_matches(*kv.second->pod, p)) match.push_back(kv.second);
@@ -476,7 +476,7 @@ void SchedulingQueue::move_locked(const std::vector<QueuedPodInfoPtr>& pods, con
 }
 
 void SchedulingQueue::move_all_to_active_or_backoff(const ClusterEvent& ev) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   std::vector<QueuedPodInfoPtr> all;
   all.reserve(unschedulable_.size());
   for (const auto& kv : unschedulable_) all.push_back(kv.second);
@@ -486,7 +486,7 @@ void SchedulingQueue::move_all_to_active_or_backoff(const ClusterEvent& ev) {
 void SchedulingQueue::flush_backoff_completed() {
   bool moved = false;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     while (!backoff_.empty()) {
       const auto& top = backoff_.top();
       if (backing_off(*top)) break;
@@ -498,7 +498,7 @@ void SchedulingQueue::flush_backoff_completed() {
 }
 
 void SchedulingQueue::flush_unschedulable_leftover() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   int64_t now = clock_->now_us();
   std::vector<QueuedPodInfoPtr> stale;
   for (const auto& kv : unschedulable_)
@@ -518,19 +518,19 @@ void SchedulingQueue::flush_unschedulable_leftover() {
 
 void SchedulingQueue::close() {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     closed_ = true;
   }
   cv_.notify_all();
 }
 
 SchedulingQueue::Counts SchedulingQueue::counts() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return Counts{active_.size(), backoff_.size(), unschedulable_.size(), parked_.size()};
 }
 
 std::vector<QueuedPodInfoPtr> SchedulingQueue::pending_pods() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   std::vector<QueuedPodInfoPtr> out = active_.items();
   auto b = backoff_.items();
   out.insert(out.end(), b.begin(), b.end());
@@ -540,7 +540,7 @@ std::vector<QueuedPodInfoPtr> SchedulingQueue::pending_pods() const {
 }
 
 bool SchedulingQueue::has_pod(const std::string& uid) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return active_.contains(uid) || backoff_.contains(uid) || unschedulable_.count(uid) || parked_.count(uid);
 }
 

@@ -7,6 +7,8 @@
 // clusterEventMap filter from plugins' EventsToRegister).
 #pragma once
 
+#include "common/adaptive_mutex.h"
+
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -159,8 +161,10 @@ class SchedulingQueue {
   std::shared_ptr<Clock> clock_;
   QueueOptions opts_;
   Nominator* nominator_;
-  mutable std::mutex mu_;
-  std::condition_variable cv_;
+  // Taken by the scheduling thread per pop and by the informer per event
+  // batch, each time briefly: a spinning mutex (common/adaptive_mutex.h).
+  mutable AdaptiveMutex mu_;
+  std::condition_variable_any cv_;
   PodHeap active_;
   PodHeap backoff_;
   std::unordered_map<std::string, QueuedPodInfoPtr> unschedulable_;

@@ -151,6 +151,17 @@ for step in "$@"; do
         abbin/xsched_stress /tmp/s_1024 6 > "$OUT/n1024.sample_run.txt" 2>&1 &&
       python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/n1024.samples" --exe abbin/xsched_stress --top 40 \
         > "$OUT/n1024_samples.txt" 2>&1 && rm -f "$OUT/n1024.samples" ;;
+    timeline64)
+      # The 64-node headline waves under the timestamped sampler (samples kept
+      # for window reports; symbolize against abbin/xsched_stress).
+      python -m flex_gpu_scheduler_amd.tools.stress /tmp/s_bench --nodes 64 &&
+      cpus=$(python -c "from flex_gpu_scheduler_amd.utils.cpuaffinity import ranked_domains; print(','.join(map(str, ranked_domains()[0])))") &&
+      XSCHED_SAMPLE_HZ=4000 XSCHED_SAMPLE="$OUT/t64.samples" timeout -k 5 200 taskset -c "$cpus" \
+        abbin/xsched_stress /tmp/s_bench 40 > "$OUT/t64.sample_run.txt" 2>&1 &&
+      python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/t64.samples" --exe abbin/xsched_stress --timeline 2 \
+        --roles xs-sched,xs-informer,xsched_stress,xs-bind > "$OUT/t64_timeline.txt" 2>&1 &&
+      python -m flex_gpu_scheduler_amd.tools.sample_report "$OUT/t64.samples" --exe abbin/xsched_stress --top 60 \
+        > "$OUT/t64_samples.txt" 2>&1 ;;
     timeline1024)
       # The 1,024-node waves under the timestamped sampler: per 5-ms bin and
       # thread role, the busy share and the top own-code frame (wave start-up,
