@@ -13,7 +13,7 @@ TimerService::~TimerService() { stop(); }
 
 void TimerService::stop() {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     stop_ = true;
   }
   cv_.notify_all();
@@ -25,7 +25,7 @@ uint64_t TimerService::schedule_at(int64_t deadline_us, Fn fn) {
   uint64_t id;
   bool earliest;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     id = next_id_++;
     Timer t;
     t.fn = std::move(fn);
@@ -44,7 +44,7 @@ uint64_t TimerService::schedule_at(int64_t deadline_us, Fn fn) {
 uint64_t TimerService::every(int64_t period_us, Fn fn) {
   uint64_t id;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     id = next_id_++;
     Timer t;
     t.fn = std::move(fn);
@@ -58,7 +58,7 @@ uint64_t TimerService::every(int64_t period_us, Fn fn) {
 }
 
 bool TimerService::cancel(uint64_t id) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = timers_.find(id);
   if (it == timers_.end()) return false;
   if (it->second.pos != heap_.end()) heap_.erase(it->second.pos);
@@ -67,7 +67,7 @@ bool TimerService::cancel(uint64_t id) {
 }
 
 void TimerService::poke_and_drain() {
-  std::unique_lock<std::mutex> lk(mu_);
+  std::unique_lock<AdaptiveMutex> lk(mu_);
   uint64_t gen = ++poke_gen_;
   ++change_gen_;
   cv_.notify_all();
@@ -75,7 +75,7 @@ void TimerService::poke_and_drain() {
 }
 
 void TimerService::loop() {
-  std::unique_lock<std::mutex> lk(mu_);
+  std::unique_lock<AdaptiveMutex> lk(mu_);
   while (!stop_) {
     int64_t now = clock_->now_us();
     if (!heap_.empty() && heap_.begin()->first <= now) {

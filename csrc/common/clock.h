@@ -8,6 +8,8 @@
 // deterministically instead of sleeping.
 #pragma once
 
+#include "common/adaptive_mutex.h"
+
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -85,8 +87,8 @@ class TimerService {
   void loop();
 
   std::shared_ptr<Clock> clock_;
-  std::mutex mu_;
-  std::condition_variable cv_, drained_cv_;
+  AdaptiveMutex mu_;  // schedule/cancel per waiting pod, from the scheduling and binder threads
+  std::condition_variable_any cv_, drained_cv_;
   std::multimap<int64_t, uint64_t> heap_;
   std::unordered_map<uint64_t, Timer> timers_;
   uint64_t next_id_ = 1;

@@ -5,7 +5,7 @@
 namespace xsched {
 
 std::vector<std::string> WaitingPod::pending_plugins() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   std::vector<std::string> out;
   for (const auto& kv : pending_) out.push_back(kv.first);
   return out;
@@ -14,7 +14,7 @@ std::vector<std::string> WaitingPod::pending_plugins() const {
 bool WaitingPod::allow(const std::string& plugin) {
   std::vector<uint64_t> cancel;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     if (done_) return false;
     auto it = pending_.find(plugin);
     if (it != pending_.end()) {
@@ -35,7 +35,7 @@ bool WaitingPod::allow(const std::string& plugin) {
 bool WaitingPod::reject(const std::string& plugin, const std::string& msg) {
   std::vector<uint64_t> cancel;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     if (done_) return false;
     done_ = true;
     for (const auto& kv : pending_) cancel.push_back(kv.second);
@@ -50,7 +50,7 @@ void WaitingPod::resolve(const Status& st) {
   owner_->remove(pod_->uid());
   Done cb;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     cb = std::move(on_done_);
   }
   if (cb) cb(st);
@@ -62,13 +62,13 @@ WaitingPodPtr WaitingPods::add(const PodPtr& pod, const std::string& node, const
   wp->on_done_ = std::move(on_done);
   wp->created_us_ = timers_->clock().now_us();
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     pods_[pod->uid()] = wp;
     if (pod->pg_key) by_group_[pod->pg_key].push_back(wp);
   }
   // Arm timers after registration so a zero timeout cannot fire before the
   // pod is visible to IterateOverWaitingPods.
-  std::lock_guard<std::mutex> g(wp->mu_);
+  std::lock_guard<AdaptiveMutex> g(wp->mu_);
   for (const auto& kv : timeouts) {
     std::string plugin = kv.first;
     std::weak_ptr<WaitingPod> weak = wp;
@@ -82,7 +82,7 @@ WaitingPodPtr WaitingPods::add(const PodPtr& pod, const std::string& node, const
 }
 
 WaitingPodPtr WaitingPods::get(const std::string& uid) const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pods_.find(uid);
   return it == pods_.end() ? nullptr : it->second;
 }
@@ -90,7 +90,7 @@ WaitingPodPtr WaitingPods::get(const std::string& uid) const {
 void WaitingPods::iterate(const std::function<void(const WaitingPodPtr&)>& fn) const {
   std::vector<WaitingPodPtr> snap;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     snap.reserve(pods_.size());
     for (const auto& kv : pods_) snap.push_back(kv.second);
   }
@@ -100,7 +100,7 @@ void WaitingPods::iterate(const std::function<void(const WaitingPodPtr&)>& fn) c
 void WaitingPods::iterate_group(uint64_t pg_key, const std::function<void(const WaitingPodPtr&)>& fn) const {
   std::vector<WaitingPodPtr> snap;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     auto it = by_group_.find(pg_key);
     if (it == by_group_.end()) return;
     snap = it->second;
@@ -109,12 +109,12 @@ void WaitingPods::iterate_group(uint64_t pg_key, const std::function<void(const 
 }
 
 size_t WaitingPods::size() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return pods_.size();
 }
 
 void WaitingPods::remove(const std::string& uid) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   auto it = pods_.find(uid);
   if (it == pods_.end()) return;
   if (uint64_t key = it->second->pod()->pg_key) {

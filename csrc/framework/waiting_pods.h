@@ -8,6 +8,8 @@
 // no threads.
 #pragma once
 
+#include "common/adaptive_mutex.h"
+
 #include <functional>
 #include <map>
 #include <memory>
@@ -42,7 +44,7 @@ class WaitingPod : public std::enable_shared_from_this<WaitingPod> {
   PodPtr pod_;
   std::string node_;
   WaitingPods* owner_;
-  mutable std::mutex mu_;
+  mutable AdaptiveMutex mu_;
   std::map<std::string, uint64_t> pending_;  // plugin -> timer id
   bool done_ = false;
   Done on_done_;
@@ -69,7 +71,7 @@ class WaitingPods {
   friend class WaitingPod;
   void remove(const std::string& uid);
   TimerService* timers_;
-  mutable std::mutex mu_;
+  mutable AdaptiveMutex mu_;
   std::unordered_map<std::string, WaitingPodPtr> pods_;
   std::unordered_map<uint64_t, std::vector<WaitingPodPtr>> by_group_;
 };

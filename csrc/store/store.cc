@@ -23,7 +23,7 @@ const char* event_type_name(EventType t) {
 // -------------------------------------------------------------- Watcher ----
 void Watcher::push(const WatchEvent& ev) {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     q_.push_back(ev);
   }
   cv_.notify_one();
@@ -31,7 +31,7 @@ void Watcher::push(const WatchEvent& ev) {
 
 void Watcher::push_batch(std::vector<WatchEvent> evs) {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     for (auto& e : evs) q_.push_back(std::move(e));
   }
   cv_.notify_one();
@@ -39,7 +39,7 @@ void Watcher::push_batch(std::vector<WatchEvent> evs) {
 
 std::vector<WatchEvent> Watcher::next(int timeout_ms, size_t max) {
   std::vector<WatchEvent> out;
-  std::unique_lock<std::mutex> lk(mu_);
+  std::unique_lock<AdaptiveMutex> lk(mu_);
   if (q_.empty() && !stopped_.load()) {
     if (timeout_ms < 0)
       cv_.wait(lk, [&] { return !q_.empty() || stopped_.load(); });
@@ -57,14 +57,14 @@ std::vector<WatchEvent> Watcher::next(int timeout_ms, size_t max) {
 
 void Watcher::stop() {
   {
-    std::lock_guard<std::mutex> g(mu_);  // no lost wake-up against next()
+    std::lock_guard<AdaptiveMutex> g(mu_);  // no lost wake-up against next()
     stopped_.store(true);
   }
   cv_.notify_all();
 }
 
 size_t Watcher::pending() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return q_.size();
 }
 

@@ -16,6 +16,8 @@
 // tests that the reference never had.
 #pragma once
 
+#include "common/adaptive_mutex.h"
+
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -76,8 +78,8 @@ class Watcher {
  private:
   std::set<std::string> kinds_;
   std::string ns_;
-  mutable std::mutex mu_;
-  std::condition_variable cv_;
+  mutable AdaptiveMutex mu_;
+  std::condition_variable_any cv_;
   std::deque<WatchEvent> q_;
   std::atomic<bool> stopped_{false};
 };
@@ -164,7 +166,9 @@ class ObjectStore {
                             const std::function<std::optional<Json>(const Json& cur)>& build);
   std::vector<WatchEvent>* batch_ = nullptr;  // bulk ops collect events here (under mu_)
 
-  mutable std::mutex mu_;
+  // Taken by every writer (16 binder threads, the informer's reads, bulk
+  // creates) for short operations: spin before sleeping.
+  mutable AdaptiveMutex mu_;
   // Holds mu_ for one store operation. History entries evicted meanwhile
   // are destroyed after the lock is released: the entry is usually the last
   // reference to a deleted object, and freeing its JSON tree under mu_ made
