@@ -102,7 +102,7 @@ bool Executor::try_pop(std::function<void()>& fn) {
 Executor::Executor(int threads) {
   if (const char* e = std::getenv("XSCHED_BIND_SPIN_NS")) spin_ns_ = std::max<int64_t>(0, std::atoll(e));
   base_ = std::max(1, threads);
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   for (int i = 0; i < base_; ++i) spawn_locked();
 }
 
@@ -124,7 +124,7 @@ void Executor::spawn_locked() {
       }
       bool chain = false;
       {
-        std::unique_lock<std::mutex> lk(mu_);
+        std::unique_lock<AdaptiveMutex> lk(mu_);
         if (!try_pop(fn)) {
           ++waiters_;
           while (!stop_ && q_.empty()) {
@@ -150,7 +150,7 @@ void Executor::spawn_locked() {
 }
 
 void Executor::enter_blocking() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   ++blocked_;
   // Keep `base_` workers able to run tasks (Go's runtime hands a P to a new
   // M when a goroutine blocks in a syscall): the pool grows to the
@@ -159,12 +159,12 @@ void Executor::enter_blocking() {
 }
 
 void Executor::exit_blocking() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   --blocked_;
 }
 
 size_t Executor::threads() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return threads_.size();
 }
 
@@ -181,7 +181,7 @@ Executor::Batch::~Batch() {
   if (fns_.empty()) return;
   bool wake = false;
   {
-    std::lock_guard<std::mutex> g(e_.mu_);
+    std::lock_guard<AdaptiveMutex> g(e_.mu_);
     for (auto& fn : fns_) e_.q_.push_back(std::move(fn));
     e_.queued_.fetch_add(static_cast<int>(fns_.size()), std::memory_order_relaxed);
     if (e_.waiters_ > 0 && e_.wakes_ == 0 && e_.queued_.load(std::memory_order_relaxed) > e_.spinners_.load()) {
@@ -200,7 +200,7 @@ void Executor::submit(std::function<void()> fn) {
     }
   bool wake = false;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     q_.push_back(std::move(fn));
     queued_.fetch_add(1, std::memory_order_relaxed);
     // Wake a sleeper unless a spinning worker is free for this task or a
@@ -215,21 +215,21 @@ void Executor::submit(std::function<void()> fn) {
 
 void Executor::stop() {
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     if (stop_) return;
     stop_ = true;
   }
   cv_.notify_all();
   std::vector<std::thread> ts;
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<AdaptiveMutex> g(mu_);
     ts.swap(threads_);  // no spawn after stop_
   }
   for (auto& t : ts) t.join();
 }
 
 size_t Executor::pending() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<AdaptiveMutex> g(mu_);
   return q_.size() + static_cast<size_t>(busy_.load());
 }
 

@@ -11,6 +11,8 @@
 // not blocked threads), the timer service, and the Filter/Score parallelizer.
 #pragma once
 
+#include "common/adaptive_mutex.h"
+
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -108,8 +110,8 @@ class Executor {
   static constexpr size_t kMaxThreads = 1024;
   int base_ = 1;
   int blocked_ = 0;  // under mu_
-  mutable std::mutex mu_;
-  std::condition_variable cv_;
+  mutable AdaptiveMutex mu_;
+  std::condition_variable_any cv_;
   std::deque<std::function<void()>> q_;
   std::vector<std::thread> threads_;
   bool stop_ = false;
