@@ -105,8 +105,9 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
                        p99_budget_ms: float = 25.0, log: list | None = None) -> float:
     """Sustained open-loop capacity (pods/s), an SLO capacity: the highest
     arrival rate, in steps x1.3 apart from `start_pods_per_s` up to
-    `max_pods_per_s` (the burst capacity) and refined by two bisection steps
-    inside the last interval, at which the p99 PG-create -> last-Bind over
+    `max_pods_per_s` (the burst capacity; when the next step would pass it,
+    the burst rate itself is the next trial) and refined by two bisection
+    steps inside the last interval, at which the p99 PG-create -> last-Bind over
     every gang of the run is within `p99_budget_ms` (a gang still unbound at
     the end counts as infinitely late). Gangs arrive one at a time and are
     held at `occupancy` of the SPX GPUs, as in the measured loads.
@@ -147,10 +148,14 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     while rate <= max_pods_per_s and served(rate):
         best = rate
         rate *= 1.3
-    # Two bisection steps inside the last x1.3 interval when a rate failed
-    # (rather than ran past the burst capacity): the capacity to ~7%.
-    hi = rate
-    if hi <= max_pods_per_s:
+    # Two bisection steps inside the last interval: below the rate that
+    # failed, or, when the next x1.3 step ran past the burst capacity, below
+    # the burst capacity itself (otherwise the grid, not the scheduler, caps
+    # the result at the last step under the burst rate).
+    hi = rate if rate <= max_pods_per_s else max_pods_per_s
+    if hi > best:
+        if rate > max_pods_per_s and served(hi):
+            return hi
         for _ in range(2):
             mid = (best + hi) / 2
             if served(mid):

@@ -144,3 +144,33 @@ def test_burst_wave_interleaves_cpx_gangs_in_queue_order():
     assert cpx[0] < len(names) // 5 and cpx[-1] > len(names) * 4 // 5
     sizes = {pg["spec"]["minMember"] for pg in w.pod_groups if not pg["metadata"]["name"].endswith("-q")}
     assert sizes == {1, 2, 4, 8}
+
+
+def test_capacity_search_reaches_the_burst_rate(monkeypatch):
+    """The search's x1.3 grid must not cap the capacity below the burst rate:
+    when the next step runs past it, the burst rate itself (then bisection
+    under it) is tried, one trial per rate."""
+    from flex_gpu_scheduler_amd.utils import openloop
+
+    tried = []
+
+    def fake_run(shard, rate, duration_s=1.0, seed=0, occupancy=0.5, timeline=False):
+        tried.append(round(rate))
+        ok = rate <= limit
+        return {"all_gangs": {"p99_create_to_bound_ms": 1.0 if ok else 90.0, "unbound": 0,
+                              "p999_create_to_bound_ms": 1.0, "max_create_to_bound_ms": 1.0},
+                "gangs": 10, "wall_s": 1.0, "denials": {"total": 0, "causes": {}}, "denied_gang_fraction": 0.0,
+                "parked_gangs": 0}
+
+    monkeypatch.setattr(openloop, "run_open_loop", fake_run)
+    limit = 1e9  # every rate served: the capacity is the burst rate
+    assert openloop.open_loop_capacity(None, 120_000.0) == 120_000.0
+    assert len(tried) == len(set(tried))  # one trial per rate
+    tried.clear()
+    limit = 110_000.0  # the burst rate fails: bisection between the last grid step and it
+    cap = openloop.open_loop_capacity(None, 120_000.0)
+    assert 102_000 < cap <= 110_000 and 120_000 in tried
+    tried.clear()
+    limit = 50_000.0  # an ordinary failing grid step: unchanged behaviour
+    cap = openloop.open_loop_capacity(None, 120_000.0)
+    assert 45_000 < cap <= 50_000 and max(tried) < 120_000
