@@ -33,7 +33,8 @@ run apiserver apiserver 4   # native HTTP API server: 4 REST clients, 2 watch st
 python -m flex_gpu_scheduler_amd.tools.stress /tmp/san_ol --nodes 16 --openloop 2000 --seconds 0.5 > /dev/null || exit 1
 run openloop /tmp/san_ol 1
 for spec in "PreemptionBasic 200 400" "SchedulingBasic 500 1000" "TopologySpreading 300 600" \
-            "SchedulingPodAntiAffinity 300 300" "Unschedulable 300 600" "MI355X-Gang8 200 800" "MI355X-FlexGPUMix 200 800"; do
+            "SchedulingPodAntiAffinity 300 300" "Unschedulable 300 600" "MI355X-Gang8 200 800" "MI355X-FlexGPUMix 200 800" \
+            "CapacityScheduling-Reclaim 300 300"; do
   set -- $spec
   python -m flex_gpu_scheduler_amd.tools.stress "/tmp/san_$1" --workload "$1" --nodes "$2" --pods "$3" > /dev/null \
     || { echo "skip $1 (no such workload)" | tee -a "$out"; continue; }
