@@ -537,15 +537,21 @@ Status Framework::run_score(CycleState& s, const Pod& p, const NodeList& nodes,
       const int64_t* sgen = table->score_gen.data();
       const uint64_t* pm = table->plain_mask.data();
       const uint64_t* cm = table->cols.data();
-      // Branch-free: hits and misses interleave unpredictably.
+      // Branch-free: hits and misses interleave unpredictably. Raw pointers:
+      // through the thread_local vectors every char store could alias their
+      // bookkeeping and forced a reload of the TLS slot per node.
       miss.resize(n);
       size_t nm = 0;
+      char* hp = hit.data();
+      uint32_t* mp = miss.data();
+      const int64_t* eg = have_gens ? eq->gen : nullptr;
+      const uint64_t pmask = plain_mask, rmask = row_mask;
       for (size_t i = 0; i < n; ++i) {
         const size_t pos = static_cast<size_t>(tpos[i]);
-        const int64_t gen = have_gens ? eq->gen[pos] : nodes[i]->generation;
-        const bool h = (sgen[pos] == gen) & (pm[pos] == plain_mask) & ((cm[pos] & row_mask) == row_mask);
-        hit[i] = h;
-        miss[nm] = static_cast<uint32_t>(i);
+        const int64_t gen = eg ? eg[pos] : nodes[i]->generation;
+        const bool h = (sgen[pos] == gen) & (pm[pos] == pmask) & ((cm[pos] & rmask) == rmask);
+        hp[i] = h;
+        mp[nm] = static_cast<uint32_t>(i);
         nm += !h;
       }
       miss.resize(nm);

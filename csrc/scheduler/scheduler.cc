@@ -1390,14 +1390,31 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
       }
       off0 += run;
     }
-    // Re-cut the list: branch-free appends (the buffers hold to_find + 1).
+    // Re-cut the list: branch-free appends (the buffers hold to_find + 1),
+    // over the window's two contiguous runs ([start, n), then [0, ...)), with
+    // every bound and base pointer in a local: a store to the int buffer
+    // could alias `start`, whose address the lambdas above hold, and forced
+    // a reload per node.
     int off = 0;
-    const char* okv = memo->ok.data();
-    for (; ok && off < m && c < to_find; ++off) {
-      const int pos = at(off);
-      found_buf_[c] = all[pos].get();
-      found_pos_buf_[c] = pos;
-      c += okv[off] != 0;
+    if (ok) {
+      const char* okv = memo->ok.data();
+      const NodeInfoPtr* allp = all.data();
+      const NodeInfo** fb = found_buf_.data();
+      int* fpb = found_pos_buf_.data();
+      const int s0 = start, nn = n, mm = m, want = to_find;
+      int cc = c;
+      for (int run = 0; run < 2 && off < mm && cc < want; ++run) {
+        const int first_off = off;
+        const int first_pos = run == 0 ? s0 : 0;
+        const int end_off = run == 0 ? std::min(mm, nn - s0) : mm;
+        for (; off < end_off && cc < want; ++off) {
+          const int pos = first_pos + (off - first_off);
+          fb[cc] = allp[pos].get();
+          fpb[cc] = pos;
+          cc += okv[off] != 0;
+        }
+      }
+      c = cc;
     }
     for (; ok && c < to_find && off < n; ++off) {  // the scan has to reach further now
       const int pos = at(off);
