@@ -239,14 +239,6 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
     for (const auto& pod : pods) {
       if (active_.holds(*pod)) continue;  // already active: no uid lookups
       const std::string& uid = pod->uid();
-      // In flight first: a gang's siblings waiting at Permit are the common
-      // case (every Permit wait activates them), and a pod in flight is in
-      // no queue (pop takes it out of activeQ; every push into a queue erases
-      // its in-flight entry), so one lookup settles it.
-      if (auto f = in_flight_.find(uid); f != in_flight_.end()) {
-        f->second = kActivate;  // remember the request for when its cycle fails
-        continue;
-      }
       if (active_.contains(uid)) continue;
       QueuedPodInfoPtr q;
       auto it = unschedulable_.find(uid);
@@ -259,7 +251,11 @@ void SchedulingQueue::activate(const std::vector<PodPtr>& pods) {
       } else if ((q = backoff_.get(uid))) {
         backoff_.erase(uid);
       }
-      if (!q) continue;  // not queued and not in flight (bound, or deleted)
+      if (!q) {  // in flight: remember the request for when its cycle fails
+        auto f = in_flight_.find(uid);
+        if (f != in_flight_.end()) f->second = kActivate;
+        continue;
+      }
       active_.push(q);
       moved = true;
     }
