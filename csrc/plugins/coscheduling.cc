@@ -360,7 +360,13 @@ class Coscheduling : public Plugin {
   void unreserve(CycleState&, const PodPtr& p, const std::string&) override {
     if (p->pod_group.empty()) return;
     auto pg = h_.informers->pod_group_of(*p);
-    if (!pg) return;
+    if (!pg) {
+      // The group was deleted while this member waited at Permit: nothing to
+      // reject or deny, but the GPUs noted as owed to it must not stay owed
+      // (they held every later gang's gate shut until the 15-min sweep).
+      if (park_) drop_outstanding(p->pg_key);
+      return;
+    }
     // A sibling rejected because its group parked (PostFilter): no denial.
     if (park_ && consume_parked_reject(p->pg_key)) return;
     reject_group(*p, "rejection in Unreserve");
@@ -418,9 +424,38 @@ class Coscheduling : public Plugin {
     full.push_back('/');
     full += md["name"].as_string();
     const uint64_t key = pg_key_of(full);
-    PatchShard& sh = patch_shard(key);
-    std::lock_guard<std::mutex> g(sh.mu);
-    sh.map.erase(key);
+    {
+      PatchShard& sh = patch_shard(key);
+      std::lock_guard<std::mutex> g(sh.mu);
+      sh.map.erase(key);
+    }
+    if (park_) forget_group(key);
+  }
+  // A deleted group leaves the parking state: GPUs owed to it at Permit, its
+  // parked entry (the oldest parked group reserves its need against every
+  // younger gang until a probe finds it empty) and its pending rejections,
+  // at once rather than at the next probe or sweep (an open-loop overload
+  // ends with thousands of gangs deleted mid-admission).
+  void forget_group(uint64_t key) {
+    std::vector<PodPtr> probe;
+    {
+      std::lock_guard<std::mutex> g(park_mu_);
+      erase_outstanding_locked(key);
+      parked_rejects_.erase(key);
+      if (auto pos = parked_pos_.find(key); pos != parked_pos_.end()) {
+        const bool head = !parked_.empty() && parked_.begin()->first == pos->second;
+        parked_.erase(pos->second);
+        parked_pos_.erase(pos);
+        parked_n_.store(parked_.size(), std::memory_order_release);
+        // The head of the line left: the next parked group may fit now.
+        if (head && !probe_key_) probe = next_probe_locked();
+      }
+      if (probe_key_ == key) {
+        probe_key_ = 0;
+        probe = next_probe_locked();
+      }
+    }
+    if (!probe.empty()) h_.activate(probe);
   }
 
   // Unit-test hook (core/core_test.go:303 TestCheckClusterResource):

@@ -1,0 +1,80 @@
+"""One open-loop trial (utils/openloop.py, as the bench's capacity search runs
+it) under the timestamped sampler, to see which thread limits the sustained
+rate near the capacity cliff.
+
+    python scripts/sample_openloop.py OUTDIR --rate 106000 [--nodes 64]
+    python scripts/sample_openloop.py OUTDIR --sequence 102371,118500,106400
+
+With --sequence, no sampling: the trials run back to back on one shard, as
+the capacity search runs them, and each one's p99 is printed.
+
+Writes OUTDIR/openloop.samples (symbolize against the extension .so) and
+OUTDIR/openloop_trial.json (the trial's summary without per-gang rows).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+from flex_gpu_scheduler_amd._native import native  # noqa: E402
+from flex_gpu_scheduler_amd.utils.benchrun import Shard  # noqa: E402
+from flex_gpu_scheduler_amd.utils.cpuaffinity import apply  # noqa: E402
+from flex_gpu_scheduler_amd.utils.openloop import run_open_loop  # noqa: E402
+from flex_gpu_scheduler_amd.utils.workload import ClusterSpec  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--nodes", type=int, default=64)
+    ap.add_argument("--rate", type=float, default=106_000.0)
+    ap.add_argument("--hz", type=int, default=4000)
+    ap.add_argument("--sequence", default="")
+    ap.add_argument("--waves", type=int, default=4, help="burst waves before the open-loop trials")
+    ap.add_argument("--sample-last", action="store_true", help="with --sequence: sample the last trial")
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    apply("l3")
+    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=7)
+    try:
+        # Warm the shard as the bench does before its search: burst waves,
+        # then one open-loop trial well below the cliff.
+        for i in range(a.waves):
+            w = shard.wave(i)
+            shard.run(w, prepared=w.chunks_json(), collect_gangs=False)
+        if a.sequence:
+            rows = []
+            rates = [float(x) for x in a.sequence.split(",")]
+            for i, rate in enumerate(rates):
+                last = i == len(rates) - 1
+                if last and a.sample_last:
+                    native().sampler_start(a.hz, 4_000_000)
+                r = run_open_loop(shard, rate, 1.0, seed=0)
+                if last and a.sample_last:
+                    native().sampler_dump(os.path.join(a.out, "openloop.samples"))
+                rows.append({"offered_pods_per_s": rate, "wall_s": r["wall_s"], "parked_gangs": r["parked_gangs"],
+                             **{k: r["all_gangs"][k] for k in ("p99_create_to_bound_ms", "max_create_to_bound_ms")}})
+                print(json.dumps(rows[-1]), flush=True)
+            with open(os.path.join(a.out, "openloop_sequence.jsonl"), "w") as f:
+                f.writelines(json.dumps(x) + "\n" for x in rows)
+            return 0
+        run_open_loop(shard, a.rate / 2, 1.0, seed=0)
+        native().sampler_start(a.hz, 4_000_000)
+        r = run_open_loop(shard, a.rate, 1.0, seed=0, timeline=True)
+        native().sampler_dump(os.path.join(a.out, "openloop.samples"))
+    finally:
+        shard.close()
+    keep = {k: v for k, v in r.items() if k not in ("by_gang",)}
+    with open(os.path.join(a.out, "openloop_trial.json"), "w") as f:
+        json.dump(keep, f)
+    print(json.dumps({k: keep[k] for k in ("offered_pods_per_s", "all_gangs", "wall_s", "parked_gangs",
+                                             "max_in_flight_pods", "max_held_pods", "hold_ms")}))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -131,3 +131,53 @@ def test_parking_mode_is_validated():
 
     with pytest.raises(ConfigError):
         load_config(flagship_config(transient_shortage="Sometimes"))
+
+
+def _parking(s, pod):
+    return s.plugin_call("Coscheduling", "parking", {"pod": pod})
+
+
+def test_group_deleted_at_permit_owes_no_gpus(store):
+    """A gang deleted while a member waits at Permit (the PodGroup gone before
+    the members' deletions reach Unreserve) leaves nothing owed: GPUs owed to
+    a gang that no longer exists would hold every later gang's gate shut until
+    the 15-min sweep."""
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    pg, pods = gang("g", 4)
+    store.create("podgroups", pg)
+    for p in pods:
+        store.create("pods", p)
+    s = new_scheduler(store, load_config(flagship_config(permit_wait_s=10, transient_shortage="Park")))
+    try:
+        s.sync_informers(50)
+        assert s.schedule_one(2000)  # r0 waits at Permit: 3 more GPUs owed to the gang
+        probe = store.get("pods", "default", "g-r1")
+        assert _parking(s, probe)["outstandingGpus"] == 3
+        store.delete("podgroups", "default", "g")
+        s.sync_informers(50)
+        for p in pods:
+            store.delete("pods", "default", p["metadata"]["name"])
+        s.sync_informers(50)
+        assert wait_for(lambda: _parking(s, probe)["outstandingGpus"] == 0, timeout=5.0), _parking(s, probe)
+    finally:
+        s.stop()
+
+
+def test_deleted_parked_group_leaves_the_line(store):
+    """A parked group that is deleted leaves the parked list at once (it would
+    otherwise reserve its need against every younger gang until a probe)."""
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = scheduler(store)
+    try:
+        a = submit(store, "a", 8)
+        assert wait_for(lambda: len(bound(store, a)) == 8)
+        b = submit(store, "b", 4)
+        assert wait_for(lambda: s.gang_parks() >= 1)
+        probe = store.get("pods", "default", b[0])
+        assert [g["podGroup"] for g in _parking(s, probe)["parked"]] == ["default/b"]
+        store.delete("podgroups", "default", "b")
+        delete_all(store, b)
+        assert wait_for(lambda: _parking(s, probe)["parked"] == [], timeout=5.0), _parking(s, probe)
+        assert _parking(s, probe)["outstandingGpus"] == 0
+    finally:
+        s.stop()
