@@ -148,6 +148,8 @@ def main() -> int:
                     help="shard CPU placement: none | l3 | l3xK | explicit list (utils/cpuaffinity.py)")
     ap.add_argument("--no-open-loop", action="store_true",
                     help="skip the untimed open-loop (Poisson arrivals) gang admission latency run")
+    ap.add_argument("--open-loop-in-process", action="store_true",
+                    help="run the open-loop search on this rank's shard instead of a GPU-free child (A/B)")
     ap.add_argument("--waves-per-step", type=int, default=16,
                     help="waves per timed step (one wave fills the shard's GPUs once)")
     ap.add_argument("--no-service-mode", action="store_true",
@@ -285,19 +287,29 @@ def main() -> int:
         # Untimed: Poisson gang arrivals at 50% / 90% of this shard's measured
         # open-loop capacity, gang types interleaved, held then deleted
         # (utils/openloop.py) — admission latency rather than burst queueing.
-        from flex_gpu_scheduler_amd.utils.openloop import open_loop_capacity, run_open_loop
+        # In a child process that never loads the GPU runtime (the scheduler's
+        # deployment shape), on a fresh shard of the same cluster pinned to
+        # this shard's CPUs (this one is idle meanwhile): with torch and HIP in
+        # the process, an overloaded trial near the cliff leaves it slower for
+        # the next trials (utils/openloop.py capacity_in_child).
+        from flex_gpu_scheduler_amd.utils.openloop import capacity_in_child, capacity_report
 
         burst = pods / t_rank if t_rank > 0 else 0.0
-        search: list[dict] = []
-        cap = open_loop_capacity(shard, burst, seed=args.seed, log=search) if burst > 0 else 0.0
+        if args.open_loop_in_process:
+            rep = capacity_report(shard, burst, seed=args.seed)
+        else:
+            rep = capacity_in_child(args.nodes, args.seed + 7919 * ctx.rank, json.loads(args.sched_options), burst,
+                                    cpus=cpus, hbm_gib=hbm_gib)
+        cap = rep["capacity"]
         extras["gang_admit_open_loop"] = {
             "burst_capacity_pods_per_s": round(burst, 1),
             "capacity_pods_per_s": round(cap, 1),
             "capacity_rule": "highest x1.3-step rate (+2 bisection steps) whose p99 PG-create->last-Bind over "
                              "all gangs (unbound = infinite) is <= 25 ms; one trial per rate",
-            "capacity_search": search,
-            **{f"load_{int(f * 100)}": run_open_loop(shard, f * cap, duration_s=1.0, seed=args.seed + 1)
-               for f in (0.5, 0.9) if cap > 0}}
+            "process": "this rank's" if args.open_loop_in_process else "child without the GPU runtime, fresh shard",
+            "capacity_search": rep["search"],
+            **{k: rep[k] for k in ("load_50", "load_90") if k in rep}}
+        search = rep["search"]
         ol = extras["gang_admit_open_loop"]
         extras["open_loop_capacity_pods_per_s"] = round(cap, 1)
         l90 = ol.get("load_90") or {}

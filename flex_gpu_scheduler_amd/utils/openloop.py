@@ -204,3 +204,76 @@ def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: 
         out["timeline"] = [list(x) for x in res.get("timeline", [])]
     out.update({"offered_pods_per_s": round(rate_pods_per_s, 1), "hold_ms": round(hold_us / 1e3, 3)})
     return out
+
+
+def capacity_report(shard, burst: float, seed: int = 0) -> dict:
+    """The bench's open-loop block on `shard`: the capacity search, then the
+    50% and 90% loads of the capacity found."""
+    search: list[dict] = []
+    cap = open_loop_capacity(shard, burst, seed=seed, log=search) if burst > 0 else 0.0
+    out = {"capacity": cap, "search": search}
+    for f in (0.5, 0.9):
+        if cap > 0:
+            out[f"load_{int(f * 100)}"] = run_open_loop(shard, f * cap, duration_s=1.0, seed=seed + 1)
+    return out
+
+
+def capacity_in_child(nodes: int, seed: int, options: dict, burst: float, cpus: list[int] | None = None,
+                      warm_waves: int = 16, hbm_gib: int = 288, timeout_s: float = 600.0) -> dict:
+    """capacity_report in a child Python process that never loads the GPU
+    runtime, on a fresh shard of the same cluster (spec, seed, options),
+    warmed with `warm_waves` burst waves and pinned to `cpus`.
+
+    The scheduler runs without the GPU runtime in deployment (it is a
+    control-plane process; the GPU probes run in the node agent). In the
+    bench's rank process, torch and HIP are loaded, and near the capacity
+    cliff an overloaded trial then leaves the process markedly slower for the
+    next ones (profiles/r5ar_openloop_torch_loaded.txt vs
+    r5aq_openloop_no_torch.txt), so the in-process search measured that
+    interaction rather than the scheduler."""
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, "-m", "flex_gpu_scheduler_amd.utils.openloop", "--nodes", str(nodes),
+           "--seed", str(seed), "--options", json.dumps(options), "--burst", repr(float(burst)),
+           "--warm-waves", str(warm_waves), "--hbm-gib", str(hbm_gib)]
+    if cpus:
+        cmd += ["--cpus", ",".join(map(str, cpus))]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, check=False)
+    if r.returncode != 0:
+        raise RuntimeError(f"open-loop child exited {r.returncode}: {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _child_main(argv: list[str] | None = None) -> int:
+    import argparse
+    import os
+
+    ap = argparse.ArgumentParser(description="open-loop capacity report on a fresh shard (bench.py child)")
+    ap.add_argument("--nodes", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--options", default="{}")
+    ap.add_argument("--burst", type=float, required=True)
+    ap.add_argument("--warm-waves", type=int, default=16)
+    ap.add_argument("--hbm-gib", type=int, default=288)
+    ap.add_argument("--cpus", default="")
+    a = ap.parse_args(argv)
+    if a.cpus:
+        os.sched_setaffinity(0, [int(c) for c in a.cpus.split(",")])  # before the shard's threads start
+    from .benchrun import Shard
+
+    shard = Shard(ClusterSpec(nodes=a.nodes, hbm_gib=a.hbm_gib), namespace="bench-ol", seed=a.seed,
+                  options=json.loads(a.options))
+    try:
+        for i in range(a.warm_waves):
+            w = shard.wave(i)
+            shard.run(w, prepared=w.chunks_json(), collect_gangs=False)
+        rep = capacity_report(shard, a.burst, seed=a.seed)
+    finally:
+        shard.close()
+    print(json.dumps(rep))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(_child_main())

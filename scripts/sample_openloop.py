@@ -34,18 +34,45 @@ def main() -> int:
     ap.add_argument("--rate", type=float, default=106_000.0)
     ap.add_argument("--hz", type=int, default=4000)
     ap.add_argument("--sequence", default="")
+    ap.add_argument("--seed", type=int, default=7, help="Shard seed (bench.py uses 0 for rank 0)")
     ap.add_argument("--waves", type=int, default=4, help="burst waves before the open-loop trials")
     ap.add_argument("--sample-last", action="store_true", help="with --sequence: sample the last trial")
+    ap.add_argument("--trim", action="store_true", help="malloc_trim(0) after every trial (heap-state A/B)")
+    ap.add_argument("--prerender", action="store_true",
+                    help="render every warm wave's JSON up front and drop it afterwards, as bench.py does")
+    ap.add_argument("--torch", action="store_true", help="initialise torch and the GPU first, as bench.py does")
+    ap.add_argument("--torch-after-pin", action="store_true", help="initialise them after the CPU pinning")
     a = ap.parse_args()
+
+    def init_torch():
+        import torch
+
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda")
+
+    if a.torch:
+        init_torch()
     os.makedirs(a.out, exist_ok=True)
     apply("l3")
-    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=7)
+    if a.torch_after_pin:
+        init_torch()
+    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed)
     try:
         # Warm the shard as the bench does before its search: burst waves,
         # then one open-loop trial well below the cliff.
-        for i in range(a.waves):
-            w = shard.wave(i)
-            shard.run(w, prepared=w.chunks_json(), collect_gangs=False)
+        if a.prerender:
+            ws = [shard.wave(i) for i in range(a.waves)]
+            prepared = [w.chunks_json() for w in ws]
+            for w, pj in zip(ws, prepared):
+                shard.run(w, prepared=pj, collect_gangs=False)
+            del ws, prepared
+            if a.trim:
+                import ctypes
+                ctypes.CDLL("libc.so.6").malloc_trim(0)
+        else:
+            for i in range(a.waves):
+                w = shard.wave(i)
+                shard.run(w, prepared=w.chunks_json(), collect_gangs=False)
         if a.sequence:
             rows = []
             rates = [float(x) for x in a.sequence.split(",")]
@@ -56,6 +83,9 @@ def main() -> int:
                 r = run_open_loop(shard, rate, 1.0, seed=0)
                 if last and a.sample_last:
                     native().sampler_dump(os.path.join(a.out, "openloop.samples"))
+                if a.trim:
+                    import ctypes
+                    ctypes.CDLL("libc.so.6").malloc_trim(0)
                 rows.append({"offered_pods_per_s": rate, "wall_s": r["wall_s"], "parked_gangs": r["parked_gangs"],
                              **{k: r["all_gangs"][k] for k in ("p99_create_to_bound_ms", "max_create_to_bound_ms")}})
                 print(json.dumps(rows[-1]), flush=True)

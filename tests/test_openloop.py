@@ -174,3 +174,23 @@ def test_capacity_search_reaches_the_burst_rate(monkeypatch):
     limit = 50_000.0  # an ordinary failing grid step: unchanged behaviour
     cap = openloop.open_loop_capacity(None, 120_000.0)
     assert 45_000 < cap <= 50_000 and max(tried) < 120_000
+
+
+def test_capacity_report_in_a_gpu_free_child():
+    """bench.py runs the open-loop block in a child process on a fresh shard
+    (utils/openloop.py capacity_in_child): the child must not load torch (the
+    GPU runtime in the process is what it avoids) and must return the search
+    and both loads."""
+    import subprocess
+    import sys
+
+    from flex_gpu_scheduler_amd.utils.openloop import capacity_in_child
+
+    probe = subprocess.run([sys.executable, "-c", "import sys, flex_gpu_scheduler_amd.utils.openloop, "
+                            "flex_gpu_scheduler_amd.utils.benchrun; print('torch' in sys.modules)"],
+                           capture_output=True, text=True, check=True)
+    assert probe.stdout.strip() == "False"
+    rep = capacity_in_child(16, 0, {}, 2600.0, warm_waves=2, timeout_s=300)
+    assert rep["capacity"] > 0 and rep["search"], rep
+    assert {"load_50", "load_90"} <= set(rep)
+    assert rep["load_90"]["all_gangs"]["unbound"] == 0
