@@ -175,9 +175,18 @@ def test_deleted_parked_group_leaves_the_line(store):
         assert wait_for(lambda: s.gang_parks() >= 1)
         probe = store.get("pods", "default", b[0])
         assert [g["podGroup"] for g in _parking(s, probe)["parked"]] == ["default/b"]
+        time.sleep(1.1)  # a later creation second: c queues behind b
+        c = submit(store, "c", 2)
+        assert wait_for(lambda: len(_parking(s, probe)["parked"]) == 2)
+        # b (the head of the line) leaves: c is probed from the informer's
+        # event (it finds the GPUs still held and parks again).
         store.delete("podgroups", "default", "b")
         delete_all(store, b)
-        assert wait_for(lambda: _parking(s, probe)["parked"] == [], timeout=5.0), _parking(s, probe)
+        assert wait_for(lambda: [g["podGroup"] for g in _parking(s, probe)["parked"]] == ["default/c"],
+                        timeout=5.0), _parking(s, probe)
         assert _parking(s, probe)["outstandingGpus"] == 0
+        store.delete("podgroups", "default", "c")
+        delete_all(store, c)
+        assert wait_for(lambda: _parking(s, probe)["parked"] == [], timeout=5.0), _parking(s, probe)
     finally:
         s.stop()
