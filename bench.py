@@ -283,6 +283,14 @@ def main() -> int:
         shard.close()
         ctx.close()
         return 0
+    def repin() -> list[int] | None:
+        # Rank 0's untimed extras run after the other ranks have exited: each
+        # phase takes the L3 domain that is least busy now (other tenants of
+        # the host may have moved onto the one ranked at the start).
+        if not args.cpus.startswith("l3"):
+            return None
+        return pin_cpus(args.cpus, 0, order=ranked_domains())
+
     if not args.no_open_loop:
         # Untimed: Poisson gang arrivals at 50% / 90% of this shard's measured
         # open-loop capacity, gang types interleaved, held then deleted
@@ -299,7 +307,7 @@ def main() -> int:
             rep = capacity_report(shard, burst, seed=args.seed)
         else:
             rep = capacity_in_child(args.nodes, args.seed + 7919 * ctx.rank, json.loads(args.sched_options), burst,
-                                    cpus=cpus, hbm_gib=hbm_gib)
+                                    cpus=repin() or cpus, hbm_gib=hbm_gib)
         cap = rep["capacity"]
         extras["gang_admit_open_loop"] = {
             "burst_capacity_pods_per_s": round(burst, 1),
@@ -328,6 +336,7 @@ def main() -> int:
 
     if args.nodes1024_waves > 0:
         # Untimed: the same workload on one 1,024-node shard (12k pods/wave).
+        repin()
         try:
             extras["nodes1024"] = run_nodes(1024, args.nodes1024_waves, args.seed, json.loads(args.sched_options))
             extras["nodes1024_pods_per_s"] = extras["nodes1024"]["pods_per_s"]
