@@ -41,6 +41,8 @@ def main() -> int:
     ap.add_argument("--prerender", action="store_true",
                     help="render every warm wave's JSON up front and drop it afterwards, as bench.py does")
     ap.add_argument("--torch", action="store_true", help="initialise torch and the GPU first, as bench.py does")
+    ap.add_argument("--fresh-after", type=int, default=-1,
+                    help="with --sequence: replace the shard by a fresh one (same process) after trial N (0-based)")
     ap.add_argument("--torch-after-pin", action="store_true", help="initialise them after the CPU pinning")
     a = ap.parse_args()
 
@@ -77,6 +79,15 @@ def main() -> int:
             rows = []
             rates = [float(x) for x in a.sequence.split(",")]
             for i, rate in enumerate(rates):
+                if i == a.fresh_after + 1:
+                    # Shard state vs process state: a new store and scheduler
+                    # in the same process (same heap), warmed as the first.
+                    shard.close()
+                    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample2", seed=a.seed)
+                    for j in range(4):
+                        w = shard.wave(j)
+                        shard.run(w, prepared=w.chunks_json(), collect_gangs=False)
+                    print(json.dumps({"fresh_shard_before_trial": i}), flush=True)
                 last = i == len(rates) - 1
                 if last and a.sample_last:
                     native().sampler_start(a.hz, 4_000_000)
@@ -87,7 +98,9 @@ def main() -> int:
                     import ctypes
                     ctypes.CDLL("libc.so.6").malloc_trim(0)
                 rows.append({"offered_pods_per_s": rate, "wall_s": r["wall_s"], "parked_gangs": r["parked_gangs"],
-                             **{k: r["all_gangs"][k] for k in ("p99_create_to_bound_ms", "max_create_to_bound_ms")}})
+                             **{k: r["all_gangs"][k] for k in ("p99_create_to_bound_ms", "max_create_to_bound_ms")},
+                             "queue_after": shard.sched.queue_counts(),
+                             "store_pods": len(shard.store.list("pods", "")[0]) if hasattr(shard, "store") else None})
                 print(json.dumps(rows[-1]), flush=True)
             with open(os.path.join(a.out, "openloop_sequence.jsonl"), "w") as f:
                 f.writelines(json.dumps(x) + "\n" for x in rows)
