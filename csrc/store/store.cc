@@ -427,9 +427,20 @@ JsonPtr ObjectStore::remove(const std::string& kind, const std::string& ns, cons
   }
   JsonPtr old = it->second.obj;
   km.erase(it);
+  shrink_locked(km);
   int64_t rv = rv_.fetch_add(1) + 1;
   emit_locked(EventType::Deleted, kind, old, old, rv);
   return old;
+}
+
+// A kind's table keeps the bucket array of its peak size (unordered_map never
+// shrinks by itself): after an overload put 10^5 pods in flight, every later
+// lookup under the store lock touched a cold, oversized array, and the
+// scheduler served ~10% less until a fresh store
+// (profiles/r5bc_openloop_fresh_scheduler_same_store.txt). Shrunk once the
+// table is 8x emptier than its buckets (amortized O(1) per removal).
+void ObjectStore::shrink_locked(KindMap& km) {
+  if (km.bucket_count() > 4096 && km.size() * 8 < km.bucket_count()) km.rehash(0);
 }
 
 size_t ObjectStore::remove_many(const std::string& kind, const std::string& ns,
@@ -449,6 +460,7 @@ size_t ObjectStore::remove_many(const std::string& kind, const std::string& ns,
     emit_locked(EventType::Deleted, kind, old, old, rv);
     ++n;
   }
+  shrink_locked(km);
   batch_ = nullptr;
   flush_batch_locked(batch);
   return n;

@@ -199,6 +199,7 @@ class ObjectStore {
   mutable std::vector<WatchEvent> reap_q_;
   mutable std::thread reaper_;
   mutable bool reap_stop_ = false;
+  void shrink_locked(KindMap& km);
   std::unordered_map<std::string, KindMap> kinds_;
   std::atomic<int64_t> rv_{0};
   std::vector<WatcherPtr> watchers_;

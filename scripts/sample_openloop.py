@@ -41,7 +41,10 @@ def main() -> int:
     ap.add_argument("--prerender", action="store_true",
                     help="render every warm wave's JSON up front and drop it afterwards, as bench.py does")
     ap.add_argument("--torch", action="store_true", help="initialise torch and the GPU first, as bench.py does")
-    ap.add_argument("--fresh-after", type=int, default=-1,
+    ap.add_argument("--options", default="{}", help="scheduler options JSON, e.g. '{\"events\": false}'")
+    ap.add_argument("--fresh-sched-after", type=int, default=-2,
+                    help="with --sequence: a new scheduler on the same store after trial N (0-based)")
+    ap.add_argument("--fresh-after", type=int, default=-2,
                     help="with --sequence: replace the shard by a fresh one (same process) after trial N (0-based)")
     ap.add_argument("--torch-after-pin", action="store_true", help="initialise them after the CPU pinning")
     a = ap.parse_args()
@@ -58,7 +61,7 @@ def main() -> int:
     apply("l3")
     if a.torch_after_pin:
         init_torch()
-    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed)
+    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed, options=json.loads(a.options))
     try:
         # Warm the shard as the bench does before its search: burst waves,
         # then one open-loop trial well below the cliff.
@@ -79,6 +82,16 @@ def main() -> int:
             rows = []
             rates = [float(x) for x in a.sequence.split(",")]
             for i, rate in enumerate(rates):
+                if i == a.fresh_sched_after + 1:
+                    # Scheduler state vs store state: the store (and its
+                    # watchers' history) stays, the scheduler is new.
+                    from flex_gpu_scheduler_amd import load_config, new_scheduler
+                    from flex_gpu_scheduler_amd.utils.workload import flagship_config
+
+                    shard.sched.stop()
+                    shard.sched = new_scheduler(shard.store, load_config(flagship_config()), seed=shard.seed + 1)
+                    shard.sched.start()
+                    print(json.dumps({"fresh_scheduler_before_trial": i}), flush=True)
                 if i == a.fresh_after + 1:
                     # Shard state vs process state: a new store and scheduler
                     # in the same process (same heap), warmed as the first.
