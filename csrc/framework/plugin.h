@@ -36,6 +36,7 @@ class Informers;
 class WaitingPods;
 class Nominator;
 class Metrics;
+class GangPlacement;
 
 enum ExtPoint : uint32_t {
   kQueueSort = 1u << 0,
@@ -91,6 +92,13 @@ struct Handle {
   std::function<void(const Pod& member, const char* why)> gang_denied;
   // Coscheduling parked `member`'s group (transient GPU shortage). Optional.
   std::function<void(const Pod& member)> gang_parked;
+  // xGMI gang co-location state of this profile (scheduler/gang_placement.h):
+  // NodeResourceTopologyMatch sets its mode and plans each rank's node set;
+  // Coscheduling's gate asks it in Required mode.
+  GangPlacement* gangs = nullptr;
+  // The first rank of `member`'s gang was planned: could one node take the
+  // whole gang at that moment (the gang record's `hostable`)? Optional.
+  std::function<void(const Pod& member, bool hostable)> gang_planned;
   // Bracket a long wait inside a binding-cycle extension point (PreBind):
   // the binder pool adds a worker for the duration, so waiting pods cannot
   // starve the bindings of unrelated pods. Optional.

@@ -113,6 +113,27 @@ struct PodsToActivate : StateData {
 };
 inline constexpr const char* kPodsToActivateKey = "kubernetes.io/pods-to-activate";
 
+// A PreFilter plugin's node set for this cycle (upstream's PreFilterResult,
+// k8s 1.24+, by snapshot position instead of node name): the scheduler runs
+// Filter only on these nodes and gives every other node `excluded`. When none
+// of them passes Filter and `fallback` is set, every node is evaluated as if
+// there were no restriction. Written under kNodeRestrictionKey.
+struct NodeRestriction : StateData {
+  size_t nodes = 0;        // snapshot size it was computed for (stale otherwise)
+  std::vector<int> list;   // the allowed positions, when `mask` is empty
+  std::vector<char> mask;  // per snapshot position (larger sets)
+  bool fallback = true;
+  Status excluded;         // verdict of the nodes outside the set
+  bool allows(int pos) const {
+    if (!mask.empty()) return mask[static_cast<size_t>(pos)] != 0;
+    for (int q : list)
+      if (q == pos) return true;
+    return false;
+  }
+  std::shared_ptr<StateData> clone() const override { return std::make_shared<NodeRestriction>(*this); }
+};
+inline constexpr const char* kNodeRestrictionKey = "xsched/node-restriction";
+
 // Node name -> pods nominated to it (Nominator::view()).
 using NominatedMap = std::unordered_map<std::string, std::vector<PodPtr>>;
 

@@ -46,6 +46,7 @@
 #include "framework/plugin.h"
 #include "framework/waiting_pods.h"
 #include "scheduler/cache.h"
+#include "scheduler/gang_placement.h"
 #include "scheduler/informers.h"
 #include "scheduler/metrics.h"
 #include "store/store.h"
@@ -163,13 +164,23 @@ class Coscheduling : public Plugin {
     if (p.pod_group.empty()) return {};
     auto pg = h_.informers->pod_group_of(p);
     if (!pg) return {};
-    if (denied_.has(p.pg_key))
+    if (denied_.has(p.pg_key)) {
+      // A parked group that is now denied leaves the parking line (its
+      // requeue timer brings the members back after the TTL).
+      if (park_) drop_parked(p.pg_key, false);
       return Status::unresolvable("pod with pgName: " + p.pg_full_name() + " last failed in " +
                                   std::to_string(denied_ttl_us_ / 1000000) + "s, deny");
+    }
     size_t n = h_.informers->count_pods_in_group_of(p);
-    if (static_cast<int64_t>(n) < pg->min_member)
+    if (static_cast<int64_t>(n) < pg->min_member) {
+      // A parked group that lost members (one deleted, the PodGroup kept)
+      // cannot pass the gate until new ones arrive: it must not stay at the
+      // head of the line, where it would hold back every younger gang. Its
+      // members return to the queues and wait for a Pod add, as upstream.
+      if (park_) drop_parked(p.pg_key, true);
       return Status::unresolvable("pre-filter pod " + p.name() + " cannot find enough sibling pods, current pods number: " +
                                   std::to_string(n) + ", minMember of group: " + std::to_string(pg->min_member));
+    }
     if (park_) {
       Status gs = gang_gate(p, *pg);
       if (!gs.is_success()) return gs;
@@ -368,7 +379,7 @@ class Coscheduling : public Plugin {
       return;
     }
     // A sibling rejected because its group parked (PostFilter): no denial.
-    if (park_ && consume_parked_reject(p->pg_key)) return;
+    if (park_ && consume_parked_reject(p->pg_key, p->uid())) return;
     reject_group(*p, "rejection in Unreserve");
     drop_outstanding(p->pg_key);
     deny(*p, "unreserve");
@@ -442,19 +453,54 @@ class Coscheduling : public Plugin {
       std::lock_guard<std::mutex> g(park_mu_);
       erase_outstanding_locked(key);
       parked_rejects_.erase(key);
-      if (auto pos = parked_pos_.find(key); pos != parked_pos_.end()) {
-        const bool head = !parked_.empty() && parked_.begin()->first == pos->second;
-        parked_.erase(pos->second);
-        parked_pos_.erase(pos);
-        parked_n_.store(parked_.size(), std::memory_order_release);
-        // The head of the line left: the next parked group may fit now.
-        if (head && !probe_key_) probe = next_probe_locked();
-      }
-      if (probe_key_ == key) {
-        probe_key_ = 0;
-        probe = next_probe_locked();
+      unpark_locked(key, probe);
+    }
+    if (!probe.empty()) h_.activate(probe);
+  }
+  // Removes `key` from the parking line. When it was the head of its kind's
+  // line or that kind's outstanding probe, the next group of the kind is
+  // probed (appended to `probe`).
+  void unpark_locked(uint64_t key, std::vector<PodPtr>& probe) {
+    auto pos = parked_pos_.find(key);
+    int slot = -1;
+    bool head = false;
+    if (pos != parked_pos_.end()) {
+      slot = kind_slot(parked_[pos->second].kind);
+      head = oldest_locked(slot) == parked_.find(pos->second);
+      parked_.erase(pos->second);
+      parked_pos_.erase(pos);
+      parked_n_.store(parked_.size(), std::memory_order_release);
+    }
+    for (int k = 0; k < 2; ++k) {
+      const bool was_probe = probe_key_[k] == key;
+      if (was_probe) probe_key_[k] = 0;
+      if ((was_probe || (head && k == slot)) && !probe_key_[k]) {
+        auto more = next_probe_locked(k);
+        probe.insert(probe.end(), more.begin(), more.end());
       }
     }
+    take_wake_locked(probe);
+  }
+  // PreFilter found p's group denied or short of members: it leaves the
+  // parking line; with `wake` its parked members return to the queues.
+  void drop_parked(uint64_t key, bool wake) {
+    if (parked_n_.load(std::memory_order_acquire) == 0) return;
+    std::vector<PodPtr> probe;
+    Pod member;
+    bool was = false;
+    {
+      std::lock_guard<std::mutex> g(park_mu_);
+      auto pos = parked_pos_.find(key);
+      if (pos == parked_pos_.end()) return;
+      member.meta.ns = parked_[pos->second].ns;
+      member.pod_group = parked_[pos->second].group;
+      member.pg_key = key;
+      was = true;
+      unpark_locked(key, probe);
+    }
+    if (was && wake)
+      for (auto& q : h_.informers->pods_in_group_of(member))
+        if (q->node_name.empty()) probe.push_back(std::move(q));
     if (!probe.empty()) h_.activate(probe);
   }
 
@@ -486,6 +532,10 @@ class Coscheduling : public Plugin {
       out.set("parked", std::move(groups));
       out.set("outstandingGpus", Json(owed_[0]));
       out.set("outstandingXcdMembers", Json(owed_[1]));
+      Json probes = Json::array();
+      for (int k = 0; k < 2; ++k)
+        if (probe_key_[k]) probes.push_back(Json(k == 0 ? "gpu" : "xcd"));
+      out.set("probing", std::move(probes));
       out.set("parksTotal", Json(static_cast<int64_t>(parks_total_)));
       return out;
     }
@@ -597,8 +647,9 @@ class Coscheduling : public Plugin {
   using ParkKey = std::pair<MicroTime, uint64_t>;  // (PodGroup creation, pg_key): oldest first
   // Gate verdict for p's group (scheduling thread, snapshot current): pass
   // when the free units, less those owed to other gangs at Permit and to an
-  // older parked group, cover the remaining members. Parks the group on
-  // failure.
+  // older parked group of the same kind, cover the remaining members, and
+  // (NRT gangColocation: Required) one node can take all of them. Parks the
+  // group on failure.
   Status gang_gate(const Pod& p, const PodGroup& pg) {
     const GpuDemand& d = p.gpu_demand;
     if (!gated(d) || !h_.snapshot) return {};
@@ -608,11 +659,16 @@ class Coscheduling : public Plugin {
     const int64_t need = units_for(d, remaining);
     const int64_t free = free_units(d);
     const int slot = kind_slot(d.kind);
+    // Required co-location: a gang that one idle node could hold waits until
+    // one node can take all of its ranks (counting ranks owed to gangs
+    // anchored on a node). Only before its first rank is placed: a started
+    // gang follows its hosts (NRT PreFilter).
+    const bool coloc_ok = assigned > 0 || colocated_now(p, remaining);
     std::vector<PodPtr> probe;
     bool pass;
     {
       std::lock_guard<std::mutex> g(park_mu_);
-      if (parked_.empty() && owed_[slot] == 0 && free >= need) return {};  // common case
+      if (parked_.empty() && owed_[slot] == 0 && free >= need && coloc_ok) return {};  // common case
       int64_t reserved = owed_[slot];
       if (auto o = outstanding_.find(p.pg_key); o != outstanding_.end() && kind_slot(o->second.kind) == slot)
         reserved -= o->second.units;
@@ -621,25 +677,21 @@ class Coscheduling : public Plugin {
       // The oldest parked group of this kind holds a reservation against
       // younger groups that have not started (so big gangs are not starved
       // by a stream of small ones).
-      if (assigned == 0)
-        for (const auto& [k, pk] : parked_) {
-          if (!(k < me)) break;
-          if (kind_slot(pk.kind) == slot) {
-            reserved += pk.need;
-            break;
-          }
-        }
-      pass = free - reserved >= need;
-      if (p.pg_key == probe_key_) probe_key_ = 0;  // the probe's answer is in
-      if (pass) {
-        if (pos != parked_pos_.end()) {
-          parked_.erase(pos->second);
-          parked_pos_.erase(pos);
-          parked_n_.store(parked_.size(), std::memory_order_release);
-          // Chain: the next parked group may fit what is left.
-          probe = next_probe_locked();
-        }
+      if (assigned == 0) {
+        auto head = oldest_locked(slot);
+        if (head != parked_.end() && head->first < me) reserved += head->second.need;
       }
+      pass = free - reserved >= need && coloc_ok;
+      if (p.pg_key == probe_key_[slot]) probe_key_[slot] = 0;  // the probe's answer is in
+      if (pass && pos != parked_pos_.end()) {
+        parked_.erase(pos->second);
+        parked_pos_.erase(pos);
+        parked_n_.store(parked_.size(), std::memory_order_release);
+        // Chain: the next parked group of this kind may fit what is left
+        // (one release can cover several gangs).
+        if (!probe_key_[slot]) probe = next_probe_locked(slot);
+      }
+      take_wake_locked(probe);
     }
     if (!probe.empty()) h_.activate(probe);
     if (pass) return {};
@@ -650,9 +702,21 @@ class Coscheduling : public Plugin {
     if (assigned > 0) park_rejecting(p, pg);
     else park(p, pg, d.kind, need);
     park_members(p);
+    if (!coloc_ok && free >= need)
+      return XS_FIXED_STATUS(Code::Unschedulable,
+                             "PodGroup parked: no node can host all of its remaining ranks on one xGMI mesh "
+                             "(gangColocation: Required); it retries when GPUs are released");
     return XS_FIXED_STATUS(Code::Unschedulable,
                            "PodGroup parked: its remaining members need more GPUs than are free; it retries when "
                            "GPUs are released");
+  }
+  // NRT gangColocation Required: can one node take `remaining` ranks of p's
+  // kind now? True when co-location is not required or the gang is larger
+  // than any node (it has to span nodes).
+  bool colocated_now(const Pod& p, int64_t remaining) {
+    if (!h_.gangs || h_.gangs->mode() != GangPlacement::Mode::Required || !h_.snapshot) return true;
+    if (remaining > h_.gangs->node_capacity(*h_.snapshot, p)) return true;
+    return h_.gangs->hostable(*h_.snapshot, p, remaining);
   }
   // PostFilter: does the gate's arithmetic (counting this member's own
   // remaining group) explain the Filter failure?
@@ -663,6 +727,7 @@ class Coscheduling : public Plugin {
     const int64_t need_all = units_for(d, pg.min_member);
     if (need_all > total_units(d)) return false;
     const int64_t remaining = std::max<int64_t>(1, pg.min_member - assigned);
+    if (assigned == 0 && !colocated_now(p, remaining)) return true;
     int64_t owed_others;
     {
       std::lock_guard<std::mutex> g(park_mu_);
@@ -692,14 +757,19 @@ class Coscheduling : public Plugin {
     if (h_.gang_parked) h_.gang_parked(p);
   }
   // PostFilter's park: the waiting siblings are rejected (their Unreserve
-  // must not deny the group), nothing stays owed, the group parks.
+  // must not deny the group: exactly those pods are remembered), nothing
+  // stays owed, the group parks.
   void park_rejecting(const Pod& p, const PodGroup& pg) {
-    const int n = count_waiting(p);
+    std::vector<std::string> uids;
+    h_.waiting_pods->iterate_group(p.pg_key, [&](const WaitingPodPtr& wp) {
+      const Pod& wpod = *wp->pod();
+      if (wpod.ns() == p.ns() && wpod.pod_group == p.pod_group) uids.push_back(wpod.uid());
+    });
     {
       std::lock_guard<std::mutex> g(park_mu_);
-      if (n > 0) {
+      if (!uids.empty()) {
         auto& r = parked_rejects_[p.pg_key];
-        r.first += n;
+        r.first.insert(r.first.end(), uids.begin(), uids.end());
         r.second = h_.clock->now_us();
       }
       erase_outstanding_locked(p.pg_key);
@@ -718,15 +788,21 @@ class Coscheduling : public Plugin {
       if (q->node_name.empty()) members.push_back(std::move(q));
     if (!members.empty()) h_.deactivate(members);
   }
-  bool consume_parked_reject(uint64_t key) {
+  // Unreserve of a sibling that park_rejecting rejected: absorbed (no denial).
+  // Any other Unreserve of the group (a Permit timeout, a bind failure) is not.
+  bool consume_parked_reject(uint64_t key, const std::string& uid) {
     std::lock_guard<std::mutex> g(park_mu_);
     if (!rejects_pending_locked(key)) return false;
     auto it = parked_rejects_.find(key);
-    if (--it->second.first <= 0) parked_rejects_.erase(it);
+    auto& v = it->second.first;
+    auto u = std::find(v.begin(), v.end(), uid);
+    if (u == v.end()) return false;
+    v.erase(u);
+    if (v.empty()) parked_rejects_.erase(it);
     return true;
   }
-  // Rejections of a just-parked group still to land (a stale count, e.g. a
-  // sibling allowed or timed out between the count and the reject, expires).
+  // Rejections of a just-parked group still to land (a stale list, e.g. a
+  // sibling allowed or timed out between the listing and the reject, expires).
   bool rejects_pending_locked(uint64_t key) {
     auto it = parked_rejects_.find(key);
     if (it == parked_rejects_.end()) return false;
@@ -736,33 +812,53 @@ class Coscheduling : public Plugin {
     }
     return true;
   }
-  // One member of the oldest parked group whose rejections have all landed
-  // (so its own GPUs are back), for the active queue. Caller holds park_mu_.
-  std::vector<PodPtr> next_probe_locked() {
+  // The oldest parked group of a kind slot (parked_.end() when none).
+  std::map<std::pair<MicroTime, uint64_t>, Parked>::iterator oldest_locked(int slot) {
+    for (auto it = parked_.begin(); it != parked_.end(); ++it)
+      if (kind_slot(it->second.kind) == slot) return it;
+    return parked_.end();
+  }
+  // One member of the oldest parked group of this kind whose rejections have
+  // all landed (so its own GPUs are back), for the active queue. Groups that
+  // can no longer pass the gate (denied, deleted, fewer pods than minMember,
+  // nothing left to schedule) leave the line here, so none of them holds the
+  // head. Caller holds park_mu_.
+  std::vector<PodPtr> next_probe_locked(int slot) {
     std::vector<PodPtr> out;
-    while (!parked_.empty()) {
-      auto it = parked_.begin();
-      if (rejects_pending_locked(it->first.second)) return out;  // the last Unreserve probes
+    for (auto it = oldest_locked(slot); it != parked_.end(); it = oldest_locked(slot)) {
+      const uint64_t key = it->first.second;
+      if (rejects_pending_locked(key)) return out;  // the last Unreserve probes
       Pod member;
       member.meta.ns = it->second.ns;
       member.pod_group = it->second.group;
-      member.pg_key = it->first.second;
+      member.pg_key = key;
+      auto pg = h_.informers->pod_group_of(member);
+      bool viable = pg && !denied_.has(key) &&
+                    static_cast<int64_t>(h_.informers->count_pods_in_group_of(member)) >= pg->min_member;
       // A member the cache does not hold (an assumed pod may not show its
       // node in the lister yet): activating one that is binding would lose
       // the probe until kProbeStaleUs.
-      for (auto& q : h_.informers->pods_in_group_of(member))
-        if (q->node_name.empty() && !q->terminating() && !h_.cache->get_pod(q->uid())) {
-          out.push_back(std::move(q));
-          break;
-        }
+      if (viable)
+        for (auto& q : h_.informers->pods_in_group_of(member))
+          if (q->node_name.empty() && !q->terminating() && !h_.cache->get_pod(q->uid())) {
+            out.push_back(std::move(q));
+            break;
+          }
       if (!out.empty()) {
-        probe_key_ = it->first.second;
-        probe_sent_us_ = h_.clock->now_us();
+        probe_key_[slot] = key;
+        probe_sent_us_[slot] = h_.clock->now_us();
         return out;
       }
-      parked_pos_.erase(it->first.second);  // nothing left to schedule: drop it
+      // Not viable: off the line; its unplaced members go back to the
+      // queues (they meet the reason in PreFilter and wait for an event, as
+      // upstream) instead of staying out of them.
+      parked_pos_.erase(key);
       parked_.erase(it);
       parked_n_.store(parked_.size(), std::memory_order_release);
+      if (!viable) {
+        for (auto& q : h_.informers->pods_in_group_of(member))
+          if (q->node_name.empty()) wake_.push_back(std::move(q));
+      }
     }
     return out;
   }
@@ -772,13 +868,26 @@ class Coscheduling : public Plugin {
     std::vector<PodPtr> probe;
     {
       std::lock_guard<std::mutex> g(park_mu_);
-      // One probe at a time: a probe still queued answers for this release
-      // too (its gate reads the snapshot of its own cycle, which includes it).
-      if (probe_key_ && h_.clock->now_us() - probe_sent_us_ < kProbeStaleUs) return;
-      if (probe_key_ && h_.metrics) h_.metrics->inc("xsched_coscheduling_probes_total", "result=\"stale\"");
-      probe = next_probe_locked();
+      // One probe per kind at a time: a probe still queued answers for this
+      // release too (its gate reads the snapshot of its own cycle, which
+      // includes it). XCD gangs are probed apart from whole-GPU gangs, so a
+      // big whole-GPU gang at the head never holds back XCD ranks that fit.
+      const int64_t now = h_.clock->now_us();
+      for (int k = 0; k < 2; ++k) {
+        if (probe_key_[k] && now - probe_sent_us_[k] < kProbeStaleUs) continue;
+        if (probe_key_[k] && h_.metrics) h_.metrics->inc("xsched_coscheduling_probes_total", "result=\"stale\"");
+        probe_key_[k] = 0;
+        auto more = next_probe_locked(k);
+        probe.insert(probe.end(), more.begin(), more.end());
+      }
+      take_wake_locked(probe);
     }
     if (!probe.empty()) h_.activate(probe);
+  }
+  void take_wake_locked(std::vector<PodPtr>& out) {
+    if (wake_.empty()) return;
+    out.insert(out.end(), std::make_move_iterator(wake_.begin()), std::make_move_iterator(wake_.end()));
+    wake_.clear();
   }
   struct Owed {
     GpuDemand::Kind kind = GpuDemand::None;
@@ -823,7 +932,7 @@ class Coscheduling : public Plugin {
   }
   // A probe not answered within this long (its pod went elsewhere: bound,
   // deleted, failed before the gate) no longer holds back the next one.
-  static constexpr int64_t kProbeStaleUs = 20'000;
+  static constexpr int64_t kProbeStaleUs = 5'000;
   static constexpr int64_t kRejectWindowUs = 1'000'000;
   static constexpr int64_t kMaxPermitUs = 15LL * 60 * 1'000'000;  // framework cap
   bool park_ = true;
@@ -835,11 +944,13 @@ class Coscheduling : public Plugin {
   std::map<ParkKey, Parked> parked_;
   std::unordered_map<uint64_t, ParkKey> parked_pos_;
   std::atomic<size_t> parked_n_{0};
-  std::unordered_map<uint64_t, std::pair<int, int64_t>> parked_rejects_;  // pg_key -> (Unreserves to absorb, when)
+  // pg_key -> (uids of the siblings park_rejecting rejected, when)
+  std::unordered_map<uint64_t, std::pair<std::vector<std::string>, int64_t>> parked_rejects_;
+  std::vector<PodPtr> wake_;  // members of groups dropped from the line, for the active queue
   std::unordered_map<uint64_t, Owed> outstanding_;
   int64_t owed_[2] = {0, 0};
-  uint64_t probe_key_ = 0;
-  int64_t probe_sent_us_ = 0;
+  uint64_t probe_key_[2] = {0, 0};  // per kind slot: the group whose probe is out
+  int64_t probe_sent_us_[2] = {0, 0};
   uint64_t parks_total_ = 0;
 
   Handle& h_;

@@ -31,6 +31,7 @@
 #include "common/log.h"
 #include "framework/plugin.h"
 #include "scheduler/cache.h"
+#include "scheduler/gang_placement.h"
 #include "scheduler/informers.h"
 
 namespace xsched {
@@ -69,7 +70,8 @@ class TopologyMatch : public Plugin {
   bool score_node_local(const Pod& p, const Snapshot&) const override {
     return strategy_ != Strategy::XGMI || p.pod_group.empty();
   }
-  TopologyMatch(const Json& args, Handle& h) : Plugin("NodeResourceTopologyMatch", kFilter | kPreScore | kScore), h_(h) {
+  TopologyMatch(const Json& args, Handle& h)
+      : Plugin("NodeResourceTopologyMatch", kPreFilter | kFilter | kPreScore | kScore), h_(h) {
     const Json& ss = args["scoringStrategy"];
     std::string t = ss["type"].str_or("LeastAllocated");
     if (t == "MostAllocated") strategy_ = Strategy::Most;
@@ -78,6 +80,47 @@ class TopologyMatch : public Plugin {
     else if (t == "LeastAllocated") strategy_ = Strategy::Least;
     else throw std::runtime_error("illegal scoring strategy found");
     for (const auto& r : ss["resources"].items()) weights_[res_id(r["name"].as_string())] = r["weight"].as_int(1);
+    // xGMI gang co-location (gang_placement.h): on by default with the
+    // XGMIGangAffinity strategy, in PreFilter when the profile enables it.
+    colocation_ = GangPlacement::parse_mode(
+        args["gangColocation"].str_or(strategy_ == Strategy::XGMI ? "Preferred" : "None"));
+    if (h_.gangs) h_.gangs->set_mode(colocation_);
+  }
+
+  // ---- PreFilter: the gang's node set (the reference's alignment Filter,
+  // filter.go:84-150,190-216, lifted from one NUMA zone to one xGMI mesh).
+  Status pre_filter(CycleState& s, const Pod& p) override {
+    if (colocation_ == GangPlacement::Mode::Off || !h_.gangs || !h_.snapshot || p.pod_group.empty() ||
+        !GangPlacement::gang_demand(p.gpu_demand))
+      return {};
+    auto pg = h_.informers->pod_group_of(p);
+    if (!pg || pg->min_member <= 1) return {};
+    GangPlacement::Plan plan = h_.gangs->plan(*h_.snapshot, p, pg->min_member);
+    if (!plan.gang) return {};
+    if (!plan.started && h_.gang_planned) h_.gang_planned(p, plan.hostable);
+    if (!plan.restriction) return {};
+    plan.restriction->excluded = excluded_status();
+    if (plan.restriction->list.empty() && plan.restriction->mask.empty() && !plan.restriction->fallback) {
+      static const Status unhostable = [this] {
+        Status x = Status::immortal(Code::Unschedulable,
+                                    "no node can host every remaining rank of the PodGroup on one xGMI mesh "
+                                    "(gangColocation: Required)");
+        x.with_plugin(name_ptr());
+        return x;
+      }();
+      return unhostable;
+    }
+    s.write(kNodeRestrictionKey, std::move(plan.restriction));
+    return {};
+  }
+  const Status& excluded_status() const {
+    static const Status st = [this] {
+      Status x = Status::immortal(Code::Unschedulable,
+                                  "node(s) cannot host the PodGroup's remaining ranks on one xGMI mesh");
+      x.with_plugin(name_ptr());
+      return x;
+    }();
+    return st;
   }
 
   int64_t weight(int id) const {
@@ -470,9 +513,40 @@ class TopologyMatch : public Plugin {
     return {{"Pod", kDelete, ""}, {"Node", kAdd | kUpdateNodeAllocatable, ""}, {"NodeResourceTopology", kAdd | kUpdate, ""}};
   }
 
+  // Unit-test hook: "gangPlan" returns the co-location plan PreFilter would
+  // use for p (allowed node names, fallback, hostable, remaining ranks).
+  Json debug_call(const std::string& what, CycleState& s, const PodPtr& p, const Json& args) override {
+    if (what != "gangPlan") return Plugin::debug_call(what, s, p, args);
+    Json out = Json::object();
+    out.set("mode", Json(GangPlacement::mode_name(colocation_)));
+    auto pg = p->pod_group.empty() ? nullptr : h_.informers->pod_group_of(*p);
+    if (!pg || !h_.gangs || !h_.snapshot) {
+      out.set("gang", Json(false));
+      return out;
+    }
+    GangPlacement::Plan plan = h_.gangs->plan(*h_.snapshot, *p, pg->min_member);
+    out.set("gang", Json(plan.gang));
+    out.set("started", Json(plan.started));
+    out.set("remaining", Json(plan.remaining));
+    out.set("hostable", Json(plan.hostable));
+    out.set("restricted", Json(static_cast<bool>(plan.restriction)));
+    if (plan.restriction) {
+      Json nodes = Json::array();
+      const auto& r = *plan.restriction;
+      for (size_t i = 0; i < h_.snapshot->names.size(); ++i)
+        if ((!r.mask.empty() || !r.list.empty()) && r.allows(static_cast<int>(i)))
+          nodes.push_back(Json(h_.snapshot->names[i]));
+      out.set("nodes", std::move(nodes));
+      out.set("fallback", Json(r.fallback));
+    }
+    out.set("openGangs", Json(static_cast<int64_t>(h_.gangs->open_gangs())));
+    return out;
+  }
+
  private:
   Handle& h_;
   Strategy strategy_ = Strategy::Least;
+  GangPlacement::Mode colocation_ = GangPlacement::Mode::Off;
   std::map<int, int64_t> weights_;
 };
 

@@ -571,6 +571,8 @@ PYBIND11_MODULE(_xsched, m) {
           d["first_enqueue_us"] = g.first_enqueue_us;
           d["admit_us"] = g.admit_us;
           d["bound_us"] = g.bound_us;
+          d["nodes"] = g.nodes;
+          d["hostable"] = g.hostable;
           out.append(d);
         }
         py::dict res;
@@ -636,6 +638,8 @@ PYBIND11_MODULE(_xsched, m) {
               d["first_enqueue_us"] = r.first_enqueue_us;
               d["admit_us"] = r.admit_us;
               d["bound_us"] = r.bound_us;
+              d["nodes"] = static_cast<int>(r.nodes.size());
+              d["hostable"] = r.hostable;
               out.append(d);
             }
             return out;

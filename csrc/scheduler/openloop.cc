@@ -92,6 +92,8 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
       g.first_enqueue_us = r.first_enqueue_us;
       g.admit_us = r.admit_us;
       g.bound_us = r.bound_us;
+      g.nodes = static_cast<int>(r.nodes.size());
+      g.hostable = r.hostable;
       deletions.push({r.bound_us + hold_us, it->second});
       in_flight -= g.size;
       held += g.size;

@@ -40,6 +40,7 @@ struct OpenLoopResult {
   struct Gang {
     int size = 0;
     int64_t create_us = 0, first_enqueue_us = 0, admit_us = 0, bound_us = 0;
+    int nodes = 0, hostable = -1;  // placement (GangRecord)
   };
   std::vector<Gang> gangs;  // in arrival order; bound_us == 0: not admitted in time
   int64_t wall_us = 0;      // first arrival -> last gang done

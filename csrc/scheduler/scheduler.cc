@@ -353,6 +353,9 @@ Scheduler::Scheduler(std::shared_ptr<ObjectStore> store, const Json& config, std
     h.deactivate = [this](const std::vector<PodPtr>& pods) { queue_->deactivate(pods); };
     h.gang_denied = [this](const Pod& p, const char* why) { note_gang_denied(p, why); };
     h.gang_parked = [this](const Pod&) { gang_parks_total_.fetch_add(1, std::memory_order_relaxed); };
+    gang_placements_.push_back(std::make_unique<GangPlacement>(cache_.get(), clock_));
+    h.gangs = gang_placements_.back().get();
+    h.gang_planned = [this](const Pod& p, bool hostable) { note_gang_planned(p, hostable); };
     h.blocking_begin = [this] {
       if (binder_) binder_->enter_blocking();
     };
@@ -941,6 +944,8 @@ void Scheduler::note_gang_event(const Pod& p, bool bound) {
     if (r.admit_us == 0) r.admit_us = now;
     return;
   }
+  const uint64_t nh = std::hash<std::string_view>{}(std::string_view(p.node_name));
+  if (std::find(r.nodes.begin(), r.nodes.end(), nh) == r.nodes.end()) r.nodes.push_back(nh);
   if (++r.bound < need) return;
   r.bound_us = now;
   if (r.admit_us == 0) r.admit_us = now;
@@ -955,6 +960,14 @@ void Scheduler::note_gang_event(const Pod& p, bool bound) {
   hist->observe(static_cast<double>(r.bound_us - r.first_enqueue_us) / 1e6);
   gang_done_.push_back(r);
   gangs_.erase(it);
+}
+
+void Scheduler::note_gang_planned(const Pod& p, bool hostable) {
+  if (p.pod_group.empty()) return;
+  const std::string& key = gang_key(p);
+  std::lock_guard<std::mutex> g(stats_mu_);
+  auto it = gangs_.find(key);
+  if (it != gangs_.end()) it->second.hostable = hostable ? 1 : 0;
 }
 
 // Why was a gang denied? The cache's view (free SPX GPUs, those held by
@@ -1270,354 +1283,459 @@ Status Scheduler::find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p
     if (!es.is_success() || !feasible.empty()) return es;
     return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status));
   }
-  // Filter verdicts are reused only when every Filter plugin is node-local for
-  // this pod. A node with nominated pods is evaluated with them added; that
-  // verdict is cached too, keyed by the set of nominated pods that count for
-  // this pod (Framework::nominated_signature), unless one of them reacts
-  // with a PreFilter extension (the state would then not be node-local).
-  bool eq_filter = eq && fw.filters_node_local(p, snapshot_);
-  const char* nom_mark = nullptr;
-  if (eq_filter && s.nominated && !s.nominated->empty()) {
-    if (!nom_mark_valid_ || s.nominated.get() != nom_src_) refresh_nom_mark(s.nominated.get());
-    nom_mark = nom_mark_.data();
-  } else if (eq_filter && nominator_ && !nominator_->empty()) {
-    // Nominations without this cycle's view (explain, or a caller that did
-    // not snapshot them): no per-node knowledge, so no reuse.
-    eq_filter = false;
-  }
-  int start = next_start_node_;
-  // The members of one gang that share a pod template are evaluated over the
-  // node window of the first of them (upstream rotates the window every
-  // cycle, numFeasibleNodesToFind > 100 nodes): a rank then reuses its
-  // sibling's Filter verdicts and node-local scores for every node but the
-  // one the sibling took, and the gang's candidates are the same nodes
-  // XGMIGangAffinity ranks.
-  if (opts_.gang_window && !full_diagnosis && p.pg_key) {
-    if (p.pg_key == window_gang_ && p.template_hash == window_tmpl_ && window_n_ == n) {
-      start = window_start_;
-    } else {
-      window_gang_ = p.pg_key;
-      window_tmpl_ = p.template_hash;
-      window_start_ = start;
-      window_n_ = n;
+  // A PreFilter node set (NodeRestriction, upstream's PreFilterResult; the
+  // xGMI gang co-location plan of NodeResourceTopologyMatch): a short list is
+  // evaluated directly, a larger set through a mask over the usual walk.
+  const NodeRestriction* rs = s.read_as<NodeRestriction>(kNodeRestrictionKey);
+  if (rs && rs->nodes != all.size()) rs = nullptr;  // planned for another node set
+  if (rs && rs->list.empty() && rs->mask.empty()) {
+    if (rs->fallback) {
+      rs = nullptr;
+    } else {  // nothing qualifies and the plugin allows no fallback
+      d.node_to_status.reserve(all.size());
+      const bool fresh = d.node_to_status.empty();
+      for (const auto& name : snapshot_.names) {
+        if (fresh) d.node_to_status.append_unique(name, rs->excluded);
+        else d.node_to_status.emplace(name, rs->excluded);
+      }
+      d.unschedulable_plugins.insert(rs->excluded.failed_plugin());
+      return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status)).with_plugin(rs->excluded.failed_plugin());
     }
   }
-  // Per-node failures go to a position-indexed buffer (no lock, no map
-  // insert per node); the NodeToStatusMap is only materialized when the
-  // diagnosis is consumed: no feasible node (PostFilter / FitError) or explain.
-  // Equivalence-cache verdicts are referenced in place, not copied: a Status
-  // copy bumps the refcount of a failure status shared by every node, and 16
-  // workers doing that per node serialize on its cache line.
-  if (static_cast<int>(fail_buf_.size()) < n) fail_buf_.resize(n);
-  fail_ptr_.assign(n, nullptr);
-  Status first_err;
-  bool has_err = false;
-  int c = 0, processed = 0;
-  uint64_t hits = 0;
-  if (static_cast<int>(found_buf_.size()) < to_find + 1) found_buf_.resize(to_find + 1);
-  if (static_cast<int>(found_pos_buf_.size()) < to_find + 1) found_pos_buf_.resize(to_find + 1);
-  // One node's verdict: from the equivalence cache when it is valid for the
-  // node's version (and, on a node with nominated pods, for the same set of
-  // nominated pods), else computed into `own` or the cache slot.
-  auto eval_node = [&](int pos, const NodeInfo& ni, Status& own, bool* hit) -> const Status* {
-    if (!eq_filter) {
-      own = fw.run_filter_with_nominated_pods(s, p, ni);
-      return &own;
+  if (rs && rs->mask.empty()) {
+    Status r = filter_listed(fw, s, p, d, feasible, eq, *rs, feasible_pos, ext);
+    if (!r.is_success() && !r.is_unschedulable()) return r;
+    if (!feasible.empty() || !rs->fallback) return r;
+    d = Diagnosis{};  // none of the listed nodes fits: every node, as without the set
+    feasible.clear();
+    if (feasible_pos) feasible_pos->clear();
+    rs = nullptr;
+  }
+  // The walk over the node window; `rmask` (may be null) excludes nodes
+  // outside the PreFilter set (verdict rs->excluded, no Filter call).
+  auto walk = [&](const char* rmask) -> Status {
+    // Filter verdicts are reused only when every Filter plugin is node-local for
+    // this pod. A node with nominated pods is evaluated with them added; that
+    // verdict is cached too, keyed by the set of nominated pods that count for
+    // this pod (Framework::nominated_signature), unless one of them reacts
+    // with a PreFilter extension (the state would then not be node-local).
+    bool eq_filter = eq && fw.filters_node_local(p, snapshot_);
+    const char* nom_mark = nullptr;
+    if (eq_filter && s.nominated && !s.nominated->empty()) {
+      if (!nom_mark_valid_ || s.nominated.get() != nom_src_) refresh_nom_mark(s.nominated.get());
+      nom_mark = nom_mark_.data();
+    } else if (eq_filter && nominator_ && !nominator_->empty()) {
+      // Nominations without this cycle's view (explain, or a caller that did
+      // not snapshot them): no per-node knowledge, so no reuse.
+      eq_filter = false;
     }
-    EqTable& t = eq->table;
-    uint64_t sig = 0;
-    bool cacheable = true;
-    if (nom_mark && nom_mark[pos]) sig = fw.nominated_signature(s, p, nom_list_[pos], &cacheable);
-    const int64_t gen = snapshot_.gen[pos];
-    if (sig == 0) {  // no nominated pod counts for this pod: the plain verdict
-      if (t.filter_gen[pos] == gen) {
+    int start = next_start_node_;
+    // The members of one gang that share a pod template are evaluated over the
+    // node window of the first of them (upstream rotates the window every
+    // cycle, numFeasibleNodesToFind > 100 nodes): a rank then reuses its
+    // sibling's Filter verdicts and node-local scores for every node but the
+    // one the sibling took, and the gang's candidates are the same nodes
+    // XGMIGangAffinity ranks.
+    if (opts_.gang_window && !full_diagnosis && p.pg_key) {
+      if (p.pg_key == window_gang_ && p.template_hash == window_tmpl_ && window_n_ == n) {
+        start = window_start_;
+      } else {
+        window_gang_ = p.pg_key;
+        window_tmpl_ = p.template_hash;
+        window_start_ = start;
+        window_n_ = n;
+      }
+    }
+    // Per-node failures go to a position-indexed buffer (no lock, no map
+    // insert per node); the NodeToStatusMap is only materialized when the
+    // diagnosis is consumed: no feasible node (PostFilter / FitError) or explain.
+    // Equivalence-cache verdicts are referenced in place, not copied: a Status
+    // copy bumps the refcount of a failure status shared by every node, and 16
+    // workers doing that per node serialize on its cache line.
+    if (static_cast<int>(fail_buf_.size()) < n) fail_buf_.resize(n);
+    fail_ptr_.assign(n, nullptr);
+    Status first_err;
+    bool has_err = false;
+    int c = 0, processed = 0;
+    uint64_t hits = 0;
+    if (static_cast<int>(found_buf_.size()) < to_find + 1) found_buf_.resize(to_find + 1);
+    if (static_cast<int>(found_pos_buf_.size()) < to_find + 1) found_pos_buf_.resize(to_find + 1);
+    // One node's verdict: from the equivalence cache when it is valid for the
+    // node's version (and, on a node with nominated pods, for the same set of
+    // nominated pods), else computed into `own` or the cache slot.
+    auto eval_node = [&](int pos, const NodeInfo& ni, Status& own, bool* hit) -> const Status* {
+      if (rmask && !rmask[pos]) {
         *hit = true;
-      } else {
-        t.filter[pos] = fw.run_filter(s, p, ni);
-        t.filter_gen[pos] = gen;
+        return &rs->excluded;
       }
-      return &t.filter[pos];
-    }
-    if (cacheable && t.nom_gen[pos] == gen && t.nom_sig[pos] == sig) {
-      *hit = true;
+      if (!eq_filter) {
+        own = fw.run_filter_with_nominated_pods(s, p, ni);
+        return &own;
+      }
+      EqTable& t = eq->table;
+      uint64_t sig = 0;
+      bool cacheable = true;
+      if (nom_mark && nom_mark[pos]) sig = fw.nominated_signature(s, p, nom_list_[pos], &cacheable);
+      const int64_t gen = snapshot_.gen[pos];
+      if (sig == 0) {  // no nominated pod counts for this pod: the plain verdict
+        if (t.filter_gen[pos] == gen) {
+          *hit = true;
+        } else {
+          t.filter[pos] = fw.run_filter(s, p, ni);
+          t.filter_gen[pos] = gen;
+        }
+        return &t.filter[pos];
+      }
+      if (cacheable && t.nom_gen[pos] == gen && t.nom_sig[pos] == sig) {
+        *hit = true;
+        return &t.nom_filter[pos];
+      }
+      Status st = fw.run_filter_with_nominated_pods(s, p, ni);
+      if (!cacheable) {
+        own = std::move(st);
+        return &own;
+      }
+      t.nom_filter[pos] = std::move(st);
+      t.nom_gen[pos] = gen;
+      t.nom_sig[pos] = sig;
       return &t.nom_filter[pos];
-    }
-    Status st = fw.run_filter_with_nominated_pods(s, p, ni);
-    if (!cacheable) {
-      own = std::move(st);
-      return &own;
-    }
-    t.nom_filter[pos] = std::move(st);
-    t.nom_gen[pos] = gen;
-    t.nom_sig[pos] = sig;
-    return &t.nom_filter[pos];
-  };
-  // The template's last scan of this window (EqEntry::scan): a gang rank
-  // after its sibling re-evaluates only the scanned nodes whose version
-  // changed since (usually the node the sibling took) and re-cuts the list at
-  // numFeasibleNodesToFind, instead of walking the whole window again.
-  EqEntry::ScanMemo* memo =
-      (opts_.scan_memo && eq && eq_filter && !nom_mark && !full_diagnosis && !ext) ? &eq->scan : nullptr;
-  if (memo && !(memo->valid && memo->start == start && memo->n == n && memo->to_find == to_find &&
-                memo->epoch == snapshot_.node_epoch))
-    memo->valid = false;
-  const bool inline_ok = parallelizer_->plan_inline(n, &filter_site_);
-  bool served = false;
-  if (memo && memo->valid && inline_ok) {
-    bool ok = true;
-    int reevaluated = 0;
-    const int m = memo->processed;
-    auto at = [&](int off) { return start + off >= n ? start + off - n : start + off; };
-    // The window is at most two contiguous runs of positions; each is checked
-    // in blocks with memcmp, and only a block that differs element-wise.
-    const int64_t* mg = memo->gens.data();
-    const int64_t* sg = snapshot_.gen.data();
-    constexpr int kBlock = 32;
-    for (int off0 = 0; off0 < m && ok;) {
-      const int pos0 = at(off0);
-      const int run = std::min({m - off0, n - pos0, kBlock});
-      if (std::memcmp(mg + off0, sg + pos0, static_cast<size_t>(run) * sizeof(int64_t)) != 0) {
-        for (int j = 0; j < run && ok; ++j) {
-          const int off = off0 + j, pos = pos0 + j;
-          if (mg[off] == sg[pos]) continue;
-          bool hit = false;
-          const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
-          ++reevaluated;
-          ok = fp->is_success() || fp->is_unschedulable();
-          memo->ok[off] = fp->is_success();
-          memo->gens[off] = sg[pos];
-        }
-      }
-      off0 += run;
-    }
-    // Re-cut the list: branch-free appends (the buffers hold to_find + 1),
-    // over the window's two contiguous runs ([start, n), then [0, ...)), with
-    // every bound and base pointer in a local: a store to the int buffer
-    // could alias `start`, whose address the lambdas above hold, and forced
-    // a reload per node.
-    int off = 0;
-    if (ok) {
-      const char* okv = memo->ok.data();
-      const NodeInfoPtr* allp = all.data();
-      const NodeInfo** fb = found_buf_.data();
-      int* fpb = found_pos_buf_.data();
-      const int s0 = start, nn = n, mm = m, want = to_find;
-      int cc = c;
-      for (int run = 0; run < 2 && off < mm && cc < want; ++run) {
-        const int first_off = off;
-        const int first_pos = run == 0 ? s0 : 0;
-        const int end_off = run == 0 ? std::min(mm, nn - s0) : mm;
-        for (; off < end_off && cc < want; ++off) {
-          const int pos = first_pos + (off - first_off);
-          fb[cc] = allp[pos].get();
-          fpb[cc] = pos;
-          cc += okv[off] != 0;
-        }
-      }
-      c = cc;
-    }
-    for (; ok && c < to_find && off < n; ++off) {  // the scan has to reach further now
-      const int pos = at(off);
-      bool hit = false;
-      const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
-      ++reevaluated;
-      ok = fp->is_success() || fp->is_unschedulable();
-      if (off < static_cast<int>(memo->gens.size())) {
-        memo->gens[off] = snapshot_.gen[pos];
-        memo->ok[off] = fp->is_success();
-      } else {
-        memo->gens.push_back(snapshot_.gen[pos]);
-        memo->ok.push_back(fp->is_success());
-      }
-      if (fp->is_success()) {
-        found_buf_[c] = all[pos].get();
-        found_pos_buf_[c] = pos;
-        ++c;
-      }
-    }
-    if (ok && c > 0) {
-      processed = off;
-      memo->processed = off;
-      hits = static_cast<uint64_t>(std::max(0, processed - reevaluated));
-      served = true;
-    } else {  // an error, or nothing feasible (the diagnosis needs every verdict): the full walk
+    };
+    // The template's last scan of this window (EqEntry::scan): a gang rank
+    // after its sibling re-evaluates only the scanned nodes whose version
+    // changed since (usually the node the sibling took) and re-cuts the list at
+    // numFeasibleNodesToFind, instead of walking the whole window again.
+    EqEntry::ScanMemo* memo =
+        (opts_.scan_memo && eq && eq_filter && !nom_mark && !full_diagnosis && !ext && !rmask) ? &eq->scan
+                                                                                                  : nullptr;
+    if (memo && !(memo->valid && memo->start == start && memo->n == n && memo->to_find == to_find &&
+                  memo->epoch == snapshot_.node_epoch))
       memo->valid = false;
-      c = 0;
-    }
-  }
-  if (served) {
-    bool mismatch = false;
-    if (opts_.scan_memo_verify) {  // the full walk must find the same nodes and stop at the same one
-      int vc = 0, vp = 0;
-      for (int i = 0; i < n && vc < to_find && !mismatch; ++i) {
-        const int pos = start + i >= n ? start + i - n : start + i;
+    const bool inline_ok = parallelizer_->plan_inline(n, &filter_site_);
+    bool served = false;
+    if (memo && memo->valid && inline_ok) {
+      bool ok = true;
+      int reevaluated = 0;
+      const int m = memo->processed;
+      auto at = [&](int off) { return start + off >= n ? start + off - n : start + off; };
+      // The window is at most two contiguous runs of positions; each is checked
+      // in blocks with memcmp, and only a block that differs element-wise.
+      const int64_t* mg = memo->gens.data();
+      const int64_t* sg = snapshot_.gen.data();
+      constexpr int kBlock = 32;
+      for (int off0 = 0; off0 < m && ok;) {
+        const int pos0 = at(off0);
+        const int run = std::min({m - off0, n - pos0, kBlock});
+        if (std::memcmp(mg + off0, sg + pos0, static_cast<size_t>(run) * sizeof(int64_t)) != 0) {
+          for (int j = 0; j < run && ok; ++j) {
+            const int off = off0 + j, pos = pos0 + j;
+            if (mg[off] == sg[pos]) continue;
+            bool hit = false;
+            const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
+            ++reevaluated;
+            ok = fp->is_success() || fp->is_unschedulable();
+            memo->ok[off] = fp->is_success();
+            memo->gens[off] = sg[pos];
+          }
+        }
+        off0 += run;
+      }
+      // Re-cut the list: branch-free appends (the buffers hold to_find + 1),
+      // over the window's two contiguous runs ([start, n), then [0, ...)), with
+      // every bound and base pointer in a local: a store to the int buffer
+      // could alias `start`, whose address the lambdas above hold, and forced
+      // a reload per node.
+      int off = 0;
+      if (ok) {
+        const char* okv = memo->ok.data();
+        const NodeInfoPtr* allp = all.data();
+        const NodeInfo** fb = found_buf_.data();
+        int* fpb = found_pos_buf_.data();
+        const int s0 = start, nn = n, mm = m, want = to_find;
+        int cc = c;
+        for (int run = 0; run < 2 && off < mm && cc < want; ++run) {
+          const int first_off = off;
+          const int first_pos = run == 0 ? s0 : 0;
+          const int end_off = run == 0 ? std::min(mm, nn - s0) : mm;
+          for (; off < end_off && cc < want; ++off) {
+            const int pos = first_pos + (off - first_off);
+            fb[cc] = allp[pos].get();
+            fpb[cc] = pos;
+            cc += okv[off] != 0;
+          }
+        }
+        c = cc;
+      }
+      for (; ok && c < to_find && off < n; ++off) {  // the scan has to reach further now
+        const int pos = at(off);
         bool hit = false;
         const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
-        ++vp;
-        if (fp->is_success()) mismatch = vc >= c || found_pos_buf_[vc++] != pos;
-      }
-      mismatch = mismatch || vc != c || vp != processed;
-    }
-    cnt_.scan_memo_served.fetch_add(1, std::memory_order_relaxed);
-    cnt_.scan_memo_mismatches.fetch_add(mismatch, std::memory_order_relaxed);
-  } else if (inline_ok) {
-    // Serial path (every cluster below the parallel threshold, and larger
-    // ones whose verdicts mostly come from the equivalence cache): plain
-    // counters, no std::function call or atomic per node.
-    const int64_t t0 = Parallelizer::now_ns();
-    if (memo) {
-      memo->gens.clear();
-      memo->ok.clear();
-    }
-    for (int i = 0; i < n; ++i) {
-      int pos = start + i;
-      if (pos >= n) pos -= n;
-      const NodeInfo& ni = *all[pos];
-      bool hit = false;
-      const Status* fp = eval_node(pos, ni, fail_buf_[pos], &hit);
-      hits += hit;
-      ++processed;
-      if (memo) {
-        memo->gens.push_back(snapshot_.gen[pos]);
-        memo->ok.push_back(fp->is_success());
-      }
-      if (fp->is_success()) {
-        found_buf_[c] = &ni;
-        found_pos_buf_[c] = pos;
-        if (++c == to_find) break;
-        continue;
-      }
-      if (fp->is_unschedulable()) {
-        fail_ptr_[pos] = fp;
-        continue;
-      }
-      first_err = *fp;
-      has_err = true;
-      break;
-    }
-    if (memo) {
-      memo->valid = !has_err && c > 0;
-      memo->start = start;
-      memo->n = n;
-      memo->to_find = to_find;
-      memo->epoch = snapshot_.node_epoch;
-      memo->processed = processed;
-    }
-    Parallelizer::record_inline(&filter_site_, Parallelizer::now_ns() - t0, processed, n);
-  } else {
-    if (memo) memo->valid = false;
-    std::atomic<int> count{0};
-    std::atomic<bool> stop{false};
-    std::atomic<uint64_t> ahits{0};
-    std::mutex mu;
-    parallelizer_->until_forked(n, [&](int i) {
-      const int pos = (start + i) % n;
-      const NodeInfo& ni = *all[pos];
-      Status own;
-      bool hit = false;
-      const Status* fp = eval_node(pos, ni, own, &hit);
-      if (hit) ahits.fetch_add(1, std::memory_order_relaxed);
-      const Status& fst = *fp;
-      if (fst.is_success()) {
-        int len = count.fetch_add(1) + 1;
-        if (len > to_find) {
-          stop.store(true);
-          count.fetch_sub(1);
+        ++reevaluated;
+        ok = fp->is_success() || fp->is_unschedulable();
+        if (off < static_cast<int>(memo->gens.size())) {
+          memo->gens[off] = snapshot_.gen[pos];
+          memo->ok[off] = fp->is_success();
         } else {
-          found_buf_[len - 1] = &ni;
-          found_pos_buf_[len - 1] = pos;
-          if (len == to_find) stop.store(true);
+          memo->gens.push_back(snapshot_.gen[pos]);
+          memo->ok.push_back(fp->is_success());
         }
-        return;
-      }
-      if (fst.is_unschedulable()) {
-        if (fp == &own) {
-          fail_buf_[pos] = std::move(own);
-          fp = &fail_buf_[pos];
+        if (fp->is_success()) {
+          found_buf_[c] = all[pos].get();
+          found_pos_buf_[c] = pos;
+          ++c;
         }
-        fail_ptr_[pos] = fp;
-        return;
       }
-      std::lock_guard<std::mutex> g(mu);
-      if (!has_err) {
-        first_err = fst;
+      if (ok && c > 0) {
+        processed = off;
+        memo->processed = off;
+        hits = static_cast<uint64_t>(std::max(0, processed - reevaluated));
+        served = true;
+      } else {  // an error, or nothing feasible (the diagnosis needs every verdict): the full walk
+        memo->valid = false;
+        c = 0;
+      }
+    }
+    if (served) {
+      bool mismatch = false;
+      if (opts_.scan_memo_verify) {  // the full walk must find the same nodes and stop at the same one
+        int vc = 0, vp = 0;
+        for (int i = 0; i < n && vc < to_find && !mismatch; ++i) {
+          const int pos = start + i >= n ? start + i - n : start + i;
+          bool hit = false;
+          const Status* fp = eval_node(pos, *all[pos], fail_buf_[pos], &hit);
+          ++vp;
+          if (fp->is_success()) mismatch = vc >= c || found_pos_buf_[vc++] != pos;
+        }
+        mismatch = mismatch || vc != c || vp != processed;
+      }
+      cnt_.scan_memo_served.fetch_add(1, std::memory_order_relaxed);
+      cnt_.scan_memo_mismatches.fetch_add(mismatch, std::memory_order_relaxed);
+    } else if (inline_ok) {
+      // Serial path (every cluster below the parallel threshold, and larger
+      // ones whose verdicts mostly come from the equivalence cache): plain
+      // counters, no std::function call or atomic per node.
+      const int64_t t0 = Parallelizer::now_ns();
+      if (memo) {
+        memo->gens.clear();
+        memo->ok.clear();
+      }
+      for (int i = 0; i < n; ++i) {
+        int pos = start + i;
+        if (pos >= n) pos -= n;
+        const NodeInfo& ni = *all[pos];
+        bool hit = false;
+        const Status* fp = eval_node(pos, ni, fail_buf_[pos], &hit);
+        hits += hit;
+        ++processed;
+        if (memo) {
+          memo->gens.push_back(snapshot_.gen[pos]);
+          memo->ok.push_back(fp->is_success());
+        }
+        if (fp->is_success()) {
+          found_buf_[c] = &ni;
+          found_pos_buf_[c] = pos;
+          if (++c == to_find) break;
+          continue;
+        }
+        if (fp->is_unschedulable()) {
+          fail_ptr_[pos] = fp;
+          continue;
+        }
+        first_err = *fp;
         has_err = true;
-        stop.store(true);
+        break;
       }
-    }, &stop, &filter_site_);
-    c = std::min(count.load(), to_find);
-    // Processed = feasible kept + failed (upstream's feasible +
-    // len(NodeToStatusMap)); counted here instead of by a shared atomic
-    // that every worker would bump per node.
-    processed = c;
-    for (int pos = 0; pos < n; ++pos) processed += fail_ptr_[pos] != nullptr;
-    hits = ahits.load();
-  }
-  if (eq_filter) {
-    cnt_.eq_filter_hits.fetch_add(hits, std::memory_order_relaxed);
-    cnt_.eq_filter_misses.fetch_add(static_cast<uint64_t>(processed) - hits, std::memory_order_relaxed);
-  }
-  if (has_err) return first_err;
-  next_start_node_ = (start + processed) % n;
-  feasible.assign(found_buf_.begin(), found_buf_.begin() + c);
-  if (feasible_pos) feasible_pos->assign(found_pos_buf_.begin(), found_pos_buf_.begin() + c);
-  // Failed nodes mostly share a few Status objects (plugins memoize their
-  // failures), so plugins and reasons are tallied per distinct Status first.
-  std::vector<std::pair<const Status*, int>> distinct;
-  if (feasible.empty() || full_diagnosis) {
-    std::unordered_map<const void*, std::unordered_map<const void*, size_t>> index;  // past 32 distinct
-    // A fresh diagnosis is recorded in deferred form: (position, status)
-    // pairs over the snapshot's names and this cycle's Filter buffers, which
-    // outlive every consumer of the diagnosis (PostFilter, FitError).
-    const bool fresh = d.node_to_status.empty();
-    if (fresh) d.node_to_status.defer(&snapshot_.names, &snapshot_.index);
-    else d.node_to_status.reserve(d.node_to_status.size() + static_cast<size_t>(n));
-    for (int pos = 0; pos < n; ++pos) {
-      const Status* fs = fail_ptr_[pos];
-      if (!fs) continue;
-      if (fresh) d.node_to_status.append_deferred(pos, fs);
-      else d.node_to_status.emplace(snapshot_.names[pos], *fs);
-      size_t k = distinct.size();
-      if (distinct.size() <= 32) {
-        for (size_t j = 0; j < distinct.size(); ++j)
-          if (distinct[j].first->reasons_id() == fs->reasons_id() && distinct[j].first->plugin_id() == fs->plugin_id()) {
-            k = j;
-            break;
+      if (memo) {
+        memo->valid = !has_err && c > 0;
+        memo->start = start;
+        memo->n = n;
+        memo->to_find = to_find;
+        memo->epoch = snapshot_.node_epoch;
+        memo->processed = processed;
+      }
+      Parallelizer::record_inline(&filter_site_, Parallelizer::now_ns() - t0, processed, n);
+    } else {
+      if (memo) memo->valid = false;
+      std::atomic<int> count{0};
+      std::atomic<bool> stop{false};
+      std::atomic<uint64_t> ahits{0};
+      std::mutex mu;
+      parallelizer_->until_forked(n, [&](int i) {
+        const int pos = (start + i) % n;
+        const NodeInfo& ni = *all[pos];
+        Status own;
+        bool hit = false;
+        const Status* fp = eval_node(pos, ni, own, &hit);
+        if (hit) ahits.fetch_add(1, std::memory_order_relaxed);
+        const Status& fst = *fp;
+        if (fst.is_success()) {
+          int len = count.fetch_add(1) + 1;
+          if (len > to_find) {
+            stop.store(true);
+            count.fetch_sub(1);
+          } else {
+            found_buf_[len - 1] = &ni;
+            found_pos_buf_[len - 1] = pos;
+            if (len == to_find) stop.store(true);
           }
-      } else {
-        auto& by_plugin = index[fs->reasons_id()];
-        auto it = by_plugin.find(fs->plugin_id());
-        if (it != by_plugin.end()) k = it->second;
-      }
-      if (k == distinct.size()) {
-        distinct.emplace_back(fs, 0);
-        if (distinct.size() == 33)  // switch to the index
+          return;
+        }
+        if (fst.is_unschedulable()) {
+          if (fp == &own) {
+            fail_buf_[pos] = std::move(own);
+            fp = &fail_buf_[pos];
+          }
+          fail_ptr_[pos] = fp;
+          return;
+        }
+        std::lock_guard<std::mutex> g(mu);
+        if (!has_err) {
+          first_err = fst;
+          has_err = true;
+          stop.store(true);
+        }
+      }, &stop, &filter_site_);
+      c = std::min(count.load(), to_find);
+      // Processed = feasible kept + failed (upstream's feasible +
+      // len(NodeToStatusMap)); counted here instead of by a shared atomic
+      // that every worker would bump per node.
+      processed = c;
+      for (int pos = 0; pos < n; ++pos) processed += fail_ptr_[pos] != nullptr;
+      hits = ahits.load();
+    }
+    if (eq_filter) {
+      cnt_.eq_filter_hits.fetch_add(hits, std::memory_order_relaxed);
+      cnt_.eq_filter_misses.fetch_add(static_cast<uint64_t>(processed) - hits, std::memory_order_relaxed);
+    }
+    if (has_err) return first_err;
+    next_start_node_ = (start + processed) % n;
+    feasible.assign(found_buf_.begin(), found_buf_.begin() + c);
+    if (feasible_pos) feasible_pos->assign(found_pos_buf_.begin(), found_pos_buf_.begin() + c);
+    // Failed nodes mostly share a few Status objects (plugins memoize their
+    // failures), so plugins and reasons are tallied per distinct Status first.
+    std::vector<std::pair<const Status*, int>> distinct;
+    if (feasible.empty() || full_diagnosis) {
+      std::unordered_map<const void*, std::unordered_map<const void*, size_t>> index;  // past 32 distinct
+      // A fresh diagnosis is recorded in deferred form: (position, status)
+      // pairs over the snapshot's names and this cycle's Filter buffers, which
+      // outlive every consumer of the diagnosis (PostFilter, FitError).
+      const bool fresh = d.node_to_status.empty();
+      if (fresh) d.node_to_status.defer(&snapshot_.names, &snapshot_.index);
+      else d.node_to_status.reserve(d.node_to_status.size() + static_cast<size_t>(n));
+      for (int pos = 0; pos < n; ++pos) {
+        const Status* fs = fail_ptr_[pos];
+        if (!fs) continue;
+        if (fresh) d.node_to_status.append_deferred(pos, fs);
+        else d.node_to_status.emplace(snapshot_.names[pos], *fs);
+        size_t k = distinct.size();
+        if (distinct.size() <= 32) {
           for (size_t j = 0; j < distinct.size(); ++j)
-            index[distinct[j].first->reasons_id()][distinct[j].first->plugin_id()] = j;
-        else if (distinct.size() > 33)
-          index[fs->reasons_id()][fs->plugin_id()] = k;
+            if (distinct[j].first->reasons_id() == fs->reasons_id() && distinct[j].first->plugin_id() == fs->plugin_id()) {
+              k = j;
+              break;
+            }
+        } else {
+          auto& by_plugin = index[fs->reasons_id()];
+          auto it = by_plugin.find(fs->plugin_id());
+          if (it != by_plugin.end()) k = it->second;
+        }
+        if (k == distinct.size()) {
+          distinct.emplace_back(fs, 0);
+          if (distinct.size() == 33)  // switch to the index
+            for (size_t j = 0; j < distinct.size(); ++j)
+              index[distinct[j].first->reasons_id()][distinct[j].first->plugin_id()] = j;
+          else if (distinct.size() > 33)
+            index[fs->reasons_id()][fs->plugin_id()] = k;
+        }
+        ++distinct[k].second;
       }
-      ++distinct[k].second;
+      for (const auto& [s0, cnt] : distinct) d.unschedulable_plugins.insert(s0->failed_plugin());
     }
-    for (const auto& [s0, cnt] : distinct) d.unschedulable_plugins.insert(s0->failed_plugin());
-  }
-  if (feasible.empty()) {
-    // FitError message: "0/N nodes are available: k reason, ..."
-    std::map<std::string, int> reasons;
-    for (const auto& [s0, cnt] : distinct)
-      for (const auto& r : s0->reasons()) reasons[r] += cnt;
-    std::string msg = "0/" + std::to_string(n) + " nodes are available:";
-    bool first = true;
-    for (const auto& kv : reasons) {
-      msg += (first ? " " : ", ") + std::to_string(kv.second) + " " + kv.first;
-      first = false;
+    if (feasible.empty()) {
+      // FitError message: "0/N nodes are available: k reason, ..."
+      std::map<std::string, int> reasons;
+      for (const auto& [s0, cnt] : distinct)
+        for (const auto& r : s0->reasons()) reasons[r] += cnt;
+      std::string msg = "0/" + std::to_string(n) + " nodes are available:";
+      bool first = true;
+      for (const auto& kv : reasons) {
+        msg += (first ? " " : ", ") + std::to_string(kv.second) + " " + kv.first;
+        first = false;
+      }
+      msg += ".";
+      return Status(Code::Unschedulable, msg);
     }
-    msg += ".";
-    return Status(Code::Unschedulable, msg);
+    if (!ext) return {};
+    Status es = run_extender_filters(p, feasible, feasible_pos, d);
+    if (!es.is_success() || !feasible.empty()) return es;
+    return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status));
+  };
+  if (rs && !rs->mask.empty()) {
+    Status r = walk(rs->mask.data());
+    if (!r.is_success() && !r.is_unschedulable()) return r;
+    if (!feasible.empty() || !rs->fallback) return r;
+    d = Diagnosis{};
+    feasible.clear();
+    if (feasible_pos) feasible_pos->clear();
   }
-  if (!ext) return {};
-  Status es = run_extender_filters(p, feasible, feasible_pos, d);
-  if (!es.is_success() || !feasible.empty()) return es;
+  return walk(nullptr);
+}
+
+Status Scheduler::filter_listed(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, NodeList& feasible,
+                                EqEntry* eq, const NodeRestriction& rs, std::vector<int>* feasible_pos, bool ext) {
+  const auto& all = snapshot_.nodes;
+  const int n = static_cast<int>(all.size());
+  // The equivalence-cache slot is reused when the verdict is node-local and
+  // no nominated pod could change it (the walk's rule, without the
+  // per-node nomination signatures).
+  const bool use_eq = eq && fw.filters_node_local(p, snapshot_) && !(s.nominated && !s.nominated->empty()) &&
+                      !(nominator_ && !nominator_->empty());
+  thread_local std::vector<std::pair<int, Status>> failed;
+  failed.clear();
+  uint64_t hits = 0;
+  for (int pos : rs.list) {
+    if (pos < 0 || pos >= n) continue;
+    const NodeInfo& ni = *all[pos];
+    Status st;
+    if (use_eq) {
+      EqTable& t = eq->table;
+      if (t.filter_gen[pos] == snapshot_.gen[pos]) {
+        ++hits;
+      } else {
+        t.filter[pos] = fw.run_filter(s, p, ni);
+        t.filter_gen[pos] = snapshot_.gen[pos];
+      }
+      st = t.filter[pos];
+    } else {
+      st = fw.run_filter_with_nominated_pods(s, p, ni);
+    }
+    if (st.is_success()) {
+      feasible.push_back(&ni);
+      if (feasible_pos) feasible_pos->push_back(pos);
+    } else if (st.is_unschedulable()) {
+      failed.emplace_back(pos, std::move(st));
+    } else {
+      return st;
+    }
+  }
+  if (use_eq) {
+    cnt_.eq_filter_hits.fetch_add(hits, std::memory_order_relaxed);
+    cnt_.eq_filter_misses.fetch_add(rs.list.size() - hits, std::memory_order_relaxed);
+  }
+  if (!feasible.empty()) {
+    if (!ext) return {};
+    Status es = run_extender_filters(p, feasible, feasible_pos, d);
+    if (!es.is_success() || !feasible.empty()) return es;
+  }
+  if (rs.fallback) return Status(Code::Unschedulable);  // the caller evaluates every node
+  d.node_to_status.reserve(all.size());
+  for (int pos = 0; pos < n; ++pos) {
+    const Status* st = &rs.excluded;
+    for (const auto& [q, fs] : failed)
+      if (q == pos) st = &fs;
+    d.node_to_status.emplace(snapshot_.names[pos], *st);
+  }
+  d.unschedulable_plugins.insert(rs.excluded.failed_plugin());
+  for (const auto& [q, fs] : failed) d.unschedulable_plugins.insert(fs.failed_plugin());
   return Status(Code::Unschedulable, fit_error_message(n, d.node_to_status));
 }
 

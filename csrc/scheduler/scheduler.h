@@ -31,6 +31,7 @@
 #include "framework/framework.h"
 #include "scheduler/cache.h"
 #include "scheduler/extender.h"
+#include "scheduler/gang_placement.h"
 #include "scheduler/informers.h"
 #include "scheduler/metrics.h"
 #include "scheduler/queue.h"
@@ -160,6 +161,11 @@ struct GangRecord {
   int64_t first_enqueue_us = 0;
   int64_t admit_us = 0;   // last member allowed at Permit
   int64_t bound_us = 0;   // last member bound
+  // Placement: distinct nodes the bound members landed on (hashes of their
+  // names), and whether one node could take the whole gang when its first
+  // rank was planned (-1: not planned, e.g. no GPU ranks or co-location off).
+  std::vector<uint64_t> nodes;
+  int hostable = -1;
 };
 
 // One Coscheduling group denial with the GPU census at that moment
@@ -334,6 +340,11 @@ class Scheduler {
   Status find_nodes_that_fit(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, NodeList& feasible,
                              EqEntry* eq = nullptr, bool full_diagnosis = false, std::vector<int>* feasible_pos = nullptr);
   int num_feasible_nodes_to_find(Framework& fw, int n) const;
+  // Filter over a PreFilter node set given as a short position list (the
+  // nodes hosting a gang): only those nodes are evaluated; the others get
+  // the set's `excluded` verdict in the diagnosis.
+  Status filter_listed(Framework& fw, CycleState& s, const Pod& p, Diagnosis& d, NodeList& feasible, EqEntry* eq,
+                       const NodeRestriction& rs, std::vector<int>* feasible_pos, bool ext);
   // findNodesThatPassExtenders: interested filter extenders narrow
   // `feasible` (and `pos`) in order; their failures join the diagnosis.
   Status run_extender_filters(const Pod& p, NodeList& feasible, std::vector<int>* pos, Diagnosis& d);
@@ -378,6 +389,7 @@ class Scheduler {
                       const std::string& nominated, int64_t cycle, const std::set<std::string>& plugins);
   void note_gang_enqueue(const Pod& p, int64_t t);
   void note_gang_event(const Pod& p, bool bound);
+  void note_gang_planned(const Pod& p, bool hostable);
   void note_gang_denied(const Pod& p, const char* why);
   bool responsible_for(const Pod& p) const;
 
@@ -398,6 +410,7 @@ class Scheduler {
   ExtenderList extenders_;
   std::shared_ptr<const GpuNames> gpu_names_;  // from the profiles' FlexGPU args
   std::vector<std::unique_ptr<WaitingPods>> waiting_;
+  std::vector<std::unique_ptr<GangPlacement>> gang_placements_;  // one per profile (Handle::gangs)
   std::vector<std::unique_ptr<Framework>> frameworks_;
   std::unordered_map<std::string, Framework*> by_name_;
   std::unique_ptr<Executor> binder_;

@@ -75,7 +75,7 @@ PLUGIN_POINTS: dict[str, tuple[str, ...]] = {
     "Coscheduling": ("queueSort", "preFilter", "postFilter", "reserve", "permit", "postBind"),
     "CapacityScheduling": ("preFilter", "postFilter", "reserve"),
     "NodeResourcesAllocatable": ("score",),
-    "NodeResourceTopologyMatch": ("filter", "preScore", "score"),
+    "NodeResourceTopologyMatch": ("preFilter", "filter", "preScore", "score"),
     "TargetLoadPacking": ("score",),
     "LoadVariationRiskBalancing": ("score",),
     "PreemptionToleration": ("postFilter",),
@@ -346,7 +346,13 @@ def default_plugin_args(name: str, args: dict | None) -> dict:
         if a.get("safeVarianceSensitivity") is None or float(a["safeVarianceSensitivity"]) < 0:
             a["safeVarianceSensitivity"] = 1.0
     elif name == "NodeResourceTopologyMatch":
-        _strict(name, a, {"scoringStrategy"})
+        # gangColocation (Preferred | Required | None) is this framework's
+        # extension: xGMI gang co-location in PreFilter (native default:
+        # Preferred with XGMIGangAffinity, None otherwise).
+        _strict(name, a, {"scoringStrategy", "gangColocation"})
+        if a.get("gangColocation", "Preferred") not in ("Preferred", "Required", "None"):
+            raise ConfigError(f"{name}Args.gangColocation must be Preferred, Required or None, "
+                              f"got {a['gangColocation']!r}")
         ss = dict(a.get("scoringStrategy") or {})
         _strict(name + ".scoringStrategy", ss, {"type", "resources"})
         ss.setdefault("type", "LeastAllocated")

@@ -32,7 +32,7 @@ Each multi-rank row is judged against an expected-bandwidth model built from
 the discovered KFD io_links (`busbw_model`): a ring all-reduce on a full mesh
 drives, per rank, the direct xGMI links to the other members of its gang, so
 the model is  min over ranks of (sum of those links' one-way bandwidth) x
-RING_EFFICIENCY. `verdict` is "pass" when the placed gang reaches at least
+RING_EFFICIENCY (one-way link bandwidth: KFD reports it per direction). `verdict` is "pass" when the placed gang reaches at least
 PASS_FRACTION of the model and beats the host-staged path, "fail" otherwise,
 and "n/a" where no xGMI model applies (one GPU, or a gloo/CPU rehearsal).
 
@@ -53,11 +53,17 @@ NODE = "mi355x-live"
 NAMESPACE = "placement"
 
 # MI355X Infinity Fabric: 7 xGMI links per GPU, 153.6 GB/s per link counting
-# both directions (1,075 GB/s aggregate). Used when KFD reports no plausible
-# per-link bandwidth (its io_links max_bandwidth is in MB/s).
+# both directions (1,075 GB/s aggregate), i.e. 76.8 GB/s each way. KFD's
+# io_links `max_bandwidth` (MB/s) is the one-way figure: the MI355X box reads
+# 76,000 MB/s per xGMI link (profiles/r5bf_bench_store_shrink.json,
+# rccl_placement.node), next to the 153.6 GB/s bidirectional spec. The spec
+# value is used when KFD reports no plausible per-link bandwidth.
 XGMI_LINK_GBPS_BIDIR = 153.6
+XGMI_LINK_GBPS_ONEWAY = XGMI_LINK_GBPS_BIDIR / 2
 # Fraction of the links' one-way bandwidth a large ring all-reduce turns into
-# bus bandwidth (protocol, reduction and scheduling overheads).
+# bus bandwidth (protocol, reduction and channel scheduling overheads). An
+# assumption, not a measurement: no run of this code has had more than one
+# GPU, so the 8-rank parity is unpinned until the driver's 8-GPU run.
 RING_EFFICIENCY = 0.75
 PASS_FRACTION = 0.7
 
@@ -84,11 +90,11 @@ def busbw_model(host, gpu_index: list[int]) -> dict:
             if peer is None or peer == i or peer not in members:
                 continue
             links += 1
-            gbps = lk.bandwidth_mbps / 1000.0
-            if not 20.0 <= gbps <= 400.0:  # no usable per-link figure: the part's spec
-                gbps = XGMI_LINK_GBPS_BIDIR
+            gbps = lk.bandwidth_mbps / 1000.0  # one way (see XGMI_LINK_GBPS_ONEWAY)
+            if not 10.0 <= gbps <= 200.0:  # no usable per-link figure: the part's spec
+                gbps = XGMI_LINK_GBPS_ONEWAY
                 source = "kfd io_links (topology) + MI355X link spec (bandwidth)"
-            oneway += gbps / 2.0
+            oneway += gbps
         per_rank.append((links, oneway))
     min_links = min(n for n, _ in per_rank)
     if min_links == 0:

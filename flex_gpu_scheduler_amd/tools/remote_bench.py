@@ -135,10 +135,13 @@ def run(nodes: int, pods: int, gangs: bool, bind_workers: int, clients: int, nat
         srv.wait(10)
 
 
-def _creator(url: str, prefix: str, duration_s: float, out_fd: int) -> None:
+def _creator(url: str, prefix: str, duration_s: float, out_fd: int, depth: int = 1) -> None:
     """One creator process: POST plain pods over one keep-alive connection
-    for `duration_s` seconds; writes {"created", "t0", "t1"} (monotonic)."""
-    import http.client
+    for `duration_s` seconds, `depth` requests in flight (HTTP/1.1
+    pipelining: a batch of requests is written, then their responses are
+    read; the native API server parses requests from a buffered stream, so a
+    batch costs one round trip instead of `depth`). Writes {"created", "t0",
+    "t1"} (monotonic)."""
     import socket
     from urllib.parse import urlsplit
 
@@ -147,29 +150,65 @@ def _creator(url: str, prefix: str, duration_s: float, out_fd: int) -> None:
 
     adopt_child_cpus()
     u = urlsplit(url)
-    conn = http.client.HTTPConnection(u.hostname, u.port)
-    conn.connect()
-    conn.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-    path = "/api/v1/namespaces/default/pods"
-    hdr = {"Content-Type": "application/json", "Accept": "application/json"}
+    sock = socket.create_connection((u.hostname, u.port))
+    sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
     tmpl = json.dumps(make_pod("NAME", requests={"cpu": "100m", "memory": "128Mi"}), separators=(",", ":"))
+    head = (f"POST /api/v1/namespaces/default/pods HTTP/1.1\r\nHost: {u.hostname}\r\n"
+            "Content-Type: application/json\r\nAccept: application/json\r\nContent-Length: ")
+    buf = bytearray()
+
+    def read_response() -> int:
+        nonlocal buf
+        while True:
+            e = buf.find(b"\r\n\r\n")
+            if e >= 0:
+                break
+            chunk = sock.recv(1 << 16)
+            if not chunk:
+                raise SystemExit("connection closed")
+            buf += chunk
+        hdr = bytes(buf[:e]).decode("latin-1")
+        status = int(hdr.split(" ", 2)[1])
+        length = 0
+        for line in hdr.split("\r\n")[1:]:
+            k, _, v = line.partition(":")
+            if k.strip().lower() == "content-length":
+                length = int(v.strip())
+        while len(buf) < e + 4 + length:
+            chunk = sock.recv(1 << 16)
+            if not chunk:
+                raise SystemExit("connection closed")
+            buf += chunk
+        del buf[:e + 4 + length]
+        return status
+
     i = 0
     t0 = time.monotonic()
     end = t0 + duration_s
+    depth = max(1, depth)
     while time.monotonic() < end:
-        conn.request("POST", path, body=tmpl.replace('"NAME"', f'"{prefix}-{i}"', 1).encode(), headers=hdr)
-        r = conn.getresponse()
-        r.read()
-        if r.status not in (200, 201):
-            raise SystemExit(f"create failed: {r.status}")
-        i += 1
+        out = []
+        for k in range(depth):
+            body = tmpl.replace('"NAME"', f'"{prefix}-{i + k}"', 1).encode()
+            out.append(head.encode() + str(len(body)).encode() + b"\r\n\r\n" + body)
+        sock.sendall(b"".join(out))
+        for _ in range(depth):
+            st = read_response()
+            if st not in (200, 201):
+                raise SystemExit(f"create failed: {st}")
+        i += depth
+    sock.close()
     os.write(out_fd, json.dumps({"created": i, "t0": t0, "t1": time.monotonic()}).encode())
 
 
 def run_steady(nodes: int = 128, duration_s: float = 2.0, creators: int = 8, bind_workers: int = 16,
-               warm_s: float = 0.25) -> dict:
+               warm_s: float = 0.25, depth: int = 1) -> dict:
     """Steady-state service mode: pods are created over HTTP by `creators`
-    separate processes while the (already synced) scheduler binds them."""
+    separate processes (`depth` pipelined requests each) while the (already
+    synced) scheduler binds them. `generator_limited` is true when the
+    scheduler kept up (bound within 10% of the offered creates and a small
+    backlog at the last create): the bound rate is then the generator's, not
+    the scheduler's ceiling."""
     from ..config import load_config
     from ..control import RestClient
     from ..control.remote import RemoteScheduler
@@ -188,14 +227,14 @@ def run_steady(nodes: int = 128, duration_s: float = 2.0, creators: int = 8, bin
         rs = RemoteScheduler(RestClient(url), load_config(flagship_config()), bindWorkers=bind_workers).start()
         try:
             code = ("import sys; from flex_gpu_scheduler_amd.tools.remote_bench import _creator; "
-                    "_creator(sys.argv[1], sys.argv[2], float(sys.argv[3]), 1)")
+                    "_creator(sys.argv[1], sys.argv[2], float(sys.argv[3]), 1, int(sys.argv[4]))")
             root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             env = child_env()
             env["PYTHONPATH"] = root + os.pathsep + os.environ.get("PYTHONPATH", "")
             base = rs.scheduler.stats()["bound"]
             t_start = time.monotonic()
             for c in range(creators):
-                p = subprocess.Popen([sys.executable, "-c", code, url, f"c{c}", str(duration_s)],
+                p = subprocess.Popen([sys.executable, "-c", code, url, f"c{c}", str(duration_s), str(depth)],
                                      stdout=subprocess.PIPE, env=env)
                 procs.append((p, c))
             samples = []  # (t, bound) every ~5 ms
@@ -221,10 +260,13 @@ def run_steady(nodes: int = 128, duration_s: float = 2.0, creators: int = 8, bin
             inwin = [(t, b) for t, b in samples if w0 <= t <= w1]
             rate = (inwin[-1][1] - inwin[0][1]) / (inwin[-1][0] - inwin[0][0]) if len(inwin) >= 2 else 0.0
             at_end = next((b for t, b in reversed(samples) if t <= t_last), 0)
-            return {"nodes": nodes, "creators": creators, "duration_s": duration_s,
+            offered = created / max(1e-9, t_last - t_first)
+            backlog = created - at_end
+            return {"nodes": nodes, "creators": creators, "pipeline_depth": depth, "duration_s": duration_s,
                     "created": created, "bound": bound, "all_bound": bound >= created,
-                    "offered_creates_per_s": round(created / max(1e-9, t_last - t_first), 1),
+                    "offered_creates_per_s": round(offered, 1),
                     "pods_per_s": round(rate, 1),
+                    "generator_limited": bool(rate >= 0.9 * offered and backlog <= 0.05 * created),
                     "window_s": round(max(0.0, w1 - w0), 3),
                     "backlog_at_last_create": created - at_end,
                     "drain_after_last_create_s": round(t_drained - t_last, 4),

@@ -96,6 +96,33 @@ class Shard:
         self.sched.stop()
 
 
+def gang_type(g: dict) -> str:
+    """"1" / "2" / "4" / "8" for whole-GPU gangs, "cpx4" for CPX quarter
+    gangs (workload.make_wave names them "s<step>-<k>-q")."""
+    return "cpx4" if g.get("pod_group", "").endswith("-q") else str(g["size"])
+
+
+def gang_split_summary(gangs: list[dict]) -> dict:
+    """Per gang type: how many gangs landed on more than one node (`split`),
+    and how many of those could have been hosted by one node when their first
+    rank was placed (`avoidable`: the record's `hostable` is 1). Gangs of one
+    rank cannot split and are left out."""
+    out: dict[str, dict] = {}
+    for g in gangs:
+        if g.get("size", 0) <= 1 or "nodes" not in g:
+            continue
+        row = out.setdefault(gang_type(g), {"n": 0, "split": 0, "avoidable": 0, "hostable": 0})
+        row["n"] += 1
+        split = g["nodes"] > 1
+        row["split"] += split
+        row["hostable"] += g.get("hostable", -1) == 1
+        row["avoidable"] += split and g.get("hostable", -1) == 1
+    for row in out.values():
+        row["split_fraction"] = round(row["split"] / max(1, row["n"]), 6)
+        row["avoidable_fraction"] = round(row["avoidable"] / max(1, row["n"]), 6)
+    return dict(sorted(out.items(), key=lambda kv: (kv[0].startswith("cpx"), int(kv[0].lstrip("cpx")))))
+
+
 def gang_latency_summary(gangs: list[dict], sizes: dict[str, int] | None = None, *, by_type: bool = False) -> dict:
     """p50/p99 first-member-enqueue -> last-member-bound (ms) per group size.
 

@@ -86,13 +86,22 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
             continue
         e2a = [(g["admit_us"] - g["first_enqueue_us"]) / 1e3 for g in ok]
         c2b = [(g["bound_us"] - g["create_us"]) / 1e3 for g in ok]
+        multi = [g for g in ok if g.get("nodes", 0) and int(k.lstrip("cpx")) > 1]
         out[k] = {"n": len(rows), "unbound": len(rows) - len(ok),
-                  "enqueue_to_allow_ms": _pct(e2a), "create_to_bound_ms": _pct(c2b)}
+                  "enqueue_to_allow_ms": _pct(e2a), "create_to_bound_ms": _pct(c2b),
+                  # Bound gangs on more than one node, and those of them one
+                  # node could have hosted when their first rank was placed.
+                  "split": sum(1 for g in multi if g["nodes"] > 1),
+                  "avoidable_split": sum(1 for g in multi if g["nodes"] > 1 and g.get("hostable") == 1),
+                  "multi_rank_bound": len(multi)}
     # Over every gang, an unbound one counting as infinitely late (the
     # capacity criterion of open_loop_capacity).
     c2b_all = sorted((g["bound_us"] - g["create_us"]) / 1e3 if g["bound_us"] else float("inf") for g in gangs)
     n = len(gangs)
+    multi = sum(v["multi_rank_bound"] for v in out.values())
     return {"by_gang": out, "gangs": n, "wall_s": round(wall_us / 1e6, 3),
+            "gang_split_fraction": round(sum(v["split"] for v in out.values()) / max(1, multi), 6),
+            "gang_avoidable_split_fraction": round(sum(v["avoidable_split"] for v in out.values()) / max(1, multi), 6),
             "all_gangs": {"n": n, "unbound": sum(1 for g in gangs if not g["bound_us"]),
                           "p99_create_to_bound_ms": _ms(percentile(c2b_all, 99) if c2b_all else None),
                           "p999_create_to_bound_ms": _ms(percentile(c2b_all, 99.9) if c2b_all else None),
@@ -112,7 +121,9 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     the end counts as infinitely late). Gangs arrive one at a time and are
     held at `occupancy` of the SPX GPUs, as in the measured loads.
 
-    One trial per rate, its arrival seed fixed by `seed`, no retries. Every
+    One trial per rate (two, with different arrival seeds, that must both
+    pass, for rates in the top two x1.3 steps under the burst rate), no
+    retries. Every
     trial is appended to `log` with its parked gangs, its Coscheduling
     denials and their causes (Scheduler::note_gang_denied), p99.9 and max.
     Near capacity the hold time (a few ms) is comparable to the admission
@@ -121,18 +132,29 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     transientShortage=Park) rather than being denied for the TTL as the
     reference's PostFilter does (which made a rate fail on < 1% of its
     gangs waiting 3 s)."""
+    top = max_pods_per_s / 1.3 ** 2  # rates in the top two grid steps get a second trial
+
     def served(rate: float) -> bool:
-        r = run_open_loop(shard, rate, duration_s, seed=seed, occupancy=occupancy)
-        p99 = r["all_gangs"]["p99_create_to_bound_ms"]
-        ok = p99 is not None and p99 != "inf" and p99 <= p99_budget_ms
-        if log is not None:
-            log.append({"offered_pods_per_s": round(rate, 1), "served": ok, "gangs": r["gangs"],
-                        "unbound_gangs": r["all_gangs"]["unbound"], "p99_create_to_bound_ms": p99,
-                        "p999_create_to_bound_ms": r["all_gangs"]["p999_create_to_bound_ms"],
-                        "max_create_to_bound_ms": r["all_gangs"]["max_create_to_bound_ms"],
-                        "wall_s": r["wall_s"], "denied_gangs": r["denials"]["total"],
-                        "denied_gang_fraction": r["denied_gang_fraction"], "parked_gangs": r["parked_gangs"],
-                        "denial_causes": r["denials"]["causes"]})
+        trials = 2 if rate >= top else 1
+        ok = True
+        for t in range(trials):
+            r = run_open_loop(shard, rate, duration_s, seed=seed + 7 * t, occupancy=occupancy)
+            p99 = r["all_gangs"]["p99_create_to_bound_ms"]
+            ok_t = p99 is not None and p99 != "inf" and p99 <= p99_budget_ms
+            if log is not None:
+                log.append({"offered_pods_per_s": round(rate, 1), "served": ok_t, "trial": t + 1, "trials": trials,
+                            "gangs": r["gangs"],
+                            "unbound_gangs": r["all_gangs"]["unbound"], "p99_create_to_bound_ms": p99,
+                            "p999_create_to_bound_ms": r["all_gangs"]["p999_create_to_bound_ms"],
+                            "max_create_to_bound_ms": r["all_gangs"]["max_create_to_bound_ms"],
+                            "wall_s": r["wall_s"], "denied_gangs": r["denials"]["total"],
+                            "denied_gang_fraction": r["denied_gang_fraction"], "parked_gangs": r["parked_gangs"],
+                            "denial_causes": r["denials"]["causes"],
+                            "gang_split_fraction": r["gang_split_fraction"],
+                            "gang_avoidable_split_fraction": r["gang_avoidable_split_fraction"]})
+            ok = ok and ok_t
+            if not ok:
+                break
         return ok
 
     rate = min(start_pods_per_s, max(max_pods_per_s, 1.0))
@@ -219,7 +241,8 @@ def capacity_report(shard, burst: float, seed: int = 0) -> dict:
 
 
 def capacity_in_child(nodes: int, seed: int, options: dict, burst: float, cpus: list[int] | None = None,
-                      warm_waves: int = 16, hbm_gib: int = 288, timeout_s: float = 600.0) -> dict:
+                      warm_waves: int = 16, hbm_gib: int = 288, timeout_s: float = 600.0,
+                      colocation: str = "Preferred") -> dict:
     """capacity_report in a child Python process that never loads the GPU
     runtime, on a fresh shard of the same cluster (spec, seed, options),
     warmed with `warm_waves` burst waves and pinned to `cpus`.
@@ -236,7 +259,7 @@ def capacity_in_child(nodes: int, seed: int, options: dict, burst: float, cpus: 
 
     cmd = [sys.executable, "-m", "flex_gpu_scheduler_amd.utils.openloop", "--nodes", str(nodes),
            "--seed", str(seed), "--options", json.dumps(options), "--burst", repr(float(burst)),
-           "--warm-waves", str(warm_waves), "--hbm-gib", str(hbm_gib)]
+           "--warm-waves", str(warm_waves), "--hbm-gib", str(hbm_gib), "--colocation", colocation]
     if cpus:
         cmd += ["--cpus", ",".join(map(str, cpus))]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, check=False)
@@ -257,13 +280,15 @@ def _child_main(argv: list[str] | None = None) -> int:
     ap.add_argument("--warm-waves", type=int, default=16)
     ap.add_argument("--hbm-gib", type=int, default=288)
     ap.add_argument("--cpus", default="")
+    ap.add_argument("--colocation", default="Preferred")
     a = ap.parse_args(argv)
     if a.cpus:
         os.sched_setaffinity(0, [int(c) for c in a.cpus.split(",")])  # before the shard's threads start
     from .benchrun import Shard
+    from .workload import flagship_config
 
     shard = Shard(ClusterSpec(nodes=a.nodes, hbm_gib=a.hbm_gib), namespace="bench-ol", seed=a.seed,
-                  options=json.loads(a.options))
+                  options=json.loads(a.options), config=flagship_config(gang_colocation=a.colocation))
     try:
         for i in range(a.warm_waves):
             w = shard.wave(i)

@@ -153,11 +153,15 @@ def make_wave(spec: ClusterSpec, step: int, *, namespace: str = "bench", fill: f
     return w
 
 
-def flagship_config(permit_wait_s: int = 10, denied_s: int = 3, transient_shortage: str = "Park") -> dict:
+def flagship_config(permit_wait_s: int = 10, denied_s: int = 3, transient_shortage: str = "Park",
+                    gang_colocation: str = "Preferred") -> dict:
     """KubeSchedulerConfiguration of the benchmark: Coscheduling gangs +
     FlexGPU MI355X packing (FlexGPU binds) + NRT xGMI gang placement.
     `transient_shortage`: "Park" (gangs short of free GPUs wait for a
-    release) or "Deny" (the reference: denied for `denied_s`)."""
+    release) or "Deny" (the reference: denied for `denied_s`).
+    `gang_colocation`: "Preferred" (a gang goes to a node that hosts all of
+    its ranks whenever one exists), "Required" (it waits, parked, until one
+    does) or "None" (score only)."""
     return {
         "apiVersion": "kubescheduler.config.k8s.io/v1beta3",
         "kind": "KubeSchedulerConfiguration",
@@ -165,7 +169,7 @@ def flagship_config(permit_wait_s: int = 10, denied_s: int = 3, transient_shorta
             "schedulerName": "default-scheduler",
             "plugins": {
                 "queueSort": {"enabled": [{"name": "Coscheduling"}], "disabled": [{"name": "*"}]},
-                "preFilter": {"enabled": [{"name": "Coscheduling"}]},
+                "preFilter": {"enabled": [{"name": "Coscheduling"}, {"name": "NodeResourceTopologyMatch"}]},
                 "filter": {"enabled": [{"name": "FlexGPU"}, {"name": "NodeResourceTopologyMatch"}]},
                 "postFilter": {"enabled": [{"name": "Coscheduling"}]},
                 "preScore": {"enabled": [{"name": "NodeResourceTopologyMatch"}]},
@@ -180,7 +184,8 @@ def flagship_config(permit_wait_s: int = 10, denied_s: int = 3, transient_shorta
                 {"name": "Coscheduling",
                  "args": {"permitWaitingTimeSeconds": permit_wait_s, "deniedPGExpirationTimeSeconds": denied_s,
                           "transientShortage": transient_shortage}},
-                {"name": "NodeResourceTopologyMatch", "args": {"scoringStrategy": {"type": "XGMIGangAffinity"}}},
+                {"name": "NodeResourceTopologyMatch", "args": {"scoringStrategy": {"type": "XGMIGangAffinity"},
+                                                               "gangColocation": gang_colocation}},
             ],
         }],
     }

@@ -136,8 +136,9 @@ def test_placement_verdict_model():
 
     host = fake_host(8)
     m8 = busbw_model(host, list(range(8)))
-    # fake_host links report 76,000 MB/s (both directions): 7 links x 38 GB/s one way.
-    assert m8["direct_links_min"] == 7 and abs(m8["model_busbw_GBps"] - RING_EFFICIENCY * 7 * 38.0) < 0.2
+    # KFD io_links max_bandwidth is one way: the captured box reads 76,000
+    # MB/s per xGMI link (below), as fake_host does: 7 links x 76 GB/s.
+    assert m8["direct_links_min"] == 7 and abs(m8["model_busbw_GBps"] - RING_EFFICIENCY * 7 * 76.0) < 0.2
     assert busbw_model(host, [0, 5])["direct_links_min"] == 1
     assert busbw_model(host, [3])["model_busbw_GBps"] is None
 
@@ -152,3 +153,35 @@ def test_placement_verdict_model():
     assert judge_row(row(0.8 * m8["model_busbw_GBps"], 1e6), m8, "nccl")["verdict"] == "fail"
     assert judge_row(row(0.8 * m8["model_busbw_GBps"], 10.0, correct=False), m8, "nccl")["verdict"] == "fail"
     assert judge_row(row(1.0, 1.0), m8, "gloo")["verdict"] == "n/a"
+
+
+def test_busbw_model_from_the_captured_box_io_links():
+    """The MI355X box's KFD io_links (captured under tests/fixtures/mi355x_box)
+    report 76,000 MB/s per xGMI link: the per-direction half of the part's
+    153.6 GB/s bidirectional link. A full 8-rank gang with those links models
+    0.75 x 7 x 76 = 399 GB/s of all-reduce bus bandwidth (RING_EFFICIENCY is an
+    assumption; parity with a measured 8-GPU run is unpinned)."""
+    import glob
+
+    from flex_gpu_scheduler_amd.gpu.discovery import discover_host, fake_host
+    from flex_gpu_scheduler_amd.parallel.placement import XGMI_LINK_GBPS_BIDIR, busbw_model
+
+    root = os.path.join(ROOT, "tests", "fixtures", "mi355x_box", "root")
+    bws = []
+    for f in glob.glob(os.path.join(root, "sys/class/kfd/kfd/topology/nodes/*/io_links/*/properties")):
+        props = dict(line.split() for line in open(f) if len(line.split()) == 2)
+        if props.get("type") == "11":  # xGMI
+            bws.append(int(props["max_bandwidth"]))
+    assert len(bws) >= 7 and set(bws) == {76000}
+    assert abs(bws[0] / 1000 - XGMI_LINK_GBPS_BIDIR / 2) < 1.0  # one way
+    live = discover_host(root)
+    g = [g for g in live.gpus if g.xgmi_links][0]
+    assert {lk.bandwidth_mbps for lk in g.xgmi_links} == {76000}
+    m8 = busbw_model(fake_host(8), list(range(8)))
+    assert 395 <= m8["model_busbw_GBps"] <= 405 and m8["source"] == "kfd io_links"
+    # Without a usable KFD figure the spec's one-way 76.8 GB/s stands in.
+    host = fake_host(8)
+    for gg in host.gpus:
+        for lk in gg.xgmi_links:
+            lk.bandwidth_mbps = 0
+    assert abs(busbw_model(host, list(range(8)))["model_busbw_GBps"] - 0.75 * 7 * 76.8) < 0.2

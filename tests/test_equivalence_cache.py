@@ -107,10 +107,13 @@ def test_bench_wave_identical_with_and_without_cache():
     assert all(results[0].values())
 
 
-def _wave_stats(options: dict) -> dict:
+def _wave_stats(options: dict, colocation: str = "None") -> dict:
     """One burst wave on 300 MI355X nodes (the adaptive share of nodes to
     score is < 100% there, so the node window matters), scheduled by
-    schedule_one on the calling thread; returns the scheduler's stats."""
+    schedule_one on the calling thread; returns the scheduler's stats.
+    Gang co-location is off by default here: with it, a gang's later ranks
+    are evaluated on their siblings' node only (NodeRestriction), so the
+    scan memo this exercises serves few cycles."""
     import json as _json
 
     from flex_gpu_scheduler_amd import Store, load_config, new_scheduler
@@ -123,7 +126,7 @@ def _wave_stats(options: dict) -> dict:
     w = make_wave(spec, 1, namespace="w", fill=0.6)
     store.create_many("podgroups", _json.dumps(w.pod_groups))
     store.create_many("pods", _json.dumps(w.pods))
-    s = new_scheduler(store, load_config(flagship_config()), seed=7, **options)
+    s = new_scheduler(store, load_config(flagship_config(gang_colocation=colocation)), seed=7, **options)
     try:
         s.sync_informers(50)
         while s.schedule_one(200):

@@ -190,3 +190,63 @@ def test_deleted_parked_group_leaves_the_line(store):
         assert wait_for(lambda: _parking(s, probe)["parked"] == [], timeout=5.0), _parking(s, probe)
     finally:
         s.stop()
+
+
+def test_parked_head_that_lost_a_member_does_not_block_younger_gangs(store):
+    """A parked head-of-line gang that loses a pod (the PodGroup kept) can no
+    longer pass the gate; it must leave the line instead of reserving its need
+    against every younger gang forever."""
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = scheduler(store)
+    try:
+        a = submit(store, "a", 8)
+        assert wait_for(lambda: len(bound(store, a)) == 8)
+        b = submit(store, "b", 8)
+        assert wait_for(lambda: s.gang_parks() >= 1)
+        time.sleep(1.1)  # younger than b in the queue order
+        c = submit(store, "c", 2)
+        assert wait_for(lambda: s.gang_parks() >= 2)
+        store.delete("pods", "default", b[-1])  # b now has 7 pods for minMember 8
+        time.sleep(0.1)
+        delete_all(store, a)
+        assert wait_for(lambda: len(bound(store, c)) == 2, timeout=5.0), _parking(s, store.get("pods", "default", c[0]))
+        assert bound(store, b[:-1]) == []
+        assert [g["podGroup"] for g in _parking(s, store.get("pods", "default", c[0]))["parked"]] == []
+    finally:
+        s.stop()
+
+
+def test_xcd_gang_is_probed_apart_from_a_parked_whole_gpu_gang(store):
+    """Parked whole-GPU and XCD gangs are probed per kind:
+    an XCD gang parked behind an oversized whole-GPU gang is admitted as soon
+    as CPX partitions are released, not at the 60 s unschedulable flush."""
+    from flex_gpu_scheduler_amd.models.mi355x import GPU_XCD
+
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    store.create("nodes", mi355x_node("cpx-0", mode="cpx"))
+    s = scheduler(store)
+    try:
+        a = submit(store, "a", 8)
+        assert wait_for(lambda: len(bound(store, a)) == 8)
+        b = submit(store, "b", 8)  # whole GPUs: parks at the head of the line
+        assert wait_for(lambda: s.gang_parks() >= 1)
+        time.sleep(1.1)
+
+        def xgang(name):
+            store.create("podgroups", make_pod_group(name, "default", 4))
+            names = [f"{name}-r{r}" for r in range(4)]
+            for n in names:
+                store.create("pods", make_pod(n, limits={GPU_XCD: "2"}, pod_group=name))
+            return names
+
+        fill = [xgang(f"f{i}") for i in range(8)]  # 8 x 4 x 2 XCDs = the 64 XCDs of cpx-0
+        assert wait_for(lambda: all(len(bound(store, f)) == 4 for f in fill))
+        q = xgang("q")
+        assert wait_for(lambda: s.gang_parks() >= 2)
+        t0 = time.time()
+        delete_all(store, fill[0])
+        assert wait_for(lambda: len(bound(store, q)) == 4, timeout=5.0)
+        assert time.time() - t0 < 2.0
+        assert bound(store, b) == []
+    finally:
+        s.stop()
