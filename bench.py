@@ -54,6 +54,12 @@ sys.path.insert(0, ROOT)
 METRIC = "pods/sec sched throughput + p99 PodGroup gang-admit latency, 1/2/4/8-GPU groups"
 
 
+def progress(msg: str) -> None:
+    """One progress line on stderr per phase (long untimed extras keep a
+    watcher that expects output every few minutes informed)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _free_port() -> int:
     import socket
 
@@ -240,8 +246,10 @@ def main() -> int:
     interleave = os.environ.get("XSCHED_BENCH_INTERLEAVE", "1") != "0"
     prepared = [w.chunks_json() if interleave else (w.groups_json(), w.pods_json()) for w in waves]
 
+    progress(f"rank {ctx.rank}: warm-up ({args.warmup * wps} waves)")
     for i in range(args.warmup * wps):
         shard.run(waves[i], prepared=prepared[i])
+    progress(f"rank {ctx.rank}: timed steps")
 
     if args.trace and ctx.rank == 0:
         shard.sched.set_trace(True)
@@ -303,7 +311,9 @@ def main() -> int:
             return None
         return pin_cpus(args.cpus, 0, order=ranked_domains())
 
+    progress(f"timed region done: {pods / t_rank if t_rank > 0 else 0:.0f} pods/s on rank 0")
     if not args.no_open_loop:
+        progress("open-loop capacity search")
         # Untimed: Poisson gang arrivals at 50% / 90% of this shard's measured
         # open-loop capacity, gang types interleaved, held then deleted
         # (utils/openloop.py) — admission latency rather than burst queueing.
@@ -355,6 +365,7 @@ def main() -> int:
     shard.close()
 
     if args.nodes1024_waves > 0:
+        progress("1,024-node run")
         # Untimed: the same workload on one 1,024-node shard (12k pods/wave).
         repin()
         try:
@@ -369,6 +380,7 @@ def main() -> int:
         except Exception as e:  # noqa: BLE001
             extras["nodes1024"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_service_mode:
+        progress("service mode")
         # Untimed: the deployable shape — scheduler and API server in separate
         # processes over loopback HTTP (tools/remote_bench.py): steady state
         # (pods created over HTTP by other processes while it schedules), and
@@ -409,6 +421,7 @@ def main() -> int:
         # (outside the timed region; utils/scenarios.py).
         from flex_gpu_scheduler_amd.utils.scenarios import run_all
 
+        progress("BASELINE scenarios")
         extras["scenarios"] = run_all()
     if ctx.rank == 0:
         lat = gang_latency_summary(all_gangs)
