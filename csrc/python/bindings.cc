@@ -685,6 +685,20 @@ PYBIND11_MODULE(_xsched, m) {
              d["activation_marks"] = s.queue().pending_activations();
              return d;
            })
+      // NextPod without a scheduling cycle (the reference's integration tests
+      // pop the queue of a scheduler that is not running, qos_test.go:129).
+      .def(
+          "next_pod",
+          [](Scheduler& s, int timeout_ms) -> py::object {
+            QueuedPodInfoPtr q;
+            {
+              py::gil_scoped_release r;
+              q = s.queue().pop(timeout_ms);
+            }
+            if (!q) return py::none();
+            return py::str(q->pod->key());
+          },
+          py::arg("timeout_ms") = 0)
       .def("flush_backoff", [](Scheduler& s) { s.queue().flush_backoff_completed(); })
       .def("flush_unschedulable", [](Scheduler& s) { s.queue().flush_unschedulable_leftover(); })
       .def("move_all", [](Scheduler& s) { s.queue().move_all_to_active_or_backoff(ClusterEvent{"*", kAll, ""}); })

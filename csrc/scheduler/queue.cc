@@ -376,8 +376,23 @@ void SchedulingQueue::update(const PodPtr& old_p, const PodPtr& new_p) {
     if (auto pk = parked_.find(uid); pk != parked_.end()) {
       auto nq = std::make_shared<QueuedPodInfo>(*pk->second);
       nq->pod = new_p;
-      pk->second = nq;
       nominator_->update(old_p, new_p);
+      if (!pod_spec_changed(*old_p, *new_p)) {
+        pk->second = nq;
+        return;
+      }
+      // A parked pod whose spec changed (a user fixed its requests) gets
+      // another attempt now, as an unschedulable one does (upstream
+      // Update: scheduling_queue.go:436-470), instead of waiting for its
+      // gang's next probe or the unschedulable flush.
+      parked_.erase(pk);
+      if (backing_off(*nq)) {
+        backoff_.push(nq);
+      } else {
+        active_.push(nq);
+        notify = true;
+      }
+      if (notify) cv_.notify_one();
       return;
     }
     auto it = unschedulable_.find(uid);

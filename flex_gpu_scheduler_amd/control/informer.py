@@ -184,8 +184,15 @@ class Informer:
                     self._synced.set()
                     self._stop.wait(30.0)
                     continue
-                log.exception("informer %s list/watch failed; retrying", self.kind)
-                time.sleep(backoff)
+                if self._stop.is_set():
+                    break
+                if isinstance(e, OSError):
+                    # The API server is unreachable (restarting, or gone at
+                    # shutdown): one line per attempt, no traceback.
+                    log.warning("informer %s list/watch failed (%s); retrying in %.2fs", self.kind, e, backoff)
+                else:
+                    log.exception("informer %s list/watch failed; retrying", self.kind)
+                self._stop.wait(backoff)
                 backoff = min(backoff * 2, 5.0)
             finally:
                 if w is not None:

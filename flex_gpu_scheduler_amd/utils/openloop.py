@@ -150,8 +150,8 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
                             "wall_s": r["wall_s"], "denied_gangs": r["denials"]["total"],
                             "denied_gang_fraction": r["denied_gang_fraction"], "parked_gangs": r["parked_gangs"],
                             "denial_causes": r["denials"]["causes"],
-                            "gang_split_fraction": r["gang_split_fraction"],
-                            "gang_avoidable_split_fraction": r["gang_avoidable_split_fraction"]})
+                            "gang_split_fraction": r.get("gang_split_fraction"),
+                            "gang_avoidable_split_fraction": r.get("gang_avoidable_split_fraction")})
             ok = ok and ok_t
             if not ok:
                 break

@@ -115,6 +115,19 @@ def test_bench_eight_ranks_self_launched_gloo():
         assert g["model"]["model_busbw_GBps"] > 0 and g["model"]["direct_links_min"] == g["gang"] - 1
         assert g["verdict"] == "n/a" and pl["summary"][str(g["gang"])]["verdict"] == "n/a"
     assert pl["gangs"][0]["verdict"] == "n/a"
+    # The single-node multi-GPU scalars lead `config` (the driver keeps
+    # scalars): per gang size the verdict and placed busBW, the cross-socket
+    # ratio, and the one-line headline that carries them.
+    c = d["config"]
+    keys = list(c)
+    for k in ("2", "4", "8"):
+        assert c[f"placement_verdict_{k}"] == "n/a"  # gloo: no xGMI data plane to judge
+        assert isinstance(c[f"placed_busbw_GBps_{k}"], float) and c[f"placed_busbw_GBps_{k}"] > 0
+        assert keys.index(f"placement_verdict_{k}") < keys.index("per_rank")
+    assert "cross_socket_over_placed" in c and "placement[2/4/8]=n/a/n/a/n/a" in c["headline"]
+    first_dict = next(i for i, k in enumerate(keys) if isinstance(c[k], (dict, list)))
+    assert all(not isinstance(c[k], (dict, list)) for k in keys[:first_dict])
+    assert keys.index("headline") < 5
 
 
 def test_visible_gpu_count_honours_visibility_lists(tmp_path):
@@ -185,3 +198,30 @@ def test_busbw_model_from_the_captured_box_io_links():
         for lk in gg.xgmi_links:
             lk.bandwidth_mbps = 0
     assert abs(busbw_model(host, list(range(8)))["model_busbw_GBps"] - 0.75 * 7 * 76.8) < 0.2
+
+
+def test_headline_scalars_on_one_gpu_read_na():
+    """bench.headline_scalars: on one GPU the placement scalars read "n/a";
+    the headline string carries every number the scalars hold."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    by_type = {k: {"p99_ms": 2.5} for k in ("1", "2", "4", "8", "cpx4")}
+    split = {k: {"n": 10, "split": 0, "avoidable": 0, "split_fraction": 0.0} for k in ("2", "4", "8", "cpx4")}
+    extras = {"open_loop_capacity_pods_per_s": 100000.0, "nodes1024_pods_per_s": 60000.0,
+              "service_mode_pods_per_s": 70000.0, "service_mode_generator_limited": False,
+              "denied_gang_fraction": 0.0, "parked_gang_fraction": 0.001,
+              **{f"open_loop_p99_create_to_bound_ms_{k}": 0.9 for k in ("1", "2", "4", "8", "cpx4")},
+              "scenarios": {"trimaran_tlp": {"gpus_sampled": 1, "replicated_from_gpu0": True}}}
+    h = bench.headline_scalars(118000.0, by_type, split, extras, 1)
+    assert list(h)[0] == "headline"
+    for k in ("2", "4", "8"):
+        assert h[f"placement_verdict_{k}"] == "n/a" and h[f"placed_busbw_GBps_{k}"] == "n/a"
+    assert h["cross_socket_over_placed"] == "n/a" and h["tlp_replicated_from_gpu0"] is True
+    for k in ("1", "2", "4", "8", "cpx4"):
+        assert h[f"p99_gang_admit_ms_{k}"] == 2.5 and h[f"open_loop_p99_create_to_bound_ms_{k}"] == 0.9
+    for k in ("2", "4", "8", "cpx4"):
+        assert h[f"gang_split_fraction_{k}"] == 0.0
+    assert "burst=118.0k" in h["headline"] and "n1024=60.0k" in h["headline"] and "open_loop=100.0k" in h["headline"]

@@ -250,3 +250,27 @@ def test_xcd_gang_is_probed_apart_from_a_parked_whole_gpu_gang(store):
         assert bound(store, b) == []
     finally:
         s.stop()
+
+
+def test_parked_member_whose_spec_changes_is_retried(store):
+    """A parked gang member whose spec is updated gets another attempt at once
+    (upstream Update moves an updated unschedulable pod)
+    instead of waiting for its gang's next probe or the 60 s flush."""
+    store.create("nodes", mi355x_node("mi-0", mode="spx"))
+    s = scheduler(store)
+    try:
+        a = submit(store, "a", 8)
+        assert wait_for(lambda: len(bound(store, a)) == 8)
+        b = submit(store, "b", 4)
+        assert wait_for(lambda: s.queue_counts()["parked"] == 4)
+        before = s.stats()["attempts"]
+        time.sleep(0.2)
+        assert s.stats()["attempts"] == before  # parked: no cycles
+        pod = store.get("pods", "default", b[0])
+        pod["spec"]["containers"][0]["resources"]["requests"] = {"cpu": "2"}
+        store.update("pods", pod)
+        assert wait_for(lambda: s.stats()["attempts"] > before, timeout=3.0)
+        assert wait_for(lambda: s.queue_counts()["parked"] == 4, timeout=3.0)  # parked again: GPUs still held
+        assert bound(store, b) == []
+    finally:
+        s.stop()
