@@ -7,7 +7,8 @@ measure it and to assert the placement property the configuration is about:
 
   coscheduling_cpu     PodGroups minMember=2 of CPU-only pods (plumbing)
   flexgpu_cpx_quarter  4 pods x 0.25 GPU (amd.com/gpu-xcd: 2) on one CPX MI355X
-  gang8_xgmi           8-rank gangs on 8x MI355X nodes, NRT XGMIGangAffinity
+  gang8_xgmi           gangs of 2-8 ranks on 8x MI355X nodes with a real choice of
+                       node, NRT XGMIGangAffinity + gangColocation
   capacity_preemption  2 namespaces contend for 8 MI355X (ElasticQuota + preemption)
   trimaran_tlp         TargetLoadPacking(GPU) fed by live amdgpu utilisation
 """
@@ -129,53 +130,68 @@ def flexgpu_cpx_quarter(iterations: int = 40) -> dict:
                                             "latency": "4-pod batch create -> all bound"}
 
 
-def gang8_xgmi(iterations: int = 30, nodes: int = 4) -> dict:
-    """8-rank gangs with XGMIGangAffinity: every gang must land on one node's
-    xGMI mesh. Background load leaves exactly one node able to host a gang."""
+def gang8_xgmi(iterations: int = 30, nodes: int = 5) -> dict:
+    """Gangs of 2-8 ranks with XGMIGangAffinity + gangColocation: every gang
+    must land on one node's xGMI mesh although the scheduler has a real
+    choice. Background load leaves 3 / 2 / 8 / 4 / 6 GPUs free on the five
+    nodes: for every gang size some node can host the whole gang and others
+    cannot, and the tightest nodes (which node bin-packing prefers) are
+    often the ones that can only take part of it. Gang sizes cycle 4, 8, 2,
+    6, 3; the 8-rank gang has exactly one choice."""
     store = Store()
     store.create_many("nodes", json.dumps([mi355x_node(f"mi355x-{i}") for i in range(nodes)]))
     store.create_many("noderesourcetopologies", json.dumps([mi355x_nrt(f"mi355x-{i}") for i in range(nodes)]))
     s = new_scheduler(store, load_config(flagship_config()), start=True)
     lat: list[float] = []
-    t_total, pods, colocated = 0.0, 0, 0
+    t_total, pods, colocated, hostable = 0.0, 0, 0, 0
+    by_size: dict[str, str] = {}
+    sizes = (4, 8, 2, 6, 3)
+    busy = (5, 6, 0, 4, 2)
     try:
-        # Background: node i (i < nodes-1) has 1..7 GPUs busy, so a gang of 8
-        # only fits on the last node; partial-fit scores must not split it.
         bg = []
-        for i in range(nodes - 1):
-            for k in range(1 + (i * 3) % 7):
+        for i in range(nodes):
+            for k in range(busy[i % len(busy)]):
                 p = make_pod(f"bg-{i}-{k}", "bg", limits={GPU: "1"}, requests={GPU: "1"})
                 p["spec"]["nodeSelector"] = {"kubernetes.io/hostname": f"mi355x-{i}"}
                 bg.append(p)
         store.create_many("pods", json.dumps(bg))
         if not _wait(lambda: len(_bound(store, "bg")) == len(bg)):
             return {"error": "background pods did not bind"}
+        ok_by: dict[int, list[int]] = {}
         for it in range(iterations + 2):
+            k = sizes[it % len(sizes)]
             ns = f"g8-{it}"
-            store.create("podgroups", make_pod_group("ranks", ns, 8))
+            store.create("podgroups", make_pod_group("ranks", ns, k))
             pl = [make_pod(f"rank-{r}", ns, pod_group="ranks", limits={GPU: "1"}, requests={GPU: "1"})
-                  for r in range(8)]
+                  for r in range(k)]
             t0 = time.perf_counter()
             store.create_many("pods", json.dumps(pl))
-            ok = _wait(lambda: len(_bound(store, ns)) == 8)
+            ok = _wait(lambda: len(_bound(store, ns)) == k)
             dt = time.perf_counter() - t0
             if not ok:
-                return {"error": "gang did not bind"}
+                return {"error": f"gang of {k} did not bind"}
             bound = _bound(store, ns)
-            if len({p["spec"]["nodeName"] for p in bound}) == 1 and \
-                    len({p["metadata"]["annotations"][INDEX_ANNOTATION] for p in bound}) == 8:
-                colocated += 1
+            one = len({p["spec"]["nodeName"] for p in bound}) == 1 and \
+                len({p["metadata"]["annotations"][INDEX_ANNOTATION] for p in bound}) == k
+            colocated += one
+            ok_by.setdefault(k, [0, 0])
+            ok_by[k][0] += one
+            ok_by[k][1] += 1
             recs = s.gang_records(True)
+            hostable += sum(1 for g in recs if g.get("hostable") == 1)
             if it >= 2:
                 t_total += dt
-                pods += 8
+                pods += k
                 lat += [(g["bound_us"] - g["first_enqueue_us"]) / 1000.0 for g in recs] or [dt * 1000.0]
             store.delete_all("pods", ns)
             store.delete_all("podgroups", ns)
             _wait(lambda: s.cache_counts()["pods"] == len(bg))
+        by_size = {str(k): f"{v[0]}/{v[1]}" for k, v in sorted(ok_by.items())}
     finally:
         s.stop()
     return _summary(lat, pods, t_total) | {"gangs_on_one_xgmi_node": f"{colocated}/{iterations + 2}",
+                                            "by_size": by_size, "hostable_at_first_rank": hostable,
+                                            "free_gpus_per_node": [8 - busy[i % len(busy)] for i in range(nodes)],
                                             "nodes": nodes}
 
 
