@@ -45,19 +45,21 @@ size_t GangPlacement::open_gangs() const {
 void GangPlacement::reservations_locked(const Snapshot& s, uint64_t self, GpuDemand::Kind kind,
                                         std::vector<std::pair<int, int64_t>>& out) {
   out.clear();
-  const int64_t now = clock_->now_us();
   for (auto it = open_.begin(); it != open_.end();) {
     const Open& o = it->second;
     if (it->first == self) {
       ++it;
       continue;
     }
+    // Only a gang with ranks placed and ranks to go is owed anything; one
+    // with none placed (not started, parked, rejected or deleted) is dropped
+    // at once and registers again when one of its ranks is planned.
     const int a = cache_->assigned_in_group(it->first);
-    if (a >= o.min_member || (a == 0 && now - o.last_us > kIdleUs)) {
+    if (a >= o.min_member || a == 0) {
       it = open_.erase(it);
       continue;
     }
-    if (a > 0 && o.kind == kind) {
+    if (o.kind == kind) {
       const auto hosts = cache_->nodes_of_group(it->first);
       if (hosts.size() == 1) {  // anchored: the rest of the gang is owed to that node
         auto ix = s.index.find(hosts[0]);
@@ -148,7 +150,6 @@ GangPlacement::Plan GangPlacement::plan(const Snapshot& s, const Pod& p, int min
     o.kind = d.kind;
     o.amount = d.amount;
     o.min_member = min_member;
-    o.last_us = clock_->now_us();
     reservations_locked(s, p.pg_key, d.kind, res);
   }
   auto reserved_at = [&](int pos) {

@@ -78,7 +78,6 @@ class GangPlacement {
     GpuDemand::Kind kind = GpuDemand::None;
     int64_t amount = 0;
     int min_member = 0;
-    int64_t last_us = 0;
   };
   // Ranks owed to other gangs anchored on one node, as (position, units of
   // `kind`); prunes gangs that completed or went idle. Caller holds mu_.
@@ -89,8 +88,7 @@ class GangPlacement {
   int scan(const Snapshot& s, const GpuDemand& d, int64_t members, const std::vector<std::pair<int, int64_t>>& res,
            std::vector<char>* out_mask, std::vector<int>* out_list) const;
 
-  static constexpr size_t kList = 16;          // restrictions up to this size are position lists
-  static constexpr int64_t kIdleUs = 2'000'000;  // an unstarted gang not seen for this long is dropped
+  static constexpr size_t kList = 16;  // restrictions up to this size are position lists
 
   SchedulerCache* cache_;
   std::shared_ptr<Clock> clock_;

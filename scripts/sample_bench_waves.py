@@ -27,10 +27,16 @@ def main() -> int:
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--waves", type=int, default=40)
     ap.add_argument("--hz", type=int, default=4000)
+    ap.add_argument("--colocation", default="Preferred", help="NRT gangColocation of the flagship profile")
+    ap.add_argument("--tag", default="bench_waves")
+    ap.add_argument("--seed", type=int, default=7)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     apply("l3")
-    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=7)
+    from flex_gpu_scheduler_amd.utils.workload import flagship_config
+
+    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed,
+                  config=flagship_config(gang_colocation=a.colocation))
     try:
         ws = [shard.wave(i) for i in range(a.waves + 4)]
         prepared = [w.chunks_json() for w in ws]
@@ -41,11 +47,11 @@ def main() -> int:
         for i in range(4, a.waves + 4):
             r = shard.run(ws[i], prepared=prepared[i], collect_gangs=False)
             split.append({k: round(v, 3) for k, v in r.split_ms.items()})
-        native().sampler_dump(os.path.join(a.out, "bench_waves.samples"))
+        native().sampler_dump(os.path.join(a.out, f"{a.tag}.samples"))
     finally:
         shard.close()
     tot = {k: round(sum(s[k] for s in split) / len(split), 3) for k in split[0]}
-    with open(os.path.join(a.out, "bench_waves_split.json"), "w") as f:
+    with open(os.path.join(a.out, f"{a.tag}_split.json"), "w") as f:
         json.dump({"nodes": a.nodes, "waves": a.waves, "mean_ms": tot, "per_wave": split}, f)
     print(json.dumps({"nodes": a.nodes, "waves": a.waves, "mean_ms": tot}))
     return 0
