@@ -46,6 +46,21 @@ void SchedulerCache::group_delta(const Pod& p, int d) {
   if (hosts.empty()) group_nodes_.erase(p.pg_key);
 }
 
+int SchedulerCache::group_placement(uint64_t pg_key, std::vector<std::string>& hosts) const {
+  std::lock_guard<AdaptiveMutex> g(group_mu_);
+  size_t k = 0;
+  auto it = group_nodes_.find(pg_key);
+  if (it != group_nodes_.end())
+    for (const auto& [node, n] : it->second) {
+      if (k < hosts.size()) hosts[k].assign(node);  // reuses the string's buffer
+      else hosts.push_back(node);
+      ++k;
+    }
+  hosts.resize(k);
+  auto a = group_assigned_.find(pg_key);
+  return a == group_assigned_.end() ? 0 : a->second;
+}
+
 std::vector<std::string> SchedulerCache::nodes_of_group(uint64_t pg_key) const {
   std::lock_guard<AdaptiveMutex> g(group_mu_);
   std::vector<std::string> out;

@@ -85,6 +85,10 @@ class SchedulerCache {
   int assigned_in_group(uint64_t pg_key) const;
   // Nodes hosting assumed or bound pods of the group (by Pod::pg_key).
   std::vector<std::string> nodes_of_group(uint64_t pg_key) const;
+  // Both of the above under one lock, into `hosts` (resized; its strings'
+  // buffers are reused, so a caller's thread_local vector allocates nothing
+  // in steady state). Returns the assigned count.
+  int group_placement(uint64_t pg_key, std::vector<std::string>& hosts) const;
   int assigned_in_group(const std::string& pg_full_name) const { return assigned_in_group(pg_key_of(pg_full_name)); }
   // Cache debugger (upstream internal/cache/debugger): compares the cache
   // with the listers' view — `assigned` pods (nodeName set) and Node names —

@@ -45,6 +45,7 @@ size_t GangPlacement::open_gangs() const {
 void GangPlacement::reservations_locked(const Snapshot& s, uint64_t self, GpuDemand::Kind kind,
                                         std::vector<std::pair<int, int64_t>>& out) {
   out.clear();
+  thread_local std::vector<std::string> hosts;
   for (auto it = open_.begin(); it != open_.end();) {
     const Open& o = it->second;
     if (it->first == self) {
@@ -54,24 +55,44 @@ void GangPlacement::reservations_locked(const Snapshot& s, uint64_t self, GpuDem
     // Only a gang with ranks placed and ranks to go is owed anything; one
     // with none placed (not started, parked, rejected or deleted) is dropped
     // at once and registers again when one of its ranks is planned.
-    const int a = cache_->assigned_in_group(it->first);
+    const int a = cache_->group_placement(it->first, hosts);
     if (a >= o.min_member || a == 0) {
       it = open_.erase(it);
       continue;
     }
-    if (o.kind == kind) {
-      const auto hosts = cache_->nodes_of_group(it->first);
-      if (hosts.size() == 1) {  // anchored: the rest of the gang is owed to that node
-        auto ix = s.index.find(hosts[0]);
-        if (ix != s.index.end()) {
-          const int pos = static_cast<int>(ix->second);
-          const int64_t per = kind == GpuDemand::Gpu ? o.amount : xcd_footprint(o.amount, s.part_mask[pos]);
-          if (per > 0) out.emplace_back(pos, (o.min_member - a) * per);
-        }
+    if (o.kind == kind && hosts.size() == 1) {  // anchored: the rest of the gang is owed to that node
+      auto ix = s.index.find(hosts[0]);
+      if (ix != s.index.end()) {
+        const int pos = static_cast<int>(ix->second);
+        const int64_t per = kind == GpuDemand::Gpu ? o.amount : xcd_footprint(o.amount, s.part_mask[pos]);
+        if (per > 0) out.emplace_back(pos, (o.min_member - a) * per);
       }
     }
     ++it;
   }
+}
+
+std::shared_ptr<NodeRestriction> GangPlacement::take_restriction(size_t nodes) {
+  // A small ring of restriction objects reused once no cycle holds them (a
+  // binding cycle keeps its CycleState, and so the restriction, alive until
+  // the bind): no allocation per gang rank in steady state.
+  for (size_t k = 0; k < pool_.size(); ++k) {
+    auto& r = pool_[(pool_next_ + k) % pool_.size()];
+    if (r && r.use_count() == 1) {
+      pool_next_ = (pool_next_ + k + 1) % pool_.size();
+      r->list.clear();
+      r->mask.clear();
+      r->nodes = nodes;
+      r->fallback = true;
+      return r;
+    }
+  }
+  auto r = std::make_shared<NodeRestriction>();
+  r->list.reserve(kList);
+  r->nodes = nodes;
+  if (pool_.size() < kPool) pool_.push_back(r);
+  else pool_[pool_next_++ % kPool] = r;
+  return r;
 }
 
 int GangPlacement::scan(const Snapshot& s, const GpuDemand& d, int64_t members,
@@ -137,21 +158,20 @@ GangPlacement::Plan GangPlacement::plan(const Snapshot& s, const Pod& p, int min
   if (mode_ == Mode::Off || !gang_demand(d) || min_member <= 1 || p.pg_key == 0) return out;
   const size_t n = s.nodes.size();
   if (n == 0 || s.free_whole.size() != n || s.free_xcd.size() != n || s.part_mask.size() != n) return out;
-  const int assigned = cache_->assigned_in_group(p.pg_key);
+  thread_local std::vector<std::string> hosts;
+  const int assigned = cache_->group_placement(p.pg_key, hosts);
   out.gang = true;
   out.started = assigned > 0;
   out.remaining = std::max<int64_t>(1, min_member - assigned);
   // Required binds only gangs one node could hold; a larger one spans nodes.
   const bool required = mode_ == Mode::Required && out.remaining <= node_capacity(s, p);
   thread_local std::vector<std::pair<int, int64_t>> res;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    Open& o = open_[p.pg_key];
-    o.kind = d.kind;
-    o.amount = d.amount;
-    o.min_member = min_member;
-    reservations_locked(s, p.pg_key, d.kind, res);
-  }
+  std::lock_guard<std::mutex> g(mu_);
+  Open& o = open_[p.pg_key];
+  o.kind = d.kind;
+  o.amount = d.amount;
+  o.min_member = min_member;
+  reservations_locked(s, p.pg_key, d.kind, res);
   auto reserved_at = [&](int pos) {
     int64_t u = 0;
     for (const auto& [q, units] : res)
@@ -164,25 +184,26 @@ GangPlacement::Plan GangPlacement::plan(const Snapshot& s, const Pod& p, int min
     const int64_t free = d.kind == GpuDemand::Gpu ? s.free_whole[i] : s.free_xcd[i];
     return per > 0 && free - reserved_at(pos) >= members * per;
   };
-  auto make = [&]() {
-    auto r = std::make_shared<NodeRestriction>();
-    r->nodes = n;
-    r->fallback = !required;
-    return r;
-  };
   if (out.started) {
-    std::vector<int> all_fit, one_fit;
-    for (const auto& h : cache_->nodes_of_group(p.pg_key)) {
+    // Hosts that take every remaining rank, else hosts with room for one
+    // more (the gang is split already: fill its nodes first).
+    int all_fit[kList], one_fit[kList];
+    size_t na = 0, no = 0;
+    for (const auto& h : hosts) {
       auto ix = s.index.find(h);
       if (ix == s.index.end()) continue;
       const int pos = static_cast<int>(ix->second);
-      if (room_at(pos, out.remaining)) all_fit.push_back(pos);
-      else if (room_at(pos, 1)) one_fit.push_back(pos);
+      if (room_at(pos, out.remaining)) {
+        if (na < kList) all_fit[na++] = pos;
+      } else if (room_at(pos, 1)) {
+        if (no < kList) one_fit[no++] = pos;
+      }
     }
-    out.hostable = !all_fit.empty();
-    if (!all_fit.empty() || !one_fit.empty()) {
-      auto r = make();
-      r->list = all_fit.empty() ? std::move(one_fit) : std::move(all_fit);
+    out.hostable = na > 0;
+    if (na > 0 || no > 0) {
+      auto r = take_restriction(n);
+      const int* src = na > 0 ? all_fit : one_fit;
+      r->list.assign(src, src + (na > 0 ? na : no));
       std::sort(r->list.begin(), r->list.end());
       // Part of the gang is placed: never strand it (the cycle may still
       // fall back to a node that takes one more rank).
@@ -192,7 +213,8 @@ GangPlacement::Plan GangPlacement::plan(const Snapshot& s, const Pod& p, int min
     }
   }
   // Nodes that take every remaining rank.
-  auto r = make();
+  auto r = take_restriction(n);
+  r->fallback = !required;
   const int count = scan(s, d, out.remaining, res, &r->mask, &r->list);
   if (!out.started) out.hostable = count > 0;
   if (count == 0) {

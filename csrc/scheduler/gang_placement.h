@@ -88,7 +88,14 @@ class GangPlacement {
   int scan(const Snapshot& s, const GpuDemand& d, int64_t members, const std::vector<std::pair<int, int64_t>>& res,
            std::vector<char>* out_mask, std::vector<int>* out_list) const;
 
+  // A restriction object from pool_ that no cycle holds any more (caller
+  // holds mu_).
+  std::shared_ptr<NodeRestriction> take_restriction(size_t nodes);
+
   static constexpr size_t kList = 16;  // restrictions up to this size are position lists
+  static constexpr size_t kPool = 64;
+  std::vector<std::shared_ptr<NodeRestriction>> pool_;
+  size_t pool_next_ = 0;
 
   SchedulerCache* cache_;
   std::shared_ptr<Clock> clock_;
