@@ -329,7 +329,8 @@ def main() -> int:
             rep = capacity_report(shard, burst, seed=args.seed)
         else:
             rep = capacity_in_child(args.nodes, args.seed + 7919 * ctx.rank, json.loads(args.sched_options), burst,
-                                    cpus=repin() or cpus, hbm_gib=hbm_gib, colocation=args.gang_colocation)
+                                    cpus=repin() or cpus, hbm_gib=hbm_gib, colocation=args.gang_colocation,
+                                    deny_check=True)
         cap = rep["capacity"]
         extras["gang_admit_open_loop"] = {
             "burst_capacity_pods_per_s": round(burst, 1),
@@ -341,7 +342,7 @@ def main() -> int:
                                   "for deniedPGExpirationTimeSeconds)",
             "process": "this rank's" if args.open_loop_in_process else "child without the GPU runtime, fresh shard",
             "capacity_search": rep["search"],
-            **{k: rep[k] for k in ("load_50", "load_90") if k in rep}}
+            **{k: rep[k] for k in ("load_50", "load_90", "deny_mode_load_90") if k in rep}}
         search = rep["search"]
         ol = extras["gang_admit_open_loop"]
         extras["open_loop_capacity_pods_per_s"] = round(cap, 1)
@@ -357,6 +358,12 @@ def main() -> int:
         n_d = sum(r.get("denied_gangs", (r.get("denials") or {}).get("total", 0)) for r in runs)
         extras["denied_gang_fraction"] = round(n_d / max(1, n_g), 6)
         extras["parked_gang_fraction"] = round(sum(r.get("parked_gangs", 0) for r in runs) / max(1, n_g), 6)
+        dn = ol.get("deny_mode_load_90")
+        if dn:
+            # The reference's semantics at the same load (Coscheduling
+            # transientShortage: Deny), for a like-for-like comparison.
+            extras["deny_mode_open_loop_p99_create_to_bound_ms"] = dn["all_gangs"]["p99_create_to_bound_ms"]
+            extras["deny_mode_denied_gang_fraction"] = dn["denied_gang_fraction"]
         loads = [ol.get(f"load_{x}") for x in (50, 90) if ol.get(f"load_{x}")]
         if loads:
             extras["open_loop_gang_split_fraction"] = max(r.get("gang_split_fraction", 0.0) for r in loads)

@@ -242,7 +242,7 @@ def capacity_report(shard, burst: float, seed: int = 0) -> dict:
 
 def capacity_in_child(nodes: int, seed: int, options: dict, burst: float, cpus: list[int] | None = None,
                       warm_waves: int = 16, hbm_gib: int = 288, timeout_s: float = 600.0,
-                      colocation: str = "Preferred") -> dict:
+                      colocation: str = "Preferred", deny_check: bool = False) -> dict:
     """capacity_report in a child Python process that never loads the GPU
     runtime, on a fresh shard of the same cluster (spec, seed, options),
     warmed with `warm_waves` burst waves and pinned to `cpus`.
@@ -260,6 +260,8 @@ def capacity_in_child(nodes: int, seed: int, options: dict, burst: float, cpus: 
     cmd = [sys.executable, "-m", "flex_gpu_scheduler_amd.utils.openloop", "--nodes", str(nodes),
            "--seed", str(seed), "--options", json.dumps(options), "--burst", repr(float(burst)),
            "--warm-waves", str(warm_waves), "--hbm-gib", str(hbm_gib), "--colocation", colocation]
+    if deny_check:
+        cmd.append("--deny-check")
     if cpus:
         cmd += ["--cpus", ",".join(map(str, cpus))]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, check=False)
@@ -281,6 +283,7 @@ def _child_main(argv: list[str] | None = None) -> int:
     ap.add_argument("--hbm-gib", type=int, default=288)
     ap.add_argument("--cpus", default="")
     ap.add_argument("--colocation", default="Preferred")
+    ap.add_argument("--deny-check", action="store_true", help="also run the 90%% load in Deny mode")
     a = ap.parse_args(argv)
     if a.cpus:
         os.sched_setaffinity(0, [int(c) for c in a.cpus.split(",")])  # before the shard's threads start
@@ -296,6 +299,20 @@ def _child_main(argv: list[str] | None = None) -> int:
         rep = capacity_report(shard, a.burst, seed=a.seed)
     finally:
         shard.close()
+    if a.deny_check and rep["capacity"] > 0:
+        # The same 90% load with the reference's semantics
+        # (transientShortage: Deny) on a fresh shard: the like-for-like
+        # comparison for the Park-mode numbers.
+        deny = Shard(ClusterSpec(nodes=a.nodes, hbm_gib=a.hbm_gib), namespace="bench-ol-deny", seed=a.seed,
+                     options=json.loads(a.options),
+                     config=flagship_config(gang_colocation=a.colocation, transient_shortage="Deny"))
+        try:
+            for i in range(a.warm_waves):
+                w = deny.wave(i)
+                deny.run(w, prepared=w.chunks_json(), collect_gangs=False)
+            rep["deny_mode_load_90"] = run_open_loop(deny, 0.9 * rep["capacity"], duration_s=1.0, seed=a.seed + 1)
+        finally:
+            deny.close()
     print(json.dumps(rep))
     return 0
 
