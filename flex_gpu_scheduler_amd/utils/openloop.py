@@ -111,7 +111,7 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
 
 def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, seed: int = 0,
                        start_pods_per_s: float = 2000.0, occupancy: float = 0.5,
-                       p99_budget_ms: float = 25.0, log: list | None = None) -> float:
+                       p99_budget_ms: float = 25.0, log: list | None = None, reset=None) -> float:
     """Sustained open-loop capacity (pods/s), an SLO capacity: the highest
     arrival rate, in steps x1.3 apart from `start_pods_per_s` up to
     `max_pods_per_s` (the burst capacity; when the next step would pass it,
@@ -123,7 +123,8 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
 
     One trial per rate (two, with different arrival seeds, that must both
     pass, for rates in the top two x1.3 steps under the burst rate), no
-    retries. Every
+    retries. With `reset` (a callable returning a fresh, warmed shard), the
+    trial after a failed one runs on a fresh shard. Every
     trial is appended to `log` with its parked gangs, its Coscheduling
     denials and their causes (Scheduler::note_gang_denied), p99.9 and max.
     Near capacity the hold time (a few ms) is comparable to the admission
@@ -133,12 +134,13 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     reference's PostFilter does (which made a rate fail on < 1% of its
     gangs waiting 3 s)."""
     top = max_pods_per_s / 1.3 ** 2  # rates in the top two grid steps get a second trial
+    cur = [shard]
 
     def served(rate: float) -> bool:
         trials = 2 if rate >= top else 1
         ok = True
         for t in range(trials):
-            r = run_open_loop(shard, rate, duration_s, seed=seed + 7 * t, occupancy=occupancy)
+            r = run_open_loop(cur[0], rate, duration_s, seed=seed + 7 * t, occupancy=occupancy)
             p99 = r["all_gangs"]["p99_create_to_bound_ms"]
             ok_t = p99 is not None and p99 != "inf" and p99 <= p99_budget_ms
             if log is not None:
@@ -155,6 +157,13 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
             ok = ok and ok_t
             if not ok:
                 break
+        if not ok and reset is not None:
+            # An overloaded trial leaves the shard slower for the next ones
+            # (docs/ARCHITECTURE.md, "the open-loop aftermath"): the next
+            # trial starts on a fresh shard of the same cluster.
+            cur[0] = reset()
+            if log is not None and log:
+                log[-1]["next_trial_on_fresh_shard"] = True
         return ok
 
     rate = min(start_pods_per_s, max(max_pods_per_s, 1.0))
@@ -228,12 +237,15 @@ def run_open_loop(shard, rate_pods_per_s: float, duration_s: float = 1.0, seed: 
     return out
 
 
-def capacity_report(shard, burst: float, seed: int = 0) -> dict:
+def capacity_report(shard, burst: float, seed: int = 0, reset=None) -> dict:
     """The bench's open-loop block on `shard`: the capacity search, then the
-    50% and 90% loads of the capacity found."""
+    50% and 90% loads of the capacity found (on a fresh shard when `reset`
+    is given, so they do not follow the search's overloaded trials)."""
     search: list[dict] = []
-    cap = open_loop_capacity(shard, burst, seed=seed, log=search) if burst > 0 else 0.0
+    cap = open_loop_capacity(shard, burst, seed=seed, log=search, reset=reset) if burst > 0 else 0.0
     out = {"capacity": cap, "search": search}
+    if cap > 0 and reset is not None:
+        shard = reset()
     for f in (0.5, 0.9):
         if cap > 0:
             out[f"load_{int(f * 100)}"] = run_open_loop(shard, f * cap, duration_s=1.0, seed=seed + 1)
@@ -284,21 +296,33 @@ def _child_main(argv: list[str] | None = None) -> int:
     ap.add_argument("--cpus", default="")
     ap.add_argument("--colocation", default="Preferred")
     ap.add_argument("--deny-check", action="store_true", help="also run the 90%% load in Deny mode")
+    ap.add_argument("--no-reset", action="store_true", help="keep one shard through the whole search")
     a = ap.parse_args(argv)
     if a.cpus:
         os.sched_setaffinity(0, [int(c) for c in a.cpus.split(",")])  # before the shard's threads start
     from .benchrun import Shard
     from .workload import flagship_config
 
-    shard = Shard(ClusterSpec(nodes=a.nodes, hbm_gib=a.hbm_gib), namespace="bench-ol", seed=a.seed,
-                  options=json.loads(a.options), config=flagship_config(gang_colocation=a.colocation))
-    try:
+    shards: list = []
+
+    def fresh():
+        """A new shard of the same cluster, warmed with burst waves (the
+        previous one is closed)."""
+        while shards:
+            shards.pop().close()
+        sh = Shard(ClusterSpec(nodes=a.nodes, hbm_gib=a.hbm_gib), namespace="bench-ol", seed=a.seed,
+                   options=json.loads(a.options), config=flagship_config(gang_colocation=a.colocation))
+        shards.append(sh)
         for i in range(a.warm_waves):
-            w = shard.wave(i)
-            shard.run(w, prepared=w.chunks_json(), collect_gangs=False)
-        rep = capacity_report(shard, a.burst, seed=a.seed)
+            w = sh.wave(i)
+            sh.run(w, prepared=w.chunks_json(), collect_gangs=False)
+        return sh
+
+    try:
+        rep = capacity_report(fresh(), a.burst, seed=a.seed, reset=None if a.no_reset else fresh)
     finally:
-        shard.close()
+        while shards:
+            shards.pop().close()
     if a.deny_check and rep["capacity"] > 0:
         # The same 90% load with the reference's semantics
         # (transientShortage: Deny) on a fresh shard: the like-for-like
