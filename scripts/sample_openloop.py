@@ -47,6 +47,7 @@ def main() -> int:
     ap.add_argument("--fresh-after", type=int, default=-2,
                     help="with --sequence: replace the shard by a fresh one (same process) after trial N (0-based)")
     ap.add_argument("--torch-after-pin", action="store_true", help="initialise them after the CPU pinning")
+    ap.add_argument("--colocation", default="Preferred", help="NRT gangColocation of the flagship profile")
     a = ap.parse_args()
 
     def init_torch():
@@ -61,7 +62,10 @@ def main() -> int:
     apply("l3")
     if a.torch_after_pin:
         init_torch()
-    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed, options=json.loads(a.options))
+    from flex_gpu_scheduler_amd.utils.workload import flagship_config
+
+    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed, options=json.loads(a.options),
+                  config=flagship_config(gang_colocation=a.colocation))
     try:
         # Warm the shard as the bench does before its search: burst waves,
         # then one open-loop trial well below the cliff.
@@ -96,7 +100,8 @@ def main() -> int:
                     # Shard state vs process state: a new store and scheduler
                     # in the same process (same heap), warmed as the first.
                     shard.close()
-                    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample2", seed=a.seed)
+                    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample2", seed=a.seed,
+                                  config=flagship_config(gang_colocation=a.colocation))
                     for j in range(4):
                         w = shard.wave(j)
                         shard.run(w, prepared=w.chunks_json(), collect_gangs=False)
