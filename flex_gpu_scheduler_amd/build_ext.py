@@ -106,6 +106,27 @@ def build_core(verbose: bool = True) -> Path:
     return out
 
 
+def build_core_debuginfo(verbose: bool = True) -> Path:
+    """The extension with -g (same optimisation: identical code, line
+    tables for tools/sample_report --lines) in dbg/, for sampling runs that
+    copy it over the package's extension on a scratch tree."""
+    import pybind11
+
+    py_inc = sysconfig.get_paths()["include"]
+    includes = [str(CSRC), pybind11.get_include(), py_inc, str(ROCM / "include")]
+    srcs = core_sources() + sorted((CSRC / "telemetry").glob("*.cc")) + [CSRC / "python" / "bindings.cc"]
+    objs = build_objects(srcs, BUILD / "core_g", ["-g1", "-gz"], includes)
+    out = ROOT / "dbg" / f"_xsched{_ext_suffix()}"
+    out.parent.mkdir(exist_ok=True)
+    cmd = ["g++", "-shared", "-pthread", *[str(o) for o in objs], *LINK_LIBS, "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
+    if verbose:
+        print(f"[build_ext] linked {out.relative_to(ROOT)}")
+    return out
+
+
 def build_hip(verbose: bool = True) -> Path | None:
     hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
     if not Path(hipcc).exists():
@@ -225,7 +246,11 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--stress", action="store_true")
     ap.add_argument("--stress-g", action="store_true", help="stress driver with -g (sample_report --lines)")
     ap.add_argument("--tests", action="store_true")
+    ap.add_argument("--core-g", action="store_true", help="the extension with -g into dbg/ (sampling runs)")
     a = ap.parse_args(argv)
+    if a.core_g:
+        build_core_debuginfo()
+        return 0
     if a.tests:
         build_tests()
         return 0

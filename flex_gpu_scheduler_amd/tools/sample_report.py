@@ -179,26 +179,41 @@ def summarize(dump: str, exe: str, top: int = 25, window: tuple[float, float] | 
 def lines(dump: str, exe: str, func: str, top: int = 25) -> list[tuple[float, str]]:
     """Source lines (addr2line on a -g build) of the busy samples whose leaf
     frame is in our code and whose function name contains `func`, as
-    fractions of those samples."""
+    fractions of those samples. Works for the stress executable and for the
+    Python extension (a shared object: offsets from its mapping)."""
     samples, resolve = load(dump, exe)
     base = 0
+    maps: list[tuple[int, int, int, str]] = []
     with open(dump) as f:
         for line in f:
             if line.startswith("exe_base "):
                 base = int(line.split()[1], 16)
-                break
+            elif line.startswith("map "):
+                m = line.split()
+                lo, hi = (int(x, 16) for x in m[1].split("-"))
+                maps.append((lo, hi, int(m[3], 16), m[6] if len(m) > 6 else "?"))
+    exe_name = exe.split("/")[-1]
+
+    def file_offset(pc: int) -> int | None:
+        for lo, hi, off, path in maps:
+            if lo <= pc < hi and path.endswith(exe_name):
+                return pc - lo + off if ".so" in path else pc - base
+        return None
+
     offs: collections.Counter = collections.Counter()
     for _tname, pcs, _t in samples:
         if len(pcs) < 3:
             continue
-        frames = [resolve(pc if i == 2 else pc - 1) for i, pc in enumerate(pcs) if i >= 2]
-        if is_idle(frames):
+        frames = frames_of(pcs, resolve)
+        if not frames or is_idle(frames):
             continue
         if func in frames[0] and "[lib" not in frames[0]:
-            offs[pcs[2] - base] += 1
-    if not offs:
-        return []
+            o = file_offset(pcs[2])
+            if o is not None:
+                offs[o] += 1
     addrs = list(offs)
+    if not addrs:
+        return []
     out = subprocess.run(["addr2line", "-C", "-e", exe, *[hex(a) for a in addrs]], capture_output=True,
                          text=True, check=False).stdout.splitlines()
     by_line: collections.Counter = collections.Counter()
