@@ -56,6 +56,11 @@ int Parallelizer::run_job(Job& job) {
     int start = job.next.fetch_add(job.chunk, std::memory_order_relaxed);
     if (start >= job.n) return done;
     int end = std::min(job.n, start + job.chunk);
+    if (job.rfn) {
+      (*job.rfn)(start, end);
+      done += end - start;
+      continue;
+    }
     for (int i = start; i < end; ++i) {
       if (job.stop && job.stop->load(std::memory_order_relaxed)) return done;
       (*job.fn)(i);
@@ -134,12 +139,27 @@ void Parallelizer::until(int n, const std::function<void(int)>& fn, const std::a
 
 void Parallelizer::until_forked(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop,
                                 ParallelSite* site) {
-  int helpers = std::max(1, std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1));
-  std::lock_guard<std::mutex> call(call_mu_);
   Job job;
   job.fn = &fn;
   job.stop = stop;
   job.n = n;
+  fork_join(job, site);
+}
+
+void Parallelizer::until_forked_ranges(int n, const std::function<void(int, int)>& fn, const std::atomic<bool>* stop,
+                                       ParallelSite* site) {
+  Job job;
+  job.rfn = &fn;
+  job.stop = stop;
+  job.n = n;
+  fork_join(job, site);
+}
+
+void Parallelizer::fork_join(Job& job, ParallelSite* site) {
+  const int n = job.n;
+  if (n <= 0) return;
+  int helpers = std::max(1, std::min<int>(static_cast<int>(threads_.size()), n / std::max(1, inline_below_ / 2) - 1));
+  std::lock_guard<std::mutex> call(call_mu_);
   job.seats = helpers;
   // chunkSizeFor: sqrt(n), capped so every participant gets work.
   job.chunk = std::max(1, std::min(static_cast<int>(std::sqrt(static_cast<double>(n))), n / (helpers + 1)));

@@ -55,6 +55,12 @@ class Parallelizer {
   // The fork/join half of `until`, for a caller that already got
   // plan_inline() == false (records the site's done fraction, no re-planning).
   void until_forked(int n, const std::function<void(int)>& fn, const std::atomic<bool>* stop, ParallelSite* site);
+  // until_forked over claimed chunks: fn(begin, end) runs [begin, end) on one
+  // thread, so the caller keeps per-chunk counters in locals and publishes
+  // them once per chunk instead of touching a shared atomic per item. fn
+  // polls `stop` itself between items.
+  void until_forked_ranges(int n, const std::function<void(int, int)>& fn, const std::atomic<bool>* stop,
+                           ParallelSite* site);
   static void record_inline(ParallelSite* site, int64_t elapsed_ns, int done, int n);
   static int64_t now_ns();
   int workers() const { return workers_; }
@@ -66,6 +72,7 @@ class Parallelizer {
  private:
   struct Job {
     const std::function<void(int)>* fn = nullptr;
+    const std::function<void(int, int)>* rfn = nullptr;  // chunk form (fn == nullptr)
     const std::atomic<bool>* stop = nullptr;
     int n = 0;
     int chunk = 1;
@@ -74,6 +81,7 @@ class Parallelizer {
     std::atomic<int> active{0};
   };
   void worker_loop();
+  void fork_join(Job& job, ParallelSite* site);
   int run_job(Job& job);  // items processed by this thread
 
   int workers_;

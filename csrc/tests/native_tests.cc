@@ -499,6 +499,29 @@ TEST(parallelizer_cost_model_inline_vs_parallel) {
   CHECK(heavy_site.ns_per_item_x16.load() / 16 >= 1000);
 }
 
+TEST(parallelizer_ranges_cover_every_item_once_and_stop) {
+  // until_forked_ranges hands out disjoint chunks that cover [0, n); a chunk
+  // function that raises `stop` ends the claiming of further chunks.
+  Parallelizer par(8, 16);
+  for (int n : {1, 7, 100, 1024, 4099}) {
+    std::vector<std::atomic<int>> seen(static_cast<size_t>(n));
+    par.until_forked_ranges(n, [&](int b, int e) {
+      CHECK(b < e);
+      for (int i = b; i < e; ++i) seen[static_cast<size_t>(i)].fetch_add(1);
+    }, nullptr, nullptr);
+    int bad = 0;
+    for (auto& s : seen) bad += s.load() != 1;
+    CHECK_EQ(bad, 0);
+  }
+  std::atomic<bool> stop{false};
+  std::atomic<int> chunks{0};
+  par.until_forked_ranges(100000, [&](int, int) {
+    chunks.fetch_add(1);
+    stop.store(true);
+  }, &stop, nullptr);
+  CHECK(chunks.load() <= 9);  // at most one chunk per participant after the stop
+}
+
 }  // namespace
 
 TEST(store_optimistic_updates_lose_nothing) {
