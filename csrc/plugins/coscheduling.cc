@@ -465,7 +465,7 @@ class Coscheduling : public Plugin {
     int slot = -1;
     bool head = false;
     if (pos != parked_pos_.end()) {
-      slot = kind_slot(parked_[pos->second].kind);
+      slot = pos->second.slot;
       head = oldest_locked(slot) == parked_.find(pos->second);
       parked_.erase(pos->second);
       parked_pos_.erase(pos);
@@ -644,7 +644,17 @@ class Coscheduling : public Plugin {
     GpuDemand::Kind kind = GpuDemand::None;
     int64_t need = 0;  // units for the group's remaining members
   };
-  using ParkKey = std::pair<MicroTime, uint64_t>;  // (PodGroup creation, pg_key): oldest first
+  // (kind slot, PodGroup creation, pg_key): each kind's line is a contiguous
+  // run of the map, oldest first, so its head is one lower_bound away even
+  // with thousands of groups of the other kind parked ahead of it.
+  struct ParkKey {
+    int slot = 0;
+    MicroTime creation = 0;
+    uint64_t key = 0;
+    bool operator<(const ParkKey& o) const {
+      return slot != o.slot ? slot < o.slot : creation != o.creation ? creation < o.creation : key < o.key;
+    }
+  };
   // Gate verdict for p's group (scheduling thread, snapshot current): pass
   // when the free units, less those owed to other gangs at Permit and to an
   // older parked group of the same kind, cover the remaining members, and
@@ -672,7 +682,7 @@ class Coscheduling : public Plugin {
       int64_t reserved = owed_[slot];
       if (auto o = outstanding_.find(p.pg_key); o != outstanding_.end() && kind_slot(o->second.kind) == slot)
         reserved -= o->second.units;
-      const ParkKey me{pg.meta.creation, p.pg_key};
+      const ParkKey me{slot, pg.meta.creation, p.pg_key};
       auto pos = parked_pos_.find(p.pg_key);
       // The oldest parked group of this kind holds a reservation against
       // younger groups that have not started (so big gangs are not starved
@@ -744,7 +754,7 @@ class Coscheduling : public Plugin {
       parked_[pos->second].need = need;
       return;
     }
-    const ParkKey k{pg.meta.creation, p.pg_key};
+    const ParkKey k{kind_slot(kind), pg.meta.creation, p.pg_key};
     Parked& pk = parked_[k];
     pk.ns = p.ns();
     pk.group = p.pod_group;
@@ -813,10 +823,9 @@ class Coscheduling : public Plugin {
     return true;
   }
   // The oldest parked group of a kind slot (parked_.end() when none).
-  std::map<std::pair<MicroTime, uint64_t>, Parked>::iterator oldest_locked(int slot) {
-    for (auto it = parked_.begin(); it != parked_.end(); ++it)
-      if (kind_slot(it->second.kind) == slot) return it;
-    return parked_.end();
+  std::map<ParkKey, Parked>::iterator oldest_locked(int slot) {
+    auto it = parked_.lower_bound(ParkKey{slot, INT64_MIN, 0});
+    return it != parked_.end() && it->first.slot == slot ? it : parked_.end();
   }
   // One member of the oldest parked group of this kind whose rejections have
   // all landed (so its own GPUs are back), for the active queue. Groups that
@@ -826,7 +835,7 @@ class Coscheduling : public Plugin {
   std::vector<PodPtr> next_probe_locked(int slot) {
     std::vector<PodPtr> out;
     for (auto it = oldest_locked(slot); it != parked_.end(); it = oldest_locked(slot)) {
-      const uint64_t key = it->first.second;
+      const uint64_t key = it->first.key;
       if (rejects_pending_locked(key)) return out;  // the last Unreserve probes
       Pod member;
       member.meta.ns = it->second.ns;

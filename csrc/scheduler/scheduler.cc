@@ -2571,7 +2571,10 @@ void Scheduler::handle_failure(Framework& fw, const QueuedPodInfoPtr& qpi, const
   // The event goes out on the status writer (kube-scheduler's recorder is
   // asynchronous too); the status update stays on the scheduling loop, as
   // upstream's updatePod: written asynchronously it could land after a later
-  // cycle bound the pod and overwrite its PodScheduled=True condition.
+  // cycle bound the pod and overwrite its PodScheduled=True condition. (Moved
+  // to the status writer with a resourceVersion precondition, it cost open-loop
+  // capacity on the box: parked gangs at 112k pods/s went from 44-86 to 1,917,
+  // profiles/r6/README.md, r6x. The inline patch is backpressure.)
   ApiClient* client = fw.handle().client;
   status_writer_->submit([client, pod, msg = st.message()] {
     try {

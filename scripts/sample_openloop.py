@@ -48,6 +48,8 @@ def main() -> int:
                     help="with --sequence: replace the shard by a fresh one (same process) after trial N (0-based)")
     ap.add_argument("--torch-after-pin", action="store_true", help="initialise them after the CPU pinning")
     ap.add_argument("--colocation", default="Preferred", help="NRT gangColocation of the flagship profile")
+    ap.add_argument("--detail", action="store_true",
+                    help="with --sequence: per-type p99, generator lags and the 5-ms timeline of every trial")
     a = ap.parse_args()
 
     def init_torch():
@@ -109,7 +111,7 @@ def main() -> int:
                 last = i == len(rates) - 1
                 if last and a.sample_last:
                     native().sampler_start(a.hz, 4_000_000)
-                r = run_open_loop(shard, rate, 1.0, seed=0)
+                r = run_open_loop(shard, rate, 1.0, seed=0, timeline=a.detail)
                 if last and a.sample_last:
                     native().sampler_dump(os.path.join(a.out, "openloop.samples"))
                 if a.trim:
@@ -119,7 +121,17 @@ def main() -> int:
                              **{k: r["all_gangs"][k] for k in ("p99_create_to_bound_ms", "max_create_to_bound_ms")},
                              "queue_after": shard.sched.queue_counts(),
                              "store_pods": len(shard.store.list("pods", "")[0]) if hasattr(shard, "store") else None})
-                print(json.dumps(rows[-1]), flush=True)
+                if a.detail:
+                    rows[-1].update({
+                        "by_type_p99_ms": {k: v["create_to_bound_ms"]["p99"] for k, v in r["by_gang"].items()},
+                        "by_type_e2a_p99_ms": {k: v["enqueue_to_allow_ms"]["p99"] for k, v in r["by_gang"].items()},
+                        "mean_arrival_lag_us": r.get("mean_arrival_lag_us"),
+                        "mean_delete_lag_us": r.get("mean_delete_lag_us"),
+                        "max_in_flight_pods": r.get("max_in_flight_pods"), "max_held_pods": r.get("max_held_pods"),
+                        "hold_ms": r.get("hold_ms"), "denials": r.get("denials", {}).get("total"),
+                        # per 5 ms: pods in flight, pods held, attempts, unschedulable, parks
+                        "timeline": r.get("timeline", [])})
+                print(json.dumps({k: v for k, v in rows[-1].items() if k != "timeline"}), flush=True)
             with open(os.path.join(a.out, "openloop_sequence.jsonl"), "w") as f:
                 f.writelines(json.dumps(x) + "\n" for x in rows)
             return 0
