@@ -254,6 +254,10 @@ class Coscheduling : public Plugin {
     if (gap <= 0.1f) return {PostFilterResult{}, Status(Code::Unschedulable)};
     if (park_ && gpu_shortage_explains(p, *pg)) {
       // Transient GPU shortage: release the siblings' GPUs, park the group.
+      if (h_.metrics)
+        h_.metrics->inc("xsched_coscheduling_gate_waits_total",
+                        kind_slot(p.gpu_demand.kind) == 0 ? "cause=\"postfilter\",kind=\"gpu\""
+                                                          : "cause=\"postfilter\",kind=\"xcd\"");
       park_rejecting(p, *pg);
       permitted_.erase(p.pg_key);
       return {PostFilterResult{}, XS_FIXED_STATUS(Code::Unschedulable,
@@ -707,6 +711,21 @@ class Coscheduling : public Plugin {
     if (pass) return {};
     // The whole group can never fit: Filter fails and PostFilter denies (reference).
     if (units_for(d, pg.min_member) > total_units(d)) return {};
+    if (h_.metrics) {  // which term of the gate held the group back
+      int64_t owed_others = 0;
+      {
+        std::lock_guard<std::mutex> g(park_mu_);
+        owed_others = owed_[slot];
+        if (auto o = outstanding_.find(p.pg_key); o != outstanding_.end() && kind_slot(o->second.kind) == slot)
+          owed_others -= o->second.units;
+      }
+      const char* cause = !coloc_ok                      ? "colocation"
+                          : free < need                  ? "free"
+                          : free - owed_others < need    ? "owed"
+                                                         : "head";
+      h_.metrics->inc("xsched_coscheduling_gate_waits_total",
+                      std::string("cause=\"") + cause + (slot == 0 ? "\",kind=\"gpu\"" : "\",kind=\"xcd\""));
+    }
     // A group already part-placed releases what its waiting members hold (no
     // hold-and-wait between gangs), as PostFilter's park does.
     if (assigned > 0) park_rejecting(p, pg);

@@ -58,11 +58,14 @@ OpenLoopResult run_open_loop(ObjectStore& store, Scheduler& sched, std::vector<O
     if (now >= next_slice) {
       const Scheduler::Stats st = sched.stats();
       const uint64_t parks = sched.gang_parks();
+      const size_t cache_pods = sched.cache().pod_count(), cache_assumed = sched.cache().assumed_count();
       while (now >= next_slice) {
         out.timeline.push_back({static_cast<int32_t>(in_flight), static_cast<int32_t>(held),
                                 static_cast<int32_t>(st.attempts - st0.attempts),
                                 static_cast<int32_t>(st.unschedulable - st0.unschedulable),
-                                static_cast<int32_t>(parks - parks0)});
+                                static_cast<int32_t>(parks - parks0), static_cast<int32_t>(cache_pods),
+                                static_cast<int32_t>(cache_assumed), static_cast<int32_t>(sched.permit_waiting()),
+                                static_cast<int32_t>(sched.bind_backlog())});
         st0 = st;
         parks0 = parks;
         next_slice += 5000;

@@ -51,8 +51,11 @@ struct OpenLoopResult {
   int64_t max_in_flight_pods = 0, max_held_pods = 0;
   // Every 5 ms of the run: pods in flight and held at the end of the slice.
   // Per 5 ms slice: pods in flight, pods held, and the scheduler's attempts,
-  // unschedulable attempts and parked groups during the slice.
-  std::vector<std::array<int32_t, 5>> timeline;
+  // unschedulable attempts and parked groups during the slice, then the pods
+  // the scheduler's cache accounts on nodes (assumed + bound, deletions not
+  // yet seen included), of them the assumed ones, the pods waiting at Permit
+  // and the binding cycles queued for the binders, at the end of the slice.
+  std::vector<std::array<int32_t, 9>> timeline;
 };
 
 // Runs to completion on the calling thread. `offsets_us[i]` is gang i's

@@ -540,7 +540,7 @@ void Scheduler::informer_loop() {
         ++hi;
         if (ev.kind != "pods" || ev.type == EventType::Deleted) continue;
         try {
-          if (ev.type == EventType::Modified) parsed[hi - 1] = bound_copy_of_assumed(ev);
+          if (ev.type == EventType::Modified) parsed[hi - 1] = copy_for_modified(ev);
         } catch (const std::exception&) {
           continue;
         }
@@ -780,7 +780,7 @@ void Scheduler::handle_pod_event(const WatchEvent& ev) {
     }
     return;
   }
-  PodPtr np = ev.type == EventType::Modified ? bound_copy_of_assumed(ev) : nullptr;
+  PodPtr np = ev.type == EventType::Modified ? copy_for_modified(ev) : nullptr;
   if (!np) np = Pod::from_json(*ev.obj, *gpu_names_);
   PodPtr old = informers_->pod(np->ns(), np->name());
   informers_->upsert_pod(np);
@@ -810,6 +810,34 @@ PodPtr Scheduler::bound_copy_of_assumed(const WatchEvent& ev) {
   const Json& rv = md["resourceVersion"];
   np->meta.resource_version = rv.is_string() ? std::atoll(rv.as_string().c_str()) : rv.as_int();
   np->template_hash = 0;  // as Pod::from_json for an assigned pod
+  const Json& status = obj["status"];
+  np->phase = status["phase"].is_string() ? status["phase"].as_string() : std::string("Pending");
+  np->nominated_node_name = status["nominatedNodeName"].as_string();
+  np->start_time = status["startTime"].is_string() ? parse_rfc3339(status["startTime"].as_string()) : 0;
+  np->scheduled_at = 0;
+  for (const auto& c : status["conditions"].items())
+    if (c["type"].as_string() == "PodScheduled" && c["status"].as_string() == "True")
+      np->scheduled_at = parse_rfc3339(c["lastTransitionTime"].as_string());
+  return np;
+}
+
+// A failed cycle's PodScheduled=False patch (handle_failure) changes status
+// only; at saturation thousands of them reach the informer while creations and
+// deletions queue behind them. The lister's object for the previous version
+// is copied and its status fields refreshed (the fields Pod::from_json reads
+// from status) instead of parsing the pod again.
+PodPtr Scheduler::status_copy_of_listed(const WatchEvent& ev) {
+  if (!ev.status_only || !ev.old) return nullptr;
+  const Json& obj = *ev.obj;
+  const Json& md = obj["metadata"];
+  PodPtr listed = informers_->pod(md["namespace"].as_string(), md["name"].as_string());
+  if (!listed || listed->uid() != md["uid"].as_string()) return nullptr;
+  const Json& old_rv = (*ev.old)["metadata"]["resourceVersion"];
+  const int64_t from_rv = old_rv.is_string() ? std::atoll(old_rv.as_string().c_str()) : old_rv.as_int();
+  if (from_rv != listed->meta.resource_version) return nullptr;  // the lister holds another version: parse
+  auto np = std::make_shared<Pod>(*listed);
+  const Json& rv = md["resourceVersion"];
+  np->meta.resource_version = rv.is_string() ? std::atoll(rv.as_string().c_str()) : rv.as_int();
   const Json& status = obj["status"];
   np->phase = status["phase"].is_string() ? status["phase"].as_string() : std::string("Pending");
   np->nominated_node_name = status["nominatedNodeName"].as_string();

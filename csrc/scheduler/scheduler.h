@@ -249,6 +249,14 @@ class Scheduler {
   uint64_t gang_parks(bool clear = false);
   size_t inflight_bindings() const { return inflight_.load(); }
   size_t bind_threads() const { return binder_ ? binder_->threads() : 0; }
+  // Pods waiting at Permit (every profile) and binding cycles queued for the
+  // binders (the open-loop driver's timeline).
+  size_t permit_waiting() const {
+    size_t n = 0;
+    for (const auto& w : waiting_) n += w->size();
+    return n;
+  }
+  size_t bind_backlog() const { return binder_ ? binder_->pending() : 0; }
   // Seconds since the scheduling loop last ticked (it ticks at least every
   // 100 ms while running; /healthz uses this). 0 before start().
   double loop_age_seconds() const;
@@ -332,6 +340,14 @@ class Scheduler {
   void report_informer_error(const WatchEvent& ev, const char* what);
   void handle_parsed_pod_event(const WatchEvent& ev, const PodPtr& np, PodPtr old);
   PodPtr bound_copy_of_assumed(const WatchEvent& ev);
+  // A status-only Modified event (WatchEvent::status_only) of the version the
+  // lister holds: that Pod copied with the new status fields, no parse.
+  PodPtr status_copy_of_listed(const WatchEvent& ev);
+  // bound_copy_of_assumed, else status_copy_of_listed (nullptr: parse).
+  PodPtr copy_for_modified(const WatchEvent& ev) {
+    PodPtr p = bound_copy_of_assumed(ev);
+    return p ? p : status_copy_of_listed(ev);
+  }
   void apply_pod_update(const WatchEvent& ev, const PodPtr& np, PodPtr old);
   void handle_node_event(const WatchEvent& ev);
   void scheduling_loop();

@@ -2,6 +2,7 @@
 
 #include "common/clock.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <thread>
@@ -37,14 +38,28 @@ void Watcher::push_batch(std::vector<WatchEvent> evs) {
   cv_.notify_one();
 }
 
+bool Watcher::push_quiet(const WatchEvent& ev) {
+  std::lock_guard<AdaptiveMutex> g(mu_);
+  q_.push_back(ev);
+  return waiters_ > 0;
+}
+
+bool Watcher::push_batch_quiet(std::vector<WatchEvent> evs) {
+  std::lock_guard<AdaptiveMutex> g(mu_);
+  for (auto& e : evs) q_.push_back(std::move(e));
+  return waiters_ > 0;
+}
+
 std::vector<WatchEvent> Watcher::next(int timeout_ms, size_t max) {
   std::vector<WatchEvent> out;
   std::unique_lock<AdaptiveMutex> lk(mu_);
   if (q_.empty() && !stopped_.load()) {
+    ++waiters_;
     if (timeout_ms < 0)
       cv_.wait(lk, [&] { return !q_.empty() || stopped_.load(); });
     else
       cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || stopped_.load(); });
+    --waiters_;
   }
   size_t n = std::min(max, q_.size());
   out.reserve(n);
@@ -151,15 +166,18 @@ void ObjectStore::clear_faults() {
   has_faults_.store(false);
 }
 
-void ObjectStore::emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv) {
-  WatchEvent ev{t, kind, obj, old, rv};
+void ObjectStore::emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv,
+                              bool status_only) {
+  WatchEvent ev{t, kind, obj, old, rv, status_only};
   if (batch_) {
     batch_->push_back(ev);
   } else {
     const Json& md = (*obj)["metadata"];
     const std::string& ns = md["namespace"].as_string();
     for (auto& w : watchers_)
-      if (!w->stopped() && w->wants(kind, ns)) w->push(ev);
+      if (!w->stopped() && w->wants(kind, ns) && w->push_quiet(ev) &&
+          std::find(wake_.begin(), wake_.end(), w) == wake_.end())
+        wake_.push_back(w);
   }
   history_.push_back(std::move(ev));
   if (history_.size() > history_cap_) {
@@ -289,7 +307,8 @@ void ObjectStore::flush_batch_locked(std::vector<WatchEvent>& batch) {
       const std::string& ns = (*ev.obj)["metadata"]["namespace"].as_string();
       if (w->wants(ev.kind, ns)) mine.push_back(ev);
     }
-    if (!mine.empty()) w->push_batch(std::move(mine));
+    if (!mine.empty() && w->push_batch_quiet(std::move(mine)) && std::find(wake_.begin(), wake_.end(), w) == wake_.end())
+      wake_.push_back(w);
   }
 }
 
@@ -351,7 +370,8 @@ JsonPtr ObjectStore::update(const std::string& kind, Json obj, bool check_rv) {
 }
 
 JsonPtr ObjectStore::update_optimistic(const std::string& kind, const std::string& key, const std::string& name,
-                                       const std::function<std::optional<Json>(const Json& cur)>& build) {
+                                       const std::function<std::optional<Json>(const Json& cur)>& build,
+                                       bool status_only) {
   for (;;) {
     JsonPtr base;
     {
@@ -372,7 +392,7 @@ JsonPtr ObjectStore::update_optimistic(const std::string& kind, const std::strin
     stamp(*next, rv);
     auto ptr = std::make_shared<const Json>(std::move(*next));
     it->second.obj = ptr;
-    emit_locked(EventType::Modified, kind, ptr, base, rv);
+    emit_locked(EventType::Modified, kind, ptr, base, rv, status_only);
     return ptr;
   }
 }
@@ -380,6 +400,14 @@ JsonPtr ObjectStore::update_optimistic(const std::string& kind, const std::strin
 JsonPtr ObjectStore::patch(const std::string& kind, const std::string& ns, const std::string& name,
                            const Json& merge_patch) {
   check_faults("patch", kind);
+  // A patch of `status` alone (plus a resourceVersion precondition) leaves
+  // spec and metadata as they were: its event says so (WatchEvent::status_only).
+  bool status_only = merge_patch.is_object() && merge_patch.size() > 0;
+  for (const auto& [k, v] : merge_patch.members()) {
+    if (k == "status") continue;
+    if (k == "metadata" && v.is_object() && v.size() == 1 && v.get("resourceVersion")) continue;
+    status_only = false;
+  }
   return update_optimistic(kind, key_of(namespaced(kind) ? ns : "", name), name,
                            [&](const Json& cur) -> std::optional<Json> {
     // A patch carrying metadata.resourceVersion is a precondition (optimistic
@@ -399,7 +427,7 @@ JsonPtr ObjectStore::patch(const std::string& kind, const std::string& ns, const
       if (const Json* v = saved_md.get(k)) md.set(k, *v);
     if (obj == cur) return std::nullopt;  // no-op patch: no new version
     return obj;
-  });
+  }, status_only);
 }
 
 JsonPtr ObjectStore::remove(const std::string& kind, const std::string& ns, const std::string& name,

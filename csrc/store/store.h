@@ -59,6 +59,10 @@ struct WatchEvent {
   JsonPtr obj;     // new object (or last state for Deleted)
   JsonPtr old;     // previous object for Modified/Deleted (nullptr for Added)
   int64_t rv = 0;
+  // A Modified event from a patch that touched only `status` (spec and
+  // metadata are those of `old`): a consumer can update its parsed copy of
+  // `old` from the status instead of parsing the whole object again.
+  bool status_only = false;
 };
 
 class Watcher {
@@ -74,6 +78,13 @@ class Watcher {
   }
   void push(const WatchEvent& ev);
   void push_batch(std::vector<WatchEvent> evs);
+  // push / push_batch without the wake-up: true when the consumer is blocked
+  // in next() and needs notify(). The store queues events under its own lock
+  // this way and wakes consumers after releasing it (a futex wake inside the
+  // store's critical section serialised every writer behind it).
+  bool push_quiet(const WatchEvent& ev);
+  bool push_batch_quiet(std::vector<WatchEvent> evs);
+  void notify() { cv_.notify_one(); }
 
  private:
   std::set<std::string> kinds_;
@@ -81,6 +92,7 @@ class Watcher {
   mutable AdaptiveMutex mu_;
   std::condition_variable_any cv_;
   std::deque<WatchEvent> q_;
+  int waiters_ = 0;  // consumers blocked in next() (guarded by mu_)
   std::atomic<bool> stopped_{false};
 };
 using WatcherPtr = std::shared_ptr<Watcher>;
@@ -152,7 +164,8 @@ class ObjectStore {
 
   void check_faults(const std::string& verb, const std::string& kind);
   void expire_events_locked(const std::string& created_key);
-  void emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv);
+  void emit_locked(EventType t, const std::string& kind, const JsonPtr& obj, const JsonPtr& old, int64_t rv,
+                   bool status_only = false);
   JsonPtr create_locked(const std::string& kind, Json obj);
   void flush_batch_locked(std::vector<WatchEvent>& batch);
   static void stamp(Json& obj, int64_t rv);
@@ -163,7 +176,7 @@ class ObjectStore {
   // longer happens while 16 binder threads queue on mu_). Returns the
   // committed (or, for a no-op, current) object.
   JsonPtr update_optimistic(const std::string& kind, const std::string& key, const std::string& name,
-                            const std::function<std::optional<Json>(const Json& cur)>& build);
+                            const std::function<std::optional<Json>(const Json& cur)>& build, bool status_only = false);
   std::vector<WatchEvent>* batch_ = nullptr;  // bulk ops collect events here (under mu_)
 
   // Taken by every writer (16 binder threads, the informer's reads, bulk
@@ -179,7 +192,10 @@ class ObjectStore {
     ~Guard() {
       std::vector<WatchEvent> dead;
       if (!s_.evicted_.empty()) dead.swap(s_.evicted_);
+      std::vector<WatcherPtr> wake;
+      if (!s_.wake_.empty()) wake.swap(s_.wake_);
       s_.mu_.unlock();
+      for (const auto& w : wake) w->notify();
       if (!dead.empty()) s_.reap(std::move(dead));
     }
     Guard(const Guard&) = delete;
@@ -189,6 +205,9 @@ class ObjectStore {
     const ObjectStore& s_;
   };
   mutable std::vector<WatchEvent> evicted_;
+  // Watchers that got events under the lock and wait for them (woken by
+  // ~Guard, after the unlock).
+  mutable std::vector<WatcherPtr> wake_;
   // Evicted entries are freed on a background thread (started on the first
   // eviction), as a garbage-collected API server would: the writer that
   // evicts them does not pay for the JSON trees of objects deleted long ago.

@@ -29,13 +29,15 @@ def main() -> int:
     ap.add_argument("--hz", type=int, default=4000)
     ap.add_argument("--colocation", default="Preferred", help="NRT gangColocation of the flagship profile")
     ap.add_argument("--tag", default="bench_waves")
+    ap.add_argument("--pin", default="l3", help="shard CPU placement (utils/cpuaffinity.py): l3 | l3x2 | none")
+    ap.add_argument("--options", default="{}", help="scheduler options JSON, e.g. '{\"bindWorkers\": 8}'")
     ap.add_argument("--seed", type=int, default=7)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
-    apply("l3")
+    apply(a.pin)
     from flex_gpu_scheduler_amd.utils.workload import flagship_config
 
-    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed,
+    shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample", seed=a.seed, options=json.loads(a.options),
                   config=flagship_config(gang_colocation=a.colocation))
     try:
         ws = [shard.wave(i) for i in range(a.waves + 4)]

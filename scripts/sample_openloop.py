@@ -48,6 +48,7 @@ def main() -> int:
                     help="with --sequence: replace the shard by a fresh one (same process) after trial N (0-based)")
     ap.add_argument("--torch-after-pin", action="store_true", help="initialise them after the CPU pinning")
     ap.add_argument("--colocation", default="Preferred", help="NRT gangColocation of the flagship profile")
+    ap.add_argument("--pin", default="l3", help="shard CPU placement (utils/cpuaffinity.py): l3 | l3x2 | none")
     ap.add_argument("--detail", action="store_true",
                     help="with --sequence: per-type p99, generator lags and the 5-ms timeline of every trial")
     a = ap.parse_args()
@@ -61,7 +62,7 @@ def main() -> int:
     if a.torch:
         init_torch()
     os.makedirs(a.out, exist_ok=True)
-    apply("l3")
+    apply(a.pin)
     if a.torch_after_pin:
         init_torch()
     from flex_gpu_scheduler_amd.utils.workload import flagship_config
@@ -87,6 +88,14 @@ def main() -> int:
         if a.sequence:
             rows = []
             rates = [float(x) for x in a.sequence.split(",")]
+
+            def gate_waits() -> dict:
+                out = {}
+                for line in shard.sched.metrics_text().splitlines():
+                    if line.startswith("xsched_coscheduling_gate_waits_total{"):
+                        k, v = line.rsplit(" ", 1)
+                        out[k[k.index("{") + 1:k.rindex("}")].replace('"', "")] = float(v)
+                return out
             for i, rate in enumerate(rates):
                 if i == a.fresh_sched_after + 1:
                     # Scheduler state vs store state: the store (and its
@@ -111,7 +120,9 @@ def main() -> int:
                 last = i == len(rates) - 1
                 if last and a.sample_last:
                     native().sampler_start(a.hz, 4_000_000)
+                gw0 = gate_waits() if a.detail else {}
                 r = run_open_loop(shard, rate, 1.0, seed=0, timeline=a.detail)
+                gw1 = gate_waits() if a.detail else {}
                 if last and a.sample_last:
                     native().sampler_dump(os.path.join(a.out, "openloop.samples"))
                 if a.trim:
@@ -129,6 +140,7 @@ def main() -> int:
                         "mean_delete_lag_us": r.get("mean_delete_lag_us"),
                         "max_in_flight_pods": r.get("max_in_flight_pods"), "max_held_pods": r.get("max_held_pods"),
                         "hold_ms": r.get("hold_ms"), "denials": r.get("denials", {}).get("total"),
+                        "gate_waits": {k: int(v - gw0.get(k, 0)) for k, v in gw1.items() if v - gw0.get(k, 0)},
                         # per 5 ms: pods in flight, pods held, attempts, unschedulable, parks
                         "timeline": r.get("timeline", [])})
                 print(json.dumps({k: v for k, v in rows[-1].items() if k != "timeline"}), flush=True)

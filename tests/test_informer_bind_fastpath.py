@@ -55,3 +55,38 @@ def test_bound_copy_matches_full_parse(store):
             assert s.node_info(node)["pods"] == count
     finally:
         s.stop()
+
+
+def test_status_only_update_matches_full_parse(store):
+    """A status-only patch (the PodScheduled=False condition a failed cycle
+    writes) reaches the informer flagged WatchEvent::status_only; the lister's
+    previous object is copied with the new status fields
+    (Scheduler::status_copy_of_listed) and must equal a full parse."""
+    store.create("nodes", mi355x_node("n0"))
+    s = new_scheduler(store, load_config(flagship_config()), start=True)
+    try:
+        # Unschedulable (asks for more GPUs than any node has): its failed
+        # cycle patches the condition; then patches of status alone follow.
+        store.create("pods", make_pod("big", requests={"cpu": "1"}, limits={GPU: "16"}, labels={"team": "b"}))
+        assert wait(lambda: any(c.get("type") == "PodScheduled" and c.get("status") == "False"
+                                for c in store.get("pods", "default", "big").get("status", {}).get("conditions", [])))
+        store.patch("pods", "default", "big", {"status": {"phase": "Pending", "nominatedNodeName": "n0",
+                                                          "startTime": "2026-01-02T03:04:05Z"}})
+        store.patch("pods", "default", "big", {"status": {"conditions": [
+            {"type": "PodScheduled", "status": "True", "lastTransitionTime": "2026-01-02T03:04:06Z"}]}})
+        obj = store.get("pods", "default", "big")
+        assert wait(lambda: (s.lister_pod("default", "big") or {}).get("resource_version") ==
+                    int(obj["metadata"]["resourceVersion"]))
+        got = s.lister_pod("default", "big")
+        want = native().pod_summary(obj)
+        for f in FIELDS:
+            assert got[f] == want[f], (f, got[f], want[f])
+        assert got["start_time"] > 0 and got["scheduled_at"] > 0
+        # A patch that is not status-only still parses (labels change the pod).
+        store.patch("pods", "default", "big", {"metadata": {"labels": {"team": "c"}}})
+        obj = store.get("pods", "default", "big")
+        assert wait(lambda: (s.lister_pod("default", "big") or {}).get("resource_version") ==
+                    int(obj["metadata"]["resourceVersion"]))
+        assert s.lister_pod("default", "big")["labels"] == native().pod_summary(obj)["labels"]
+    finally:
+        s.stop()

