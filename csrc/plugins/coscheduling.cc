@@ -350,7 +350,13 @@ class Coscheduling : public Plugin {
     int assigned = h_.cache->assigned_in_group(p->pg_key);
     if (assigned < pg->min_member) {
       if (park_) note_outstanding(*p, pg->min_member - assigned);
-      activate_siblings(*p, s);
+      // The first waiting member activates its siblings; the next ones of the
+      // same gang, arriving in order with more members assigned, would list
+      // and re-activate the same pods (O(k^2) per gang of k). A gang that
+      // starts over (fewer assigned than last time) activates again.
+      if (p->pg_key != act_key_ || assigned <= act_assigned_) activate_siblings(*p, s);
+      act_key_ = p->pg_key;
+      act_assigned_ = assigned;
       return {Status(Code::Wait), wait_time(*pg)};
     }
     if (park_) drop_outstanding(p->pg_key);
@@ -980,6 +986,10 @@ class Coscheduling : public Plugin {
   uint64_t probe_key_[2] = {0, 0};  // per kind slot: the group whose probe is out
   int64_t probe_sent_us_[2] = {0, 0};
   uint64_t parks_total_ = 0;
+  // Permit (scheduling thread only): the gang whose waiting member last
+  // activated its siblings, and how many members it had assigned then.
+  uint64_t act_key_ = 0;
+  int act_assigned_ = 0;
 
   Handle& h_;
   TTLSet denied_, permitted_;
