@@ -335,9 +335,10 @@ def main() -> int:
         extras["gang_admit_open_loop"] = {
             "burst_capacity_pods_per_s": round(burst, 1),
             "capacity_pods_per_s": round(cap, 1),
-            "capacity_rule": "highest x1.3-step rate (+2 bisection steps) whose p99 PG-create->last-Bind over "
-                             "all gangs (unbound = infinite) is <= 25 ms; one trial per rate, two (both must "
-                             "pass) in the top two steps under the burst rate",
+            "capacity_rule": "highest rate of a rising ladder (x1.3 steps, then x1.07 steps from one x1.3 step "
+                             "under the burst rate up to it) whose p99 PG-create->last-Bind over all gangs "
+                             "(unbound = infinite) is <= 25 ms; the search stops at the first failed rate; one "
+                             "trial per rate, two (both must pass) within two x1.3 steps of the burst rate",
             "transient_shortage": "Park (gangs short of GPUs wait for a release; the reference denies them "
                                   "for deniedPGExpirationTimeSeconds)",
             "process": "this rank's" if args.open_loop_in_process else "child without the GPU runtime, fresh shard",

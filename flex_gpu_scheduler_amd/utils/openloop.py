@@ -111,21 +111,29 @@ def summarize(kinds: list[str], gangs: list[dict], wall_us: int, late_us: int) -
 
 def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, seed: int = 0,
                        start_pods_per_s: float = 2000.0, occupancy: float = 0.5,
-                       p99_budget_ms: float = 25.0, log: list | None = None, reset=None) -> float:
+                       p99_budget_ms: float = 25.0, log: list | None = None, reset=None,
+                       fine_step: float = 1.07) -> float:
     """Sustained open-loop capacity (pods/s), an SLO capacity: the highest
-    arrival rate, in steps x1.3 apart from `start_pods_per_s` up to
-    `max_pods_per_s` (the burst capacity; when the next step would pass it,
-    the burst rate itself is the next trial) and refined by two bisection
-    steps inside the last interval, at which the p99 PG-create -> last-Bind over
-    every gang of the run is within `p99_budget_ms` (a gang still unbound at
-    the end counts as infinitely late). Gangs arrive one at a time and are
-    held at `occupancy` of the SPX GPUs, as in the measured loads.
+    arrival rate of a rising ladder at which the p99 PG-create -> last-Bind
+    over every gang of the run is within `p99_budget_ms` (a gang still
+    unbound at the end counts as infinitely late). The ladder climbs x1.3 from
+    `start_pods_per_s` while the next step stays a full x1.3 step under
+    `max_pods_per_s` (the burst capacity), then in steps of `fine_step` (x1.07,
+    the resolution two bisection steps of x1.3 gave) up to the burst rate
+    itself. Gangs arrive one at a time and are held at `occupancy` of the SPX
+    GPUs, as in the measured loads.
 
-    One trial per rate (two, with different arrival seeds, that must both
-    pass, for rates in the top two x1.3 steps under the burst rate), no
-    retries. With `reset` (a callable returning a fresh, warmed shard), the
-    trial after a failed one runs on a fresh shard. Every
-    trial is appended to `log` with its parked gangs, its Coscheduling
+    The search ends at the first failed rate: the capacity is the rate below
+    it. An overloaded trial leaves thousands of parked gangs and a lagging
+    informer behind, and trials after one, even on a fresh shard in the same
+    process, failed at rates that pass on their own (docs/ARCHITECTURE.md,
+    "the open-loop edge is metastable"): climbing in fine steps, the first
+    failure is at most one step past the edge, and no trial follows it.
+
+    One trial per rate; two, with different arrival seeds, that must both
+    pass, for rates within two x1.3 steps of the burst rate. No retries.
+    `reset` is accepted for callers of the bisection version and not used.
+    Every trial is appended to `log` with its parked gangs, its Coscheduling
     denials and their causes (Scheduler::note_gang_denied), p99.9 and max.
     Near capacity the hold time (a few ms) is comparable to the admission
     pipeline and GPUs held by gangs in flight push the SPX pool to full: a
@@ -133,14 +141,14 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     transientShortage=Park) rather than being denied for the TTL as the
     reference's PostFilter does (which made a rate fail on < 1% of its
     gangs waiting 3 s)."""
-    top = max_pods_per_s / 1.3 ** 2  # rates in the top two grid steps get a second trial
-    cur = [shard]
+    del reset
+    top = max_pods_per_s / 1.3 ** 2  # rates within two x1.3 steps of the burst rate get a second trial
 
     def served(rate: float) -> bool:
         trials = 2 if rate >= top else 1
         ok = True
         for t in range(trials):
-            r = run_open_loop(cur[0], rate, duration_s, seed=seed + 7 * t, occupancy=occupancy)
+            r = run_open_loop(shard, rate, duration_s, seed=seed + 7 * t, occupancy=occupancy)
             p99 = r["all_gangs"]["p99_create_to_bound_ms"]
             ok_t = p99 is not None and p99 != "inf" and p99 <= p99_budget_ms
             if log is not None:
@@ -157,13 +165,6 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
             ok = ok and ok_t
             if not ok:
                 break
-        if not ok and reset is not None:
-            # An overloaded trial leaves the shard slower for the next ones
-            # (docs/ARCHITECTURE.md, "the open-loop aftermath"): the next
-            # trial starts on a fresh shard of the same cluster.
-            cur[0] = reset()
-            if log is not None and log:
-                log[-1]["next_trial_on_fresh_shard"] = True
         return ok
 
     rate = min(start_pods_per_s, max(max_pods_per_s, 1.0))
@@ -175,25 +176,18 @@ def open_loop_capacity(shard, max_pods_per_s: float, duration_s: float = 1.0, se
     if rate <= floor:
         return 0.0
     best = rate
-    rate *= 1.3
-    while rate <= max_pods_per_s and served(rate):
-        best = rate
-        rate *= 1.3
-    # Two bisection steps inside the last interval: below the rate that
-    # failed, or, when the next x1.3 step ran past the burst capacity, below
-    # the burst capacity itself (otherwise the grid, not the scheduler, caps
-    # the result at the last step under the burst rate).
-    hi = rate if rate <= max_pods_per_s else max_pods_per_s
-    if hi > best:
-        if rate > max_pods_per_s and served(hi):
-            return hi
-        for _ in range(2):
-            mid = (best + hi) / 2
-            if served(mid):
-                best = mid
-            else:
-                hi = mid
-    return best
+    coarse_top = max_pods_per_s / 1.3
+    while True:
+        nxt = rate * 1.3 if rate * 1.3 <= coarse_top else rate * fine_step
+        if nxt > max_pods_per_s:
+            # The last rung is the burst rate itself (otherwise the ladder,
+            # not the scheduler, would cap the result just under it).
+            if rate >= max_pods_per_s:
+                return best
+            nxt = max_pods_per_s
+        if not served(nxt):
+            return best
+        best = rate = nxt
 
 
 def denial_summary(total: int, recs: list[dict], keep: int = 3) -> dict:

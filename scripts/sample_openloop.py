@@ -48,6 +48,8 @@ def main() -> int:
                     help="with --sequence: replace the shard by a fresh one (same process) after trial N (0-based)")
     ap.add_argument("--torch-after-pin", action="store_true", help="initialise them after the CPU pinning")
     ap.add_argument("--colocation", default="Preferred", help="NRT gangColocation of the flagship profile")
+    ap.add_argument("--settle", type=float, default=0.0,
+                    help="with --fresh-after: seconds to wait (after malloc_trim) once the old shard is dropped")
     ap.add_argument("--pin", default="l3", help="shard CPU placement (utils/cpuaffinity.py): l3 | l3x2 | none")
     ap.add_argument("--detail", action="store_true",
                     help="with --sequence: per-type p99, generator lags and the 5-ms timeline of every trial")
@@ -111,6 +113,15 @@ def main() -> int:
                     # Shard state vs process state: a new store and scheduler
                     # in the same process (same heap), warmed as the first.
                     shard.close()
+                    shard = None
+                    if a.settle > 0:
+                        import ctypes
+                        import gc
+                        import time
+
+                        gc.collect()
+                        time.sleep(a.settle)
+                        ctypes.CDLL("libc.so.6").malloc_trim(0)
                     shard = Shard(ClusterSpec(nodes=a.nodes), namespace="sample2", seed=a.seed,
                                   config=flagship_config(gang_colocation=a.colocation))
                     for j in range(4):

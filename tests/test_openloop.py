@@ -147,9 +147,10 @@ def test_burst_wave_interleaves_cpx_gangs_in_queue_order():
 
 
 def test_capacity_search_reaches_the_burst_rate(monkeypatch):
-    """The search's x1.3 grid must not cap the capacity below the burst rate:
-    when the next step runs past it, the burst rate itself (then bisection
-    under it) is tried; one trial per rate, two near the top."""
+    """The search's ladder must not cap the capacity below the burst rate:
+    its last rung is the burst rate itself. It climbs x1.3, then x1.07 from
+    one x1.3 step under the burst rate, stops at the first failed rate (no
+    trial follows a failure), and runs one trial per rate, two near the top."""
     from flex_gpu_scheduler_amd.utils import openloop
 
     tried = []
@@ -165,18 +166,23 @@ def test_capacity_search_reaches_the_burst_rate(monkeypatch):
     monkeypatch.setattr(openloop, "run_open_loop", fake_run)
     limit = 1e9  # every rate served: the capacity is the burst rate
     assert openloop.open_loop_capacity(None, 120_000.0) == 120_000.0
-    # One trial per rate, two in the top two x1.3 steps under the burst rate.
+    # One trial per rate, two within two x1.3 steps of the burst rate.
     top = 120_000.0 / 1.3 ** 2
     for r in set(tried):
         assert tried.count(r) == (2 if r >= top else 1), (r, tried)
+    rates = sorted(set(tried))
+    steps = [b / a for a, b in zip(rates, rates[1:])]
+    assert all(abs(x - 1.3) < 1e-2 or x <= 1.07 + 1e-2 for x in steps), steps
+    assert rates[-1] == 120_000 and any(x <= 1.071 for x in steps)
     tried.clear()
-    limit = 110_000.0  # the burst rate fails: bisection between the last grid step and it
+    limit = 110_000.0  # the edge under the burst rate: found to within one x1.07 step
     cap = openloop.open_loop_capacity(None, 120_000.0)
-    assert 102_000 < cap <= 110_000 and 120_000 in tried
+    assert 110_000 / 1.071 < cap <= 110_000, cap
+    assert max(tried) > 110_000 and tried[-1] == max(tried)  # the failed rate is the last trial
     tried.clear()
-    limit = 50_000.0  # an ordinary failing grid step: unchanged behaviour
+    limit = 50_000.0  # an ordinary failing coarse step: the search ends there
     cap = openloop.open_loop_capacity(None, 120_000.0)
-    assert 45_000 < cap <= 50_000 and max(tried) < 120_000
+    assert 50_000 / 1.31 < cap <= 50_000 and max(tried) < 120_000 and tried[-1] == max(tried)
 
 
 def test_capacity_report_in_a_gpu_free_child():
