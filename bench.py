@@ -341,7 +341,9 @@ def main() -> int:
                              "trial per rate, two (both must pass) within two x1.3 steps of the burst rate",
             "transient_shortage": "Park (gangs short of GPUs wait for a release; the reference denies them "
                                   "for deniedPGExpirationTimeSeconds)",
-            "process": "this rank's" if args.open_loop_in_process else "child without the GPU runtime, fresh shard",
+            "process": "this rank's" if args.open_loop_in_process else (
+                "children without the GPU runtime: the search on one fresh shard, the 50%/90% loads on "
+                "another in a second process"),
             "capacity_search": rep["search"],
             **{k: rep[k] for k in ("load_50", "load_90", "deny_mode_load_90") if k in rep}}
         search = rep["search"]

@@ -263,17 +263,27 @@ def capacity_in_child(nodes: int, seed: int, options: dict, burst: float, cpus: 
     import subprocess
     import sys
 
-    cmd = [sys.executable, "-m", "flex_gpu_scheduler_amd.utils.openloop", "--nodes", str(nodes),
-           "--seed", str(seed), "--options", json.dumps(options), "--burst", repr(float(burst)),
-           "--warm-waves", str(warm_waves), "--hbm-gib", str(hbm_gib), "--colocation", colocation]
-    if deny_check:
-        cmd.append("--deny-check")
+    base = [sys.executable, "-m", "flex_gpu_scheduler_amd.utils.openloop", "--nodes", str(nodes),
+            "--seed", str(seed), "--options", json.dumps(options), "--burst", repr(float(burst)),
+            "--warm-waves", str(warm_waves), "--hbm-gib", str(hbm_gib), "--colocation", colocation]
     if cpus:
-        cmd += ["--cpus", ",".join(map(str, cpus))]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, check=False)
-    if r.returncode != 0:
-        raise RuntimeError(f"open-loop child exited {r.returncode}: {r.stderr[-2000:]}")
-    return json.loads(r.stdout.strip().splitlines()[-1])
+        base += ["--cpus", ",".join(map(str, cpus))]
+
+    def child(extra: list[str]) -> dict:
+        r = subprocess.run(base + extra, capture_output=True, text=True, timeout=timeout_s, check=False)
+        if r.returncode != 0:
+            raise RuntimeError(f"open-loop child exited {r.returncode}: {r.stderr[-2000:]}")
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    # The search ends with an overloaded trial; the 50% / 90% loads then run
+    # in a second fresh process, so they never follow it (a fresh shard in
+    # the overloaded process still served the 90% load at 11 ms p99 where a
+    # fresh process serves it at 1 ms: profiles/r6/README.md, r6ah).
+    rep = child(["--search-only"])
+    if rep["capacity"] > 0:
+        loads = child(["--loads-at", repr(float(rep["capacity"]))] + (["--deny-check"] if deny_check else []))
+        rep.update({k: v for k, v in loads.items() if k.startswith(("load_", "deny_mode_"))})
+    return rep
 
 
 def _child_main(argv: list[str] | None = None) -> int:
@@ -291,6 +301,9 @@ def _child_main(argv: list[str] | None = None) -> int:
     ap.add_argument("--colocation", default="Preferred")
     ap.add_argument("--deny-check", action="store_true", help="also run the 90%% load in Deny mode")
     ap.add_argument("--no-reset", action="store_true", help="keep one shard through the whole search")
+    ap.add_argument("--search-only", action="store_true", help="the capacity search alone (no 50%%/90%% loads)")
+    ap.add_argument("--loads-at", type=float, default=0.0,
+                    help="no search: the 50%% and 90%% loads of this capacity on a fresh shard")
     a = ap.parse_args(argv)
     if a.cpus:
         os.sched_setaffinity(0, [int(c) for c in a.cpus.split(",")])  # before the shard's threads start
@@ -313,7 +326,17 @@ def _child_main(argv: list[str] | None = None) -> int:
         return sh
 
     try:
-        rep = capacity_report(fresh(), a.burst, seed=a.seed, reset=None if a.no_reset else fresh)
+        if a.loads_at > 0:
+            sh = fresh()
+            rep = {"capacity": a.loads_at, "search": []}
+            for f in (0.5, 0.9):
+                rep[f"load_{int(f * 100)}"] = run_open_loop(sh, f * a.loads_at, duration_s=1.0, seed=a.seed + 1)
+        elif a.search_only:
+            search: list[dict] = []
+            cap = open_loop_capacity(fresh(), a.burst, seed=a.seed, log=search) if a.burst > 0 else 0.0
+            rep = {"capacity": cap, "search": search}
+        else:
+            rep = capacity_report(fresh(), a.burst, seed=a.seed, reset=None if a.no_reset else fresh)
     finally:
         while shards:
             shards.pop().close()
