@@ -250,28 +250,28 @@ void dump_string(std::string& out, const std::string& s) {
 }
 }  // namespace
 
-const std::string& Json::as_string() const { return t_ == Type::String ? s_ : kEmptyString; }
-const Json::Array& Json::items() const { return t_ == Type::Array ? a_ : kEmptyArray; }
+const std::string& Json::as_string() const { return t_ == Type::String ? h_.s : kEmptyString; }
+const Json::Array& Json::items() const { return t_ == Type::Array ? h_.a : kEmptyArray; }
 Json::Array& Json::items_mut() {
   if (t_ != Type::Array) { *this = array(); }
-  return a_;
+  return h_.a;
 }
-const Json::Object& Json::members() const { return t_ == Type::Object ? o_ : kEmptyObject; }
+const Json::Object& Json::members() const { return t_ == Type::Object ? h_.o : kEmptyObject; }
 Json::Object& Json::members_mut() {
   if (t_ != Type::Object) { *this = object(); }
-  return o_;
+  return h_.o;
 }
 
 const Json* Json::get(std::string_view key) const {
   if (t_ != Type::Object) return nullptr;
-  for (const auto& kv : o_)
+  for (const auto& kv : h_.o)
     if (kv.first == key) return &kv.second;
   return nullptr;
 }
 
 Json* Json::get_mut(std::string_view key) {
   if (t_ != Type::Object) return nullptr;
-  for (auto& kv : o_)
+  for (auto& kv : h_.o)
     if (kv.first == key) return &kv.second;
   return nullptr;
 }
@@ -315,9 +315,9 @@ Json& Json::at_or_create(std::string_view key) {
 
 bool Json::erase(std::string_view key) {
   if (t_ != Type::Object) return false;
-  for (auto it = o_.begin(); it != o_.end(); ++it) {
+  for (auto it = h_.o.begin(); it != h_.o.end(); ++it) {
     if (it->first == key) {
-      o_.erase(it);
+      h_.o.erase(it);
       return true;
     }
   }
@@ -335,11 +335,11 @@ bool Json::operator==(const Json& o) const {
   switch (t_) {
     case Type::Null: return true;
     case Type::Bool: return i_ == o.i_;
-    case Type::String: return s_ == o.s_;
-    case Type::Array: return a_ == o.a_;
+    case Type::String: return h_.s == o.h_.s;
+    case Type::Array: return h_.a == o.h_.a;
     case Type::Object: {
-      if (o_.size() != o.o_.size()) return false;
-      for (const auto& kv : o_) {
+      if (h_.o.size() != o.h_.o.size()) return false;
+      for (const auto& kv : h_.o) {
         const Json* other = o.get(kv.first);
         if (!other || !(*other == kv.second)) return false;
       }
@@ -361,11 +361,11 @@ void Json::dump_to(std::string& out) const {
       out += buf;
       break;
     }
-    case Type::String: dump_string(out, s_); break;
+    case Type::String: dump_string(out, h_.s); break;
     case Type::Array: {
       out.push_back('[');
       bool first = true;
-      for (const auto& v : a_) {
+      for (const auto& v : h_.a) {
         if (!first) out.push_back(',');
         first = false;
         v.dump_to(out);
@@ -376,7 +376,7 @@ void Json::dump_to(std::string& out) const {
     case Type::Object: {
       out.push_back('{');
       bool first = true;
-      for (const auto& kv : o_) {
+      for (const auto& kv : h_.o) {
         if (!first) out.push_back(',');
         first = false;
         dump_string(out, kv.first);
@@ -408,7 +408,7 @@ void Json::merge_patch(const Json& patch) {
     return;
   }
   if (!is_object()) *this = object();
-  for (const auto& kv : patch.o_) {
+  for (const auto& kv : patch.h_.o) {
     if (kv.second.is_null()) {
       erase(kv.first);
     } else if (kv.second.is_object()) {
@@ -429,10 +429,10 @@ void Json::merge_patch(const Json& patch) {
 Json Json::diff_merge_patch(const Json& from, const Json& to) {
   if (!from.is_object() || !to.is_object()) return to;
   Json patch = object();
-  for (const auto& kv : from.o_) {
+  for (const auto& kv : from.h_.o) {
     if (!to.get(kv.first)) patch.set(kv.first, Json());
   }
-  for (const auto& kv : to.o_) {
+  for (const auto& kv : to.h_.o) {
     const Json* old = from.get(kv.first);
     if (!old) {
       patch.set(kv.first, kv.second);
@@ -447,11 +447,27 @@ Json Json::diff_merge_patch(const Json& from, const Json& to) {
 }
 
 namespace {
+// Word-at-a-time mixing (a multiply-xorshift per 8 bytes, the length mixed in
+// first so "ab"+"c" and "a"+"bc" differ). The byte-at-a-time FNV it replaces
+// was 6% of the informer thread at 1,024 nodes (template and spec hashes of
+// every parsed pod).
+inline uint64_t mix(uint64_t h, uint64_t v) {
+  h ^= v;
+  h *= 0xff51afd7ed558ccdULL;
+  return h ^ (h >> 33);
+}
 inline uint64_t fnv(uint64_t h, const void* data, size_t n) {
   const unsigned char* p = static_cast<const unsigned char*>(data);
-  for (size_t i = 0; i < n; ++i) {
-    h ^= p[i];
-    h *= 1099511628211ULL;
+  h = mix(h, n);
+  for (; n >= 8; n -= 8, p += 8) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    h = mix(h, w);
+  }
+  if (n) {
+    uint64_t w = 0;
+    std::memcpy(&w, p, n);
+    h = mix(h, w);
   }
   return h;
 }
@@ -487,7 +503,7 @@ uint64_t json_hash(const Json& j, uint64_t h, std::string_view skip_key) {
     case Json::Type::Object:
       for (const auto& [k, v] : j.members()) {
         if (!skip_key.empty() && k == skip_key) continue;
-        h = fnv(h, k.data(), k.size() + 1);  // include the terminator: "ab"+"c" != "a"+"bc"
+        h = fnv(h, k.data(), k.size());  // length-prefixed: "ab"+"c" != "a"+"bc"
         h = json_hash(v, h);
       }
       break;

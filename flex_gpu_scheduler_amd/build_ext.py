@@ -33,7 +33,8 @@ CORE_DIRS = ["common", "api", "store", "framework", "scheduler", "plugins", "res
 # OpenSSL for the native REST client's TLS (rest/http.cc).
 LINK_LIBS = ["-lssl", "-lcrypto"]
 CXXFLAGS = ["-std=c++20", "-O3", "-fPIC", "-Wall", "-Wno-unused-variable", "-Wno-unused-parameter",
-            "-Wno-sign-compare", "-fvisibility=hidden", "-pthread"]
+            "-Wno-sign-compare", "-fvisibility=hidden", "-pthread",
+            *os.environ.get("XSCHED_CXXFLAGS_EXTRA", "").split()]
 
 
 def _ext_suffix() -> str:
