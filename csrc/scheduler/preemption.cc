@@ -235,7 +235,10 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
     if (nv > 0 && k + 1 >= num_candidates) stop.store(true);
     return &slots[static_cast<size_t>(k)];
   };
-  h_.parallelizer->until(n, [&](int i) {
+  // One node's dry run. Memo hits and misses are counted by the caller per
+  // chunk of nodes: a shared counter bumped per node serialised the 16
+  // workers on one cache line (as the forked Filter walk did, round 6).
+  auto one = [&](int i, uint64_t& hits, uint64_t& misses) {
     const NodeInfoPtr& src = potential[(offset + i) % n];
     Memo::Shard* shard = nullptr;
     const std::vector<PodPtr>* noms = nullptr;
@@ -272,7 +275,7 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
         for (size_t j = 0; j < nmatch && !hit; ++j)
           if (!match[j]->guards || policy_->guards_hold(s, *match[j]->guards, run)) hit = match[j];
         if (hit) {
-          memo_->hits.fetch_add(1, std::memory_order_relaxed);
+          ++hits;
           if (!hit->candidate) return;
           if (Slot* sl = claim(i, hit->num_pdb_violations)) {
             sl->run = run;
@@ -282,7 +285,7 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
           }
           return;
         }
-        memo_->misses.fetch_add(1, std::memory_order_relaxed);
+        ++misses;
       }
     }
     // The candidate is evaluated on this worker's scratch NodeInfo: copy
@@ -357,7 +360,17 @@ void Evaluator::dry_run_refs(CycleState& s, const Pod& pod, const std::vector<No
       sl->c.victims.swap(c.victims);
       sl->c.num_pdb_violations = c.num_pdb_violations;
     }
-  }, &stop);
+  };
+  auto range = [&](int b, int e) {
+    uint64_t hits = 0, misses = 0;
+    for (int i = b; i < e && !stop.load(std::memory_order_relaxed); ++i) one(i, hits, misses);
+    if (hits) memo_->hits.fetch_add(hits, std::memory_order_relaxed);
+    if (misses) memo_->misses.fetch_add(misses, std::memory_order_relaxed);
+  };
+  if (h_.parallelizer->plan_inline(n, nullptr))
+    range(0, n);
+  else
+    h_.parallelizer->until_forked_ranges(n, range, &stop, nullptr);
   // Non-violating candidates first, then the violating ones (upstream order).
   const int k = by_index ? n : std::min(used.load(), cap);
   dr.refs.clear();
