@@ -337,7 +337,8 @@ def main() -> int:
             "capacity_pods_per_s": round(cap, 1),
             "capacity_rule": "highest rate of a rising ladder (x1.3 steps, then x1.07 steps from one x1.3 step "
                              "under the burst rate up to it) whose p99 PG-create->last-Bind over all gangs "
-                             "(unbound = infinite) is <= 25 ms; the search stops at the first failed rate; one "
+                             "(unbound = infinite) is <= 25 ms; the search stops at the first failed rate, which "
+                             "is tried once more in a fresh process (the ladder goes on there if it passes); one "
                              "trial per rate, two (both must pass) within two x1.3 steps of the burst rate",
             "transient_shortage": "Park (gangs short of GPUs wait for a release; the reference denies them "
                                   "for deniedPGExpirationTimeSeconds)",
@@ -345,6 +346,7 @@ def main() -> int:
                 "children without the GPU runtime: the search on one fresh shard, the 50%/90% loads on "
                 "another in a second process"),
             "capacity_search": rep["search"],
+            "retried_rate": rep.get("retried_rate"),
             **{k: rep[k] for k in ("load_50", "load_90", "deny_mode_load_90") if k in rep}}
         search = rep["search"]
         ol = extras["gang_admit_open_loop"]

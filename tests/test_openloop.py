@@ -181,8 +181,21 @@ def test_capacity_search_reaches_the_burst_rate(monkeypatch):
     assert max(tried) > 110_000 and tried[-1] == max(tried)  # the failed rate is the last trial
     tried.clear()
     limit = 50_000.0  # an ordinary failing coarse step: the search ends there
-    cap = openloop.open_loop_capacity(None, 120_000.0)
+    out: dict = {}
+    cap = openloop.open_loop_capacity(None, 120_000.0, outcome=out)
     assert 50_000 / 1.31 < cap <= 50_000 and max(tried) < 120_000 and tried[-1] == max(tried)
+    assert round(out["failed_at"]) == max(tried)
+    # The retry in a fresh process resumes the ladder at the failed rung: a
+    # transient failure (the rung passes now) lets the climb go on from it.
+    tried.clear()
+    limit = 110_000.0
+    rung = out["failed_at"]
+    cap2 = openloop.open_loop_capacity(None, 120_000.0, resume_at=rung, outcome=out)
+    assert tried[0] == round(rung) and 110_000 / 1.071 < cap2 <= 110_000 and out["failed_at"] > 110_000
+    tried.clear()
+    limit = 1.0  # the resumed rung fails again: nothing gained
+    assert openloop.open_loop_capacity(None, 120_000.0, resume_at=66_000.0, outcome=out) == 0.0
+    assert tried == [66_000] and out["failed_at"] == 66_000.0
 
 
 def test_capacity_report_in_a_gpu_free_child():
