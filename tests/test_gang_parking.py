@@ -255,9 +255,14 @@ def test_xcd_gang_is_probed_apart_from_a_parked_whole_gpu_gang(store):
 def test_parked_member_whose_spec_changes_is_retried(store):
     """A parked gang member whose spec is updated gets another attempt at once
     (upstream Update moves an updated unschedulable pod)
-    instead of waiting for its gang's next probe or the 60 s flush."""
+    instead of waiting for its gang's next probe or the 60 s flush. It still
+    serves its backoff (upstream: backoffQ while backing off), which grows
+    with the attempts the member happened to get before its gang parked; the
+    short backoff here keeps that under the wait below."""
     store.create("nodes", mi355x_node("mi-0", mode="spx"))
-    s = scheduler(store)
+    s = new_scheduler(store, load_config(flagship_config(permit_wait_s=10, denied_s=20, transient_shortage="Park")),
+                      podInitialBackoffSeconds=0.05, podMaxBackoffSeconds=0.5)
+    s.start()
     try:
         a = submit(store, "a", 8)
         assert wait_for(lambda: len(bound(store, a)) == 8)
