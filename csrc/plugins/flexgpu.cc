@@ -26,6 +26,7 @@
 //  C3 whole-GPU pods are checked per GPU in Filter (Reserve can no longer
 //     fail after Filter passed) and k > 1 GPUs are supported.
 #include <algorithm>
+#include <cstdint>
 #include <string>
 
 #include "common/log.h"
@@ -50,24 +51,35 @@ struct Placement {
 Placement place_whole(const GpuLedger& L, int64_t k) {
   Placement pl;
   if (k <= 0) k = 1;
-  std::vector<int> free;
-  for (int g = 0; g < L.gpu_count; ++g)
-    if (L.whole_gpu_free(g)) free.push_back(g);
-  if (static_cast<int64_t>(free.size()) < k) return pl;
-  std::map<int, std::vector<int>> by_numa;
-  for (int g : free) by_numa[L.numa[g]].push_back(g);
-  if (by_numa.size() > 1 || (by_numa.size() == 1 && by_numa.begin()->first >= 0)) {
-    const std::vector<int>* best = nullptr;
-    for (const auto& [numa, gs] : by_numa) {
-      if (numa < 0 || static_cast<int64_t>(gs.size()) < k) continue;
-      if (!best || gs.size() < best->size()) best = &gs;
-    }
-    if (best) {
-      pl.gpus.assign(best->begin(), best->begin() + k);
-      return pl;
+  // Free GPUs per NUMA node, counted in place (no per-call containers: this
+  // runs in every whole-GPU pod's Reserve).
+  int n_free = 0;
+  for (int g = 0; g < L.gpu_count; ++g) n_free += L.whole_gpu_free(g);
+  if (n_free < k) return pl;
+  // The NUMA node with the fewest free GPUs that still fits (lowest id among
+  // equals); -1 ("unknown") never qualifies. Used only when the free GPUs
+  // span more than one NUMA value or sit on one known node.
+  int best_numa = INT32_MIN, best_count = 0, distinct = 0, first_numa = INT32_MAX;
+  for (int g = 0; g < L.gpu_count; ++g) {
+    if (!L.whole_gpu_free(g)) continue;
+    const int numa = L.numa[g];
+    bool seen = false;
+    for (int h = 0; h < g && !seen; ++h) seen = L.whole_gpu_free(h) && L.numa[h] == numa;
+    if (seen) continue;  // counted with its first GPU
+    ++distinct;
+    first_numa = std::min(first_numa, numa);
+    if (numa < 0) continue;
+    int count = 0;
+    for (int h = g; h < L.gpu_count; ++h) count += L.whole_gpu_free(h) && L.numa[h] == numa;
+    if (count < k) continue;
+    if (best_numa == INT32_MIN || count < best_count || (count == best_count && numa < best_numa)) {
+      best_numa = numa;
+      best_count = count;
     }
   }
-  pl.gpus.assign(free.begin(), free.begin() + k);
+  const bool by_numa = distinct > 1 || (distinct == 1 && first_numa >= 0);
+  for (int g = 0; g < L.gpu_count && static_cast<int64_t>(pl.gpus.size()) < k; ++g)
+    if (L.whole_gpu_free(g) && (!by_numa || best_numa == INT32_MIN || L.numa[g] == best_numa)) pl.gpus.push_back(g);
   return pl;
 }
 
@@ -81,7 +93,8 @@ int xcd_waste(const GpuLedger& L, int g, int64_t x) {
   return static_cast<int>(need * xpp - x);
 }
 
-Placement place_xcd(const GpuLedger& L, int64_t x, int* waste_out = nullptr) {
+// `build` false: only *waste_out is wanted (Score), no placement vectors.
+Placement place_xcd(const GpuLedger& L, int64_t x, int* waste_out = nullptr, bool build = true) {
   Placement pl;
   if (x <= 0) return pl;
   int best_g = -1, best_free = 1 << 30, best_waste = 1 << 30;
@@ -101,7 +114,7 @@ Placement place_xcd(const GpuLedger& L, int64_t x, int* waste_out = nullptr) {
     }
   }
   if (waste_out) *waste_out = best_g < 0 ? 0 : best_waste;
-  if (best_g < 0) return pl;
+  if (best_g < 0 || !build) return pl;
   int xpp = L.xcds_per_part(best_g);
   int need = static_cast<int>((x + xpp - 1) / xpp);
   for (int p = 0; p < L.parts[best_g] && static_cast<int>(pl.parts.size()) < need; ++p)
@@ -114,13 +127,16 @@ Placement place_xcd(const GpuLedger& L, int64_t x, int* waste_out = nullptr) {
 // placement (best fit, value semantics — fixes Appendix C1). A slice never
 // breaks an untouched SPX GPU while any other partition can take it: that GPU
 // is the only kind a whole-GPU (training-rank) pod can use.
-Placement place_memory(const GpuLedger& L, int64_t m, bool* breaks_whole = nullptr) {
+// `build` false: only *breaks_whole is wanted (Score), no placement vectors.
+Placement place_memory(const GpuLedger& L, int64_t m, bool* breaks_whole = nullptr, bool build = true) {
   Placement pl;
   int bg = -1, bp = -1;
   int64_t best_remain = 0;
   bool best_breaks = true;
   for (int g = 0; g < L.gpu_count; ++g) {
-    if (L.monopoly[g] > 0) continue;
+    // No partition of g has m free (the ledger's per-GPU maximum): skip its
+    // partitions (-1 for a monopolised GPU).
+    if (L.monopoly[g] > 0 || L.free[g].max_slot_mem < m) continue;
     int64_t cap = L.part_mem(g);
     bool breaks = L.whole_gpu_free(g);
     for (int p = 0; p < L.parts[g]; ++p) {
@@ -137,7 +153,7 @@ Placement place_memory(const GpuLedger& L, int64_t m, bool* breaks_whole = nullp
     }
   }
   if (breaks_whole) *breaks_whole = bg >= 0 && best_breaks;
-  if (bg < 0) return pl;
+  if (bg < 0 || !build) return pl;
   pl.gpus.push_back(bg);
   pl.parts.emplace_back(bg, bp);
   return pl;
@@ -265,13 +281,13 @@ class FlexGPU : public Plugin {
         // Stranded XCDs dominate: a node that can host the slice without
         // waste always outranks one that would burn a whole SPX GPU on it.
         int waste = 0;
-        place_xcd(ni.gpu, d.amount, &waste);
+        place_xcd(ni.gpu, d.amount, &waste, /*build=*/false);
         return {ni.gpu.free_xcds() + 64 * waste, {}};
       }
       case Demand::Memory: {
         // Breaking a whole SPX GPU for a slice costs more than any packing gain.
         bool breaks = false;
-        place_memory(ni.gpu, d.amount, &breaks);
+        place_memory(ni.gpu, d.amount, &breaks, /*build=*/false);
         return {ni.gpu.free_memory() + (breaks ? 8 * ni.gpu.mem_per_gpu : 0), {}};
       }
       default: return {0, {}};

@@ -210,3 +210,51 @@ def test_profiles_of_one_scheduler_must_agree_on_gpu_names(store):
     c["profiles"].append(other)
     with pytest.raises(Exception, match="FlexGPU resource names differ"):
         new_scheduler(store, c)
+
+
+def _reference_place_whole(free: list[int], numa: dict[int, int], k: int) -> list[int]:
+    """The whole-GPU chooser as first written (a map of NUMA node -> free
+    GPUs): the NUMA node with the fewest free GPUs that still fits, lowest id
+    among equals, -1 never; else the lowest free GPUs."""
+    by: dict[int, list[int]] = {}
+    for g in free:
+        by.setdefault(numa[g], []).append(g)
+    if len(by) > 1 or (len(by) == 1 and min(by) >= 0):
+        best = None
+        for n in sorted(by):
+            if n < 0 or len(by[n]) < k:
+                continue
+            if best is None or len(by[n]) < len(by[best]):
+                best = n
+        if best is not None:
+            return by[best][:k]
+    return free[:k]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_whole_gpu_choice_matches_reference_model(store, seed):
+    """Randomised: GPUs held on a node with an irregular NUMA layout (some
+    GPUs of unknown NUMA), then a k-GPU pod: the GPUs chosen equal the
+    reference model's (place_whole is allocation-free since round 6)."""
+    import random
+
+    rng = random.Random(seed)
+    numa = {g: rng.choice([-1, 0, 0, 1, 1, 2]) for g in range(8)}
+    store.create("nodes", mi355x_node("n0", gpus=[GpuInfo(g, numa=numa[g]) for g in range(8)]))
+    held = sorted(rng.sample(range(8), rng.randint(0, 5)))
+    s = start(store, cfg())
+    try:
+        for g in held:
+            p = make_pod(f"h{g}", limits={GPU: "1"})
+            p["spec"]["nodeName"] = "n0"
+            p["metadata"].setdefault("annotations", {})["amd.com/gpu-index"] = str(g)
+            store.create("pods", p)
+        free = [g for g in range(8) if g not in held]
+        k = rng.randint(1, len(free))
+        time.sleep(0.1)  # the held pods reach the cache before the new one is scheduled
+        store.create("pods", make_pod("want", limits={GPU: str(k)}))
+        wait_bound(s, 1)
+        got = [int(x) for x in annotations(store, "want")["amd.com/gpu-index"].split(",")]
+        assert got == _reference_place_whole(free, numa, k), (numa, held, k, got)
+    finally:
+        s.stop()
