@@ -450,17 +450,28 @@ class Coscheduling : public Plugin {
       std::lock_guard<std::mutex> g(sh.mu);
       sh.map.erase(key);
     }
-    if (park_) forget_group(key);
+    if (park_) forget_group(key, md["uid"].as_string());
   }
   // A deleted group leaves the parking state: GPUs owed to it at Permit, its
   // parked entry (the oldest parked group reserves its need against every
   // younger gang until a probe finds it empty) and its pending rejections,
   // at once rather than at the next probe or sweep (an open-loop overload
   // ends with thousands of gangs deleted mid-admission).
-  void forget_group(uint64_t key) {
+  void forget_group(uint64_t key, const std::string& uid) {
     std::vector<PodPtr> probe;
     {
       std::lock_guard<std::mutex> g(park_mu_);
+      // A member of the group may be inside its cycle right now, holding the
+      // PodGroup object from before the deletion: its gate must not park the
+      // group again after this (it would stay in the line with no event left
+      // to remove it). Remembered by uid, so a group recreated under the same
+      // name parks as usual.
+      if (!uid.empty()) {
+        const int64_t now = h_.clock->now_us();
+        for (auto it = deleted_uids_.begin(); it != deleted_uids_.end();)
+          it = now - it->second > kRejectWindowUs ? deleted_uids_.erase(it) : std::next(it);
+        deleted_uids_[uid] = now;
+      }
       erase_outstanding_locked(key);
       parked_rejects_.erase(key);
       unpark_locked(key, probe);
@@ -686,6 +697,8 @@ class Coscheduling : public Plugin {
     const bool coloc_ok = assigned > 0 || colocated_now(p, remaining);
     std::vector<PodPtr> probe;
     bool pass;
+    bool probe_answer = false;  // p's cycle is the probe its group was sent
+    uint64_t probe_seq = 0;     // releases seen when that probe went out
     {
       std::lock_guard<std::mutex> g(park_mu_);
       if (parked_.empty() && owed_[slot] == 0 && free >= need && coloc_ok) return {};  // common case
@@ -702,7 +715,11 @@ class Coscheduling : public Plugin {
         if (head != parked_.end() && head->first < me) reserved += head->second.need;
       }
       pass = free - reserved >= need && coloc_ok;
-      if (p.pg_key == probe_key_[slot]) probe_key_[slot] = 0;  // the probe's answer is in
+      if (p.pg_key == probe_key_[slot]) {  // the probe's answer is in
+        probe_key_[slot] = 0;
+        probe_answer = true;
+        probe_seq = probe_seq_[slot];
+      }
       if (pass && pos != parked_pos_.end()) {
         parked_.erase(pos->second);
         parked_pos_.erase(pos);
@@ -735,8 +752,21 @@ class Coscheduling : public Plugin {
     // A group already part-placed releases what its waiting members hold (no
     // hold-and-wait between gangs), as PostFilter's park does.
     if (assigned > 0) park_rejecting(p, pg);
-    else park(p, pg, d.kind, need);
-    park_members(p);
+    else if (park(p, pg, d.kind, need)) park_members(p);
+    if (probe_answer) {
+      // GPUs released after this probe went out skipped their own probe (one
+      // was outstanding), yet this cycle may have read a snapshot from before
+      // them: with no later release to come, the line would wait forever. So
+      // a negative answer is probed again when a release happened meanwhile
+      // (after park_members, so the activation wins over the park mark).
+      std::vector<PodPtr> again;
+      {
+        std::lock_guard<std::mutex> g(park_mu_);
+        if (release_seq_ != probe_seq && !probe_key_[slot]) again = next_probe_locked(slot);
+        take_wake_locked(again);
+      }
+      if (!again.empty()) h_.activate(again);
+    }
     if (!coloc_ok && free >= need)
       return XS_FIXED_STATUS(Code::Unschedulable,
                              "PodGroup parked: no node can host all of its remaining ranks on one xGMI mesh "
@@ -772,12 +802,14 @@ class Coscheduling : public Plugin {
     }
     return free_units(d) - owed_others < units_for(d, remaining);
   }
-  void park(const Pod& p, const PodGroup& pg, GpuDemand::Kind kind, int64_t need) {
+  // False when the group was deleted meanwhile (forget_group): not parked.
+  bool park(const Pod& p, const PodGroup& pg, GpuDemand::Kind kind, int64_t need) {
     std::lock_guard<std::mutex> g(park_mu_);
+    if (!deleted_uids_.empty() && deleted_uids_.count(pg.meta.uid)) return false;
     auto pos = parked_pos_.find(p.pg_key);
     if (pos != parked_pos_.end()) {
       parked_[pos->second].need = need;
-      return;
+      return true;
     }
     const ParkKey k{kind_slot(kind), pg.meta.creation, p.pg_key};
     Parked& pk = parked_[k];
@@ -790,6 +822,7 @@ class Coscheduling : public Plugin {
     ++parks_total_;
     if (h_.metrics) h_.metrics->inc("xsched_coscheduling_parked_total", "");
     if (h_.gang_parked) h_.gang_parked(p);
+    return true;
   }
   // PostFilter's park: the waiting siblings are rejected (their Unreserve
   // must not deny the group: exactly those pods are remembered), nothing
@@ -809,8 +842,8 @@ class Coscheduling : public Plugin {
       }
       erase_outstanding_locked(p.pg_key);
     }
-    park(p, pg, p.gpu_demand.kind, units_for(p.gpu_demand, pg.min_member));
-    park_members(p);  // before the rejections, so the rejected siblings park as their cycles fail
+    if (park(p, pg, p.gpu_demand.kind, units_for(p.gpu_demand, pg.min_member)))
+      park_members(p);  // before the rejections, so the rejected siblings park as their cycles fail
     reject_group(p, "PodGroup parked in PostFilter: GPUs are short for its remaining members");
   }
   // The group's unplaced members leave the scheduling queues until a probe
@@ -881,6 +914,7 @@ class Coscheduling : public Plugin {
       if (!out.empty()) {
         probe_key_[slot] = key;
         probe_sent_us_[slot] = h_.clock->now_us();
+        probe_seq_[slot] = release_seq_;
         return out;
       }
       // Not viable: off the line; its unplaced members go back to the
@@ -902,6 +936,7 @@ class Coscheduling : public Plugin {
     std::vector<PodPtr> probe;
     {
       std::lock_guard<std::mutex> g(park_mu_);
+      ++release_seq_;
       // One probe per kind at a time: a probe still queued answers for this
       // release too (its gate reads the snapshot of its own cycle, which
       // includes it). XCD gangs are probed apart from whole-GPU gangs, so a
@@ -980,11 +1015,14 @@ class Coscheduling : public Plugin {
   std::atomic<size_t> parked_n_{0};
   // pg_key -> (uids of the siblings park_rejecting rejected, when)
   std::unordered_map<uint64_t, std::pair<std::vector<std::string>, int64_t>> parked_rejects_;
+  std::unordered_map<std::string, int64_t> deleted_uids_;  // PodGroups deleted in the last second (uid -> when)
   std::vector<PodPtr> wake_;  // members of groups dropped from the line, for the active queue
   std::unordered_map<uint64_t, Owed> outstanding_;
   int64_t owed_[2] = {0, 0};
   uint64_t probe_key_[2] = {0, 0};  // per kind slot: the group whose probe is out
   int64_t probe_sent_us_[2] = {0, 0};
+  uint64_t release_seq_ = 0;         // capacity_freed calls (guarded by park_mu_)
+  uint64_t probe_seq_[2] = {0, 0};   // release_seq_ when each kind's probe went out
   uint64_t parks_total_ = 0;
   // Permit (scheduling thread only): the gang whose waiting member last
   // activated its siblings, and how many members it had assigned then.

@@ -281,7 +281,11 @@ void SchedulingQueue::deactivate(const std::vector<PodPtr>& pods) {
       parked_[uid] = std::move(q);
       continue;
     }
-    if (auto f = in_flight_.find(uid); f != in_flight_.end()) f->second = kPark;
+    // In flight: parked when its cycle fails, unless an activation came in
+    // meanwhile (a probe sent for capacity released during the cycle): that
+    // is newer than the park and must not be lost (the pod then gets one
+    // more attempt and parks again if the capacity is not there).
+    if (auto f = in_flight_.find(uid); f != in_flight_.end() && f->second != kActivate) f->second = kPark;
   }
 }
 
