@@ -35,6 +35,7 @@
 // fragmentation, CPU/memory) and Permit timeouts are denied for the TTL.
 // "Deny" restores the reference's behaviour everywhere.
 #include <algorithm>
+#include <unordered_set>
 #include <array>
 #include <deque>
 #include <map>
@@ -467,10 +468,14 @@ class Coscheduling : public Plugin {
       // to remove it). Remembered by uid, so a group recreated under the same
       // name parks as usual.
       if (!uid.empty()) {
+        // Expired in insertion order (O(1) amortised: a burst wave deletes
+        // thousands of groups per second).
         const int64_t now = h_.clock->now_us();
-        for (auto it = deleted_uids_.begin(); it != deleted_uids_.end();)
-          it = now - it->second > kRejectWindowUs ? deleted_uids_.erase(it) : std::next(it);
-        deleted_uids_[uid] = now;
+        while (!deleted_order_.empty() && now - deleted_order_.front().first > kRejectWindowUs) {
+          deleted_uids_.erase(deleted_order_.front().second);
+          deleted_order_.pop_front();
+        }
+        if (deleted_uids_.insert(uid).second) deleted_order_.emplace_back(now, uid);
       }
       erase_outstanding_locked(key);
       parked_rejects_.erase(key);
@@ -1015,7 +1020,10 @@ class Coscheduling : public Plugin {
   std::atomic<size_t> parked_n_{0};
   // pg_key -> (uids of the siblings park_rejecting rejected, when)
   std::unordered_map<uint64_t, std::pair<std::vector<std::string>, int64_t>> parked_rejects_;
-  std::unordered_map<std::string, int64_t> deleted_uids_;  // PodGroups deleted in the last second (uid -> when)
+  // PodGroups deleted in the last second (forget_group), by uid, and in
+  // deletion order for expiry.
+  std::unordered_set<std::string> deleted_uids_;
+  std::deque<std::pair<int64_t, std::string>> deleted_order_;
   std::vector<PodPtr> wake_;  // members of groups dropped from the line, for the active queue
   std::unordered_map<uint64_t, Owed> outstanding_;
   int64_t owed_[2] = {0, 0};
