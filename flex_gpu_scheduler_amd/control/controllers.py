@@ -81,6 +81,9 @@ class _Controller:
     def __init__(self, client: Client, workers: int = 1, factory: InformerFactory | None = None):
         self.client = client
         self.workers = workers
+        # A factory passed in is shared and stopped by its owner; one made
+        # here stops with the controller.
+        self._own_factory = factory is None
         self.factory = factory or InformerFactory(client)
         self.queue = WorkQueue(self.name)
         self._threads: list[threading.Thread] = []
@@ -121,6 +124,8 @@ class _Controller:
         self.queue.shutdown()
         for t in self._threads:
             t.join(timeout=5)
+        if self._own_factory:
+            self.factory.stop()
 
     def wait_idle(self, timeout: float = 10.0) -> bool:
         """Test helper: queue empty and nothing in flight."""

@@ -18,11 +18,16 @@ import heapq
 import logging
 import threading
 import time
+import weakref
 from typing import Callable
 
 from .. import _lifecycle
 from .client import Client
 from .selectors import label_matcher
+
+# Informers started in this process (weak): the test suite stops any that a
+# test left running, so none retries against a server that is gone.
+STARTED: "weakref.WeakSet[Informer]" = weakref.WeakSet()
 
 log = logging.getLogger(__name__)
 
@@ -104,7 +109,11 @@ class Informer:
     def start(self) -> "Informer":
         self._thread = threading.Thread(target=self._run, name=f"informer-{self.kind}", daemon=True)
         self._thread.start()
+        STARTED.add(self)
         return self
+
+    def running(self) -> bool:
+        return self._thread is not None and self._thread.is_alive() and not self._stop.is_set()
 
     def stop(self) -> None:
         self._stop.set()

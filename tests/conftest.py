@@ -18,6 +18,24 @@ def pytest_configure(config):
     build_ext.build_core(verbose=False)
 
 
+@pytest.fixture(autouse=True)
+def _stop_leaked_informers(request):
+    """Python informers a test started and left running are stopped at its
+    end (their API server is gone, so they would retry and log forever)."""
+    from flex_gpu_scheduler_amd.control.informer import STARTED
+
+    before = set(STARTED)
+    yield
+    leaked = [i for i in list(STARTED) if i not in before and i.running()]
+    for inf in leaked:
+        inf.stop()
+    if leaked:
+        request.node.user_properties.append(("leaked_informers", sorted(i.kind for i in leaked)))
+        import warnings
+
+        warnings.warn(f"{request.node.nodeid} left informers running: {sorted(i.kind for i in leaked)}")
+
+
 @pytest.fixture
 def store():
     from flex_gpu_scheduler_amd import Store
