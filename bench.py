@@ -27,7 +27,8 @@ dict-valued key, led by `headline` (one string with all of them):
 p99_gang_admit_ms_<type> (burst), open_loop_p99_create_to_bound_ms_<type> (at
 90% of the open-loop capacity), open_loop_capacity_pods_per_s,
 nodes1024_pods_per_s, service_mode_pods_per_s (+ generator_limited),
-denied_gang_fraction, parked_gang_fraction, gang_split_fraction_<type> (gangs
+denied_gang_fraction, parked_gang_fraction (over the served open-loop runs;
+*_all_trials adds the failed overload rung), gang_split_fraction_<type> (gangs
 placed on more than one node) and gang_avoidable_split_fraction (split although
 one node could host the gang), and on >= 2 GPUs placement_verdict_<k> and
 placed_busbw_GBps_<k>.
@@ -357,12 +358,26 @@ def main() -> int:
         if l90:
             extras["open_loop_p999_create_to_bound_ms"] = l90["all_gangs"]["p999_create_to_bound_ms"]
             extras["open_loop_max_create_to_bound_ms"] = l90["all_gangs"]["max_create_to_bound_ms"]
-        # Over every open-loop run of the search and the two loads.
-        runs = [*search, *(ol.get(f"load_{x}") for x in (50, 90) if ol.get(f"load_{x}"))]
-        n_g = sum(r["gangs"] for r in runs)
-        n_d = sum(r.get("denied_gangs", (r.get("denials") or {}).get("total", 0)) for r in runs)
-        extras["denied_gang_fraction"] = round(n_d / max(1, n_g), 6)
-        extras["parked_gang_fraction"] = round(sum(r.get("parked_gangs", 0) for r in runs) / max(1, n_g), 6)
+        # Over the served open-loop runs (search rungs that passed and the two
+        # loads); the rung that failed is an overload by construction, so its
+        # parked gangs are reported apart (all_trials) instead of diluting the
+        # fraction a user sees below capacity.
+        loads_r = [ol.get(f"load_{x}") for x in (50, 90) if ol.get(f"load_{x}")]
+
+        def frac(rs, key):
+            n_g = sum(r["gangs"] for r in rs)
+            if key == "denied":
+                n = sum(r.get("denied_gangs", (r.get("denials") or {}).get("total", 0)) for r in rs)
+            else:
+                n = sum(r.get("parked_gangs", 0) for r in rs)
+            return round(n / max(1, n_g), 6)
+
+        served = [*(r for r in search if r.get("served")), *loads_r]
+        every = [*search, *loads_r]
+        extras["denied_gang_fraction"] = frac(served, "denied")
+        extras["parked_gang_fraction"] = frac(served, "parked")
+        extras["denied_gang_fraction_all_trials"] = frac(every, "denied")
+        extras["parked_gang_fraction_all_trials"] = frac(every, "parked")
         dn = ol.get("deny_mode_load_90")
         if dn:
             # The reference's semantics at the same load (Coscheduling

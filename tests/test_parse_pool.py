@@ -28,13 +28,16 @@ def test_wave_binds_and_cache_is_clean(monkeypatch, pool):
                 store.create_many("pods", pods_js)
         assert s.wait_bound(len(w.pods), 30.0), s.stats()
         # Bound counts at the Bind call; the informer confirms the assumed
-        # pods when their Modified events arrive (a loaded host lags).
+        # pods when their Modified events arrive (a loaded host lags). The
+        # debugger reads the listers and then the cache, two snapshots: an
+        # event landing between them reads as a transient difference, so
+        # only a difference that persists fails.
         deadline = time.time() + 10.0
         check = s.check_cache()
-        while not check["clean"] and check.get("assumed") and time.time() < deadline:
+        while not check["clean"] and time.time() < deadline:
             time.sleep(0.01)
             check = s.check_cache()
-        assert check["clean"], check
+        assert check["clean"], {k: v for k, v in check.items() if v}
         store.delete_all("pods", "w")
         assert s.wait_cache_empty(30.0)
     finally:
