@@ -2180,12 +2180,24 @@ bool Scheduler::wait_cache_empty(int64_t timeout_us) const {
 }
 
 Json Scheduler::check_cache() const {
-  std::vector<PodPtr> assigned;
-  for (auto& p : informers_->all_pods())
-    if (!p->node_name.empty()) assigned.push_back(std::move(p));
-  std::vector<std::string> nodes;
-  for (const auto& n : store_->list("nodes", "")) nodes.push_back((*n)["metadata"]["name"].as_string());
-  return cache_->check(assigned, nodes);
+  // The listers and the cache are read one after the other, not atomically:
+  // an informer event landing between the two reads shows as a difference
+  // that the next read no longer has. Such a difference is read again (up to
+  // ~50 ms); one that persists is reported. `reads` says how many it took.
+  Json out;
+  int reads = 0;
+  for (; reads < 25; ++reads) {
+    if (reads) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    std::vector<PodPtr> assigned;
+    for (auto& p : informers_->all_pods())
+      if (!p->node_name.empty()) assigned.push_back(std::move(p));
+    std::vector<std::string> nodes;
+    for (const auto& n : store_->list("nodes", "")) nodes.push_back((*n)["metadata"]["name"].as_string());
+    out = cache_->check(assigned, nodes);
+    if (out["clean"].as_bool()) break;
+  }
+  out.set("reads", Json(static_cast<int64_t>(std::min(reads + 1, 25))));
+  return out;
 }
 
 Json Scheduler::dump_cache() const {
