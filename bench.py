@@ -362,22 +362,7 @@ def main() -> int:
         # loads); the rung that failed is an overload by construction, so its
         # parked gangs are reported apart (all_trials) instead of diluting the
         # fraction a user sees below capacity.
-        loads_r = [ol.get(f"load_{x}") for x in (50, 90) if ol.get(f"load_{x}")]
-
-        def frac(rs, key):
-            n_g = sum(r["gangs"] for r in rs)
-            if key == "denied":
-                n = sum(r.get("denied_gangs", (r.get("denials") or {}).get("total", 0)) for r in rs)
-            else:
-                n = sum(r.get("parked_gangs", 0) for r in rs)
-            return round(n / max(1, n_g), 6)
-
-        served = [*(r for r in search if r.get("served")), *loads_r]
-        every = [*search, *loads_r]
-        extras["denied_gang_fraction"] = frac(served, "denied")
-        extras["parked_gang_fraction"] = frac(served, "parked")
-        extras["denied_gang_fraction_all_trials"] = frac(every, "denied")
-        extras["parked_gang_fraction_all_trials"] = frac(every, "parked")
+        extras.update(gang_fractions(search, [ol.get(f"load_{x}") for x in (50, 90) if ol.get(f"load_{x}")]))
         dn = ol.get("deny_mode_load_90")
         if dn:
             # The reference's semantics at the same load (Coscheduling
@@ -501,6 +486,25 @@ def main() -> int:
         print(json.dumps(line), flush=True)
     ctx.close()
     return 0
+
+
+def gang_fractions(search: list[dict], loads: list[dict]) -> dict:
+    """Denied and parked gang fractions of the open loop: over the served runs
+    (search rungs that passed, and the 50%/90% loads), and over every run
+    including the failed rung (`*_all_trials`)."""
+    def frac(rs: list[dict], key: str) -> float:
+        n_g = sum(r["gangs"] for r in rs)
+        if key == "denied":
+            n = sum(r.get("denied_gangs", (r.get("denials") or {}).get("total", 0)) for r in rs)
+        else:
+            n = sum(r.get("parked_gangs", 0) for r in rs)
+        return round(n / max(1, n_g), 6)
+
+    served = [*(r for r in search if r.get("served")), *loads]
+    every = [*search, *loads]
+    return {"denied_gang_fraction": frac(served, "denied"), "parked_gang_fraction": frac(served, "parked"),
+            "denied_gang_fraction_all_trials": frac(every, "denied"),
+            "parked_gang_fraction_all_trials": frac(every, "parked")}
 
 
 def headline_scalars(value: float, by_type: dict, split: dict, extras: dict, world: int) -> dict:

@@ -225,3 +225,24 @@ def test_headline_scalars_on_one_gpu_read_na():
     for k in ("2", "4", "8", "cpx4"):
         assert h[f"gang_split_fraction_{k}"] == 0.0
     assert "burst=118.0k" in h["headline"] and "n1024=60.0k" in h["headline"] and "open_loop=100.0k" in h["headline"]
+
+
+def test_gang_fractions_count_served_runs_apart_from_the_failed_rung():
+    """bench.gang_fractions: the headline parked/denied fractions are over the
+    served open-loop runs; the failed (overloaded) rung only enters the
+    *_all_trials figures."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    search = [{"served": True, "gangs": 1000, "parked_gangs": 2, "denied_gangs": 0},
+              {"served": True, "gangs": 1000, "parked_gangs": 4, "denied_gangs": 1},
+              {"served": False, "gangs": 1000, "parked_gangs": 900, "denied_gangs": 0}]
+    loads = [{"gangs": 500, "parked_gangs": 0, "denials": {"total": 1}},
+             {"gangs": 500, "parked_gangs": 2, "denials": {"total": 0}}]
+    f = bench.gang_fractions(search, loads)
+    assert f["parked_gang_fraction"] == round(8 / 3000, 6) and f["denied_gang_fraction"] == round(2 / 3000, 6)
+    assert f["parked_gang_fraction_all_trials"] == round(908 / 4000, 6)
+    assert f["denied_gang_fraction_all_trials"] == 2 / 4000
+    assert bench.gang_fractions([], [])["parked_gang_fraction"] == 0.0
