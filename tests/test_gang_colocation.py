@@ -195,3 +195,35 @@ def test_xcd_gang_stays_on_one_cpx_node(store):
             assert len(set(node_of(store, g))) == 1
     finally:
         s.stop()
+
+
+def test_random_clusters_keep_a_hostable_gang_on_one_node():
+    """Randomised: 4 nodes with 0-8 GPUs already held each and one gang of
+    2/4/8 that at least one node can host. Under Preferred every rank lands on
+    one node, and that node had room for the whole gang."""
+    import random
+
+    from flex_gpu_scheduler_amd import Store
+
+    rng = random.Random(20261019)
+    trials = 0
+    while trials < 12:
+        held = [rng.randint(0, 8) for _ in range(4)]
+        k = rng.choice((2, 4, 8))
+        if max(8 - h for h in held) < k:
+            continue
+        trials += 1
+        store = Store()
+        for i, h in enumerate(held):
+            add_node(store, f"mi-{i}")
+            occupy(store, f"mi-{i}", h)
+        s = scheduler(store)
+        try:
+            g = submit(store, f"g{trials}", k)
+            assert wait_for(lambda: all(node_of(store, g))), (held, k)
+            nodes = set(node_of(store, g))
+            assert len(nodes) == 1, (held, k, node_of(store, g))
+            host = int(next(iter(nodes)).split("-")[1])
+            assert 8 - held[host] >= k, (held, k, nodes)
+        finally:
+            s.stop()
