@@ -227,3 +227,38 @@ def test_random_clusters_keep_a_hostable_gang_on_one_node():
             assert 8 - held[host] >= k, (held, k, nodes)
         finally:
             s.stop()
+
+
+def test_concurrent_gangs_split_only_when_no_node_could_host_them():
+    """Randomised, many gangs in flight at once: 6 empty nodes and gangs of
+    1/2/4/8 submitted together (up to 40 of the 48 GPUs). A gang may span
+    nodes only if, when its first rank was placed, no node could host it
+    (`hostable` 0): an avoidable split never happens."""
+    import random
+
+    from flex_gpu_scheduler_amd import Store
+
+    rng = random.Random(6)
+    for trial in range(4):
+        store = Store()
+        for i in range(6):
+            add_node(store, f"mi-{i}")
+        s = scheduler(store)
+        try:
+            sizes, total = [], 0
+            while True:
+                k = rng.choice((1, 2, 4, 8))
+                if total + k > 40:
+                    break
+                sizes.append(k)
+                total += k
+            groups = [submit(store, f"t{trial}-g{i}", k) for i, k in enumerate(sizes)]
+            assert wait_for(lambda: all(all(node_of(store, g)) for g in groups), timeout=20.0), sizes
+            recs = {r["pod_group"]: r for r in s.gang_records()}
+            for i, g in enumerate(groups):
+                r = recs.get(f"default/t{trial}-g{i}")
+                assert r is not None
+                if len(set(node_of(store, g))) > 1:
+                    assert r["hostable"] == 0, (sizes, i, node_of(store, g), r)
+        finally:
+            s.stop()
